@@ -1,0 +1,166 @@
+/*
+ * oracle.h -- TEST INFRASTRUCTURE ONLY.
+ *
+ * A plain-C, single-threaded restatement of the reference (YIVEK/aom-av1-lavish,
+ * a libaom v3.6.0 fork) hot-path arithmetic, used only as the *checker* by
+ * tests/, __graft_entry__.smoke() and the cpu_baseline leg of bench.py.  The
+ * product (aom-av1-lavish_amd/, liblavish_hip.so) never links, loads or calls
+ * anything in oracle/.
+ *
+ * Parity pinning (see DESIGN.md "Oracle"):
+ *   - 1-D transforms: bit-exact against tests/golden/txfm1d_golden.npz, whose
+ *     outputs were produced by executing the reference's own statement lists
+ *     (tests/golden/gen_golden.py).
+ *   - tables (cospi/sinpi, shifts, cos_bit, scans, quant lookups): equal to the
+ *     values parsed from the reference source (tests/golden/ref_tables.json).
+ *   - SATD: the reference's known answers (test/avg_test.cc:972-977).
+ *   - 2-D transforms: the reference's own accuracy bound vs a double-precision
+ *     DCT/ADST (test/av1_fwd_txfm2d_test.cc:71-187).
+ *   Everything else (quantizers, SAD/variance, ...) is a careful restatement
+ *   citing file:line; bit-exact pinning of those against executed reference
+ *   code is not possible here (the reference is unbuildable in this image).
+ */
+#ifndef LAVISH_ORACLE_H_
+#define LAVISH_ORACLE_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* TX_SIZE / TX_TYPE numbering follows aom_dsp/txfm_common.h:25-71. */
+enum {
+  ORC_TX_4X4, ORC_TX_8X8, ORC_TX_16X16, ORC_TX_32X32, ORC_TX_64X64,
+  ORC_TX_4X8, ORC_TX_8X4, ORC_TX_8X16, ORC_TX_16X8, ORC_TX_16X32,
+  ORC_TX_32X16, ORC_TX_32X64, ORC_TX_64X32, ORC_TX_4X16, ORC_TX_16X4,
+  ORC_TX_8X32, ORC_TX_32X8, ORC_TX_16X64, ORC_TX_64X16, ORC_TX_SIZES_ALL
+};
+
+int orc_tx_w(int tx_size);
+int orc_tx_h(int tx_size);
+int orc_max_eob(int tx_size);     /* av1_get_max_eob, av1/common/blockd.h:1596 */
+int orc_tx_scale(int tx_size);    /* av1_get_tx_scale, av1/common/idct.c:24 */
+int orc_tx_type_valid(int tx_size, int tx_type); /* test/av1_txfm_test.h:89 */
+
+/* tables */
+int32_t orc_cospi(int cos_bit, int idx);
+int32_t orc_sinpi(int cos_bit, int idx);
+const int32_t *orc_cospi_table(int cos_bit);
+void orc_fwd_shift(int tx_size, int8_t out[3]);
+int orc_fwd_cos_bit_col(int tx_size);
+int orc_fwd_cos_bit_row(int tx_size);
+
+/* 1-D kernels: kind 0=DCT 1=ADST 2=IDENTITY (av1/encoder/av1_fwd_txfm1d.c) */
+void orc_fwd_txfm1d(int kind, int n, const int32_t *in, int32_t *out,
+                    int cos_bit);
+/* inverse 1-D (av1/common/av1_inv_txfm1d.c); stage_range[] as the reference */
+void orc_inv_txfm1d(int kind, int n, const int32_t *in, int32_t *out,
+                    int cos_bit, const int8_t *stage_range);
+
+/* 2-D forward: av1_fwd_txfm2d_WxH_c (av1/encoder/av1_fwd_txfm2d.c:56-312) */
+void orc_fwd_txfm2d(const int16_t *input, int32_t *output, int stride,
+                    int tx_type, int tx_size, int bd);
+/* av1_fwht4x4_c (av1/encoder/hybrid_fwd_txfm.c:24-76) */
+void orc_fwht4x4(const int16_t *input, int32_t *output, int stride);
+
+/* 2-D inverse add: av1_inv_txfm2d_add_WxH_c (av1/common/av1_inv_txfm2d.c) */
+void orc_inv_txfm2d_add(const int32_t *input, uint16_t *output, int stride,
+                        int tx_type, int tx_size, int bd);
+
+/* scans: av1_scan_orders[tx_size][tx_type] (av1/common/scan.c) */
+const int16_t *orc_scan(int tx_size, int tx_type);
+const int16_t *orc_iscan(int tx_size, int tx_type);
+
+/* quantizer tables: av1_build_quantizer (av1/encoder/av1_quantize.c:590-686) */
+typedef struct {
+  int16_t quant[2], quant_shift[2], zbin[2], round[2];
+  int16_t quant_fp[2], round_fp[2], dequant[2];
+} OrcQuant;
+void orc_build_quant(int bd, int qindex, int sharpness, int y_dc_delta_q,
+                     OrcQuant *q);
+int16_t orc_dc_quant(int qindex, int delta, int bd);
+int16_t orc_ac_quant(int qindex, int delta, int bd);
+
+/* quantizers (args as the reference; zbin/round/... point at [2] arrays) */
+void orc_quantize_fp(const int32_t *coeff, intptr_t n, const int16_t *zbin,
+                     const int16_t *round, const int16_t *quant,
+                     const int16_t *quant_shift, int32_t *qcoeff,
+                     int32_t *dqcoeff, const int16_t *dequant, uint16_t *eob,
+                     const int16_t *scan, const int16_t *iscan, int log_scale);
+void orc_quantize_b(const int32_t *coeff, intptr_t n, const int16_t *zbin,
+                    const int16_t *round, const int16_t *quant,
+                    const int16_t *quant_shift, int32_t *qcoeff,
+                    int32_t *dqcoeff, const int16_t *dequant, uint16_t *eob,
+                    const int16_t *scan, const int16_t *iscan, int log_scale);
+void orc_highbd_quantize_fp(const int32_t *coeff, intptr_t n,
+                            const int16_t *zbin, const int16_t *round,
+                            const int16_t *quant, const int16_t *quant_shift,
+                            int32_t *qcoeff, int32_t *dqcoeff,
+                            const int16_t *dequant, uint16_t *eob,
+                            const int16_t *scan, const int16_t *iscan,
+                            int log_scale);
+void orc_highbd_quantize_b(const int32_t *coeff, intptr_t n,
+                           const int16_t *zbin, const int16_t *round,
+                           const int16_t *quant, const int16_t *quant_shift,
+                           int32_t *qcoeff, int32_t *dqcoeff,
+                           const int16_t *dequant, uint16_t *eob,
+                           const int16_t *scan, const int16_t *iscan,
+                           int log_scale);
+
+/* ---- pixel kernels (aom_dsp/ sad, variance, avg, sse, ...) ---- */
+unsigned int orc_sad(const uint8_t *a, int a_stride, const uint8_t *b,
+                     int b_stride, int w, int h);
+unsigned int orc_sad_skip(const uint8_t *a, int a_stride, const uint8_t *b,
+                          int b_stride, int w, int h);
+unsigned int orc_sad_avg(const uint8_t *src, int src_stride,
+                         const uint8_t *ref, int ref_stride, int w, int h,
+                         const uint8_t *second_pred);
+unsigned int orc_highbd_sad(const uint16_t *a, int a_stride, const uint16_t *b,
+                            int b_stride, int w, int h);
+unsigned int orc_variance(const uint8_t *a, int a_stride, const uint8_t *b,
+                          int b_stride, int w, int h, unsigned int *sse);
+unsigned int orc_highbd_variance(const uint16_t *a, int a_stride,
+                                 const uint16_t *b, int b_stride, int w, int h,
+                                 int bd, unsigned int *sse);
+unsigned int orc_sub_pixel_variance(const uint8_t *a, int a_stride,
+                                    int xoffset, int yoffset, const uint8_t *b,
+                                    int b_stride, int w, int h,
+                                    unsigned int *sse);
+unsigned int orc_mse(const uint8_t *a, int a_stride, const uint8_t *b,
+                     int b_stride, int w, int h, unsigned int *sse);
+int64_t orc_sse(const uint8_t *a, int a_stride, const uint8_t *b, int b_stride,
+                int w, int h);
+int64_t orc_highbd_sse(const uint16_t *a, int a_stride, const uint16_t *b,
+                       int b_stride, int w, int h);
+void orc_subtract_block(int rows, int cols, int16_t *diff, ptrdiff_t ds,
+                        const uint8_t *src, ptrdiff_t ss, const uint8_t *pred,
+                        ptrdiff_t ps);
+void orc_highbd_subtract_block(int rows, int cols, int16_t *diff,
+                               ptrdiff_t ds, const uint16_t *src,
+                               ptrdiff_t ss, const uint16_t *pred,
+                               ptrdiff_t ps);
+uint64_t orc_sum_squares_2d_i16(const int16_t *src, int stride, int w, int h);
+void orc_hadamard(int n, const int16_t *src_diff, ptrdiff_t src_stride,
+                  int32_t *coeff);
+int orc_satd(const int32_t *coeff, int length);
+int64_t orc_block_error(const int32_t *coeff, const int32_t *dqcoeff,
+                        intptr_t block_size, int64_t *ssz);
+int64_t orc_highbd_block_error(const int32_t *coeff, const int32_t *dqcoeff,
+                               intptr_t block_size, int64_t *ssz, int bd);
+
+/* ---- C2 pipeline: fwd_txfm + quantize_fp over a residual plane ----
+ * For one tx_size, tile the plane with full blocks (row-major block order),
+ * evaluate each tx_type whose bit is set in type_mask (ascending type order),
+ * write qcoeff/dqcoeff [block][type_slot][n] and eob [block][type_slot].
+ * threads > 1 uses pthreads over block rows.  Returns the number of blocks. */
+long orc_txq_plane(const int16_t *residual, int stride, int width, int height,
+                   int tx_size, unsigned type_mask, int bd,
+                   const OrcQuant *q, int quant_b, int32_t *qcoeff,
+                   int32_t *dqcoeff, uint16_t *eob, int threads);
+
+#ifdef __cplusplus
+}
+#endif
+#endif  // LAVISH_ORACLE_H_

@@ -1,0 +1,235 @@
+"""ctypes binding of the test-only CPU oracle (oracle/liboracle.so).
+
+Test infrastructure: imported only by tests/, __graft_entry__.smoke() and the
+cpu_baseline leg of bench.py.  The product never imports this module."""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ORACLE_DIR = os.path.join(ROOT, "oracle")
+LIB_PATH = os.path.join(ORACLE_DIR, "liboracle.so")
+
+_lib = None
+
+
+def build():
+    subprocess.check_call(["make", "-s", "-C", ORACLE_DIR])
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            build()
+        _lib = ctypes.CDLL(LIB_PATH)
+        _declare(_lib)
+    return _lib
+
+
+def P(a):
+    return a.ctypes.data_as(ctypes.c_void_p)
+
+
+class OrcQuant(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_int16 * 2) for n in
+                ("quant", "quant_shift", "zbin", "round", "quant_fp", "round_fp", "dequant")]
+
+
+def _declare(L):
+    vp, i32, i64 = ctypes.c_void_p, ctypes.c_int, ctypes.c_int64
+    L.orc_fwd_txfm1d.argtypes = [i32, i32, vp, vp, i32]
+    L.orc_inv_txfm1d.argtypes = [i32, i32, vp, vp, i32, vp]
+    L.orc_fwd_txfm2d.argtypes = [vp, vp, i32, i32, i32, i32]
+    L.orc_inv_txfm2d_add.argtypes = [vp, vp, i32, i32, i32, i32]
+    L.orc_fwht4x4.argtypes = [vp, vp, i32]
+    L.orc_scan.restype = ctypes.POINTER(ctypes.c_int16)
+    L.orc_iscan.restype = ctypes.POINTER(ctypes.c_int16)
+    L.orc_cospi.restype = ctypes.c_int32
+    L.orc_sinpi.restype = ctypes.c_int32
+    L.orc_dc_quant.restype = ctypes.c_int16
+    L.orc_ac_quant.restype = ctypes.c_int16
+    L.orc_build_quant.argtypes = [i32, i32, i32, i32, ctypes.POINTER(OrcQuant)]
+    qargs = [vp, ctypes.c_ssize_t, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, i32]
+    for n in ("orc_quantize_fp", "orc_quantize_b", "orc_highbd_quantize_fp",
+              "orc_highbd_quantize_b"):
+        getattr(L, n).argtypes = qargs
+    L.orc_txq_plane.argtypes = [vp, i32, i32, i32, i32, ctypes.c_uint, i32,
+                                ctypes.POINTER(OrcQuant), i32, vp, vp, vp, i32]
+    L.orc_txq_plane.restype = ctypes.c_long
+    L.orc_sad.restype = ctypes.c_uint
+    L.orc_sad.argtypes = [vp, i32, vp, i32, i32, i32]
+    L.orc_sad_skip.restype = ctypes.c_uint
+    L.orc_sad_skip.argtypes = [vp, i32, vp, i32, i32, i32]
+    L.orc_sad_avg.restype = ctypes.c_uint
+    L.orc_sad_avg.argtypes = [vp, i32, vp, i32, i32, i32, vp]
+    L.orc_highbd_sad.restype = ctypes.c_uint
+    L.orc_highbd_sad.argtypes = [vp, i32, vp, i32, i32, i32]
+    L.orc_variance.restype = ctypes.c_uint
+    L.orc_variance.argtypes = [vp, i32, vp, i32, i32, i32, vp]
+    L.orc_mse.restype = ctypes.c_uint
+    L.orc_mse.argtypes = [vp, i32, vp, i32, i32, i32, vp]
+    L.orc_highbd_variance.restype = ctypes.c_uint
+    L.orc_highbd_variance.argtypes = [vp, i32, vp, i32, i32, i32, i32, vp]
+    L.orc_sub_pixel_variance.restype = ctypes.c_uint
+    L.orc_sub_pixel_variance.argtypes = [vp, i32, i32, i32, vp, i32, i32, i32, vp]
+    L.orc_sse.restype = i64
+    L.orc_sse.argtypes = [vp, i32, vp, i32, i32, i32]
+    L.orc_highbd_sse.restype = i64
+    L.orc_highbd_sse.argtypes = [vp, i32, vp, i32, i32, i32]
+    L.orc_subtract_block.argtypes = [i32, i32, vp, ctypes.c_ssize_t, vp,
+                                     ctypes.c_ssize_t, vp, ctypes.c_ssize_t]
+    L.orc_highbd_subtract_block.argtypes = L.orc_subtract_block.argtypes
+    L.orc_sum_squares_2d_i16.restype = ctypes.c_uint64
+    L.orc_sum_squares_2d_i16.argtypes = [vp, i32, i32, i32]
+    L.orc_hadamard.argtypes = [i32, vp, ctypes.c_ssize_t, vp]
+    L.orc_satd.argtypes = [vp, i32]
+    L.orc_block_error.restype = i64
+    L.orc_block_error.argtypes = [vp, vp, ctypes.c_ssize_t, vp]
+    L.orc_highbd_block_error.restype = i64
+    L.orc_highbd_block_error.argtypes = [vp, vp, ctypes.c_ssize_t, vp, i32]
+
+
+TX_W = [4, 8, 16, 32, 64, 4, 8, 8, 16, 16, 32, 32, 64, 4, 16, 8, 32, 16, 64]
+TX_H = [4, 8, 16, 32, 64, 8, 4, 16, 8, 32, 16, 64, 32, 16, 4, 32, 8, 64, 16]
+TX_NAMES = ["4x4", "8x8", "16x16", "32x32", "64x64", "4x8", "8x4", "8x16",
+            "16x8", "16x32", "32x16", "32x64", "64x32", "4x16", "16x4",
+            "8x32", "32x8", "16x64", "64x16"]
+
+
+def max_eob(s):
+    if s in (17, 18):
+        return 512
+    if TX_W[s] == 64 or TX_H[s] == 64:
+        return 1024
+    return TX_W[s] * TX_H[s]
+
+
+def tx_scale(s):
+    p = TX_W[s] * TX_H[s]
+    return int(p > 256) + int(p > 1024)
+
+
+def type_valid(s, t):
+    m = max(TX_W[s], TX_H[s])
+    if m == 64:
+        return t == 0
+    if m == 32:
+        return t in (0, 9)
+    return 0 <= t < 16
+
+
+def fwd_txfm1d(kind, x, cos_bit):
+    x = np.ascontiguousarray(x, dtype=np.int32)
+    y = np.zeros_like(x)
+    lib().orc_fwd_txfm1d(kind, len(x), P(x), P(y), cos_bit)
+    return y
+
+
+def inv_txfm1d(kind, x, cos_bit, stage_range):
+    x = np.ascontiguousarray(x, dtype=np.int32)
+    y = np.zeros_like(x)
+    sr = np.ascontiguousarray(stage_range, dtype=np.int8)
+    lib().orc_inv_txfm1d(kind, len(x), P(x), P(y), cos_bit, P(sr))
+    return y
+
+
+def fwd_txfm2d(block, tx_type, tx_size, bd=8):
+    """block: int16 [H, stride>=W] array; returns int32 coefficient buffer of
+    W*H words (the reference's output buffer, column-major)."""
+    block = np.ascontiguousarray(block, dtype=np.int16)
+    out = np.zeros(TX_W[tx_size] * TX_H[tx_size], dtype=np.int32)
+    lib().orc_fwd_txfm2d(P(block), P(out), block.shape[1], tx_type, tx_size, bd)
+    return out
+
+
+def inv_txfm2d_add(coeff, dst, tx_type, tx_size, bd):
+    coeff = np.ascontiguousarray(coeff, dtype=np.int32)
+    dst = np.ascontiguousarray(dst, dtype=np.uint16).copy()
+    lib().orc_inv_txfm2d_add(P(coeff), P(dst), dst.shape[1], tx_type, tx_size, bd)
+    return dst
+
+
+def scan(tx_size, tx_type):
+    W, H = min(TX_W[tx_size], 32), min(TX_H[tx_size], 32)
+    p = lib().orc_scan(tx_size, tx_type)
+    return np.ctypeslib.as_array(p, shape=(W * H,)).copy()
+
+
+def iscan(tx_size, tx_type):
+    W, H = min(TX_W[tx_size], 32), min(TX_H[tx_size], 32)
+    p = lib().orc_iscan(tx_size, tx_type)
+    return np.ctypeslib.as_array(p, shape=(W * H,)).copy()
+
+
+def build_quant(bd, qindex, sharpness=0, y_dc_delta_q=0):
+    q = OrcQuant()
+    lib().orc_build_quant(bd, qindex, sharpness, y_dc_delta_q, ctypes.byref(q))
+    return q
+
+
+def quant_arrays(q):
+    return {n: np.array(list(getattr(q, n)), dtype=np.int16) for n, _ in OrcQuant._fields_}
+
+
+def quantize(kind, coeff, n, q, scan_, iscan_, log_scale, highbd=False):
+    """kind 'fp' or 'b' with the reference's argument wiring
+    (av1_quantize_fp_facade / av1_quantize_b_facade)."""
+    qa = quant_arrays(q)
+    coeff = np.ascontiguousarray(coeff, dtype=np.int32)
+    qc = np.zeros(n, np.int32)
+    dq = np.zeros(n, np.int32)
+    eob = np.zeros(1, np.uint16)
+    if kind == "fp":
+        rnd, qt = qa["round_fp"], qa["quant_fp"]
+        fn = lib().orc_highbd_quantize_fp if highbd else lib().orc_quantize_fp
+    else:
+        rnd, qt = qa["round"], qa["quant"]
+        fn = lib().orc_highbd_quantize_b if highbd else lib().orc_quantize_b
+    sc = np.ascontiguousarray(scan_, np.int16)
+    isc = np.ascontiguousarray(iscan_, np.int16)
+    fn(P(coeff), n, P(qa["zbin"]), P(rnd), P(qt), P(qa["quant_shift"]), P(qc),
+       P(dq), P(qa["dequant"]), P(eob), P(sc), P(isc), log_scale)
+    return qc, dq, int(eob[0])
+
+
+def txq_plane(residual, tx_size, type_mask, q, bd=8, quant_b=False, threads=1):
+    residual = np.ascontiguousarray(residual, dtype=np.int16)
+    H, W = residual.shape
+    bw, bh = W // TX_W[tx_size], H // TX_H[tx_size]
+    nt = bin(type_mask).count("1")
+    n = max_eob(tx_size)
+    qc = np.zeros((bh * bw, nt, n), np.int32)
+    dq = np.zeros((bh * bw, nt, n), np.int32)
+    eob = np.zeros((bh * bw, nt), np.uint16)
+    lib().orc_txq_plane(P(residual), W, W, H, tx_size, type_mask, bd,
+                        ctypes.byref(q), int(quant_b), P(qc), P(dq), P(eob), threads)
+    return qc, dq, eob
+
+
+class ACMRandom:
+    """test/acm_random.h over gtest's LCG (gtest.cc:378-381)."""
+
+    def __init__(self, seed=0xBABA):
+        self.state = seed
+
+    def _gen(self, rng):
+        self.state = (1103515245 * self.state + 12345) % (1 << 31)
+        return self.state % rng
+
+    def rand31(self):
+        return self._gen(1 << 31)
+
+    def rand16(self):
+        return (self._gen(1 << 31) >> 15) & 0xFFFF
+
+    def rand8(self):
+        return (self._gen(1 << 31) >> 23) & 0xFF
+
+    def rand12(self):
+        return (self._gen(1 << 31) >> 19) & 0xFFF
+
+    def pseudo_uniform(self, r):
+        return self._gen(r)
