@@ -1,0 +1,43 @@
+// lavish_internal.h -- host-side plumbing shared by the HIP translation units
+// of liblavish_hip.so (error reporting, tables, launch helpers).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+
+#include "../../include/lavish_dsp.h"
+
+namespace lavish {
+
+// Sticky status (lavish_hip_status): the reference's DSP entry points have no
+// error channel (void / value returns), so a device failure is recorded here
+// and reported loudly on stderr; by default the process aborts, because a
+// silent wrong answer is worse than a crash for an encoder.
+void set_error(const char* what, hipError_t e, const char* file, int line);
+
+#define LAVISH_CHECK(x)                                              \
+  do {                                                               \
+    hipError_t e__ = (x);                                            \
+    if (e__ != hipSuccess) ::lavish::set_error(#x, e__, __FILE__, __LINE__); \
+  } while (0)
+
+int tx_w(int tx_size);
+int tx_h(int tx_size);
+int max_eob(int tx_size);
+int tx_scale(int tx_size);
+bool tx_type_valid(int tx_size, int tx_type);
+int scan_kind(int tx_type);  // 0 default, 1 mcol, 2 mrow
+
+// host copies of the scan / inverse-scan orders (av1_scan_orders)
+const int16_t* host_scan(int tx_size, int tx_type);
+const int16_t* host_iscan(int tx_size, int tx_type);
+// device copies (uploaded on first use, per device)
+const int16_t* dev_iscan(int tx_size, int tx_type);
+const int16_t* dev_scan(int tx_size, int tx_type);
+
+// per-thread scratch device buffer for the per-call (host pointer) shims
+void* shim_scratch(size_t bytes);
+hipStream_t shim_stream();
+
+}  // namespace lavish

@@ -1,0 +1,370 @@
+// txq.hip -- batched forward transform + quantization for gfx950.
+//
+// The reference evaluates, per TX block and per candidate TX type, av1_xform
+// (av1/encoder/encodemb.c:295 -> hybrid_fwd_txfm.c:233-313 ->
+// av1_fwd_txfm2d.c:56-127) followed by av1_quant (encodemb.c:308 ->
+// av1_quantize.c:36-122 / aom_dsp/quantize.c:108-169), one block at a time
+// on one CPU thread.  Here one 256-thread workgroup owns P = 256/min(W,H)
+// blocks of one TX size and walks every requested TX type over them:
+//
+//   residual (HBM, read once) -> registers (one column per thread)
+//   per type: column 1-D transform (registers) -> LDS t1 (padded rows)
+//             row 1-D transform + fp/b quantizer + eob reduction
+//                                               -> LDS t2 (coefficient order)
+//             coalesced 16-byte copy-out of qcoeff, dqcoeff (recomputed from
+//             qcoeff: dq = sign * ((|q| * dequant) >> log_scale))
+//
+// The transforms are fully unrolled straight-line integer code (txfm_dev.h);
+// no MFMA: AV1 butterflies with per-stage 64-bit rounding are not a matrix
+// product.  HBM traffic is the residual once plus 8 bytes per output
+// coefficient per type, so the kernel is bounded by the output write stream.
+#include "lavish_internal.h"
+#include "txfm_dev.h"
+
+namespace lavish {
+
+struct QP {
+  int16_t zbin[2], round[2], quant[2], quant_shift[2], dequant[2];
+};
+
+struct TxqArgs {
+  const int16_t* res;
+  int stride;
+  int bw;       // blocks per row
+  int nblocks;  // total blocks
+  int ntypes;
+  int types[16];
+  int quant_kind;
+  int highbd;
+  QP qp;
+  const int16_t* iscan_default;  // default-scan inverse table (n entries)
+  int32_t* qcoeff;
+  int32_t* dqcoeff;
+  uint16_t* eob;
+  int32_t* coeff;
+};
+
+// vtx_tab / htx_tab (av1/common/common_data.h:149-159): 0 DCT 1 ADST 2 FLIPADST 3 IDTX
+// packed 2 bits per type (a runtime-indexed array would live in scratch)
+constexpr uint32_t pack2(const uint8_t (&v)[16]) {
+  uint32_t r = 0;
+  for (int i = 0; i < 16; ++i) r |= (uint32_t)v[i] << (2 * i);
+  return r;
+}
+constexpr uint8_t kVtxTab[16] = {0, 1, 0, 1, 2, 0, 2, 1, 2, 3, 0, 3, 1, 3, 2, 3};
+constexpr uint8_t kHtxTab[16] = {0, 0, 1, 1, 0, 2, 2, 2, 1, 3, 3, 0, 3, 1, 3, 2};
+constexpr uint32_t kVtxPacked = pack2(kVtxTab);
+constexpr uint32_t kHtxPacked = pack2(kHtxTab);
+
+// one coefficient through av1_quantize_fp / aom_quantize_b (lowbd clamps the
+// rounded magnitude to int16, highbd does not).  Returns the signed qcoeff.
+// pick [0] (DC) or [1] (AC) without a runtime-indexed array (which would go
+// to scratch)
+__device__ __forceinline__ int32_t pick(const int16_t (&v)[2], int ac) {
+  return ac ? v[1] : v[0];
+}
+
+// one coefficient through av1_quantize_fp / aom_quantize_b (lowbd clamps the
+// rounded magnitude to int16, highbd does not).  Returns the signed qcoeff.
+template <int LS>
+__device__ __forceinline__ int32_t quant_one(int32_t c, int ac, int kind,
+                                             int highbd, const QP& qp) {
+  const int32_t sgn = c >> 31;
+  const int32_t a = (c ^ sgn) - sgn;
+  const int32_t deq = pick(qp.dequant, ac);
+  const int32_t rnd = (pick(qp.round, ac) + ((1 << LS) >> 1)) >> LS;
+  const int32_t qt = pick(qp.quant, ac);
+  int32_t q = 0;
+  if (kind == LAVISH_QUANT_FP) {
+    if (((int64_t)a << (1 + LS)) >= deq) {
+      int64_t t = (int64_t)a + rnd;
+      if (!highbd) t = t > 32767 ? 32767 : (t < -32768 ? -32768 : t);
+      q = (int32_t)((t * qt) >> (16 - LS));
+    }
+  } else {
+    const int32_t zb = (pick(qp.zbin, ac) + ((1 << LS) >> 1)) >> LS;
+    if (a >= zb) {
+      int64_t t = (int64_t)a + rnd;
+      if (!highbd) t = t > 32767 ? 32767 : (t < -32768 ? -32768 : t);
+      const int64_t tw = t * 32;  // qm weight 1 << AOM_QM_BITS
+      q = (int32_t)(((((tw * qt) >> 16) + tw) * pick(qp.quant_shift, ac)) >> (16 - LS + 5));
+    }
+  }
+  return (q ^ sgn) - sgn;
+}
+
+template <int LS>
+__device__ __forceinline__ int32_t dequant_one(int32_t q, int ac, const QP& qp) {
+  const int32_t sgn = q >> 31;
+  const int32_t aq = (q ^ sgn) - sgn;
+  const int32_t adq = (int32_t)((uint32_t)aq * (uint32_t)pick(qp.dequant, ac)) >> LS;
+  return (adq ^ sgn) - sgn;
+}
+
+template <int W, int H>
+__global__ __launch_bounds__(256, 2) void txq_plane_kernel(TxqArgs a) {
+  using C = TxCfg<W, H>;
+  constexpr int MN = W < H ? W : H;
+  constexpr int P = 256 / MN;   // blocks per workgroup
+  constexpr int CPT = W / MN;   // column transforms per thread
+  constexpr int RPT = H / MN;   // row transforms per thread
+  constexpr int N = W * H;      // coefficients per block (sizes <= 32)
+  constexpr int T1S = W + 1;    // padded LDS row stride: conflict-free row reads
+  constexpr int LS = C::log_scale;
+  __shared__ int32_t t1[P * H * T1S];
+  __shared__ __attribute__((aligned(16))) int32_t t2[P * N];
+  __shared__ int16_t isc[N];
+
+  const int tid = threadIdx.x;
+  const int blk0 = blockIdx.x * P;
+  const int nvalid = min(P, a.nblocks - blk0);
+
+  for (int i = tid; i < N; i += 256) isc[i] = a.iscan_default[i];
+
+  // residual columns -> registers (read once for all TX types)
+  int32_t res[CPT][H];
+#pragma unroll
+  for (int k = 0; k < CPT; ++k) {
+    const int j = k * 256 + tid;
+    const int b = j / W, c = j % W;
+    const int blk = blk0 + b;
+    if (b < nvalid) {
+      const int by = blk / a.bw, bx = blk - by * a.bw;
+      const int16_t* src = a.res + (size_t)by * H * a.stride + bx * W + c;
+#pragma unroll
+      for (int r = 0; r < H; ++r) res[k][r] = src[(size_t)r * a.stride];
+    } else {
+#pragma unroll
+      for (int r = 0; r < H; ++r) res[k][r] = 0;
+    }
+  }
+  __syncthreads();
+
+  for (int ti = 0; ti < a.ntypes; ++ti) {
+    // wave-uniform by construction; readfirstlane keeps the transform-kind
+    // branches scalar (otherwise hipcc if-converts all three kernels)
+    const int t = __builtin_amdgcn_readfirstlane(a.types[ti]);
+    const int vt = (kVtxPacked >> (2 * t)) & 3, ht = (kHtxPacked >> (2 * t)) & 3;
+    const int kc = vt == 3 ? 2 : (vt == 0 ? 0 : 1);
+    const int kr = ht == 3 ? 2 : (ht == 0 ? 0 : 1);
+    const bool ud = vt == 2, lr = ht == 2;
+    const int skind = t < 10 ? 0 : ((t & 1) ? 1 : 2);
+
+    // ---- columns (av1_fwd_txfm2d.c:88-106) ----
+#pragma unroll
+    for (int k = 0; k < CPT; ++k) {
+      const int j = k * 256 + tid;
+      const int b = j / W, c = j % W;
+      int32_t in[H], out[H];
+#pragma unroll
+      for (int r = 0; r < H; ++r)
+        in[r] = round_shift_1<-C::s0>(ud ? res[k][H - 1 - r] : res[k][r]);
+      fwd_1d<H, C::cos_bit_col>(kc, in, out);
+      const int cc = lr ? W - 1 - c : c;
+#pragma unroll
+      for (int r = 0; r < H; ++r)
+        t1[(b * H + r) * T1S + cc] = round_shift_1<-C::s1>(out[r]);
+    }
+    __syncthreads();
+
+    // ---- rows + quantization (av1_fwd_txfm2d.c:110-126, av1_quantize.c) ----
+#pragma unroll
+    for (int k = 0; k < RPT; ++k) {
+      const int j = k * 256 + tid;
+      const int b = j / H, r = j % H;
+      int32_t in[W], out[W];
+#pragma unroll
+      for (int c = 0; c < W; ++c) in[c] = t1[(b * H + r) * T1S + c];
+      fwd_1d<W, C::cos_bit_row>(kr, in, out);
+      int last = 0;
+      const size_t obase = ((size_t)ti * a.nblocks + blk0 + b) * N;
+#pragma unroll
+      for (int c = 0; c < W; ++c) {
+        int32_t v = round_shift_1<-C::s2>(out[c]);
+        if constexpr (C::rect2) v = rshift64((int64_t)v * 5793, 12);
+        const int rc = c * H + r;
+        if (a.coeff != nullptr && b < nvalid) a.coeff[obase + rc] = v;
+        int32_t q = 0;
+        if (a.quant_kind != LAVISH_QUANT_NONE)
+          q = quant_one<LS>(v, rc != 0, a.quant_kind, a.highbd, a.qp);
+        t2[b * N + rc] = q;
+        const int pos = skind == 0 ? isc[rc] : (skind == 1 ? rc : r * W + c);
+        if (q != 0) last = max(last, pos + 1);
+      }
+#pragma unroll
+      for (int m = 1; m < H; m <<= 1) last = max(last, __shfl_xor(last, m));
+      if (r == 0 && b < nvalid && a.eob != nullptr)
+        a.eob[(size_t)ti * a.nblocks + blk0 + b] = (uint16_t)last;
+    }
+    __syncthreads();
+
+    // ---- coalesced copy-out of qcoeff / dqcoeff ----
+    if (a.qcoeff != nullptr) {
+      const int total = nvalid * N;
+      const size_t gbase = ((size_t)ti * a.nblocks + blk0) * N;
+      for (int i = tid * 4; i < total; i += 256 * 4) {
+        const int4 q4 = *reinterpret_cast<const int4*>(&t2[i]);
+        *reinterpret_cast<int4*>(&a.qcoeff[gbase + i]) = q4;
+        if (a.dqcoeff != nullptr) {
+          const int rc0 = i % N;  // N % 4 == 0: all four share the block
+          int4 d4;
+          d4.x = dequant_one<LS>(q4.x, rc0 != 0, a.qp);
+          d4.y = dequant_one<LS>(q4.y, 1, a.qp);
+          d4.z = dequant_one<LS>(q4.z, 1, a.qp);
+          d4.w = dequant_one<LS>(q4.w, 1, a.qp);
+          *reinterpret_cast<int4*>(&a.dqcoeff[gbase + i]) = d4;
+        }
+      }
+    }
+  }
+}
+
+// generic quantizer: one workgroup per block, any scan order.
+template <int LS>
+__global__ __launch_bounds__(256) void quant_kernel(const int32_t* coeff, int n,
+                                                     const int16_t* scan, int kind,
+                                                     int highbd, QP qp,
+                                                     int32_t* qcoeff, int32_t* dqcoeff,
+                                                     uint16_t* eob) {
+  __shared__ int red[4];
+  const size_t base = (size_t)blockIdx.x * n;
+  const int tid = threadIdx.x;
+  int last = 0;
+  for (int i = tid; i < n; i += 256) {
+    const int rc = scan[i];
+    const int32_t q = quant_one<LS>(coeff[base + rc], rc != 0, kind, highbd, qp);
+    qcoeff[base + rc] = q;
+    dqcoeff[base + rc] = dequant_one<LS>(q, rc != 0, qp);
+    if (q != 0) last = max(last, i + 1);
+  }
+#pragma unroll
+  for (int m = 1; m < 64; m <<= 1) last = max(last, __shfl_xor(last, m));
+  if ((tid & 63) == 0) red[tid >> 6] = last;
+  __syncthreads();
+  if (tid == 0) eob[blockIdx.x] = (uint16_t)max(max(red[0], red[1]), max(red[2], red[3]));
+}
+
+// ----------------------------------------------------------------------------
+// launchers
+// ----------------------------------------------------------------------------
+template <int W, int H>
+static void launch_plane(const TxqArgs& a, hipStream_t s) {
+  constexpr int MN = W < H ? W : H;
+  constexpr int P = 256 / MN;
+  const int grid = (a.nblocks + P - 1) / P;
+  if (grid == 0) return;
+  hipLaunchKernelGGL((txq_plane_kernel<W, H>), dim3(grid), dim3(256), 0, s, a);
+  LAVISH_CHECK(hipGetLastError());
+}
+
+static QP to_qp(const LavishQuantParams* p) {
+  QP q{};
+  if (p) {
+    for (int i = 0; i < 2; ++i) {
+      q.zbin[i] = p->zbin[i];
+      q.round[i] = p->round[i];
+      q.quant[i] = p->quant[i];
+      q.quant_shift[i] = p->quant_shift[i];
+      q.dequant[i] = p->dequant[i];
+    }
+  }
+  return q;
+}
+
+int txq_plane(const int16_t* residual, int stride, int width, int height, int tx_size,
+              uint32_t type_mask, int bd, int quant_kind, const LavishQuantParams* qp,
+              int32_t* qcoeff, int32_t* dqcoeff, uint16_t* eob, int32_t* coeff,
+              hipStream_t s) {
+  if (tx_size < 0 || tx_size >= 19) return -1;
+  const int W = tx_w(tx_size), H = tx_h(tx_size);
+  if (W > 32 || H > 32) return -2;  // 64-point sizes: see DESIGN.md (next)
+  if (quant_kind < 0 || quant_kind > 2) return -3;
+  if (quant_kind != LAVISH_QUANT_NONE && qp == nullptr) return -3;
+  if (width <= 0 || height <= 0 || stride < width) return -4;
+  TxqArgs a{};
+  a.res = residual;
+  a.stride = stride;
+  a.bw = width / W;
+  a.nblocks = (width / W) * (height / H);
+  for (int t = 0; t < 16; ++t) {
+    if (!((type_mask >> t) & 1)) continue;
+    if (!tx_type_valid(tx_size, t)) return -5;
+    a.types[a.ntypes++] = t;
+  }
+  if (a.ntypes == 0) return -5;
+  a.quant_kind = quant_kind;
+  a.highbd = bd > 8;
+  a.qp = to_qp(qp);
+  a.iscan_default = dev_iscan(tx_size, 0);
+  a.qcoeff = qcoeff;
+  a.dqcoeff = dqcoeff;
+  a.eob = eob;
+  a.coeff = coeff;
+  switch (tx_size) {
+    case 0: launch_plane<4, 4>(a, s); break;
+    case 1: launch_plane<8, 8>(a, s); break;
+    case 2: launch_plane<16, 16>(a, s); break;
+    case 3: launch_plane<32, 32>(a, s); break;
+    case 5: launch_plane<4, 8>(a, s); break;
+    case 6: launch_plane<8, 4>(a, s); break;
+    case 7: launch_plane<8, 16>(a, s); break;
+    case 8: launch_plane<16, 8>(a, s); break;
+    case 9: launch_plane<16, 32>(a, s); break;
+    case 10: launch_plane<32, 16>(a, s); break;
+    case 13: launch_plane<4, 16>(a, s); break;
+    case 14: launch_plane<16, 4>(a, s); break;
+    case 15: launch_plane<8, 32>(a, s); break;
+    case 16: launch_plane<32, 8>(a, s); break;
+    default: return -2;
+  }
+  return 0;
+}
+
+int quantize_batch(const int32_t* coeff, int n, int nblocks, const int16_t* scan,
+                   int log_scale, int bd, int quant_kind, const LavishQuantParams* qp,
+                   int32_t* qcoeff, int32_t* dqcoeff, uint16_t* eob, hipStream_t s) {
+  if (n <= 0 || nblocks <= 0 || qp == nullptr) return -1;
+  if (quant_kind != LAVISH_QUANT_FP && quant_kind != LAVISH_QUANT_B) return -3;
+  const QP q = to_qp(qp);
+  const int hb = bd > 8;
+  switch (log_scale) {
+    case 0:
+      hipLaunchKernelGGL(quant_kernel<0>, dim3(nblocks), dim3(256), 0, s, coeff, n, scan,
+                         quant_kind, hb, q, qcoeff, dqcoeff, eob);
+      break;
+    case 1:
+      hipLaunchKernelGGL(quant_kernel<1>, dim3(nblocks), dim3(256), 0, s, coeff, n, scan,
+                         quant_kind, hb, q, qcoeff, dqcoeff, eob);
+      break;
+    case 2:
+      hipLaunchKernelGGL(quant_kernel<2>, dim3(nblocks), dim3(256), 0, s, coeff, n, scan,
+                         quant_kind, hb, q, qcoeff, dqcoeff, eob);
+      break;
+    default:
+      return -2;
+  }
+  LAVISH_CHECK(hipGetLastError());
+  return 0;
+}
+
+}  // namespace lavish
+
+extern "C" int lavish_txq_plane(const int16_t* residual, int stride, int width, int height,
+                                int tx_size, uint32_t type_mask, int bit_depth,
+                                int quant_kind, const LavishQuantParams* qp,
+                                int32_t* qcoeff, int32_t* dqcoeff, uint16_t* eob,
+                                int32_t* coeff, void* stream) {
+  return lavish::txq_plane(residual, stride, width, height, tx_size, type_mask, bit_depth,
+                           quant_kind, qp, qcoeff, dqcoeff, eob, coeff,
+                           (hipStream_t)stream);
+}
+
+extern "C" int lavish_quantize_batch(const int32_t* coeff, int n, int nblocks,
+                                     const int16_t* scan, const int16_t* iscan,
+                                     int log_scale, int bit_depth, int quant_kind,
+                                     const LavishQuantParams* qp, int32_t* qcoeff,
+                                     int32_t* dqcoeff, uint16_t* eob, void* stream) {
+  (void)iscan;  // the reference quantizers walk `scan` only
+  return lavish::quantize_batch(coeff, n, nblocks, scan, log_scale, bit_depth, quant_kind,
+                                qp, qcoeff, dqcoeff, eob, (hipStream_t)stream);
+}

@@ -1,0 +1,264 @@
+"""lavish_dsp -- host-side mirror of the reference's RTCD DSP entry points for
+the MI355X backend (liblavish_hip.so).
+
+Two layers, as in include/lavish_dsp.h:
+
+* per-call functions named exactly like the reference's rtcd entries
+  (``av1_fwd_txfm2d_4x4``, ``av1_quantize_fp``, ``aom_quantize_b_32x32`` ...)
+  taking numpy arrays with the reference's argument meaning -- they call the
+  ``*_hip`` C shims, which run the HIP kernels;
+* batch functions (``txq_plane``, ``quantize_batch``) on torch device tensors,
+  launched asynchronously on the current torch stream.
+
+There is no CPU fallback: if liblavish_hip.so is missing the import fails.
+"""
+import ctypes
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(os.path.dirname(_HERE), "liblavish_hip.so")
+
+if not os.path.exists(LIB_PATH):
+    raise ImportError(
+        "liblavish_hip.so not found at %s -- build it with `make -C aom-av1-lavish_amd` "
+        "(or __graft_entry__.build()); there is no CPU fallback" % LIB_PATH)
+
+_lib = ctypes.CDLL(LIB_PATH)
+
+TX_SIZES = ["4x4", "8x8", "16x16", "32x32", "64x64", "4x8", "8x4", "8x16", "16x8",
+            "16x32", "32x16", "32x64", "64x32", "4x16", "16x4", "8x32", "32x8", "16x64",
+            "64x16"]
+TX_W = [4, 8, 16, 32, 64, 4, 8, 8, 16, 16, 32, 32, 64, 4, 16, 8, 32, 16, 64]
+TX_H = [4, 8, 16, 32, 64, 8, 4, 16, 8, 32, 16, 64, 32, 16, 4, 32, 8, 64, 16]
+TX_TYPES = ["DCT_DCT", "ADST_DCT", "DCT_ADST", "ADST_ADST", "FLIPADST_DCT", "DCT_FLIPADST",
+            "FLIPADST_FLIPADST", "ADST_FLIPADST", "FLIPADST_ADST", "IDTX", "V_DCT", "H_DCT",
+            "V_ADST", "H_ADST", "V_FLIPADST", "H_FLIPADST"]
+QUANT_FP, QUANT_B, QUANT_NONE = 0, 1, 2
+
+
+def max_eob(tx_size):
+    """av1_get_max_eob (av1/common/blockd.h:1596-1604)."""
+    if tx_size in (17, 18):
+        return 512
+    if TX_W[tx_size] == 64 or TX_H[tx_size] == 64:
+        return 1024
+    return TX_W[tx_size] * TX_H[tx_size]
+
+
+def tx_scale(tx_size):
+    """av1_get_tx_scale (av1/common/idct.c:24-28)."""
+    p = TX_W[tx_size] * TX_H[tx_size]
+    return int(p > 256) + int(p > 1024)
+
+
+def tx_type_valid(tx_size, tx_type):
+    m = max(TX_W[tx_size], TX_H[tx_size])
+    if m == 64:
+        return tx_type == 0
+    if m == 32:
+        return tx_type in (0, 9)
+    return 0 <= tx_type < 16
+
+
+def valid_type_mask(tx_size):
+    return sum(1 << t for t in range(16) if tx_type_valid(tx_size, t))
+
+
+class TxfmParam(ctypes.Structure):
+    """TxfmParam (aom_dsp/txfm_common.h:89-101)."""
+    _fields_ = [("tx_type", ctypes.c_uint8), ("tx_size", ctypes.c_uint8),
+                ("lossless", ctypes.c_int), ("bd", ctypes.c_int), ("is_hbd", ctypes.c_int),
+                ("tx_set_type", ctypes.c_uint8), ("eob", ctypes.c_int)]
+
+
+class QuantParams(ctypes.Structure):
+    """LavishQuantParams: [0] = DC, [1] = AC."""
+    _fields_ = [(n, ctypes.c_int16 * 2) for n in
+                ("zbin", "round", "quant", "quant_shift", "dequant")]
+
+    def as_dict(self):
+        return {n: np.array(list(getattr(self, n)), np.int16) for n, _ in self._fields_}
+
+
+_vp, _i32, _i64 = ctypes.c_void_p, ctypes.c_int, ctypes.c_int64
+_lib.lavish_hip_status.restype = _i32
+_lib.lavish_hip_status_string.restype = ctypes.c_char_p
+_lib.lavish_hip_set_abort_on_error.argtypes = [_i32]
+_lib.lavish_hip_init.argtypes = [_i32]
+_lib.lavish_hip_version.restype = _i32
+_lib.lavish_build_quant_params.argtypes = [_i32, _i32, _i32, _i32, _i32,
+                                           ctypes.POINTER(QuantParams)]
+_lib.lavish_scan.restype = ctypes.POINTER(ctypes.c_int16)
+_lib.lavish_scan.argtypes = [_i32, _i32]
+_lib.lavish_iscan.restype = ctypes.POINTER(ctypes.c_int16)
+_lib.lavish_iscan.argtypes = [_i32, _i32]
+_lib.lavish_txq_plane.argtypes = [_vp, _i32, _i32, _i32, _i32, ctypes.c_uint32, _i32, _i32,
+                                  ctypes.POINTER(QuantParams), _vp, _vp, _vp, _vp, _vp]
+_lib.lavish_txq_plane.restype = _i32
+_lib.lavish_quantize_batch.argtypes = [_vp, _i32, _i32, _vp, _vp, _i32, _i32, _i32,
+                                       ctypes.POINTER(QuantParams), _vp, _vp, _vp, _vp]
+_lib.lavish_quantize_batch.restype = _i32
+
+_FWD2D = {}
+for _s, _name in enumerate(TX_SIZES):
+    if TX_W[_s] <= 32 and TX_H[_s] <= 32:
+        f = getattr(_lib, "av1_fwd_txfm2d_%s_hip" % _name)
+        f.argtypes = [_vp, _vp, _i32, ctypes.c_uint8, _i32]
+        f.restype = None
+        _FWD2D[_s] = f
+_lib.av1_lowbd_fwd_txfm_hip.argtypes = [_vp, _vp, _i32, ctypes.POINTER(TxfmParam)]
+
+_QARGS = [_vp, ctypes.c_ssize_t, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]
+_QUANT_NAMES = ["av1_quantize_fp", "av1_quantize_fp_32x32", "av1_quantize_fp_64x64",
+                "aom_quantize_b", "aom_quantize_b_32x32", "aom_quantize_b_64x64",
+                "aom_highbd_quantize_b", "aom_highbd_quantize_b_32x32",
+                "aom_highbd_quantize_b_64x64"]
+for _n in _QUANT_NAMES:
+    getattr(_lib, _n + "_hip").argtypes = _QARGS
+_lib.av1_highbd_quantize_fp_hip.argtypes = _QARGS + [_i32]
+
+
+def lib():
+    return _lib
+
+
+def status():
+    return _lib.lavish_hip_status(), _lib.lavish_hip_status_string().decode()
+
+
+def _p(a):
+    return a.ctypes.data_as(ctypes.c_void_p)
+
+
+# ---------------------------------------------------------------- tables --
+def build_quant_params(bit_depth, qindex, kind=QUANT_FP, quant_sharpness=0, y_dc_delta_q=0):
+    """av1_build_quantizer row for luma at `qindex` (av1/encoder/av1_quantize.c:590)."""
+    q = QuantParams()
+    rc = _lib.lavish_build_quant_params(bit_depth, qindex, quant_sharpness, y_dc_delta_q,
+                                        kind, ctypes.byref(q))
+    if rc != 0:
+        raise ValueError("lavish_build_quant_params(%d, %d) failed" % (bit_depth, qindex))
+    return q
+
+
+def scan_order(tx_size, tx_type):
+    """(scan, iscan) of av1_scan_orders[tx_size][tx_type]."""
+    n = min(TX_W[tx_size], 32) * min(TX_H[tx_size], 32)
+    s = np.ctypeslib.as_array(_lib.lavish_scan(tx_size, tx_type), shape=(n,)).copy()
+    i = np.ctypeslib.as_array(_lib.lavish_iscan(tx_size, tx_type), shape=(n,)).copy()
+    return s, i
+
+
+# ------------------------------------------------- per-call RTCD mirror --
+def _fwd2d(tx_size):
+    def fn(input, output, stride, tx_type, bd):
+        """av1_fwd_txfm2d_%s (av1/common/av1_rtcd_defs.pl:358-399): int16
+        residual rows of `stride` -> int32 coefficient buffer (column-major)."""
+        assert input.dtype == np.int16 and output.dtype == np.int32
+        assert input.size >= (TX_H[tx_size] - 1) * stride + TX_W[tx_size]
+        assert output.size >= TX_W[tx_size] * TX_H[tx_size]
+        _FWD2D[tx_size](_p(input), _p(output), stride, tx_type, bd)
+    fn.__name__ = "av1_fwd_txfm2d_" + TX_SIZES[tx_size]
+    return fn
+
+
+for _s in _FWD2D:
+    globals()["av1_fwd_txfm2d_" + TX_SIZES[_s]] = _fwd2d(_s)
+
+
+def av1_lowbd_fwd_txfm(src_diff, coeff, diff_stride, txfm_param):
+    _lib.av1_lowbd_fwd_txfm_hip(_p(src_diff), _p(coeff), diff_stride, ctypes.byref(txfm_param))
+
+
+def _quant(name):
+    cfn = getattr(_lib, name + "_hip")
+
+    def fn(coeff_ptr, n_coeffs, zbin_ptr, round_ptr, quant_ptr, quant_shift_ptr, qcoeff_ptr,
+           dqcoeff_ptr, dequant_ptr, eob_ptr, scan, iscan):
+        cfn(_p(coeff_ptr), n_coeffs, _p(zbin_ptr), _p(round_ptr), _p(quant_ptr),
+            _p(quant_shift_ptr), _p(qcoeff_ptr), _p(dqcoeff_ptr), _p(dequant_ptr), _p(eob_ptr),
+            _p(scan), _p(iscan))
+    fn.__name__ = name
+    return fn
+
+
+for _n in _QUANT_NAMES:
+    globals()[_n] = _quant(_n)
+
+
+def av1_highbd_quantize_fp(coeff_ptr, count, zbin_ptr, round_ptr, quant_ptr, quant_shift_ptr,
+                           qcoeff_ptr, dqcoeff_ptr, dequant_ptr, eob_ptr, scan, iscan,
+                           log_scale):
+    _lib.av1_highbd_quantize_fp_hip(_p(coeff_ptr), count, _p(zbin_ptr), _p(round_ptr),
+                                    _p(quant_ptr), _p(quant_shift_ptr), _p(qcoeff_ptr),
+                                    _p(dqcoeff_ptr), _p(dequant_ptr), _p(eob_ptr), _p(scan),
+                                    _p(iscan), log_scale)
+
+
+# ---------------------------------------------------------- batch layer --
+def _stream_ptr(stream):
+    import torch
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return ctypes.c_void_p(s.cuda_stream)
+
+
+def txq_plane_out(residual, tx_size, type_mask, with_coeff=False):
+    """Allocate the output tensors of txq_plane for a residual plane."""
+    import torch
+    H, W = residual.shape
+    nb = (W // TX_W[tx_size]) * (H // TX_H[tx_size])
+    nt = bin(type_mask).count("1")
+    n = max_eob(tx_size)
+    dev = residual.device
+    out = {
+        "qcoeff": torch.empty((nt, nb, n), dtype=torch.int32, device=dev),
+        "dqcoeff": torch.empty((nt, nb, n), dtype=torch.int32, device=dev),
+        "eob": torch.empty((nt, nb), dtype=torch.int16, device=dev),
+    }
+    if with_coeff:
+        out["coeff"] = torch.empty((nt, nb, n), dtype=torch.int32, device=dev)
+    return out
+
+
+def txq_plane(residual, tx_size, type_mask, qp, bit_depth=8, quant_kind=QUANT_FP, out=None,
+              stride=None, width=None, height=None, with_coeff=False, stream=None):
+    """Batch fwd transform + quantize of every full `tx_size` block of a device
+    int16 residual plane for every type in `type_mask` (see lavish_txq_plane).
+    Returns dict of tensors qcoeff/dqcoeff [slot, block, n], eob [slot, block]
+    (uint16 values stored in an int16 tensor)."""
+    import torch
+    assert residual.dtype == torch.int16 and residual.is_cuda
+    Hh, Ww = residual.shape
+    stride = residual.stride(0) if stride is None else stride
+    width = Ww if width is None else width
+    height = Hh if height is None else height
+    if out is None:
+        out = txq_plane_out(residual[:height, :width], tx_size, type_mask, with_coeff)
+    coeff = out.get("coeff")
+    rc = _lib.lavish_txq_plane(
+        ctypes.c_void_p(residual.data_ptr()), stride, width, height, tx_size, type_mask,
+        bit_depth, quant_kind, ctypes.byref(qp) if qp is not None else None,
+        ctypes.c_void_p(out["qcoeff"].data_ptr()), ctypes.c_void_p(out["dqcoeff"].data_ptr()),
+        ctypes.c_void_p(out["eob"].data_ptr()),
+        ctypes.c_void_p(coeff.data_ptr()) if coeff is not None else None, _stream_ptr(stream))
+    if rc != 0:
+        raise ValueError("lavish_txq_plane rejected arguments (rc=%d)" % rc)
+    return out
+
+
+def quantize_batch(coeff, scan, log_scale, qp, bit_depth=8, quant_kind=QUANT_FP, stream=None):
+    """Quantize coeff[nblocks, n] (device int32) with one scan order."""
+    import torch
+    nb, n = coeff.shape
+    q = torch.empty_like(coeff)
+    dq = torch.empty_like(coeff)
+    eob = torch.empty((nb,), dtype=torch.int16, device=coeff.device)
+    rc = _lib.lavish_quantize_batch(
+        ctypes.c_void_p(coeff.data_ptr()), n, nb, ctypes.c_void_p(scan.data_ptr()), None,
+        log_scale, bit_depth, quant_kind, ctypes.byref(qp), ctypes.c_void_p(q.data_ptr()),
+        ctypes.c_void_p(dq.data_ptr()), ctypes.c_void_p(eob.data_ptr()), _stream_ptr(stream))
+    if rc != 0:
+        raise ValueError("lavish_quantize_batch rejected arguments (rc=%d)" % rc)
+    return q, dq, eob

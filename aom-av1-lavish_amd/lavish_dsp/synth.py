@@ -1,0 +1,32 @@
+"""Deterministic synthetic video content for tests and bench.py (no datasets
+are available offline).  SURVEY.md section 8(d): a smooth moving gradient plus
+texture plus N(0, 2% of max) noise, seed 1234; the "prediction" for the
+residual is the same content displaced by a known motion vector."""
+import numpy as np
+
+
+def frame(width, height, bit_depth=8, seed=1234, t=0):
+    """One luma plane (uint8 for 8-bit, uint16 otherwise)."""
+    rng = np.random.RandomState(seed + 7919 * t)
+    maxv = (1 << bit_depth) - 1
+    y, x = np.mgrid[0:height, 0:width].astype(np.float32)
+    base = 0.45 + 0.25 * np.sin((x + 3.0 * t) / 97.0) * np.cos((y - 2.0 * t) / 71.0)
+    tex = 0.12 * np.sin((x * 0.9 + y * 0.4) / 5.3) * np.sin((y * 1.1 - x * 0.3) / 7.9)
+    img = (base + tex) * maxv + rng.normal(0.0, 0.02 * maxv, size=(height, width))
+    img = np.clip(np.rint(img), 0, maxv)
+    return img.astype(np.uint8 if bit_depth == 8 else np.uint16)
+
+
+def shifted(img, dx, dy):
+    """img displaced by (dx, dy) with edge replication."""
+    h, w = img.shape
+    ys = np.clip(np.arange(h) - dy, 0, h - 1)
+    xs = np.clip(np.arange(w) - dx, 0, w - 1)
+    return img[ys][:, xs]
+
+
+def residual_plane(width, height, bit_depth=8, seed=1234, mv=(3, -2)):
+    """int16 residual = src - pred, pred = src displaced by mv (C2 input)."""
+    src = frame(width, height, bit_depth, seed)
+    pred = shifted(frame(width, height, bit_depth, seed), *mv)
+    return src.astype(np.int16) - pred.astype(np.int16)

@@ -369,8 +369,8 @@ void orc_fwd_txfm2d(const int16_t *input, int32_t *output, int stride,
   const int cbr = orc_fwd_cos_bit_row(tx_size);
   int rect = 0;
   if (W == 2 * H || H == 2 * W) rect = 1;
-  int32_t *buf = (int32_t *)malloc(sizeof(int32_t) * W * H);
-  int32_t *full = (int32_t *)malloc(sizeof(int32_t) * W * H);
+  int32_t buf[64 * 64];
+  int32_t full[64 * 64];
   int32_t tin[64], tout[64];
   for (int c = 0; c < W; ++c) {
     for (int r = 0; r < H; ++r)
@@ -403,8 +403,6 @@ void orc_fwd_txfm2d(const int16_t *input, int32_t *output, int stride,
   } else if (W == 64) {
     memset(output + H * 32, 0, (size_t)H * 32 * sizeof(int32_t));
   }
-  free(buf);
-  free(full);
 }
 
 void orc_fwht4x4(const int16_t *input, int32_t *output, int stride) {
