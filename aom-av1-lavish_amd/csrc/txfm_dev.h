@@ -52,13 +52,24 @@ __device__ __forceinline__ constexpr int32_t cospi(int j) {
 //   floor((p0 + p1 + h) / 2^B) = (p0 >> B) + (p1 >> B)
 //                                + (((p0 & m) + (p1 & m) + h) >> B)
 // (arithmetic shifts floor; the low-part sum is < 3 * 2^B).
-template <int BIT>
+//
+// FAST = the caller has certified (tools/range_analysis.py) that every operand
+// is below 2^23 in magnitude and every sum below 2^31: then the products are
+// v_mul_i32_i24 (full rate) and the sum fits one 32-bit register, giving the
+// same bits with 4 VALU ops instead of ~10.
+__device__ __forceinline__ int32_t sext24(int32_t x) { return (x << 8) >> 8; }
+
+template <int BIT, bool FAST = false>
 __device__ __forceinline__ int32_t hbtf(int32_t w0, int32_t in0, int32_t w1,
                                         int32_t in1) {
-  const int32_t p0 = (int32_t)((uint32_t)w0 * (uint32_t)in0);
-  const int32_t p1 = (int32_t)((uint32_t)w1 * (uint32_t)in1);
-  constexpr int32_t m = (1 << BIT) - 1, h = 1 << (BIT - 1);
-  return (p0 >> BIT) + (p1 >> BIT) + (((p0 & m) + (p1 & m) + h) >> BIT);
+  if constexpr (FAST) {
+    return (w0 * sext24(in0) + w1 * sext24(in1) + (1 << (BIT - 1))) >> BIT;
+  } else {
+    const int32_t p0 = (int32_t)((uint32_t)w0 * (uint32_t)in0);
+    const int32_t p1 = (int32_t)((uint32_t)w1 * (uint32_t)in1);
+    constexpr int32_t m = (1 << BIT) - 1, h = 1 << (BIT - 1);
+    return (p0 >> BIT) + (p1 >> BIT) + (((p0 & m) + (p1 & m) + h) >> BIT);
+  }
 }
 
 __device__ __forceinline__ int32_t rshift64(int64_t v, int bit) {
@@ -96,7 +107,7 @@ __device__ __forceinline__ int32_t clamp_bits(int32_t v) {
 // ----------------------------------------------------------------------------
 // forward DCT
 // ----------------------------------------------------------------------------
-template <int M, int BIT>
+template <int M, int BIT, bool FAST = false>
 __device__ __forceinline__ void fdct_odd(const int32_t* v, int32_t* O) {
   int32_t a[M], t[M];
 #pragma unroll
@@ -114,11 +125,11 @@ __device__ __forceinline__ void fdct_odd(const int32_t* v, int32_t* O) {
       const int al = base * (1 + 4 * ce_bitrev(j / S, nbits));
       const int p = M - 1 - j;
       if (lj >= S / 4 && lj < S / 2) {
-        t[j] = hbtf<BIT>(-cospi<BIT>(al), a[j], cospi<BIT>(64 - al), a[p]);
-        t[p] = hbtf<BIT>(cospi<BIT>(al), a[p], cospi<BIT>(64 - al), a[j]);
+        t[j] = hbtf<BIT, FAST>(-cospi<BIT>(al), a[j], cospi<BIT>(64 - al), a[p]);
+        t[p] = hbtf<BIT, FAST>(cospi<BIT>(al), a[p], cospi<BIT>(64 - al), a[j]);
       } else if (lj >= S / 2 && lj < 3 * S / 4) {
-        t[j] = hbtf<BIT>(-cospi<BIT>(64 - al), a[j], -cospi<BIT>(al), a[p]);
-        t[p] = hbtf<BIT>(cospi<BIT>(64 - al), a[p], -cospi<BIT>(al), a[j]);
+        t[j] = hbtf<BIT, FAST>(-cospi<BIT>(64 - al), a[j], -cospi<BIT>(al), a[p]);
+        t[p] = hbtf<BIT, FAST>(cospi<BIT>(64 - al), a[p], -cospi<BIT>(al), a[j]);
       }
     }
     const int B = S / 2;
@@ -139,16 +150,16 @@ __device__ __forceinline__ void fdct_odd(const int32_t* v, int32_t* O) {
   for (int j = 0; j < M / 2; ++j) {
     const int be = base * (1 + 4 * ce_bitrev(j, nbits));
     const int p = M - 1 - j;
-    O[j] = hbtf<BIT>(cospi<BIT>(64 - be), a[j], cospi<BIT>(be), a[p]);
-    O[p] = hbtf<BIT>(cospi<BIT>(64 - be), a[p], -cospi<BIT>(be), a[j]);
+    O[j] = hbtf<BIT, FAST>(cospi<BIT>(64 - be), a[j], cospi<BIT>(be), a[p]);
+    O[p] = hbtf<BIT, FAST>(cospi<BIT>(64 - be), a[p], -cospi<BIT>(be), a[j]);
   }
 }
 
-template <int N, int BIT>
+template <int N, int BIT, bool FAST = false>
 __device__ __forceinline__ void fdct(const int32_t* x, int32_t* X) {
   if constexpr (N == 2) {
-    X[0] = hbtf<BIT>(cospi<BIT>(32), x[0], cospi<BIT>(32), x[1]);
-    X[1] = hbtf<BIT>(-cospi<BIT>(32), x[1], cospi<BIT>(32), x[0]);
+    X[0] = hbtf<BIT, FAST>(cospi<BIT>(32), x[0], cospi<BIT>(32), x[1]);
+    X[1] = hbtf<BIT, FAST>(-cospi<BIT>(32), x[1], cospi<BIT>(32), x[0]);
   } else {
     constexpr int M = N / 2;
     int32_t e[M], v[M], E[M], O[M];
@@ -157,8 +168,8 @@ __device__ __forceinline__ void fdct(const int32_t* x, int32_t* X) {
       e[i] = add32(x[i], x[N - 1 - i]);
       v[i] = sub32(x[M - 1 - i], x[M + i]);
     }
-    fdct<M, BIT>(e, E);
-    fdct_odd<M, BIT>(v, O);
+    fdct<M, BIT, FAST>(e, E);
+    fdct_odd<M, BIT, FAST>(v, O);
 #pragma unroll
     for (int k = 0; k < M; ++k) {
       X[2 * k] = E[k];
@@ -170,28 +181,41 @@ __device__ __forceinline__ void fdct(const int32_t* x, int32_t* X) {
 // ----------------------------------------------------------------------------
 // forward ADST
 // ----------------------------------------------------------------------------
-template <int BIT>
+template <int BIT, bool FAST = false>
 __device__ __forceinline__ void fadst4(const int32_t* in, int32_t* out) {
   constexpr const int32_t* s = kSinpi[BIT - 10];
+  // 32-bit products as in the reference (av1_fwd_txfm1d.c:695-721); in the
+  // FAST range they are exact 24-bit multiplies.
+  auto mul = [](int32_t w, int32_t x) -> int32_t {
+    if constexpr (FAST) return w * sext24(x);
+    else return (int32_t)((uint32_t)w * (uint32_t)x);
+  };
   const int32_t x0 = in[0], x1 = in[1], x2 = in[2], x3 = in[3];
   // the reference returns zeros early for an all-zero input; the arithmetic
   // below yields exactly 0 for it as well, so no branch is needed.
-  const int32_t s0 = (int32_t)((uint32_t)s[1] * (uint32_t)x0);
-  const int32_t s1 = (int32_t)((uint32_t)s[4] * (uint32_t)x0);
-  const int32_t s2 = (int32_t)((uint32_t)s[2] * (uint32_t)x1);
-  const int32_t s3 = (int32_t)((uint32_t)s[1] * (uint32_t)x1);
-  const int32_t s4 = (int32_t)((uint32_t)s[3] * (uint32_t)x2);
-  const int32_t s5 = (int32_t)((uint32_t)s[4] * (uint32_t)x3);
-  const int32_t s6 = (int32_t)((uint32_t)s[2] * (uint32_t)x3);
+  const int32_t s0 = mul(s[1], x0);
+  const int32_t s1 = mul(s[4], x0);
+  const int32_t s2 = mul(s[2], x1);
+  const int32_t s3 = mul(s[1], x1);
+  const int32_t s4 = mul(s[3], x2);
+  const int32_t s5 = mul(s[4], x3);
+  const int32_t s6 = mul(s[2], x3);
   const int32_t s7 = sub32(add32(x0, x1), x3);
   const int32_t a0 = add32(add32(s0, s2), s5);
-  const int32_t a1 = (int32_t)((uint32_t)s[3] * (uint32_t)s7);
+  const int32_t a1 = mul(s[3], s7);
   const int32_t a2 = add32(sub32(s1, s3), s6);
   const int32_t a3 = s4;
-  out[0] = rshift64(add32(a0, a3), BIT);
-  out[1] = rshift64(a1, BIT);
-  out[2] = rshift64(sub32(a2, a3), BIT);
-  out[3] = rshift64(add32(sub32(a2, a0), a3), BIT);
+  if constexpr (FAST) {
+    out[0] = (add32(a0, a3) + (1 << (BIT - 1))) >> BIT;
+    out[1] = (a1 + (1 << (BIT - 1))) >> BIT;
+    out[2] = (sub32(a2, a3) + (1 << (BIT - 1))) >> BIT;
+    out[3] = (add32(sub32(a2, a0), a3) + (1 << (BIT - 1))) >> BIT;
+  } else {
+    out[0] = rshift64(add32(a0, a3), BIT);
+    out[1] = rshift64(a1, BIT);
+    out[2] = rshift64(sub32(a2, a3), BIT);
+    out[3] = rshift64(add32(sub32(a2, a0), a3), BIT);
+  }
 }
 
 // a-sequence of the fadst input permutation: a -> (e, M-1-e) expansion
@@ -208,10 +232,10 @@ __host__ __device__ __forceinline__ constexpr int adst_a(int N, int k) {
   return a;
 }
 
-template <int N, int BIT>
+template <int N, int BIT, bool FAST = false>
 __device__ __forceinline__ void fadst(const int32_t* in, int32_t* out) {
   if constexpr (N == 4) {
-    fadst4<BIT>(in, out);
+    fadst4<BIT, FAST>(in, out);
   } else {
     int32_t b[N], t[N];
 #pragma unroll
@@ -234,12 +258,12 @@ __device__ __forceinline__ void fadst(const int32_t* in, int32_t* out) {
           const int half = npairs / 2;
           if (G == 4 || q < half) {
             const int ph = (1 + 4 * (G == 4 ? 0 : q)) * 128 / G;
-            t[p] = hbtf<BIT>(cospi<BIT>(ph), b[p], cospi<BIT>(64 - ph), b[p + 1]);
-            t[p + 1] = hbtf<BIT>(cospi<BIT>(64 - ph), b[p], -cospi<BIT>(ph), b[p + 1]);
+            t[p] = hbtf<BIT, FAST>(cospi<BIT>(ph), b[p], cospi<BIT>(64 - ph), b[p + 1]);
+            t[p + 1] = hbtf<BIT, FAST>(cospi<BIT>(64 - ph), b[p], -cospi<BIT>(ph), b[p + 1]);
           } else {
             const int ph = (1 + 4 * (q - half)) * 128 / G;
-            t[p] = hbtf<BIT>(-cospi<BIT>(64 - ph), b[p], cospi<BIT>(ph), b[p + 1]);
-            t[p + 1] = hbtf<BIT>(cospi<BIT>(ph), b[p], cospi<BIT>(64 - ph), b[p + 1]);
+            t[p] = hbtf<BIT, FAST>(-cospi<BIT>(64 - ph), b[p], cospi<BIT>(ph), b[p + 1]);
+            t[p + 1] = hbtf<BIT, FAST>(cospi<BIT>(ph), b[p], cospi<BIT>(64 - ph), b[p + 1]);
           }
         }
       }
@@ -256,8 +280,8 @@ __device__ __forceinline__ void fadst(const int32_t* in, int32_t* out) {
 #pragma unroll
     for (int j = 0; j < N / 2; ++j) {
       const int th = (1 + 4 * j) * 32 / N;
-      t[2 * j] = hbtf<BIT>(cospi<BIT>(th), b[2 * j], cospi<BIT>(64 - th), b[2 * j + 1]);
-      t[2 * j + 1] = hbtf<BIT>(cospi<BIT>(64 - th), b[2 * j], -cospi<BIT>(th), b[2 * j + 1]);
+      t[2 * j] = hbtf<BIT, FAST>(cospi<BIT>(th), b[2 * j], cospi<BIT>(64 - th), b[2 * j + 1]);
+      t[2 * j + 1] = hbtf<BIT, FAST>(cospi<BIT>(64 - th), b[2 * j], -cospi<BIT>(th), b[2 * j + 1]);
     }
 #pragma unroll
     for (int k = 0; k < N / 2; ++k) {
@@ -279,12 +303,12 @@ __device__ __forceinline__ void fidentity(const int32_t* in, int32_t* out) {
 }
 
 // kind: 0 DCT, 1 ADST, 2 IDENTITY (uniform across the workgroup)
-template <int N, int BIT>
+template <int N, int BIT, bool FAST = false>
 __device__ __forceinline__ void fwd_1d(int kind, const int32_t* in, int32_t* out) {
   if (kind == 0) {
-    fdct<N, BIT>(in, out);
+    fdct<N, BIT, FAST>(in, out);
   } else if (kind == 1) {
-    if constexpr (N <= 16) fadst<N, BIT>(in, out);
+    if constexpr (N <= 16) fadst<N, BIT, FAST>(in, out);
   } else {
     if constexpr (N <= 32) fidentity<N>(in, out);
   }

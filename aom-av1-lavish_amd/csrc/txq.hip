@@ -34,6 +34,8 @@ struct TxqArgs {
   int nblocks;  // total blocks
   int ntypes;
   int types[16];
+  int tgroups;          // type groups along the grid
+  int types_per_group;
   int quant_kind;
   int highbd;
   QP qp;
@@ -77,9 +79,14 @@ __device__ __forceinline__ int32_t quant_one(int32_t c, int ac, int kind,
   int32_t q = 0;
   if (kind == LAVISH_QUANT_FP) {
     if (((int64_t)a << (1 + LS)) >= deq) {
-      int64_t t = (int64_t)a + rnd;
-      if (!highbd) t = t > 32767 ? 32767 : (t < -32768 ? -32768 : t);
-      q = (int32_t)((t * qt) >> (16 - LS));
+      if (!highbd) {
+        // clamp to int16 first: t < 2^15 and quant_fp < 2^15, so the product
+        // is an exact 24-bit multiply with a 32-bit result
+        const int32_t t = min(a + rnd, 32767);
+        q = (sext24(t) * qt) >> (16 - LS);
+      } else {
+        q = (int32_t)((((int64_t)a + rnd) * qt) >> (16 - LS));
+      }
     }
   } else {
     const int32_t zb = (pick(qp.zbin, ac) + ((1 << LS) >> 1)) >> LS;
@@ -101,46 +108,24 @@ __device__ __forceinline__ int32_t dequant_one(int32_t q, int ac, const QP& qp) 
   return (adq ^ sgn) - sgn;
 }
 
-template <int W, int H>
-__global__ __launch_bounds__(256, 2) void txq_plane_kernel(TxqArgs a) {
+// Largest residual magnitude for which the FAST (24-bit multiply, 32-bit sum)
+// transform arithmetic is certified exact for every size <= 32x32 by
+// tools/range_analysis.py (worst case 16x4: sums < 2^30.8).  Covers all 8-
+// and 10-bit residuals; larger inputs take the exact 64-bit-sum path.
+constexpr int kFastResidualMax = 1023;
+
+template <int W, int H, bool FAST>
+__device__ __forceinline__ void txq_types(const TxqArgs& a, const int32_t (&res)[W / (W < H ? W : H)][H],
+                                          int32_t* t1, int32_t* t2, const int16_t* isc, int tid,
+                                          int blk0, int nvalid, int ty0, int ty1) {
   using C = TxCfg<W, H>;
   constexpr int MN = W < H ? W : H;
-  constexpr int P = 256 / MN;   // blocks per workgroup
-  constexpr int CPT = W / MN;   // column transforms per thread
-  constexpr int RPT = H / MN;   // row transforms per thread
-  constexpr int N = W * H;      // coefficients per block (sizes <= 32)
-  constexpr int T1S = W + 1;    // padded LDS row stride: conflict-free row reads
+  constexpr int CPT = W / MN;
+  constexpr int RPT = H / MN;
+  constexpr int N = W * H;
+  constexpr int T1S = W + 1;
   constexpr int LS = C::log_scale;
-  __shared__ int32_t t1[P * H * T1S];
-  __shared__ __attribute__((aligned(16))) int32_t t2[P * N];
-  __shared__ int16_t isc[N];
-
-  const int tid = threadIdx.x;
-  const int blk0 = blockIdx.x * P;
-  const int nvalid = min(P, a.nblocks - blk0);
-
-  for (int i = tid; i < N; i += 256) isc[i] = a.iscan_default[i];
-
-  // residual columns -> registers (read once for all TX types)
-  int32_t res[CPT][H];
-#pragma unroll
-  for (int k = 0; k < CPT; ++k) {
-    const int j = k * 256 + tid;
-    const int b = j / W, c = j % W;
-    const int blk = blk0 + b;
-    if (b < nvalid) {
-      const int by = blk / a.bw, bx = blk - by * a.bw;
-      const int16_t* src = a.res + (size_t)by * H * a.stride + bx * W + c;
-#pragma unroll
-      for (int r = 0; r < H; ++r) res[k][r] = src[(size_t)r * a.stride];
-    } else {
-#pragma unroll
-      for (int r = 0; r < H; ++r) res[k][r] = 0;
-    }
-  }
-  __syncthreads();
-
-  for (int ti = 0; ti < a.ntypes; ++ti) {
+  for (int ti = ty0; ti < ty1; ++ti) {
     // wave-uniform by construction; readfirstlane keeps the transform-kind
     // branches scalar (otherwise hipcc if-converts all three kernels)
     const int t = __builtin_amdgcn_readfirstlane(a.types[ti]);
@@ -157,9 +142,12 @@ __global__ __launch_bounds__(256, 2) void txq_plane_kernel(TxqArgs a) {
       const int b = j / W, c = j % W;
       int32_t in[H], out[H];
 #pragma unroll
-      for (int r = 0; r < H; ++r)
-        in[r] = round_shift_1<-C::s0>(ud ? res[k][H - 1 - r] : res[k][r]);
-      fwd_1d<H, C::cos_bit_col>(kc, in, out);
+      for (int r = 0; r < H; ++r) {
+        const int32_t x = ud ? res[k][H - 1 - r] : res[k][r];
+        if constexpr (FAST) in[r] = x * (1 << C::s0);  // |x| <= 1023: no saturation
+        else in[r] = round_shift_1<-C::s0>(x);
+      }
+      fwd_1d<H, C::cos_bit_col, FAST>(kc, in, out);
       const int cc = lr ? W - 1 - c : c;
 #pragma unroll
       for (int r = 0; r < H; ++r)
@@ -175,7 +163,7 @@ __global__ __launch_bounds__(256, 2) void txq_plane_kernel(TxqArgs a) {
       int32_t in[W], out[W];
 #pragma unroll
       for (int c = 0; c < W; ++c) in[c] = t1[(b * H + r) * T1S + c];
-      fwd_1d<W, C::cos_bit_row>(kr, in, out);
+      fwd_1d<W, C::cos_bit_row, FAST>(kr, in, out);
       int last = 0;
       const size_t obase = ((size_t)ti * a.nblocks + blk0 + b) * N;
 #pragma unroll
@@ -219,6 +207,64 @@ __global__ __launch_bounds__(256, 2) void txq_plane_kernel(TxqArgs a) {
   }
 }
 
+// Grid: (block group, type group) pairs.  The G type groups of one block
+// group get workgroup ids that are congruent mod 8, i.e. they are dealt to the
+// same XCD and re-read the residual tile from that XCD's L2.
+template <int W, int H>
+__global__ __launch_bounds__(256, 2) void txq_plane_kernel(TxqArgs a) {
+  using C = TxCfg<W, H>;
+  constexpr int MN = W < H ? W : H;
+  constexpr int P = 256 / MN;   // blocks per workgroup
+  constexpr int CPT = W / MN;   // column transforms per thread
+  constexpr int N = W * H;      // coefficients per block (sizes <= 32)
+  constexpr int T1S = W + 1;    // padded LDS row stride: conflict-free row reads
+  __shared__ int32_t t1[P * H * T1S];
+  __shared__ __attribute__((aligned(16))) int32_t t2[P * N];
+  __shared__ int16_t isc[N];
+  (void)sizeof(C);
+
+  const int id = blockIdx.x;
+  const int inner = id & 7, rest = id >> 3;
+  const int tg = rest % a.tgroups, bg = (rest / a.tgroups) * 8 + inner;
+  const int nbg = (a.nblocks + P - 1) / P;
+  if (bg >= nbg) return;
+  const int ty0 = tg * a.types_per_group;
+  const int ty1 = min(a.ntypes, ty0 + a.types_per_group);
+
+  const int tid = threadIdx.x;
+  const int blk0 = bg * P;
+  const int nvalid = min(P, a.nblocks - blk0);
+
+  for (int i = tid; i < N; i += 256) isc[i] = a.iscan_default[i];
+
+  // residual columns -> registers (read once for all TX types of the group)
+  int32_t res[CPT][H];
+  int32_t amax = 0;
+#pragma unroll
+  for (int k = 0; k < CPT; ++k) {
+    const int j = k * 256 + tid;
+    const int b = j / W, c = j % W;
+    const int blk = blk0 + b;
+    if (b < nvalid) {
+      const int by = blk / a.bw, bx = blk - by * a.bw;
+      const int16_t* src = a.res + (size_t)by * H * a.stride + bx * W + c;
+#pragma unroll
+      for (int r = 0; r < H; ++r) {
+        res[k][r] = src[(size_t)r * a.stride];
+        amax = max(amax, abs(res[k][r]));
+      }
+    } else {
+#pragma unroll
+      for (int r = 0; r < H; ++r) res[k][r] = 0;
+    }
+  }
+  const bool fast = __syncthreads_and(amax <= kFastResidualMax);
+  if (fast)
+    txq_types<W, H, true>(a, res, t1, t2, isc, tid, blk0, nvalid, ty0, ty1);
+  else
+    txq_types<W, H, false>(a, res, t1, t2, isc, tid, blk0, nvalid, ty0, ty1);
+}
+
 // generic quantizer: one workgroup per block, any scan order.
 template <int LS>
 __global__ __launch_bounds__(256) void quant_kernel(const int32_t* coeff, int n,
@@ -247,12 +293,21 @@ __global__ __launch_bounds__(256) void quant_kernel(const int32_t* coeff, int n,
 // ----------------------------------------------------------------------------
 // launchers
 // ----------------------------------------------------------------------------
+// Split the TX types over enough workgroups to give every CU several
+// (>= ~8 per CU over 256 CUs); each extra group re-reads the residual tile
+// (2 bytes/pixel against 8 bytes/coefficient/type written).
 template <int W, int H>
-static void launch_plane(const TxqArgs& a, hipStream_t s) {
+static void launch_plane(TxqArgs a, hipStream_t s) {
   constexpr int MN = W < H ? W : H;
   constexpr int P = 256 / MN;
-  const int grid = (a.nblocks + P - 1) / P;
-  if (grid == 0) return;
+  const int nbg = (a.nblocks + P - 1) / P;
+  if (nbg == 0) return;
+  int groups = 1;
+  while (groups < a.ntypes && nbg * groups < 2048) groups *= 2;
+  if (groups > a.ntypes) groups = a.ntypes;
+  a.types_per_group = (a.ntypes + groups - 1) / groups;
+  a.tgroups = (a.ntypes + a.types_per_group - 1) / a.types_per_group;
+  const int grid = ((nbg + 7) / 8) * 8 * a.tgroups;
   hipLaunchKernelGGL((txq_plane_kernel<W, H>), dim3(grid), dim3(256), 0, s, a);
   LAVISH_CHECK(hipGetLastError());
 }
