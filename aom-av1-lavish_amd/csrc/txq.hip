@@ -58,54 +58,68 @@ constexpr uint8_t kHtxTab[16] = {0, 0, 1, 1, 0, 2, 2, 2, 1, 3, 3, 0, 3, 1, 3, 2}
 constexpr uint32_t kVtxPacked = pack2(kVtxTab);
 constexpr uint32_t kHtxPacked = pack2(kHtxTab);
 
-// one coefficient through av1_quantize_fp / aom_quantize_b (lowbd clamps the
-// rounded magnitude to int16, highbd does not).  Returns the signed qcoeff.
-// pick [0] (DC) or [1] (AC) without a runtime-indexed array (which would go
-// to scratch)
-__device__ __forceinline__ int32_t pick(const int16_t (&v)[2], int ac) {
-  return ac ? v[1] : v[0];
-}
-
-// one coefficient through av1_quantize_fp / aom_quantize_b (lowbd clamps the
-// rounded magnitude to int16, highbd does not).  Returns the signed qcoeff.
-template <int LS>
-__device__ __forceinline__ int32_t quant_one(int32_t c, int ac, int kind,
-                                             int highbd, const QP& qp) {
+// One coefficient through av1_quantize_fp* / aom_quantize_b* (qm off),
+// branch-free.  QK: LAVISH_QUANT_FP or LAVISH_QUANT_B; HBD: highbd variant
+// (no int16 clamp of the rounded magnitude).  `ac` selects the [1] entries.
+// Exactness of the 32-bit forms:
+//  * fp lowbd: t <= 32767, quant_fp < 2^15 -> t*quant < 2^30;
+//  * b: ((t*32)*quant) >> 16 == (t*quant) >> 11 exactly (32 t q / 2^16);
+//    t*quant < 2^30 in lowbd, 64-bit in highbd; the final multiply by
+//    quant_shift is 64-bit (quant_shift may be any int16 in the per-call API).
+template <int LS, int QK, bool HBD>
+__device__ __forceinline__ int32_t quant_one(int32_t c, bool ac, const QP& qp) {
   const int32_t sgn = c >> 31;
   const int32_t a = (c ^ sgn) - sgn;
-  const int32_t deq = pick(qp.dequant, ac);
-  const int32_t rnd = (pick(qp.round, ac) + ((1 << LS) >> 1)) >> LS;
-  const int32_t qt = pick(qp.quant, ac);
-  int32_t q = 0;
-  if (kind == LAVISH_QUANT_FP) {
-    if (((int64_t)a << (1 + LS)) >= deq) {
-      if (!highbd) {
-        // clamp to int16 first: t < 2^15 and quant_fp < 2^15, so the product
-        // is an exact 24-bit multiply with a 32-bit result
-        const int32_t t = min(a + rnd, 32767);
-        q = (sext24(t) * qt) >> (16 - LS);
-      } else {
-        q = (int32_t)((((int64_t)a + rnd) * qt) >> (16 - LS));
-      }
+  const int32_t rnd = ((ac ? qp.round[1] : qp.round[0]) + ((1 << LS) >> 1)) >> LS;
+  const int32_t qt = ac ? qp.quant[1] : qp.quant[0];
+  int32_t q;
+  if constexpr (QK == LAVISH_QUANT_FP) {
+    const int32_t deq = ac ? qp.dequant[1] : qp.dequant[0];
+    const bool pass = ((int64_t)a << (1 + LS)) >= deq;
+    if constexpr (!HBD) {
+      const int32_t t = min(a + rnd, 32767);
+      q = (sext24(t) * qt) >> (16 - LS);
+    } else {
+      q = (int32_t)(((int64_t)(a + rnd) * qt) >> (16 - LS));
     }
+    q = pass ? q : 0;
   } else {
-    const int32_t zb = (pick(qp.zbin, ac) + ((1 << LS) >> 1)) >> LS;
-    if (a >= zb) {
-      int64_t t = (int64_t)a + rnd;
-      if (!highbd) t = t > 32767 ? 32767 : (t < -32768 ? -32768 : t);
-      const int64_t tw = t * 32;  // qm weight 1 << AOM_QM_BITS
-      q = (int32_t)(((((tw * qt) >> 16) + tw) * pick(qp.quant_shift, ac)) >> (16 - LS + 5));
+    const int32_t zb = ((ac ? qp.zbin[1] : qp.zbin[0]) + ((1 << LS) >> 1)) >> LS;
+    const int32_t qs = ac ? qp.quant_shift[1] : qp.quant_shift[0];
+    const bool pass = a >= zb;
+    int64_t u;
+    if constexpr (!HBD) {
+      const int32_t t = min(a + rnd, 32767);
+      u = (int64_t)(((sext24(t) * qt) >> 11) + (t << 5));
+    } else {
+      const int64_t t = (int64_t)a + rnd;
+      u = ((t * qt) >> 11) + (t << 5);
     }
+    q = (int32_t)((u * qs) >> (16 - LS + 5));
+    q = pass ? q : 0;
   }
   return (q ^ sgn) - sgn;
 }
 
 template <int LS>
-__device__ __forceinline__ int32_t dequant_one(int32_t q, int ac, const QP& qp) {
+__device__ __forceinline__ int32_t dequant_one(int32_t q, bool ac, const QP& qp) {
   const int32_t sgn = q >> 31;
   const int32_t aq = (q ^ sgn) - sgn;
-  const int32_t adq = (int32_t)((uint32_t)aq * (uint32_t)pick(qp.dequant, ac)) >> LS;
+  const int32_t d = ac ? qp.dequant[1] : qp.dequant[0];
+  // (abs_q * dequant) >> log_scale as an int multiply (wraps like the reference)
+  const int32_t adq = (int32_t)((uint32_t)aq * (uint32_t)d) >> LS;
   return (adq ^ sgn) - sgn;
+}
+
+// runtime-kind wrapper for the generic per-block quantizer kernel
+template <int LS>
+__device__ __forceinline__ int32_t quant_rt(int32_t c, bool ac, int kind, int highbd,
+                                            const QP& qp) {
+  if (kind == LAVISH_QUANT_FP)
+    return highbd ? quant_one<LS, LAVISH_QUANT_FP, true>(c, ac, qp)
+                  : quant_one<LS, LAVISH_QUANT_FP, false>(c, ac, qp);
+  return highbd ? quant_one<LS, LAVISH_QUANT_B, true>(c, ac, qp)
+                : quant_one<LS, LAVISH_QUANT_B, false>(c, ac, qp);
 }
 
 // Largest residual magnitude for which the FAST (24-bit multiply, 32-bit sum)
@@ -114,16 +128,36 @@ __device__ __forceinline__ int32_t dequant_one(int32_t q, int ac, const QP& qp) 
 // and 10-bit residuals; larger inputs take the exact 64-bit-sum path.
 constexpr int kFastResidualMax = 1023;
 
-template <int W, int H, bool FAST>
-__device__ __forceinline__ void txq_types(const TxqArgs& a, const int32_t (&res)[W / (W < H ? W : H)][H],
-                                          int32_t* t1, int32_t* t2, const int16_t* isc, int tid,
+// Wave-local memory ordering: lanes of one wave exchange data through LDS
+// with no workgroup barrier (each wave owns its tile); these fences only stop
+// the compiler from moving LDS accesses across the exchange point (LDS ops of
+// one wave are processed in order).
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+template <int W, int H>
+struct Tile {
+  static constexpr int MN = W < H ? W : H;
+  static constexpr int P = 64 / MN;     // blocks per wave tile
+  static constexpr int CPT = W / MN;    // column transforms per lane
+  static constexpr int RPT = H / MN;    // row transforms per lane
+  static constexpr int N = W * H;       // coefficients per block (sizes <= 32)
+  static constexpr int T1S = W + 1;     // padded LDS row stride
+  static constexpr int T1 = P * H * T1S;
+  static constexpr int T2 = P * N;
+};
+
+template <int W, int H, bool FAST, int QK, bool HBD>
+__device__ __forceinline__ void txq_types(const TxqArgs& a,
+                                          const int32_t (&res)[Tile<W, H>::CPT][H],
+                                          int32_t* t1, int32_t* t2, const int16_t* isc, int lane,
                                           int blk0, int nvalid, int ty0, int ty1) {
   using C = TxCfg<W, H>;
-  constexpr int MN = W < H ? W : H;
-  constexpr int CPT = W / MN;
-  constexpr int RPT = H / MN;
-  constexpr int N = W * H;
-  constexpr int T1S = W + 1;
+  using T = Tile<W, H>;
+  constexpr int N = T::N, T1S = T::T1S;
   constexpr int LS = C::log_scale;
   for (int ti = ty0; ti < ty1; ++ti) {
     // wave-uniform by construction; readfirstlane keeps the transform-kind
@@ -137,8 +171,8 @@ __device__ __forceinline__ void txq_types(const TxqArgs& a, const int32_t (&res)
 
     // ---- columns (av1_fwd_txfm2d.c:88-106) ----
 #pragma unroll
-    for (int k = 0; k < CPT; ++k) {
-      const int j = k * 256 + tid;
+    for (int k = 0; k < T::CPT; ++k) {
+      const int j = k * 64 + lane;
       const int b = j / W, c = j % W;
       int32_t in[H], out[H];
 #pragma unroll
@@ -153,50 +187,58 @@ __device__ __forceinline__ void txq_types(const TxqArgs& a, const int32_t (&res)
       for (int r = 0; r < H; ++r)
         t1[(b * H + r) * T1S + cc] = round_shift_1<-C::s1>(out[r]);
     }
-    __syncthreads();
+    wave_sync();
 
     // ---- rows + quantization (av1_fwd_txfm2d.c:110-126, av1_quantize.c) ----
 #pragma unroll
-    for (int k = 0; k < RPT; ++k) {
-      const int j = k * 256 + tid;
+    for (int k = 0; k < T::RPT; ++k) {
+      const int j = k * 64 + lane;
       const int b = j / H, r = j % H;
       int32_t in[W], out[W];
 #pragma unroll
       for (int c = 0; c < W; ++c) in[c] = t1[(b * H + r) * T1S + c];
       fwd_1d<W, C::cos_bit_row, FAST>(kr, in, out);
-      int last = 0;
       const size_t obase = ((size_t)ti * a.nblocks + blk0 + b) * N;
+      // eob = 1 + last scan position holding a nonzero qcoeff; the inverse
+      // scan of this type's scan kind is row skind of the LDS table
+      const int16_t* iscan = isc + skind * N;
+      int last = 0;
 #pragma unroll
       for (int c = 0; c < W; ++c) {
         int32_t v = round_shift_1<-C::s2>(out[c]);
         if constexpr (C::rect2) v = rshift64((int64_t)v * 5793, 12);
         const int rc = c * H + r;
-        if (a.coeff != nullptr && b < nvalid) a.coeff[obase + rc] = v;
         int32_t q = 0;
-        if (a.quant_kind != LAVISH_QUANT_NONE)
-          q = quant_one<LS>(v, rc != 0, a.quant_kind, a.highbd, a.qp);
+        if constexpr (QK == LAVISH_QUANT_NONE) {
+          if (b < nvalid) a.coeff[obase + rc] = v;
+        } else {
+          if (a.coeff != nullptr) {
+            if (b < nvalid) a.coeff[obase + rc] = v;
+          }
+          q = quant_one<LS, QK, HBD>(v, c != 0 || r != 0, a.qp);
+        }
         t2[b * N + rc] = q;
-        const int pos = skind == 0 ? isc[rc] : (skind == 1 ? rc : r * W + c);
-        if (q != 0) last = max(last, pos + 1);
+        const int pos1 = iscan[rc] + 1;
+        last = q != 0 ? max(last, pos1) : last;
       }
 #pragma unroll
       for (int m = 1; m < H; m <<= 1) last = max(last, __shfl_xor(last, m));
       if (r == 0 && b < nvalid && a.eob != nullptr)
         a.eob[(size_t)ti * a.nblocks + blk0 + b] = (uint16_t)last;
     }
-    __syncthreads();
+    wave_sync();
 
-    // ---- coalesced copy-out of qcoeff / dqcoeff ----
+    // ---- coalesced copy-out of qcoeff / dqcoeff (1 KiB per instruction) ----
     if (a.qcoeff != nullptr) {
       const int total = nvalid * N;
       const size_t gbase = ((size_t)ti * a.nblocks + blk0) * N;
-      for (int i = tid * 4; i < total; i += 256 * 4) {
+      for (int i = lane * 4; i < total; i += 64 * 4) {
         const int4 q4 = *reinterpret_cast<const int4*>(&t2[i]);
         *reinterpret_cast<int4*>(&a.qcoeff[gbase + i]) = q4;
         if (a.dqcoeff != nullptr) {
           const int rc0 = i % N;  // N % 4 == 0: all four share the block
           int4 d4;
-          d4.x = dequant_one<LS>(q4.x, rc0 != 0, a.qp);
+          d4.x = dequant_one<LS>(q4.x, rc0 != 0, a.qp);  // only x can be DC
           d4.y = dequant_one<LS>(q4.y, 1, a.qp);
           d4.z = dequant_one<LS>(q4.z, 1, a.qp);
           d4.w = dequant_one<LS>(q4.w, 1, a.qp);
@@ -204,45 +246,52 @@ __device__ __forceinline__ void txq_types(const TxqArgs& a, const int32_t (&res)
         }
       }
     }
+    wave_sync();  // t2 is rewritten by the next type's row pass
   }
 }
 
-// Grid: (block group, type group) pairs.  The G type groups of one block
-// group get workgroup ids that are congruent mod 8, i.e. they are dealt to the
-// same XCD and re-read the residual tile from that XCD's L2.
+// One 256-thread workgroup = 4 independent wave tiles (no workgroup
+// barriers after the shared iscan load).  Grid: (tile quad, type group); the
+// type groups of one tile quad get workgroup ids congruent mod 8, i.e. the
+// same XCD, so repeated residual reads hit that XCD's L2.
 template <int W, int H>
 __global__ __launch_bounds__(256, 2) void txq_plane_kernel(TxqArgs a) {
-  using C = TxCfg<W, H>;
-  constexpr int MN = W < H ? W : H;
-  constexpr int P = 256 / MN;   // blocks per workgroup
-  constexpr int CPT = W / MN;   // column transforms per thread
-  constexpr int N = W * H;      // coefficients per block (sizes <= 32)
-  constexpr int T1S = W + 1;    // padded LDS row stride: conflict-free row reads
-  __shared__ int32_t t1[P * H * T1S];
-  __shared__ __attribute__((aligned(16))) int32_t t2[P * N];
-  __shared__ int16_t isc[N];
-  (void)sizeof(C);
+  using T = Tile<W, H>;
+  constexpr int H_ = H;
+  __shared__ int32_t t1s[4 * T::T1];
+  __shared__ __attribute__((aligned(16))) int32_t t2s[4 * T::T2];
+  __shared__ int16_t isc[3 * T::N];  // inverse scans: default, mcol, mrow
 
   const int id = blockIdx.x;
   const int inner = id & 7, rest = id >> 3;
-  const int tg = rest % a.tgroups, bg = (rest / a.tgroups) * 8 + inner;
-  const int nbg = (a.nblocks + P - 1) / P;
-  if (bg >= nbg) return;
+  const int tg = rest % a.tgroups, quad = (rest / a.tgroups) * 8 + inner;
+  const int ntiles = (a.nblocks + T::P - 1) / T::P;
+  if (quad * 4 >= ntiles) return;
   const int ty0 = tg * a.types_per_group;
   const int ty1 = min(a.ntypes, ty0 + a.types_per_group);
 
   const int tid = threadIdx.x;
-  const int blk0 = bg * P;
-  const int nvalid = min(P, a.nblocks - blk0);
+  for (int i = tid; i < T::N; i += 256) {
+    isc[i] = a.iscan_default[i];
+    isc[T::N + i] = (int16_t)i;                                   // mcol: identity
+    isc[2 * T::N + i] = (int16_t)((i % H) * W + i / H);           // mrow: r*W + c
+  }
+  __syncthreads();
 
-  for (int i = tid; i < N; i += 256) isc[i] = a.iscan_default[i];
+  const int wave = tid >> 6, lane = tid & 63;
+  const int tile = quad * 4 + wave;
+  if (tile >= ntiles) return;
+  const int blk0 = tile * T::P;
+  const int nvalid = min(T::P, a.nblocks - blk0);
+  int32_t* t1 = t1s + wave * T::T1;
+  int32_t* t2 = t2s + wave * T::T2;
 
   // residual columns -> registers (read once for all TX types of the group)
-  int32_t res[CPT][H];
+  int32_t res[T::CPT][H_];
   int32_t amax = 0;
 #pragma unroll
-  for (int k = 0; k < CPT; ++k) {
-    const int j = k * 256 + tid;
+  for (int k = 0; k < T::CPT; ++k) {
+    const int j = k * 64 + lane;
     const int b = j / W, c = j % W;
     const int blk = blk0 + b;
     if (b < nvalid) {
@@ -258,11 +307,32 @@ __global__ __launch_bounds__(256, 2) void txq_plane_kernel(TxqArgs a) {
       for (int r = 0; r < H; ++r) res[k][r] = 0;
     }
   }
-  const bool fast = __syncthreads_and(amax <= kFastResidualMax);
-  if (fast)
-    txq_types<W, H, true>(a, res, t1, t2, isc, tid, blk0, nvalid, ty0, ty1);
-  else
-    txq_types<W, H, false>(a, res, t1, t2, isc, tid, blk0, nvalid, ty0, ty1);
+  // wave-uniform choice of the certified-exact fast arithmetic
+  const bool fast = __builtin_amdgcn_ballot_w64(amax > kFastResidualMax) == 0;
+#define LAVISH_TXQ_RUN(F, Q, HB) \
+  txq_types<W, H, F, Q, HB>(a, res, t1, t2, isc, lane, blk0, nvalid, ty0, ty1)
+  const int qk = a.quant_kind;
+  if (qk == LAVISH_QUANT_NONE) {
+    if (fast) LAVISH_TXQ_RUN(true, LAVISH_QUANT_NONE, false);
+    else LAVISH_TXQ_RUN(false, LAVISH_QUANT_NONE, false);
+  } else if (qk == LAVISH_QUANT_FP) {
+    if (a.highbd) {
+      if (fast) LAVISH_TXQ_RUN(true, LAVISH_QUANT_FP, true);
+      else LAVISH_TXQ_RUN(false, LAVISH_QUANT_FP, true);
+    } else {
+      if (fast) LAVISH_TXQ_RUN(true, LAVISH_QUANT_FP, false);
+      else LAVISH_TXQ_RUN(false, LAVISH_QUANT_FP, false);
+    }
+  } else {
+    if (a.highbd) {
+      if (fast) LAVISH_TXQ_RUN(true, LAVISH_QUANT_B, true);
+      else LAVISH_TXQ_RUN(false, LAVISH_QUANT_B, true);
+    } else {
+      if (fast) LAVISH_TXQ_RUN(true, LAVISH_QUANT_B, false);
+      else LAVISH_TXQ_RUN(false, LAVISH_QUANT_B, false);
+    }
+  }
+#undef LAVISH_TXQ_RUN
 }
 
 // generic quantizer: one workgroup per block, any scan order.
@@ -278,7 +348,7 @@ __global__ __launch_bounds__(256) void quant_kernel(const int32_t* coeff, int n,
   int last = 0;
   for (int i = tid; i < n; i += 256) {
     const int rc = scan[i];
-    const int32_t q = quant_one<LS>(coeff[base + rc], rc != 0, kind, highbd, qp);
+    const int32_t q = quant_rt<LS>(coeff[base + rc], rc != 0, kind, highbd, qp);
     qcoeff[base + rc] = q;
     dqcoeff[base + rc] = dequant_one<LS>(q, rc != 0, qp);
     if (q != 0) last = max(last, i + 1);
@@ -298,8 +368,7 @@ __global__ __launch_bounds__(256) void quant_kernel(const int32_t* coeff, int n,
 // (2 bytes/pixel against 8 bytes/coefficient/type written).
 template <int W, int H>
 static void launch_plane(TxqArgs a, hipStream_t s) {
-  constexpr int MN = W < H ? W : H;
-  constexpr int P = 256 / MN;
+  constexpr int P = Tile<W, H>::P * 4;  // blocks per workgroup (4 wave tiles)
   const int nbg = (a.nblocks + P - 1) / P;
   if (nbg == 0) return;
   int groups = 1;
