@@ -127,6 +127,7 @@ __device__ __forceinline__ int32_t quant_rt(int32_t c, bool ac, int kind, int hi
 // tools/range_analysis.py (worst case 16x4: sums < 2^30.8).  Covers all 8-
 // and 10-bit residuals; larger inputs take the exact 64-bit-sum path.
 constexpr int kFastResidualMax = 1023;
+constexpr int kFrameStreams = 3;
 
 // Wave-local memory ordering: lanes of one wave exchange data through LDS
 // with no workgroup barrier (each wave owns its tile); these fences only stop
@@ -471,7 +472,76 @@ int quantize_batch(const int32_t* coeff, int n, int nblocks, const int16_t* scan
   return 0;
 }
 
+// Frame batch: every requested TX size over the same residual plane.  The
+// per-size kernels are independent, so they are spread over a few internal
+// streams (forked from / joined back to the caller's stream with events):
+// register-heavy 16/32-point kernels and light 4/8-point kernels then share
+// the CUs, which a single in-order stream cannot do.
+struct FrameStreams {
+  int device = -1;
+  hipStream_t s[kFrameStreams] = {};
+  hipEvent_t fork = nullptr, join[kFrameStreams] = {};
+};
+static thread_local FrameStreams t_fs;
+
+static FrameStreams& frame_streams() {
+  int dev = 0;
+  LAVISH_CHECK(hipGetDevice(&dev));
+  if (t_fs.device != dev) {
+    for (int i = 0; i < kFrameStreams; ++i) {
+      LAVISH_CHECK(hipStreamCreateWithFlags(&t_fs.s[i], hipStreamNonBlocking));
+      LAVISH_CHECK(hipEventCreateWithFlags(&t_fs.join[i], hipEventDisableTiming));
+    }
+    LAVISH_CHECK(hipEventCreateWithFlags(&t_fs.fork, hipEventDisableTiming));
+    t_fs.device = dev;
+  }
+  return t_fs;
+}
+
+int txq_frame(const int16_t* residual, int stride, int width, int height, uint32_t size_mask,
+              const uint32_t* type_masks, int bd, int quant_kind, const LavishQuantParams* qp,
+              int32_t* const* qcoeff, int32_t* const* dqcoeff, uint16_t* const* eob,
+              hipStream_t caller) {
+  // order: most output bytes first, dealt round-robin over the streams
+  int order[19], n = 0;
+  for (int s = 0; s < 19; ++s)
+    if ((size_mask >> s) & 1) order[n++] = s;
+  auto work = [&](int s) {
+    return (long)__builtin_popcount(type_masks[s]) * max_eob(s) * (width / tx_w(s)) *
+           (height / tx_h(s));
+  };
+  for (int i = 1; i < n; ++i)
+    for (int j = i; j > 0 && work(order[j]) > work(order[j - 1]); --j) {
+      const int t = order[j];
+      order[j] = order[j - 1];
+      order[j - 1] = t;
+    }
+  FrameStreams& fs = frame_streams();
+  LAVISH_CHECK(hipEventRecord(fs.fork, caller));
+  for (int i = 0; i < kFrameStreams; ++i) LAVISH_CHECK(hipStreamWaitEvent(fs.s[i], fs.fork, 0));
+  int rc = 0;
+  for (int i = 0; i < n && rc == 0; ++i) {
+    const int s = order[i];
+    rc = txq_plane(residual, stride, width, height, s, type_masks[s], bd, quant_kind, qp,
+                   qcoeff[s], dqcoeff[s], eob[s], nullptr, fs.s[i % kFrameStreams]);
+  }
+  for (int i = 0; i < kFrameStreams; ++i) {
+    LAVISH_CHECK(hipEventRecord(fs.join[i], fs.s[i]));
+    LAVISH_CHECK(hipStreamWaitEvent(caller, fs.join[i], 0));
+  }
+  return rc;
+}
+
 }  // namespace lavish
+
+extern "C" int lavish_txq_frame(const int16_t* residual, int stride, int width, int height,
+                                uint32_t size_mask, const uint32_t* type_masks, int bit_depth,
+                                int quant_kind, const LavishQuantParams* qp,
+                                int32_t* const* qcoeff, int32_t* const* dqcoeff,
+                                uint16_t* const* eob, void* stream) {
+  return lavish::txq_frame(residual, stride, width, height, size_mask, type_masks, bit_depth,
+                           quant_kind, qp, qcoeff, dqcoeff, eob, (hipStream_t)stream);
+}
 
 extern "C" int lavish_txq_plane(const int16_t* residual, int stride, int width, int height,
                                 int tx_size, uint32_t type_mask, int bit_depth,

@@ -97,6 +97,9 @@ _lib.lavish_iscan.argtypes = [_i32, _i32]
 _lib.lavish_txq_plane.argtypes = [_vp, _i32, _i32, _i32, _i32, ctypes.c_uint32, _i32, _i32,
                                   ctypes.POINTER(QuantParams), _vp, _vp, _vp, _vp, _vp]
 _lib.lavish_txq_plane.restype = _i32
+_lib.lavish_txq_frame.argtypes = [_vp, _i32, _i32, _i32, ctypes.c_uint32, _vp, _i32, _i32,
+                                  ctypes.POINTER(QuantParams), _vp, _vp, _vp, _vp]
+_lib.lavish_txq_frame.restype = _i32
 _lib.lavish_quantize_batch.argtypes = [_vp, _i32, _i32, _vp, _vp, _i32, _i32, _i32,
                                        ctypes.POINTER(QuantParams), _vp, _vp, _vp, _vp]
 _lib.lavish_quantize_batch.restype = _i32
@@ -246,6 +249,37 @@ def txq_plane(residual, tx_size, type_mask, qp, bit_depth=8, quant_kind=QUANT_FP
     if rc != 0:
         raise ValueError("lavish_txq_plane rejected arguments (rc=%d)" % rc)
     return out
+
+
+class FrameOutputs:
+    """Per-size output tensors of txq_frame plus the pointer tables the C ABI
+    takes (built once, reused every call)."""
+
+    def __init__(self, residual, sizes, type_masks=None):
+        self.sizes = list(sizes)
+        self.type_masks = {s: (type_masks or {}).get(s, valid_type_mask(s)) for s in self.sizes}
+        self.outs = {s: txq_plane_out(residual, s, self.type_masks[s]) for s in self.sizes}
+        self.size_mask = sum(1 << s for s in self.sizes)
+        P19 = ctypes.c_void_p * 19
+        self.tm = (ctypes.c_uint32 * 19)(*[self.type_masks.get(s, 0) for s in range(19)])
+        self.q = P19(*[self.outs[s]["qcoeff"].data_ptr() if s in self.outs else 0 for s in range(19)])
+        self.dq = P19(*[self.outs[s]["dqcoeff"].data_ptr() if s in self.outs else 0 for s in range(19)])
+        self.eob = P19(*[self.outs[s]["eob"].data_ptr() if s in self.outs else 0 for s in range(19)])
+
+
+def txq_frame(residual, frame_out, qp, bit_depth=8, quant_kind=QUANT_FP, stream=None):
+    """lavish_txq_frame: every size of `frame_out` over one residual plane, the
+    per-size kernels running concurrently on internal streams."""
+    import torch
+    assert residual.dtype == torch.int16 and residual.is_cuda
+    H, W = residual.shape
+    rc = _lib.lavish_txq_frame(ctypes.c_void_p(residual.data_ptr()), residual.stride(0), W, H,
+                               frame_out.size_mask, frame_out.tm, bit_depth, quant_kind,
+                               ctypes.byref(qp), frame_out.q, frame_out.dq, frame_out.eob,
+                               _stream_ptr(stream))
+    if rc != 0:
+        raise ValueError("lavish_txq_frame rejected arguments (rc=%d)" % rc)
+    return frame_out.outs
 
 
 def quantize_batch(coeff, scan, log_scale, qp, bit_depth=8, quant_kind=QUANT_FP, stream=None):

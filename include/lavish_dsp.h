@@ -114,6 +114,19 @@ int lavish_txq_plane(const int16_t *residual, int stride, int width,
                      int32_t *dqcoeff, uint16_t *eob, int32_t *coeff,
                      void *stream);
 
+/* Frame batch: lavish_txq_plane for every TX size whose bit is set in
+ * size_mask (bit = TX_SIZE), with type_masks[tx_size] and per-size output
+ * pointers qcoeff[tx_size] / dqcoeff[tx_size] / eob[tx_size] (arrays of 19
+ * entries, unused entries ignored).  The independent per-size kernels run
+ * concurrently on internal streams forked from and joined back to `stream`;
+ * the call is asynchronous with respect to the host like the others. */
+int lavish_txq_frame(const int16_t *residual, int stride, int width,
+                     int height, uint32_t size_mask,
+                     const uint32_t *type_masks, int bit_depth,
+                     int quant_kind, const LavishQuantParams *qp,
+                     int32_t *const *qcoeff, int32_t *const *dqcoeff,
+                     uint16_t *const *eob, void *stream);
+
 /* Quantize `nblocks` coefficient blocks of n words each (contiguous) with one
  * scan order (device pointers to scan / iscan of n entries). */
 int lavish_quantize_batch(const int32_t *coeff, int n, int nblocks,

@@ -290,3 +290,19 @@ def test_full_frame_properties(L):
                 rq, rdq, reob = O.quantize("fp", coeff, n, oq, scan, iscan, ls)
                 np.testing.assert_array_equal(qn[si, bi], rq)
                 assert eob[si, bi] == reob
+
+
+def test_txq_frame_matches_per_size(L):
+    """lavish_txq_frame (concurrent per-size kernels) == per-size launches ==
+    oracle on a small plane with every size <= 32."""
+    res = _plane(256, 96, 8, 77, "random")
+    dres = torch.from_numpy(res).cuda()
+    qp = L.build_quant_params(8, 140, L.QUANT_FP)
+    frame = L.FrameOutputs(dres, SIZES_LE32)
+    outs = L.txq_frame(dres, frame, qp)
+    torch.cuda.synchronize()
+    for s in SIZES_LE32:
+        qc, dq, eob = _oracle_plane(res, s, _mask(s), 8, 140, False)
+        np.testing.assert_array_equal(outs[s]["qcoeff"].cpu().numpy(), qc)
+        np.testing.assert_array_equal(outs[s]["dqcoeff"].cpu().numpy(), dq)
+        np.testing.assert_array_equal(outs[s]["eob"].cpu().numpy().view(np.uint16), eob)

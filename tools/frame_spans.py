@@ -1,0 +1,20 @@
+#!/usr/bin/env python3
+"""Group a rocprofv3 kernel trace into lavish_txq_frame launches (the 14
+txq_plane_kernel dispatches of one step, possibly overlapping on 3 streams)
+and report the average frame span (first start -> last end), to compare with
+bench.py's event-timed roofline.avg_launch_ms."""
+import csv, sys
+
+def main(path, per_frame=14):
+    rows = [r for r in csv.DictReader(open(path)) if "txq_plane_kernel" in r["Kernel_Name"]]
+    rows.sort(key=lambda r: int(r["Start_Timestamp"]))
+    spans = []
+    for i in range(0, len(rows) - per_frame + 1, per_frame):
+        grp = rows[i:i + per_frame]
+        spans.append((max(int(r["End_Timestamp"]) for r in grp) - min(int(r["Start_Timestamp"]) for r in grp)) / 1e6)
+    # skip warmup frames (first 2)
+    tail = spans[2:] if len(spans) > 4 else spans
+    print("frames=%d avg_span_ms=%.4f min=%.4f max=%.4f" % (len(tail), sum(tail) / len(tail), min(tail), max(tail)))
+
+if __name__ == "__main__":
+    main(sys.argv[1])
