@@ -1,0 +1,474 @@
+// pixel.hip -- batched pixel-domain kernels of the RDO hot path for gfx950:
+// SAD (+skip, +avg, x4d), variance / MSE / get_var, bilinear sub-pixel
+// variance, SSE, residual subtract, sum of squares, Hadamard 4..32, SATD and
+// block error.  Each job is one block; one wave owns a job (or, for the tiny
+// per-coefficient ones, a group of lanes), and reductions use wave shuffles.
+//
+// Semantics (all integer, bit-exact):
+//   sad/_skip/_avg/x4d      aom_dsp/sad.c:22-129, aom_comp_avg_pred_c
+//                           aom_dsp/variance.c:285-298
+//   variance / mse / getvar aom_dsp/variance.c:38-55,123-130,187-238
+//   highbd 8/10/12 variance aom_dsp/variance.c:321-408
+//   sub-pixel variance      aom_dsp/variance.c:73-145,454-520
+//   sse                     aom_dsp/sse.c:19-54
+//   subtract                aom_dsp/subtract.c:20-54
+//   sum_squares_2d_i16      aom_dsp/sum_squares.c:16-30
+//   hadamard / satd         aom_dsp/avg.c:102-348,509-516
+//   block_error             av1/encoder/rdopt.c:635-682
+#include "lavish_internal.h"
+
+namespace lavish {
+
+__device__ __forceinline__ int64_t wave_sum64(int64_t v) {
+#pragma unroll
+  for (int m = 1; m < 64; m <<= 1) v += __shfl_xor(v, m);
+  return v;
+}
+__device__ __forceinline__ uint32_t wave_sum32(uint32_t v) {
+#pragma unroll
+  for (int m = 1; m < 64; m <<= 1) v += __shfl_xor(v, m);
+  return v;
+}
+
+// ---------------------------------------------------------------- SAD ----
+// mode 0: SAD, 1: 2 x SAD of even rows (sad_skip), 2: SAD against the
+// rounded average of ref and second_pred (w x h, stride w) (sad_avg).
+template <typename Pix>
+__global__ __launch_bounds__(64) void sad_kernel(const Pix* src, int ss, const Pix* ref, int rs,
+                                                 int w, int h, const LavishPixJob* jobs,
+                                                 int nrefs, int mode, const Pix* second,
+                                                 uint32_t* out) {
+  const LavishPixJob jb = jobs[blockIdx.x];
+  const int lane = threadIdx.x;
+  const int rows = mode == 1 ? h / 2 : h;
+  const int rstep = mode == 1 ? 2 : 1;
+  const Pix* s = src + jb.src_off;
+  for (int k = 0; k < nrefs; ++k) {
+    const Pix* r = ref + jb.ref_off[k];
+    uint32_t acc = 0;
+    for (int i = lane; i < rows * w; i += 64) {
+      const int y = i / w, x = i - y * w;
+      const int sv = s[(int64_t)y * rstep * ss + x];
+      int rv = r[(int64_t)y * rstep * rs + x];
+      if (mode == 2) rv = (second[jb.aux_off + (int64_t)y * w + x] + rv + 1) >> 1;
+      acc += (uint32_t)abs(sv - rv);
+    }
+    acc = wave_sum32(acc);
+    if (lane == 0) out[(int64_t)blockIdx.x * nrefs + k] = mode == 1 ? 2 * acc : acc;
+  }
+}
+
+// ------------------------------------------------------------ variance ----
+// d = a - b with a = the first rtcd pointer (src; the bilinear-filtered one
+// for sub-pixel variance) at job.src_off and b = the second at job.ref_off[0].  kind 0: variance, 1: mse (returns sse), 2: get_var
+// (sse + sum), 3: sub-pixel variance of the bilinear-filtered `a`
+// (xoff/yoff per job), 4: sse only with uint64 result (aom_sse, highbd sse),
+// 5: as 3 with the filtered block first averaged with second_pred (w x h,
+// stride w, at job.aux_off): sub_pixel_avg_variance.
+// bd: 8 for lowbd; 8/10/12 for the highbd rounding variants (Pix=uint16).
+template <typename Pix>
+__global__ __launch_bounds__(64) void var_kernel(const Pix* a, int as, const Pix* b, int bs,
+                                                 int w, int h, const LavishPixJob* jobs,
+                                                 int kind, int bd, const Pix* second,
+                                                 uint32_t* var_out,
+                                                 uint32_t* sse_out, int32_t* sum_out,
+                                                 int64_t* sse64_out) {
+  constexpr uint8_t kBil[8][2] = {{128, 0}, {112, 16}, {96, 32}, {80, 48},
+                                  {64, 64}, {48, 80},  {32, 96}, {16, 112}};
+  const LavishPixJob jb = jobs[blockIdx.x];
+  const int lane = threadIdx.x;
+  const Pix* pa = a + jb.src_off;
+  const Pix* pb = b + jb.ref_off[0];
+  int64_t sum = 0;
+  uint64_t sse = 0;
+  const int xo = jb.xoff, yo = jb.yoff;
+  for (int i = lane; i < w * h; i += 64) {
+    const int y = i / w, x = i - y * w;
+    int av;
+    if (kind == 3 || kind == 5) {
+      // first pass rows y and y+1 at column x, then the vertical tap
+      const Pix* r0 = pa + (int64_t)y * as + x;
+      const Pix* r1 = r0 + as;
+      const int f0 = kBil[xo][0], f1 = kBil[xo][1];
+      const int h0 = (r0[0] * f0 + r0[1] * f1 + 64) >> 7;
+      const int h1 = (r1[0] * f0 + r1[1] * f1 + 64) >> 7;
+      av = (h0 * kBil[yo][0] + h1 * kBil[yo][1] + 64) >> 7;
+      if (sizeof(Pix) == 1) av &= 0xFF;  // lowbd second pass stores uint8
+      else av &= 0xFFFF;
+      if (kind == 5) av = (second[jb.aux_off + (int64_t)y * w + x] + av + 1) >> 1;
+    } else {
+      av = pa[(int64_t)y * as + x];
+    }
+    const int d = av - (int)pb[(int64_t)y * bs + x];
+    sum += d;
+    sse += (uint32_t)(d * d);
+  }
+  sum = wave_sum64(sum);
+  sse = (uint64_t)wave_sum64((int64_t)sse);
+  if (lane != 0) return;
+  const int64_t j = blockIdx.x;
+  if (kind == 4) {
+    sse64_out[j] = (int64_t)sse;
+    return;
+  }
+  uint32_t s32;
+  int sm;
+  if (bd == 8) {
+    s32 = (uint32_t)sse;
+    sm = (int)sum;
+  } else {
+    const int ss_ = bd == 10 ? 4 : 8, sh = bd == 10 ? 2 : 4;
+    s32 = (uint32_t)((sse + ((1ull << ss_) >> 1)) >> ss_);
+    sm = (int)((sum + ((1ll << sh) >> 1)) >> sh);
+  }
+  if (sse_out) sse_out[j] = s32;
+  if (sum_out) sum_out[j] = sm;
+  if (var_out) {
+    if (kind == 1) {
+      var_out[j] = s32;
+    } else if (sizeof(Pix) == 1 || bd == 8) {
+      var_out[j] = s32 - (uint32_t)(((int64_t)sm * sm) / (w * h));
+    } else {
+      const int64_t v = (int64_t)s32 - (((int64_t)sm * sm) / (w * h));
+      var_out[j] = v >= 0 ? (uint32_t)v : 0;
+    }
+  }
+}
+
+// ------------------------------------------------------------ subtract ----
+template <typename Pix>
+__global__ void subtract_kernel(int rows, int cols, int16_t* diff, int ds, const Pix* src, int ss,
+                                const Pix* pred, int ps, const LavishPixJob* jobs) {
+  const LavishPixJob jb = jobs[blockIdx.x];
+  for (int i = threadIdx.x; i < rows * cols; i += blockDim.x) {
+    const int y = i / cols, x = i - y * cols;
+    diff[jb.aux_off + (int64_t)y * ds + x] =
+        (int16_t)((int)src[jb.src_off + (int64_t)y * ss + x] -
+                  (int)pred[jb.ref_off[0] + (int64_t)y * ps + x]);
+  }
+}
+
+// --------------------------------------------------------- sum squares ----
+__global__ __launch_bounds__(64) void sum_squares_kernel(const int16_t* src, int stride, int w,
+                                                         int h, const LavishPixJob* jobs,
+                                                         uint64_t* out) {
+  const LavishPixJob jb = jobs[blockIdx.x];
+  uint64_t acc = 0;
+  for (int i = threadIdx.x; i < w * h; i += 64) {
+    const int y = i / w, x = i - y * w;
+    const int v = src[jb.src_off + (int64_t)y * stride + x];
+    acc += (uint64_t)(v * v);
+  }
+  acc = (uint64_t)wave_sum64((int64_t)acc);
+  if (threadIdx.x == 0) out[blockIdx.x] = acc;
+}
+
+// ------------------------------------------------------------ hadamard ----
+// int16 butterflies with the reference's output permutations.
+__device__ __forceinline__ void had_col8(const int16_t* s, int st, int16_t* o) {
+  int16_t b[8], c[8];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    b[2 * k] = (int16_t)(s[2 * k * st] + s[(2 * k + 1) * st]);
+    b[2 * k + 1] = (int16_t)(s[2 * k * st] - s[(2 * k + 1) * st]);
+  }
+  c[0] = (int16_t)(b[0] + b[2]);
+  c[1] = (int16_t)(b[1] + b[3]);
+  c[2] = (int16_t)(b[0] - b[2]);
+  c[3] = (int16_t)(b[1] - b[3]);
+  c[4] = (int16_t)(b[4] + b[6]);
+  c[5] = (int16_t)(b[5] + b[7]);
+  c[6] = (int16_t)(b[4] - b[6]);
+  c[7] = (int16_t)(b[5] - b[7]);
+  o[0] = (int16_t)(c[0] + c[4]);
+  o[7] = (int16_t)(c[1] + c[5]);
+  o[3] = (int16_t)(c[2] + c[6]);
+  o[4] = (int16_t)(c[3] + c[7]);
+  o[2] = (int16_t)(c[0] - c[4]);
+  o[6] = (int16_t)(c[1] - c[5]);
+  o[1] = (int16_t)(c[2] - c[6]);
+  o[5] = (int16_t)(c[3] - c[7]);
+}
+__device__ __forceinline__ void had_col4(const int16_t* s, int st, int16_t* o) {
+  const int16_t b0 = (int16_t)((s[0] + s[st]) >> 1);
+  const int16_t b1 = (int16_t)((s[0] - s[st]) >> 1);
+  const int16_t b2 = (int16_t)((s[2 * st] + s[3 * st]) >> 1);
+  const int16_t b3 = (int16_t)((s[2 * st] - s[3 * st]) >> 1);
+  o[0] = (int16_t)(b0 + b2);
+  o[1] = (int16_t)(b1 + b3);
+  o[2] = (int16_t)(b0 - b2);
+  o[3] = (int16_t)(b1 - b3);
+}
+
+// second column pass of aom_highbd_hadamard_8x8_c: int16 in, int32 math
+__device__ __forceinline__ void had_col8_i32(const int16_t* s, int st, int32_t* o) {
+  int32_t b[8], c[8];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    b[2 * k] = s[2 * k * st] + s[(2 * k + 1) * st];
+    b[2 * k + 1] = s[2 * k * st] - s[(2 * k + 1) * st];
+  }
+  c[0] = b[0] + b[2];
+  c[1] = b[1] + b[3];
+  c[2] = b[0] - b[2];
+  c[3] = b[1] - b[3];
+  c[4] = b[4] + b[6];
+  c[5] = b[5] + b[7];
+  c[6] = b[4] - b[6];
+  c[7] = b[5] - b[7];
+  o[0] = c[0] + c[4];
+  o[7] = c[1] + c[5];
+  o[3] = c[2] + c[6];
+  o[4] = c[3] + c[7];
+  o[2] = c[0] - c[4];
+  o[6] = c[1] - c[5];
+  o[1] = c[2] - c[6];
+  o[5] = c[3] - c[7];
+}
+
+// n x n (n = 4, 8) Hadamard of one block by one lane: two column passes.
+// lowbd: int16 throughout and a transposed output (aom_hadamard_{4x4,8x8}_c
+// "extra transpose"); highbd 8x8: int32 second pass, no transpose.
+template <int n, bool HBD>
+__device__ __forceinline__ void had_small(const int16_t* src, int st, int32_t* coeff) {
+  int16_t b1[n * n];
+#pragma unroll
+  for (int i = 0; i < n; ++i) {
+    if constexpr (n == 4) had_col4(src + i, st, b1 + 4 * i);
+    else had_col8(src + i, st, b1 + 8 * i);
+  }
+  if constexpr (HBD) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) had_col8_i32(b1 + i, 8, coeff + 8 * i);
+  } else {
+    int16_t b2[n * n];
+#pragma unroll
+    for (int i = 0; i < n; ++i) {
+      if constexpr (n == 4) had_col4(b1 + i, 4, b2 + 4 * i);
+      else had_col8(b1 + i, 8, b2 + 8 * i);
+    }
+#pragma unroll
+    for (int i = 0; i < n; ++i)
+#pragma unroll
+      for (int j = 0; j < n; ++j) coeff[i * n + j] = b2[j * n + i];
+  }
+}
+
+// jobs: src_off = element offset of the block, aux_off = coefficient offset
+__global__ __launch_bounds__(64) void hadamard_small_kernel(int n, int highbd, const int16_t* src,
+                                                            int stride, const LavishPixJob* jobs,
+                                                            int njobs, int32_t* coeff) {
+  const int j = blockIdx.x * 64 + threadIdx.x;
+  if (j >= njobs) return;
+  const LavishPixJob jb = jobs[j];
+  int32_t c[64];
+  if (n == 4) had_small<4, false>(src + jb.src_off, stride, c);
+  else if (highbd) had_small<8, true>(src + jb.src_off, stride, c);
+  else had_small<8, false>(src + jb.src_off, stride, c);
+  for (int i = 0; i < n * n; ++i) coeff[jb.aux_off + i] = c[i];
+}
+
+// 16x16 / 32x32: one wave per job; 8x8 sub-blocks by lanes into LDS, then the
+// combine stages (avg.c:226-348) over all lanes.
+__global__ __launch_bounds__(64) void hadamard_big_kernel(int n, int highbd, const int16_t* src,
+                                                          int stride, const LavishPixJob* jobs,
+                                                          int32_t* coeff) {
+  __shared__ int32_t c[1024];
+  const LavishPixJob jb = jobs[blockIdx.x];
+  const int lane = threadIdx.x;
+  const int16_t* s = src + jb.src_off;
+  // 16x16 quadrant q of the block at (qy, qx) holds 4 8x8 sub-blocks idx
+  const int nq = n == 32 ? 4 : 1;
+  if (lane < 4 * nq) {
+    const int q = lane >> 2, idx = lane & 3;
+    const int qy = (q >> 1) * 16, qx = (q & 1) * 16;
+    const int16_t* p = s + (int64_t)(qy + (idx >> 1) * 8) * stride + qx + (idx & 1) * 8;
+    if (highbd) had_small<8, true>(p, stride, c + q * 256 + idx * 64);
+    else had_small<8, false>(p, stride, c + q * 256 + idx * 64);
+  }
+  __syncthreads();
+  for (int q = 0; q < nq; ++q) {
+    int32_t* cq = c + q * 256;
+    const int i = lane;  // 64 lanes x one column of 4
+    const int32_t a0 = cq[i], a1 = cq[64 + i], a2 = cq[128 + i], a3 = cq[192 + i];
+    const int32_t b0 = (a0 + a1) >> 1, b1 = (a0 - a1) >> 1;
+    const int32_t b2 = (a2 + a3) >> 1, b3 = (a2 - a3) >> 1;
+    __syncthreads();
+    cq[i] = b0 + b2;
+    cq[64 + i] = b1 + b3;
+    cq[128 + i] = b0 - b2;
+    cq[192 + i] = b1 - b3;
+    __syncthreads();
+    // lowbd only: swap of 4-wide groups to match the AVX2 order (avg.c:281-287)
+    if (!highbd) {
+      const int row = lane >> 2, jj = lane & 3;
+      const int32_t t = cq[row * 16 + 4 + jj];
+      const int32_t u = cq[row * 16 + 8 + jj];
+      cq[row * 16 + 4 + jj] = u;
+      cq[row * 16 + 8 + jj] = t;
+    }
+    __syncthreads();
+  }
+  if (n == 32) {
+    for (int i = lane; i < 256; i += 64) {
+      const int32_t a0 = c[i], a1 = c[256 + i], a2 = c[512 + i], a3 = c[768 + i];
+      const int32_t b0 = (a0 + a1) >> 2, b1 = (a0 - a1) >> 2;
+      const int32_t b2 = (a2 + a3) >> 2, b3 = (a2 - a3) >> 2;
+      c[i] = b0 + b2;
+      c[256 + i] = b1 + b3;
+      c[512 + i] = b0 - b2;
+      c[768 + i] = b1 - b3;
+    }
+    __syncthreads();
+  }
+  for (int i = lane; i < n * n; i += 64) coeff[jb.aux_off + i] = c[i];
+}
+
+// ---------------------------------------------------------------- SATD ----
+__global__ __launch_bounds__(64) void satd_kernel(const int32_t* coeff, int length, int* out) {
+  const int32_t* c = coeff + (int64_t)blockIdx.x * length;
+  uint32_t acc = 0;
+  for (int i = threadIdx.x; i < length; i += 64) acc += (uint32_t)abs(c[i]);
+  acc = wave_sum32(acc);
+  if (threadIdx.x == 0) out[blockIdx.x] = (int)acc;
+}
+
+// --------------------------------------------------------- block error ----
+__global__ __launch_bounds__(64) void block_error_kernel(const int32_t* coeff,
+                                                         const int32_t* dqcoeff, int n, int bd,
+                                                         int64_t* err_out, int64_t* ssz_out) {
+  const int64_t base = (int64_t)blockIdx.x * n;
+  int64_t err = 0, sq = 0;
+  for (int i = threadIdx.x; i < n; i += 64) {
+    const int32_t c = coeff[base + i], d = dqcoeff[base + i];
+    if (bd == 0) {  // lowbd: the reference squares in int (wrapping) arithmetic
+      const int32_t df = (int32_t)((uint32_t)c - (uint32_t)d);
+      err += (int32_t)((uint32_t)df * (uint32_t)df);
+      sq += (int32_t)((uint32_t)c * (uint32_t)c);
+    } else {
+      const int64_t df = (int64_t)c - d;
+      err += df * df;
+      sq += (int64_t)c * c;
+    }
+  }
+  err = wave_sum64(err);
+  sq = wave_sum64(sq);
+  if (threadIdx.x == 0) {
+    if (bd > 8) {
+      const int shift = 2 * (bd - 8);
+      const int64_t rnd = (int64_t)1 << (shift - 1);
+      err = (err + rnd) >> shift;
+      sq = (sq + rnd) >> shift;
+    }
+    err_out[blockIdx.x] = err;
+    ssz_out[blockIdx.x] = sq;
+  }
+}
+
+}  // namespace lavish
+
+using namespace lavish;
+
+#define LCHK() LAVISH_CHECK(hipGetLastError())
+
+extern "C" {
+
+int lavish_sad_batch(const void* src, int src_stride, const void* ref, int ref_stride, int w,
+                     int h, const LavishPixJob* jobs, int njobs, int nrefs, int mode,
+                     const void* second_pred, int highbd, uint32_t* sad_out, void* stream) {
+  if (njobs <= 0) return 0;
+  if (nrefs < 1 || nrefs > 4 || mode < 0 || mode > 2 || (mode == 2 && !second_pred)) return -1;
+  hipStream_t s = (hipStream_t)stream;
+  if (highbd)
+    hipLaunchKernelGGL(sad_kernel<uint16_t>, dim3(njobs), dim3(64), 0, s, (const uint16_t*)src,
+                       src_stride, (const uint16_t*)ref, ref_stride, w, h, jobs, nrefs, mode,
+                       (const uint16_t*)second_pred, sad_out);
+  else
+    hipLaunchKernelGGL(sad_kernel<uint8_t>, dim3(njobs), dim3(64), 0, s, (const uint8_t*)src,
+                       src_stride, (const uint8_t*)ref, ref_stride, w, h, jobs, nrefs, mode,
+                       (const uint8_t*)second_pred, sad_out);
+  LCHK();
+  return 0;
+}
+
+int lavish_variance_batch(const void* a, int a_stride, const void* b, int b_stride, int w, int h,
+                          const LavishPixJob* jobs, int njobs, int kind, int bit_depth,
+                          int highbd, const void* second_pred, uint32_t* var_out, uint32_t* sse_out, int32_t* sum_out,
+                          int64_t* sse64_out, void* stream) {
+  if (njobs <= 0) return 0;
+  if (kind < 0 || kind > 5 || (kind == 5 && !second_pred)) return -1;
+  hipStream_t s = (hipStream_t)stream;
+  if (highbd)
+    hipLaunchKernelGGL(var_kernel<uint16_t>, dim3(njobs), dim3(64), 0, s, (const uint16_t*)a,
+                       a_stride, (const uint16_t*)b, b_stride, w, h, jobs, kind, bit_depth,
+                       (const uint16_t*)second_pred, var_out, sse_out, sum_out, sse64_out);
+  else
+    hipLaunchKernelGGL(var_kernel<uint8_t>, dim3(njobs), dim3(64), 0, s, (const uint8_t*)a,
+                       a_stride, (const uint8_t*)b, b_stride, w, h, jobs, kind, 8,
+                       (const uint8_t*)second_pred, var_out,
+                       sse_out, sum_out, sse64_out);
+  LCHK();
+  return 0;
+}
+
+int lavish_subtract_batch(int rows, int cols, int16_t* diff, int diff_stride, const void* src,
+                          int src_stride, const void* pred, int pred_stride,
+                          const LavishPixJob* jobs, int njobs, int highbd, void* stream) {
+  if (njobs <= 0) return 0;
+  hipStream_t s = (hipStream_t)stream;
+  if (highbd)
+    hipLaunchKernelGGL(subtract_kernel<uint16_t>, dim3(njobs), dim3(256), 0, s, rows, cols, diff,
+                       diff_stride, (const uint16_t*)src, src_stride, (const uint16_t*)pred,
+                       pred_stride, jobs);
+  else
+    hipLaunchKernelGGL(subtract_kernel<uint8_t>, dim3(njobs), dim3(256), 0, s, rows, cols, diff,
+                       diff_stride, (const uint8_t*)src, src_stride, (const uint8_t*)pred,
+                       pred_stride, jobs);
+  LCHK();
+  return 0;
+}
+
+int lavish_sum_squares_batch(const int16_t* src, int stride, int w, int h,
+                             const LavishPixJob* jobs, int njobs, uint64_t* out, void* stream) {
+  if (njobs <= 0) return 0;
+  hipLaunchKernelGGL(sum_squares_kernel, dim3(njobs), dim3(64), 0, (hipStream_t)stream, src,
+                     stride, w, h, jobs, out);
+  LCHK();
+  return 0;
+}
+
+int lavish_hadamard_batch(int n, int highbd, const int16_t* src_diff, int stride,
+                          const LavishPixJob* jobs, int njobs, int32_t* coeff, void* stream) {
+  if (njobs <= 0) return 0;
+  if (highbd && n == 4) return -1;  // no aom_highbd_hadamard_4x4 in the reference
+  hipStream_t s = (hipStream_t)stream;
+  if (n == 4 || n == 8)
+    hipLaunchKernelGGL(hadamard_small_kernel, dim3((njobs + 63) / 64), dim3(64), 0, s, n, highbd,
+                       src_diff, stride, jobs, njobs, coeff);
+  else if (n == 16 || n == 32)
+    hipLaunchKernelGGL(hadamard_big_kernel, dim3(njobs), dim3(64), 0, s, n, highbd, src_diff,
+                       stride, jobs, coeff);
+  else
+    return -1;
+  LCHK();
+  return 0;
+}
+
+int lavish_satd_batch(const int32_t* coeff, int length, int nblocks, int* out, void* stream) {
+  if (nblocks <= 0) return 0;
+  hipLaunchKernelGGL(satd_kernel, dim3(nblocks), dim3(64), 0, (hipStream_t)stream, coeff, length,
+                     out);
+  LCHK();
+  return 0;
+}
+
+int lavish_block_error_batch(const int32_t* coeff, const int32_t* dqcoeff, int n, int nblocks,
+                             int bit_depth, int64_t* err, int64_t* ssz, void* stream) {
+  if (nblocks <= 0) return 0;
+  hipLaunchKernelGGL(block_error_kernel, dim3(nblocks), dim3(64), 0, (hipStream_t)stream, coeff,
+                     dqcoeff, n, bit_depth, err, ssz);
+  LCHK();
+  return 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,363 @@
+// pixel_shims.hip -- per-call RTCD shims (host pointers) for the pixel-domain
+// kernels of pixel.hip: SAD, variance, MSE, SSE, subtract, sum of squares,
+// Hadamard, SATD, block error.  Each call stages the caller's block(s) into a
+// per-thread device scratch (hipMemcpy2DAsync, so only the w x h window of a
+// strided plane is read), runs the batch kernel on a single job, and copies
+// the result back.  Drop-in parity, not speed (SURVEY.md 8(b) "Granularity").
+// Highbd pixel pointers arrive tagged (CONVERT_TO_BYTEPTR, aom_ports/mem.h:79-80).
+#include <string.h>
+
+#include "lavish_internal.h"
+
+namespace lavish {
+namespace {
+
+template <typename T>
+T* untag(const uint8_t* p) {
+  if constexpr (sizeof(T) == 2) return (T*)((uintptr_t)p << 1);
+  else return (T*)p;
+}
+
+// bump allocator over the per-thread scratch for one shim call
+struct Stage {
+  char* base;
+  size_t used = 0;
+  hipStream_t s;
+  explicit Stage(size_t cap) : base((char*)shim_scratch(cap)), s(shim_stream()) {}
+  void* take(size_t bytes) {
+    void* p = base + used;
+    used += (bytes + 255) & ~(size_t)255;
+    return p;
+  }
+  // copy a w x h window (stride in elements) into a compact device block
+  template <typename T>
+  T* block(const T* host, ptrdiff_t stride, int w, int h) {
+    T* d = (T*)take((size_t)w * h * sizeof(T));
+    LAVISH_CHECK(hipMemcpy2DAsync(d, (size_t)w * sizeof(T), host, (size_t)stride * sizeof(T),
+                                  (size_t)w * sizeof(T), h, hipMemcpyHostToDevice, s));
+    return d;
+  }
+  template <typename T>
+  T* copy_in(const T* host, size_t n) {
+    T* d = (T*)take(n * sizeof(T));
+    LAVISH_CHECK(hipMemcpyAsync(d, host, n * sizeof(T), hipMemcpyHostToDevice, s));
+    return d;
+  }
+  template <typename T>
+  void copy_out(T* host, const T* dev, size_t n) {
+    LAVISH_CHECK(hipMemcpyAsync(host, dev, n * sizeof(T), hipMemcpyDeviceToHost, s));
+  }
+  void sync() { LAVISH_CHECK(hipStreamSynchronize(s)); }
+};
+
+constexpr size_t kStageCap = 4u << 20;  // 128x128 u16 x (src + 4 refs + second) + outputs
+
+void must(int rc, const char* what) {
+  if (rc != 0) {
+    fprintf(stderr, "[lavish_hip] %s rejected its arguments (rc %d)\n", what, rc);
+    abort();
+  }
+}
+
+template <typename Pix>
+void sad_shim(const uint8_t* src8, int ss, const uint8_t* const* refs8, int nrefs, int rs, int w,
+              int h, int mode, const uint8_t* second8, uint32_t* out) {
+  Stage st(kStageCap);
+  const Pix* src = st.block(untag<Pix>(src8), ss, w, h);
+  Pix* ref = (Pix*)st.take((size_t)nrefs * w * h * sizeof(Pix));
+  LavishPixJob jb{};
+  for (int k = 0; k < nrefs; ++k) {
+    LAVISH_CHECK(hipMemcpy2DAsync(ref + (size_t)k * w * h, (size_t)w * sizeof(Pix),
+                                  untag<Pix>(refs8[k]), (size_t)rs * sizeof(Pix),
+                                  (size_t)w * sizeof(Pix), h, hipMemcpyHostToDevice, st.s));
+    jb.ref_off[k] = (int64_t)k * w * h;
+  }
+  const Pix* second = mode == 2 ? st.copy_in(untag<Pix>(second8), (size_t)w * h) : nullptr;
+  const LavishPixJob* djob = st.copy_in(&jb, 1);
+  uint32_t* dout = (uint32_t*)st.take(4 * sizeof(uint32_t));
+  must(lavish_sad_batch(src, w, ref, w, w, h, djob, 1, nrefs, mode, second, sizeof(Pix) == 2,
+                        dout, st.s),
+       "lavish_sad_batch");
+  st.copy_out(out, dout, nrefs);
+  st.sync();
+}
+
+template <typename Pix>
+uint32_t sad1(const uint8_t* src, int ss, const uint8_t* ref, int rs, int w, int h, int mode,
+              const uint8_t* second) {
+  uint32_t r;
+  const uint8_t* refs[1] = {ref};
+  sad_shim<Pix>(src, ss, refs, 1, rs, w, h, mode, second, &r);
+  return r;
+}
+
+// variance family: returns var_out; sse / sum through the pointers
+template <typename Pix>
+uint32_t var_shim(const uint8_t* a8, int as, const uint8_t* b8, int bs, int w, int h, int kind,
+                  int bd, int xoff, int yoff, const uint8_t* second8, uint32_t* sse, int* sum) {
+  Stage st(kStageCap);
+  const bool sub = kind == 3 || kind == 5;
+  const Pix* a = st.block(untag<Pix>(a8), as, sub ? w + 1 : w, sub ? h + 1 : h);
+  const Pix* b = st.block(untag<Pix>(b8), bs, w, h);
+  const Pix* second = kind == 5 ? st.copy_in(untag<Pix>(second8), (size_t)w * h) : nullptr;
+  LavishPixJob jb{};
+  jb.xoff = xoff;
+  jb.yoff = yoff;
+  const LavishPixJob* djob = st.copy_in(&jb, 1);
+  uint32_t* dv = (uint32_t*)st.take(64);
+  uint32_t* ds = (uint32_t*)st.take(64);
+  int32_t* dsum = (int32_t*)st.take(64);
+  must(lavish_variance_batch(a, sub ? w + 1 : w, b, w, w, h, djob, 1, kind, bd, sizeof(Pix) == 2,
+                             second, dv, ds, dsum, nullptr, st.s),
+       "lavish_variance_batch");
+  uint32_t v = 0;
+  st.copy_out(&v, dv, 1);
+  if (sse) st.copy_out(sse, ds, 1);
+  if (sum) st.copy_out(sum, dsum, 1);
+  st.sync();
+  return v;
+}
+
+template <typename Pix>
+int64_t sse_shim(const uint8_t* a8, int as, const uint8_t* b8, int bs, int w, int h) {
+  Stage st(kStageCap + (size_t)w * h * 2 * sizeof(Pix));
+  const Pix* a = st.block(untag<Pix>(a8), as, w, h);
+  const Pix* b = st.block(untag<Pix>(b8), bs, w, h);
+  LavishPixJob jb{};
+  const LavishPixJob* djob = st.copy_in(&jb, 1);
+  int64_t* d = (int64_t*)st.take(64);
+  must(lavish_variance_batch(a, w, b, w, w, h, djob, 1, 4, 8, sizeof(Pix) == 2, nullptr, nullptr,
+                             nullptr, nullptr, d, st.s),
+       "lavish_variance_batch");
+  int64_t r = 0;
+  st.copy_out(&r, d, 1);
+  st.sync();
+  return r;
+}
+
+template <typename Pix>
+void subtract_shim(int rows, int cols, int16_t* diff, ptrdiff_t ds, const uint8_t* src8,
+                   ptrdiff_t ss, const uint8_t* pred8, ptrdiff_t ps) {
+  Stage st(kStageCap + (size_t)rows * cols * 4 * sizeof(Pix));
+  const Pix* src = st.block(untag<Pix>(src8), ss, cols, rows);
+  const Pix* pred = st.block(untag<Pix>(pred8), ps, cols, rows);
+  int16_t* dd = (int16_t*)st.take((size_t)rows * cols * sizeof(int16_t));
+  LavishPixJob jb{};
+  const LavishPixJob* djob = st.copy_in(&jb, 1);
+  must(lavish_subtract_batch(rows, cols, dd, cols, src, cols, pred, cols, djob, 1,
+                             sizeof(Pix) == 2, st.s),
+       "lavish_subtract_batch");
+  LAVISH_CHECK(hipMemcpy2DAsync(diff, (size_t)ds * sizeof(int16_t), dd, (size_t)cols * 2,
+                                (size_t)cols * 2, rows, hipMemcpyDeviceToHost, st.s));
+  st.sync();
+}
+
+void hadamard_shim(int n, int highbd, const int16_t* src, ptrdiff_t stride, int32_t* coeff) {
+  Stage st(kStageCap);
+  const int16_t* d = st.block(src, stride, n, n);
+  int32_t* dc = (int32_t*)st.take((size_t)n * n * sizeof(int32_t));
+  LavishPixJob jb{};
+  const LavishPixJob* djob = st.copy_in(&jb, 1);
+  must(lavish_hadamard_batch(n, highbd, d, n, djob, 1, dc, st.s), "lavish_hadamard_batch");
+  st.copy_out(coeff, dc, (size_t)n * n);
+  st.sync();
+}
+
+int64_t block_error_shim(const int32_t* coeff, const int32_t* dqcoeff, intptr_t n, int64_t* ssz,
+                         int bd) {
+  Stage st(kStageCap + (size_t)n * 8);
+  const int32_t* c = st.copy_in(coeff, n);
+  const int32_t* dq = st.copy_in(dqcoeff, n);
+  int64_t* de = (int64_t*)st.take(64);
+  int64_t* dz = (int64_t*)st.take(64);
+  must(lavish_block_error_batch(c, dq, (int)n, 1, bd, de, dz, st.s), "lavish_block_error_batch");
+  int64_t e = 0;
+  st.copy_out(&e, de, 1);
+  st.copy_out(ssz, dz, 1);
+  st.sync();
+  return e;
+}
+
+}  // namespace
+}  // namespace lavish
+
+using namespace lavish;
+
+extern "C" {
+
+#define SAD_SHIMS(w, h)                                                                          \
+  unsigned int aom_sad##w##x##h##_hip(const uint8_t* s, int ss, const uint8_t* r, int rs) {      \
+    return sad1<uint8_t>(s, ss, r, rs, w, h, 0, nullptr);                                        \
+  }                                                                                              \
+  unsigned int aom_sad_skip_##w##x##h##_hip(const uint8_t* s, int ss, const uint8_t* r,          \
+                                            int rs) {                                            \
+    return sad1<uint8_t>(s, ss, r, rs, w, h, 1, nullptr);                                        \
+  }                                                                                              \
+  unsigned int aom_sad##w##x##h##_avg_hip(const uint8_t* s, int ss, const uint8_t* r, int rs,    \
+                                          const uint8_t* sp) {                                   \
+    return sad1<uint8_t>(s, ss, r, rs, w, h, 2, sp);                                             \
+  }                                                                                              \
+  void aom_sad##w##x##h##x4d_hip(const uint8_t* s, int ss, const uint8_t* const r[4], int rs,    \
+                                 uint32_t out[4]) {                                              \
+    sad_shim<uint8_t>(s, ss, r, 4, rs, w, h, 0, nullptr, out);                                   \
+  }                                                                                              \
+  /* x3d forwards to x4d in the reference (sad.c:122-128) */                                     \
+  void aom_sad##w##x##h##x3d_hip(const uint8_t* s, int ss, const uint8_t* const r[4], int rs,    \
+                                 uint32_t out[4]) {                                              \
+    sad_shim<uint8_t>(s, ss, r, 4, rs, w, h, 0, nullptr, out);                                   \
+  }                                                                                              \
+  void aom_sad##w##x##h##x4d_avg_hip(const uint8_t* s, int ss, const uint8_t* const r[4],        \
+                                     int rs, const uint8_t* sp, uint32_t out[4]) {               \
+    sad_shim<uint8_t>(s, ss, r, 4, rs, w, h, 2, sp, out);                                        \
+  }                                                                                              \
+  void aom_sad_skip_##w##x##h##x4d_hip(const uint8_t* s, int ss, const uint8_t* const r[4],      \
+                                       int rs, uint32_t out[4]) {                                \
+    sad_shim<uint8_t>(s, ss, r, 4, rs, w, h, 1, nullptr, out);                                   \
+  }                                                                                              \
+  unsigned int aom_highbd_sad##w##x##h##_hip(const uint8_t* s, int ss, const uint8_t* r,         \
+                                             int rs) {                                           \
+    return sad1<uint16_t>(s, ss, r, rs, w, h, 0, nullptr);                                       \
+  }                                                                                              \
+  unsigned int aom_highbd_sad_skip_##w##x##h##_hip(const uint8_t* s, int ss, const uint8_t* r,   \
+                                                   int rs) {                                     \
+    return sad1<uint16_t>(s, ss, r, rs, w, h, 1, nullptr);                                       \
+  }                                                                                              \
+  unsigned int aom_highbd_sad##w##x##h##_avg_hip(const uint8_t* s, int ss, const uint8_t* r,     \
+                                                 int rs, const uint8_t* sp) {                    \
+    return sad1<uint16_t>(s, ss, r, rs, w, h, 2, sp);                                            \
+  }                                                                                              \
+  void aom_highbd_sad##w##x##h##x4d_hip(const uint8_t* s, int ss, const uint8_t* const r[],      \
+                                        int rs, uint32_t* out) {                                 \
+    sad_shim<uint16_t>(s, ss, r, 4, rs, w, h, 0, nullptr, out);                                  \
+  }                                                                                              \
+  void aom_highbd_sad##w##x##h##x3d_hip(const uint8_t* s, int ss, const uint8_t* const r[],      \
+                                        int rs, uint32_t* out) {                                 \
+    sad_shim<uint16_t>(s, ss, r, 4, rs, w, h, 0, nullptr, out);                                  \
+  }                                                                                              \
+  void aom_highbd_sad_skip_##w##x##h##x4d_hip(const uint8_t* s, int ss,                          \
+                                              const uint8_t* const r[], int rs, uint32_t* out) { \
+    sad_shim<uint16_t>(s, ss, r, 4, rs, w, h, 1, nullptr, out);                                  \
+  }
+
+#define VAR_SHIMS_BD(pre, Pix, bd, w, h)                                                       \
+  unsigned int pre##variance##w##x##h##_hip(const uint8_t* s, int ss, const uint8_t* r, int rs, \
+                                            uint32_t* sse) {                                    \
+    return var_shim<Pix>(s, ss, r, rs, w, h, 0, bd, 0, 0, nullptr, sse, nullptr);              \
+  }                                                                                             \
+  uint32_t pre##sub_pixel_variance##w##x##h##_hip(const uint8_t* s, int ss, int xo, int yo,     \
+                                                  const uint8_t* r, int rs, uint32_t* sse) {    \
+    return var_shim<Pix>(s, ss, r, rs, w, h, 3, bd, xo, yo, nullptr, sse, nullptr);            \
+  }                                                                                             \
+  uint32_t pre##sub_pixel_avg_variance##w##x##h##_hip(const uint8_t* s, int ss, int xo, int yo, \
+                                                      const uint8_t* r, int rs, uint32_t* sse,  \
+                                                      const uint8_t* sp) {                      \
+    return var_shim<Pix>(s, ss, r, rs, w, h, 5, bd, xo, yo, sp, sse, nullptr);                 \
+  }
+#define VAR_SHIMS(w, h)                          \
+  VAR_SHIMS_BD(aom_, uint8_t, 8, w, h)           \
+  VAR_SHIMS_BD(aom_highbd_8_, uint16_t, 8, w, h) \
+  VAR_SHIMS_BD(aom_highbd_10_, uint16_t, 10, w, h) \
+  VAR_SHIMS_BD(aom_highbd_12_, uint16_t, 12, w, h)
+
+LAVISH_ENCODER_BLOCK_SIZES(SAD_SHIMS)
+LAVISH_ENCODER_BLOCK_SIZES(VAR_SHIMS)
+
+#define MSE_SHIMS(pre, Pix, bd)                                                                 \
+  void pre##get16x16var_hip(const uint8_t* s, int ss, const uint8_t* r, int rs,                 \
+                            unsigned int* sse, int* sum) {                                      \
+    var_shim<Pix>(s, ss, r, rs, 16, 16, 2, bd, 0, 0, nullptr, sse, sum);                        \
+  }                                                                                             \
+  void pre##get8x8var_hip(const uint8_t* s, int ss, const uint8_t* r, int rs, unsigned int* sse, \
+                          int* sum) {                                                           \
+    var_shim<Pix>(s, ss, r, rs, 8, 8, 2, bd, 0, 0, nullptr, sse, sum);                          \
+  }                                                                                             \
+  unsigned int pre##mse16x16_hip(const uint8_t* s, int ss, const uint8_t* r, int rs,            \
+                                 unsigned int* sse) {                                           \
+    return var_shim<Pix>(s, ss, r, rs, 16, 16, 1, bd, 0, 0, nullptr, sse, nullptr);             \
+  }                                                                                             \
+  unsigned int pre##mse16x8_hip(const uint8_t* s, int ss, const uint8_t* r, int rs,             \
+                                unsigned int* sse) {                                            \
+    return var_shim<Pix>(s, ss, r, rs, 16, 8, 1, bd, 0, 0, nullptr, sse, nullptr);              \
+  }                                                                                             \
+  unsigned int pre##mse8x16_hip(const uint8_t* s, int ss, const uint8_t* r, int rs,             \
+                                unsigned int* sse) {                                            \
+    return var_shim<Pix>(s, ss, r, rs, 8, 16, 1, bd, 0, 0, nullptr, sse, nullptr);              \
+  }                                                                                             \
+  unsigned int pre##mse8x8_hip(const uint8_t* s, int ss, const uint8_t* r, int rs,              \
+                               unsigned int* sse) {                                             \
+    return var_shim<Pix>(s, ss, r, rs, 8, 8, 1, bd, 0, 0, nullptr, sse, nullptr);               \
+  }
+MSE_SHIMS(aom_, uint8_t, 8)
+MSE_SHIMS(aom_highbd_8_, uint16_t, 8)
+MSE_SHIMS(aom_highbd_10_, uint16_t, 10)
+MSE_SHIMS(aom_highbd_12_, uint16_t, 12)
+
+void aom_subtract_block_hip(int rows, int cols, int16_t* diff, ptrdiff_t ds, const uint8_t* src,
+                            ptrdiff_t ss, const uint8_t* pred, ptrdiff_t ps) {
+  subtract_shim<uint8_t>(rows, cols, diff, ds, src, ss, pred, ps);
+}
+void aom_highbd_subtract_block_hip(int rows, int cols, int16_t* diff, ptrdiff_t ds,
+                                   const uint8_t* src, ptrdiff_t ss, const uint8_t* pred,
+                                   ptrdiff_t ps) {
+  subtract_shim<uint16_t>(rows, cols, diff, ds, src, ss, pred, ps);
+}
+
+int64_t aom_sse_hip(const uint8_t* a, int as, const uint8_t* b, int bs, int w, int h) {
+  return sse_shim<uint8_t>(a, as, b, bs, w, h);
+}
+int64_t aom_highbd_sse_hip(const uint8_t* a, int as, const uint8_t* b, int bs, int w, int h) {
+  return sse_shim<uint16_t>(a, as, b, bs, w, h);
+}
+
+uint64_t aom_sum_squares_2d_i16_hip(const int16_t* src, int stride, int w, int h) {
+  Stage st(kStageCap + (size_t)w * h * 2);
+  const int16_t* d = st.block(src, stride, w, h);
+  LavishPixJob jb{};
+  const LavishPixJob* djob = st.copy_in(&jb, 1);
+  uint64_t* dout = (uint64_t*)st.take(64);
+  must(lavish_sum_squares_batch(d, w, w, h, djob, 1, dout, st.s), "lavish_sum_squares_batch");
+  uint64_t r = 0;
+  st.copy_out(&r, dout, 1);
+  st.sync();
+  return r;
+}
+
+void aom_hadamard_4x4_hip(const int16_t* s, ptrdiff_t st, int32_t* c) { hadamard_shim(4, 0, s, st, c); }
+void aom_hadamard_8x8_hip(const int16_t* s, ptrdiff_t st, int32_t* c) { hadamard_shim(8, 0, s, st, c); }
+void aom_hadamard_16x16_hip(const int16_t* s, ptrdiff_t st, int32_t* c) {
+  hadamard_shim(16, 0, s, st, c);
+}
+void aom_hadamard_32x32_hip(const int16_t* s, ptrdiff_t st, int32_t* c) {
+  hadamard_shim(32, 0, s, st, c);
+}
+void aom_highbd_hadamard_8x8_hip(const int16_t* s, ptrdiff_t st, int32_t* c) {
+  hadamard_shim(8, 1, s, st, c);
+}
+void aom_highbd_hadamard_16x16_hip(const int16_t* s, ptrdiff_t st, int32_t* c) {
+  hadamard_shim(16, 1, s, st, c);
+}
+void aom_highbd_hadamard_32x32_hip(const int16_t* s, ptrdiff_t st, int32_t* c) {
+  hadamard_shim(32, 1, s, st, c);
+}
+
+int aom_satd_hip(const int32_t* coeff, int length) {
+  Stage st(kStageCap + (size_t)length * 4);
+  const int32_t* d = st.copy_in(coeff, length);
+  int* dout = (int*)st.take(64);
+  must(lavish_satd_batch(d, length, 1, dout, st.s), "lavish_satd_batch");
+  int r = 0;
+  st.copy_out(&r, dout, 1);
+  st.sync();
+  return r;
+}
+
+int64_t av1_block_error_hip(const int32_t* coeff, const int32_t* dqcoeff, intptr_t n,
+                            int64_t* ssz) {
+  return block_error_shim(coeff, dqcoeff, n, ssz, 0);
+}
+int64_t av1_highbd_block_error_hip(const int32_t* coeff, const int32_t* dqcoeff, intptr_t n,
+                                   int64_t* ssz, int bd) {
+  return block_error_shim(coeff, dqcoeff, n, ssz, bd);
+}
+
+}  // extern "C"

@@ -135,6 +135,74 @@ int lavish_quantize_batch(const int32_t *coeff, int n, int nblocks,
                           const LavishQuantParams *qp, int32_t *qcoeff,
                           int32_t *dqcoeff, uint16_t *eob, void *stream);
 
+/* ---- pixel-domain batch kernels ----------------------------------------- */
+/* One job = one block.  Offsets are in ELEMENTS (u8 or u16 samples / int16
+ * residual words) from the plane base pointers passed to the call.  Which
+ * fields a kernel reads is stated per call. */
+typedef struct LavishPixJob {
+  int64_t src_off;    /* first operand (src) */
+  int64_t ref_off[4]; /* second operand(s): ref / candidate positions */
+  int64_t aux_off;    /* second_pred / diff / coefficient offset */
+  int32_t xoff, yoff; /* sub-pixel offsets (1/8 pel, 0..7) */
+} LavishPixJob;
+
+/* SAD of a w x h block against nrefs (1..4) reference positions
+ * (aom_dsp/sad.c:22-129, highbd :240-330).
+ *   mode 0: aom_sad, 1: aom_sad_skip (2 x SAD of even rows),
+ *        2: aom_sad_avg against ROUND_POWER_OF_TWO(ref + second_pred, 1)
+ *           with second_pred at second_pred + job.aux_off, stride w.
+ *   highbd: 0 = u8 planes, 1 = u16 planes (plain device pointers).
+ *   sad_out[job * nrefs + k]. */
+int lavish_sad_batch(const void *src, int src_stride, const void *ref,
+                     int ref_stride, int w, int h, const LavishPixJob *jobs,
+                     int njobs, int nrefs, int mode, const void *second_pred,
+                     int highbd, uint32_t *sad_out, void *stream);
+
+/* Variance family, d = a[src_off] - b[ref_off[0]]
+ * (aom_dsp/variance.c:38-145,321-408,454-670).
+ *   kind 0: variance (var_out, sse_out), 1: mse (var_out = sse),
+ *        2: get_var (sse_out, sum_out), 3: sub-pixel variance of the
+ *        bilinear-filtered a (job.xoff/yoff; reads (h+1) x (w+1) of a),
+ *        4: sse as int64 (aom_sse / aom_highbd_sse; sse64_out),
+ *        5: sub-pixel avg variance (second_pred + job.aux_off, stride w).
+ *   bit_depth 8/10/12 selects the highbd rounding (highbd = 1 only).
+ * Unused output pointers may be NULL. */
+int lavish_variance_batch(const void *a, int a_stride, const void *b,
+                          int b_stride, int w, int h, const LavishPixJob *jobs,
+                          int njobs, int kind, int bit_depth, int highbd,
+                          const void *second_pred, uint32_t *var_out,
+                          uint32_t *sse_out, int32_t *sum_out,
+                          int64_t *sse64_out, void *stream);
+
+/* diff[aux_off + r*diff_stride + c] = src[src_off..] - pred[ref_off[0]..]
+ * (aom_subtract_block / aom_highbd_subtract_block, aom_dsp/subtract.c). */
+int lavish_subtract_batch(int rows, int cols, int16_t *diff, int diff_stride,
+                          const void *src, int src_stride, const void *pred,
+                          int pred_stride, const LavishPixJob *jobs,
+                          int njobs, int highbd, void *stream);
+
+/* aom_sum_squares_2d_i16 (aom_dsp/sum_squares.c:16-30) at src + src_off. */
+int lavish_sum_squares_batch(const int16_t *src, int stride, int w, int h,
+                             const LavishPixJob *jobs, int njobs,
+                             uint64_t *out, void *stream);
+
+/* aom_hadamard_{4x4,8x8,16x16,32x32} (highbd = 0) and
+ * aom_highbd_hadamard_{8x8,16x16,32x32} (highbd = 1), aom_dsp/avg.c:102-507:
+ * src_diff + job.src_off (stride) -> coeff + job.aux_off (n*n words). */
+int lavish_hadamard_batch(int n, int highbd, const int16_t *src_diff,
+                          int stride, const LavishPixJob *jobs, int njobs,
+                          int32_t *coeff, void *stream);
+
+/* aom_satd (aom_dsp/avg.c:509-516) of nblocks contiguous blocks. */
+int lavish_satd_batch(const int32_t *coeff, int length, int nblocks, int *out,
+                      void *stream);
+
+/* av1_block_error (bit_depth 0) / av1_highbd_block_error (bit_depth 8/10/12)
+ * (av1/encoder/rdopt.c:635-682) of nblocks contiguous blocks of n words. */
+int lavish_block_error_batch(const int32_t *coeff, const int32_t *dqcoeff,
+                             int n, int nblocks, int bit_depth, int64_t *err,
+                             int64_t *ssz, void *stream);
+
 /* ------------------------------------------------------------------------ */
 /* Per-call RTCD shims (host pointers)                                      */
 /* ------------------------------------------------------------------------ */
@@ -191,6 +259,150 @@ void av1_highbd_quantize_fp_hip(const int32_t *coeff_ptr, intptr_t count,
                                 const int16_t *dequant_ptr, uint16_t *eob_ptr,
                                 const int16_t *scan, const int16_t *iscan,
                                 int log_scale);
+
+/* ---- pixel shims ---------------------------------------------------------
+ * @encoder_block_sizes of aom_dsp/aom_dsp_rtcd_defs.pl:42-58. */
+#define LAVISH_ENCODER_BLOCK_SIZES(X)                                     \
+  X(128, 128) X(128, 64) X(64, 128) X(64, 64) X(64, 32) X(32, 64)         \
+  X(32, 32) X(32, 16) X(16, 32) X(16, 16) X(16, 8) X(8, 16) X(8, 8)       \
+  X(8, 4) X(4, 8) X(4, 4) X(4, 16) X(16, 4) X(8, 32) X(32, 8) X(16, 64)   \
+  X(64, 16)
+
+/* aom_dsp_rtcd_defs.pl:764-766,1003-1006 (lowbd) and :882-884,1139-1141
+ * (highbd) */
+#define LAVISH_SAD_PROTOS(w, h)                                               \
+  unsigned int aom_sad##w##x##h##_hip(const uint8_t *src_ptr, int src_stride, \
+                                      const uint8_t *ref_ptr, int ref_stride); \
+  unsigned int aom_sad_skip_##w##x##h##_hip(const uint8_t *src_ptr,           \
+                                            int src_stride,                   \
+                                            const uint8_t *ref_ptr,           \
+                                            int ref_stride);                  \
+  unsigned int aom_sad##w##x##h##_avg_hip(                                    \
+      const uint8_t *src_ptr, int src_stride, const uint8_t *ref_ptr,         \
+      int ref_stride, const uint8_t *second_pred);                            \
+  void aom_sad##w##x##h##x4d_hip(const uint8_t *src_ptr, int src_stride,      \
+                                 const uint8_t *const ref_ptr[4],             \
+                                 int ref_stride, uint32_t sad_array[4]);      \
+  void aom_sad##w##x##h##x3d_hip(const uint8_t *src_ptr, int src_stride,      \
+                                 const uint8_t *const ref_ptr[4],             \
+                                 int ref_stride, uint32_t sad_array[4]);      \
+  void aom_sad##w##x##h##x4d_avg_hip(                                         \
+      const uint8_t *src_ptr, int src_stride,                                 \
+      const uint8_t *const ref_ptr[4], int ref_stride,                        \
+      const uint8_t *second_pred, uint32_t sad_array[4]);                     \
+  void aom_sad_skip_##w##x##h##x4d_hip(const uint8_t *src_ptr,                \
+                                       int src_stride,                        \
+                                       const uint8_t *const ref_ptr[4],       \
+                                       int ref_stride, uint32_t sad_array[4]); \
+  unsigned int aom_highbd_sad##w##x##h##_hip(                                 \
+      const uint8_t *src_ptr, int src_stride, const uint8_t *ref_ptr,         \
+      int ref_stride);                                                        \
+  unsigned int aom_highbd_sad_skip_##w##x##h##_hip(                           \
+      const uint8_t *src_ptr, int src_stride, const uint8_t *ref_ptr,         \
+      int ref_stride);                                                        \
+  unsigned int aom_highbd_sad##w##x##h##_avg_hip(                             \
+      const uint8_t *src_ptr, int src_stride, const uint8_t *ref_ptr,         \
+      int ref_stride, const uint8_t *second_pred);                            \
+  void aom_highbd_sad##w##x##h##x4d_hip(const uint8_t *src_ptr,               \
+                                        int src_stride,                       \
+                                        const uint8_t *const ref_ptr[],       \
+                                        int ref_stride, uint32_t *sad_array); \
+  void aom_highbd_sad##w##x##h##x3d_hip(const uint8_t *src_ptr,               \
+                                        int src_stride,                       \
+                                        const uint8_t *const ref_ptr[],       \
+                                        int ref_stride, uint32_t *sad_array); \
+  void aom_highbd_sad_skip_##w##x##h##x4d_hip(                                \
+      const uint8_t *src_ptr, int src_stride,                                 \
+      const uint8_t *const ref_ptr[], int ref_stride, uint32_t *sad_array);
+
+/* aom_dsp_rtcd_defs.pl:1363-1365 (lowbd) and :1476-1478 (highbd 8/10/12) */
+#define LAVISH_VAR_PROTOS_BD(pre, w, h)                                       \
+  unsigned int pre##variance##w##x##h##_hip(const uint8_t *src_ptr,           \
+                                            int source_stride,                \
+                                            const uint8_t *ref_ptr,           \
+                                            int ref_stride, uint32_t *sse);   \
+  uint32_t pre##sub_pixel_variance##w##x##h##_hip(                            \
+      const uint8_t *src_ptr, int source_stride, int xoffset, int yoffset,    \
+      const uint8_t *ref_ptr, int ref_stride, uint32_t *sse);                 \
+  uint32_t pre##sub_pixel_avg_variance##w##x##h##_hip(                        \
+      const uint8_t *src_ptr, int source_stride, int xoffset, int yoffset,    \
+      const uint8_t *ref_ptr, int ref_stride, uint32_t *sse,                  \
+      const uint8_t *second_pred);
+#define LAVISH_VAR_PROTOS(w, h)                  \
+  LAVISH_VAR_PROTOS_BD(aom_, w, h)               \
+  LAVISH_VAR_PROTOS_BD(aom_highbd_8_, w, h)      \
+  LAVISH_VAR_PROTOS_BD(aom_highbd_10_, w, h)     \
+  LAVISH_VAR_PROTOS_BD(aom_highbd_12_, w, h)
+
+LAVISH_ENCODER_BLOCK_SIZES(LAVISH_SAD_PROTOS)
+LAVISH_ENCODER_BLOCK_SIZES(LAVISH_VAR_PROTOS)
+
+/* aom_dsp_rtcd_defs.pl:1303-1318,1326-1333 */
+#define LAVISH_MSE_PROTOS(pre)                                                 \
+  void pre##get16x16var_hip(const uint8_t *src_ptr, int source_stride,        \
+                            const uint8_t *ref_ptr, int ref_stride,           \
+                            unsigned int *sse, int *sum);                     \
+  void pre##get8x8var_hip(const uint8_t *src_ptr, int source_stride,          \
+                          const uint8_t *ref_ptr, int ref_stride,             \
+                          unsigned int *sse, int *sum);                       \
+  unsigned int pre##mse16x16_hip(const uint8_t *src_ptr, int source_stride,   \
+                                 const uint8_t *ref_ptr, int recon_stride,    \
+                                 unsigned int *sse);                          \
+  unsigned int pre##mse16x8_hip(const uint8_t *src_ptr, int source_stride,    \
+                                const uint8_t *ref_ptr, int recon_stride,     \
+                                unsigned int *sse);                           \
+  unsigned int pre##mse8x16_hip(const uint8_t *src_ptr, int source_stride,    \
+                                const uint8_t *ref_ptr, int recon_stride,     \
+                                unsigned int *sse);                           \
+  unsigned int pre##mse8x8_hip(const uint8_t *src_ptr, int source_stride,     \
+                               const uint8_t *ref_ptr, int recon_stride,      \
+                               unsigned int *sse);
+LAVISH_MSE_PROTOS(aom_)
+LAVISH_MSE_PROTOS(aom_highbd_8_)
+LAVISH_MSE_PROTOS(aom_highbd_10_)
+LAVISH_MSE_PROTOS(aom_highbd_12_)
+
+/* aom_dsp_rtcd_defs.pl:725-746 */
+void aom_subtract_block_hip(int rows, int cols, int16_t *diff_ptr,
+                            ptrdiff_t diff_stride, const uint8_t *src_ptr,
+                            ptrdiff_t src_stride, const uint8_t *pred_ptr,
+                            ptrdiff_t pred_stride);
+void aom_highbd_subtract_block_hip(int rows, int cols, int16_t *diff_ptr,
+                                   ptrdiff_t diff_stride,
+                                   const uint8_t *src_ptr,
+                                   ptrdiff_t src_stride,
+                                   const uint8_t *pred_ptr,
+                                   ptrdiff_t pred_stride);
+int64_t aom_sse_hip(const uint8_t *a, int a_stride, const uint8_t *b,
+                    int b_stride, int width, int height);
+int64_t aom_highbd_sse_hip(const uint8_t *a8, int a_stride, const uint8_t *b8,
+                           int b_stride, int width, int height);
+uint64_t aom_sum_squares_2d_i16_hip(const int16_t *src, int stride, int width,
+                                    int height);
+
+/* aom_dsp_rtcd_defs.pl:1244-1278 */
+void aom_hadamard_4x4_hip(const int16_t *src_diff, ptrdiff_t src_stride,
+                          int32_t *coeff);
+void aom_hadamard_8x8_hip(const int16_t *src_diff, ptrdiff_t src_stride,
+                          int32_t *coeff);
+void aom_hadamard_16x16_hip(const int16_t *src_diff, ptrdiff_t src_stride,
+                            int32_t *coeff);
+void aom_hadamard_32x32_hip(const int16_t *src_diff, ptrdiff_t src_stride,
+                            int32_t *coeff);
+void aom_highbd_hadamard_8x8_hip(const int16_t *src_diff,
+                                 ptrdiff_t src_stride, int32_t *coeff);
+void aom_highbd_hadamard_16x16_hip(const int16_t *src_diff,
+                                   ptrdiff_t src_stride, int32_t *coeff);
+void aom_highbd_hadamard_32x32_hip(const int16_t *src_diff,
+                                   ptrdiff_t src_stride, int32_t *coeff);
+int aom_satd_hip(const int32_t *coeff, int length);
+
+/* av1/common/av1_rtcd_defs.pl:328,423 */
+int64_t av1_block_error_hip(const int32_t *coeff, const int32_t *dqcoeff,
+                            intptr_t block_size, int64_t *ssz);
+int64_t av1_highbd_block_error_hip(const int32_t *coeff,
+                                   const int32_t *dqcoeff,
+                                   intptr_t block_size, int64_t *ssz, int bd);
 
 #ifdef __cplusplus
 }

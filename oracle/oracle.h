@@ -128,6 +128,22 @@ unsigned int orc_sub_pixel_variance(const uint8_t *a, int a_stride,
                                     int xoffset, int yoffset, const uint8_t *b,
                                     int b_stride, int w, int h,
                                     unsigned int *sse);
+unsigned int orc_sub_pixel_avg_variance(const uint8_t *a, int a_stride,
+                                        int xoffset, int yoffset,
+                                        const uint8_t *b, int b_stride, int w,
+                                        int h, unsigned int *sse,
+                                        const uint8_t *second_pred);
+unsigned int orc_highbd_sub_pixel_variance(const uint16_t *a, int a_stride,
+                                           int xoffset, int yoffset,
+                                           const uint16_t *b, int b_stride,
+                                           int w, int h, int bd,
+                                           unsigned int *sse,
+                                           const uint16_t *second_pred);
+unsigned int orc_highbd_sad_avg(const uint16_t *src, int src_stride,
+                                const uint16_t *ref, int ref_stride, int w,
+                                int h, const uint16_t *second_pred);
+void orc_highbd_hadamard(int n, const int16_t *src_diff, ptrdiff_t src_stride,
+                         int32_t *coeff);
 unsigned int orc_mse(const uint8_t *a, int a_stride, const uint8_t *b,
                      int b_stride, int w, int h, unsigned int *sse);
 int64_t orc_sse(const uint8_t *a, int a_stride, const uint8_t *b, int b_stride,

@@ -106,6 +106,32 @@ unsigned int orc_sub_pixel_variance(const uint8_t *a, int as, int xo, int yo,
   return r;
 }
 
+/* aom_sub_pixel_avg_variance{W}x{H}_c (variance.c:132-145 + comp avg
+ * aom_comp_avg_pred_c :285-298): filter as above, average with second_pred
+ * (w x h, stride w), then variance against b. */
+unsigned int orc_sub_pixel_avg_variance(const uint8_t *a, int as, int xo,
+                                        int yo, const uint8_t *b, int bs,
+                                        int w, int h, unsigned int *sse,
+                                        const uint8_t *second_pred) {
+  uint16_t *f = (uint16_t *)malloc(sizeof(uint16_t) * (h + 1) * w);
+  uint8_t *t = (uint8_t *)malloc((size_t)h * w);
+  for (int i = 0; i < h + 1; ++i)
+    for (int j = 0; j < w; ++j) {
+      const int v = a[i * as + j] * kBil[xo][0] + a[i * as + j + 1] * kBil[xo][1];
+      f[i * w + j] = (uint16_t)((v + 64) >> 7);
+    }
+  for (int i = 0; i < h; ++i)
+    for (int j = 0; j < w; ++j) {
+      const int v = f[i * w + j] * kBil[yo][0] + f[(i + 1) * w + j] * kBil[yo][1];
+      const uint8_t p = (uint8_t)((v + 64) >> 7);
+      t[i * w + j] = (uint8_t)((second_pred[i * w + j] + p + 1) >> 1);
+    }
+  const unsigned int r = orc_variance(t, w, b, bs, w, h, sse);
+  free(f);
+  free(t);
+  return r;
+}
+
 unsigned int orc_highbd_variance(const uint16_t *a, int as, const uint16_t *b,
                                  int bs, int w, int h, int bd,
                                  unsigned int *sse) {
@@ -311,4 +337,115 @@ int64_t orc_highbd_block_error(const int32_t *coeff, const int32_t *dqcoeff,
   }
   *ssz = (sq + rnd) >> shift;
   return (err + rnd) >> shift;
+}
+
+/* aom_highbd_{8,10,12}_sub_pixel_variance / _avg_variance (variance.c:454-670):
+ * u16 first pass (H+1 rows), u16 second pass, optional comp avg with
+ * second_pred (nullable), then the bd variance against b. */
+unsigned int orc_highbd_sub_pixel_variance(const uint16_t *a, int as, int xo,
+                                           int yo, const uint16_t *b, int bs,
+                                           int w, int h, int bd,
+                                           unsigned int *sse,
+                                           const uint16_t *second_pred) {
+  uint16_t *f = (uint16_t *)malloc(sizeof(uint16_t) * (h + 1) * w);
+  uint16_t *t = (uint16_t *)malloc(sizeof(uint16_t) * h * w);
+  for (int i = 0; i < h + 1; ++i)
+    for (int j = 0; j < w; ++j) {
+      const int v = a[i * as + j] * kBil[xo][0] + a[i * as + j + 1] * kBil[xo][1];
+      f[i * w + j] = (uint16_t)((v + 64) >> 7);
+    }
+  for (int i = 0; i < h; ++i)
+    for (int j = 0; j < w; ++j) {
+      const int v = f[i * w + j] * kBil[yo][0] + f[(i + 1) * w + j] * kBil[yo][1];
+      uint16_t p = (uint16_t)((v + 64) >> 7);
+      if (second_pred) p = (uint16_t)((second_pred[i * w + j] + p + 1) >> 1);
+      t[i * w + j] = p;
+    }
+  const unsigned int r = orc_highbd_variance(t, w, b, bs, w, h, bd, sse);
+  free(f);
+  free(t);
+  return r;
+}
+
+/* aom_highbd_sad{W}x{H}_avg_c (sad.c:289-296, aom_highbd_comp_avg_pred) */
+unsigned int orc_highbd_sad_avg(const uint16_t *src, int ss, const uint16_t *ref,
+                                int rs, int w, int h,
+                                const uint16_t *second_pred) {
+  unsigned int s = 0;
+  for (int i = 0; i < h; ++i)
+    for (int j = 0; j < w; ++j) {
+      const int c = (second_pred[i * w + j] + ref[i * rs + j] + 1) >> 1;
+      s += (unsigned)abs(src[i * ss + j] - c);
+    }
+  return s;
+}
+
+/* aom_highbd_hadamard_{8x8,16x16,32x32}_c (avg.c:350-507): int16 first
+ * pass, int32 second pass, no output transpose and no 16x16 group swap. */
+static void hbd_had8(const int16_t *src, ptrdiff_t st, int32_t *coeff) {
+  int16_t b1[64];
+  for (int i = 0; i < 8; ++i) had_col8(src + i, st, b1 + 8 * i);
+  for (int i = 0; i < 8; ++i) {
+    const int16_t *s = b1 + i;
+    int32_t b[8], c[8];
+    for (int k = 0; k < 4; ++k) {
+      b[2 * k] = s[2 * k * 8] + s[(2 * k + 1) * 8];
+      b[2 * k + 1] = s[2 * k * 8] - s[(2 * k + 1) * 8];
+    }
+    c[0] = b[0] + b[2];
+    c[1] = b[1] + b[3];
+    c[2] = b[0] - b[2];
+    c[3] = b[1] - b[3];
+    c[4] = b[4] + b[6];
+    c[5] = b[5] + b[7];
+    c[6] = b[4] - b[6];
+    c[7] = b[5] - b[7];
+    int32_t *o = coeff + 8 * i;
+    o[0] = c[0] + c[4];
+    o[7] = c[1] + c[5];
+    o[3] = c[2] + c[6];
+    o[4] = c[3] + c[7];
+    o[2] = c[0] - c[4];
+    o[6] = c[1] - c[5];
+    o[1] = c[2] - c[6];
+    o[5] = c[3] - c[7];
+  }
+}
+
+static void hbd_had16(const int16_t *src, ptrdiff_t st, int32_t *coeff) {
+  for (int idx = 0; idx < 4; ++idx)
+    hbd_had8(src + (idx >> 1) * 8 * st + (idx & 1) * 8, st, coeff + idx * 64);
+  for (int i = 0; i < 64; ++i) {
+    const int32_t a0 = coeff[i], a1 = coeff[64 + i], a2 = coeff[128 + i],
+                  a3 = coeff[192 + i];
+    const int32_t b0 = (a0 + a1) >> 1, b1 = (a0 - a1) >> 1;
+    const int32_t b2 = (a2 + a3) >> 1, b3 = (a2 - a3) >> 1;
+    coeff[i] = b0 + b2;
+    coeff[64 + i] = b1 + b3;
+    coeff[128 + i] = b0 - b2;
+    coeff[192 + i] = b1 - b3;
+  }
+}
+
+void orc_highbd_hadamard(int n, const int16_t *src, ptrdiff_t st,
+                         int32_t *coeff) {
+  if (n == 8) {
+    hbd_had8(src, st, coeff);
+  } else if (n == 16) {
+    hbd_had16(src, st, coeff);
+  } else {
+    for (int idx = 0; idx < 4; ++idx)
+      hbd_had16(src + (idx >> 1) * 16 * st + (idx & 1) * 16, st,
+                coeff + idx * 256);
+    for (int i = 0; i < 256; ++i) {
+      const int32_t a0 = coeff[i], a1 = coeff[256 + i], a2 = coeff[512 + i],
+                    a3 = coeff[768 + i];
+      const int32_t b0 = (a0 + a1) >> 2, b1 = (a0 - a1) >> 2;
+      const int32_t b2 = (a2 + a3) >> 2, b3 = (a2 - a3) >> 2;
+      coeff[i] = b0 + b2;
+      coeff[256 + i] = b1 + b3;
+      coeff[512 + i] = b0 - b2;
+      coeff[768 + i] = b1 - b3;
+    }
+  }
 }

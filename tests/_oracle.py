@@ -75,6 +75,14 @@ def _declare(L):
     L.orc_highbd_variance.argtypes = [vp, i32, vp, i32, i32, i32, i32, vp]
     L.orc_sub_pixel_variance.restype = ctypes.c_uint
     L.orc_sub_pixel_variance.argtypes = [vp, i32, i32, i32, vp, i32, i32, i32, vp]
+    L.orc_sub_pixel_avg_variance.restype = ctypes.c_uint
+    L.orc_sub_pixel_avg_variance.argtypes = [vp, i32, i32, i32, vp, i32, i32, i32, vp, vp]
+    L.orc_highbd_sub_pixel_variance.restype = ctypes.c_uint
+    L.orc_highbd_sub_pixel_variance.argtypes = [vp, i32, i32, i32, vp, i32, i32, i32, i32,
+                                                vp, vp]
+    L.orc_highbd_sad_avg.restype = ctypes.c_uint
+    L.orc_highbd_sad_avg.argtypes = [vp, i32, vp, i32, i32, i32, vp]
+    L.orc_highbd_hadamard.argtypes = [i32, vp, ctypes.c_ssize_t, vp]
     L.orc_sse.restype = i64
     L.orc_sse.argtypes = [vp, i32, vp, i32, i32, i32]
     L.orc_highbd_sse.restype = i64
@@ -233,3 +241,115 @@ class ACMRandom:
 
     def pseudo_uniform(self, r):
         return self._gen(r)
+
+    def rand9signed(self):
+        return self._gen(512) - 256
+
+    def rand15signed(self):
+        return ((self._gen(1 << 31) >> 16) & 0x7FFF) - (1 << 14)
+
+    def rand8extremes(self):
+        r = self.rand8()
+        return (r << 4) & 0xFF if r < 128 else r >> 4
+
+
+# ---------------------------------------------------------- pixel kernels --
+def sad(a, a_stride, b, b_stride, w, h, highbd=False, skip=False, second_pred=None):
+    L = lib()
+    if second_pred is not None:
+        f = L.orc_highbd_sad_avg if highbd else L.orc_sad_avg
+        return f(P(a), a_stride, P(b), b_stride, w, h, P(second_pred))
+    if highbd:
+        if skip:
+            return 2 * L.orc_highbd_sad(P(a), 2 * a_stride, P(b), 2 * b_stride, w, h // 2)
+        return L.orc_highbd_sad(P(a), a_stride, P(b), b_stride, w, h)
+    f = L.orc_sad_skip if skip else L.orc_sad
+    return f(P(a), a_stride, P(b), b_stride, w, h)
+
+
+def variance(a, a_stride, b, b_stride, w, h, bd=8, highbd=False):
+    L = lib()
+    sse = ctypes.c_uint(0)
+    if highbd:
+        v = L.orc_highbd_variance(P(a), a_stride, P(b), b_stride, w, h, bd, ctypes.byref(sse))
+    else:
+        v = L.orc_variance(P(a), a_stride, P(b), b_stride, w, h, ctypes.byref(sse))
+    return v, sse.value
+
+
+def mse(a, a_stride, b, b_stride, w, h, bd=8, highbd=False):
+    if highbd:
+        v, s = variance(a, a_stride, b, b_stride, w, h, bd, True)
+        return s, s
+    sse = ctypes.c_uint(0)
+    v = lib().orc_mse(P(a), a_stride, P(b), b_stride, w, h, ctypes.byref(sse))
+    return v, sse.value
+
+
+def get_var(a, a_stride, b, b_stride, w, h, bd=8, highbd=False):
+    """(sse, sum) as aom[_highbd_bd]_get{n}x{n}var (variance.c:187-238)."""
+    if highbd:
+        # sum = the rounded sum of highbd_{bd}_variance: recover it from var/sse
+        a64 = a[:h, :w].astype(np.int64)
+        b64 = b[:h, :w].astype(np.int64)
+        d = a64 - b64
+        tsum = int(d.sum())
+        _, sse = variance(a, a_stride, b, b_stride, w, h, bd, True)
+        if bd == 8:
+            return sse, tsum
+        sh = 2 if bd == 10 else 4
+        return sse, (tsum + ((1 << sh) >> 1)) >> sh
+    _, sse = variance(a, a_stride, b, b_stride, w, h)
+    d = a[:h, :w].astype(np.int64) - b[:h, :w].astype(np.int64)
+    return sse, int(d.sum())
+
+
+def sub_pixel_variance(a, a_stride, xo, yo, b, b_stride, w, h, bd=8, highbd=False,
+                       second_pred=None):
+    L = lib()
+    sse = ctypes.c_uint(0)
+    if highbd:
+        v = L.orc_highbd_sub_pixel_variance(P(a), a_stride, xo, yo, P(b), b_stride, w, h, bd,
+                                            ctypes.byref(sse),
+                                            P(second_pred) if second_pred is not None else None)
+    elif second_pred is not None:
+        v = L.orc_sub_pixel_avg_variance(P(a), a_stride, xo, yo, P(b), b_stride, w, h,
+                                         ctypes.byref(sse), P(second_pred))
+    else:
+        v = L.orc_sub_pixel_variance(P(a), a_stride, xo, yo, P(b), b_stride, w, h,
+                                     ctypes.byref(sse))
+    return v, sse.value
+
+
+def sse(a, a_stride, b, b_stride, w, h, highbd=False):
+    f = lib().orc_highbd_sse if highbd else lib().orc_sse
+    return f(P(a), a_stride, P(b), b_stride, w, h)
+
+
+def subtract_block(rows, cols, diff, ds, src, ss, pred, ps, highbd=False):
+    f = lib().orc_highbd_subtract_block if highbd else lib().orc_subtract_block
+    f(rows, cols, P(diff), ds, P(src), ss, P(pred), ps)
+
+
+def sum_squares_2d_i16(src, stride, w, h):
+    return lib().orc_sum_squares_2d_i16(P(src), stride, w, h)
+
+
+def hadamard(n, src, stride, highbd=False):
+    out = np.zeros(n * n, np.int32)
+    f = lib().orc_highbd_hadamard if highbd else lib().orc_hadamard
+    f(n, P(src), stride, P(out))
+    return out
+
+
+def satd(coeff, length):
+    return lib().orc_satd(P(coeff), length)
+
+
+def block_error(coeff, dqcoeff, n, bd=None):
+    ssz = ctypes.c_int64(0)
+    if bd is None:
+        e = lib().orc_block_error(P(coeff), P(dqcoeff), n, ctypes.byref(ssz))
+    else:
+        e = lib().orc_highbd_block_error(P(coeff), P(dqcoeff), n, ctypes.byref(ssz), bd)
+    return e, ssz.value
