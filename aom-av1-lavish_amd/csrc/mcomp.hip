@@ -1,0 +1,363 @@
+// mcomp.hip -- batched DIAMOND full-pixel motion search for gfx950 (C3).
+//
+// Reference (one block, one reference frame, one CPU thread):
+//   av1_full_pixel_search (av1/encoder/mcomp.c:1755-1895, method DIAMOND)
+//   -> full_pixel_diamond (:1479-1526) -> diamond_search_sad (:1318-1477)
+//   sites of av1_init_dsmotion_compensation (:369-404, level 0: radius
+//   1024 >> k, 8 sites per step), mvsad_err_cost / mv_err_cost (:257-360),
+//   sdf / sdx4df = aom_sad{W}x{H}[x4d] or the _skip variants when
+//   use_downsampled_sad (:132-142) with the quality recheck (:1840-1867),
+//   vf = aom_variance{W}x{H}.
+//
+// Here one wave64 owns one (block, reference) job and runs that sequential
+// walk.  A step's 8 candidate sites are evaluated at once: lane group
+// g = lane / 8 takes site g + 1, its 8 lanes split the block's rows, each
+// lane accumulates v_sad_u8 over 4-byte words (unaligned rows are assembled
+// from aligned dwords with v_alignbyte), and a 3-level xor shuffle leaves the
+// group's SAD in every lane.  The 8 SADs are then read into scalar registers
+// and the reference's sequential "strictly better" scan in site order runs
+// on the SALU, so the walk (and every tie) is exactly the reference's.  The
+// source block stays in VGPRs for the whole search; reference pixels come
+// from L2 / MALL (a 1080p padded reference is ~2.5 MB).
+#include "lavish_internal.h"
+
+namespace lavish {
+namespace {
+
+constexpr int kMaxSteps = 11;  // MAX_MVSEARCH_STEPS (mcomp_structs.h:19)
+
+__device__ __forceinline__ uint32_t sad4(uint32_t a, uint32_t b, uint32_t acc) {
+  return __builtin_amdgcn_sad_u8(a, b, acc);
+}
+
+// DW consecutive 4-byte words starting at an arbitrary byte address, from
+// aligned dword loads (reads at most 3 bytes past the row only when the
+// address is unaligned).
+template <int DW>
+__device__ __forceinline__ void load_row(const uint8_t* p, uint32_t (&out)[DW]) {
+  const uintptr_t a = (uintptr_t)p;
+  const uint32_t* q = (const uint32_t*)(a & ~(uintptr_t)3);
+  const uint32_t sh = (uint32_t)(a & 3);
+  uint32_t prev = q[0];
+#pragma unroll
+  for (int i = 0; i < DW; ++i) {
+    const uint32_t nxt = (i + 1 < DW) ? q[i + 1] : (sh ? q[DW] : 0u);
+    out[i] = __builtin_amdgcn_alignbyte(nxt, prev, sh);
+    prev = nxt;
+  }
+}
+
+__device__ __forceinline__ uint32_t rdlane(uint32_t v, int l) {
+  return (uint32_t)__builtin_amdgcn_readlane((int)v, l);
+}
+
+struct Job {
+  int64_t src_off, ref_off;
+  int16_t start_row, start_col, ref_mv_row, ref_mv_col;
+  int16_t col_min, col_max, row_min, row_max;
+};
+static_assert(sizeof(Job) == sizeof(LavishDiamondJob), "job layout");
+
+struct Ctx {
+  const uint8_t* src;
+  const uint8_t* ref;  // block origin at mv (0,0)
+  int ss, rs;
+  int col_min, col_max, row_min, row_max;
+  int ref_mv_row, ref_mv_col, full_ref_row, full_ref_col;
+  int cost_type;
+};
+
+__device__ __forceinline__ int sad_lambda(int t) { return t == 1 ? 32 : t == 2 ? 15 : t == 3 ? 8 : 0; }
+__device__ __forceinline__ int sse_lambda(int t) { return t == 1 ? 2 : t == 2 ? 0 : t == 3 ? 1 : 0; }
+
+// mvsad_err_cost (mcomp.c:329-350) for the L1 types; 0 for MV_COST_NONE
+__device__ __forceinline__ uint32_t mvsad_cost(const Ctx& c, int row, int col) {
+  const int dr = (row - c.full_ref_row) * 8, dc = (col - c.full_ref_col) * 8;
+  return (uint32_t)((sad_lambda(c.cost_type) * (abs(dr) + abs(dc))) >> 3);
+}
+// mv_err_cost (mcomp.c:287-314) for the L1 types
+__device__ __forceinline__ int mv_cost(const Ctx& c, int row, int col) {
+  const int dr = row * 8 - c.ref_mv_row, dc = col * 8 - c.ref_mv_col;
+  return (sse_lambda(c.cost_type) * (abs(dr) + abs(dc))) >> 3;
+}
+
+// Row split of a block inside one 8-lane group.
+template <int W, int H, bool SKIP>
+struct Geo {
+  static constexpr int RH = SKIP ? H / 2 : H;        // rows the SAD reads
+  static constexpr int RPL = RH >= 8 ? RH / 8 : 1;   // rows per lane
+  static constexpr int DW = W / 4;                   // words per row
+  static constexpr int YS = SKIP ? 2 : 1;            // row step
+};
+
+template <int W, int H, bool SKIP>
+struct Search {
+  using G = Geo<W, H, SKIP>;
+  // source rows live in VGPRs up to 32 words per lane (32x32 and smaller);
+  // larger blocks re-read them through L2 with the candidate rows
+  static constexpr bool kCache = G::RPL * G::DW <= 32;
+  uint32_t s[kCache ? G::RPL : 1][kCache ? G::DW : 1];
+  int l;  // lane within the group
+
+  __device__ __forceinline__ void load_src(const Ctx& c, int lane) {
+    l = lane & 7;
+    if constexpr (kCache) {
+#pragma unroll
+      for (int k = 0; k < G::RPL; ++k) {
+        const int row = l + 8 * k;
+        if (row < G::RH) load_row<G::DW>(c.src + (int64_t)row * G::YS * c.ss, s[k]);
+      }
+    }
+  }
+
+  // group-partial SAD of the block at ref + off, reduced over the 8 lanes
+  __device__ __forceinline__ uint32_t group_sad(const Ctx& c, int64_t off, bool valid) const {
+    uint32_t acc = 0;
+    if (valid) {
+      if constexpr (kCache) {
+#pragma unroll
+        for (int k = 0; k < G::RPL; ++k) {
+          const int row = l + 8 * k;
+          if (row < G::RH) {
+            uint32_t r[G::DW];
+            load_row<G::DW>(c.ref + off + (int64_t)row * G::YS * c.rs, r);
+#pragma unroll
+            for (int i = 0; i < G::DW; ++i) acc = sad4(s[k][i], r[i], acc);
+          }
+        }
+      } else {
+        // rows in 32-byte chunks, not unrolled (keeps code and VGPRs small)
+        constexpr int CH = G::DW < 8 ? G::DW : 8;
+#pragma unroll 1
+        for (int k = 0; k < G::RPL; ++k) {
+          const int row = l + 8 * k;
+          const uint8_t* rp = c.ref + off + (int64_t)row * G::YS * c.rs;
+          const uint8_t* sp = c.src + (int64_t)row * G::YS * c.ss;
+#pragma unroll 1
+          for (int x = 0; x < G::DW; x += CH) {
+            uint32_t r[CH], q[CH];
+            load_row<CH>(rp + 4 * x, r);
+            load_row<CH>(sp + 4 * x, q);
+#pragma unroll
+            for (int i = 0; i < CH; ++i) acc = sad4(q[i], r[i], acc);
+          }
+        }
+      }
+    }
+    acc += __shfl_xor(acc, 1);
+    acc += __shfl_xor(acc, 2);
+    acc += __shfl_xor(acc, 4);
+    return SKIP ? 2 * acc : acc;
+  }
+
+  // diamond_search_sad (no second_pred): returns bestsad
+  __device__ uint32_t diamond(const Ctx& c, int lane, int srow, int scol, int search_step,
+                              int& brow, int& bcol, int& num00, int& steps) const {
+    const int g = lane >> 3;
+    // site g + 1 of av1_init_dsmotion_compensation (row, col) in units of radius
+    const int sdr = (g == 0 || g == 4 || g == 6) ? -1 : (g == 1 || g == 5 || g == 7) ? 1 : 0;
+    const int sdc = (g == 2 || g == 4 || g == 7) ? -1 : (g == 3 || g == 5 || g == 6) ? 1 : 0;
+    srow = min(max(srow, c.row_min), c.row_max);
+    scol = min(max(scol, c.col_min), c.col_max);
+    int row = srow, col = scol, off_center = 0, center = 0;
+    uint32_t best = mvsad_cost(c, row, col) +
+                    rdlane(group_sad(c, (int64_t)row * c.rs + col, true), 0);
+    const int tot = kMaxSteps - search_step;
+    for (int step = tot - 1; step >= 0; --step) {
+      const int rad = 1 << step;
+      const bool all_in = row - rad >= c.row_min && row + rad <= c.row_max &&
+                          col - rad >= c.col_min && col + rad <= c.col_max;
+      const int r = row + sdr * rad, cc = col + sdc * rad;
+      const bool valid = all_in || (cc >= c.col_min && cc <= c.col_max && r >= c.row_min &&
+                                    r <= c.row_max);
+      const uint32_t mine = group_sad(c, (int64_t)r * c.rs + cc, valid);
+      const uint64_t vmask = __ballot(valid);
+      int best_site = 0;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        if (!((vmask >> (8 * i)) & 1)) continue;
+        const uint32_t sd = rdlane(mine, 8 * i);
+        if (sd < best) {
+          const int ir = (i == 0 || i == 4 || i == 6) ? -1 : (i == 1 || i == 5 || i == 7) ? 1 : 0;
+          const int ic = (i == 2 || i == 4 || i == 7) ? -1 : (i == 3 || i == 5 || i == 6) ? 1 : 0;
+          const uint32_t t = sd + mvsad_cost(c, row + ir * rad, col + ic * rad);
+          if (t < best) {
+            best = t;
+            best_site = i + 1;
+          }
+        }
+      }
+      ++steps;
+      if (best_site) {
+        const int i = best_site - 1;
+        row += ((i == 0 || i == 4 || i == 6) ? -1 : (i == 1 || i == 5 || i == 7) ? 1 : 0) * rad;
+        col += ((i == 2 || i == 4 || i == 7) ? -1 : (i == 3 || i == 5 || i == 6) ? 1 : 0) * rad;
+        off_center = 1;
+      }
+      if (!off_center) ++center;
+    }
+    brow = row;
+    bcol = col;
+    num00 = center;
+    return best;
+  }
+};
+
+// vf (aom_variance{W}x{H}) + mv_err_cost at a full-pel mv: the whole wave
+// walks the W*H pixels one word per lane.
+template <int W, int H>
+__device__ int var_cost(const Ctx& c, int lane, int row, int col) {
+  constexpr int DW = W / 4;
+  int sum = 0;
+  uint32_t sse = 0;
+  const uint8_t* rb = c.ref + (int64_t)row * c.rs + col;
+  for (int i = lane; i < H * DW; i += 64) {
+    const int y = i / DW, x = i - y * DW;
+    uint32_t a[1], b[1];
+    load_row<1>(c.src + (int64_t)y * c.ss + 4 * x, a);
+    load_row<1>(rb + (int64_t)y * c.rs + 4 * x, b);
+    sum += (int)sad4(a[0], 0, 0) - (int)sad4(b[0], 0, 0);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int d = (int)((a[0] >> (8 * j)) & 255) - (int)((b[0] >> (8 * j)) & 255);
+      sse += (uint32_t)(d * d);
+    }
+  }
+#pragma unroll
+  for (int m = 1; m < 64; m <<= 1) {
+    sum += __shfl_xor(sum, m);
+    sse += __shfl_xor(sse, m);
+  }
+  sum = __builtin_amdgcn_readfirstlane(sum);
+  sse = (uint32_t)__builtin_amdgcn_readfirstlane((int)sse);
+  const uint32_t var = sse - (uint32_t)(((int64_t)sum * sum) / (W * H));
+  return (int)var + mv_cost(c, row, col);
+}
+
+// full_pixel_diamond (mcomp.c:1479-1526)
+template <int W, int H, bool SKIP>
+__device__ int full_pixel_diamond(const Ctx& c, int lane, int srow, int scol, int step_param,
+                                  int& brow, int& bcol, int& steps, int& searches) {
+  Search<W, H, SKIP> S;
+  S.load_src(c, lane);
+  int n, num00 = 0;
+  S.diamond(c, lane, srow, scol, step_param, brow, bcol, n, steps);
+  ++searches;
+  int bestsme = var_cost<W, H>(c, lane, brow, bcol);
+  const int further = kMaxSteps - 1 - step_param;
+  while (n < further) {
+    ++n;
+    int tr, tc;
+    S.diamond(c, lane, srow, scol, step_param + n, tr, tc, num00, steps);
+    ++searches;
+    const int sme = var_cost<W, H>(c, lane, tr, tc);
+    if (sme < bestsme) {
+      bestsme = sme;
+      brow = tr;
+      bcol = tc;
+    }
+    if (num00) {
+      n += num00;
+      num00 = 0;
+    }
+  }
+  return bestsme;
+}
+
+__device__ __forceinline__ int rawpel(int x) { return (x + 3 + (x >= 0)) >> 3; }  // mv.h:28
+
+template <int W, int H>
+__global__ __launch_bounds__(256) void diamond_kernel(const uint8_t* __restrict__ src, int ss,
+                                                      const uint8_t* __restrict__ ref, int rs,
+                                                      const Job* __restrict__ jobs, int njobs,
+                                                      int step_param, int cost_type, int skip,
+                                                      LavishDiamondResult* __restrict__ out) {
+  // XCD-aware: consecutive job quads (neighbouring blocks) share an XCD's L2
+  const int nwg = gridDim.x;  // multiple of 8
+  const int wg = (blockIdx.x & 7) * (nwg >> 3) + (blockIdx.x >> 3);
+  const int lane = threadIdx.x & 63;
+  const int j = wg * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  if (j >= njobs) return;
+  const Job jb = jobs[j];
+  Ctx c;
+  c.src = src + jb.src_off;
+  c.ref = ref + jb.ref_off;
+  c.ss = ss;
+  c.rs = rs;
+  c.col_min = jb.col_min;
+  c.col_max = jb.col_max;
+  c.row_min = jb.row_min;
+  c.row_max = jb.row_max;
+  c.ref_mv_row = jb.ref_mv_row;
+  c.ref_mv_col = jb.ref_mv_col;
+  c.full_ref_row = rawpel(jb.ref_mv_row);
+  c.full_ref_col = rawpel(jb.ref_mv_col);
+  c.cost_type = cost_type;
+  int br, bc, steps = 0, searches = 0, sme;
+  // use_downsampled_sad applies to blocks at least 16 high (mcomp.c:132-133)
+  if (skip && H >= 16) {
+    sme = full_pixel_diamond<W, H, true>(c, lane, jb.start_row, jb.start_col, step_param, br, bc,
+                                         steps, searches);
+    // quality check of the row-skipping search (mcomp.c:1840-1867)
+    Search<W, H, false> F;
+    F.load_src(c, lane);
+    const int64_t off = (int64_t)br * rs + bc;
+    const int sad = (int)rdlane(F.group_sad(c, off, true), 0);
+    Search<W, H, true> K;
+    K.load_src(c, lane);
+    const int ssad = (int)rdlane(K.group_sad(c, off, true), 0);
+    const int thresh = (W >> 2) * (H >> 2);
+    if (sad > thresh && abs(ssad - sad) * 10 >= max(sad, 1) * 9)
+      sme = full_pixel_diamond<W, H, false>(c, lane, jb.start_row, jb.start_col, step_param, br,
+                                            bc, steps, searches);
+  } else {
+    sme = full_pixel_diamond<W, H, false>(c, lane, jb.start_row, jb.start_col, step_param, br, bc,
+                                          steps, searches);
+  }
+  if (lane == 0) {
+    LavishDiamondResult r;
+    r.best_row = (int16_t)br;
+    r.best_col = (int16_t)bc;
+    r.bestsme = sme;
+    r.steps = steps;
+    r.searches = searches;
+    out[j] = r;
+  }
+}
+
+template <int W, int H>
+void launch(const uint8_t* src, int ss, const uint8_t* ref, int rs, const LavishDiamondJob* jobs,
+            int njobs, int step_param, int cost_type, int skip, LavishDiamondResult* out,
+            hipStream_t s) {
+  int nwg = (njobs + 3) / 4;
+  nwg = (nwg + 7) & ~7;
+  hipLaunchKernelGGL((diamond_kernel<W, H>), dim3(nwg), dim3(256), 0, s, src, ss, ref, rs,
+                     (const Job*)jobs, njobs, step_param, cost_type, skip, out);
+}
+
+}  // namespace
+}  // namespace lavish
+
+using namespace lavish;
+
+extern "C" int lavish_diamond_search_batch(const uint8_t* src, int src_stride, const uint8_t* ref,
+                                           int ref_stride, int w, int h,
+                                           const LavishDiamondJob* jobs, int njobs,
+                                           int step_param, int mv_cost_type,
+                                           int use_downsampled_sad, LavishDiamondResult* out,
+                                           void* stream) {
+  if (njobs <= 0) return 0;
+  if (step_param < 0 || step_param >= kMaxSteps) return -1;
+  if (mv_cost_type < 1 || mv_cost_type > 4) return -2;  // MV_COST_ENTROPY not supported
+  hipStream_t s = (hipStream_t)stream;
+#define LAVISH_DIA_CASE(W, H)                                                                 \
+  if (w == W && h == H) {                                                                     \
+    launch<W, H>(src, src_stride, ref, ref_stride, jobs, njobs, step_param, mv_cost_type,     \
+                 use_downsampled_sad, out, s);                                                \
+    LAVISH_CHECK(hipGetLastError());                                                          \
+    return 0;                                                                                 \
+  }
+  LAVISH_ENCODER_BLOCK_SIZES(LAVISH_DIA_CASE)
+#undef LAVISH_DIA_CASE
+  return -3;
+}

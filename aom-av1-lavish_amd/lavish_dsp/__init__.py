@@ -233,6 +233,7 @@ def txq_plane(residual, tx_size, type_mask, qp, bit_depth=8, quant_kind=QUANT_FP
     (uint16 values stored in an int16 tensor)."""
     import torch
     assert residual.dtype == torch.int16 and residual.is_cuda
+    assert residual.stride(1) == 1, "residual rows must be contiguous"
     Hh, Ww = residual.shape
     stride = residual.stride(0) if stride is None else stride
     width = Ww if width is None else width
@@ -272,6 +273,7 @@ def txq_frame(residual, frame_out, qp, bit_depth=8, quant_kind=QUANT_FP, stream=
     per-size kernels running concurrently on internal streams."""
     import torch
     assert residual.dtype == torch.int16 and residual.is_cuda
+    assert residual.stride(1) == 1, "residual rows must be contiguous"
     H, W = residual.shape
     rc = _lib.lavish_txq_frame(ctypes.c_void_p(residual.data_ptr()), residual.stride(0), W, H,
                                frame_out.size_mask, frame_out.tm, bit_depth, quant_kind,

@@ -236,7 +236,10 @@ def jobs_tensor(jobs, device):
 
 
 def _d(t):
-    return _vp(t.data_ptr()) if t is not None else None
+    if t is None:
+        return None
+    assert t.dim() == 1 or t.stride(-1) == 1, "rows must be contiguous"
+    return _vp(t.data_ptr())
 
 
 def _check(rc, name):

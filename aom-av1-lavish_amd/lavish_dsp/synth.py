@@ -22,7 +22,7 @@ def shifted(img, dx, dy):
     h, w = img.shape
     ys = np.clip(np.arange(h) - dy, 0, h - 1)
     xs = np.clip(np.arange(w) - dx, 0, w - 1)
-    return img[ys][:, xs]
+    return np.ascontiguousarray(img[ys][:, xs])
 
 
 def residual_plane(width, height, bit_depth=8, seed=1234, mv=(3, -2)):
@@ -30,3 +30,18 @@ def residual_plane(width, height, bit_depth=8, seed=1234, mv=(3, -2)):
     src = frame(width, height, bit_depth, seed)
     pred = shifted(frame(width, height, bit_depth, seed), *mv)
     return src.astype(np.int16) - pred.astype(np.int16)
+
+
+def pad_plane(img, border):
+    """aom_extend_frame_borders-style edge replication by `border` pixels."""
+    return np.pad(img, border, mode="edge")
+
+
+def motion_planes(width, height, nrefs, border=160, seed=1234):
+    """C3 input: the current frame and `nrefs` references,
+    ref_k = the current content displaced by (3k, -2k) with fresh noise, all
+    padded by `border` pixels.  Returns (src[Hp, Wp], refs[nrefs, Hp, Wp])."""
+    src = pad_plane(frame(width, height, 8, seed), border)
+    refs = np.stack([pad_plane(shifted(frame(width, height, 8, seed + 101 * k), 3 * k, -2 * k),
+                               border) for k in range(1, nrefs + 1)])
+    return np.ascontiguousarray(src), np.ascontiguousarray(refs)

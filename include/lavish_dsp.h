@@ -203,6 +203,41 @@ int lavish_block_error_batch(const int32_t *coeff, const int32_t *dqcoeff,
                              int n, int nblocks, int bit_depth, int64_t *err,
                              int64_t *ssz, void *stream);
 
+/* ---- C3: DIAMOND full-pixel motion search ------------------------------
+ * av1_full_pixel_search with search_method DIAMOND (av1/encoder/mcomp.c:
+ * 1755-1895 -> full_pixel_diamond :1479-1526 -> diamond_search_sad
+ * :1318-1477), one (block, reference) per job, 8-bit planes.
+ * Offsets in bytes from src / ref; ref_off is the block origin at mv (0,0);
+ * both planes must be padded so that every mv inside the limits (as
+ * av1_set_mv_limits computes them) addresses memory, plus 3 bytes of slack
+ * after each row end. */
+typedef struct LavishDiamondJob {
+  int64_t src_off;
+  int64_t ref_off;
+  int16_t start_row, start_col;   /* FULLPEL_MV start */
+  int16_t ref_mv_row, ref_mv_col; /* MV (1/8 pel) the mv cost refers to */
+  int16_t col_min, col_max, row_min, row_max; /* FullMvLimits */
+} LavishDiamondJob;
+
+typedef struct LavishDiamondResult {
+  int16_t best_row, best_col; /* FULLPEL_MV */
+  int32_t bestsme;  /* returned var cost: aom_variance + mv_err_cost */
+  int32_t steps;    /* 8-site diamond steps evaluated */
+  int32_t searches; /* diamond_search_sad runs */
+} LavishDiamondResult;
+
+/* mv_cost_type: MV_COST_TYPE (av1/encoder/mcomp.h:31-38) 1 L1_LOWRES,
+ * 2 L1_MIDRES, 3 L1_HDRES, 4 NONE (ENTROPY needs the entropy context's cost
+ * tables: -2).  use_downsampled_sad: sdf/sdx4df = aom_sad_skip_* for blocks
+ * >= 16 high with the reference's quality recheck.  w x h: any
+ * @encoder_block_sizes entry (else -3). */
+int lavish_diamond_search_batch(const uint8_t *src, int src_stride,
+                                const uint8_t *ref, int ref_stride, int w,
+                                int h, const LavishDiamondJob *jobs, int njobs,
+                                int step_param, int mv_cost_type,
+                                int use_downsampled_sad,
+                                LavishDiamondResult *out, void *stream);
+
 /* ------------------------------------------------------------------------ */
 /* Per-call RTCD shims (host pointers)                                      */
 /* ------------------------------------------------------------------------ */

@@ -166,6 +166,40 @@ int64_t orc_block_error(const int32_t *coeff, const int32_t *dqcoeff,
 int64_t orc_highbd_block_error(const int32_t *coeff, const int32_t *dqcoeff,
                                intptr_t block_size, int64_t *ssz, int bd);
 
+/* ---- C3: DIAMOND full-pixel motion search (oracle_mcomp.c) ---- */
+typedef struct OrcMsParams {
+  const uint8_t *src; /* block origin */
+  int src_stride;
+  const uint8_t *ref; /* reference block origin at mv (0,0) */
+  int ref_stride;
+  int w, h;
+  int col_min, col_max, row_min, row_max; /* FullMvLimits */
+  int ref_mv_row, ref_mv_col;             /* MV (1/8 pel) for the mv cost */
+  int mv_cost_type; /* MV_COST_TYPE: 1 L1_LOWRES 2 L1_MIDRES 3 L1_HDRES 4 NONE */
+  int skip_sad;     /* use_downsampled_sad: sdf = aom_sad_skip */
+} OrcMsParams;
+/* av1_full_pixel_search with search_method DIAMOND (no mesh): returns the
+ * var cost, writes the best FULLPEL_MV and the number of diamond steps. */
+int orc_full_pixel_search_diamond(const OrcMsParams *p, int start_row,
+                                  int start_col, int step_param, int *best_row,
+                                  int *best_col, int *steps);
+
+/* batch over jobs laid out like LavishDiamondJob / LavishDiamondResult
+ * (include/lavish_dsp.h); threads > 1 uses pthreads. */
+typedef struct OrcDiamondJob {
+  int64_t src_off, ref_off;
+  int16_t start_row, start_col, ref_mv_row, ref_mv_col;
+  int16_t col_min, col_max, row_min, row_max;
+} OrcDiamondJob;
+typedef struct OrcDiamondResult {
+  int16_t best_row, best_col;
+  int32_t bestsme, steps, reserved;
+} OrcDiamondResult;
+void orc_diamond_batch(const uint8_t *src, int src_stride, const uint8_t *ref,
+                       int ref_stride, int w, int h, const OrcDiamondJob *jobs,
+                       long njobs, int step_param, int mv_cost_type,
+                       int skip_sad, OrcDiamondResult *out, int threads);
+
 /* ---- C2 pipeline: fwd_txfm + quantize_fp over a residual plane ----
  * For one tx_size, tile the plane with full blocks (row-major block order),
  * evaluate each tx_type whose bit is set in type_mask (ascending type order),

@@ -30,6 +30,8 @@ def lib():
 
 
 def P(a):
+    # callers pass explicit row strides: the rows must be contiguous in memory
+    assert a.ndim == 0 or a.strides[-1] == a.itemsize, "row-contiguous array expected"
     return a.ctypes.data_as(ctypes.c_void_p)
 
 
@@ -353,3 +355,22 @@ def block_error(coeff, dqcoeff, n, bd=None):
     else:
         e = lib().orc_highbd_block_error(P(coeff), P(dqcoeff), n, ctypes.byref(ssz), bd)
     return e, ssz.value
+
+
+# ------------------------------------------------------ C3 diamond search --
+def diamond_batch(src, ref, stride, w, h, jobs, step_param=0, mv_cost_type=3, skip=False,
+                  threads=1):
+    """orc_diamond_batch over JOB_DTYPE records (lavish_dsp.motion); src and
+    ref are the flat padded planes (ref holds all reference planes)."""
+    L = lib()
+    L.orc_diamond_batch.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_int,
+                                    ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_long,
+                                    ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
+                                    ctypes.c_int]
+    jobs = np.ascontiguousarray(jobs)
+    out = np.zeros(len(jobs), np.dtype([("best_row", "<i2"), ("best_col", "<i2"),
+                                        ("bestsme", "<i4"), ("steps", "<i4"),
+                                        ("searches", "<i4")], align=True))
+    L.orc_diamond_batch(P(src), stride, P(ref), stride, w, h, P(jobs), len(jobs), step_param,
+                        mv_cost_type, int(skip), P(out), threads)
+    return out
