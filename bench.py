@@ -1,12 +1,22 @@
 #!/usr/bin/env python3
 """bench.py -- MI355X throughput of the per-block RDO hot path.
 
-One step = one 1920x1080 luma residual plane (synthetic, seeded; SURVEY.md
-section 8(d) config C2) pushed through the batched forward transform +
-quantize_fp of every TX size <= 32x32 and every valid TX type (9 sizes x 16
-types + 5 sizes x 2 types): the work search_tx_type's per-type loop does for
-a frame (av1/encoder/tx_search.c:2148-2312).  A 1080p frame is 30 x 17 = 510
-64x64 superblocks; value = superblocks processed per second by the whole job.
+One step = one pass of the RDO inner loop over a synthetic, seeded 1080p
+frame; a 1080p frame is 30 x 17 = 510 64x64
+superblocks and value = superblocks processed per second by the whole job.
+The default workload ("rdo") is the metric's "fwd_txfm+quant+SAD" loop:
+
+  C2  the 1920x1080 luma residual through the batched forward transform +
+      quantize_fp of every TX size <= 32x32 and every valid TX type (9 sizes
+      x 16 types + 5 sizes x 2 types): search_tx_type's per-type loop
+      (av1/encoder/tx_search.c:2148-2312) for the frame (lavish_txq_frame);
+  C3  DIAMOND full-pixel motion search of every 16x16 block against 7
+      reference frames (av1_full_pixel_search, av1/encoder/mcomp.c:1755),
+      with the 1080p speed features (use_downsampled_sad, MV_COST_L1_HDRES)
+      (lavish_diamond_search_batch),
+
+the two legs running concurrently on two streams.  --workload c2 / c3 times
+one leg alone.
 
 Multi-GPU: one process per GPU (torchrun), each rank processes its own frame
 (independent units, no data-path collective): weak scaling.  Timing: barrier +
@@ -34,9 +44,12 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--workload", choices=("rdo", "c2", "c3"), default="rdo")
     ap.add_argument("--width", type=int, default=1920)
     ap.add_argument("--height", type=int, default=1080)
     ap.add_argument("--qindex", type=int, default=128)
+    ap.add_argument("--refs", type=int, default=7)
+    ap.add_argument("--border", type=int, default=160)
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
@@ -48,8 +61,8 @@ def sb64_count(w, h):
 
 
 def algorithmic_bytes(L, s, width, height):
-    """Bytes one launch must move: the residual once, then per
-    (block, type) qcoeff + dqcoeff (8 B/coefficient) + a 2-byte eob."""
+    """C2 bytes one launch must move: the residual once, then
+    per (block, type) qcoeff + dqcoeff (8 B/coefficient) + a 2-byte eob."""
     W, H = L.TX_W[s], L.TX_H[s]
     nb = (width // W) * (height // H)
     nt = bin(L.valid_type_mask(s)).count("1")
@@ -57,33 +70,60 @@ def algorithmic_bytes(L, s, width, height):
     return nb * (2 * W * H + nt * (8 * n + 2))
 
 
+def c3_algorithmic_bytes(res, njobs, bw, bh, skip):
+    """C3 bytes: per (block, ref) the source block once,
+    8 candidate blocks per executed diamond step (the x4d contract; skip rows
+    halve it), the source + reference block for every var cost, 16 B out."""
+    rows = bh // 2 if skip and bh >= 16 else bh
+    steps = int(res["steps"].astype("int64").sum())
+    searches = int(res["searches"].astype("int64").sum())
+    return njobs * (bw * bh + 16) + steps * 8 * rows * bw + searches * 2 * bw * bh
+
+
+C3_BLOCK = 16
+C3_COST = 3     # MV_COST_L1_HDRES
+C3_SKIP = True  # use_downsampled_sad (>= 720p, speed_features.c:205-209)
+
+
 def cpu_baseline(args):
     """The oracle's C restatement (oracle/liboracle.so, -O3, pthreads) on a
-    bounded sample: 4 superblock rows of the same synthetic frame, repeated
-    until ~cpu_seconds of wall time; reported as SB64/s."""
+    bounded sample: a 4-superblock-row strip (1920x256) of the same synthetic
+    content through the same step, repeated until ~cpu_seconds of wall time;
+    reported as SB64/s."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import _oracle as O
     import lavish_dsp as L
+    import lavish_dsp.motion as M
     import lavish_dsp.synth as synth
     threads = min(16, os.cpu_count() or 1)
-    res = synth.residual_plane(args.width, 256, 8)
+    W, Hs = args.width, 256
+    do_c2 = args.workload in ("rdo", "c2")
+    do_c3 = args.workload in ("rdo", "c3")
+    res = synth.residual_plane(W, Hs, 8)
     q = O.build_quant(8, args.qindex)
     sizes = [s for s in range(19) if L.TX_W[s] <= 32 and L.TX_H[s] <= 32]
-    sb = sb64_count(args.width, 256)
+    src, refs = synth.motion_planes(W, Hs, args.refs, args.border)
+    st = src.shape[1]
+    jobs = M.frame_jobs(W, Hs, st, args.border, src.size, C3_BLOCK, C3_BLOCK, args.refs)
+    sb = sb64_count(W, Hs)
     passes = 0
     t0 = time.perf_counter()
     while True:
-        for s in sizes:
-            O.txq_plane(res, s, L.valid_type_mask(s), q, threads=threads)
+        if do_c2:
+            for s in sizes:
+                O.txq_plane(res, s, L.valid_type_mask(s), q, threads=threads)
+        if do_c3:
+            O.diamond_batch(src.reshape(-1), refs.reshape(-1), st, C3_BLOCK, C3_BLOCK, jobs, 0,
+                            C3_COST, C3_SKIP, threads=threads)
         passes += 1
         dt = time.perf_counter() - t0
         if dt >= args.cpu_seconds:
             break
     return {"value": round(passes * sb / dt, 2), "unit": "SB64/s", "cores": threads,
             "kind": "port",
-            "sample": "%d passes of a %dx256 strip (%d SB64), all 14 sizes <=32 x valid types, "
-                      "quantize_fp q%d, oracle C restatement (-O3, %d pthreads), %.1f s"
-                      % (passes, args.width, sb, args.qindex, threads, dt)}
+            "sample": "%d passes of a %dx%d strip (%d SB64) through the %s step, oracle C "
+                      "restatement (-O3, %d pthreads), %.1f s"
+                      % (passes, W, Hs, sb, args.workload, threads, dt)}
 
 
 def main():
@@ -91,6 +131,7 @@ def main():
     import torch
     import torch.distributed as dist
     import lavish_dsp as L
+    import lavish_dsp.motion as M
     import lavish_dsp.synth as synth
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -101,14 +142,40 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
 
     W, H = args.width, args.height
+    do_c2 = args.workload in ("rdo", "c2")
+    do_c3 = args.workload in ("rdo", "c3")
+    stream = torch.cuda.current_stream()
+    side = torch.cuda.Stream()
+
+    # C2 input: residual plane (each rank its own frame)
     res = torch.from_numpy(synth.residual_plane(W, H, 8, seed=1234 + rank)).cuda()
     sizes = [s for s in range(19) if L.TX_W[s] <= 32 and L.TX_H[s] <= 32]
     qp = L.build_quant_params(8, args.qindex, L.QUANT_FP)
     frame = L.FrameOutputs(res, sizes)
-    stream = torch.cuda.current_stream()
+    # C3 input: padded current frame + references, jobs for every 16x16 block x ref
+    src_np, refs_np = synth.motion_planes(W, H, args.refs, args.border, seed=1234 + rank)
+    st = src_np.shape[1]
+    jobs_np = M.frame_jobs(W, H, st, args.border, src_np.size, C3_BLOCK, C3_BLOCK, args.refs)
+    tsrc, trefs = torch.from_numpy(src_np).cuda(), torch.from_numpy(refs_np).cuda()
+    tjobs = M.to_device(jobs_np)
+    c3_out = torch.empty(len(jobs_np) * M.RESULT_DTYPE.itemsize, dtype=torch.uint8,
+                         device="cuda")
+    torch.cuda.synchronize()
+
+    def c3(on):
+        M.diamond_search_batch(tsrc, trefs, C3_BLOCK, C3_BLOCK, tjobs, 0, C3_COST, C3_SKIP,
+                               out=c3_out, stream=on)
 
     def step():
-        L.txq_frame(res, frame, qp, stream=stream)
+        if do_c3 and do_c2:
+            side.wait_stream(stream)      # fork
+            c3(side)
+            L.txq_frame(res, frame, qp, stream=stream)
+            stream.wait_stream(side)      # join
+        elif do_c2:
+            L.txq_frame(res, frame, qp, stream=stream)
+        else:
+            c3(stream)
 
     for _ in range(args.warmup):
         step()
@@ -135,38 +202,56 @@ def main():
     status = L.status()
     if status[0] != 0:
         raise RuntimeError("HIP error during bench: %s" % (status,))
+    step_ms = sum(ev[k][0].elapsed_time(ev[k][1]) for k in range(args.steps)) / args.steps
 
-    # The dominant (indeed the only) launch of a step is the frame batch
-    # lavish_txq_frame: 14 per-size kernels forked over 3 streams and joined
-    # back; its duration is timed with HIP events on the caller stream.
-    frame_ms = sum(ev[k][0].elapsed_time(ev[k][1]) for k in range(args.steps)) / args.steps
-    step_bytes = sum(algorithmic_bytes(L, s, W, H) for s in sizes)
-    achieved = step_bytes / (frame_ms * 1e-3) / 1e9
-
-    # informational: per-size kernel durations, serialized, outside the timed region
-    kev = {s: (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-           for s in sizes}
-    kern_ms = {s: 0.0 for s in sizes}
-    for _ in range(3):
-        for s in sizes:
-            kev[s][0].record(stream)
-            L.txq_plane(res, s, frame.type_masks[s], qp, out=frame.outs[s], stream=stream)
-            kev[s][1].record(stream)
+    # per-leg launch durations, each leg alone on the caller stream (HIP events
+    # on the stream the work is launched on), outside the timed region
+    def leg_ms(fn, reps=5):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record(stream)
+        for _ in range(reps):
+            fn()
+        b.record(stream)
         torch.cuda.synchronize()
-        for s in sizes:
-            kern_ms[s] += kev[s][0].elapsed_time(kev[s][1]) / 3
+        return a.elapsed_time(b) / reps
+
+    c2_ms = leg_ms(lambda: L.txq_frame(res, frame, qp, stream=stream)) if do_c2 else 0.0
+    c3_ms = leg_ms(lambda: c3(stream)) if do_c3 else 0.0
+    c2_bytes = sum(algorithmic_bytes(L, s, W, H) for s in sizes)
+    c3_res = M.results_numpy(c3_out) if do_c3 else None
+    c3_bytes = c3_algorithmic_bytes(c3_res, len(jobs_np), C3_BLOCK, C3_BLOCK, C3_SKIP) \
+        if do_c3 else 0
 
     traffic = None
-    kname = "lavish_txq_frame"
     if os.path.exists(args.pmc_json):
         try:
-            pmc = json.load(open(args.pmc_json))
-            traffic = pmc.get("frame_hbm_bytes_per_launch")
+            traffic = json.load(open(args.pmc_json)).get("frame_hbm_bytes_per_launch")
         except (ValueError, OSError):
             traffic = None
 
+    # dominant kernel: the longer leg
+    if do_c2 and (c2_ms >= c3_ms):
+        roof = {"bound": "hbm",
+                "kernel": "lavish_txq_frame (14 txq_plane_kernel<W,H> over 3 streams)",
+                "achieved": round(c2_bytes / (c2_ms * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBS,
+                "unit": "GB/s", "traffic": traffic, "avg_launch_ms": round(c2_ms, 4),
+                "algorithmic_bytes_per_launch": c2_bytes}
+    else:
+        roof = {"bound": "hbm", "kernel": "diamond_kernel<16,16> (lavish_diamond_search_batch)",
+                "achieved": round(c3_bytes / (c3_ms * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBS,
+                "unit": "GB/s", "traffic": None, "avg_launch_ms": round(c3_ms, 4),
+                "algorithmic_bytes_per_launch": c3_bytes}
+    roof["frac"] = round(roof["achieved"] / HBM_PEAK_GBS, 4)
+
     sb = sb64_count(W, H)
     value = world * sb * args.steps / elapsed
+    legs = []
+    if do_c2:
+        legs.append("C2 fwd_txfm2d + quantize_fp (qindex %d) of all 14 TX sizes <=32x32 x every "
+                    "valid TX type" % args.qindex)
+    if do_c3:
+        legs.append("C3 DIAMOND full-pel search of every %dx%d block x %d refs (downsampled SAD, "
+                    "MV_COST_L1_HDRES, step_param 0)" % (C3_BLOCK, C3_BLOCK, args.refs))
     line = {
         "metric": METRIC,
         "value": round(value, 2),
@@ -179,28 +264,22 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "int32",
-        "data": "synthetic (seeded 1080p luma residual, lavish_dsp/synth.py)",
+        "data": "synthetic (seeded 1080p content, lavish_dsp/synth.py)",
         "config": {
-            "workload": "C2: %dx%d 8-bit residual, fwd_txfm2d + quantize_fp (qindex %d) of "
-                        "all 14 TX sizes <=32x32 x every valid TX type per step "
-                        "(lavish_txq_frame); %d SB64/frame"
-                        % (W, H, args.qindex, sb),
-            "tx_sizes": [L.TX_SIZES[s] for s in sizes],
+            "workload": "%s: %dx%d 8-bit frame per step; %s; %d SB64/frame"
+                        % (args.workload, W, H, " + ".join(legs), sb),
+            "tx_sizes": [L.TX_SIZES[s] for s in sizes] if do_c2 else [],
             "parallelism": "frame-per-rank x%d" % world,
         },
-        "roofline": {
-            "bound": "hbm",
-            "kernel": kname + " (14 txq_plane_kernel<W,H> over 3 streams)",
-            "achieved": round(achieved, 1),
-            "peak": HBM_PEAK_GBS,
-            "unit": "GB/s",
-            "frac": round(achieved / HBM_PEAK_GBS, 4),
-            "traffic": traffic,
-            "avg_launch_ms": round(frame_ms, 4),
-            "algorithmic_bytes_per_launch": step_bytes,
-        },
-        "kernel_ms_serialized": {L.TX_SIZES[s]: round(kern_ms[s], 4) for s in sizes},
+        "roofline": roof,
+        "legs_ms": {"c2_txq_frame": round(c2_ms, 4), "c3_diamond": round(c3_ms, 4),
+                    "step_event_ms": round(step_ms, 4)},
     }
+    if do_c3:
+        line["c3"] = {"jobs": len(jobs_np),
+                      "steps_per_job": round(float(c3_res["steps"].mean()), 2),
+                      "algorithmic_bytes": c3_bytes,
+                      "achieved_GBps": round(c3_bytes / (c3_ms * 1e-3) / 1e9, 1)}
     if rank == 0 and world == 1 and not args.no_cpu:
         line["cpu_baseline"] = cpu_baseline(args)
     if rank == 0:
