@@ -1,0 +1,232 @@
+// inv.hip -- batched inverse 2-D transform + reconstruction add for gfx950
+// (SURVEY.md section 8 row a17).
+//
+// Reference, per block: av1_inverse_transform_block (av1/common/idct.c:304-322)
+// -> av1_inv_txfm_add_c (u8 through a u16 copy, :281-302) /
+// av1_highbd_inv_txfm_add (:212-279) -> inv_txfm2d_add_facade ->
+// inv_txfm2d_add_c (av1/common/av1_inv_txfm2d.c:234-316): rows (x NewInvSqrt2
+// for 2:1 shapes, clamp to bd+8, row 1-D, round shift[0]), columns (lr flip,
+// clamp to max(bd+6, 16), column 1-D, round shift[1], ud flip,
+// highbd_clip_pixel_add).  64-point sizes read the packed 32x32 quadrant.
+//
+// Here one wave64 owns P = 64 / min(W,H) blocks ("tile") of one TX size:
+//   dqcoeff (HBM, coalesced) -> LDS -> row transforms (one row per lane per
+//   pass, registers) -> LDS (padded rows) -> column transforms -> add to the
+//   destination pixels (each lane one column, rows coalesced across lanes).
+// The 1-D transforms are the same straight-line code as the forward kernels
+// (txfm_dev.h, inv_1d), with the reference's per-stage clamps at the bit
+// depth's ranges (template BDI).
+#include "lavish_internal.h"
+#include "txfm_dev.h"
+
+namespace lavish {
+namespace {
+
+struct InvJob {
+  int64_t dst_off;
+  int64_t coeff_off;
+  int32_t tx_type;
+  int32_t eob;
+};
+static_assert(sizeof(InvJob) == sizeof(LavishInvJob), "job layout");
+
+constexpr uint8_t kVtx[16] = {0, 1, 0, 1, 2, 0, 2, 1, 2, 3, 0, 3, 1, 3, 2, 3};
+constexpr uint8_t kHtx[16] = {0, 0, 1, 1, 0, 2, 2, 2, 1, 3, 3, 0, 3, 1, 3, 2};
+constexpr uint32_t pack2(const uint8_t (&v)[16]) {
+  uint32_t r = 0;
+  for (int i = 0; i < 16; ++i) r |= (uint32_t)v[i] << (2 * i);
+  return r;
+}
+constexpr uint32_t kVtxP = pack2(kVtx), kHtxP = pack2(kHtx);
+
+template <int W, int H>
+struct InvTile {
+  static constexpr int MN = W < H ? W : H;
+  static constexpr int P = 64 / MN;            // blocks per wave
+  static constexpr int RPT = H / MN;           // row transforms per lane
+  static constexpr int CPT = W / MN;           // column transforms per lane
+  static constexpr int KW = W > 32 ? 32 : W;   // stored coefficient columns
+  static constexpr int KH = H > 32 ? 32 : H;   // stored coefficient rows
+  static constexpr int NC = KW * KH;           // stored words per block
+  static constexpr int T1S = W + 1;
+};
+
+// bd index: 0 -> 8, 1 -> 10, 2 -> 12 (row / column clamp ranges of
+// av1_gen_inv_stage_range with opt_range_row / opt_range_col)
+template <int BDI>
+struct Bd {
+  static constexpr int bd = 8 + 2 * BDI;
+  static constexpr int rng_row = BDI == 0 ? 16 : (BDI == 1 ? 18 : 20);
+  static constexpr int rng_col = BDI == 2 ? 18 : 16;
+  static constexpr int clamp_in_row = bd + 8;
+  static constexpr int clamp_in_col = bd + 6 > 16 ? bd + 6 : 16;
+};
+
+__device__ __forceinline__ int32_t rshift_r(int32_t v, int bit) {
+  return bit == 0 ? v : (int32_t)(((int64_t)v + ((int64_t)1 << (bit - 1))) >> bit);
+}
+
+template <int W, int H, int BDI, typename PIX>
+__global__ __launch_bounds__(64) void inv_tile_kernel(const int32_t* __restrict__ dq,
+                                                      const InvJob* __restrict__ jobs, int njobs,
+                                                      PIX* __restrict__ dst, int stride) {
+  using T = InvTile<W, H>;
+  using C = TxCfg<W, H>;
+  using B = Bd<BDI>;
+  constexpr int P = T::P, T1S = T::T1S;
+  __shared__ int32_t cf[P * T::NC];
+  __shared__ int32_t t1[P * H * T1S];
+  __shared__ InvJob jb[P];
+
+  const int lane = threadIdx.x;
+  const int j0 = blockIdx.x * P;
+  if (lane < P) {
+    InvJob z{};
+    z.eob = 0;
+    jb[lane] = (j0 + lane < njobs) ? jobs[j0 + lane] : z;
+  }
+  __syncthreads();
+  // stage the tile's dequantized coefficients (coalesced within a block)
+  for (int i = lane; i < P * T::NC; i += 64) {
+    const int b = i / T::NC, w = i - b * T::NC;
+    cf[i] = jb[b].eob ? dq[jb[b].coeff_off + w] : 0;
+  }
+  __syncthreads();
+
+  // ---- rows (inv_txfm2d_add_c "Rows") ----
+  // Blocks of a tile may carry different TX types: a waterfall over the
+  // distinct types keeps the transform-kind branches scalar (one pass when
+  // the tile is uniform, the common case).
+#pragma unroll
+  for (int k = 0; k < T::RPT; ++k) {
+    const int idx = k * 64 + lane;
+    const int b = idx / H, r = idx - b * H;
+    const int mine = jb[b].tx_type;
+    bool pending = true;
+    while (__ballot(pending)) {
+      if (pending) {
+        const int t = __builtin_amdgcn_readfirstlane(mine);
+        if (mine == t) {
+          pending = false;
+          const int ht = (kHtxP >> (2 * t)) & 3;
+          const int kr = ht == 3 ? 2 : (ht == 0 ? 0 : 1);
+          int32_t in[W], out[W];
+#pragma unroll
+          for (int c = 0; c < W; ++c) {
+            int32_t v = (c < T::KW && r < T::KH) ? cf[b * T::NC + c * T::KH + r] : 0;
+            if constexpr (C::rect2) v = rshift64((int64_t)v * 2896, 12);
+            in[c] = clamp_bits<B::clamp_in_row>(v);
+          }
+          inv_1d<W, 12, B::rng_row>(kr, in, out);
+#pragma unroll
+          for (int c = 0; c < W; ++c) t1[(b * H + r) * T1S + c] = rshift_r(out[c], -C::is0);
+        }
+      }
+    }
+  }
+  __syncthreads();
+
+  // ---- columns + reconstruction ("Columns", highbd_clip_pixel_add) ----
+  constexpr int maxv = (1 << B::bd) - 1;
+#pragma unroll
+  for (int k = 0; k < T::CPT; ++k) {
+    const int idx = k * 64 + lane;
+    const int b = idx / W, c = idx - b * W;
+    const int mine = jb[b].tx_type;
+    bool pending = true;
+    while (__ballot(pending)) {
+      if (pending) {
+        const int t = __builtin_amdgcn_readfirstlane(mine);
+        if (mine == t) {
+          pending = false;
+          const int vt = (kVtxP >> (2 * t)) & 3, ht = (kHtxP >> (2 * t)) & 3;
+          const int kc = vt == 3 ? 2 : (vt == 0 ? 0 : 1);
+          const bool ud = vt == 2, lr = ht == 2;
+          const int cc = lr ? W - 1 - c : c;
+          int32_t in[H], out[H];
+#pragma unroll
+          for (int r = 0; r < H; ++r)
+            in[r] = clamp_bits<B::clamp_in_col>(t1[(b * H + r) * T1S + cc]);
+          inv_1d<H, 12, B::rng_col>(kc, in, out);
+          if (jb[b].eob != 0) {
+            PIX* d = dst + jb[b].dst_off + c;
+#pragma unroll
+            for (int r = 0; r < H; ++r) {
+              const int32_t res = rshift_r(ud ? out[H - 1 - r] : out[r], -C::is1);
+              const int v = (int)d[(int64_t)r * stride] + res;
+              d[(int64_t)r * stride] = (PIX)(v < 0 ? 0 : (v > maxv ? maxv : v));
+            }
+          }
+        }
+      }
+    }
+  }
+}
+
+template <int W, int H, int BDI, typename PIX>
+void launch(const int32_t* dq, const LavishInvJob* jobs, int njobs, PIX* dst, int stride,
+            hipStream_t s) {
+  constexpr int P = InvTile<W, H>::P;
+  hipLaunchKernelGGL((inv_tile_kernel<W, H, BDI, PIX>), dim3((njobs + P - 1) / P), dim3(64), 0,
+                     s, dq, (const InvJob*)jobs, njobs, dst, stride);
+}
+
+template <int W, int H>
+int dispatch_bd(const int32_t* dq, const LavishInvJob* jobs, int njobs, void* dst, int stride,
+                int bd, int highbd, hipStream_t s) {
+  if (!highbd) {
+    if (bd != 8) return -4;
+    launch<W, H, 0, uint8_t>(dq, jobs, njobs, (uint8_t*)dst, stride, s);
+  } else if (bd == 8) {
+    launch<W, H, 0, uint16_t>(dq, jobs, njobs, (uint16_t*)dst, stride, s);
+  } else if (bd == 10) {
+    launch<W, H, 1, uint16_t>(dq, jobs, njobs, (uint16_t*)dst, stride, s);
+  } else if (bd == 12) {
+    launch<W, H, 2, uint16_t>(dq, jobs, njobs, (uint16_t*)dst, stride, s);
+  } else {
+    return -4;
+  }
+  return 0;
+}
+
+}  // namespace
+
+int inv_txfm_add_batch(const int32_t* dq, int tx_size, const LavishInvJob* jobs, int njobs,
+                       void* dst, int stride, int bd, int highbd, hipStream_t s) {
+  if (njobs <= 0) return 0;
+  int rc;
+  switch (tx_size) {
+    case 0: rc = dispatch_bd<4, 4>(dq, jobs, njobs, dst, stride, bd, highbd, s); break;
+    case 1: rc = dispatch_bd<8, 8>(dq, jobs, njobs, dst, stride, bd, highbd, s); break;
+    case 2: rc = dispatch_bd<16, 16>(dq, jobs, njobs, dst, stride, bd, highbd, s); break;
+    case 3: rc = dispatch_bd<32, 32>(dq, jobs, njobs, dst, stride, bd, highbd, s); break;
+    case 4: rc = dispatch_bd<64, 64>(dq, jobs, njobs, dst, stride, bd, highbd, s); break;
+    case 5: rc = dispatch_bd<4, 8>(dq, jobs, njobs, dst, stride, bd, highbd, s); break;
+    case 6: rc = dispatch_bd<8, 4>(dq, jobs, njobs, dst, stride, bd, highbd, s); break;
+    case 7: rc = dispatch_bd<8, 16>(dq, jobs, njobs, dst, stride, bd, highbd, s); break;
+    case 8: rc = dispatch_bd<16, 8>(dq, jobs, njobs, dst, stride, bd, highbd, s); break;
+    case 9: rc = dispatch_bd<16, 32>(dq, jobs, njobs, dst, stride, bd, highbd, s); break;
+    case 10: rc = dispatch_bd<32, 16>(dq, jobs, njobs, dst, stride, bd, highbd, s); break;
+    case 11: rc = dispatch_bd<32, 64>(dq, jobs, njobs, dst, stride, bd, highbd, s); break;
+    case 12: rc = dispatch_bd<64, 32>(dq, jobs, njobs, dst, stride, bd, highbd, s); break;
+    case 13: rc = dispatch_bd<4, 16>(dq, jobs, njobs, dst, stride, bd, highbd, s); break;
+    case 14: rc = dispatch_bd<16, 4>(dq, jobs, njobs, dst, stride, bd, highbd, s); break;
+    case 15: rc = dispatch_bd<8, 32>(dq, jobs, njobs, dst, stride, bd, highbd, s); break;
+    case 16: rc = dispatch_bd<32, 8>(dq, jobs, njobs, dst, stride, bd, highbd, s); break;
+    case 17: rc = dispatch_bd<16, 64>(dq, jobs, njobs, dst, stride, bd, highbd, s); break;
+    case 18: rc = dispatch_bd<64, 16>(dq, jobs, njobs, dst, stride, bd, highbd, s); break;
+    default: return -1;
+  }
+  if (rc == 0) LAVISH_CHECK(hipGetLastError());
+  return rc;
+}
+
+}  // namespace lavish
+
+extern "C" int lavish_inv_txfm_add_batch(const int32_t* dqcoeff, int tx_size,
+                                         const LavishInvJob* jobs, int njobs, void* dst,
+                                         int dst_stride, int bit_depth, int highbd,
+                                         void* stream) {
+  return lavish::inv_txfm_add_batch(dqcoeff, tx_size, jobs, njobs, dst, dst_stride, bit_depth,
+                                    highbd, (hipStream_t)stream);
+}

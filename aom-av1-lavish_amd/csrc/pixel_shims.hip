@@ -178,6 +178,37 @@ int64_t block_error_shim(const int32_t* coeff, const int32_t* dqcoeff, intptr_t 
   return e;
 }
 
+// one block of av1_inv_txfm2d_add_* / av1_[highbd_]inv_txfm_add on host
+// buffers: stage the coefficients and the destination window, run the batch
+// kernel on a single job, copy the window back.
+template <typename Pix>
+void inv_shim(int tx_size, const int32_t* input, Pix* dst, int stride, int tx_type, int bd) {
+  if (!tx_type_valid(tx_size, tx_type)) {
+    fprintf(stderr, "[lavish_hip] invalid tx_type %d for tx_size %d\n", tx_type, tx_size);
+    abort();
+  }
+  const int W = tx_w(tx_size), H = tx_h(tx_size), n = max_eob(tx_size);
+  Stage st(kStageCap);
+  const int32_t* dc = st.copy_in(input, (size_t)n);
+  Pix* dd = st.block(dst, stride, W, H);
+  LavishInvJob jb{};
+  jb.tx_type = tx_type;
+  jb.eob = 1;  // the 2-D functions ignore eob
+  const LavishInvJob* djob = st.copy_in(&jb, 1);
+  must(lavish_inv_txfm_add_batch(dc, tx_size, djob, 1, dd, W, bd, sizeof(Pix) == 2, st.s),
+       "lavish_inv_txfm_add_batch");
+  LAVISH_CHECK(hipMemcpy2DAsync(dst, (size_t)stride * sizeof(Pix), dd, (size_t)W * sizeof(Pix),
+                                (size_t)W * sizeof(Pix), H, hipMemcpyDeviceToHost, st.s));
+  st.sync();
+}
+
+void check_lossless(const LavishTxfmParam* p) {
+  if (p->lossless) {
+    fprintf(stderr, "[lavish_hip] lossless (WHT) inverse transform is not implemented\n");
+    abort();
+  }
+}
+
 }  // namespace
 }  // namespace lavish
 
@@ -359,5 +390,44 @@ int64_t av1_highbd_block_error_hip(const int32_t* coeff, const int32_t* dqcoeff,
                                    int64_t* ssz, int bd) {
   return block_error_shim(coeff, dqcoeff, n, ssz, bd);
 }
+
+
+// ---- inverse transforms (av1/common/av1_rtcd_defs.pl:137-243) ----
+static int size_of(int w, int h) {
+  for (int s = 0; s < 19; ++s)
+    if (tx_w(s) == w && tx_h(s) == h) return s;
+  return -1;
+}
+#define INV2D_SHIM(w, h)                                                                      \
+  void av1_inv_txfm2d_add_##w##x##h##_hip(const int32_t* input, uint16_t* output, int stride,  \
+                                          uint8_t tx_type, int bd) {                          \
+    inv_shim<uint16_t>(size_of(w, h), input, output, stride, tx_type, bd);                    \
+  }
+LAVISH_TX_SIZES_ALL(INV2D_SHIM)
+
+// av1_inv_txfm_add_c (idct.c:281-302): u8 destination, bd 8
+void av1_inv_txfm_add_hip(const int32_t* dqcoeff, uint8_t* dst, int stride,
+                          const LavishTxfmParam* p) {
+  check_lossless(p);
+  inv_shim<uint8_t>(p->tx_size, dqcoeff, dst, stride, p->tx_type, 8);
+}
+// av1_highbd_inv_txfm_add_c (idct.c:212-279): tagged u16 destination
+void av1_highbd_inv_txfm_add_hip(const int32_t* input, uint8_t* dest, int stride,
+                                 const LavishTxfmParam* p) {
+  check_lossless(p);
+  inv_shim<uint16_t>(p->tx_size, input, untag<uint16_t>(dest), stride, p->tx_type, p->bd);
+}
+#define HBD_INV_SHIM(w, h)                                                                    \
+  void av1_highbd_inv_txfm_add_##w##x##h##_hip(const int32_t* input, uint8_t* dest,           \
+                                               int stride, const LavishTxfmParam* p) {        \
+    check_lossless(p);                                                                        \
+    inv_shim<uint16_t>(size_of(w, h), input, untag<uint16_t>(dest), stride, p->tx_type,      \
+                       p->bd);                                                                \
+  }
+HBD_INV_SHIM(4, 4) HBD_INV_SHIM(8, 8) HBD_INV_SHIM(4, 8) HBD_INV_SHIM(8, 4)
+HBD_INV_SHIM(4, 16) HBD_INV_SHIM(16, 4) HBD_INV_SHIM(8, 16) HBD_INV_SHIM(16, 8)
+HBD_INV_SHIM(16, 32) HBD_INV_SHIM(32, 16) HBD_INV_SHIM(32, 32) HBD_INV_SHIM(32, 64)
+HBD_INV_SHIM(64, 32) HBD_INV_SHIM(64, 64) HBD_INV_SHIM(8, 32) HBD_INV_SHIM(32, 8)
+HBD_INV_SHIM(16, 64) HBD_INV_SHIM(64, 16)
 
 }  // extern "C"

@@ -139,6 +139,8 @@ __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+typedef int32_t v4i __attribute__((ext_vector_type(4)));
+
 template <int W, int H>
 struct Tile {
   static constexpr int MN = W < H ? W : H;
@@ -233,17 +235,19 @@ __device__ __forceinline__ void txq_types(const TxqArgs& a,
     if (a.qcoeff != nullptr) {
       const int total = nvalid * N;
       const size_t gbase = ((size_t)ti * a.nblocks + blk0) * N;
+      // streaming (nontemporal) stores: the outputs are written once and
+      // far exceed the 256 MiB Infinity Cache
       for (int i = lane * 4; i < total; i += 64 * 4) {
-        const int4 q4 = *reinterpret_cast<const int4*>(&t2[i]);
-        *reinterpret_cast<int4*>(&a.qcoeff[gbase + i]) = q4;
+        const v4i q4 = *reinterpret_cast<const v4i*>(&t2[i]);
+        __builtin_nontemporal_store(q4, reinterpret_cast<v4i*>(&a.qcoeff[gbase + i]));
         if (a.dqcoeff != nullptr) {
           const int rc0 = i % N;  // N % 4 == 0: all four share the block
-          int4 d4;
+          v4i d4;
           d4.x = dequant_one<LS>(q4.x, rc0 != 0, a.qp);  // only x can be DC
           d4.y = dequant_one<LS>(q4.y, 1, a.qp);
           d4.z = dequant_one<LS>(q4.z, 1, a.qp);
           d4.w = dequant_one<LS>(q4.w, 1, a.qp);
-          *reinterpret_cast<int4*>(&a.dqcoeff[gbase + i]) = d4;
+          __builtin_nontemporal_store(d4, reinterpret_cast<v4i*>(&a.dqcoeff[gbase + i]));
         }
       }
     }

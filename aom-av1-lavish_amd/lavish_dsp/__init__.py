@@ -298,3 +298,54 @@ def quantize_batch(coeff, scan, log_scale, qp, bit_depth=8, quant_kind=QUANT_FP,
     if rc != 0:
         raise ValueError("lavish_quantize_batch rejected arguments (rc=%d)" % rc)
     return q, dq, eob
+
+
+# ------------------------------------------------- inverse transforms --
+INV_JOB_DTYPE = np.dtype([("dst_off", "<i8"), ("coeff_off", "<i8"), ("tx_type", "<i4"),
+                          ("eob", "<i4")], align=True)
+assert INV_JOB_DTYPE.itemsize == 24
+_lib.lavish_inv_txfm_add_batch.argtypes = [_vp, _i32, _vp, _i32, _vp, _i32, _i32, _i32, _vp]
+_lib.lavish_inv_txfm_add_batch.restype = _i32
+for _s in range(19):
+    _f = getattr(_lib, "av1_inv_txfm2d_add_%s_hip" % TX_SIZES[_s])
+    _f.argtypes = [_vp, _vp, _i32, ctypes.c_uint8, _i32]
+    _f.restype = None
+_lib.av1_inv_txfm_add_hip.argtypes = [_vp, _vp, _i32, ctypes.POINTER(TxfmParam)]
+_lib.av1_highbd_inv_txfm_add_hip.argtypes = [_vp, _vp, _i32, ctypes.POINTER(TxfmParam)]
+
+
+def av1_inv_txfm2d_add(tx_size, input, output, stride, tx_type, bd):
+    """av1_inv_txfm2d_add_{WxH} (av1/common/av1_rtcd_defs.pl:222-243): int32
+    dqcoeff (reference layout) added into a uint16 destination in place."""
+    assert input.dtype == np.int32 and output.dtype == np.uint16
+    assert output.strides[-1] == 2
+    getattr(_lib, "av1_inv_txfm2d_add_%s_hip" % TX_SIZES[tx_size])(
+        _p(input), _p(output), stride, tx_type, bd)
+
+
+def av1_inv_txfm_add(dqcoeff, dst, stride, txfm_param):
+    """av1_inv_txfm_add (u8 destination) / av1_highbd_inv_txfm_add when
+    txfm_param.is_hbd (u16 destination, tagged pointer as the reference)."""
+    if txfm_param.is_hbd:
+        assert dst.dtype == np.uint16
+        _lib.av1_highbd_inv_txfm_add_hip(_p(dqcoeff), ctypes.c_void_p(dst.ctypes.data >> 1),
+                                         stride, ctypes.byref(txfm_param))
+    else:
+        assert dst.dtype == np.uint8
+        _lib.av1_inv_txfm_add_hip(_p(dqcoeff), _p(dst), stride, ctypes.byref(txfm_param))
+
+
+def inv_txfm_add_batch(dqcoeff, tx_size, jobs, dst, bit_depth=8, stream=None):
+    """lavish_inv_txfm_add_batch on device tensors: dqcoeff int32 (flat),
+    jobs a device byte tensor of INV_JOB_DTYPE records, dst a 2-D uint8
+    (bit_depth 8) or int16-viewed uint16 plane updated in place."""
+    import torch
+    assert dst.stride(1) == 1
+    highbd = dst.element_size() == 2
+    nj = jobs.numel() // INV_JOB_DTYPE.itemsize
+    rc = _lib.lavish_inv_txfm_add_batch(ctypes.c_void_p(dqcoeff.data_ptr()), tx_size,
+                                        ctypes.c_void_p(jobs.data_ptr()), nj,
+                                        ctypes.c_void_p(dst.data_ptr()), dst.stride(0),
+                                        bit_depth, int(highbd), _stream_ptr(stream))
+    if rc != 0:
+        raise ValueError("lavish_inv_txfm_add_batch rejected its arguments (rc=%d)" % rc)

@@ -15,8 +15,11 @@ The default workload ("rdo") is the metric's "fwd_txfm+quant+SAD" loop:
       with the 1080p speed features (use_downsampled_sad, MV_COST_L1_HDRES)
       (lavish_diamond_search_batch),
 
-the two legs running concurrently on two streams.  --workload c2 / c3 times
-one leg alone.
+the two legs back to back on the caller stream (C2 forks its per-size
+kernels over internal streams).  Running the legs concurrently on two streams
+measured no gain (both saturate the CUs), and sequential legs keep each
+kernel's rocprof duration equal to its event-timed duration.  --workload c2 /
+c3 times one leg alone.
 
 Multi-GPU: one process per GPU (torchrun), each rank processes its own frame
 (independent units, no data-path collective): weak scaling.  Timing: barrier +
@@ -145,7 +148,6 @@ def main():
     do_c2 = args.workload in ("rdo", "c2")
     do_c3 = args.workload in ("rdo", "c3")
     stream = torch.cuda.current_stream()
-    side = torch.cuda.Stream()
 
     # C2 input: residual plane (each rank its own frame)
     res = torch.from_numpy(synth.residual_plane(W, H, 8, seed=1234 + rank)).cuda()
@@ -166,22 +168,20 @@ def main():
         M.diamond_search_batch(tsrc, trefs, C3_BLOCK, C3_BLOCK, tjobs, 0, C3_COST, C3_SKIP,
                                out=c3_out, stream=on)
 
-    def step():
-        if do_c3 and do_c2:
-            side.wait_stream(stream)      # fork
-            c3(side)
-            L.txq_frame(res, frame, qp, stream=stream)
-            stream.wait_stream(side)      # join
-        elif do_c2:
-            L.txq_frame(res, frame, qp, stream=stream)
-        else:
+    def step(evs=None):
+        if do_c3:
             c3(stream)
+        if evs is not None:
+            evs[1].record(stream)
+        if do_c2:
+            L.txq_frame(res, frame, qp, stream=stream)
 
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
 
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+    # per step: start, after C3, end -- HIP events on the launch stream
+    ev = [tuple(torch.cuda.Event(enable_timing=True) for _ in range(3))
           for _ in range(args.steps)]
     if world > 1:
         dist.barrier()
@@ -189,8 +189,8 @@ def main():
     t0 = time.perf_counter()
     for k in range(args.steps):
         ev[k][0].record(stream)
-        step()
-        ev[k][1].record(stream)
+        step(ev[k])
+        ev[k][2].record(stream)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -202,21 +202,10 @@ def main():
     status = L.status()
     if status[0] != 0:
         raise RuntimeError("HIP error during bench: %s" % (status,))
-    step_ms = sum(ev[k][0].elapsed_time(ev[k][1]) for k in range(args.steps)) / args.steps
-
-    # per-leg launch durations, each leg alone on the caller stream (HIP events
-    # on the stream the work is launched on), outside the timed region
-    def leg_ms(fn, reps=5):
-        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        a.record(stream)
-        for _ in range(reps):
-            fn()
-        b.record(stream)
-        torch.cuda.synchronize()
-        return a.elapsed_time(b) / reps
-
-    c2_ms = leg_ms(lambda: L.txq_frame(res, frame, qp, stream=stream)) if do_c2 else 0.0
-    c3_ms = leg_ms(lambda: c3(stream)) if do_c3 else 0.0
+    K = args.steps
+    step_ms = sum(ev[k][0].elapsed_time(ev[k][2]) for k in range(K)) / K
+    c3_ms = sum(ev[k][0].elapsed_time(ev[k][1]) for k in range(K)) / K if do_c3 else 0.0
+    c2_ms = sum(ev[k][1].elapsed_time(ev[k][2]) for k in range(K)) / K if do_c2 else 0.0
     c2_bytes = sum(algorithmic_bytes(L, s, W, H) for s in sizes)
     c3_res = M.results_numpy(c3_out) if do_c3 else None
     c3_bytes = c3_algorithmic_bytes(c3_res, len(jobs_np), C3_BLOCK, C3_BLOCK, C3_SKIP) \

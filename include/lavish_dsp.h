@@ -203,6 +203,26 @@ int lavish_block_error_batch(const int32_t *coeff, const int32_t *dqcoeff,
                              int n, int nblocks, int bit_depth, int64_t *err,
                              int64_t *ssz, void *stream);
 
+/* ---- inverse transform + reconstruction (a17) ---------------------------
+ * av1_inverse_transform_block (av1/common/idct.c:304-322) for a list of
+ * blocks of one tx_size: dst (u8 when highbd = 0, then bit_depth must be 8;
+ * u16 otherwise) += inverse 2-D transform of the block's dqcoeff, clipped to
+ * the bit depth.  Blocks with eob == 0 are left untouched (the reference
+ * returns early).  coeff_off addresses av1_get_max_eob(tx_size) words in the
+ * reference's layout (64-point sizes: the packed 32-column quadrant).  Jobs of
+ * one call must not overlap in dst. */
+typedef struct LavishInvJob {
+  int64_t dst_off;   /* element offset of the block's top-left pixel */
+  int64_t coeff_off; /* word offset of the block's dqcoeff */
+  int32_t tx_type;
+  int32_t eob;
+} LavishInvJob;
+
+int lavish_inv_txfm_add_batch(const int32_t *dqcoeff, int tx_size,
+                              const LavishInvJob *jobs, int njobs, void *dst,
+                              int dst_stride, int bit_depth, int highbd,
+                              void *stream);
+
 /* ---- C3: DIAMOND full-pixel motion search ------------------------------
  * av1_full_pixel_search with search_method DIAMOND (av1/encoder/mcomp.c:
  * 1755-1895 -> full_pixel_diamond :1479-1526 -> diamond_search_sad
@@ -294,6 +314,34 @@ void av1_highbd_quantize_fp_hip(const int32_t *coeff_ptr, intptr_t count,
                                 const int16_t *dequant_ptr, uint16_t *eob_ptr,
                                 const int16_t *scan, const int16_t *iscan,
                                 int log_scale);
+
+/* ---- inverse transform shims (av1/common/av1_rtcd_defs.pl:137-243) ---- */
+#define LAVISH_TX_SIZES_ALL(X)                                               \
+  X(4, 4) X(8, 8) X(16, 16) X(32, 32) X(64, 64) X(4, 8) X(8, 4) X(8, 16)    \
+  X(16, 8) X(16, 32) X(32, 16) X(32, 64) X(64, 32) X(4, 16) X(16, 4)        \
+  X(8, 32) X(32, 8) X(16, 64) X(64, 16)
+#define LAVISH_INV2D(w, h)                                                   \
+  void av1_inv_txfm2d_add_##w##x##h##_hip(const int32_t *input,             \
+                                          uint16_t *output, int stride,     \
+                                          uint8_t tx_type, int bd);
+LAVISH_TX_SIZES_ALL(LAVISH_INV2D)
+#undef LAVISH_INV2D
+void av1_inv_txfm_add_hip(const int32_t *dqcoeff, uint8_t *dst, int stride,
+                          const LavishTxfmParam *txfm_param);
+void av1_highbd_inv_txfm_add_hip(const int32_t *input, uint8_t *dest,
+                                 int stride,
+                                 const LavishTxfmParam *txfm_param);
+#define LAVISH_HBD_INV(w, h)                                                 \
+  void av1_highbd_inv_txfm_add_##w##x##h##_hip(                             \
+      const int32_t *input, uint8_t *dest, int stride,                      \
+      const LavishTxfmParam *txfm_param);
+LAVISH_HBD_INV(4, 4) LAVISH_HBD_INV(8, 8) LAVISH_HBD_INV(4, 8)
+LAVISH_HBD_INV(8, 4) LAVISH_HBD_INV(4, 16) LAVISH_HBD_INV(16, 4)
+LAVISH_HBD_INV(8, 16) LAVISH_HBD_INV(16, 8) LAVISH_HBD_INV(16, 32)
+LAVISH_HBD_INV(32, 16) LAVISH_HBD_INV(32, 32) LAVISH_HBD_INV(32, 64)
+LAVISH_HBD_INV(64, 32) LAVISH_HBD_INV(64, 64) LAVISH_HBD_INV(8, 32)
+LAVISH_HBD_INV(32, 8) LAVISH_HBD_INV(16, 64) LAVISH_HBD_INV(64, 16)
+#undef LAVISH_HBD_INV
 
 /* ---- pixel shims ---------------------------------------------------------
  * @encoder_block_sizes of aom_dsp/aom_dsp_rtcd_defs.pl:42-58. */
