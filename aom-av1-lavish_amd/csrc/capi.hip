@@ -268,21 +268,37 @@ static void fwd2d_shim(int tx_size, const int16_t* input, int32_t* output, int s
     abort();
   }
   hipStream_t s = shim_stream();
-  const size_t in_bytes = (size_t)H * stride * sizeof(int16_t);
+  const int n = max_eob(tx_size);
+  const size_t in_bytes = (size_t)H * W * sizeof(int16_t);
   const size_t in_pad = (in_bytes + 255) & ~(size_t)255;
-  char* scratch = (char*)shim_scratch(in_pad + (size_t)W * H * sizeof(int32_t));
+  char* scratch = (char*)shim_scratch(in_pad + (size_t)n * sizeof(int32_t));
   int16_t* din = (int16_t*)scratch;
   int32_t* dout = (int32_t*)(scratch + in_pad);
-  LAVISH_CHECK(hipMemcpyAsync(din, input, in_bytes, hipMemcpyHostToDevice, s));
-  const int rc = txq_plane(din, stride, W, H, tx_size, 1u << tx_type, 8, LAVISH_QUANT_NONE,
-                           nullptr, nullptr, nullptr, nullptr, dout, s);
+  // only the H x W window of the caller's rows is read
+  LAVISH_CHECK(hipMemcpy2DAsync(din, (size_t)W * sizeof(int16_t), input,
+                                (size_t)stride * sizeof(int16_t), (size_t)W * sizeof(int16_t), H,
+                                hipMemcpyHostToDevice, s));
+  const int rc = txq_plane(din, W, W, H, tx_size, 1u << tx_type, 8, LAVISH_QUANT_NONE, nullptr,
+                           nullptr, nullptr, nullptr, dout, s);
   if (rc != 0) {
     fprintf(stderr, "[lavish_hip] txq_plane rejected tx_size %d (rc %d)\n", tx_size, rc);
     abort();
   }
-  LAVISH_CHECK(hipMemcpyAsync(output, dout, (size_t)W * H * sizeof(int32_t),
-                              hipMemcpyDeviceToHost, s));
+  LAVISH_CHECK(hipMemcpyAsync(output, dout, (size_t)n * sizeof(int32_t), hipMemcpyDeviceToHost,
+                              s));
   LAVISH_CHECK(hipStreamSynchronize(s));
+  // 64-point sizes: the reference zeroes and re-packs in place
+  // (av1_fwd_txfm2d.c:248-311), which leaves, past the n packed words, the
+  // original copies of columns KW/2..KW-1 (rows < 32) of a 64-high buffer
+  // and zeros everywhere else.
+  for (int pos = n; pos < W * H; ++pos) {
+    int32_t v = 0;
+    if (H == 64) {
+      const int c = pos / 64, r = pos % 64;
+      if (c < (W < 32 ? W : 32) && r < 32) v = output[c * 32 + r];
+    }
+    output[pos] = v;
+  }
 }
 
 #define FWD2D_SHIM(w, h, sz)                                                          \
@@ -292,6 +308,11 @@ static void fwd2d_shim(int tx_size, const int16_t* input, int32_t* output, int s
     fwd2d_shim(sz, input, output, stride, tx_type);                                   \
   }
 FWD2D_SHIM(4, 4, 0)
+FWD2D_SHIM(64, 64, 4)
+FWD2D_SHIM(32, 64, 11)
+FWD2D_SHIM(64, 32, 12)
+FWD2D_SHIM(16, 64, 17)
+FWD2D_SHIM(64, 16, 18)
 FWD2D_SHIM(8, 8, 1)
 FWD2D_SHIM(16, 16, 2)
 FWD2D_SHIM(32, 32, 3)

@@ -36,6 +36,12 @@ const int16_t* host_iscan(int tx_size, int tx_type);
 const int16_t* dev_iscan(int tx_size, int tx_type);
 const int16_t* dev_scan(int tx_size, int tx_type);
 
+// lavish_txq_plane for the 64-point TX sizes (rdo.hip)
+int txq_plane_64(const int16_t* residual, int stride, int width, int height, int tx_size,
+                 uint32_t type_mask, int bd, int quant_kind, const LavishQuantParams* qp,
+                 int32_t* qcoeff, int32_t* dqcoeff, uint16_t* eob, int32_t* coeff,
+                 hipStream_t s);
+
 // per-thread scratch device buffer for the per-call (host pointer) shims
 void* shim_scratch(size_t bytes);
 hipStream_t shim_stream();

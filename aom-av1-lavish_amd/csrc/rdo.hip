@@ -1,0 +1,463 @@
+// rdo.hip -- C4: fused per-block TX-type RDO for gfx950, and the 64-point
+// forward transform sizes.
+//
+// Per TX block and candidate TX type (the body of
+// search_tx_type, av1/encoder/tx_search.c:2148-2312, with TX-domain
+// distortion):
+//   aom_highbd_subtract_block (aom_dsp/subtract.c:38-54)
+//   -> av1_fwd_txfm2d_WxH (av1/encoder/av1_fwd_txfm2d.c:56-312, 64-point
+//      sizes zeroed + re-packed to the 32x32 quadrant)
+//   -> av1_highbd_quantize_fp (av1/encoder/av1_quantize.c:125-198,565-577)
+//   -> aom_satd on the coefficients (aom_dsp/avg.c:509-516)
+//   -> dist_block_tx_domain: av1_highbd_block_error, RIGHT_SIGNED_SHIFT by
+//      (MAX_TX_SCALE - tx_scale) * 2 (tx_search.c:1077-1116)
+//   -> rate_estimator (av1/encoder/tpl_model.c:214-226, DCT_DCT scan)
+//   -> RDCOST(rdmult, rate, dist) (av1/encoder/rd.h:31-33)
+// and the block keeps the first type with the strictly smallest cost (the
+// `<` test of tx_search.c:2246).  Output per block: the decision record and
+// the winning qcoeff / dqcoeff.
+//
+// Mode 0 of the same kernel is the plain lavish_txq_plane contract (every
+// type's qcoeff / dqcoeff / eob) for the 64-point sizes, which txq.hip does
+// not instantiate.
+//
+// Layout per wave: P = 64 / min(W,H) blocks.  Column pass: one column per
+// lane (registers) -> LDS.  Row pass: only the KH = min(H,32) rows that
+// survive the 64-point zeroing are transformed, one per lane; the lane then
+// holds the row's KW = min(W,32) kept coefficients, quantizes them and
+// contributes to the block reductions (xor shuffles over the KH lanes of the
+// block).  The FAST 24-bit path is certified for |residual| <= 1023 for every
+// size including the 64-point ones (tools/range_analysis.py).
+#include "lavish_internal.h"
+#include "quant_dev.h"
+
+namespace lavish {
+
+struct RdoArgs {
+  const int16_t* res;    // mode 0: residual plane
+  const uint16_t* src;   // mode 1: source / prediction planes (u16)
+  const uint16_t* pred;
+  int stride;
+  int bw, nblocks;
+  int ntypes;
+  int types[16];
+  int bd;
+  int quant_kind;  // mode 0
+  int highbd;      // mode 0
+  int rdmult;      // mode 1
+  QP qp;
+  const int16_t* iscan_type[16];  // per slot: inverse scan of the type (n)
+  const int16_t* iscan_dct;       // DCT_DCT inverse scan (rate_estimator)
+  int32_t* qcoeff;
+  int32_t* dqcoeff;
+  uint16_t* eob;
+  int32_t* coeff;
+  LavishRdoBlock* out;
+};
+
+namespace {
+
+template <int W, int H>
+struct RTile {
+  static constexpr int MN = W < H ? W : H;
+  static constexpr int P = 64 / MN;
+  static constexpr int CPT = W / MN;
+  static constexpr int KW = W > 32 ? 32 : W;
+  static constexpr int KH = H > 32 ? 32 : H;
+  static constexpr int NC = KW * KH;                 // coefficients kept per block
+  static constexpr int RPT = (P * KH + 63) / 64;     // kept rows per lane
+  static constexpr int T1S = W + 1;
+  static constexpr int T1 = P * KH * T1S;
+  static constexpr int T2 = P * NC;
+};
+
+__device__ __forceinline__ int get_msb(uint32_t n) { return 31 - __builtin_clz(n); }
+
+template <int W, int H, int MODE, bool FAST, int QK, bool HBD>
+__device__ __forceinline__ void rdo_types(const RdoArgs& a, const int32_t (&res)[RTile<W, H>::CPT][H],
+                                          int32_t* t1, int32_t* t2, int32_t* tb, int lane,
+                                          int blk0, int nvalid) {
+  using C = TxCfg<W, H>;
+  using T = RTile<W, H>;
+  constexpr int NC = T::NC, KW = T::KW, KH = T::KH, T1S = T::T1S;
+  constexpr int LS = C::log_scale;
+  // per (row-pass slot k) running best of the block that slot belongs to
+  int64_t best_rd[T::RPT], best_dist[T::RPT], best_sse[T::RPT];
+  int best_type[T::RPT], best_eob[T::RPT], best_rate[T::RPT], best_satd[T::RPT];
+#pragma unroll
+  for (int k = 0; k < T::RPT; ++k) {
+    best_rd[k] = INT64_MAX;
+    best_dist[k] = best_sse[k] = 0;
+    best_type[k] = best_eob[k] = best_rate[k] = best_satd[k] = 0;
+  }
+
+  for (int ti = 0; ti < a.ntypes; ++ti) {
+    const int t = __builtin_amdgcn_readfirstlane(a.types[ti]);
+    const int vt = (kVtxPacked >> (2 * t)) & 3, ht = (kHtxPacked >> (2 * t)) & 3;
+    const int kc = vt == 3 ? 2 : (vt == 0 ? 0 : 1);
+    const int kr = ht == 3 ? 2 : (ht == 0 ? 0 : 1);
+    const bool ud = vt == 2, lr = ht == 2;
+    const int16_t* iscan = a.iscan_type[ti];
+
+    // ---- columns (av1_fwd_txfm2d.c:88-106); only rows < KH are kept ----
+#pragma unroll
+    for (int k = 0; k < T::CPT; ++k) {
+      const int j = k * 64 + lane;
+      const int b = j / W, c = j % W;
+      int32_t in[H], out[H];
+#pragma unroll
+      for (int r = 0; r < H; ++r) {
+        const int32_t x = ud ? res[k][H - 1 - r] : res[k][r];
+        if constexpr (FAST) in[r] = x * (1 << C::s0);
+        else in[r] = round_shift_1<-C::s0>(x);
+      }
+      fwd_1d<H, C::cos_bit_col, FAST>(kc, in, out);
+      const int cc = lr ? W - 1 - c : c;
+#pragma unroll
+      for (int r = 0; r < KH; ++r) t1[(b * KH + r) * T1S + cc] = round_shift_1<-C::s1>(out[r]);
+    }
+    wave_sync();
+
+    // ---- kept rows + quantization + per-block statistics ----
+#pragma unroll
+    for (int k = 0; k < T::RPT; ++k) {
+      const int j = k * 64 + lane;
+      const int b = j / KH, r = j % KH;
+      const bool live = b < T::P;
+      const int bb = live ? b : 0;
+      int32_t in[W], out[W];
+#pragma unroll
+      for (int c = 0; c < W; ++c) in[c] = t1[(bb * KH + r) * T1S + c];
+      fwd_1d<W, C::cos_bit_row, FAST>(kr, in, out);
+      int32_t q[KW];
+      int last = 0, satd = 0;
+      int64_t err = 0, sse = 0;
+      const size_t obase = ((size_t)ti * a.nblocks + blk0 + bb) * NC;
+#pragma unroll
+      for (int c = 0; c < KW; ++c) {
+        int32_t v = round_shift_1<-C::s2>(out[c]);
+        if constexpr (C::rect2) v = rshift64((int64_t)v * 5793, 12);
+        const int rc = c * KH + r;
+        const bool ac = c != 0 || r != 0;
+        if constexpr (MODE == 0 && QK == LAVISH_QUANT_NONE) {
+          q[c] = 0;
+          if (live && bb < nvalid) a.coeff[obase + rc] = v;
+        } else {
+          if constexpr (MODE == 0) {
+            if (a.coeff != nullptr && live && bb < nvalid) a.coeff[obase + rc] = v;
+          }
+          q[c] = quant_one<LS, QK, HBD>(v, ac, a.qp);
+        }
+        if constexpr (MODE == 1) {
+          const int32_t dq = dequant_one<LS>(q[c], ac, a.qp);
+          const int64_t d = (int64_t)v - dq;
+          err += d * d;
+          sse += (int64_t)v * v;
+          satd += abs(v);
+        }
+        if (live) t2[bb * NC + rc] = q[c];
+        last = q[c] != 0 ? max(last, iscan[rc] + 1) : last;
+      }
+#pragma unroll
+      for (int m = 1; m < KH; m <<= 1) last = max(last, __shfl_xor(last, m));
+      if constexpr (MODE == 0) {
+        if (r == 0 && live && bb < nvalid && a.eob != nullptr)
+          a.eob[(size_t)ti * a.nblocks + blk0 + bb] = (uint16_t)last;
+      } else {
+        // rate_estimator: positions of the DCT_DCT scan below eob
+        int rate = 0;
+#pragma unroll
+        for (int c = 0; c < KW; ++c) {
+          const int rc = c * KH + r;
+          const uint32_t al = (uint32_t)abs(q[c]);
+          if (a.iscan_dct[rc] < last) rate += get_msb(al + 1) + 1 + (al > 0);
+        }
+#pragma unroll
+        for (int m = 1; m < KH; m <<= 1) {
+          rate += __shfl_xor(rate, m);
+          satd += __shfl_xor(satd, m);
+          err += __shfl_xor(err, m);
+          sse += __shfl_xor(sse, m);
+        }
+        rate = (rate + 1) << 9;  // AV1_PROB_COST_SHIFT
+        // av1_highbd_block_error rounding, then the TX-domain shift
+        const int sh = 2 * (a.bd - 8);
+        if (sh > 0) {
+          const int64_t rnd = (int64_t)1 << (sh - 1);
+          err = (err + rnd) >> sh;
+          sse = (sse + rnd) >> sh;
+        }
+        constexpr int dshift = (1 - LS) * 2;  // (MAX_TX_SCALE - tx_scale) * 2
+        int64_t dist, dsse;
+        if constexpr (dshift >= 0) {
+          dist = err >> dshift;
+          dsse = sse >> dshift;
+        } else {
+          dist = err << -dshift;
+          dsse = sse << -dshift;
+        }
+        const int64_t rd = (((int64_t)rate * a.rdmult + 256) >> 9) + dist * 128;
+        if (rd < best_rd[k]) {
+          best_rd[k] = rd;
+          best_dist[k] = dist;
+          best_sse[k] = dsse;
+          best_type[k] = t;
+          best_eob[k] = last;
+          best_rate[k] = rate;
+          best_satd[k] = satd;
+#pragma unroll
+          for (int c = 0; c < KW; ++c)
+            if (live) tb[bb * NC + c * KH + r] = q[c];
+        }
+      }
+    }
+    wave_sync();
+
+    if constexpr (MODE == 0) {
+      // coalesced copy-out of this type's qcoeff / dqcoeff
+      if (a.qcoeff != nullptr) {
+        const int total = nvalid * NC;
+        const size_t gbase = ((size_t)ti * a.nblocks + blk0) * NC;
+        for (int i = lane * 4; i < total; i += 64 * 4) {
+          const v4i q4 = *reinterpret_cast<const v4i*>(&t2[i]);
+          __builtin_nontemporal_store(q4, reinterpret_cast<v4i*>(&a.qcoeff[gbase + i]));
+          if (a.dqcoeff != nullptr) {
+            const int rc0 = i % NC;
+            v4i d4;
+            d4.x = dequant_one<LS>(q4.x, rc0 != 0, a.qp);
+            d4.y = dequant_one<LS>(q4.y, 1, a.qp);
+            d4.z = dequant_one<LS>(q4.z, 1, a.qp);
+            d4.w = dequant_one<LS>(q4.w, 1, a.qp);
+            __builtin_nontemporal_store(d4, reinterpret_cast<v4i*>(&a.dqcoeff[gbase + i]));
+          }
+        }
+      }
+      wave_sync();
+    }
+  }
+
+  if constexpr (MODE == 1) {
+    // decision records (one lane per block) and the winner's coefficients
+#pragma unroll
+    for (int k = 0; k < T::RPT; ++k) {
+      const int j = k * 64 + lane;
+      const int b = j / KH, r = j % KH;
+      if (b < T::P && b < nvalid && r == 0) {
+        LavishRdoBlock o;
+        o.best_type = best_type[k];
+        o.eob = best_eob[k];
+        o.rate = best_rate[k];
+        o.satd = best_satd[k];
+        o.dist = best_dist[k];
+        o.sse = best_sse[k];
+        o.rdcost = best_rd[k];
+        a.out[blk0 + b] = o;
+      }
+    }
+    const int total = nvalid * NC;
+    const size_t gbase = (size_t)blk0 * NC;
+    for (int i = lane * 4; i < total; i += 64 * 4) {
+      const v4i q4 = *reinterpret_cast<const v4i*>(&tb[i]);
+      __builtin_nontemporal_store(q4, reinterpret_cast<v4i*>(&a.qcoeff[gbase + i]));
+      const int rc0 = i % NC;
+      v4i d4;
+      d4.x = dequant_one<LS>(q4.x, rc0 != 0, a.qp);
+      d4.y = dequant_one<LS>(q4.y, 1, a.qp);
+      d4.z = dequant_one<LS>(q4.z, 1, a.qp);
+      d4.w = dequant_one<LS>(q4.w, 1, a.qp);
+      __builtin_nontemporal_store(d4, reinterpret_cast<v4i*>(&a.dqcoeff[gbase + i]));
+    }
+  }
+}
+
+// one wave = one tile of P blocks; 64-thread workgroups (LDS per tile is up
+// to ~20 KB for the 64-point sizes)
+template <int W, int H, int MODE>
+__global__ __launch_bounds__(64) void rdo_kernel(RdoArgs a) {
+  using T = RTile<W, H>;
+  __shared__ int32_t t1[T::T1];
+  __shared__ __attribute__((aligned(16))) int32_t t2[T::T2];
+  __shared__ __attribute__((aligned(16))) int32_t tb[MODE == 1 ? T::T2 : 4];
+
+  const int lane = threadIdx.x;
+  const int blk0 = blockIdx.x * T::P;
+  if (blk0 >= a.nblocks) return;
+  const int nvalid = min(T::P, a.nblocks - blk0);
+
+  int32_t res[T::CPT][H];
+  int32_t amax = 0;
+#pragma unroll
+  for (int k = 0; k < T::CPT; ++k) {
+    const int j = k * 64 + lane;
+    const int b = j / W, c = j % W;
+    const int blk = blk0 + b;
+    if (b < nvalid) {
+      const int by = blk / a.bw, bx = blk - by * a.bw;
+      const size_t off = (size_t)by * H * a.stride + (size_t)bx * W + c;
+#pragma unroll
+      for (int r = 0; r < H; ++r) {
+        int32_t v;
+        if constexpr (MODE == 0) v = a.res[off + (size_t)r * a.stride];
+        else v = (int32_t)a.src[off + (size_t)r * a.stride] - (int32_t)a.pred[off + (size_t)r * a.stride];
+        res[k][r] = v;
+        amax = max(amax, abs(v));
+      }
+    } else {
+#pragma unroll
+      for (int r = 0; r < H; ++r) res[k][r] = 0;
+    }
+  }
+  const bool fast = __builtin_amdgcn_ballot_w64(amax > kFastResidualMax) == 0;
+  if constexpr (MODE == 1) {
+    if (fast) rdo_types<W, H, 1, true, LAVISH_QUANT_FP, true>(a, res, t1, t2, tb, lane, blk0, nvalid);
+    else rdo_types<W, H, 1, false, LAVISH_QUANT_FP, true>(a, res, t1, t2, tb, lane, blk0, nvalid);
+  } else {
+#define LAVISH_RDO_RUN(F, Q, HB) rdo_types<W, H, 0, F, Q, HB>(a, res, t1, t2, tb, lane, blk0, nvalid)
+    if (a.quant_kind == LAVISH_QUANT_NONE) {
+      if (fast) LAVISH_RDO_RUN(true, LAVISH_QUANT_NONE, false);
+      else LAVISH_RDO_RUN(false, LAVISH_QUANT_NONE, false);
+    } else if (a.quant_kind == LAVISH_QUANT_FP) {
+      if (a.highbd) {
+        if (fast) LAVISH_RDO_RUN(true, LAVISH_QUANT_FP, true);
+        else LAVISH_RDO_RUN(false, LAVISH_QUANT_FP, true);
+      } else {
+        if (fast) LAVISH_RDO_RUN(true, LAVISH_QUANT_FP, false);
+        else LAVISH_RDO_RUN(false, LAVISH_QUANT_FP, false);
+      }
+    } else {
+      if (a.highbd) {
+        if (fast) LAVISH_RDO_RUN(true, LAVISH_QUANT_B, true);
+        else LAVISH_RDO_RUN(false, LAVISH_QUANT_B, true);
+      } else {
+        if (fast) LAVISH_RDO_RUN(true, LAVISH_QUANT_B, false);
+        else LAVISH_RDO_RUN(false, LAVISH_QUANT_B, false);
+      }
+    }
+#undef LAVISH_RDO_RUN
+  }
+}
+
+template <int W, int H, int MODE>
+void launch_rdo(const RdoArgs& a, hipStream_t s) {
+  const int grid = (a.nblocks + RTile<W, H>::P - 1) / RTile<W, H>::P;
+  if (grid == 0) return;
+  hipLaunchKernelGGL((rdo_kernel<W, H, MODE>), dim3(grid), dim3(64), 0, s, a);
+  LAVISH_CHECK(hipGetLastError());
+}
+
+template <int MODE>
+int launch_size(int tx_size, const RdoArgs& a, hipStream_t s) {
+  switch (tx_size) {
+    case 4: launch_rdo<64, 64, MODE>(a, s); return 0;
+    case 11: launch_rdo<32, 64, MODE>(a, s); return 0;
+    case 12: launch_rdo<64, 32, MODE>(a, s); return 0;
+    case 17: launch_rdo<16, 64, MODE>(a, s); return 0;
+    case 18: launch_rdo<64, 16, MODE>(a, s); return 0;
+    default: break;
+  }
+  if constexpr (MODE == 1) {
+    switch (tx_size) {
+      case 0: launch_rdo<4, 4, 1>(a, s); return 0;
+      case 1: launch_rdo<8, 8, 1>(a, s); return 0;
+      case 2: launch_rdo<16, 16, 1>(a, s); return 0;
+      case 3: launch_rdo<32, 32, 1>(a, s); return 0;
+      case 5: launch_rdo<4, 8, 1>(a, s); return 0;
+      case 6: launch_rdo<8, 4, 1>(a, s); return 0;
+      case 7: launch_rdo<8, 16, 1>(a, s); return 0;
+      case 8: launch_rdo<16, 8, 1>(a, s); return 0;
+      case 9: launch_rdo<16, 32, 1>(a, s); return 0;
+      case 10: launch_rdo<32, 16, 1>(a, s); return 0;
+      case 13: launch_rdo<4, 16, 1>(a, s); return 0;
+      case 14: launch_rdo<16, 4, 1>(a, s); return 0;
+      case 15: launch_rdo<8, 32, 1>(a, s); return 0;
+      case 16: launch_rdo<32, 8, 1>(a, s); return 0;
+      default: break;
+    }
+  }
+  return -2;
+}
+
+int fill_types(RdoArgs& a, int tx_size, uint32_t type_mask) {
+  a.ntypes = 0;
+  for (int t = 0; t < 16; ++t) {
+    if (!((type_mask >> t) & 1)) continue;
+    if (!tx_type_valid(tx_size, t)) return -5;
+    a.iscan_type[a.ntypes] = dev_iscan(tx_size, t);
+    a.types[a.ntypes++] = t;
+  }
+  return a.ntypes == 0 ? -5 : 0;
+}
+
+QP qp_of(const LavishQuantParams* p) {
+  QP q{};
+  for (int i = 0; i < 2; ++i) {
+    q.zbin[i] = p->zbin[i];
+    q.round[i] = p->round[i];
+    q.quant[i] = p->quant[i];
+    q.quant_shift[i] = p->quant_shift[i];
+    q.dequant[i] = p->dequant[i];
+  }
+  return q;
+}
+
+}  // namespace
+
+// lavish_txq_plane for the 64-point sizes (called from txq.hip)
+int txq_plane_64(const int16_t* residual, int stride, int width, int height, int tx_size,
+                 uint32_t type_mask, int bd, int quant_kind, const LavishQuantParams* qp,
+                 int32_t* qcoeff, int32_t* dqcoeff, uint16_t* eob, int32_t* coeff,
+                 hipStream_t s) {
+  const int W = tx_w(tx_size), H = tx_h(tx_size);
+  RdoArgs a{};
+  a.res = residual;
+  a.stride = stride;
+  a.bw = width / W;
+  a.nblocks = (width / W) * (height / H);
+  const int rc = fill_types(a, tx_size, type_mask);
+  if (rc) return rc;
+  a.bd = bd;
+  a.quant_kind = quant_kind;
+  a.highbd = bd > 8;
+  if (qp) a.qp = qp_of(qp);
+  a.qcoeff = qcoeff;
+  a.dqcoeff = dqcoeff;
+  a.eob = eob;
+  a.coeff = coeff;
+  return launch_size<0>(tx_size, a, s);
+}
+
+int rdo_plane(const uint16_t* src, const uint16_t* pred, int stride, int width, int height,
+              int tx_size, uint32_t type_mask, int bd, const LavishQuantParams* qp, int rdmult,
+              LavishRdoBlock* out, int32_t* qcoeff, int32_t* dqcoeff, hipStream_t s) {
+  if (tx_size < 0 || tx_size >= 19) return -1;
+  if (qp == nullptr || out == nullptr || qcoeff == nullptr || dqcoeff == nullptr) return -3;
+  if (bd != 8 && bd != 10 && bd != 12) return -3;
+  const int W = tx_w(tx_size), H = tx_h(tx_size);
+  if (width <= 0 || height <= 0 || stride < width) return -4;
+  RdoArgs a{};
+  a.src = src;
+  a.pred = pred;
+  a.stride = stride;
+  a.bw = width / W;
+  a.nblocks = (width / W) * (height / H);
+  const int rc = fill_types(a, tx_size, type_mask);
+  if (rc) return rc;
+  a.bd = bd;
+  a.rdmult = rdmult;
+  a.qp = qp_of(qp);
+  a.iscan_dct = dev_iscan(tx_size, 0);
+  a.out = out;
+  a.qcoeff = qcoeff;
+  a.dqcoeff = dqcoeff;
+  return launch_size<1>(tx_size, a, s);
+}
+
+}  // namespace lavish
+
+extern "C" int lavish_rdo_plane(const uint16_t* src, const uint16_t* pred, int stride, int width,
+                                int height, int tx_size, uint32_t type_mask, int bit_depth,
+                                const LavishQuantParams* qp, int rdmult, LavishRdoBlock* out,
+                                int32_t* qcoeff, int32_t* dqcoeff, void* stream) {
+  return lavish::rdo_plane(src, pred, stride, width, height, tx_size, type_mask, bit_depth, qp,
+                           rdmult, out, qcoeff, dqcoeff, (hipStream_t)stream);
+}

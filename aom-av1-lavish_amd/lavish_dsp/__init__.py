@@ -106,11 +106,10 @@ _lib.lavish_quantize_batch.restype = _i32
 
 _FWD2D = {}
 for _s, _name in enumerate(TX_SIZES):
-    if TX_W[_s] <= 32 and TX_H[_s] <= 32:
-        f = getattr(_lib, "av1_fwd_txfm2d_%s_hip" % _name)
-        f.argtypes = [_vp, _vp, _i32, ctypes.c_uint8, _i32]
-        f.restype = None
-        _FWD2D[_s] = f
+    f = getattr(_lib, "av1_fwd_txfm2d_%s_hip" % _name)
+    f.argtypes = [_vp, _vp, _i32, ctypes.c_uint8, _i32]
+    f.restype = None
+    _FWD2D[_s] = f
 _lib.av1_lowbd_fwd_txfm_hip.argtypes = [_vp, _vp, _i32, ctypes.POINTER(TxfmParam)]
 
 _QARGS = [_vp, ctypes.c_ssize_t, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]
@@ -349,3 +348,47 @@ def inv_txfm_add_batch(dqcoeff, tx_size, jobs, dst, bit_depth=8, stream=None):
                                         bit_depth, int(highbd), _stream_ptr(stream))
     if rc != 0:
         raise ValueError("lavish_inv_txfm_add_batch rejected its arguments (rc=%d)" % rc)
+
+
+# ---------------------------------------------------------------- C4 RDO --
+RDO_DTYPE = np.dtype([("best_type", "<i4"), ("eob", "<i4"), ("rate", "<i4"), ("satd", "<i4"),
+                      ("dist", "<i8"), ("sse", "<i8"), ("rdcost", "<i8")], align=True)
+assert RDO_DTYPE.itemsize == 40
+_lib.lavish_rdo_plane.argtypes = [_vp, _vp, _i32, _i32, _i32, _i32, ctypes.c_uint32, _i32,
+                                  ctypes.POINTER(QuantParams), _i32, _vp, _vp, _vp, _vp]
+_lib.lavish_rdo_plane.restype = _i32
+
+
+def rdo_out(src, tx_size):
+    """Output tensors of rdo_plane for a u16 plane (stored as int16)."""
+    import torch
+    H, W = src.shape
+    nb = (W // TX_W[tx_size]) * (H // TX_H[tx_size])
+    n = max_eob(tx_size)
+    dev = src.device
+    return {"records": torch.empty(nb * RDO_DTYPE.itemsize, dtype=torch.uint8, device=dev),
+            "qcoeff": torch.empty((nb, n), dtype=torch.int32, device=dev),
+            "dqcoeff": torch.empty((nb, n), dtype=torch.int32, device=dev)}
+
+
+def rdo_plane(src, pred, tx_size, type_mask, qp, rdmult, bit_depth=10, out=None, stream=None):
+    """lavish_rdo_plane (C4) on device u16 planes held as int16 tensors."""
+    import torch
+    assert src.dtype == torch.int16 and pred.dtype == torch.int16
+    assert src.shape == pred.shape and src.stride(1) == 1 and pred.stride(0) == src.stride(0)
+    H, W = src.shape
+    if out is None:
+        out = rdo_out(src, tx_size)
+    rc = _lib.lavish_rdo_plane(ctypes.c_void_p(src.data_ptr()), ctypes.c_void_p(pred.data_ptr()),
+                               src.stride(0), W, H, tx_size, type_mask, bit_depth,
+                               ctypes.byref(qp), rdmult,
+                               ctypes.c_void_p(out["records"].data_ptr()),
+                               ctypes.c_void_p(out["qcoeff"].data_ptr()),
+                               ctypes.c_void_p(out["dqcoeff"].data_ptr()), _stream_ptr(stream))
+    if rc != 0:
+        raise ValueError("lavish_rdo_plane rejected its arguments (rc=%d)" % rc)
+    return out
+
+
+def rdo_records(out):
+    return out["records"].cpu().numpy().view(RDO_DTYPE)

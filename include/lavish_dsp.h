@@ -97,6 +97,8 @@ const int16_t *lavish_iscan(int tx_size, int tx_type);
  * av1/encoder/encodemb.c:295-341).
  *   residual : int16 plane, `stride` elements per row, width x height.
  *   blocks   : B = (width / W) * (height / H), raster order (full blocks).
+ *   tx_size  : any of the 19 sizes; the 64-point ones keep the reference's
+ *              packed 32x32 (or 32x16 / 16x32) low-frequency quadrant.
  *   slots    : the set bits of type_mask in ascending TX_TYPE order; every
  *              set type must be valid for tx_size (EXT_TX_SET rules).
  *   outputs  : qcoeff/dqcoeff[slot][block][n], eob[slot][block], with
@@ -223,6 +225,31 @@ int lavish_inv_txfm_add_batch(const int32_t *dqcoeff, int tx_size,
                               int dst_stride, int bit_depth, int highbd,
                               void *stream);
 
+/* ---- C4: fused TX-type RDO ----------------------------------------------
+ * For every full tx_size block of (src - pred) (u16 planes, bit_depth 8/10/12)
+ * and every TX type in type_mask: forward transform -> av1_highbd_quantize_fp
+ * -> aom_satd(coeff) -> av1_highbd_block_error -> TX-domain distortion shift
+ * (tx_search.c:1077-1116) -> rate_estimator (tpl_model.c:214-226) ->
+ * RDCOST(rdmult, rate, dist) (rd.h:31-33); the block keeps the first type
+ * with the strictly lowest cost.  Outputs per block (raster order): the
+ * decision record and the winner's qcoeff / dqcoeff (n words each,
+ * n = av1_get_max_eob). */
+typedef struct LavishRdoBlock {
+  int32_t best_type;
+  int32_t eob;
+  int32_t rate;   /* rate_estimator (<< AV1_PROB_COST_SHIFT) */
+  int32_t satd;   /* aom_satd of the winner's coefficients */
+  int64_t dist;   /* TX-domain distortion after the tx-scale shift */
+  int64_t sse;
+  int64_t rdcost;
+} LavishRdoBlock;
+
+int lavish_rdo_plane(const uint16_t *src, const uint16_t *pred, int stride,
+                     int width, int height, int tx_size, uint32_t type_mask,
+                     int bit_depth, const LavishQuantParams *qp, int rdmult,
+                     LavishRdoBlock *out, int32_t *qcoeff, int32_t *dqcoeff,
+                     void *stream);
+
 /* ---- C3: DIAMOND full-pixel motion search ------------------------------
  * av1_full_pixel_search with search_method DIAMOND (av1/encoder/mcomp.c:
  * 1755-1895 -> full_pixel_diamond :1479-1526 -> diamond_search_sad
@@ -261,11 +288,18 @@ int lavish_diamond_search_batch(const uint8_t *src, int src_stride,
 /* ------------------------------------------------------------------------ */
 /* Per-call RTCD shims (host pointers)                                      */
 /* ------------------------------------------------------------------------ */
-/* av1_fwd_txfm2d_WxH (av1/common/av1_rtcd_defs.pl:358-399) */
+/* av1_fwd_txfm2d_WxH (av1/common/av1_rtcd_defs.pl:358-399); the 64-point
+ * sizes reproduce the reference's in-place zero + re-pack of the whole W*H
+ * output buffer (av1/encoder/av1_fwd_txfm2d.c:240-311). */
 #define LAVISH_FWD2D(w, h)                                                   \
   void av1_fwd_txfm2d_##w##x##h##_hip(const int16_t *input, int32_t *output, \
                                       int stride, uint8_t tx_type, int bd);
 LAVISH_FWD2D(4, 4)
+LAVISH_FWD2D(64, 64)
+LAVISH_FWD2D(32, 64)
+LAVISH_FWD2D(64, 32)
+LAVISH_FWD2D(16, 64)
+LAVISH_FWD2D(64, 16)
 LAVISH_FWD2D(8, 8)
 LAVISH_FWD2D(16, 16)
 LAVISH_FWD2D(32, 32)

@@ -200,6 +200,16 @@ void orc_diamond_batch(const uint8_t *src, int src_stride, const uint8_t *ref,
                        long njobs, int step_param, int mv_cost_type,
                        int skip_sad, OrcDiamondResult *out, int threads);
 
+/* ---- C4: per-block TX-type RDO (oracle_rdo.c); layout = LavishRdoBlock */
+typedef struct OrcRdoBlock {
+  int32_t best_type, eob, rate, satd;
+  int64_t dist, sse, rdcost;
+} OrcRdoBlock;
+long orc_rdo_plane(const uint16_t *src, const uint16_t *pred, int stride,
+                   int width, int height, int tx_size, unsigned type_mask,
+                   int bd, const OrcQuant *q, int rdmult, OrcRdoBlock *out,
+                   int32_t *qcoeff, int32_t *dqcoeff, int threads);
+
 /* ---- C2 pipeline: fwd_txfm + quantize_fp over a residual plane ----
  * For one tx_size, tile the plane with full blocks (row-major block order),
  * evaluate each tx_type whose bit is set in type_mask (ascending type order),

@@ -1,0 +1,131 @@
+/* oracle_rdo.c -- TEST INFRASTRUCTURE ONLY (see oracle.h).
+ *
+ * CPU restatement of the C4 per-block TX-type RDO: for
+ * every full tx_size block of (src - pred) and every requested type:
+ *   aom_highbd_subtract_block      aom_dsp/subtract.c:38-54
+ *   av1_fwd_txfm2d_*               av1/encoder/av1_fwd_txfm2d.c:56-312
+ *   av1_highbd_quantize_fp         av1/encoder/av1_quantize.c:125-198,565-577
+ *   aom_satd                       aom_dsp/avg.c:509-516
+ *   av1_highbd_block_error         av1/encoder/rdopt.c:664-682
+ *   dist_block_tx_domain shift     av1/encoder/tx_search.c:1077-1116
+ *   rate_estimator                 av1/encoder/tpl_model.c:214-226
+ *   RDCOST                         av1/encoder/rd.h:31-33
+ * keeping the first type with the strictly lowest cost
+ * (tx_search.c:2246 `if (rd < best_rd)`).
+ */
+#include <pthread.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "oracle.h"
+
+static int get_msb(unsigned n) { return 31 - __builtin_clz(n); }
+
+/* rate_estimator (tpl_model.c:214-226): DCT_DCT scan of tx_size */
+static int rate_estimator(const int32_t *qcoeff, int eob, int tx_size) {
+  const int16_t *scan = orc_scan(tx_size, 0);
+  int rate_cost = 1;
+  for (int idx = 0; idx < eob; ++idx) {
+    const unsigned abs_level = (unsigned)abs(qcoeff[scan[idx]]);
+    rate_cost += get_msb(abs_level + 1) + 1 + (abs_level > 0);
+  }
+  return rate_cost << 9; /* AV1_PROB_COST_SHIFT */
+}
+
+typedef struct {
+  const uint16_t *src, *pred;
+  int stride, width, tx_size, bd, rdmult, row0, row1, ntypes;
+  int types[16];
+  const OrcQuant *q;
+  OrcRdoBlock *out;
+  int32_t *qcoeff, *dqcoeff;
+} RdoJob;
+
+static void *rdo_rows(void *arg) {
+  RdoJob *j = (RdoJob *)arg;
+  const int W = orc_tx_w(j->tx_size), H = orc_tx_h(j->tx_size);
+  const int bw = j->width / W;
+  const int n = orc_max_eob(j->tx_size);
+  const int ls = orc_tx_scale(j->tx_size);
+  const int shift = (1 - ls) * 2; /* (MAX_TX_SCALE - tx_scale) * 2 */
+  int16_t diff[64 * 64];
+  int32_t coeff[64 * 64], qc[4096], dq[4096];
+  for (int by = j->row0; by < j->row1; ++by) {
+    for (int bx = 0; bx < bw; ++bx) {
+      const long blk = (long)by * bw + bx;
+      const size_t off = (size_t)by * H * j->stride + (size_t)bx * W;
+      orc_highbd_subtract_block(H, W, diff, W, j->src + off, j->stride, j->pred + off,
+                                j->stride);
+      OrcRdoBlock best;
+      memset(&best, 0, sizeof(best));
+      best.rdcost = INT64_MAX;
+      for (int ti = 0; ti < j->ntypes; ++ti) {
+        const int t = j->types[ti];
+        orc_fwd_txfm2d(diff, coeff, W, t, j->tx_size, j->bd);
+        uint16_t eob;
+        orc_highbd_quantize_fp(coeff, n, j->q->zbin, j->q->round_fp, j->q->quant_fp,
+                               j->q->quant_shift, qc, dq, j->q->dequant, &eob,
+                               orc_scan(j->tx_size, t), orc_iscan(j->tx_size, t), ls);
+        const int satd = orc_satd(coeff, n);
+        int64_t ssz;
+        int64_t err = orc_highbd_block_error(coeff, dq, n, &ssz, j->bd);
+        /* RIGHT_SIGNED_SHIFT (aom_ports/mem.h:69-70) */
+        const int64_t dist = shift < 0 ? err << -shift : err >> shift;
+        const int64_t sse = shift < 0 ? ssz << -shift : ssz >> shift;
+        const int rate = rate_estimator(qc, eob, j->tx_size);
+        const int64_t rd = ((((int64_t)rate) * j->rdmult + 256) >> 9) + dist * 128;
+        if (rd < best.rdcost) {
+          best.best_type = t;
+          best.eob = eob;
+          best.rate = rate;
+          best.satd = satd;
+          best.dist = dist;
+          best.sse = sse;
+          best.rdcost = rd;
+          memcpy(j->qcoeff + blk * n, qc, sizeof(int32_t) * n);
+          memcpy(j->dqcoeff + blk * n, dq, sizeof(int32_t) * n);
+        }
+      }
+      j->out[blk] = best;
+    }
+  }
+  return NULL;
+}
+
+long orc_rdo_plane(const uint16_t *src, const uint16_t *pred, int stride, int width,
+                   int height, int tx_size, unsigned type_mask, int bd, const OrcQuant *q,
+                   int rdmult, OrcRdoBlock *out, int32_t *qcoeff, int32_t *dqcoeff,
+                   int threads) {
+  const int W = orc_tx_w(tx_size), H = orc_tx_h(tx_size);
+  const int bh = height / H;
+  RdoJob base;
+  memset(&base, 0, sizeof(base));
+  base.src = src;
+  base.pred = pred;
+  base.stride = stride;
+  base.width = width;
+  base.tx_size = tx_size;
+  base.bd = bd;
+  base.rdmult = rdmult;
+  base.q = q;
+  base.out = out;
+  base.qcoeff = qcoeff;
+  base.dqcoeff = dqcoeff;
+  for (int t = 0; t < 16; ++t)
+    if ((type_mask >> t) & 1) base.types[base.ntypes++] = t;
+  if (threads < 1) threads = 1;
+  if (threads > 64) threads = 64;
+  if (threads > bh) threads = bh > 0 ? bh : 1;
+  pthread_t tid[64];
+  RdoJob jobs[64];
+  for (int i = 0; i < threads; ++i) {
+    jobs[i] = base;
+    jobs[i].row0 = bh * i / threads;
+    jobs[i].row1 = bh * (i + 1) / threads;
+    if (threads > 1) pthread_create(&tid[i], NULL, rdo_rows, &jobs[i]);
+    else rdo_rows(&jobs[i]);
+  }
+  if (threads > 1)
+    for (int i = 0; i < threads; ++i) pthread_join(tid[i], NULL);
+  return (long)bh * (width / W);
+}

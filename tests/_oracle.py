@@ -374,3 +374,30 @@ def diamond_batch(src, ref, stride, w, h, jobs, step_param=0, mv_cost_type=3, sk
     L.orc_diamond_batch(P(src), stride, P(ref), stride, w, h, P(jobs), len(jobs), step_param,
                         mv_cost_type, int(skip), P(out), threads)
     return out
+
+
+# ------------------------------------------------------------- C4 RDO --
+RDO_DTYPE = np.dtype([("best_type", "<i4"), ("eob", "<i4"), ("rate", "<i4"), ("satd", "<i4"),
+                      ("dist", "<i8"), ("sse", "<i8"), ("rdcost", "<i8")], align=True)
+
+
+def rdo_plane(src, pred, tx_size, type_mask, bd, q, rdmult, threads=1):
+    """orc_rdo_plane over u16 planes of equal shape; returns (records,
+    qcoeff[block, n], dqcoeff[block, n])."""
+    L = lib()
+    L.orc_rdo_plane.restype = ctypes.c_long
+    L.orc_rdo_plane.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
+                                ctypes.c_int, ctypes.c_int, ctypes.c_uint, ctypes.c_int,
+                                ctypes.POINTER(OrcQuant), ctypes.c_int, ctypes.c_void_p,
+                                ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
+    src = np.ascontiguousarray(src, dtype=np.uint16)
+    pred = np.ascontiguousarray(pred, dtype=np.uint16)
+    H, W = src.shape
+    nb = (W // TX_W[tx_size]) * (H // TX_H[tx_size])
+    n = max_eob(tx_size)
+    out = np.zeros(nb, RDO_DTYPE)
+    qc = np.zeros((nb, n), np.int32)
+    dq = np.zeros((nb, n), np.int32)
+    L.orc_rdo_plane(P(src), P(pred), W, W, H, tx_size, type_mask, bd, ctypes.byref(q), rdmult,
+                    P(out), P(qc), P(dq), threads)
+    return out, qc, dq

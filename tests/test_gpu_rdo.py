@@ -1,0 +1,104 @@
+"""GPU parity of the 64-point forward transforms and of the C4 fused TX-type
+RDO (lavish_rdo_plane) against the oracle (oracle/oracle_txfm.c,
+oracle/oracle_rdo.c): coefficients, eobs, decision records (best type, eob,
+rate, satd, distortion, sse, rd cost) and the winner's qcoeff / dqcoeff, all
+bit-exact."""
+import numpy as np
+import pytest
+
+import _oracle as O
+
+pytestmark = pytest.mark.gpu
+
+SIZES64 = [4, 11, 12, 17, 18]
+
+
+@pytest.fixture(scope="module")
+def L():
+    import torch
+    assert torch.cuda.is_available()
+    import lavish_dsp
+    return lavish_dsp
+
+
+@pytest.mark.parametrize("s", SIZES64)
+def test_fwd_txfm2d_64_shims(L, s):
+    """Whole W*H output buffer, including the stale words the reference's
+    in-place zero + re-pack leaves behind."""
+    rng = np.random.default_rng(s)
+    W, H = O.TX_W[s], O.TX_H[s]
+    for lim in (255, 1023, 4095, 32767):
+        blk = rng.integers(-lim, lim + 1, size=(H, W + 3)).astype(np.int16)
+        exp = O.fwd_txfm2d(blk, 0, s)
+        got = np.full(W * H, 12345, np.int32)
+        getattr(L, "av1_fwd_txfm2d_" + L.TX_SIZES[s])(blk, got, W + 3, 0, 8)
+        np.testing.assert_array_equal(got, exp, err_msg="lim %d" % lim)
+
+
+@pytest.mark.parametrize("s", SIZES64)
+@pytest.mark.parametrize("bd,kind", [(8, 0), (8, 1), (10, 0), (12, 1)])
+def test_txq_plane_64(L, s, bd, kind):
+    import torch
+    import lavish_dsp.synth as synth
+    W, H = O.TX_W[s], O.TX_H[s]
+    res = synth.residual_plane(256, 192, bd, seed=s)
+    qp = L.build_quant_params(bd, 96, kind)
+    out = L.txq_plane(torch.from_numpy(res).cuda(), s, 1, qp, bit_depth=bd, quant_kind=kind)
+    qc, dq, eob = O.txq_plane(res, s, 1, O.build_quant(bd, 96), bd=bd, quant_b=bool(kind))
+    n = O.max_eob(s)
+    nb = (256 // W) * (192 // H)
+    np.testing.assert_array_equal(out["qcoeff"].cpu().numpy().reshape(nb, n), qc.reshape(nb, n))
+    np.testing.assert_array_equal(out["dqcoeff"].cpu().numpy().reshape(nb, n), dq.reshape(nb, n))
+    np.testing.assert_array_equal(out["eob"].cpu().numpy().view(np.uint16).reshape(-1),
+                                  eob.reshape(-1))
+
+
+def _planes(bd, seed, Wp=384, Hp=192):
+    import lavish_dsp.synth as synth
+    src = synth.frame(Wp, Hp, bd, seed)
+    pred = synth.shifted(synth.frame(Wp, Hp, bd, seed + 1), 3, -2)
+    return src.astype(np.uint16), pred.astype(np.uint16)
+
+
+# the C4 candidate set plus rectangular sizes
+C4_CASES = [(4, 0x1), (3, 0x201), (2, 0xFFFF), (1, 0xFFFF), (0, 0xFFFF), (5, 0xFFFF),
+            (9, 0x0201), (13, 0xFFFF), (16, 0x0201), (11, 0x1), (18, 0x1)]
+
+
+@pytest.mark.parametrize("s,mask", C4_CASES)
+@pytest.mark.parametrize("bd", [10, 8, 12])
+def test_rdo_plane_vs_oracle(L, s, mask, bd):
+    import torch
+    src, pred = _planes(bd, 40 + s)
+    q = O.build_quant(bd, 128)
+    qp = L.build_quant_params(bd, 128, L.QUANT_FP)
+    rdmult = 1234 + 17 * s
+    exp, eq, ed = O.rdo_plane(src, pred, s, mask, bd, q, rdmult, threads=8)
+    out = L.rdo_plane(torch.from_numpy(src.view(np.int16)).cuda(),
+                      torch.from_numpy(pred.view(np.int16)).cuda(), s, mask, qp, rdmult, bd)
+    got = L.rdo_records(out)
+    for f in ("best_type", "eob", "rate", "satd", "dist", "sse", "rdcost"):
+        np.testing.assert_array_equal(got[f], exp[f], err_msg=f)
+    np.testing.assert_array_equal(out["qcoeff"].cpu().numpy(), eq)
+    np.testing.assert_array_equal(out["dqcoeff"].cpu().numpy(), ed)
+    # more than one type wins somewhere when several are offered
+    if bin(mask).count("1") > 2:
+        assert len(np.unique(got["best_type"])) > 1
+
+
+def test_rdo_large_residual_exact_path(L):
+    """|src - pred| > 1023 (12-bit content) takes the exact 64-bit path."""
+    import torch
+    rng = np.random.default_rng(9)
+    src = rng.integers(0, 4096, size=(64, 128)).astype(np.uint16)
+    pred = rng.integers(0, 4096, size=(64, 128)).astype(np.uint16)
+    q = O.build_quant(12, 60)
+    qp = L.build_quant_params(12, 60, L.QUANT_FP)
+    for s, mask in ((2, 0xFFFF), (4, 1), (3, 0x201)):
+        exp, eq, ed = O.rdo_plane(src, pred, s, mask, 12, q, 4321)
+        out = L.rdo_plane(torch.from_numpy(src.view(np.int16)).cuda(),
+                          torch.from_numpy(pred.view(np.int16)).cuda(), s, mask, qp, 4321, 12)
+        got = L.rdo_records(out)
+        for f in ("best_type", "eob", "rate", "satd", "dist", "sse", "rdcost"):
+            np.testing.assert_array_equal(got[f], exp[f], err_msg=f)
+        np.testing.assert_array_equal(out["qcoeff"].cpu().numpy(), eq)

@@ -107,7 +107,10 @@ def one_d(st, kind, x, N, bit):
 SHIFT = {(4, 4): (2, 0, 0), (8, 8): (2, -1, 0), (16, 16): (2, -2, 0), (32, 32): (2, -4, 0),
          (4, 8): (2, -1, 0), (8, 4): (2, -1, 0), (8, 16): (2, -2, 0), (16, 8): (2, -2, 0),
          (16, 32): (2, -4, 0), (32, 16): (2, -4, 0), (4, 16): (2, -1, 0), (16, 4): (2, -1, 0),
-         (8, 32): (2, -2, 0), (32, 8): (2, -2, 0)}
+         (8, 32): (2, -2, 0), (32, 8): (2, -2, 0),
+         # 64-point sizes (DCT_DCT only; fwd_shift_* of av1_fwd_txfm2d.c)
+         (64, 64): (0, -2, -2), (32, 64): (0, -2, -2), (64, 32): (2, -4, -2),
+         (16, 64): (0, -2, 0), (64, 16): (2, -4, 0)}
 CBC = [[13, 13, 13, 0, 0], [13, 13, 13, 12, 0], [13, 13, 13, 12, 13], [0, 13, 13, 12, 13], [0, 0, 13, 12, 13]]
 CBR = [[13, 13, 12, 0, 0], [13, 13, 13, 12, 0], [13, 13, 12, 13, 12], [0, 12, 13, 12, 11], [0, 0, 12, 11, 10]]
 
@@ -118,12 +121,14 @@ def analyse(W, H, T):
     worst_row_in = 0
     for kc in (0, 1, 2):
         if kc == 1 and H > 16: continue
+        if kc != 0 and (W == 64 or H == 64): continue
         col = one_d(st, kc, [T << s0] * H, H, CBC[wl][hl])
         m = max(col)
         m = (m + (1 << -s1) - 1) >> -s1 if s1 < 0 else m
         worst_row_in = max(worst_row_in, m)
     for kr in (0, 1, 2):
         if kr == 1 and W > 16: continue
+        if kr != 0 and (W == 64 or H == 64): continue
         one_d(st, kr, [worst_row_in] * W, W, CBR[wl][hl])
     return st.op, st.sum
 
