@@ -42,6 +42,18 @@ int txq_plane_64(const int16_t* residual, int stride, int width, int height, int
                  int32_t* qcoeff, int32_t* dqcoeff, uint16_t* eob, int32_t* coeff,
                  hipStream_t s);
 
+// inverse transform batch (inv.hip)
+int inv_txfm_add_batch(const int32_t* dq, int tx_size, const LavishInvJob* jobs, int njobs,
+                       void* dst, int stride, int bd, int highbd, hipStream_t s);
+int rdo_plane(const uint16_t* src, const uint16_t* pred, int stride, int width, int height,
+              int tx_size, uint32_t type_mask, int bd, const LavishQuantParams* qp, int rdmult,
+              LavishRdoBlock* out, int32_t* qcoeff, int32_t* dqcoeff, hipStream_t s);
+
+// fork / join over the library's per-thread internal streams
+int fan_width();
+hipStream_t* fan_out(hipStream_t caller);
+void fan_in(hipStream_t caller);
+
 // per-thread scratch device buffer for the per-call (host pointer) shims
 void* shim_scratch(size_t bytes);
 hipStream_t shim_stream();

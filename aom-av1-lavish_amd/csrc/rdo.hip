@@ -452,6 +452,175 @@ int rdo_plane(const uint16_t* src, const uint16_t* pred, int stride, int width, 
   return launch_size<1>(tx_size, a, s);
 }
 
+// ---------------------------------------------------------------------------
+// frame level: every candidate TX size of a frame, the per-superblock TX-size
+// decision and the reconstruction
+// ---------------------------------------------------------------------------
+int rdo_frame(const uint16_t* src, const uint16_t* pred, int stride, int width, int height,
+              uint32_t size_mask, const uint32_t* type_masks, int bd,
+              const LavishQuantParams* qp, int rdmult, LavishRdoBlock* const* out,
+              int32_t* const* qcoeff, int32_t* const* dqcoeff, hipStream_t caller) {
+  int order[19], n = 0;
+  for (int s = 0; s < 19; ++s)
+    if ((size_mask >> s) & 1) order[n++] = s;
+  // most work first, dealt round-robin over the internal streams
+  auto work = [&](int s) {
+    return (long)__builtin_popcount(type_masks[s]) * (width / tx_w(s)) * (height / tx_h(s)) *
+           max_eob(s);
+  };
+  for (int i = 1; i < n; ++i)
+    for (int j = i; j > 0 && work(order[j]) > work(order[j - 1]); --j) {
+      const int t = order[j];
+      order[j] = order[j - 1];
+      order[j - 1] = t;
+    }
+  hipStream_t* fs = fan_out(caller);
+  int rc = 0;
+  for (int i = 0; i < n && rc == 0; ++i) {
+    const int s = order[i];
+    rc = rdo_plane(src, pred, stride, width, height, s, type_masks[s], bd, qp, rdmult, out[s],
+                   qcoeff[s], dqcoeff[s], fs[i % fan_width()]);
+  }
+  fan_in(caller);
+  return rc;
+}
+
+namespace {
+
+__constant__ uint8_t kTxWd[19] = {4, 8, 16, 32, 64, 4, 8, 8, 16, 16, 32, 32, 64, 4, 16, 8, 32, 16, 64};
+__constant__ uint8_t kTxHd[19] = {4, 8, 16, 32, 64, 8, 4, 16, 8, 32, 16, 64, 32, 16, 4, 32, 8, 64, 16};
+__device__ __forceinline__ int tx_w_dev(int s) { return kTxWd[s]; }
+__device__ __forceinline__ int tx_h_dev(int s) { return kTxHd[s]; }
+// av1_get_max_eob (av1/common/blockd.h:1596-1604)
+__device__ __forceinline__ int max_eob_dev(int s) {
+  const int w = kTxWd[s], h = kTxHd[s];
+  if (w == 64 || h == 64) return (w == 16 || h == 16) ? 512 : 1024;
+  return w * h;
+}
+
+struct SbArgs {
+  int nsizes;
+  int sizes[19];                       // candidate order: largest area first
+  const LavishRdoBlock* rec[19];
+  int sbw, sbh;                        // superblocks per row / column
+  int width, height;
+  uint8_t* sb_tx_size;
+};
+
+// per SB64: the candidate TX size whose blocks' summed RD cost is lowest
+// (sizes that do not tile the SB with full blocks are skipped; ties keep
+// the earlier, larger size)
+__global__ void sb_decide_kernel(SbArgs a) {
+  const int sb = blockIdx.x * blockDim.x + threadIdx.x;
+  if (sb >= a.sbw * a.sbh) return;
+  const int sy = sb / a.sbw, sx = sb - sy * a.sbw;
+  int64_t best = INT64_MAX;
+  int best_s = 255;
+  for (int i = 0; i < a.nsizes; ++i) {
+    const int s = a.sizes[i];
+    const int W = tx_w_dev(s), H = tx_h_dev(s);
+    const int bw = a.width / W;
+    const int y1 = min(64, a.height - sy * 64), x1 = min(64, a.width - sx * 64);
+    if (y1 % H || x1 % W) continue;
+    int64_t sum = 0;
+    for (int y = 0; y < y1; y += H)
+      for (int x = 0; x < x1; x += W) {
+        const int blk = ((sy * 64 + y) / H) * bw + (sx * 64 + x) / W;
+        sum += a.rec[s][blk].rdcost;
+      }
+    if (sum < best) {
+      best = sum;
+      best_s = s;
+    }
+  }
+  a.sb_tx_size[sb] = (uint8_t)best_s;
+}
+
+// inverse-transform jobs of one size: the block's best type / eob where its
+// SB chose this size, eob 0 (untouched) elsewhere
+__global__ void inv_jobs_kernel(int s, const LavishRdoBlock* rec, int nblocks, int bw, int stride,
+                                int sbw, const uint8_t* sb_tx_size, LavishInvJob* jobs) {
+  const int blk = blockIdx.x * blockDim.x + threadIdx.x;
+  if (blk >= nblocks) return;
+  const int W = tx_w_dev(s), H = tx_h_dev(s);
+  const int by = blk / bw, bx = blk - by * bw;
+  const int y = by * H, x = bx * W;
+  LavishInvJob j;
+  j.dst_off = (int64_t)y * stride + x;
+  j.coeff_off = (int64_t)blk * max_eob_dev(s);
+  j.tx_type = rec[blk].best_type;
+  j.eob = sb_tx_size[(y / 64) * sbw + x / 64] == s ? rec[blk].eob : 0;
+  jobs[blk] = j;
+}
+
+struct ReconScratch {
+  int device = -1;
+  LavishInvJob* jobs = nullptr;
+  size_t cap = 0;
+};
+thread_local ReconScratch t_rs;
+
+LavishInvJob* job_scratch(size_t n) {
+  int dev = 0;
+  LAVISH_CHECK(hipGetDevice(&dev));
+  if (t_rs.device != dev || n > t_rs.cap) {
+    // previous users of the buffer are ordered before us on the same stream
+    if (t_rs.jobs && t_rs.device == dev) LAVISH_CHECK(hipFree(t_rs.jobs));
+    t_rs.cap = n < 4096 ? 4096 : n;
+    LAVISH_CHECK(hipMalloc(&t_rs.jobs, t_rs.cap * sizeof(LavishInvJob)));
+    t_rs.device = dev;
+  }
+  return t_rs.jobs;
+}
+
+}  // namespace
+
+int rdo_reconstruct(uint32_t size_mask, const LavishRdoBlock* const* rec,
+                    const int32_t* const* dqcoeff, int width, int height, const uint16_t* pred,
+                    uint16_t* recon, int stride, int bd, uint8_t* sb_tx_size, hipStream_t s) {
+  SbArgs a{};
+  for (int t = 0; t < 19; ++t)
+    if ((size_mask >> t) & 1) a.sizes[a.nsizes++] = t;
+  if (a.nsizes == 0) return -1;
+  for (int i = 1; i < a.nsizes; ++i)  // largest area first
+    for (int j = i; j > 0 && tx_w(a.sizes[j]) * tx_h(a.sizes[j]) >
+                                 tx_w(a.sizes[j - 1]) * tx_h(a.sizes[j - 1]); --j) {
+      const int t = a.sizes[j];
+      a.sizes[j] = a.sizes[j - 1];
+      a.sizes[j - 1] = t;
+    }
+  for (int i = 0; i < a.nsizes; ++i) a.rec[a.sizes[i]] = rec[a.sizes[i]];
+  a.sbw = (width + 63) / 64;
+  a.sbh = (height + 63) / 64;
+  a.width = width;
+  a.height = height;
+  a.sb_tx_size = sb_tx_size;
+  const int nsb = a.sbw * a.sbh;
+  hipLaunchKernelGGL(sb_decide_kernel, dim3((nsb + 255) / 256), dim3(256), 0, s, a);
+  LAVISH_CHECK(hipGetLastError());
+  // recon = pred, then add the chosen blocks' residuals size by size
+  LAVISH_CHECK(hipMemcpy2DAsync(recon, (size_t)stride * 2, pred, (size_t)stride * 2,
+                                (size_t)width * 2, height, hipMemcpyDeviceToDevice, s));
+  size_t maxb = 0;
+  for (int i = 0; i < a.nsizes; ++i) {
+    const int t = a.sizes[i];
+    maxb = max(maxb, (size_t)(width / tx_w(t)) * (height / tx_h(t)));
+  }
+  LavishInvJob* jobs = job_scratch(maxb);
+  for (int i = 0; i < a.nsizes; ++i) {
+    const int t = a.sizes[i];
+    const int bw = width / tx_w(t);
+    const int nb = bw * (height / tx_h(t));
+    if (nb == 0) continue;
+    hipLaunchKernelGGL(inv_jobs_kernel, dim3((nb + 255) / 256), dim3(256), 0, s, t, rec[t], nb,
+                       bw, stride, a.sbw, sb_tx_size, jobs);
+    LAVISH_CHECK(hipGetLastError());
+    const int rc = inv_txfm_add_batch(dqcoeff[t], t, jobs, nb, recon, stride, bd, 1, s);
+    if (rc) return rc;
+  }
+  return 0;
+}
+
 }  // namespace lavish
 
 extern "C" int lavish_rdo_plane(const uint16_t* src, const uint16_t* pred, int stride, int width,
@@ -460,4 +629,21 @@ extern "C" int lavish_rdo_plane(const uint16_t* src, const uint16_t* pred, int s
                                 int32_t* qcoeff, int32_t* dqcoeff, void* stream) {
   return lavish::rdo_plane(src, pred, stride, width, height, tx_size, type_mask, bit_depth, qp,
                            rdmult, out, qcoeff, dqcoeff, (hipStream_t)stream);
+}
+
+extern "C" int lavish_rdo_frame(const uint16_t* src, const uint16_t* pred, int stride, int width,
+                                int height, uint32_t size_mask, const uint32_t* type_masks,
+                                int bit_depth, const LavishQuantParams* qp, int rdmult,
+                                LavishRdoBlock* const* out, int32_t* const* qcoeff,
+                                int32_t* const* dqcoeff, void* stream) {
+  return lavish::rdo_frame(src, pred, stride, width, height, size_mask, type_masks, bit_depth, qp,
+                           rdmult, out, qcoeff, dqcoeff, (hipStream_t)stream);
+}
+
+extern "C" int lavish_rdo_reconstruct(uint32_t size_mask, const LavishRdoBlock* const* records,
+                                      const int32_t* const* dqcoeff, int width, int height,
+                                      const uint16_t* pred, uint16_t* recon, int stride,
+                                      int bit_depth, uint8_t* sb_tx_size, void* stream) {
+  return lavish::rdo_reconstruct(size_mask, records, dqcoeff, width, height, pred, recon, stride,
+                                 bit_depth, sb_tx_size, (hipStream_t)stream);
 }

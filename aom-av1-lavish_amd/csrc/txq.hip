@@ -423,6 +423,25 @@ static FrameStreams& frame_streams() {
   return t_fs;
 }
 
+int fan_width() { return kFrameStreams; }
+
+// fork: the internal streams wait for everything queued on `caller`
+hipStream_t* fan_out(hipStream_t caller) {
+  FrameStreams& fs = frame_streams();
+  LAVISH_CHECK(hipEventRecord(fs.fork, caller));
+  for (int i = 0; i < kFrameStreams; ++i) LAVISH_CHECK(hipStreamWaitEvent(fs.s[i], fs.fork, 0));
+  return fs.s;
+}
+
+// join: `caller` waits for everything queued on the internal streams
+void fan_in(hipStream_t caller) {
+  FrameStreams& fs = frame_streams();
+  for (int i = 0; i < kFrameStreams; ++i) {
+    LAVISH_CHECK(hipEventRecord(fs.join[i], fs.s[i]));
+    LAVISH_CHECK(hipStreamWaitEvent(caller, fs.join[i], 0));
+  }
+}
+
 int txq_frame(const int16_t* residual, int stride, int width, int height, uint32_t size_mask,
               const uint32_t* type_masks, int bd, int quant_kind, const LavishQuantParams* qp,
               int32_t* const* qcoeff, int32_t* const* dqcoeff, uint16_t* const* eob,
@@ -441,19 +460,14 @@ int txq_frame(const int16_t* residual, int stride, int width, int height, uint32
       order[j] = order[j - 1];
       order[j - 1] = t;
     }
-  FrameStreams& fs = frame_streams();
-  LAVISH_CHECK(hipEventRecord(fs.fork, caller));
-  for (int i = 0; i < kFrameStreams; ++i) LAVISH_CHECK(hipStreamWaitEvent(fs.s[i], fs.fork, 0));
+  hipStream_t* fs = fan_out(caller);
   int rc = 0;
   for (int i = 0; i < n && rc == 0; ++i) {
     const int s = order[i];
     rc = txq_plane(residual, stride, width, height, s, type_masks[s], bd, quant_kind, qp,
-                   qcoeff[s], dqcoeff[s], eob[s], nullptr, fs.s[i % kFrameStreams]);
+                   qcoeff[s], dqcoeff[s], eob[s], nullptr, fs[i % kFrameStreams]);
   }
-  for (int i = 0; i < kFrameStreams; ++i) {
-    LAVISH_CHECK(hipEventRecord(fs.join[i], fs.s[i]));
-    LAVISH_CHECK(hipStreamWaitEvent(caller, fs.join[i], 0));
-  }
+  fan_in(caller);
   return rc;
 }
 

@@ -392,3 +392,62 @@ def rdo_plane(src, pred, tx_size, type_mask, qp, rdmult, bit_depth=10, out=None,
 
 def rdo_records(out):
     return out["records"].cpu().numpy().view(RDO_DTYPE)
+
+
+_P19 = ctypes.c_void_p * 19
+_lib.lavish_rdo_frame.argtypes = [_vp, _vp, _i32, _i32, _i32, ctypes.c_uint32, _vp, _i32,
+                                  ctypes.POINTER(QuantParams), _i32, _vp, _vp, _vp, _vp]
+_lib.lavish_rdo_frame.restype = _i32
+_lib.lavish_rdo_reconstruct.argtypes = [ctypes.c_uint32, _vp, _vp, _i32, _i32, _vp, _vp, _i32,
+                                        _i32, _vp, _vp]
+_lib.lavish_rdo_reconstruct.restype = _i32
+
+# C4 candidate set: 64x64 DCT, 32x32 DCT + IDTX, 16x16 / 8x8 /
+# 4x4 every type
+C4_TYPE_MASKS = {4: 0x0001, 3: 0x0201, 2: 0xFFFF, 1: 0xFFFF, 0: 0xFFFF}
+
+
+class RdoFrame:
+    """Per-size outputs of rdo_frame + the reconstruction buffers, allocated
+    once for a plane shape and reused every call."""
+
+    def __init__(self, src, type_masks=None):
+        import torch
+        self.type_masks = dict(type_masks or C4_TYPE_MASKS)
+        self.sizes = sorted(self.type_masks)
+        self.size_mask = sum(1 << s for s in self.sizes)
+        self.outs = {s: rdo_out(src, s) for s in self.sizes}
+        self.tm = (ctypes.c_uint32 * 19)(*[self.type_masks.get(s, 0) for s in range(19)])
+        self.rec = _P19(*[self.outs[s]["records"].data_ptr() if s in self.outs else 0
+                          for s in range(19)])
+        self.q = _P19(*[self.outs[s]["qcoeff"].data_ptr() if s in self.outs else 0
+                        for s in range(19)])
+        self.dq = _P19(*[self.outs[s]["dqcoeff"].data_ptr() if s in self.outs else 0
+                         for s in range(19)])
+        H, W = src.shape
+        self.recon = torch.empty_like(src)
+        self.sb_tx_size = torch.empty(((W + 63) // 64) * ((H + 63) // 64), dtype=torch.uint8,
+                                      device=src.device)
+
+
+def rdo_frame(src, pred, frame, qp, rdmult, bit_depth=10, reconstruct=True, stream=None):
+    """C4 on one frame: lavish_rdo_frame over the candidate sizes, then (by
+    default) lavish_rdo_reconstruct into frame.recon."""
+    import torch
+    assert src.dtype == torch.int16 and src.stride(1) == 1 and src.shape == pred.shape
+    H, W = src.shape
+    st = _stream_ptr(stream)
+    rc = _lib.lavish_rdo_frame(ctypes.c_void_p(src.data_ptr()), ctypes.c_void_p(pred.data_ptr()),
+                               src.stride(0), W, H, frame.size_mask, frame.tm, bit_depth,
+                               ctypes.byref(qp), rdmult, frame.rec, frame.q, frame.dq, st)
+    if rc != 0:
+        raise ValueError("lavish_rdo_frame rejected its arguments (rc=%d)" % rc)
+    if reconstruct:
+        rc = _lib.lavish_rdo_reconstruct(frame.size_mask, frame.rec, frame.dq, W, H,
+                                         ctypes.c_void_p(pred.data_ptr()),
+                                         ctypes.c_void_p(frame.recon.data_ptr()), src.stride(0),
+                                         bit_depth, ctypes.c_void_p(frame.sb_tx_size.data_ptr()),
+                                         st)
+        if rc != 0:
+            raise ValueError("lavish_rdo_reconstruct rejected its arguments (rc=%d)" % rc)
+    return frame

@@ -250,6 +250,28 @@ int lavish_rdo_plane(const uint16_t *src, const uint16_t *pred, int stride,
                      LavishRdoBlock *out, int32_t *qcoeff, int32_t *dqcoeff,
                      void *stream);
 
+/* Frame level: lavish_rdo_plane for every size set in size_mask (bit =
+ * TX_SIZE) with type_masks[tx_size] and per-size outputs (arrays of 19
+ * pointers), the sizes running concurrently on internal streams. */
+int lavish_rdo_frame(const uint16_t *src, const uint16_t *pred, int stride,
+                     int width, int height, uint32_t size_mask,
+                     const uint32_t *type_masks, int bit_depth,
+                     const LavishQuantParams *qp, int rdmult,
+                     LavishRdoBlock *const *records, int32_t *const *qcoeff,
+                     int32_t *const *dqcoeff, void *stream);
+
+/* Per 64x64 superblock: the candidate size (of size_mask) whose blocks tile
+ * the SB with the lowest summed rd cost (ties: the larger size) -> sb_tx_size
+ * (255 when none tiles it); then recon = pred + the chosen blocks' inverse
+ * transforms with their best types (lavish_inv_txfm_add_batch semantics:
+ * eob 0 leaves the prediction).  u16 planes, `stride` elements. */
+int lavish_rdo_reconstruct(uint32_t size_mask,
+                           const LavishRdoBlock *const *records,
+                           const int32_t *const *dqcoeff, int width,
+                           int height, const uint16_t *pred, uint16_t *recon,
+                           int stride, int bit_depth, uint8_t *sb_tx_size,
+                           void *stream);
+
 /* ---- C3: DIAMOND full-pixel motion search ------------------------------
  * av1_full_pixel_search with search_method DIAMOND (av1/encoder/mcomp.c:
  * 1755-1895 -> full_pixel_diamond :1479-1526 -> diamond_search_sad

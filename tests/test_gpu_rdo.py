@@ -102,3 +102,68 @@ def test_rdo_large_residual_exact_path(L):
         for f in ("best_type", "eob", "rate", "satd", "dist", "sse", "rdcost"):
             np.testing.assert_array_equal(got[f], exp[f], err_msg=f)
         np.testing.assert_array_equal(out["qcoeff"].cpu().numpy(), eq)
+
+
+def _oracle_frame(src, pred, bd, masks, rdmult):
+    """C4 frame reference: per-size oracle decisions, the per-SB TX-size
+    choice (lowest summed rd cost, ties to the larger size) and the
+    reconstruction with the oracle's inverse transform."""
+    H, W = src.shape
+    q = O.build_quant(bd, 128)
+    per = {s: O.rdo_plane(src, pred, s, m, bd, q, rdmult, threads=8) for s, m in masks.items()}
+    sizes = sorted(masks, key=lambda s: -O.TX_W[s] * O.TX_H[s])
+    sbw, sbh = (W + 63) // 64, (H + 63) // 64
+    choice = np.full(sbw * sbh, 255, np.uint8)
+    for sy in range(sbh):
+        for sx in range(sbw):
+            best = None
+            for s in sizes:
+                bw_, bh_ = O.TX_W[s], O.TX_H[s]
+                y1, x1 = min(64, H - sy * 64), min(64, W - sx * 64)
+                if y1 % bh_ or x1 % bw_:
+                    continue
+                nbx = W // bw_
+                tot = 0
+                for y in range(0, y1, bh_):
+                    for x in range(0, x1, bw_):
+                        tot += int(per[s][0]["rdcost"][((sy * 64 + y) // bh_) * nbx
+                                                       + (sx * 64 + x) // bw_])
+                if best is None or tot < best[0]:
+                    best = (tot, s)
+            if best is not None:
+                choice[sy * sbw + sx] = best[1]
+    recon = pred.copy()
+    for s in sizes:
+        bw_, bh_ = O.TX_W[s], O.TX_H[s]
+        rec, qc, dq = per[s]
+        nbx = W // bw_
+        for blk in range(len(rec)):
+            by, bx = divmod(blk, nbx)
+            y, x = by * bh_, bx * bw_
+            if choice[(y // 64) * sbw + x // 64] != s or rec["eob"][blk] == 0:
+                continue
+            recon[y:y + bh_, x:x + bw_] = O.inv_txfm2d_add(dq[blk], recon[y:y + bh_, x:x + bw_],
+                                                           int(rec["best_type"][blk]), s, bd)
+    return per, choice, recon
+
+
+@pytest.mark.parametrize("bd", [10, 8])
+def test_rdo_frame_and_reconstruct(L, bd):
+    """Whole C4 frame step (partial last SB row and column) vs the oracle."""
+    import torch
+    src, pred = _planes(bd, 77, Wp=328, Hp=200)
+    masks = dict(L.C4_TYPE_MASKS)
+    rdmult = 2000
+    per, choice, recon = _oracle_frame(src, pred, bd, masks, rdmult)
+    ts = torch.from_numpy(src.view(np.int16)).cuda()
+    tp = torch.from_numpy(pred.view(np.int16)).cuda()
+    fr = L.RdoFrame(ts)
+    L.rdo_frame(ts, tp, fr, L.build_quant_params(bd, 128, L.QUANT_FP), rdmult, bd)
+    for s in masks:
+        got = L.rdo_records(fr.outs[s])
+        for f in ("best_type", "eob", "rdcost"):
+            np.testing.assert_array_equal(got[f], per[s][0][f], err_msg="%d %s" % (s, f))
+        np.testing.assert_array_equal(fr.outs[s]["dqcoeff"].cpu().numpy(), per[s][2])
+    np.testing.assert_array_equal(fr.sb_tx_size.cpu().numpy(), choice)
+    np.testing.assert_array_equal(fr.recon.cpu().numpy().view(np.uint16), recon)
+    assert len(np.unique(choice)) > 1
