@@ -31,6 +31,8 @@ launch duration, from HIP events on the launch stream) and `cpu_baseline`
 """
 import argparse
 import json
+
+import numpy as np
 import os
 import sys
 import time
@@ -47,7 +49,8 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--workload", choices=("rdo", "c2", "c3"), default="rdo")
+    ap.add_argument("--workload", choices=("rdo", "c2", "c3", "c4", "c5"), default="rdo")
+    ap.add_argument("--rdmult", type=int, default=2000)
     ap.add_argument("--width", type=int, default=1920)
     ap.add_argument("--height", type=int, default=1080)
     ap.add_argument("--qindex", type=int, default=128)
@@ -129,8 +132,154 @@ def cpu_baseline(args):
                       % (passes, W, Hs, sb, args.workload, threads, dt)}
 
 
+def c4_algorithmic_bytes(L, W, H):
+    """C4 bytes per frame (decision mode): per candidate size
+    src + pred read once (2 x 2 B / pixel), the winner's qcoeff + dqcoeff
+    (8 B / coefficient) and a 40 B decision record per block; then the
+    reconstruction reads pred and writes recon (4 B / pixel) and reads the
+    chosen dqcoeff (<= 4 B / pixel)."""
+    tot = 0
+    for s in L.C4_TYPE_MASKS:
+        nb = (W // L.TX_W[s]) * (H // L.TX_H[s])
+        tot += 4 * W * H + nb * (8 * L.max_eob(s) + 40)
+    return tot + 8 * W * H
+
+
+def cpu_baseline_c4(args):
+    """Oracle C4 (oracle/oracle_rdo.c + the per-SB choice + oracle inverse
+    transforms, tests/_c4ref.py) on a 3840x128 strip (2 SB rows) of the same
+    content, repeated for ~cpu_seconds."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import _c4ref
+    import lavish_dsp as L
+    threads = min(16, os.cpu_count() or 1)
+    W = args.width if args.width != 1920 else 3840
+    src, pred = _c4ref.planes(10, 1234, Wp=W, Hp=128)
+    sb = sb64_count(W, 128)
+    passes = 0
+    t0 = time.perf_counter()
+    while True:
+        _c4ref.oracle_frame_c(src, pred, 10, dict(L.C4_TYPE_MASKS), args.rdmult, threads=threads)
+        passes += 1
+        dt = time.perf_counter() - t0
+        if dt >= args.cpu_seconds:
+            break
+    return {"value": round(passes * sb / dt, 2), "unit": "SB64/s", "cores": threads,
+            "kind": "port",
+            "sample": "%d passes of a %dx128 10-bit strip (%d SB64) through the C4 step (RDO of "
+                      "all candidate sizes/types, per-SB TX size, reconstruction), oracle C "
+                      "restatement (-O3, %d pthreads), %.1f s"
+                      % (passes, W, sb, threads, dt)}
+
+
+def main_c4(args):
+    """C4 (1 GPU) / C5 (SB rows sharded over the ranks, reconstructed rows
+    all-gathered over RCCL) on a 4K 10-bit frame."""
+    import torch
+    import torch.distributed as dist
+    import lavish_dsp as L
+    import lavish_dsp.shard as shard
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local_rank)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    W = args.width if args.width != 1920 else 3840
+    H = args.height if args.height != 1080 else 2160
+    import lavish_dsp.synth as synth
+    src_np = synth.frame(W, H, 10, 1234).astype(np.uint16)
+    pred_np = synth.shifted(synth.frame(W, H, 10, 1235), 3, -2).astype(np.uint16)
+    src = torch.from_numpy(src_np.view(np.int16)).cuda()
+    pred = torch.from_numpy(pred_np.view(np.int16)).cuda()
+    qp = L.build_quant_params(10, args.qindex, L.QUANT_FP)
+    stream = torch.cuda.current_stream()
+    frames = {}
+    if args.workload == "c5":
+        proc = shard.c4_band_processor(src, pred, qp, args.rdmult, 10, frames)
+
+        def step():
+            return shard.sharded_frame(H, rank, world, proc)
+    else:
+        fr = L.RdoFrame(src)
+
+        def step():
+            L.rdo_frame(src, pred, fr, qp, args.rdmult, 10)
+            return fr.recon
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+          for _ in range(args.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        ev[k][0].record(stream)
+        step()
+        ev[k][1].record(stream)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    status = L.status()
+    if status[0] != 0:
+        raise RuntimeError("HIP error during bench: %s" % (status,))
+    step_ms = sum(a.elapsed_time(b) for a, b in ev) / args.steps
+    sb = sb64_count(W, H)
+    value = sb * args.steps / elapsed  # one frame per step for the whole job
+    c4_bytes = c4_algorithmic_bytes(L, W, H)
+    y0, y1 = shard.bands(H, world)[rank]
+    line = {
+        "metric": METRIC,
+        "value": round(value, 2),
+        "unit": "SB64/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "strong" if args.workload == "c5" else "weak",
+        "vs_baseline": None,
+        "dtype": "int32",
+        "data": "synthetic (seeded 4K 10-bit content, lavish_dsp/synth.py)",
+        "config": {
+            "workload": "%s: %dx%d 10-bit frame per step; fused TX-type RDO (subtract, fwd "
+                        "txfm, highbd quantize_fp, satd, block error, rate_estimator, RDCOST) of "
+                        "64x64 DCT, 32x32 DCT+IDTX, 16x16/8x8/4x4 all types; per-SB TX size; "
+                        "reconstruction%s; %d SB64/frame"
+                        % (args.workload, W, H,
+                           "; SB rows sharded over ranks + RCCL all-gather of the "
+                           "reconstruction" if args.workload == "c5" else "", sb),
+            "parallelism": ("sb-row bands x%d (rank %d rows %d-%d)" % (world, rank, y0, y1))
+            if args.workload == "c5" else "frame-per-rank x%d" % world,
+        },
+        "roofline": {"bound": "hbm", "kernel": "rdo_kernel<W,H,1> x5 sizes + reconstruction "
+                     "(lavish_rdo_frame + lavish_rdo_reconstruct)",
+                     "achieved": round(c4_bytes / (step_ms * 1e-3) / 1e9, 1),
+                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "traffic": None,
+                     "avg_launch_ms": round(step_ms, 4),
+                     "algorithmic_bytes_per_launch": c4_bytes},
+    }
+    line["roofline"]["frac"] = round(line["roofline"]["achieved"] / HBM_PEAK_GBS, 4)
+    if rank == 0 and world == 1 and not args.no_cpu:
+        line["cpu_baseline"] = cpu_baseline_c4(args)
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def main():
     args = parse()
+    if args.workload in ("c4", "c5"):
+        return main_c4(args)
     import torch
     import torch.distributed as dist
     import lavish_dsp as L

@@ -209,6 +209,11 @@ long orc_rdo_plane(const uint16_t *src, const uint16_t *pred, int stride,
                    int width, int height, int tx_size, unsigned type_mask,
                    int bd, const OrcQuant *q, int rdmult, OrcRdoBlock *out,
                    int32_t *qcoeff, int32_t *dqcoeff, int threads);
+void orc_rdo_reconstruct(int nsizes, const int *sizes,
+                         const OrcRdoBlock *const *recs,
+                         const int32_t *const *dqs, int width, int height,
+                         const uint16_t *pred, uint16_t *recon, int stride,
+                         int bd, uint8_t *sb_tx_size);
 
 /* ---- C2 pipeline: fwd_txfm + quantize_fp over a residual plane ----
  * For one tx_size, tile the plane with full blocks (row-major block order),

@@ -129,3 +129,47 @@ long orc_rdo_plane(const uint16_t *src, const uint16_t *pred, int stride, int wi
     for (int i = 0; i < threads; ++i) pthread_join(tid[i], NULL);
   return (long)bh * (width / W);
 }
+
+/* Per 64x64 SB: the size (of `sizes`, largest area first) whose full blocks
+ * tile the SB with the lowest summed rdcost (ties: the earlier size), then
+ * recon = pred + inverse transforms of the chosen blocks (eob 0: untouched).
+ * recs / dqs: per size (index into `sizes`), raster block order. */
+void orc_rdo_reconstruct(int nsizes, const int *sizes, const OrcRdoBlock *const *recs,
+                         const int32_t *const *dqs, int width, int height,
+                         const uint16_t *pred, uint16_t *recon, int stride, int bd,
+                         uint8_t *sb_tx_size) {
+  const int sbw = (width + 63) / 64, sbh = (height + 63) / 64;
+  for (int sy = 0; sy < sbh; ++sy)
+    for (int sx = 0; sx < sbw; ++sx) {
+      int64_t best = INT64_MAX;
+      int best_s = 255;
+      for (int i = 0; i < nsizes; ++i) {
+        const int s = sizes[i], W = orc_tx_w(s), H = orc_tx_h(s);
+        const int y1 = height - sy * 64 < 64 ? height - sy * 64 : 64;
+        const int x1 = width - sx * 64 < 64 ? width - sx * 64 : 64;
+        if (y1 % H || x1 % W) continue;
+        int64_t sum = 0;
+        for (int y = 0; y < y1; y += H)
+          for (int x = 0; x < x1; x += W)
+            sum += recs[i][((sy * 64 + y) / H) * (width / W) + (sx * 64 + x) / W].rdcost;
+        if (sum < best) {
+          best = sum;
+          best_s = s;
+        }
+      }
+      sb_tx_size[sy * sbw + sx] = (uint8_t)best_s;
+    }
+  for (int y = 0; y < height; ++y)
+    memcpy(recon + (size_t)y * stride, pred + (size_t)y * stride, sizeof(uint16_t) * width);
+  for (int i = 0; i < nsizes; ++i) {
+    const int s = sizes[i], W = orc_tx_w(s), H = orc_tx_h(s), n = orc_max_eob(s);
+    const int bw = width / W, bh = height / H;
+    for (int by = 0; by < bh; ++by)
+      for (int bx = 0; bx < bw; ++bx) {
+        const int y = by * H, x = bx * W, blk = by * bw + bx;
+        if (sb_tx_size[(y / 64) * sbw + x / 64] != s || recs[i][blk].eob == 0) continue;
+        orc_inv_txfm2d_add(dqs[i] + (size_t)blk * n, recon + (size_t)y * stride + x, stride,
+                           recs[i][blk].best_type, s, bd);
+      }
+  }
+}

@@ -53,11 +53,7 @@ def test_txq_plane_64(L, s, bd, kind):
                                   eob.reshape(-1))
 
 
-def _planes(bd, seed, Wp=384, Hp=192):
-    import lavish_dsp.synth as synth
-    src = synth.frame(Wp, Hp, bd, seed)
-    pred = synth.shifted(synth.frame(Wp, Hp, bd, seed + 1), 3, -2)
-    return src.astype(np.uint16), pred.astype(np.uint16)
+from _c4ref import planes as _planes, oracle_frame as _oracle_frame  # noqa: E402
 
 
 # the C4 candidate set plus rectangular sizes
@@ -102,49 +98,6 @@ def test_rdo_large_residual_exact_path(L):
         for f in ("best_type", "eob", "rate", "satd", "dist", "sse", "rdcost"):
             np.testing.assert_array_equal(got[f], exp[f], err_msg=f)
         np.testing.assert_array_equal(out["qcoeff"].cpu().numpy(), eq)
-
-
-def _oracle_frame(src, pred, bd, masks, rdmult):
-    """C4 frame reference: per-size oracle decisions, the per-SB TX-size
-    choice (lowest summed rd cost, ties to the larger size) and the
-    reconstruction with the oracle's inverse transform."""
-    H, W = src.shape
-    q = O.build_quant(bd, 128)
-    per = {s: O.rdo_plane(src, pred, s, m, bd, q, rdmult, threads=8) for s, m in masks.items()}
-    sizes = sorted(masks, key=lambda s: -O.TX_W[s] * O.TX_H[s])
-    sbw, sbh = (W + 63) // 64, (H + 63) // 64
-    choice = np.full(sbw * sbh, 255, np.uint8)
-    for sy in range(sbh):
-        for sx in range(sbw):
-            best = None
-            for s in sizes:
-                bw_, bh_ = O.TX_W[s], O.TX_H[s]
-                y1, x1 = min(64, H - sy * 64), min(64, W - sx * 64)
-                if y1 % bh_ or x1 % bw_:
-                    continue
-                nbx = W // bw_
-                tot = 0
-                for y in range(0, y1, bh_):
-                    for x in range(0, x1, bw_):
-                        tot += int(per[s][0]["rdcost"][((sy * 64 + y) // bh_) * nbx
-                                                       + (sx * 64 + x) // bw_])
-                if best is None or tot < best[0]:
-                    best = (tot, s)
-            if best is not None:
-                choice[sy * sbw + sx] = best[1]
-    recon = pred.copy()
-    for s in sizes:
-        bw_, bh_ = O.TX_W[s], O.TX_H[s]
-        rec, qc, dq = per[s]
-        nbx = W // bw_
-        for blk in range(len(rec)):
-            by, bx = divmod(blk, nbx)
-            y, x = by * bh_, bx * bw_
-            if choice[(y // 64) * sbw + x // 64] != s or rec["eob"][blk] == 0:
-                continue
-            recon[y:y + bh_, x:x + bw_] = O.inv_txfm2d_add(dq[blk], recon[y:y + bh_, x:x + bw_],
-                                                           int(rec["best_type"][blk]), s, bd)
-    return per, choice, recon
 
 
 @pytest.mark.parametrize("bd", [10, 8])
