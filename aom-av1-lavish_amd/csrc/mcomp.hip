@@ -12,13 +12,16 @@
 // Here one wave64 owns one (block, reference) job and runs that sequential
 // walk.  A step's 8 candidate sites are evaluated at once: lane group
 // g = lane / 8 takes site g + 1, its 8 lanes split the block's rows, each
-// lane accumulates v_sad_u8 over 4-byte words (unaligned rows are assembled
-// from aligned dwords with v_alignbyte), and a 3-level xor shuffle leaves the
-// group's SAD in every lane.  The 8 SADs are then read into scalar registers
-// and the reference's sequential "strictly better" scan in site order runs
-// on the SALU, so the walk (and every tie) is exactly the reference's.  The
-// source block stays in VGPRs for the whole search; reference pixels come
-// from L2 / MALL (a 1080p padded reference is ~2.5 MB).
+// lane accumulates v_sad_u8 over 4-byte words (rows assembled with
+// v_alignbyte from dword-aligned loads), and three DPP adds leave the
+// group's SAD in every lane.  Each group then forms the key
+// (sad + mvsad_cost) * 8 + site for its site and the wave takes the minimum
+// over the 8 groups (8 readlanes + s_min): the reference's sequential
+// "strictly better" scan in site order keeps exactly the first site of
+// minimal cost (its sad < bestsad prefilter never rejects a site whose cost
+// is lower, since the mv cost is >= 0), so the walk and every tie are the
+// reference's.  The source block stays in VGPRs for the whole search;
+// reference pixels come from L2 / MALL (a 1080p padded reference is ~2.5 MB).
 #include "lavish_internal.h"
 
 namespace lavish {
@@ -31,20 +34,32 @@ __device__ __forceinline__ uint32_t sad4(uint32_t a, uint32_t b, uint32_t acc) {
 }
 
 // DW consecutive 4-byte words starting at an arbitrary byte address, from
-// aligned dword loads (reads at most 3 bytes past the row only when the
-// address is unaligned).
+// dword-aligned loads (DW words + one more, merged into dwordx4 loads) and
+// v_alignbyte.  The extra word is the next one only when the address is
+// unaligned (else the last one again), so no byte outside the row is read.
 template <int DW>
 __device__ __forceinline__ void load_row(const uint8_t* p, uint32_t (&out)[DW]) {
   const uintptr_t a = (uintptr_t)p;
-  const uint32_t* q = (const uint32_t*)(a & ~(uintptr_t)3);
+  // global address space: global_load (not flat: no LDS-aperture check and
+  // no lgkmcnt dependency)
+  typedef const __attribute__((address_space(1))) uint32_t* gptr;
+  const gptr q = (gptr)(a & ~(uintptr_t)3);
   const uint32_t sh = (uint32_t)(a & 3);
-  uint32_t prev = q[0];
+  uint32_t w[DW + 1];
 #pragma unroll
-  for (int i = 0; i < DW; ++i) {
-    const uint32_t nxt = (i + 1 < DW) ? q[i + 1] : (sh ? q[DW] : 0u);
-    out[i] = __builtin_amdgcn_alignbyte(nxt, prev, sh);
-    prev = nxt;
-  }
+  for (int i = 0; i < DW; ++i) w[i] = q[i];
+  w[DW] = q[sh ? DW : DW - 1];
+#pragma unroll
+  for (int i = 0; i < DW; ++i) out[i] = __builtin_amdgcn_alignbyte(w[i + 1], w[i], sh);
+}
+
+// sum over the 8-lane group (every lane of the group gets it): quad_perm
+// [1,0,3,2], quad_perm [2,3,0,1], row_half_mirror
+__device__ __forceinline__ uint32_t group_sum8(uint32_t v) {
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, false);
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xF, 0xF, false);
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x141, 0xF, 0xF, false);
+  return v;
 }
 
 __device__ __forceinline__ uint32_t rdlane(uint32_t v, int l) {
@@ -65,6 +80,7 @@ struct Ctx {
   int col_min, col_max, row_min, row_max;
   int ref_mv_row, ref_mv_col, full_ref_row, full_ref_col;
   int cost_type;
+  int sad_lambda, sse_lambda;  // per cost_type, hoisted out of the walk
 };
 
 __device__ __forceinline__ int sad_lambda(int t) { return t == 1 ? 32 : t == 2 ? 15 : t == 3 ? 8 : 0; }
@@ -73,12 +89,12 @@ __device__ __forceinline__ int sse_lambda(int t) { return t == 1 ? 2 : t == 2 ? 
 // mvsad_err_cost (mcomp.c:329-350) for the L1 types; 0 for MV_COST_NONE
 __device__ __forceinline__ uint32_t mvsad_cost(const Ctx& c, int row, int col) {
   const int dr = (row - c.full_ref_row) * 8, dc = (col - c.full_ref_col) * 8;
-  return (uint32_t)((sad_lambda(c.cost_type) * (abs(dr) + abs(dc))) >> 3);
+  return (uint32_t)((c.sad_lambda * (abs(dr) + abs(dc))) >> 3);
 }
 // mv_err_cost (mcomp.c:287-314) for the L1 types
 __device__ __forceinline__ int mv_cost(const Ctx& c, int row, int col) {
   const int dr = row * 8 - c.ref_mv_row, dc = col * 8 - c.ref_mv_col;
-  return (sse_lambda(c.cost_type) * (abs(dr) + abs(dc))) >> 3;
+  return (c.sse_lambda * (abs(dr) + abs(dc))) >> 3;
 }
 
 // Row split of a block inside one 8-lane group.
@@ -144,9 +160,7 @@ struct Search {
         }
       }
     }
-    acc += __shfl_xor(acc, 1);
-    acc += __shfl_xor(acc, 2);
-    acc += __shfl_xor(acc, 4);
+    acc = group_sum8(acc);
     return SKIP ? 2 * acc : acc;
   }
 
@@ -171,22 +185,13 @@ struct Search {
       const bool valid = all_in || (cc >= c.col_min && cc <= c.col_max && r >= c.row_min &&
                                     r <= c.row_max);
       const uint32_t mine = group_sad(c, (int64_t)r * c.rs + cc, valid);
-      const uint64_t vmask = __ballot(valid);
-      int best_site = 0;
+      // key = cost * 8 + site (costs < 2^26 for blocks <= 128x128)
+      const uint32_t key = valid ? ((mine + mvsad_cost(c, r, cc)) << 3) | (uint32_t)g : ~0u;
+      uint32_t kmin = rdlane(key, 0);
 #pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        if (!((vmask >> (8 * i)) & 1)) continue;
-        const uint32_t sd = rdlane(mine, 8 * i);
-        if (sd < best) {
-          const int ir = (i == 0 || i == 4 || i == 6) ? -1 : (i == 1 || i == 5 || i == 7) ? 1 : 0;
-          const int ic = (i == 2 || i == 4 || i == 7) ? -1 : (i == 3 || i == 5 || i == 6) ? 1 : 0;
-          const uint32_t t = sd + mvsad_cost(c, row + ir * rad, col + ic * rad);
-          if (t < best) {
-            best = t;
-            best_site = i + 1;
-          }
-        }
-      }
+      for (int i = 1; i < 8; ++i) kmin = min(kmin, rdlane(key, 8 * i));
+      const int best_site = kmin < (best << 3) ? (int)(kmin & 7) + 1 : 0;
+      if (best_site) best = kmin >> 3;
       ++steps;
       if (best_site) {
         const int i = best_site - 1;
@@ -223,13 +228,15 @@ __device__ int var_cost(const Ctx& c, int lane, int row, int col) {
       sse += (uint32_t)(d * d);
     }
   }
+  const uint32_t gs = group_sum8((uint32_t)sum), gq = group_sum8(sse);
+  uint32_t ts = rdlane(gs, 0), tq = rdlane(gq, 0);
 #pragma unroll
-  for (int m = 1; m < 64; m <<= 1) {
-    sum += __shfl_xor(sum, m);
-    sse += __shfl_xor(sse, m);
+  for (int i = 1; i < 8; ++i) {
+    ts += rdlane(gs, 8 * i);
+    tq += rdlane(gq, 8 * i);
   }
-  sum = __builtin_amdgcn_readfirstlane(sum);
-  sse = (uint32_t)__builtin_amdgcn_readfirstlane((int)sse);
+  sum = (int)ts;
+  sse = tq;
   const uint32_t var = sse - (uint32_t)(((int64_t)sum * sum) / (W * H));
   return (int)var + mv_cost(c, row, col);
 }
@@ -293,6 +300,8 @@ __global__ __launch_bounds__(256) void diamond_kernel(const uint8_t* __restrict_
   c.full_ref_row = rawpel(jb.ref_mv_row);
   c.full_ref_col = rawpel(jb.ref_mv_col);
   c.cost_type = cost_type;
+  c.sad_lambda = sad_lambda(cost_type);
+  c.sse_lambda = sse_lambda(cost_type);
   int br, bc, steps = 0, searches = 0, sme;
   // use_downsampled_sad applies to blocks at least 16 high (mcomp.c:132-133)
   if (skip && H >= 16) {

@@ -510,30 +510,34 @@ struct SbArgs {
 // per SB64: the candidate TX size whose blocks' summed RD cost is lowest
 // (sizes that do not tile the SB with full blocks are skipped; ties keep
 // the earlier, larger size)
-__global__ void sb_decide_kernel(SbArgs a) {
-  const int sb = blockIdx.x * blockDim.x + threadIdx.x;
+// One wave64 per SB: lanes stride the SB's blocks of a size, a 64-bit xor
+// reduction sums their costs; the size scan stays sequential (strict <).
+__global__ __launch_bounds__(256) void sb_decide_kernel(SbArgs a) {
+  const int sb = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
   if (sb >= a.sbw * a.sbh) return;
   const int sy = sb / a.sbw, sx = sb - sy * a.sbw;
+  const int y1 = min(64, a.height - sy * 64), x1 = min(64, a.width - sx * 64);
   int64_t best = INT64_MAX;
   int best_s = 255;
   for (int i = 0; i < a.nsizes; ++i) {
     const int s = a.sizes[i];
     const int W = tx_w_dev(s), H = tx_h_dev(s);
-    const int bw = a.width / W;
-    const int y1 = min(64, a.height - sy * 64), x1 = min(64, a.width - sx * 64);
     if (y1 % H || x1 % W) continue;
+    const int bw = a.width / W, nx = x1 / W, nblk = nx * (y1 / H);
     int64_t sum = 0;
-    for (int y = 0; y < y1; y += H)
-      for (int x = 0; x < x1; x += W) {
-        const int blk = ((sy * 64 + y) / H) * bw + (sx * 64 + x) / W;
-        sum += a.rec[s][blk].rdcost;
-      }
+    for (int k = lane; k < nblk; k += 64) {
+      const int y = k / nx, x = k - y * nx;
+      sum += a.rec[s][(sy * 64 / H + y) * bw + sx * 64 / W + x].rdcost;
+    }
+#pragma unroll
+    for (int m = 1; m < 64; m <<= 1) sum += __shfl_xor(sum, m);
     if (sum < best) {
       best = sum;
       best_s = s;
     }
   }
-  a.sb_tx_size[sb] = (uint8_t)best_s;
+  if (lane == 0) a.sb_tx_size[sb] = (uint8_t)best_s;
 }
 
 // inverse-transform jobs of one size: the block's best type / eob where its
@@ -596,7 +600,7 @@ int rdo_reconstruct(uint32_t size_mask, const LavishRdoBlock* const* rec,
   a.height = height;
   a.sb_tx_size = sb_tx_size;
   const int nsb = a.sbw * a.sbh;
-  hipLaunchKernelGGL(sb_decide_kernel, dim3((nsb + 255) / 256), dim3(256), 0, s, a);
+  hipLaunchKernelGGL(sb_decide_kernel, dim3((nsb + 3) / 4), dim3(256), 0, s, a);
   LAVISH_CHECK(hipGetLastError());
   // recon = pred, then add the chosen blocks' residuals size by size
   LAVISH_CHECK(hipMemcpy2DAsync(recon, (size_t)stride * 2, pred, (size_t)stride * 2,

@@ -25,6 +25,15 @@ if not os.path.exists(LIB_PATH):
         "liblavish_hip.so not found at %s -- build it with `make -C aom-av1-lavish_amd` "
         "(or __graft_entry__.build()); there is no CPU fallback" % LIB_PATH)
 
+# One HIP runtime per process: torch ships its own libamdhip64.so.7 (same
+# soname as /opt/rocm's).  Whichever loads first serves both; device
+# tensors come from torch, so load torch's first and let the library bind to
+# it (loading ours first left its launches seeing no device on the MI355X box).
+try:
+    import torch  # noqa: F401
+except ImportError:  # a C-only consumer: the library brings /opt/rocm's runtime
+    pass
+
 _lib = ctypes.CDLL(LIB_PATH)
 
 TX_SIZES = ["4x4", "8x8", "16x16", "32x32", "64x64", "4x8", "8x4", "8x16", "16x8",
