@@ -58,4 +58,14 @@ void fan_in(hipStream_t caller);
 void* shim_scratch(size_t bytes);
 hipStream_t shim_stream();
 
+// Wave-local memory ordering: lanes of one wave exchange data through LDS
+// with no workgroup barrier (each wave owns its tile); these fences only stop
+// the compiler from moving LDS accesses across the exchange point (LDS ops of
+// one wave are processed in order).
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 }  // namespace lavish

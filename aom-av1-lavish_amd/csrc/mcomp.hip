@@ -48,7 +48,7 @@ __device__ __forceinline__ void load_row(const uint8_t* p, uint32_t (&out)[DW]) 
   uint32_t w[DW + 1];
 #pragma unroll
   for (int i = 0; i < DW; ++i) w[i] = q[i];
-  w[DW] = q[sh ? DW : DW - 1];
+  w[DW] = sh ? q[DW] : 0u;  // only lanes whose row is unaligned issue it
 #pragma unroll
   for (int i = 0; i < DW; ++i) out[i] = __builtin_amdgcn_alignbyte(w[i + 1], w[i], sh);
 }
@@ -106,17 +106,101 @@ struct Geo {
   static constexpr int YS = SKIP ? 2 : 1;            // row step
 };
 
+// vf (aom_variance{W}x{H}) + mv_err_cost at a full-pel mv, in two parts:
+// per-lane (sum, sse) of src/ref words, then the wave reduction.
+__device__ __forceinline__ void var_acc(uint32_t a, uint32_t b, int& sum, uint32_t& sse) {
+  sum += (int)sad4(a, 0, 0) - (int)sad4(b, 0, 0);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int d = (int)((a >> (8 * j)) & 255) - (int)((b >> (8 * j)) & 255);
+    sse += (uint32_t)(d * d);
+  }
+}
+
+template <int W, int H>
+__device__ __forceinline__ int var_finish(const Ctx& c, int sum, uint32_t sse, int row, int col) {
+  const uint32_t gs = group_sum8((uint32_t)sum), gq = group_sum8(sse);
+  uint32_t ts = rdlane(gs, 0), tq = rdlane(gq, 0);
+#pragma unroll
+  for (int i = 1; i < 8; ++i) {
+    ts += rdlane(gs, 8 * i);
+    tq += rdlane(gq, 8 * i);
+  }
+  const uint32_t var = tq - (uint32_t)(((int64_t)(int)ts * (int)ts) / (W * H));
+  return (int)var + mv_cost(c, row, col);
+}
+
+// the whole wave walks the W*H pixels one word per lane, from global memory
+template <int W, int H>
+__device__ int var_cost(const Ctx& c, int lane, int row, int col) {
+  constexpr int DW = W / 4;
+  int sum = 0;
+  uint32_t sse = 0;
+  const uint8_t* rb = c.ref + (int64_t)row * c.rs + col;
+  for (int i = lane; i < H * DW; i += 64) {
+    const int y = i / DW, x = i - y * DW;
+    uint32_t a[1], b[1];
+    load_row<1>(c.src + (int64_t)y * c.ss + 4 * x, a);
+    load_row<1>(rb + (int64_t)y * c.rs + 4 * x, b);
+    var_acc(a[0], b[0], sum, sse);
+  }
+  return var_finish<W, H>(c, sum, sse, row, col);
+}
+
+typedef __attribute__((address_space(3))) uint32_t* lds_u32;
+
+// LDS window of the reference for the small-radius tail of a search: once the
+// radius drops to <= 8 the walk can move at most 8+4+2+1 = 15 pixels, so every
+// later candidate lies in (H + 30) x (W + 30) pixels around the centre at that
+// point.  The wave copies that window once (whole rows: one cache line access
+// per row instead of one per candidate row per step) and the remaining steps
+// read their candidates from LDS.
+template <int W, int H>
+struct Win {
+  static constexpr int R = 15;                  // displacement bound after the fill
+  static constexpr int MAXRAD = 8;              // fill at the first step with rad <= 8
+  static constexpr bool kOn = W <= 32 && H <= 32;
+  static constexpr int ROWS = H + 2 * R;
+  // dwords per row: W + 30 bytes + misalignment, filled by 16-byte loads
+  static constexpr int Q = (W + 2 * R + 3 + 15) / 16;
+  static constexpr int DW = 4 * Q;
+  static constexpr int SIZE = kOn ? ROWS * DW : 1;
+};
+
 template <int W, int H, bool SKIP>
 struct Search {
   using G = Geo<W, H, SKIP>;
+  using WN = Win<W, H>;
   // source rows live in VGPRs up to 32 words per lane (32x32 and smaller);
   // larger blocks re-read them through L2 with the candidate rows
   static constexpr bool kCache = G::RPL * G::DW <= 32;
   uint32_t s[kCache ? G::RPL : 1][kCache ? G::DW : 1];
+  // source words of the variance (one per lane per 64 words), for the
+  // window-served var cost
+  static constexpr int VN = (H * (W / 4) + 63) / 64;
+  static constexpr bool kVarWin = WN::kOn && VN <= 4;
+  uint32_t sv[kVarWin ? VN : 1];
+  bool inwin;               // the last diamond() ended inside its window
   int l;  // lane within the group
+  lds_u32 win;              // this wave's window (WN::SIZE dwords), or null
+  int wr0, wc0;             // window origin (mv units: block top-left at ref + wr0*rs + wc0)
+  uintptr_t wbase;          // byte address of the window origin
 
-  __device__ __forceinline__ void load_src(const Ctx& c, int lane) {
+  __device__ __forceinline__ void load_src(const Ctx& c, int lane, lds_u32 w = nullptr) {
     l = lane & 7;
+    win = w;
+    inwin = false;
+    if constexpr (kVarWin) {
+#pragma unroll
+      for (int v = 0; v < VN; ++v) {
+        const int i = lane + 64 * v;
+        if (i < H * (W / 4)) {
+          uint32_t t[1];
+          load_row<1>(c.src + (int64_t)(i / (W / 4)) * c.ss + 4 * (i % (W / 4)), t);
+          sv[v] = t[0];
+        }
+      }
+    }
     if constexpr (kCache) {
 #pragma unroll
       for (int k = 0; k < G::RPL; ++k) {
@@ -164,9 +248,85 @@ struct Search {
     return SKIP ? 2 * acc : acc;
   }
 
+  // copy the window around (row, col): rows outside [row_min, row_max + H)
+  // (never touched by a valid candidate) are not read
+  __device__ __forceinline__ void fill(const Ctx& c, int lane, int row, int col) {
+    typedef const __attribute__((address_space(1))) uint32_t* gptr;
+    wr0 = row - WN::R;
+    wc0 = col - WN::R;
+    wbase = (uintptr_t)(c.ref + (int64_t)wr0 * c.rs + wc0);
+    const int rlo = max(0, c.row_min - wr0), rhi = min(WN::ROWS, c.row_max + H - wr0);
+    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+    typedef __attribute__((address_space(3))) u32x4* lptr4;
+#pragma unroll
+    for (int i0 = 0; i0 < WN::ROWS * WN::Q; i0 += 64) {
+      const int i = i0 + lane;
+      const int wr = i / WN::Q, d = i - wr * WN::Q;
+      if (i < WN::ROWS * WN::Q && wr >= rlo && wr < rhi) {
+        // dword-aligned 16-byte load (any dword alignment is a single access)
+        const uintptr_t ra = ((wbase + (int64_t)wr * c.rs) & ~(uintptr_t)3) + 16 * d;
+        const gptr q = (gptr)ra;
+        u32x4 v = {q[0], q[1], q[2], q[3]};
+        ((lptr4)win)[i] = v;
+      }
+    }
+    wave_sync();
+  }
+
+  // group SAD of the candidate at (r, cc) from the window
+  __device__ __forceinline__ uint32_t group_sad_win(const Ctx& c, int r, int cc,
+                                                    bool valid) const {
+    uint32_t acc = 0;
+    if (valid) {
+#pragma unroll
+      for (int k = 0; k < G::RPL; ++k) {
+        const int row = l + 8 * k;
+        if (row < G::RH) {
+          const int wr = r - wr0 + row * G::YS;
+          const int x = cc - wc0 + (int)((wbase + (int64_t)wr * c.rs) & 3);
+          const lds_u32 p = win + wr * WN::DW + (x >> 2);
+          const uint32_t sh = (uint32_t)(x & 3);
+          uint32_t w[G::DW + 1];
+#pragma unroll
+          for (int i = 0; i <= G::DW; ++i) w[i] = p[i];
+#pragma unroll
+          for (int i = 0; i < G::DW; ++i)
+            acc = sad4(s[k][i], __builtin_amdgcn_alignbyte(w[i + 1], w[i], sh), acc);
+        }
+      }
+    }
+    acc = group_sum8(acc);
+    return SKIP ? 2 * acc : acc;
+  }
+
+  // var cost at (row, col): from the window when the last search filled one
+  // (its result lies within 15 pixels of the fill centre)
+  __device__ __forceinline__ int var_cost_at(const Ctx& c, int lane, int row, int col) const {
+    if constexpr (kVarWin) {
+      if (inwin) {
+        int sum = 0;
+        uint32_t sse = 0;
+#pragma unroll
+        for (int v = 0; v < VN; ++v) {
+          const int i = lane + 64 * v;
+          if (i < H * (W / 4)) {
+            const int y = i / (W / 4), x4 = i % (W / 4);
+            const int wr = row - wr0 + y;
+            const int xb = col - wc0 + 4 * x4 + (int)((wbase + (int64_t)wr * c.rs) & 3);
+            const lds_u32 p = win + wr * WN::DW + (xb >> 2);
+            var_acc(sv[v], __builtin_amdgcn_alignbyte(p[1], p[0], (uint32_t)(xb & 3)), sum,
+                    sse);
+          }
+        }
+        return var_finish<W, H>(c, sum, sse, row, col);
+      }
+    }
+    return var_cost<W, H>(c, lane, row, col);
+  }
+
   // diamond_search_sad (no second_pred): returns bestsad
   __device__ uint32_t diamond(const Ctx& c, int lane, int srow, int scol, int search_step,
-                              int& brow, int& bcol, int& num00, int& steps) const {
+                              int& brow, int& bcol, int& num00, int& steps) {
     const int g = lane >> 3;
     // site g + 1 of av1_init_dsmotion_compensation (row, col) in units of radius
     const int sdr = (g == 0 || g == 4 || g == 6) ? -1 : (g == 1 || g == 5 || g == 7) ? 1 : 0;
@@ -177,14 +337,22 @@ struct Search {
     uint32_t best = mvsad_cost(c, row, col) +
                     rdlane(group_sad(c, (int64_t)row * c.rs + col, true), 0);
     const int tot = kMaxSteps - search_step;
+    inwin = false;
     for (int step = tot - 1; step >= 0; --step) {
       const int rad = 1 << step;
+      if constexpr (WN::kOn && kCache) {
+        if (!inwin && rad <= WN::MAXRAD && win != nullptr) {
+          fill(c, lane, row, col);
+          inwin = true;
+        }
+      }
       const bool all_in = row - rad >= c.row_min && row + rad <= c.row_max &&
                           col - rad >= c.col_min && col + rad <= c.col_max;
       const int r = row + sdr * rad, cc = col + sdc * rad;
       const bool valid = all_in || (cc >= c.col_min && cc <= c.col_max && r >= c.row_min &&
                                     r <= c.row_max);
-      const uint32_t mine = group_sad(c, (int64_t)r * c.rs + cc, valid);
+      const uint32_t mine = inwin ? group_sad_win(c, r, cc, valid)
+                                  : group_sad(c, (int64_t)r * c.rs + cc, valid);
       // key = cost * 8 + site (costs < 2^26 for blocks <= 128x128)
       const uint32_t key = valid ? ((mine + mvsad_cost(c, r, cc)) << 3) | (uint32_t)g : ~0u;
       uint32_t kmin = rdlane(key, 0);
@@ -208,56 +376,23 @@ struct Search {
   }
 };
 
-// vf (aom_variance{W}x{H}) + mv_err_cost at a full-pel mv: the whole wave
-// walks the W*H pixels one word per lane.
-template <int W, int H>
-__device__ int var_cost(const Ctx& c, int lane, int row, int col) {
-  constexpr int DW = W / 4;
-  int sum = 0;
-  uint32_t sse = 0;
-  const uint8_t* rb = c.ref + (int64_t)row * c.rs + col;
-  for (int i = lane; i < H * DW; i += 64) {
-    const int y = i / DW, x = i - y * DW;
-    uint32_t a[1], b[1];
-    load_row<1>(c.src + (int64_t)y * c.ss + 4 * x, a);
-    load_row<1>(rb + (int64_t)y * c.rs + 4 * x, b);
-    sum += (int)sad4(a[0], 0, 0) - (int)sad4(b[0], 0, 0);
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int d = (int)((a[0] >> (8 * j)) & 255) - (int)((b[0] >> (8 * j)) & 255);
-      sse += (uint32_t)(d * d);
-    }
-  }
-  const uint32_t gs = group_sum8((uint32_t)sum), gq = group_sum8(sse);
-  uint32_t ts = rdlane(gs, 0), tq = rdlane(gq, 0);
-#pragma unroll
-  for (int i = 1; i < 8; ++i) {
-    ts += rdlane(gs, 8 * i);
-    tq += rdlane(gq, 8 * i);
-  }
-  sum = (int)ts;
-  sse = tq;
-  const uint32_t var = sse - (uint32_t)(((int64_t)sum * sum) / (W * H));
-  return (int)var + mv_cost(c, row, col);
-}
-
 // full_pixel_diamond (mcomp.c:1479-1526)
 template <int W, int H, bool SKIP>
 __device__ int full_pixel_diamond(const Ctx& c, int lane, int srow, int scol, int step_param,
-                                  int& brow, int& bcol, int& steps, int& searches) {
+                                  int& brow, int& bcol, int& steps, int& searches, lds_u32 win) {
   Search<W, H, SKIP> S;
-  S.load_src(c, lane);
+  S.load_src(c, lane, win);
   int n, num00 = 0;
   S.diamond(c, lane, srow, scol, step_param, brow, bcol, n, steps);
   ++searches;
-  int bestsme = var_cost<W, H>(c, lane, brow, bcol);
+  int bestsme = S.var_cost_at(c, lane, brow, bcol);
   const int further = kMaxSteps - 1 - step_param;
   while (n < further) {
     ++n;
     int tr, tc;
     S.diamond(c, lane, srow, scol, step_param + n, tr, tc, num00, steps);
     ++searches;
-    const int sme = var_cost<W, H>(c, lane, tr, tc);
+    const int sme = S.var_cost_at(c, lane, tr, tc);
     if (sme < bestsme) {
       bestsme = sme;
       brow = tr;
@@ -283,8 +418,11 @@ __global__ __launch_bounds__(256) void diamond_kernel(const uint8_t* __restrict_
   const int nwg = gridDim.x;  // multiple of 8
   const int wg = (blockIdx.x & 7) * (nwg >> 3) + (blockIdx.x >> 3);
   const int lane = threadIdx.x & 63;
-  const int j = wg * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int j = wg * 4 + wave;
   if (j >= njobs) return;
+  __shared__ uint32_t win_s[4 * Win<W, H>::SIZE];
+  const lds_u32 win = Win<W, H>::kOn ? (lds_u32)(win_s + wave * Win<W, H>::SIZE) : nullptr;
   const Job jb = jobs[j];
   Ctx c;
   c.src = src + jb.src_off;
@@ -306,7 +444,7 @@ __global__ __launch_bounds__(256) void diamond_kernel(const uint8_t* __restrict_
   // use_downsampled_sad applies to blocks at least 16 high (mcomp.c:132-133)
   if (skip && H >= 16) {
     sme = full_pixel_diamond<W, H, true>(c, lane, jb.start_row, jb.start_col, step_param, br, bc,
-                                         steps, searches);
+                                         steps, searches, win);
     // quality check of the row-skipping search (mcomp.c:1840-1867)
     Search<W, H, false> F;
     F.load_src(c, lane);
@@ -318,10 +456,10 @@ __global__ __launch_bounds__(256) void diamond_kernel(const uint8_t* __restrict_
     const int thresh = (W >> 2) * (H >> 2);
     if (sad > thresh && abs(ssad - sad) * 10 >= max(sad, 1) * 9)
       sme = full_pixel_diamond<W, H, false>(c, lane, jb.start_row, jb.start_col, step_param, br,
-                                            bc, steps, searches);
+                                            bc, steps, searches, win);
   } else {
     sme = full_pixel_diamond<W, H, false>(c, lane, jb.start_row, jb.start_col, step_param, br, bc,
-                                          steps, searches);
+                                          steps, searches, win);
   }
   if (lane == 0) {
     LavishDiamondResult r;

@@ -80,16 +80,6 @@ __device__ __forceinline__ int32_t dequant_one(int32_t q, bool ac, const QP& qp)
 // and 10-bit residuals; larger inputs take the exact 64-bit-sum path.
 constexpr int kFastResidualMax = 1023;
 
-// Wave-local memory ordering: lanes of one wave exchange data through LDS
-// with no workgroup barrier (each wave owns its tile); these fences only stop
-// the compiler from moving LDS accesses across the exchange point (LDS ops of
-// one wave are processed in order).
-__device__ __forceinline__ void wave_sync() {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
-
 typedef int32_t v4i __attribute__((ext_vector_type(4)));
 
 }  // namespace lavish

@@ -32,8 +32,12 @@ struct TxqArgs {
   int nblocks;  // total blocks
   int ntypes;
   int types[16];
-  int tgroups;          // type groups along the grid
-  int types_per_group;
+  // type chunks along the grid: the types of a chunk share one vertical
+  // (column) 1-D kind, so a workgroup runs the column pass once per chunk;
+  // chunk g holds type slots chunk_ti[chunk_off[g] .. chunk_off[g+1])
+  int tgroups;
+  int chunk_off[17];
+  int chunk_ti[16];
   int quant_kind;
   int highbd;
   QP qp;
@@ -76,22 +80,19 @@ template <int W, int H, bool FAST, int QK, bool HBD>
 __device__ __forceinline__ void txq_types(const TxqArgs& a,
                                           const int32_t (&res)[Tile<W, H>::CPT][H],
                                           int32_t* t1, int32_t* t2, const int16_t* isc, int lane,
-                                          int blk0, int nvalid, int ty0, int ty1) {
+                                          int blk0, int nvalid, int c0, int c1) {
   using C = TxCfg<W, H>;
   using T = Tile<W, H>;
   constexpr int N = T::N, T1S = T::T1S;
   constexpr int LS = C::log_scale;
-  for (int ti = ty0; ti < ty1; ++ti) {
+  // ---- columns, once for the chunk's vertical kind (av1_fwd_txfm2d.c:88-106) ----
+  {
     // wave-uniform by construction; readfirstlane keeps the transform-kind
     // branches scalar (otherwise hipcc if-converts all three kernels)
-    const int t = __builtin_amdgcn_readfirstlane(a.types[ti]);
-    const int vt = (kVtxPacked >> (2 * t)) & 3, ht = (kHtxPacked >> (2 * t)) & 3;
+    const int t = __builtin_amdgcn_readfirstlane(a.types[a.chunk_ti[c0]]);
+    const int vt = (kVtxPacked >> (2 * t)) & 3;
     const int kc = vt == 3 ? 2 : (vt == 0 ? 0 : 1);
-    const int kr = ht == 3 ? 2 : (ht == 0 ? 0 : 1);
-    const bool ud = vt == 2, lr = ht == 2;
-    const int skind = t < 10 ? 0 : ((t & 1) ? 1 : 2);
-
-    // ---- columns (av1_fwd_txfm2d.c:88-106) ----
+    const bool ud = vt == 2;
 #pragma unroll
     for (int k = 0; k < T::CPT; ++k) {
       const int j = k * 64 + lane;
@@ -104,12 +105,19 @@ __device__ __forceinline__ void txq_types(const TxqArgs& a,
         else in[r] = round_shift_1<-C::s0>(x);
       }
       fwd_1d<H, C::cos_bit_col, FAST>(kc, in, out);
-      const int cc = lr ? W - 1 - c : c;
 #pragma unroll
-      for (int r = 0; r < H; ++r)
-        t1[(b * H + r) * T1S + cc] = round_shift_1<-C::s1>(out[r]);
+      for (int r = 0; r < H; ++r) t1[(b * H + r) * T1S + c] = round_shift_1<-C::s1>(out[r]);
     }
     wave_sync();
+  }
+
+  for (int ci = c0; ci < c1; ++ci) {
+    const int ti = __builtin_amdgcn_readfirstlane(a.chunk_ti[ci]);
+    const int t = __builtin_amdgcn_readfirstlane(a.types[ti]);
+    const int ht = (kHtxPacked >> (2 * t)) & 3;
+    const int kr = ht == 3 ? 2 : (ht == 0 ? 0 : 1);
+    const bool lr = ht == 2;  // FLIPADST rows: the column results read right to left
+    const int skind = t < 10 ? 0 : ((t & 1) ? 1 : 2);
 
     // ---- rows + quantization (av1_fwd_txfm2d.c:110-126, av1_quantize.c) ----
 #pragma unroll
@@ -117,8 +125,14 @@ __device__ __forceinline__ void txq_types(const TxqArgs& a,
       const int j = k * 64 + lane;
       const int b = j / H, r = j % H;
       int32_t in[W], out[W];
+      const int32_t* row = t1 + (b * H + r) * T1S;
+      if (lr) {
 #pragma unroll
-      for (int c = 0; c < W; ++c) in[c] = t1[(b * H + r) * T1S + c];
+        for (int c = 0; c < W; ++c) in[c] = row[W - 1 - c];
+      } else {
+#pragma unroll
+        for (int c = 0; c < W; ++c) in[c] = row[c];
+      }
       fwd_1d<W, C::cos_bit_row, FAST>(kr, in, out);
       const size_t obase = ((size_t)ti * a.nblocks + blk0 + b) * N;
       // eob = 1 + last scan position holding a nonzero qcoeff; the inverse
@@ -191,8 +205,7 @@ __global__ __launch_bounds__(256, 2) void txq_plane_kernel(TxqArgs a) {
   const int tg = rest % a.tgroups, quad = (rest / a.tgroups) * 8 + inner;
   const int ntiles = (a.nblocks + T::P - 1) / T::P;
   if (quad * 4 >= ntiles) return;
-  const int ty0 = tg * a.types_per_group;
-  const int ty1 = min(a.ntypes, ty0 + a.types_per_group);
+  const int c0 = a.chunk_off[tg], c1 = a.chunk_off[tg + 1];
 
   const int tid = threadIdx.x;
   for (int i = tid; i < T::N; i += 256) {
@@ -234,7 +247,7 @@ __global__ __launch_bounds__(256, 2) void txq_plane_kernel(TxqArgs a) {
   // wave-uniform choice of the certified-exact fast arithmetic
   const bool fast = __builtin_amdgcn_ballot_w64(amax > kFastResidualMax) == 0;
 #define LAVISH_TXQ_RUN(F, Q, HB) \
-  txq_types<W, H, F, Q, HB>(a, res, t1, t2, isc, lane, blk0, nvalid, ty0, ty1)
+  txq_types<W, H, F, Q, HB>(a, res, t1, t2, isc, lane, blk0, nvalid, c0, c1)
   const int qk = a.quant_kind;
   if (qk == LAVISH_QUANT_NONE) {
     if (fast) LAVISH_TXQ_RUN(true, LAVISH_QUANT_NONE, false);
@@ -287,19 +300,45 @@ __global__ __launch_bounds__(256) void quant_kernel(const int32_t* coeff, int n,
 // ----------------------------------------------------------------------------
 // launchers
 // ----------------------------------------------------------------------------
-// Split the TX types over enough workgroups to give every CU several
-// (>= ~8 per CU over 256 CUs); each extra group re-reads the residual tile
-// (2 bytes/pixel against 8 bytes/coefficient/type written).
+// Type chunks: one per vertical 1-D kind present (DCT, ADST, FLIPADST,
+// IDTX; the 16 types are all 4 x 4 (vertical, horizontal) pairs, so a block
+// needs 4 column passes, not 16), split further -- largest first -- until the
+// grid has enough workgroups to give every CU several (>= ~8 per CU over 256
+// CUs).  Each extra chunk re-reads the residual tile (2 bytes/pixel against
+// 8 bytes/coefficient/type written) and repeats one column pass.
+static void build_chunks(TxqArgs& a, int nbg) {
+  int cnt = 0, sz[16] = {}, ti[16][16];
+  for (int vk = 0; vk < 4; ++vk) {
+    int n = 0;
+    for (int i = 0; i < a.ntypes; ++i)
+      if (((kVtxPacked >> (2 * a.types[i])) & 3) == (uint32_t)vk) ti[cnt][n++] = i;
+    if (n) sz[cnt++] = n;
+  }
+  while (nbg * cnt < 2048 && cnt < 16) {
+    int big = 0;
+    for (int g = 1; g < cnt; ++g)
+      if (sz[g] > sz[big]) big = g;
+    if (sz[big] < 2) break;
+    const int keep = (sz[big] + 1) / 2;
+    for (int i = keep; i < sz[big]; ++i) ti[cnt][i - keep] = ti[big][i];
+    sz[cnt++] = sz[big] - keep;
+    sz[big] = keep;
+  }
+  int o = 0;
+  for (int g = 0; g < cnt; ++g) {
+    a.chunk_off[g] = o;
+    for (int i = 0; i < sz[g]; ++i) a.chunk_ti[o++] = ti[g][i];
+  }
+  a.chunk_off[cnt] = o;
+  a.tgroups = cnt;
+}
+
 template <int W, int H>
 static void launch_plane(TxqArgs a, hipStream_t s) {
   constexpr int P = Tile<W, H>::P * 4;  // blocks per workgroup (4 wave tiles)
   const int nbg = (a.nblocks + P - 1) / P;
   if (nbg == 0) return;
-  int groups = 1;
-  while (groups < a.ntypes && nbg * groups < 2048) groups *= 2;
-  if (groups > a.ntypes) groups = a.ntypes;
-  a.types_per_group = (a.ntypes + groups - 1) / groups;
-  a.tgroups = (a.ntypes + a.types_per_group - 1) / a.types_per_group;
+  build_chunks(a, nbg);
   const int grid = ((nbg + 7) / 8) * 8 * a.tgroups;
   hipLaunchKernelGGL((txq_plane_kernel<W, H>), dim3(grid), dim3(256), 0, s, a);
   LAVISH_CHECK(hipGetLastError());

@@ -18,7 +18,9 @@ import os
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(os.path.dirname(_HERE), "liblavish_hip.so")
+# LAVISH_HIP_LIB: an alternative build of the same library (A/B experiments)
+LIB_PATH = os.environ.get("LAVISH_HIP_LIB") or os.path.join(os.path.dirname(_HERE),
+                                                            "liblavish_hip.so")
 
 if not os.path.exists(LIB_PATH):
     raise ImportError(

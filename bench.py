@@ -15,11 +15,13 @@ The default workload ("rdo") is the metric's "fwd_txfm+quant+SAD" loop:
       with the 1080p speed features (use_downsampled_sad, MV_COST_L1_HDRES)
       (lavish_diamond_search_batch),
 
-the two legs back to back on the caller stream (C2 forks its per-size
-kernels over internal streams).  Running the legs concurrently on two streams
-measured no gain (both saturate the CUs), and sequential legs keep each
-kernel's rocprof duration equal to its event-timed duration.  --workload c2 /
-c3 times one leg alone.
+the two legs independent (the residual is given), so C3 runs on a second
+stream beside C2 (C2 forks its per-size kernels over internal streams): C3 is
+bound by the vector-memory address path and latency, C2 by HBM writes, and
+they overlap.  Each leg is timed with HIP events on its own stream; the
+roofline kernel is C2, timed while overlapped (a conservative figure).
+--serial runs the legs back to back on one stream; --workload c2 / c3 times
+one leg alone.
 
 Multi-GPU: one process per GPU (torchrun), each rank processes its own frame
 (independent units, no data-path collective): weak scaling.  Timing: barrier +
@@ -58,6 +60,9 @@ def parse():
     ap.add_argument("--border", type=int, default=160)
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--serial", action="store_true",
+                    help="run the C3 leg before the C2 leg on one stream (default: C3 on a "
+                         "second stream, overlapping C2)")
     ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
     return ap.parse_args()
 
@@ -317,29 +322,49 @@ def main():
         M.diamond_search_batch(tsrc, trefs, C3_BLOCK, C3_BLOCK, tjobs, 0, C3_COST, C3_SKIP,
                                out=c3_out, stream=on)
 
-    def step(evs=None):
+    overlap = do_c2 and do_c3 and not args.serial
+    side = torch.cuda.Stream() if overlap else stream
+    fork = torch.cuda.Event()
+    join = torch.cuda.Event()
+
+    def step(ev=None):
+        """One frame.  ev = (start, c3 start, c3 end, c2 start, c2 end, end),
+        each leg's pair recorded on the stream that leg runs on."""
+        if ev is not None:
+            ev[0].record(stream)
+        if overlap:  # the legs are independent: C3 (TA / latency bound) beside C2 (HBM writes)
+            fork.record(stream)
+            side.wait_event(fork)
         if do_c3:
-            c3(stream)
-        if evs is not None:
-            evs[1].record(stream)
+            if ev is not None:
+                ev[1].record(side)
+            c3(side)
+            if ev is not None:
+                ev[2].record(side)
         if do_c2:
+            if ev is not None:
+                ev[3].record(stream)
             L.txq_frame(res, frame, qp, stream=stream)
+            if ev is not None:
+                ev[4].record(stream)
+        if overlap:
+            join.record(side)
+            stream.wait_event(join)
+        if ev is not None:
+            ev[5].record(stream)
 
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
 
-    # per step: start, after C3, end -- HIP events on the launch stream
-    ev = [tuple(torch.cuda.Event(enable_timing=True) for _ in range(3))
+    ev = [tuple(torch.cuda.Event(enable_timing=True) for _ in range(6))
           for _ in range(args.steps)]
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for k in range(args.steps):
-        ev[k][0].record(stream)
         step(ev[k])
-        ev[k][2].record(stream)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -352,9 +377,9 @@ def main():
     if status[0] != 0:
         raise RuntimeError("HIP error during bench: %s" % (status,))
     K = args.steps
-    step_ms = sum(ev[k][0].elapsed_time(ev[k][2]) for k in range(K)) / K
-    c3_ms = sum(ev[k][0].elapsed_time(ev[k][1]) for k in range(K)) / K if do_c3 else 0.0
-    c2_ms = sum(ev[k][1].elapsed_time(ev[k][2]) for k in range(K)) / K if do_c2 else 0.0
+    step_ms = sum(ev[k][0].elapsed_time(ev[k][5]) for k in range(K)) / K
+    c3_ms = sum(ev[k][1].elapsed_time(ev[k][2]) for k in range(K)) / K if do_c3 else 0.0
+    c2_ms = sum(ev[k][3].elapsed_time(ev[k][4]) for k in range(K)) / K if do_c2 else 0.0
     c2_bytes = sum(algorithmic_bytes(L, s, W, H) for s in sizes)
     c3_res = M.results_numpy(c3_out) if do_c3 else None
     c3_bytes = c3_algorithmic_bytes(c3_res, len(jobs_np), C3_BLOCK, C3_BLOCK, C3_SKIP) \
@@ -408,6 +433,7 @@ def main():
                         % (args.workload, W, H, " + ".join(legs), sb),
             "tx_sizes": [L.TX_SIZES[s] for s in sizes] if do_c2 else [],
             "parallelism": "frame-per-rank x%d" % world,
+            "legs": "C3 on a second stream beside C2" if overlap else "C3 then C2, one stream",
         },
         "roofline": roof,
         "legs_ms": {"c2_txq_frame": round(c2_ms, 4), "c3_diamond": round(c3_ms, 4),
