@@ -437,13 +437,15 @@ int quantize_batch(const int32_t* coeff, int n, int nblocks, const int16_t* scan
 }
 
 // Frame batch: every requested TX size over the same residual plane.  The
-// per-size kernels are independent, so they are spread over a few internal
-// streams (forked from / joined back to the caller's stream with events):
-// register-heavy 16/32-point kernels and light 4/8-point kernels then share
-// the CUs, which a single in-order stream cannot do.
+// per-size kernels are independent, so they are spread over the caller's
+// stream plus two internal streams (forked from / joined back to the caller
+// with events): register-heavy 16/32-point kernels and light 4/8-point
+// kernels then share the CUs, which a single in-order stream cannot do.  The
+// caller's stream takes every third kernel (the largest first) so it never
+// waits on a fork; a cross-stream event wait costs tens of microseconds.
 struct FrameStreams {
   int device = -1;
-  hipStream_t s[kFrameStreams] = {};
+  hipStream_t s[kFrameStreams] = {};  // s[0] = the caller's stream (set per call)
   hipEvent_t fork = nullptr, join[kFrameStreams] = {};
 };
 static thread_local FrameStreams t_fs;
@@ -452,7 +454,7 @@ static FrameStreams& frame_streams() {
   int dev = 0;
   LAVISH_CHECK(hipGetDevice(&dev));
   if (t_fs.device != dev) {
-    for (int i = 0; i < kFrameStreams; ++i) {
+    for (int i = 1; i < kFrameStreams; ++i) {
       LAVISH_CHECK(hipStreamCreateWithFlags(&t_fs.s[i], hipStreamNonBlocking));
       LAVISH_CHECK(hipEventCreateWithFlags(&t_fs.join[i], hipEventDisableTiming));
     }
@@ -464,18 +466,20 @@ static FrameStreams& frame_streams() {
 
 int fan_width() { return kFrameStreams; }
 
-// fork: the internal streams wait for everything queued on `caller`
+// fork: the internal streams wait for everything queued on `caller`; slot 0
+// is the caller itself
 hipStream_t* fan_out(hipStream_t caller) {
   FrameStreams& fs = frame_streams();
+  fs.s[0] = caller;
   LAVISH_CHECK(hipEventRecord(fs.fork, caller));
-  for (int i = 0; i < kFrameStreams; ++i) LAVISH_CHECK(hipStreamWaitEvent(fs.s[i], fs.fork, 0));
+  for (int i = 1; i < kFrameStreams; ++i) LAVISH_CHECK(hipStreamWaitEvent(fs.s[i], fs.fork, 0));
   return fs.s;
 }
 
 // join: `caller` waits for everything queued on the internal streams
 void fan_in(hipStream_t caller) {
   FrameStreams& fs = frame_streams();
-  for (int i = 0; i < kFrameStreams; ++i) {
+  for (int i = 1; i < kFrameStreams; ++i) {
     LAVISH_CHECK(hipEventRecord(fs.join[i], fs.s[i]));
     LAVISH_CHECK(hipStreamWaitEvent(caller, fs.join[i], 0));
   }
@@ -499,8 +503,8 @@ int txq_frame(const int16_t* residual, int stride, int width, int height, uint32
       order[j] = order[j - 1];
       order[j - 1] = t;
     }
-  hipStream_t* fs = fan_out(caller);
   int rc = 0;
+  hipStream_t* fs = fan_out(caller);
   for (int i = 0; i < n && rc == 0; ++i) {
     const int s = order[i];
     rc = txq_plane(residual, stride, width, height, s, type_masks[s], bd, quant_kind, qp,

@@ -15,13 +15,13 @@ The default workload ("rdo") is the metric's "fwd_txfm+quant+SAD" loop:
       with the 1080p speed features (use_downsampled_sad, MV_COST_L1_HDRES)
       (lavish_diamond_search_batch),
 
-the two legs independent (the residual is given), so C3 runs on a second
-stream beside C2 (C2 forks its per-size kernels over internal streams): C3 is
-bound by the vector-memory address path and latency, C2 by HBM writes, and
-they overlap.  Each leg is timed with HIP events on its own stream; the
-roofline kernel is C2, timed while overlapped (a conservative figure).
---serial runs the legs back to back on one stream; --workload c2 / c3 times
-one leg alone.
+by default back to back on the caller stream (C2 forks its per-size kernels
+over internal streams), so each leg's event-timed duration is its kernel
+duration (what rocprof reports).  The legs are independent (the residual is
+given): --overlap runs C3 on a second stream beside C2 -- C3 is bound by the
+vector-memory address path and latency, C2 by HBM writes -- which shortens
+the step by ~7 % while stretching each leg.  --workload c2 / c3 times one
+leg alone.
 
 Multi-GPU: one process per GPU (torchrun), each rank processes its own frame
 (independent units, no data-path collective): weak scaling.  Timing: barrier +
@@ -60,9 +60,9 @@ def parse():
     ap.add_argument("--border", type=int, default=160)
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--serial", action="store_true",
-                    help="run the C3 leg before the C2 leg on one stream (default: C3 on a "
-                         "second stream, overlapping C2)")
+    ap.add_argument("--overlap", action="store_true",
+                    help="run the C3 leg on a second stream beside the C2 leg (default: C3 "
+                         "then C2 on one stream)")
     ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
     return ap.parse_args()
 
@@ -322,7 +322,7 @@ def main():
         M.diamond_search_batch(tsrc, trefs, C3_BLOCK, C3_BLOCK, tjobs, 0, C3_COST, C3_SKIP,
                                out=c3_out, stream=on)
 
-    overlap = do_c2 and do_c3 and not args.serial
+    overlap = do_c2 and do_c3 and args.overlap
     side = torch.cuda.Stream() if overlap else stream
     fork = torch.cuda.Event()
     join = torch.cuda.Event()
