@@ -47,6 +47,10 @@ struct RdoArgs {
   int rdmult;      // mode 1
   QP qp;
   const int16_t* iscan_type[16];  // per slot: inverse scan of the type (n)
+  // evaluation order: slots grouped by vertical 1-D kind (one column pass per
+  // group); newcol[i] = 1 where order[i] starts a group
+  int order[16];
+  int newcol[16];
   const int16_t* iscan_dct;       // DCT_DCT inverse scan (rate_estimator)
   int32_t* qcoeff;
   int32_t* dqcoeff;
@@ -91,32 +95,36 @@ __device__ __forceinline__ void rdo_types(const RdoArgs& a, const int32_t (&res)
     best_type[k] = best_eob[k] = best_rate[k] = best_satd[k] = 0;
   }
 
-  for (int ti = 0; ti < a.ntypes; ++ti) {
+  for (int oi = 0; oi < a.ntypes; ++oi) {
+    const int ti = __builtin_amdgcn_readfirstlane(a.order[oi]);
     const int t = __builtin_amdgcn_readfirstlane(a.types[ti]);
     const int vt = (kVtxPacked >> (2 * t)) & 3, ht = (kHtxPacked >> (2 * t)) & 3;
     const int kc = vt == 3 ? 2 : (vt == 0 ? 0 : 1);
     const int kr = ht == 3 ? 2 : (ht == 0 ? 0 : 1);
-    const bool ud = vt == 2, lr = ht == 2;
+    const bool ud = vt == 2;
+    const bool lr = ht == 2;  // FLIPADST rows: the column results read right to left
     const int16_t* iscan = a.iscan_type[ti];
 
-    // ---- columns (av1_fwd_txfm2d.c:88-106); only rows < KH are kept ----
+    // ---- columns (av1_fwd_txfm2d.c:88-106), once per vertical kind; only
+    // rows < KH are kept ----
+    if (__builtin_amdgcn_readfirstlane(a.newcol[oi])) {
 #pragma unroll
-    for (int k = 0; k < T::CPT; ++k) {
-      const int j = k * 64 + lane;
-      const int b = j / W, c = j % W;
-      int32_t in[H], out[H];
+      for (int k = 0; k < T::CPT; ++k) {
+        const int j = k * 64 + lane;
+        const int b = j / W, c = j % W;
+        int32_t in[H], out[H];
 #pragma unroll
-      for (int r = 0; r < H; ++r) {
-        const int32_t x = ud ? res[k][H - 1 - r] : res[k][r];
-        if constexpr (FAST) in[r] = x * (1 << C::s0);
-        else in[r] = round_shift_1<-C::s0>(x);
+        for (int r = 0; r < H; ++r) {
+          const int32_t x = ud ? res[k][H - 1 - r] : res[k][r];
+          if constexpr (FAST) in[r] = x * (1 << C::s0);
+          else in[r] = round_shift_1<-C::s0>(x);
+        }
+        fwd_1d<H, C::cos_bit_col, FAST>(kc, in, out);
+#pragma unroll
+        for (int r = 0; r < KH; ++r) t1[(b * KH + r) * T1S + c] = round_shift_1<-C::s1>(out[r]);
       }
-      fwd_1d<H, C::cos_bit_col, FAST>(kc, in, out);
-      const int cc = lr ? W - 1 - c : c;
-#pragma unroll
-      for (int r = 0; r < KH; ++r) t1[(b * KH + r) * T1S + cc] = round_shift_1<-C::s1>(out[r]);
+      wave_sync();
     }
-    wave_sync();
 
     // ---- kept rows + quantization + per-block statistics ----
 #pragma unroll
@@ -126,8 +134,14 @@ __device__ __forceinline__ void rdo_types(const RdoArgs& a, const int32_t (&res)
       const bool live = b < T::P;
       const int bb = live ? b : 0;
       int32_t in[W], out[W];
+      const int32_t* row = t1 + (bb * KH + r) * T1S;
+      if (lr) {
 #pragma unroll
-      for (int c = 0; c < W; ++c) in[c] = t1[(bb * KH + r) * T1S + c];
+        for (int c = 0; c < W; ++c) in[c] = row[W - 1 - c];
+      } else {
+#pragma unroll
+        for (int c = 0; c < W; ++c) in[c] = row[c];
+      }
       fwd_1d<W, C::cos_bit_row, FAST>(kr, in, out);
       int32_t q[KW];
       int last = 0, satd = 0;
@@ -197,7 +211,10 @@ __device__ __forceinline__ void rdo_types(const RdoArgs& a, const int32_t (&res)
           dsse = sse << -dshift;
         }
         const int64_t rd = (((int64_t)rate * a.rdmult + 256) >> 9) + dist * 128;
-        if (rd < best_rd[k]) {
+        // the reference keeps the first type (ascending) of strictly
+        // smallest cost; types are visited grouped by vertical kind, so
+        // equal costs resolve to the lower type index
+        if (rd < best_rd[k] || (rd == best_rd[k] && t < best_type[k])) {
           best_rd[k] = rd;
           best_dist[k] = dist;
           best_sse[k] = dsse;
@@ -384,6 +401,16 @@ int fill_types(RdoArgs& a, int tx_size, uint32_t type_mask) {
     if (!tx_type_valid(tx_size, t)) return -5;
     a.iscan_type[a.ntypes] = dev_iscan(tx_size, t);
     a.types[a.ntypes++] = t;
+  }
+  int n = 0;
+  for (int vk = 0; vk < 4; ++vk) {
+    bool first = true;
+    for (int i = 0; i < a.ntypes; ++i) {
+      if (((kVtxPacked >> (2 * a.types[i])) & 3) != (uint32_t)vk) continue;
+      a.order[n] = i;
+      a.newcol[n++] = first;
+      first = false;
+    }
   }
   return a.ntypes == 0 ? -5 : 0;
 }
