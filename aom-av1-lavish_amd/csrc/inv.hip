@@ -51,21 +51,6 @@ struct InvTile {
   static constexpr int T1S = W + 1;
 };
 
-// bd index: 0 -> 8, 1 -> 10, 2 -> 12 (row / column clamp ranges of
-// av1_gen_inv_stage_range with opt_range_row / opt_range_col)
-template <int BDI>
-struct Bd {
-  static constexpr int bd = 8 + 2 * BDI;
-  static constexpr int rng_row = BDI == 0 ? 16 : (BDI == 1 ? 18 : 20);
-  static constexpr int rng_col = BDI == 2 ? 18 : 16;
-  static constexpr int clamp_in_row = bd + 8;
-  static constexpr int clamp_in_col = bd + 6 > 16 ? bd + 6 : 16;
-};
-
-__device__ __forceinline__ int32_t rshift_r(int32_t v, int bit) {
-  return bit == 0 ? v : (int32_t)(((int64_t)v + ((int64_t)1 << (bit - 1))) >> bit);
-}
-
 template <int W, int H, int BDI, typename PIX>
 __global__ __launch_bounds__(64) void inv_tile_kernel(const int32_t* __restrict__ dq,
                                                       const InvJob* __restrict__ jobs, int njobs,

@@ -47,7 +47,8 @@ int inv_txfm_add_batch(const int32_t* dq, int tx_size, const LavishInvJob* jobs,
                        void* dst, int stride, int bd, int highbd, hipStream_t s);
 int rdo_plane(const uint16_t* src, const uint16_t* pred, int stride, int width, int height,
               int tx_size, uint32_t type_mask, int bd, const LavishQuantParams* qp, int rdmult,
-              LavishRdoBlock* out, int32_t* qcoeff, int32_t* dqcoeff, hipStream_t s);
+              LavishRdoBlock* out, int32_t* qcoeff, int32_t* dqcoeff, hipStream_t s,
+              int px = 0);
 
 // fork / join over the library's per-thread internal streams
 int fan_width();

@@ -28,6 +28,8 @@
 // contributes to the block reductions (xor shuffles over the KH lanes of the
 // block).  The FAST 24-bit path is certified for |residual| <= 1023 for every
 // size including the 64-point ones (tools/range_analysis.py).
+#include <type_traits>
+
 #include "lavish_internal.h"
 #include "quant_dev.h"
 
@@ -77,14 +79,28 @@ struct RTile {
 
 __device__ __forceinline__ int get_msb(uint32_t n) { return 31 - __builtin_clz(n); }
 
-template <int W, int H, int MODE, bool FAST, int QK, bool HBD>
+// Per-tile LDS of the pixel-domain mode (MODE 2): the prediction pixels, the
+// inverse transform's transposition buffer, and per-block sums.
+template <int W, int H>
+struct PxLds {
+  static constexpr int P = RTile<W, H>::P;
+  static constexpr int T1S = W + 1;
+  uint16_t pred[P * H * W];
+  int32_t tx[P * H * T1S];
+  int64_t bsse[P];  // block_sse (rounded, x16)
+  uint64_t psse[P]; // this type's sum of (src - recon)^2
+};
+
+template <int W, int H, int MODE, bool FAST, int QK, bool HBD, int BDI>
 __device__ __forceinline__ void rdo_types(const RdoArgs& a, const int32_t (&res)[RTile<W, H>::CPT][H],
-                                          int32_t* t1, int32_t* t2, int32_t* tb, int lane,
-                                          int blk0, int nvalid) {
+                                          int32_t* t1, int32_t* t2, int32_t* tb, PxLds<W, H>* px,
+                                          int lane, int blk0, int nvalid) {
   using C = TxCfg<W, H>;
   using T = RTile<W, H>;
+  using B = Bd<BDI>;
   constexpr int NC = T::NC, KW = T::KW, KH = T::KH, T1S = T::T1S;
   constexpr int LS = C::log_scale;
+  constexpr bool DEC = MODE >= 1;  // decision modes (1: TX-domain, 2: pixel-domain distortion)
   // per (row-pass slot k) running best of the block that slot belongs to
   int64_t best_rd[T::RPT], best_dist[T::RPT], best_sse[T::RPT];
   int best_type[T::RPT], best_eob[T::RPT], best_rate[T::RPT], best_satd[T::RPT];
@@ -127,6 +143,9 @@ __device__ __forceinline__ void rdo_types(const RdoArgs& a, const int32_t (&res)
     }
 
     // ---- kept rows + quantization + per-block statistics ----
+    int st_last[T::RPT], st_rate[T::RPT], st_satd[T::RPT];
+    int64_t st_dist[T::RPT], st_sse[T::RPT];
+    int32_t st_q[DEC ? T::RPT : 1][DEC ? KW : 1];
 #pragma unroll
     for (int k = 0; k < T::RPT; ++k) {
       const int j = k * 64 + lane;
@@ -162,14 +181,16 @@ __device__ __forceinline__ void rdo_types(const RdoArgs& a, const int32_t (&res)
           }
           q[c] = quant_one<LS, QK, HBD>(v, ac, a.qp);
         }
-        if constexpr (MODE == 1) {
+        if constexpr (DEC) {
           const int32_t dq = dequant_one<LS>(q[c], ac, a.qp);
           const int64_t d = (int64_t)v - dq;
           err += d * d;
           sse += (int64_t)v * v;
           satd += abs(v);
         }
-        if (live) t2[bb * NC + rc] = q[c];
+        if constexpr (MODE == 0) {
+          if (live) t2[bb * NC + rc] = q[c];
+        }
         last = q[c] != 0 ? max(last, iscan[rc] + 1) : last;
       }
 #pragma unroll
@@ -202,15 +223,94 @@ __device__ __forceinline__ void rdo_types(const RdoArgs& a, const int32_t (&res)
           sse = (sse + rnd) >> sh;
         }
         constexpr int dshift = (1 - LS) * 2;  // (MAX_TX_SCALE - tx_scale) * 2
-        int64_t dist, dsse;
         if constexpr (dshift >= 0) {
-          dist = err >> dshift;
-          dsse = sse >> dshift;
+          st_dist[k] = err >> dshift;
+          st_sse[k] = sse >> dshift;
         } else {
-          dist = err << -dshift;
-          dsse = sse << -dshift;
+          st_dist[k] = err << -dshift;
+          st_sse[k] = sse << -dshift;
         }
-        const int64_t rd = (((int64_t)rate * a.rdmult + 256) >> 9) + dist * 128;
+        st_last[k] = last;
+        st_rate[k] = rate;
+        st_satd[k] = satd;
+#pragma unroll
+        for (int c = 0; c < KW; ++c) st_q[k][c] = q[c];
+      }
+      if constexpr (MODE == 2) {
+        // inverse rows (inv_txfm2d_add_c "Rows") straight from this lane's
+        // quantized row: dequantize, x NewInvSqrt2 for 2:1, clamp, 1-D, shift
+        int32_t vin[W], vout[W];
+#pragma unroll
+        for (int c = 0; c < W; ++c) {
+          int32_t v = dequant_one<LS>(q[c], c != 0 || r != 0, a.qp);
+          if constexpr (C::rect2) v = rshift64((int64_t)v * 2896, 12);
+          vin[c] = clamp_bits<B::clamp_in_row>(v);
+        }
+        inv_1d<W, 12, B::rng_row>(kr, vin, vout);
+        if (live) {
+#pragma unroll
+          for (int c = 0; c < W; ++c) px->tx[(bb * H + r) * T1S + c] = rshift_r(vout[c], -C::is0);
+        }
+      }
+    }
+
+    if constexpr (MODE == 2) {
+      wave_sync();
+      // ---- inverse columns + reconstruction + pixel SSE against src ----
+      constexpr int maxv = (1 << B::bd) - 1;
+#pragma unroll
+      for (int k = 0; k < T::CPT; ++k) {
+        const int j = k * 64 + lane;
+        const int b = j / W, c = j % W;
+        const int cc = lr ? W - 1 - c : c;
+        int32_t in[H], out[H];
+#pragma unroll
+        for (int r = 0; r < H; ++r)
+          in[r] = clamp_bits<B::clamp_in_col>(px->tx[(b * H + r) * T1S + cc]);
+        inv_1d<H, 12, B::rng_col>(kc, in, out);
+        uint64_t ps = 0;
+#pragma unroll
+        for (int r = 0; r < H; ++r) {
+          const int p = px->pred[(b * H + r) * W + c];
+          const int v = p + rshift_r(ud ? out[H - 1 - r] : out[r], -C::is1);
+          const int rec = v < 0 ? 0 : (v > maxv ? maxv : v);
+          const int d = p + res[k][r] - rec;  // src - recon
+          ps += (uint64_t)(d * d);
+        }
+#pragma unroll
+        for (int m = 1; m < W; m <<= 1) ps += __shfl_xor(ps, m);
+        if (c == 0) px->psse[b] = ps;
+      }
+      wave_sync();
+    }
+
+    if constexpr (DEC) {
+      // ---- distortion, RDCOST and the running best per block ----
+#pragma unroll
+      for (int k = 0; k < T::RPT; ++k) {
+        const int j = k * 64 + lane;
+        const int b = j / KH, r = j % KH;
+        const bool live = b < T::P;
+        const int bb = live ? b : 0;
+        int64_t dist = st_dist[k], dsse = st_sse[k];
+        if constexpr (MODE == 2) {
+          // search_tx_type with pixel-domain distortion (tx_search.c:2187-2231);
+          // sizes here are <= 32x32, never TX_64X64
+          const int64_t bsse = px->bsse[bb];
+          if (st_last[k] == 0) {
+            dist = bsse;
+          } else {
+            const int sh = 2 * (a.bd - 8);
+            uint64_t ps = px->psse[bb];
+            if (sh > 0) ps = (ps + ((uint64_t)1 << (sh - 1))) >> sh;
+            // 16 * pixel_dist(): an unsigned 32-bit product
+            const int64_t pxd = (int64_t)(uint32_t)(16u * (uint32_t)ps);
+            const bool high = bsse >= (int64_t)128 * 128 * W * H;
+            dist = (high && pxd < dist) ? dist : pxd;
+          }
+          dsse = bsse;
+        }
+        const int64_t rd = (((int64_t)st_rate[k] * a.rdmult + 256) >> 9) + dist * 128;
         // the reference keeps the first type (ascending) of strictly
         // smallest cost; types are visited grouped by vertical kind, so
         // equal costs resolve to the lower type index
@@ -219,12 +319,12 @@ __device__ __forceinline__ void rdo_types(const RdoArgs& a, const int32_t (&res)
           best_dist[k] = dist;
           best_sse[k] = dsse;
           best_type[k] = t;
-          best_eob[k] = last;
-          best_rate[k] = rate;
-          best_satd[k] = satd;
+          best_eob[k] = st_last[k];
+          best_rate[k] = st_rate[k];
+          best_satd[k] = st_satd[k];
 #pragma unroll
           for (int c = 0; c < KW; ++c)
-            if (live) tb[bb * NC + c * KH + r] = q[c];
+            if (live) tb[bb * NC + c * KH + r] = st_q[k][c];
         }
       }
     }
@@ -253,7 +353,7 @@ __device__ __forceinline__ void rdo_types(const RdoArgs& a, const int32_t (&res)
     }
   }
 
-  if constexpr (MODE == 1) {
+  if constexpr (DEC) {
     // decision records (one lane per block) and the winner's coefficients
 #pragma unroll
     for (int k = 0; k < T::RPT; ++k) {
@@ -288,13 +388,17 @@ __device__ __forceinline__ void rdo_types(const RdoArgs& a, const int32_t (&res)
 }
 
 // one wave = one tile of P blocks; 64-thread workgroups (LDS per tile is up
-// to ~20 KB for the 64-point sizes)
-template <int W, int H, int MODE>
+// to ~20 KB for the 64-point sizes).  MODE 0: per-type coefficients (the
+// txq_plane contract), 1: decision with TX-domain distortion, 2: decision
+// with pixel-domain distortion (sizes <= 32x32; BDI = bit-depth index).
+template <int W, int H, int MODE, int BDI>
 __global__ __launch_bounds__(64) void rdo_kernel(RdoArgs a) {
   using T = RTile<W, H>;
   __shared__ int32_t t1[T::T1];
-  __shared__ __attribute__((aligned(16))) int32_t t2[T::T2];
-  __shared__ __attribute__((aligned(16))) int32_t tb[MODE == 1 ? T::T2 : 4];
+  __shared__ __attribute__((aligned(16))) int32_t t2[MODE == 0 ? T::T2 : 4];
+  __shared__ __attribute__((aligned(16))) int32_t tb[MODE >= 1 ? T::T2 : 4];
+  __shared__ typename std::conditional<MODE == 2, PxLds<W, H>, int>::type pxs;
+  PxLds<W, H>* px = MODE == 2 ? reinterpret_cast<PxLds<W, H>*>(&pxs) : nullptr;
 
   const int lane = threadIdx.x;
   const int blk0 = blockIdx.x * T::P;
@@ -308,28 +412,53 @@ __global__ __launch_bounds__(64) void rdo_kernel(RdoArgs a) {
     const int j = k * 64 + lane;
     const int b = j / W, c = j % W;
     const int blk = blk0 + b;
+    int64_t ss = 0;
     if (b < nvalid) {
       const int by = blk / a.bw, bx = blk - by * a.bw;
       const size_t off = (size_t)by * H * a.stride + (size_t)bx * W + c;
 #pragma unroll
       for (int r = 0; r < H; ++r) {
         int32_t v;
-        if constexpr (MODE == 0) v = a.res[off + (size_t)r * a.stride];
-        else v = (int32_t)a.src[off + (size_t)r * a.stride] - (int32_t)a.pred[off + (size_t)r * a.stride];
+        if constexpr (MODE == 0) {
+          v = a.res[off + (size_t)r * a.stride];
+        } else {
+          const int32_t p = a.pred[off + (size_t)r * a.stride];
+          v = (int32_t)a.src[off + (size_t)r * a.stride] - p;
+          if constexpr (MODE == 2) px->pred[(b * H + r) * W + c] = (uint16_t)p;
+        }
         res[k][r] = v;
         amax = max(amax, abs(v));
+        ss += (int64_t)v * v;
       }
     } else {
 #pragma unroll
-      for (int r = 0; r < H; ++r) res[k][r] = 0;
+      for (int r = 0; r < H; ++r) {
+        res[k][r] = 0;
+        if constexpr (MODE == 2) px->pred[(b * H + r) * W + c] = 0;
+      }
+    }
+    if constexpr (MODE == 2) {
+      // block_sse (tx_search.c:2079-2094): sum of squares of the residual,
+      // highbd-rounded by 2 (bd - 8) bits, x 16
+#pragma unroll
+      for (int m = 1; m < W; m <<= 1) ss += __shfl_xor(ss, m);
+      constexpr int sh = 2 * (Bd<BDI>::bd - 8);
+      if constexpr (sh > 0) ss = (ss + ((int64_t)1 << (sh - 1))) >> sh;
+      if (c == 0) px->bsse[b] = ss * 16;
     }
   }
+  if constexpr (MODE == 2) wave_sync();
   const bool fast = __builtin_amdgcn_ballot_w64(amax > kFastResidualMax) == 0;
-  if constexpr (MODE == 1) {
-    if (fast) rdo_types<W, H, 1, true, LAVISH_QUANT_FP, true>(a, res, t1, t2, tb, lane, blk0, nvalid);
-    else rdo_types<W, H, 1, false, LAVISH_QUANT_FP, true>(a, res, t1, t2, tb, lane, blk0, nvalid);
+  if constexpr (MODE >= 1) {
+    if (fast)
+      rdo_types<W, H, MODE, true, LAVISH_QUANT_FP, true, BDI>(a, res, t1, t2, tb, px, lane, blk0,
+                                                              nvalid);
+    else
+      rdo_types<W, H, MODE, false, LAVISH_QUANT_FP, true, BDI>(a, res, t1, t2, tb, px, lane, blk0,
+                                                               nvalid);
   } else {
-#define LAVISH_RDO_RUN(F, Q, HB) rdo_types<W, H, 0, F, Q, HB>(a, res, t1, t2, tb, lane, blk0, nvalid)
+#define LAVISH_RDO_RUN(F, Q, HB) \
+  rdo_types<W, H, 0, F, Q, HB, 0>(a, res, t1, t2, tb, px, lane, blk0, nvalid)
     if (a.quant_kind == LAVISH_QUANT_NONE) {
       if (fast) LAVISH_RDO_RUN(true, LAVISH_QUANT_NONE, false);
       else LAVISH_RDO_RUN(false, LAVISH_QUANT_NONE, false);
@@ -358,36 +487,47 @@ template <int W, int H, int MODE>
 void launch_rdo(const RdoArgs& a, hipStream_t s) {
   const int grid = (a.nblocks + RTile<W, H>::P - 1) / RTile<W, H>::P;
   if (grid == 0) return;
-  hipLaunchKernelGGL((rdo_kernel<W, H, MODE>), dim3(grid), dim3(64), 0, s, a);
+  if constexpr (MODE == 2) {
+    if (a.bd == 8)
+      hipLaunchKernelGGL((rdo_kernel<W, H, 2, 0>), dim3(grid), dim3(64), 0, s, a);
+    else if (a.bd == 10)
+      hipLaunchKernelGGL((rdo_kernel<W, H, 2, 1>), dim3(grid), dim3(64), 0, s, a);
+    else
+      hipLaunchKernelGGL((rdo_kernel<W, H, 2, 2>), dim3(grid), dim3(64), 0, s, a);
+  } else {
+    hipLaunchKernelGGL((rdo_kernel<W, H, MODE, 0>), dim3(grid), dim3(64), 0, s, a);
+  }
   LAVISH_CHECK(hipGetLastError());
 }
 
 template <int MODE>
 int launch_size(int tx_size, const RdoArgs& a, hipStream_t s) {
-  switch (tx_size) {
-    case 4: launch_rdo<64, 64, MODE>(a, s); return 0;
-    case 11: launch_rdo<32, 64, MODE>(a, s); return 0;
-    case 12: launch_rdo<64, 32, MODE>(a, s); return 0;
-    case 17: launch_rdo<16, 64, MODE>(a, s); return 0;
-    case 18: launch_rdo<64, 16, MODE>(a, s); return 0;
-    default: break;
-  }
-  if constexpr (MODE == 1) {
+  if constexpr (MODE <= 1) {
     switch (tx_size) {
-      case 0: launch_rdo<4, 4, 1>(a, s); return 0;
-      case 1: launch_rdo<8, 8, 1>(a, s); return 0;
-      case 2: launch_rdo<16, 16, 1>(a, s); return 0;
-      case 3: launch_rdo<32, 32, 1>(a, s); return 0;
-      case 5: launch_rdo<4, 8, 1>(a, s); return 0;
-      case 6: launch_rdo<8, 4, 1>(a, s); return 0;
-      case 7: launch_rdo<8, 16, 1>(a, s); return 0;
-      case 8: launch_rdo<16, 8, 1>(a, s); return 0;
-      case 9: launch_rdo<16, 32, 1>(a, s); return 0;
-      case 10: launch_rdo<32, 16, 1>(a, s); return 0;
-      case 13: launch_rdo<4, 16, 1>(a, s); return 0;
-      case 14: launch_rdo<16, 4, 1>(a, s); return 0;
-      case 15: launch_rdo<8, 32, 1>(a, s); return 0;
-      case 16: launch_rdo<32, 8, 1>(a, s); return 0;
+      case 4: launch_rdo<64, 64, MODE>(a, s); return 0;
+      case 11: launch_rdo<32, 64, MODE>(a, s); return 0;
+      case 12: launch_rdo<64, 32, MODE>(a, s); return 0;
+      case 17: launch_rdo<16, 64, MODE>(a, s); return 0;
+      case 18: launch_rdo<64, 16, MODE>(a, s); return 0;
+      default: break;
+    }
+  }
+  if constexpr (MODE >= 1) {
+    switch (tx_size) {
+      case 0: launch_rdo<4, 4, MODE>(a, s); return 0;
+      case 1: launch_rdo<8, 8, MODE>(a, s); return 0;
+      case 2: launch_rdo<16, 16, MODE>(a, s); return 0;
+      case 3: launch_rdo<32, 32, MODE>(a, s); return 0;
+      case 5: launch_rdo<4, 8, MODE>(a, s); return 0;
+      case 6: launch_rdo<8, 4, MODE>(a, s); return 0;
+      case 7: launch_rdo<8, 16, MODE>(a, s); return 0;
+      case 8: launch_rdo<16, 8, MODE>(a, s); return 0;
+      case 9: launch_rdo<16, 32, MODE>(a, s); return 0;
+      case 10: launch_rdo<32, 16, MODE>(a, s); return 0;
+      case 13: launch_rdo<4, 16, MODE>(a, s); return 0;
+      case 14: launch_rdo<16, 4, MODE>(a, s); return 0;
+      case 15: launch_rdo<8, 32, MODE>(a, s); return 0;
+      case 16: launch_rdo<32, 8, MODE>(a, s); return 0;
       default: break;
     }
   }
@@ -453,9 +593,15 @@ int txq_plane_64(const int16_t* residual, int stride, int width, int height, int
   return launch_size<0>(tx_size, a, s);
 }
 
+// 64-point sizes with pixel-domain distortion (one candidate type: DCT_DCT):
+// the TX-domain decision kernel, then the inverse of its winner into a
+// scratch copy of the prediction, the pixel SSE and the reference's
+// TX_64X64 / high-energy rules (px64_finish_kernel).
+int rdo_plane_px64(RdoArgs& a, int tx_size, int width, int height, hipStream_t s);
+
 int rdo_plane(const uint16_t* src, const uint16_t* pred, int stride, int width, int height,
               int tx_size, uint32_t type_mask, int bd, const LavishQuantParams* qp, int rdmult,
-              LavishRdoBlock* out, int32_t* qcoeff, int32_t* dqcoeff, hipStream_t s) {
+              LavishRdoBlock* out, int32_t* qcoeff, int32_t* dqcoeff, hipStream_t s, int px) {
   if (tx_size < 0 || tx_size >= 19) return -1;
   if (qp == nullptr || out == nullptr || qcoeff == nullptr || dqcoeff == nullptr) return -3;
   if (bd != 8 && bd != 10 && bd != 12) return -3;
@@ -476,6 +622,10 @@ int rdo_plane(const uint16_t* src, const uint16_t* pred, int stride, int width, 
   a.out = out;
   a.qcoeff = qcoeff;
   a.dqcoeff = dqcoeff;
+  if (px) {
+    if (W > 32 || H > 32) return rdo_plane_px64(a, tx_size, width, height, s);
+    return launch_size<2>(tx_size, a, s);
+  }
   return launch_size<1>(tx_size, a, s);
 }
 
@@ -486,7 +636,7 @@ int rdo_plane(const uint16_t* src, const uint16_t* pred, int stride, int width, 
 int rdo_frame(const uint16_t* src, const uint16_t* pred, int stride, int width, int height,
               uint32_t size_mask, const uint32_t* type_masks, int bd,
               const LavishQuantParams* qp, int rdmult, LavishRdoBlock* const* out,
-              int32_t* const* qcoeff, int32_t* const* dqcoeff, hipStream_t caller) {
+              int32_t* const* qcoeff, int32_t* const* dqcoeff, hipStream_t caller, int px = 0) {
   int order[19], n = 0;
   for (int s = 0; s < 19; ++s)
     if ((size_mask >> s) & 1) order[n++] = s;
@@ -506,7 +656,7 @@ int rdo_frame(const uint16_t* src, const uint16_t* pred, int stride, int width, 
   for (int i = 0; i < n && rc == 0; ++i) {
     const int s = order[i];
     rc = rdo_plane(src, pred, stride, width, height, s, type_masks[s], bd, qp, rdmult, out[s],
-                   qcoeff[s], dqcoeff[s], fs[i % fan_width()]);
+                   qcoeff[s], dqcoeff[s], fs[i % fan_width()], px);
   }
   fan_in(caller);
   return rc;
@@ -606,6 +756,122 @@ LavishInvJob* job_scratch(size_t n) {
 
 }  // namespace
 
+namespace {
+
+// px64 helpers: inverse jobs of the TX-domain winners, then per block the
+// pixel SSE and the distortion rules of search_tx_type (tx_search.c:2187-2231)
+__global__ void px64_jobs_kernel(const LavishRdoBlock* rec, int nblocks, int bw, int W, int H,
+                                 int n, int stride, LavishInvJob* jobs) {
+  const int blk = blockIdx.x * blockDim.x + threadIdx.x;
+  if (blk >= nblocks) return;
+  const int by = blk / bw, bx = blk - by * bw;
+  LavishInvJob j;
+  j.dst_off = (int64_t)by * H * stride + (int64_t)bx * W;
+  j.coeff_off = (int64_t)blk * n;
+  j.tx_type = rec[blk].best_type;
+  j.eob = rec[blk].eob;
+  jobs[blk] = j;
+}
+
+__global__ __launch_bounds__(256) void px64_finish_kernel(const uint16_t* src, const uint16_t* pred,
+                                                          const uint16_t* recon, int stride,
+                                                          int bw, int W, int H, int is64, int bd,
+                                                          int rdmult, LavishRdoBlock* rec) {
+  const int blk = blockIdx.x;
+  const int by = blk / bw, bx = blk - by * bw;
+  const size_t base = (size_t)by * H * stride + (size_t)bx * W;
+  uint64_t s1 = 0, s2 = 0;
+  for (int i = threadIdx.x; i < W * H; i += 256) {
+    const size_t o = base + (size_t)(i / W) * stride + (i % W);
+    const int64_t d1 = (int64_t)src[o] - pred[o], d2 = (int64_t)src[o] - recon[o];
+    s1 += (uint64_t)(d1 * d1);
+    s2 += (uint64_t)(d2 * d2);
+  }
+  __shared__ uint64_t r1[4], r2[4];
+#pragma unroll
+  for (int m = 1; m < 64; m <<= 1) {
+    s1 += __shfl_xor(s1, m);
+    s2 += __shfl_xor(s2, m);
+  }
+  if ((threadIdx.x & 63) == 0) {
+    r1[threadIdx.x >> 6] = s1;
+    r2[threadIdx.x >> 6] = s2;
+  }
+  __syncthreads();
+  if (threadIdx.x != 0) return;
+  s1 = r1[0] + r1[1] + r1[2] + r1[3];
+  s2 = r2[0] + r2[1] + r2[2] + r2[3];
+  const int sh = 2 * (bd - 8);
+  if (sh > 0) {
+    s1 = (s1 + ((uint64_t)1 << (sh - 1))) >> sh;
+    s2 = (s2 + ((uint64_t)1 << (sh - 1))) >> sh;
+  }
+  const int64_t bsse = (int64_t)s1 * 16;
+  LavishRdoBlock o = rec[blk];
+  int64_t dist = o.dist;
+  if (o.eob == 0) {
+    dist = bsse;
+  } else {
+    const bool high = bsse >= (int64_t)128 * 128 * W * H;
+    const int64_t sse_diff = bsse - o.sse;
+    if (!is64 || !high || sse_diff * 2 < o.sse) {
+      const int64_t pxd = (int64_t)(uint32_t)(16u * (uint32_t)s2);
+      dist = (high && pxd < dist) ? dist : pxd;
+    } else {
+      dist += sse_diff;
+    }
+  }
+  o.dist = dist;
+  o.sse = bsse;
+  o.rdcost = (((int64_t)o.rate * rdmult + 256) >> 9) + dist * 128;
+  rec[blk] = o;
+}
+
+struct Px64Scratch {
+  int device = -1;
+  uint16_t* plane = nullptr;
+  size_t cap = 0;
+  LavishInvJob* jobs = nullptr;
+  size_t jcap = 0;
+};
+thread_local Px64Scratch t_px;
+
+}  // namespace
+
+int rdo_plane_px64(RdoArgs& a, int tx_size, int width, int height, hipStream_t s) {
+  if (a.ntypes != 1) return -6;  // 64-point sizes have one candidate type
+  int rc = launch_size<1>(tx_size, a, s);
+  if (rc || a.nblocks == 0) return rc;
+  const int W = tx_w(tx_size), H = tx_h(tx_size);
+  int dev = 0;
+  LAVISH_CHECK(hipGetDevice(&dev));
+  const size_t need = (size_t)a.stride * height;
+  if (t_px.device != dev || need > t_px.cap || (size_t)a.nblocks > t_px.jcap) {
+    // earlier users of the buffers are ordered before us on this thread's streams
+    LAVISH_CHECK(hipDeviceSynchronize());
+    if (t_px.plane && t_px.device == dev) LAVISH_CHECK(hipFree(t_px.plane));
+    if (t_px.jobs && t_px.device == dev) LAVISH_CHECK(hipFree(t_px.jobs));
+    t_px.cap = need > t_px.cap ? need : t_px.cap;
+    t_px.jcap = (size_t)a.nblocks > t_px.jcap ? (size_t)a.nblocks : t_px.jcap;
+    LAVISH_CHECK(hipMalloc(&t_px.plane, t_px.cap * sizeof(uint16_t)));
+    LAVISH_CHECK(hipMalloc(&t_px.jobs, t_px.jcap * sizeof(LavishInvJob)));
+    t_px.device = dev;
+  }
+  LAVISH_CHECK(hipMemcpy2DAsync(t_px.plane, (size_t)a.stride * 2, a.pred, (size_t)a.stride * 2,
+                                (size_t)width * 2, height, hipMemcpyDeviceToDevice, s));
+  hipLaunchKernelGGL(px64_jobs_kernel, dim3((a.nblocks + 255) / 256), dim3(256), 0, s, a.out,
+                     a.nblocks, a.bw, W, H, max_eob(tx_size), a.stride, t_px.jobs);
+  LAVISH_CHECK(hipGetLastError());
+  rc = inv_txfm_add_batch(a.dqcoeff, tx_size, t_px.jobs, a.nblocks, t_px.plane, a.stride, a.bd,
+                          1, s);
+  if (rc) return rc;
+  hipLaunchKernelGGL(px64_finish_kernel, dim3(a.nblocks), dim3(256), 0, s, a.src, a.pred,
+                     t_px.plane, a.stride, a.bw, W, H, tx_size == 4 ? 1 : 0, a.bd, a.rdmult,
+                     a.out);
+  LAVISH_CHECK(hipGetLastError());
+  return 0;
+}
+
 int rdo_reconstruct(uint32_t size_mask, const LavishRdoBlock* const* rec,
                     const int32_t* const* dqcoeff, int width, int height, const uint16_t* pred,
                     uint16_t* recon, int stride, int bd, uint8_t* sb_tx_size, hipStream_t s) {
@@ -662,6 +928,15 @@ extern "C" int lavish_rdo_plane(const uint16_t* src, const uint16_t* pred, int s
                            rdmult, out, qcoeff, dqcoeff, (hipStream_t)stream);
 }
 
+extern "C" int lavish_rdo_plane_px(const uint16_t* src, const uint16_t* pred, int stride,
+                                   int width, int height, int tx_size, uint32_t type_mask,
+                                   int bit_depth, const LavishQuantParams* qp, int rdmult,
+                                   LavishRdoBlock* out, int32_t* qcoeff, int32_t* dqcoeff,
+                                   void* stream) {
+  return lavish::rdo_plane(src, pred, stride, width, height, tx_size, type_mask, bit_depth, qp,
+                           rdmult, out, qcoeff, dqcoeff, (hipStream_t)stream, 1);
+}
+
 extern "C" int lavish_rdo_frame(const uint16_t* src, const uint16_t* pred, int stride, int width,
                                 int height, uint32_t size_mask, const uint32_t* type_masks,
                                 int bit_depth, const LavishQuantParams* qp, int rdmult,
@@ -669,6 +944,16 @@ extern "C" int lavish_rdo_frame(const uint16_t* src, const uint16_t* pred, int s
                                 int32_t* const* dqcoeff, void* stream) {
   return lavish::rdo_frame(src, pred, stride, width, height, size_mask, type_masks, bit_depth, qp,
                            rdmult, out, qcoeff, dqcoeff, (hipStream_t)stream);
+}
+
+extern "C" int lavish_rdo_frame_px(const uint16_t* src, const uint16_t* pred, int stride,
+                                   int width, int height, uint32_t size_mask,
+                                   const uint32_t* type_masks, int bit_depth,
+                                   const LavishQuantParams* qp, int rdmult,
+                                   LavishRdoBlock* const* out, int32_t* const* qcoeff,
+                                   int32_t* const* dqcoeff, void* stream) {
+  return lavish::rdo_frame(src, pred, stride, width, height, size_mask, type_masks, bit_depth, qp,
+                           rdmult, out, qcoeff, dqcoeff, (hipStream_t)stream, 1);
 }
 
 extern "C" int lavish_rdo_reconstruct(uint32_t size_mask, const LavishRdoBlock* const* records,

@@ -540,4 +540,20 @@ struct TxCfg {
   static constexpr int is1 = -4;
 };
 
+// Inverse-transform ranges per bit depth (index 0 -> 8, 1 -> 10, 2 -> 12):
+// row / column stage ranges of av1_gen_inv_stage_range with opt_range_row /
+// opt_range_col, and the input clamps of inv_txfm2d_add_c.
+template <int BDI>
+struct Bd {
+  static constexpr int bd = 8 + 2 * BDI;
+  static constexpr int rng_row = BDI == 0 ? 16 : (BDI == 1 ? 18 : 20);
+  static constexpr int rng_col = BDI == 2 ? 18 : 16;
+  static constexpr int clamp_in_row = bd + 8;
+  static constexpr int clamp_in_col = bd + 6 > 16 ? bd + 6 : 16;
+};
+
+__device__ __forceinline__ int32_t rshift_r(int32_t v, int bit) {
+  return bit == 0 ? v : (int32_t)(((int64_t)v + ((int64_t)1 << (bit - 1))) >> bit);
+}
+
 }  // namespace lavish

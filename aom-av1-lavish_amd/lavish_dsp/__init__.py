@@ -368,6 +368,8 @@ assert RDO_DTYPE.itemsize == 40
 _lib.lavish_rdo_plane.argtypes = [_vp, _vp, _i32, _i32, _i32, _i32, ctypes.c_uint32, _i32,
                                   ctypes.POINTER(QuantParams), _i32, _vp, _vp, _vp, _vp]
 _lib.lavish_rdo_plane.restype = _i32
+_lib.lavish_rdo_plane_px.argtypes = _lib.lavish_rdo_plane.argtypes
+_lib.lavish_rdo_plane_px.restype = _i32
 
 
 def rdo_out(src, tx_size):
@@ -382,15 +384,18 @@ def rdo_out(src, tx_size):
             "dqcoeff": torch.empty((nb, n), dtype=torch.int32, device=dev)}
 
 
-def rdo_plane(src, pred, tx_size, type_mask, qp, rdmult, bit_depth=10, out=None, stream=None):
-    """lavish_rdo_plane (C4) on device u16 planes held as int16 tensors."""
+def rdo_plane(src, pred, tx_size, type_mask, qp, rdmult, bit_depth=10, out=None, stream=None,
+              px=False):
+    """lavish_rdo_plane (C4) on device u16 planes held as int16 tensors;
+    px=True: lavish_rdo_plane_px (pixel-domain distortion)."""
     import torch
     assert src.dtype == torch.int16 and pred.dtype == torch.int16
     assert src.shape == pred.shape and src.stride(1) == 1 and pred.stride(0) == src.stride(0)
     H, W = src.shape
     if out is None:
         out = rdo_out(src, tx_size)
-    rc = _lib.lavish_rdo_plane(ctypes.c_void_p(src.data_ptr()), ctypes.c_void_p(pred.data_ptr()),
+    fn = _lib.lavish_rdo_plane_px if px else _lib.lavish_rdo_plane
+    rc = fn(ctypes.c_void_p(src.data_ptr()), ctypes.c_void_p(pred.data_ptr()),
                                src.stride(0), W, H, tx_size, type_mask, bit_depth,
                                ctypes.byref(qp), rdmult,
                                ctypes.c_void_p(out["records"].data_ptr()),
@@ -409,6 +414,8 @@ _P19 = ctypes.c_void_p * 19
 _lib.lavish_rdo_frame.argtypes = [_vp, _vp, _i32, _i32, _i32, ctypes.c_uint32, _vp, _i32,
                                   ctypes.POINTER(QuantParams), _i32, _vp, _vp, _vp, _vp]
 _lib.lavish_rdo_frame.restype = _i32
+_lib.lavish_rdo_frame_px.argtypes = _lib.lavish_rdo_frame.argtypes
+_lib.lavish_rdo_frame_px.restype = _i32
 _lib.lavish_rdo_reconstruct.argtypes = [ctypes.c_uint32, _vp, _vp, _i32, _i32, _vp, _vp, _i32,
                                         _i32, _vp, _vp]
 _lib.lavish_rdo_reconstruct.restype = _i32
@@ -441,14 +448,17 @@ class RdoFrame:
                                       device=src.device)
 
 
-def rdo_frame(src, pred, frame, qp, rdmult, bit_depth=10, reconstruct=True, stream=None):
-    """C4 on one frame: lavish_rdo_frame over the candidate sizes, then (by
-    default) lavish_rdo_reconstruct into frame.recon."""
+def rdo_frame(src, pred, frame, qp, rdmult, bit_depth=10, reconstruct=True, stream=None,
+              px=False):
+    """C4 on one frame: lavish_rdo_frame (px=True: lavish_rdo_frame_px,
+    pixel-domain distortion) over the candidate sizes, then (by default)
+    lavish_rdo_reconstruct into frame.recon."""
     import torch
     assert src.dtype == torch.int16 and src.stride(1) == 1 and src.shape == pred.shape
     H, W = src.shape
     st = _stream_ptr(stream)
-    rc = _lib.lavish_rdo_frame(ctypes.c_void_p(src.data_ptr()), ctypes.c_void_p(pred.data_ptr()),
+    fn = _lib.lavish_rdo_frame_px if px else _lib.lavish_rdo_frame
+    rc = fn(ctypes.c_void_p(src.data_ptr()), ctypes.c_void_p(pred.data_ptr()),
                                src.stride(0), W, H, frame.size_mask, frame.tm, bit_depth,
                                ctypes.byref(qp), rdmult, frame.rec, frame.q, frame.dq, st)
     if rc != 0:

@@ -51,7 +51,8 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--workload", choices=("rdo", "c2", "c3", "c4", "c5"), default="rdo")
+    ap.add_argument("--workload", choices=("rdo", "c2", "c3", "c4", "c4px", "c5"),
+                    default="rdo")
     ap.add_argument("--rdmult", type=int, default=2000)
     ap.add_argument("--width", type=int, default=1920)
     ap.add_argument("--height", type=int, default=1080)
@@ -163,18 +164,20 @@ def cpu_baseline_c4(args):
     sb = sb64_count(W, 128)
     passes = 0
     t0 = time.perf_counter()
+    px = args.workload == "c4px"
     while True:
-        _c4ref.oracle_frame_c(src, pred, 10, dict(L.C4_TYPE_MASKS), args.rdmult, threads=threads)
+        _c4ref.oracle_frame_c(src, pred, 10, dict(L.C4_TYPE_MASKS), args.rdmult, threads=threads,
+                              px=px)
         passes += 1
         dt = time.perf_counter() - t0
         if dt >= args.cpu_seconds:
             break
     return {"value": round(passes * sb / dt, 2), "unit": "SB64/s", "cores": threads,
             "kind": "port",
-            "sample": "%d passes of a %dx128 10-bit strip (%d SB64) through the C4 step (RDO of "
+            "sample": "%d passes of a %dx128 10-bit strip (%d SB64) through the %s step (RDO of "
                       "all candidate sizes/types, per-SB TX size, reconstruction), oracle C "
                       "restatement (-O3, %d pthreads), %.1f s"
-                      % (passes, W, sb, threads, dt)}
+                      % (passes, W, sb, args.workload, threads, dt)}
 
 
 def main_c4(args):
@@ -209,8 +212,10 @@ def main_c4(args):
     else:
         fr = L.RdoFrame(src)
 
+        px = args.workload == "c4px"
+
         def step():
-            L.rdo_frame(src, pred, fr, qp, args.rdmult, 10)
+            L.rdo_frame(src, pred, fr, qp, args.rdmult, 10, px=px)
             return fr.recon
     for _ in range(args.warmup):
         step()
@@ -256,17 +261,20 @@ def main_c4(args):
         "data": "synthetic (seeded 4K 10-bit content, lavish_dsp/synth.py)",
         "config": {
             "workload": "%s: %dx%d 10-bit frame per step; fused TX-type RDO (subtract, fwd "
-                        "txfm, highbd quantize_fp, satd, block error, rate_estimator, RDCOST) of "
+                        "txfm, highbd quantize_fp, satd, %s, rate_estimator, RDCOST) of "
                         "64x64 DCT, 32x32 DCT+IDTX, 16x16/8x8/4x4 all types; per-SB TX size; "
                         "reconstruction%s; %d SB64/frame"
                         % (args.workload, W, H,
+                           "pixel-domain distortion (inverse txfm + recon + sse per type)"
+                           if args.workload == "c4px" else "TX-domain block error",
                            "; SB rows sharded over ranks + RCCL all-gather of the "
                            "reconstruction" if args.workload == "c5" else "", sb),
             "parallelism": ("sb-row bands x%d (rank %d rows %d-%d)" % (world, rank, y0, y1))
             if args.workload == "c5" else "frame-per-rank x%d" % world,
         },
-        "roofline": {"bound": "hbm", "kernel": "rdo_kernel<W,H,1> x5 sizes + reconstruction "
-                     "(lavish_rdo_frame + lavish_rdo_reconstruct)",
+        "roofline": {"bound": "hbm", "kernel": "rdo_kernel<W,H,%d> x5 sizes + reconstruction "
+                     "(lavish_rdo_frame%s + lavish_rdo_reconstruct)"
+                     % ((2, "_px") if args.workload == "c4px" else (1, "")),
                      "achieved": round(c4_bytes / (step_ms * 1e-3) / 1e9, 1),
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "traffic": None,
                      "avg_launch_ms": round(step_ms, 4),
@@ -283,7 +291,7 @@ def main_c4(args):
 
 def main():
     args = parse()
-    if args.workload in ("c4", "c5"):
+    if args.workload in ("c4", "c4px", "c5"):
         return main_c4(args)
     import torch
     import torch.distributed as dist

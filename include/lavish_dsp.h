@@ -260,6 +260,30 @@ int lavish_rdo_frame(const uint16_t *src, const uint16_t *pred, int stride,
                      LavishRdoBlock *const *records, int32_t *const *qcoeff,
                      int32_t *const *dqcoeff, void *stream);
 
+/* Pixel-domain distortion: search_tx_type with
+ * use_transform_domain_distortion == 0 and predict_dc_level 0
+ * (tx_search.c:2060-2103, 2187-2231).  Same outputs; per block
+ * block_sse = ROUND_POWER_OF_TWO(sum of squared residual, 2 (bd-8)) * 16 and,
+ * per type: eob 0 -> dist = block_sse; otherwise dist = dist_block_px_domain
+ * (tx_search.c:969-1017: recon = pred + av1_inverse_transform_block,
+ * 16 * the highbd-rounded sse of src - recon), a high-energy block
+ * (block_sse >= 128*128*pels) keeping the TX-domain distortion when that is
+ * larger, and TX_64X64 with high energy using TX-domain + the energy outside
+ * the kept quadrant unless that energy is small; sse = block_sse.  The 64-point
+ * sizes take exactly one type (DCT_DCT); -6 otherwise.
+ * Replaces the search_tx_type distortion step (tx_search.c:2187-2231). */
+int lavish_rdo_plane_px(const uint16_t *src, const uint16_t *pred, int stride,
+                        int width, int height, int tx_size, uint32_t type_mask,
+                        int bit_depth, const LavishQuantParams *qp, int rdmult,
+                        LavishRdoBlock *out, int32_t *qcoeff, int32_t *dqcoeff,
+                        void *stream);
+int lavish_rdo_frame_px(const uint16_t *src, const uint16_t *pred, int stride,
+                        int width, int height, uint32_t size_mask,
+                        const uint32_t *type_masks, int bit_depth,
+                        const LavishQuantParams *qp, int rdmult,
+                        LavishRdoBlock *const *records, int32_t *const *qcoeff,
+                        int32_t *const *dqcoeff, void *stream);
+
 /* Per 64x64 superblock: the candidate size (of size_mask) whose blocks tile
  * the SB with the lowest summed rd cost (ties: the larger size) -> sb_tx_size
  * (255 when none tiles it); then recon = pred + the chosen blocks' inverse

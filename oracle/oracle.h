@@ -209,6 +209,11 @@ long orc_rdo_plane(const uint16_t *src, const uint16_t *pred, int stride,
                    int width, int height, int tx_size, unsigned type_mask,
                    int bd, const OrcQuant *q, int rdmult, OrcRdoBlock *out,
                    int32_t *qcoeff, int32_t *dqcoeff, int threads);
+/* the same with pixel-domain distortion (see oracle_rdo.c) */
+long orc_rdo_plane_px(const uint16_t *src, const uint16_t *pred, int stride,
+                      int width, int height, int tx_size, unsigned type_mask,
+                      int bd, const OrcQuant *q, int rdmult, OrcRdoBlock *out,
+                      int32_t *qcoeff, int32_t *dqcoeff, int threads);
 void orc_rdo_reconstruct(int nsizes, const int *sizes,
                          const OrcRdoBlock *const *recs,
                          const int32_t *const *dqs, int width, int height,

@@ -12,6 +12,22 @@
  *   RDCOST                         av1/encoder/rd.h:31-33
  * keeping the first type with the strictly lowest cost
  * (tx_search.c:2246 `if (rd < best_rd)`).
+ *
+ * Pixel-domain distortion (orc_rdo_plane_px; search_tx_type with
+ * use_transform_domain_distortion == 0, predict_dc_level 0,
+ * tx_search.c:2060-2103, 2187-2231):
+ *   block_sse = ROUND_POWER_OF_TWO(sum_squares(residual), 2 (bd-8)) * 16
+ *   eob == 0        -> dist = sse = block_sse
+ *   otherwise       -> is_high_energy = block_sse >= 128*128*pels;
+ *     TX_64X64 or high energy: tx-domain (dist_td, sse_td) as above and
+ *       sse_diff = block_sse - sse_td;
+ *     if (tx_size != TX_64X64 || !high || 2*sse_diff < sse_td):
+ *       dist = dist_block_px_domain (tx_search.c:969-1017): recon = pred +
+ *       av1_inverse_transform_block, 16 * vf-sse(src, recon) (highbd vf
+ *       rounds the sse by 2 (bd-8) bits, variance.c:321-408); a high-energy
+ *       block keeps dist_td when that is larger;
+ *     else dist = dist_td + sse_diff;
+ *     sse = block_sse.
  */
 #include <pthread.h>
 #include <stdlib.h>
@@ -34,7 +50,7 @@ static int rate_estimator(const int32_t *qcoeff, int eob, int tx_size) {
 
 typedef struct {
   const uint16_t *src, *pred;
-  int stride, width, tx_size, bd, rdmult, row0, row1, ntypes;
+  int stride, width, tx_size, bd, rdmult, row0, row1, ntypes, px;
   int types[16];
   const OrcQuant *q;
   OrcRdoBlock *out;
@@ -50,12 +66,21 @@ static void *rdo_rows(void *arg) {
   const int shift = (1 - ls) * 2; /* (MAX_TX_SCALE - tx_scale) * 2 */
   int16_t diff[64 * 64];
   int32_t coeff[64 * 64], qc[4096], dq[4096];
+  uint16_t rec[64 * 64];
+  const int rsh = 2 * (j->bd - 8);
   for (int by = j->row0; by < j->row1; ++by) {
     for (int bx = 0; bx < bw; ++bx) {
       const long blk = (long)by * bw + bx;
       const size_t off = (size_t)by * H * j->stride + (size_t)bx * W;
       orc_highbd_subtract_block(H, W, diff, W, j->src + off, j->stride, j->pred + off,
                                 j->stride);
+      int64_t block_sse = 0;
+      if (j->px) {
+        uint64_t ss = 0;
+        for (int i = 0; i < W * H; ++i) ss += (uint64_t)((int64_t)diff[i] * diff[i]);
+        if (rsh) ss = (ss + ((uint64_t)1 << (rsh - 1))) >> rsh;
+        block_sse = (int64_t)ss * 16;
+      }
       OrcRdoBlock best;
       memset(&best, 0, sizeof(best));
       best.rdcost = INT64_MAX;
@@ -70,8 +95,35 @@ static void *rdo_rows(void *arg) {
         int64_t ssz;
         int64_t err = orc_highbd_block_error(coeff, dq, n, &ssz, j->bd);
         /* RIGHT_SIGNED_SHIFT (aom_ports/mem.h:69-70) */
-        const int64_t dist = shift < 0 ? err << -shift : err >> shift;
-        const int64_t sse = shift < 0 ? ssz << -shift : ssz >> shift;
+        int64_t dist = shift < 0 ? err << -shift : err >> shift;
+        int64_t sse = shift < 0 ? ssz << -shift : ssz >> shift;
+        if (j->px) {
+          if (eob == 0) {
+            dist = block_sse;
+          } else {
+            const int high = block_sse >= (int64_t)128 * 128 * W * H;
+            const int is64 = j->tx_size == 4; /* TX_64X64 */
+            const int64_t sse_diff = block_sse - sse;
+            if (!is64 || !high || sse_diff * 2 < sse) {
+              for (int r = 0; r < H; ++r)
+                memcpy(rec + r * W, j->pred + off + (size_t)r * j->stride, 2 * W);
+              orc_inv_txfm2d_add(dq, rec, W, t, j->tx_size, j->bd);
+              uint64_t ps = 0;
+              for (int r = 0; r < H; ++r)
+                for (int c = 0; c < W; ++c) {
+                  const int64_t d = (int64_t)j->src[off + (size_t)r * j->stride + c] - rec[r * W + c];
+                  ps += (uint64_t)(d * d);
+                }
+              if (rsh) ps = (ps + ((uint64_t)1 << (rsh - 1))) >> rsh;
+              /* `16 * pixel_dist(...)` is an unsigned (32-bit) product */
+              const int64_t px = (int64_t)(uint32_t)(16u * (uint32_t)ps);
+              dist = (high && px < dist) ? dist : px;
+            } else {
+              dist += sse_diff;
+            }
+          }
+          sse = block_sse;
+        }
         const int rate = rate_estimator(qc, eob, j->tx_size);
         const int64_t rd = ((((int64_t)rate) * j->rdmult + 256) >> 9) + dist * 128;
         if (rd < best.rdcost) {
@@ -92,10 +144,10 @@ static void *rdo_rows(void *arg) {
   return NULL;
 }
 
-long orc_rdo_plane(const uint16_t *src, const uint16_t *pred, int stride, int width,
-                   int height, int tx_size, unsigned type_mask, int bd, const OrcQuant *q,
-                   int rdmult, OrcRdoBlock *out, int32_t *qcoeff, int32_t *dqcoeff,
-                   int threads) {
+static long rdo_plane(const uint16_t *src, const uint16_t *pred, int stride, int width,
+                      int height, int tx_size, unsigned type_mask, int bd, const OrcQuant *q,
+                      int rdmult, OrcRdoBlock *out, int32_t *qcoeff, int32_t *dqcoeff,
+                      int threads, int px) {
   const int W = orc_tx_w(tx_size), H = orc_tx_h(tx_size);
   const int bh = height / H;
   RdoJob base;
@@ -111,6 +163,7 @@ long orc_rdo_plane(const uint16_t *src, const uint16_t *pred, int stride, int wi
   base.out = out;
   base.qcoeff = qcoeff;
   base.dqcoeff = dqcoeff;
+  base.px = px;
   for (int t = 0; t < 16; ++t)
     if ((type_mask >> t) & 1) base.types[base.ntypes++] = t;
   if (threads < 1) threads = 1;
@@ -128,6 +181,22 @@ long orc_rdo_plane(const uint16_t *src, const uint16_t *pred, int stride, int wi
   if (threads > 1)
     for (int i = 0; i < threads; ++i) pthread_join(tid[i], NULL);
   return (long)bh * (width / W);
+}
+
+long orc_rdo_plane(const uint16_t *src, const uint16_t *pred, int stride, int width,
+                   int height, int tx_size, unsigned type_mask, int bd, const OrcQuant *q,
+                   int rdmult, OrcRdoBlock *out, int32_t *qcoeff, int32_t *dqcoeff,
+                   int threads) {
+  return rdo_plane(src, pred, stride, width, height, tx_size, type_mask, bd, q, rdmult, out,
+                   qcoeff, dqcoeff, threads, 0);
+}
+
+long orc_rdo_plane_px(const uint16_t *src, const uint16_t *pred, int stride, int width,
+                      int height, int tx_size, unsigned type_mask, int bd, const OrcQuant *q,
+                      int rdmult, OrcRdoBlock *out, int32_t *qcoeff, int32_t *dqcoeff,
+                      int threads) {
+  return rdo_plane(src, pred, stride, width, height, tx_size, type_mask, bd, q, rdmult, out,
+                   qcoeff, dqcoeff, threads, 1);
 }
 
 /* Per 64x64 SB: the size (of `sizes`, largest area first) whose full blocks

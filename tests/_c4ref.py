@@ -13,13 +13,14 @@ def planes(bd, seed, Wp=384, Hp=192):
     return src.astype(np.uint16), pred.astype(np.uint16)
 
 
-def oracle_frame(src, pred, bd, masks, rdmult, threads=8):
-    """C4 frame reference: per-size oracle decisions, the per-SB TX-size
-    choice (lowest summed rd cost, ties to the larger size) and the
-    reconstruction with the oracle's inverse transform."""
+def oracle_frame(src, pred, bd, masks, rdmult, threads=8, px=False):
+    """C4 frame reference: per-size oracle decisions (px: pixel-domain
+    distortion), the per-SB TX-size choice (lowest summed rd cost, ties to
+    the larger size) and the reconstruction with the oracle's inverse
+    transform."""
     H, W = src.shape
     q = O.build_quant(bd, 128)
-    per = {s: O.rdo_plane(src, pred, s, m, bd, q, rdmult, threads=threads)
+    per = {s: O.rdo_plane(src, pred, s, m, bd, q, rdmult, threads=threads, px=px)
            for s, m in masks.items()}
     sizes = sorted(masks, key=lambda s: -O.TX_W[s] * O.TX_H[s])
     sbw, sbh = (W + 63) // 64, (H + 63) // 64
@@ -59,14 +60,15 @@ def oracle_frame(src, pred, bd, masks, rdmult, threads=8):
 
 
 
-def oracle_frame_c(src, pred, bd, masks, rdmult, threads=8):
+def oracle_frame_c(src, pred, bd, masks, rdmult, threads=8, px=False):
     """oracle_frame with the SB decision and reconstruction in C
     (orc_rdo_reconstruct); used as bench.py's C4 CPU baseline."""
     import ctypes
     H, W = src.shape
     q = O.build_quant(bd, 128)
     sizes = sorted(masks, key=lambda s: -O.TX_W[s] * O.TX_H[s])
-    per = {s: O.rdo_plane(src, pred, s, masks[s], bd, q, rdmult, threads=threads) for s in sizes}
+    per = {s: O.rdo_plane(src, pred, s, masks[s], bd, q, rdmult, threads=threads, px=px)
+           for s in sizes}
     L = O.lib()
     vp = ctypes.c_void_p
     L.orc_rdo_reconstruct.argtypes = [ctypes.c_int, vp, vp, vp, ctypes.c_int, ctypes.c_int, vp,

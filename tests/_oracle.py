@@ -381,12 +381,13 @@ RDO_DTYPE = np.dtype([("best_type", "<i4"), ("eob", "<i4"), ("rate", "<i4"), ("s
                       ("dist", "<i8"), ("sse", "<i8"), ("rdcost", "<i8")], align=True)
 
 
-def rdo_plane(src, pred, tx_size, type_mask, bd, q, rdmult, threads=1):
-    """orc_rdo_plane over u16 planes of equal shape; returns (records,
-    qcoeff[block, n], dqcoeff[block, n])."""
+def rdo_plane(src, pred, tx_size, type_mask, bd, q, rdmult, threads=1, px=False):
+    """orc_rdo_plane (px: orc_rdo_plane_px, pixel-domain distortion) over u16
+    planes of equal shape; returns (records, qcoeff[block, n], dqcoeff[block, n])."""
     L = lib()
-    L.orc_rdo_plane.restype = ctypes.c_long
-    L.orc_rdo_plane.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
+    fn = L.orc_rdo_plane_px if px else L.orc_rdo_plane
+    fn.restype = ctypes.c_long
+    fn.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
                                 ctypes.c_int, ctypes.c_int, ctypes.c_uint, ctypes.c_int,
                                 ctypes.POINTER(OrcQuant), ctypes.c_int, ctypes.c_void_p,
                                 ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
@@ -398,6 +399,6 @@ def rdo_plane(src, pred, tx_size, type_mask, bd, q, rdmult, threads=1):
     out = np.zeros(nb, RDO_DTYPE)
     qc = np.zeros((nb, n), np.int32)
     dq = np.zeros((nb, n), np.int32)
-    L.orc_rdo_plane(P(src), P(pred), W, W, H, tx_size, type_mask, bd, ctypes.byref(q), rdmult,
-                    P(out), P(qc), P(dq), threads)
+    fn(P(src), P(pred), W, W, H, tx_size, type_mask, bd, ctypes.byref(q), rdmult, P(out), P(qc),
+       P(dq), threads)
     return out, qc, dq

@@ -1,5 +1,6 @@
 """GPU parity of the 64-point forward transforms and of the C4 fused TX-type
-RDO (lavish_rdo_plane) against the oracle (oracle/oracle_txfm.c,
+RDO (lavish_rdo_plane, and lavish_rdo_plane_px with pixel-domain
+distortion) against the oracle (oracle/oracle_txfm.c,
 oracle/oracle_rdo.c): coefficients, eobs, decision records (best type, eob,
 rate, satd, distortion, sse, rd cost) and the winner's qcoeff / dqcoeff, all
 bit-exact."""
@@ -120,3 +121,78 @@ def test_rdo_frame_and_reconstruct(L, bd):
     np.testing.assert_array_equal(fr.sb_tx_size.cpu().numpy(), choice)
     np.testing.assert_array_equal(fr.recon.cpu().numpy().view(np.uint16), recon)
     assert len(np.unique(choice)) > 1
+
+
+# ---- pixel-domain distortion (lavish_rdo_plane_px / lavish_rdo_frame_px) ----
+
+@pytest.mark.parametrize("s,mask", C4_CASES + [(15, 0x0201), (7, 0xFFFF), (14, 0xFFFF)])
+@pytest.mark.parametrize("bd", [10, 8, 12])
+def test_rdo_plane_px_vs_oracle(L, s, mask, bd):
+    import torch
+    src, pred = _planes(bd, 90 + s)
+    q = O.build_quant(bd, 128)
+    qp = L.build_quant_params(bd, 128, L.QUANT_FP)
+    rdmult = 1500 + 13 * s
+    exp, eq, ed = O.rdo_plane(src, pred, s, mask, bd, q, rdmult, threads=8, px=True)
+    out = L.rdo_plane(torch.from_numpy(src.view(np.int16)).cuda(),
+                      torch.from_numpy(pred.view(np.int16)).cuda(), s, mask, qp, rdmult, bd,
+                      px=True)
+    got = L.rdo_records(out)
+    for f in ("best_type", "eob", "rate", "satd", "dist", "sse", "rdcost"):
+        np.testing.assert_array_equal(got[f], exp[f], err_msg=f)
+    np.testing.assert_array_equal(out["qcoeff"].cpu().numpy(), eq)
+    np.testing.assert_array_equal(out["dqcoeff"].cpu().numpy(), ed)
+    # pixel-domain distortion differs from the TX-domain one somewhere
+    td, _, _ = O.rdo_plane(src, pred, s, mask, bd, q, rdmult, threads=8)
+    assert (td["dist"] != exp["dist"]).any()
+
+
+def test_rdo_px_high_energy(L):
+    """Full-range random content: every block is high-energy, so the
+    TX-domain fallbacks (and the TX_64X64 quadrant-energy rule) are taken."""
+    import torch
+    rng = np.random.default_rng(5)
+    for bd in (10, 12):
+        mx = (1 << bd) - 1
+        src = rng.integers(0, mx + 1, size=(128, 192)).astype(np.uint16)
+        pred = rng.integers(0, mx + 1, size=(128, 192)).astype(np.uint16)
+        q = O.build_quant(bd, 40)
+        qp = L.build_quant_params(bd, 40, L.QUANT_FP)
+        for s, mask in ((2, 0xFFFF), (4, 1), (3, 0x201), (0, 0xFFFF), (17, 1)):
+            exp, _, _ = O.rdo_plane(src, pred, s, mask, bd, q, 777, px=True)
+            out = L.rdo_plane(torch.from_numpy(src.view(np.int16)).cuda(),
+                              torch.from_numpy(pred.view(np.int16)).cuda(), s, mask, qp, 777,
+                              bd, px=True)
+            got = L.rdo_records(out)
+            for f in ("best_type", "eob", "rate", "satd", "dist", "sse", "rdcost"):
+                np.testing.assert_array_equal(got[f], exp[f], err_msg="%d %d %s" % (bd, s, f))
+
+
+def test_rdo_px_64_rejects_several_types(L):
+    import torch
+    src, pred = _planes(10, 3)
+    qp = L.build_quant_params(10, 128, L.QUANT_FP)
+    with pytest.raises(ValueError):
+        L.rdo_plane(torch.from_numpy(src.view(np.int16)).cuda(),
+                    torch.from_numpy(pred.view(np.int16)).cuda(), 4, 0x201, qp, 100, 10,
+                    px=True)
+
+
+@pytest.mark.parametrize("bd", [10, 8])
+def test_rdo_frame_px_and_reconstruct(L, bd):
+    import torch
+    src, pred = _planes(bd, 78, Wp=328, Hp=200)
+    masks = dict(L.C4_TYPE_MASKS)
+    rdmult = 2000
+    per, choice, recon = _oracle_frame(src, pred, bd, masks, rdmult, px=True)
+    ts = torch.from_numpy(src.view(np.int16)).cuda()
+    tp = torch.from_numpy(pred.view(np.int16)).cuda()
+    fr = L.RdoFrame(ts)
+    L.rdo_frame(ts, tp, fr, L.build_quant_params(bd, 128, L.QUANT_FP), rdmult, bd, px=True)
+    for s in masks:
+        got = L.rdo_records(fr.outs[s])
+        for f in ("best_type", "eob", "dist", "sse", "rdcost"):
+            np.testing.assert_array_equal(got[f], per[s][0][f], err_msg="%d %s" % (s, f))
+        np.testing.assert_array_equal(fr.outs[s]["dqcoeff"].cpu().numpy(), per[s][2])
+    np.testing.assert_array_equal(fr.sb_tx_size.cpu().numpy(), choice)
+    np.testing.assert_array_equal(fr.recon.cpu().numpy().view(np.uint16), recon)
