@@ -1,0 +1,353 @@
+// subpel.hip -- batched sub-pixel motion refinement for gfx950 (SURVEY.md
+// 8(f) rank 2).
+//
+// Reference (one block, one reference, one CPU thread), the speed >= 4
+// subpel_search_method SUBPEL_TREE_PRUNED_MORE without a cost list:
+//   av1_find_best_sub_pixel_tree_pruned_more (av1/encoder/mcomp.c:2907-2981)
+//   -> setup_center_error (:2781-2838, vf at the full-pel start)
+//   -> two_level_checks_fast (:2675) per half / quarter / (hp) eighth step:
+//      first_level_check_fast (:2566: left, right, up, down, then the
+//      diagonal toward the cheaper sides) and, with iters_per_step > 1,
+//      second_level_check_fast (:2608)
+//   -> check_better_fast (:2496): in-range test, estimated_pref_error =
+//      svf = aom_sub_pixel_variance (bilinear, aom_dsp/variance.c:73-145) +
+//      mv_err_cost_ (:290-323), "strictly better" update.
+//
+// Here one wave64 owns one (block, reference) job.  Every check of a round
+// whose candidates are known in advance (the 4 cardinal points, the 2-3
+// second-level points) is evaluated at once: each lane owns 4-pixel row
+// segments of the block (source words kept in VGPRs), reads the 5 bytes of
+// rows y and y+1 it needs per candidate (two dword loads + v_alignbyte
+// each), applies the two bilinear passes with the reference's rounding and
+// accumulates (sum, sse); wave sums end in SGPRs and the sequential
+// check_better_fast updates run on the scalar unit in the reference's order.
+#include "lavish_internal.h"
+
+namespace lavish {
+namespace {
+
+struct SJob {
+  int64_t src_off, ref_off;
+  int16_t start_row, start_col, ref_mv_row, ref_mv_col;
+  int16_t col_min, col_max, row_min, row_max;
+};
+static_assert(sizeof(SJob) == sizeof(LavishSubpelJob), "job layout");
+static_assert(sizeof(LavishSubpelResult) == 16, "result layout");
+
+__constant__ uint8_t kBil2t[8][2] = {{128, 0}, {112, 16}, {96, 32}, {80, 48},
+                                     {64, 64}, {48, 80},  {32, 96}, {16, 112}};
+
+__device__ __forceinline__ uint32_t wave_total(uint32_t v) {
+  v += __shfl_xor(v, 1);
+  v += __shfl_xor(v, 2);
+  v += __shfl_xor(v, 4);
+  v += __shfl_xor(v, 8);
+  v += __shfl_xor(v, 16);
+  v += __shfl_xor(v, 32);
+  return (uint32_t)__builtin_amdgcn_readfirstlane((int)v);
+}
+
+// 5 consecutive bytes at p as (dword of bytes 0..3, byte 4) from two
+// dword-aligned loads
+__device__ __forceinline__ void load5(const uint8_t* p, uint32_t& lo, uint32_t& hi) {
+  typedef const __attribute__((address_space(1))) uint32_t* gptr;
+  const uintptr_t a = (uintptr_t)p;
+  const gptr q = (gptr)(a & ~(uintptr_t)3);
+  const uint32_t sh = (uint32_t)(a & 3);
+  const uint32_t w0 = q[0], w1 = q[1];
+  lo = __builtin_amdgcn_alignbyte(w1, w0, sh);
+  hi = (sh == 0 ? w1 : (w1 >> (8 * sh))) & 0xFF;
+}
+
+template <int W, int H>
+struct Sp {
+  static constexpr int SEG = W * H / 4;              // 4-pixel row segments
+  static constexpr int NSEG = (SEG + 63) / 64;       // segments per lane
+  static constexpr int SPR = W / 4;                  // segments per row
+  // source words live in VGPRs up to 8 per lane (32x32 and smaller); larger
+  // blocks re-read them with the candidate rows
+  static constexpr bool kCache = NSEG <= 8;
+  static constexpr int NS = kCache ? NSEG : 1;
+};
+
+struct SpCtx {
+  const uint8_t* src;
+  const uint8_t* ref;
+  int ss, rs;
+  int ref_mv_row, ref_mv_col;
+  int col_min, col_max, row_min, row_max;
+  int lambda;  // mv_err_cost_ L1 lambda (0: MV_COST_NONE)
+};
+
+__device__ __forceinline__ int mv_cost(const SpCtx& c, int row, int col) {
+  return (c.lambda * (abs(row - c.ref_mv_row) + abs(col - c.ref_mv_col))) >> 3;
+}
+__device__ __forceinline__ bool in_range(const SpCtx& c, int row, int col) {
+  return col >= c.col_min && col <= c.col_max && row >= c.row_min && row <= c.row_max;
+}
+
+__device__ __forceinline__ void seg4(const SpCtx& c, const uint8_t* base, int y, int x,
+                                     uint32_t sw, int f0, int f1, int g0, int g1, int& sum,
+                                     uint32_t& sse) {
+  uint32_t a0, a4, b0, b4;
+  load5(base + (int64_t)y * c.rs + x, a0, a4);
+  load5(base + (int64_t)(y + 1) * c.rs + x, b0, b4);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int p0 = (a0 >> (8 * i)) & 0xFF, p1 = i < 3 ? (a0 >> (8 * i + 8)) & 0xFF : a4;
+    const int q0 = (b0 >> (8 * i)) & 0xFF, q1 = i < 3 ? (b0 >> (8 * i + 8)) & 0xFF : b4;
+    const int h0 = (p0 * f0 + p1 * f1 + 64) >> 7;  // first pass (FILTER_BITS 7)
+    const int h1 = (q0 * f0 + q1 * f1 + 64) >> 7;
+    const int v = ((h0 * g0 + h1 * g1 + 64) >> 7) & 0xFF;  // second pass -> uint8
+    const int d = v - (int)((sw >> (8 * i)) & 0xFF);
+    sum += d;
+    sse += (uint32_t)(d * d);
+  }
+}
+
+// (sum, sse) of src - bilinear(ref at mv) over this lane's segments
+template <int W, int H>
+__device__ __forceinline__ void seg_err(const SpCtx& c, const uint32_t (&sv)[Sp<W, H>::NS],
+                                        int lane, int row, int col, int& sum, uint32_t& sse) {
+  using S = Sp<W, H>;
+  const int xo = col & 7, yo = row & 7;
+  const int f0 = kBil2t[xo][0], f1 = kBil2t[xo][1];
+  const int g0 = kBil2t[yo][0], g1 = kBil2t[yo][1];
+  const uint8_t* base = c.ref + (int64_t)(row >> 3) * c.rs + (col >> 3);
+  if constexpr (S::kCache) {
+#pragma unroll
+    for (int n = 0; n < S::NS; ++n) {
+      const int sg = lane + 64 * n;
+      if (sg < S::SEG)
+        seg4(c, base, sg / S::SPR, 4 * (sg % S::SPR), sv[n], f0, f1, g0, g1, sum, sse);
+    }
+  } else {
+#pragma unroll 1
+    for (int sg = lane; sg < S::SEG; sg += 64) {
+      const int y = sg / S::SPR, x = 4 * (sg % S::SPR);
+      uint32_t sw, dummy;
+      load5(c.src + (int64_t)y * c.ss + x, sw, dummy);
+      seg4(c, base, y, x, sw, f0, f1, g0, g1, sum, sse);
+    }
+  }
+}
+
+struct Best {
+  int row, col;
+  uint32_t besterr, sse1;
+  int distortion;
+};
+
+// evaluate up to 4 candidates (wave-uniform mvs), then the sequential
+// check_better_fast updates; returns each candidate's cost (INT_MAX when out
+// of range) through cost[]
+template <int W, int H, int N>
+__device__ __forceinline__ void check_n(const SpCtx& c, const uint32_t (&sv)[Sp<W, H>::NS],
+                                        int lane, const int (&r)[N], const int (&cl)[N],
+                                        Best& b, uint32_t (&cost)[N]) {
+  int sum[N];
+  uint32_t sse[N];
+  bool ok[N];
+#pragma unroll
+  for (int k = 0; k < N; ++k) {
+    sum[k] = 0;
+    sse[k] = 0;
+    ok[k] = in_range(c, r[k], cl[k]);
+    if (ok[k]) seg_err<W, H>(c, sv, lane, r[k], cl[k], sum[k], sse[k]);
+  }
+#pragma unroll
+  for (int k = 0; k < N; ++k) {
+    cost[k] = 0x7FFFFFFFu;  // INT_MAX
+    if (!ok[k]) continue;
+    const int ts = (int)wave_total((uint32_t)sum[k]);
+    const uint32_t tq = wave_total(sse[k]);
+    const uint32_t var = tq - (uint32_t)(((int64_t)ts * ts) / (W * H));
+    cost[k] = (uint32_t)mv_cost(c, r[k], cl[k]) + var;
+    if (cost[k] < b.besterr) {
+      b.besterr = cost[k];
+      b.row = r[k];
+      b.col = cl[k];
+      b.distortion = (int)var;
+      b.sse1 = tq;
+    }
+  }
+}
+
+template <int W, int H>
+__device__ void two_level(const SpCtx& c, const uint32_t (&sv)[Sp<W, H>::NS], int lane, int tr,
+                          int tc, int hstep, int iters, Best& b) {
+  uint32_t cst[4];
+  {
+    const int r[4] = {tr, tr, tr - hstep, tr + hstep};
+    const int cl[4] = {tc - hstep, tc + hstep, tc, tc};
+    check_n<W, H, 4>(c, sv, lane, r, cl, b, cst);
+  }
+  // get_best_diag_step: toward the cheaper of up/down and left/right
+  const int dr = cst[2] <= cst[3] ? -hstep : hstep;
+  const int dc = cst[0] <= cst[1] ? -hstep : hstep;
+  uint32_t d1[1];
+  {
+    const int r[1] = {tr + dr};
+    const int cl[1] = {tc + dc};
+    check_n<W, H, 1>(c, sv, lane, r, cl, b, d1);
+  }
+  if (iters <= 1) return;
+  const int br = b.row, bc = b.col;
+  if (tr != br && tc != bc) {
+    const int r[2] = {br, br + dr};
+    const int cl[2] = {bc + dc, bc};
+    uint32_t d2[2];
+    check_n<W, H, 2>(c, sv, lane, r, cl, b, d2);
+  } else if (tr == br && tc != bc) {
+    const int r[3] = {br + hstep, br - hstep, br - dr};
+    const int cl[3] = {bc + dc, bc + dc, bc};
+    uint32_t d3[3];
+    check_n<W, H, 3>(c, sv, lane, r, cl, b, d3);
+  } else if (tr != br && tc == bc) {
+    const int r[3] = {br + dr, br + dr, br};
+    const int cl[3] = {bc + hstep, bc - hstep, bc - dc};
+    uint32_t d3[3];
+    check_n<W, H, 3>(c, sv, lane, r, cl, b, d3);
+  }
+}
+
+template <int W, int H>
+__global__ __launch_bounds__(256) void subpel_kernel(const uint8_t* __restrict__ src, int ss,
+                                                     const uint8_t* __restrict__ ref, int rs,
+                                                     const SJob* __restrict__ jobs, int njobs,
+                                                     const LavishDiamondResult* __restrict__ fp,
+                                                     int forced_stop, int allow_hp, int iters,
+                                                     int lambda, LavishSubpelResult* out) {
+  using S = Sp<W, H>;
+  // XCD-aware: consecutive job quads share an XCD's L2
+  const int nwg = gridDim.x;  // multiple of 8
+  const int wg = (blockIdx.x & 7) * (nwg >> 3) + (blockIdx.x >> 3);
+  const int lane = threadIdx.x & 63;
+  const int j = wg * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  if (j >= njobs) return;
+  const SJob jb = jobs[j];
+  SpCtx c;
+  c.src = src + jb.src_off;
+  c.ref = ref + jb.ref_off;
+  c.ss = ss;
+  c.rs = rs;
+  c.ref_mv_row = jb.ref_mv_row;
+  c.ref_mv_col = jb.ref_mv_col;
+  c.col_min = jb.col_min;
+  c.col_max = jb.col_max;
+  c.row_min = jb.row_min;
+  c.row_max = jb.row_max;
+  c.lambda = lambda;
+  // source words of this lane's segments
+  uint32_t sv[S::NS];
+#pragma unroll
+  for (int n = 0; n < S::NS; ++n) {
+    const int sg = lane + 64 * n;
+    sv[n] = 0;
+    if (S::kCache && sg < S::SEG) {
+      const int y = sg / S::SPR, x = 4 * (sg % S::SPR);
+      uint32_t lo, hi;
+      load5(c.src + (int64_t)y * ss + x, lo, hi);
+      sv[n] = lo;
+    }
+  }
+  // setup_center_error: vf at the full-pel start (the bilinear passes with
+  // zero offsets reproduce the plain pixels exactly)
+  // start: the job's, or the full-pel search result of the same job index
+  const int start_row = fp ? 8 * fp[j].best_row : jb.start_row;
+  const int start_col = fp ? 8 * fp[j].best_col : jb.start_col;
+  Best b;
+  b.row = start_row;
+  b.col = start_col;
+  {
+    int sum = 0;
+    uint32_t sse = 0;
+    seg_err<W, H>(c, sv, lane, b.row, b.col, sum, sse);
+    const int ts = (int)wave_total((uint32_t)sum);
+    const uint32_t tq = wave_total(sse);
+    const uint32_t var = tq - (uint32_t)(((int64_t)ts * ts) / (W * H));
+    b.distortion = (int)var;
+    b.sse1 = tq;
+    b.besterr = var + (uint32_t)mv_cost(c, b.row, b.col);
+  }
+  if (forced_stop != 3) {  // FULL_PEL
+    int hstep = 4;         // INIT_SUBPEL_STEP_SIZE: half pel
+    two_level<W, H>(c, sv, lane, start_row, start_col, hstep, iters, b);
+    if (forced_stop < 2) {  // below HALF_PEL
+      hstep >>= 1;
+      two_level<W, H>(c, sv, lane, b.row, b.col, hstep, iters, b);
+    }
+    if (allow_hp && forced_stop == 0) {  // EIGHTH_PEL
+      hstep >>= 1;
+      two_level<W, H>(c, sv, lane, b.row, b.col, hstep, iters, b);
+    }
+  }
+  if (lane == 0) {
+    LavishSubpelResult r;
+    r.best_row = (int16_t)b.row;
+    r.best_col = (int16_t)b.col;
+    r.besterr = b.besterr;
+    r.distortion = b.distortion;
+    r.sse = b.sse1;
+    out[j] = r;
+  }
+}
+
+template <int W, int H>
+void launch(const uint8_t* src, int ss, const uint8_t* ref, int rs, const LavishSubpelJob* jobs,
+            int njobs, const LavishDiamondResult* fp, int forced_stop, int allow_hp, int iters,
+            int lambda, LavishSubpelResult* out, hipStream_t s) {
+  int nwg = (njobs + 3) / 4;
+  nwg = (nwg + 7) & ~7;
+  hipLaunchKernelGGL((subpel_kernel<W, H>), dim3(nwg), dim3(256), 0, s, src, ss, ref, rs,
+                     (const SJob*)jobs, njobs, fp, forced_stop, allow_hp, iters, lambda, out);
+}
+
+int subpel_batch(const uint8_t* src, int src_stride, const uint8_t* ref, int ref_stride, int w,
+                 int h, const LavishSubpelJob* jobs, int njobs, const LavishDiamondResult* fp,
+                 int forced_stop, int allow_hp, int iters_per_step, int mv_cost_type,
+                 LavishSubpelResult* out, hipStream_t s) {
+  if (njobs <= 0) return 0;
+  if (forced_stop < 0 || forced_stop > 3) return -1;
+  if (mv_cost_type < 1 || mv_cost_type > 4) return -2;  // MV_COST_ENTROPY not supported
+  if (iters_per_step < 1 || iters_per_step > 2) return -4;
+  // mv_err_cost_ lambdas: SSE_LAMBDA_LOWRES 2, MIDRES 0, HDRES 1; NONE 0
+  const int lambda = mv_cost_type == 1 ? 2 : mv_cost_type == 3 ? 1 : 0;
+#define LAVISH_SP_CASE(W, H)                                                                   \
+  if (w == W && h == H) {                                                                      \
+    launch<W, H>(src, src_stride, ref, ref_stride, jobs, njobs, fp, forced_stop, allow_hp,     \
+                 iters_per_step, lambda, out, s);                                              \
+    LAVISH_CHECK(hipGetLastError());                                                           \
+    return 0;                                                                                  \
+  }
+  LAVISH_ENCODER_BLOCK_SIZES(LAVISH_SP_CASE)
+#undef LAVISH_SP_CASE
+  return -3;
+}
+
+}  // namespace
+}  // namespace lavish
+
+using namespace lavish;
+
+extern "C" int lavish_subpel_search_batch(const uint8_t* src, int src_stride, const uint8_t* ref,
+                                          int ref_stride, int w, int h,
+                                          const LavishSubpelJob* jobs, int njobs,
+                                          int forced_stop, int allow_hp, int iters_per_step,
+                                          int mv_cost_type, LavishSubpelResult* out,
+                                          void* stream) {
+  return subpel_batch(src, src_stride, ref, ref_stride, w, h, jobs, njobs, nullptr, forced_stop,
+                      allow_hp, iters_per_step, mv_cost_type, out, (hipStream_t)stream);
+}
+
+extern "C" int lavish_subpel_search_after_diamond(const uint8_t* src, int src_stride,
+                                                  const uint8_t* ref, int ref_stride, int w,
+                                                  int h, const LavishSubpelJob* jobs,
+                                                  const LavishDiamondResult* fullpel, int njobs,
+                                                  int forced_stop, int allow_hp,
+                                                  int iters_per_step, int mv_cost_type,
+                                                  LavishSubpelResult* out, void* stream) {
+  if (fullpel == nullptr) return -5;
+  return subpel_batch(src, src_stride, ref, ref_stride, w, h, jobs, njobs, fullpel, forced_stop,
+                      allow_hp, iters_per_step, mv_cost_type, out, (hipStream_t)stream);
+}

@@ -1,8 +1,9 @@
-"""C3 full-pixel DIAMOND motion search on the MI355X backend
-(lavish_diamond_search_batch) plus the host-side job construction the
-reference does per block before calling av1_full_pixel_search:
-av1_set_mv_limits (av1/encoder/mcomp.h:225-258) and av1_set_mv_search_range
-(av1/encoder/mcomp.c:206-234)."""
+"""C3 full-pixel DIAMOND motion search and the sub-pixel refinement that
+follows it on the MI355X backend (lavish_diamond_search_batch,
+lavish_subpel_search_batch) plus the host-side job construction the
+reference does per block: av1_set_mv_limits (av1/encoder/mcomp.h:225-258),
+av1_set_mv_search_range (av1/encoder/mcomp.c:206-234) and
+av1_set_subpel_mv_search_range (av1/encoder/mcomp.h:357-373)."""
 import ctypes
 
 import numpy as np
@@ -29,9 +30,9 @@ _lib.lavish_diamond_search_batch.argtypes = [_vp, _i32, _vp, _i32, _i32, _i32, _
 _lib.lavish_diamond_search_batch.restype = _i32
 
 
-def mv_limits(mi_rows, mi_cols, mi_row, mi_col, mi_height, mi_width, border, ref_mv=(0, 0)):
-    """(col_min, col_max, row_min, row_max) as av1_set_mv_limits followed by
-    av1_set_mv_search_range(ref_mv) (ref_mv in 1/8 pel, (row, col))."""
+def block_mv_limits(mi_rows, mi_cols, mi_row, mi_col, mi_height, mi_width, border):
+    """x->mv_limits: (col_min, col_max, row_min, row_max) of av1_set_mv_limits
+    (full pel)."""
     e2 = 2 * AOM_INTERP_EXTEND
     row_min = max(-(mi_row * MI_SIZE + border - e2), -((mi_row + mi_height) * MI_SIZE + e2))
     row_max = min((mi_rows - mi_row - mi_height) * MI_SIZE + border - e2,
@@ -39,6 +40,29 @@ def mv_limits(mi_rows, mi_cols, mi_row, mi_col, mi_height, mi_width, border, ref
     col_min = max(-(mi_col * MI_SIZE + border - e2), -((mi_col + mi_width) * MI_SIZE + e2))
     col_max = min((mi_cols - mi_col - mi_width) * MI_SIZE + border - e2,
                   (mi_cols - mi_col) * MI_SIZE + e2)
+    return col_min, col_max, row_min, row_max
+
+
+def subpel_limits(lim, ref_mv=(0, 0)):
+    """av1_set_subpel_mv_search_range (mcomp.h:357-373): SubpelMvLimits (1/8
+    pel) from x->mv_limits and ref_mv ((row, col), 1/8 pel)."""
+    col_min, col_max, row_min, row_max = lim
+    max_mv = MAX_FULL_PEL_VAL * 8
+    r, c = ref_mv
+    minc = max(col_min * 8, c - max_mv)
+    maxc = min(col_max * 8, c + max_mv)
+    minr = max(row_min * 8, r - max_mv)
+    maxr = min(row_max * 8, r + max_mv)
+    maxc, maxr = max(minc, maxc), max(minr, maxr)
+    return (max(MV_LOW + 1, minc), min(MV_UPP - 1, maxc), max(MV_LOW + 1, minr),
+            min(MV_UPP - 1, maxr))
+
+
+def mv_limits(mi_rows, mi_cols, mi_row, mi_col, mi_height, mi_width, border, ref_mv=(0, 0)):
+    """(col_min, col_max, row_min, row_max) as av1_set_mv_limits followed by
+    av1_set_mv_search_range(ref_mv) (ref_mv in 1/8 pel, (row, col))."""
+    col_min, col_max, row_min, row_max = block_mv_limits(mi_rows, mi_cols, mi_row, mi_col,
+                                                         mi_height, mi_width, border)
     r, c = ref_mv
     cmin = max(((c + 7) >> 3) - MAX_FULL_PEL_VAL, (MV_LOW >> 3) + 1)
     rmin = max(((r + 7) >> 3) - MAX_FULL_PEL_VAL, (MV_LOW >> 3) + 1)
@@ -102,3 +126,92 @@ def diamond_search_batch(src, ref, w, h, jobs, step_param=0, mv_cost_type=MV_COS
 
 def results_numpy(out):
     return out.cpu().numpy().view(RESULT_DTYPE)
+
+
+# ------------------------------------------------------- sub-pixel search --
+SUBPEL_JOB_DTYPE = np.dtype([("src_off", "<i8"), ("ref_off", "<i8"), ("start_row", "<i2"),
+                             ("start_col", "<i2"), ("ref_mv_row", "<i2"), ("ref_mv_col", "<i2"),
+                             ("col_min", "<i2"), ("col_max", "<i2"), ("row_min", "<i2"),
+                             ("row_max", "<i2")], align=True)
+SUBPEL_RESULT_DTYPE = np.dtype([("best_row", "<i2"), ("best_col", "<i2"), ("besterr", "<u4"),
+                                ("distortion", "<i4"), ("sse", "<u4")], align=True)
+assert SUBPEL_JOB_DTYPE.itemsize == 32 and SUBPEL_RESULT_DTYPE.itemsize == 16
+EIGHTH_PEL, QUARTER_PEL, HALF_PEL, FULL_PEL = 0, 1, 2, 3
+
+_lib.lavish_subpel_search_batch.argtypes = [_vp, _i32, _vp, _i32, _i32, _i32, _vp, _i32, _i32,
+                                            _i32, _i32, _i32, _vp, _vp]
+_lib.lavish_subpel_search_batch.restype = _i32
+_lib.lavish_subpel_search_after_diamond.argtypes = [_vp, _i32, _vp, _i32, _i32, _i32, _vp, _vp,
+                                                    _i32, _i32, _i32, _i32, _i32, _vp, _vp]
+_lib.lavish_subpel_search_after_diamond.restype = _i32
+
+
+def subpel_jobs(width, height, border, bw, bh, fullpel_jobs, fullpel_results, ref_mv=(0, 0)):
+    """Sub-pixel jobs continuing the full-pel jobs of frame_jobs (same order):
+    start = the full-pel best x 8, SubpelMvLimits from the block's
+    x->mv_limits and ref_mv."""
+    mi_rows = ((height + 7) & ~7) // MI_SIZE
+    mi_cols = ((width + 7) & ~7) // MI_SIZE
+    nbx, nby = width // bw, height // bh
+    ys = np.repeat(np.arange(nby) * bh, nbx)
+    xs = np.tile(np.arange(nbx) * bw, nby)
+    lim = np.array([subpel_limits(block_mv_limits(mi_rows, mi_cols, y // MI_SIZE, x // MI_SIZE,
+                                                  bh // MI_SIZE, bw // MI_SIZE, border), ref_mv)
+                    for y, x in zip(ys, xs)])
+    nrefs = len(fullpel_jobs) // len(lim)
+    lim = np.concatenate([lim] * nrefs)
+    out = np.zeros(len(fullpel_jobs), SUBPEL_JOB_DTYPE)
+    out["src_off"] = fullpel_jobs["src_off"]
+    out["ref_off"] = fullpel_jobs["ref_off"]
+    out["start_row"] = fullpel_results["best_row"].astype(np.int32) * 8
+    out["start_col"] = fullpel_results["best_col"].astype(np.int32) * 8
+    out["ref_mv_row"], out["ref_mv_col"] = ref_mv
+    out["col_min"], out["col_max"], out["row_min"], out["row_max"] = lim.T
+    return out
+
+
+def subpel_search_batch(src, ref, w, h, jobs, forced_stop=EIGHTH_PEL, allow_hp=False,
+                        iters_per_step=1, mv_cost_type=MV_COST_L1_HDRES, out=None, stream=None):
+    """lavish_subpel_search_batch over device planes (as diamond_search_batch)
+    and a device byte tensor of SUBPEL_JOB_DTYPE records; returns a device
+    byte tensor of SUBPEL_RESULT_DTYPE records."""
+    import torch
+    assert src.dtype == torch.uint8 and ref.dtype == torch.uint8
+    assert src.is_contiguous() and ref.is_contiguous(), "planes must be C-contiguous"
+    nj = jobs.numel() // SUBPEL_JOB_DTYPE.itemsize
+    if out is None:
+        out = torch.empty(nj * SUBPEL_RESULT_DTYPE.itemsize, dtype=torch.uint8,
+                          device=src.device)
+    rc = _lib.lavish_subpel_search_batch(_vp(src.data_ptr()), src.stride(0),
+                                         _vp(ref.data_ptr()), src.stride(0), w, h,
+                                         _vp(jobs.data_ptr()), nj, forced_stop, int(allow_hp),
+                                         iters_per_step, mv_cost_type, _vp(out.data_ptr()),
+                                         _stream_ptr(stream))
+    if rc != 0:
+        raise ValueError("lavish_subpel_search_batch rejected its arguments (rc=%d)" % rc)
+    return out
+
+
+def subpel_after_diamond(src, ref, w, h, jobs, fullpel, forced_stop=EIGHTH_PEL, allow_hp=False,
+                         iters_per_step=1, mv_cost_type=MV_COST_L1_HDRES, out=None,
+                         stream=None):
+    """lavish_subpel_search_after_diamond: as subpel_search_batch with every
+    job starting at the device-resident full-pel result `fullpel` (the
+    RESULT_DTYPE bytes diamond_search_batch returned)."""
+    import torch
+    nj = jobs.numel() // SUBPEL_JOB_DTYPE.itemsize
+    assert fullpel.numel() >= nj * RESULT_DTYPE.itemsize
+    if out is None:
+        out = torch.empty(nj * SUBPEL_RESULT_DTYPE.itemsize, dtype=torch.uint8,
+                          device=src.device)
+    rc = _lib.lavish_subpel_search_after_diamond(
+        _vp(src.data_ptr()), src.stride(0), _vp(ref.data_ptr()), src.stride(0), w, h,
+        _vp(jobs.data_ptr()), _vp(fullpel.data_ptr()), nj, forced_stop, int(allow_hp),
+        iters_per_step, mv_cost_type, _vp(out.data_ptr()), _stream_ptr(stream))
+    if rc != 0:
+        raise ValueError("lavish_subpel_search_after_diamond rejected its arguments (rc=%d)" % rc)
+    return out
+
+
+def subpel_results_numpy(out):
+    return out.cpu().numpy().view(SUBPEL_RESULT_DTYPE)

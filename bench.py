@@ -51,7 +51,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--workload", choices=("rdo", "c2", "c3", "c4", "c4px", "c5"),
+    ap.add_argument("--workload", choices=("rdo", "c2", "c3", "c3sub", "c4", "c4px", "c5"),
                     default="rdo")
     ap.add_argument("--rdmult", type=int, default=2000)
     ap.add_argument("--width", type=int, default=1920)
@@ -95,6 +95,11 @@ def c3_algorithmic_bytes(res, njobs, bw, bh, skip):
 C3_BLOCK = 16
 C3_COST = 3     # MV_COST_L1_HDRES
 C3_SKIP = True  # use_downsampled_sad (>= 720p, speed_features.c:205-209)
+# sub-pixel refinement after the full-pel search (c3sub): SUBPEL_TREE_PRUNED_MORE
+# (speed >= 4), subpel_force_stop EIGHTH_PEL, iters_per_step 1 (speed >= 2),
+# allow_high_precision_mv = qindex < HIGH_PRECISION_MV_QTHRESH (128)
+SUB_FORCED_STOP = 0
+SUB_ITERS = 1
 
 
 def cpu_baseline(args):
@@ -110,7 +115,8 @@ def cpu_baseline(args):
     threads = min(16, os.cpu_count() or 1)
     W, Hs = args.width, 256
     do_c2 = args.workload in ("rdo", "c2")
-    do_c3 = args.workload in ("rdo", "c3")
+    do_c3 = args.workload in ("rdo", "c3", "c3sub")
+    do_sub = args.workload == "c3sub"
     res = synth.residual_plane(W, Hs, 8)
     q = O.build_quant(8, args.qindex)
     sizes = [s for s in range(19) if L.TX_W[s] <= 32 and L.TX_H[s] <= 32]
@@ -125,8 +131,13 @@ def cpu_baseline(args):
             for s in sizes:
                 O.txq_plane(res, s, L.valid_type_mask(s), q, threads=threads)
         if do_c3:
-            O.diamond_batch(src.reshape(-1), refs.reshape(-1), st, C3_BLOCK, C3_BLOCK, jobs, 0,
-                            C3_COST, C3_SKIP, threads=threads)
+            fp = O.diamond_batch(src.reshape(-1), refs.reshape(-1), st, C3_BLOCK, C3_BLOCK, jobs,
+                                 0, C3_COST, C3_SKIP, threads=threads)
+        if do_sub:
+            sj = M.subpel_jobs(W, Hs, args.border, C3_BLOCK, C3_BLOCK, jobs, fp)
+            O.subpel_batch(src.reshape(-1), refs.reshape(-1), st, C3_BLOCK, C3_BLOCK, sj,
+                           SUB_FORCED_STOP, args.qindex < 128, SUB_ITERS, C3_COST,
+                           threads=threads)
         passes += 1
         dt = time.perf_counter() - t0
         if dt >= args.cpu_seconds:
@@ -308,7 +319,8 @@ def main():
 
     W, H = args.width, args.height
     do_c2 = args.workload in ("rdo", "c2")
-    do_c3 = args.workload in ("rdo", "c3")
+    do_c3 = args.workload in ("rdo", "c3", "c3sub")
+    do_sub = args.workload == "c3sub"
     stream = torch.cuda.current_stream()
 
     # C2 input: residual plane (each rank its own frame)
@@ -326,9 +338,19 @@ def main():
                          device="cuda")
     torch.cuda.synchronize()
 
+    if do_sub:
+        sub_jobs = M.to_device(M.subpel_jobs(W, H, args.border, C3_BLOCK, C3_BLOCK, jobs_np,
+                                             np.zeros(len(jobs_np), M.RESULT_DTYPE)))
+        sub_out = torch.empty(len(jobs_np) * M.SUBPEL_RESULT_DTYPE.itemsize, dtype=torch.uint8,
+                              device="cuda")
+
     def c3(on):
         M.diamond_search_batch(tsrc, trefs, C3_BLOCK, C3_BLOCK, tjobs, 0, C3_COST, C3_SKIP,
                                out=c3_out, stream=on)
+        if do_sub:  # chained on the device: starts = the full-pel results
+            M.subpel_after_diamond(tsrc, trefs, C3_BLOCK, C3_BLOCK, sub_jobs, c3_out,
+                                   SUB_FORCED_STOP, args.qindex < 128, SUB_ITERS, C3_COST,
+                                   out=sub_out, stream=on)
 
     overlap = do_c2 and do_c3 and args.overlap
     side = torch.cuda.Stream() if overlap else stream
@@ -423,6 +445,10 @@ def main():
     if do_c3:
         legs.append("C3 DIAMOND full-pel search of every %dx%d block x %d refs (downsampled SAD, "
                     "MV_COST_L1_HDRES, step_param 0)" % (C3_BLOCK, C3_BLOCK, args.refs))
+    if do_sub:
+        legs.append("sub-pel refinement SUBPEL_TREE_PRUNED_MORE to %s pel (bilinear svf, "
+                    "iters_per_step %d) chained on the device"
+                    % ("1/8" if args.qindex < 128 else "1/4", SUB_ITERS))
     line = {
         "metric": METRIC,
         "value": round(value, 2),

@@ -331,6 +331,52 @@ int lavish_diamond_search_batch(const uint8_t *src, int src_stride,
                                 int use_downsampled_sad,
                                 LavishDiamondResult *out, void *stream);
 
+/* ---- sub-pixel refinement ------------------------
+ * av1_find_best_sub_pixel_tree_pruned_more (av1/encoder/mcomp.c:2907-2981;
+ * subpel_search_method SUBPEL_TREE_PRUNED_MORE, speed >= 4) without a cost
+ * list or a repeated-mv list, unscaled reference: setup_center_error at the
+ * start, then two_level_checks_fast at half, quarter (forced_stop <
+ * HALF_PEL) and eighth pel (allow_hp && forced_stop == EIGHTH_PEL), every
+ * check check_better_fast with svf = aom_sub_pixel_variance (bilinear) +
+ * mv_err_cost_.  8-bit planes.  One job per (block, reference): offsets as
+ * LavishDiamondJob, start / ref mv and the SubpelMvLimits
+ * (av1_set_subpel_mv_search_range, mcomp.h:357-373) in 1/8 pel.  The
+ * search reads up to H+1 rows and W+5 bytes per row from the floor of every
+ * in-range candidate.  forced_stop: 0 EIGHTH_PEL .. 3 FULL_PEL;
+ * iters_per_step 1 or 2; mv_cost_type as lavish_diamond_search_batch. */
+typedef struct LavishSubpelJob {
+  int64_t src_off, ref_off;
+  int16_t start_row, start_col;    /* full-pel best x 8 */
+  int16_t ref_mv_row, ref_mv_col;
+  int16_t col_min, col_max, row_min, row_max;
+} LavishSubpelJob;
+
+typedef struct LavishSubpelResult {
+  int16_t best_row, best_col;      /* 1/8 pel */
+  uint32_t besterr;                /* variance + mv cost of the best mv */
+  int32_t distortion;              /* its variance */
+  uint32_t sse;
+} LavishSubpelResult;
+
+int lavish_subpel_search_batch(const uint8_t *src, int src_stride,
+                               const uint8_t *ref, int ref_stride, int w, int h,
+                               const LavishSubpelJob *jobs, int njobs,
+                               int forced_stop, int allow_hp,
+                               int iters_per_step, int mv_cost_type,
+                               LavishSubpelResult *out, void *stream);
+
+/* The same, chained on the device after lavish_diamond_search_batch: job j
+ * starts at fullpel[j].best_{row,col} x 8 (the jobs' start fields are
+ * ignored), so the full-pel and sub-pel searches of a frame need no host
+ * round trip. */
+int lavish_subpel_search_after_diamond(const uint8_t *src, int src_stride,
+                                       const uint8_t *ref, int ref_stride, int w,
+                                       int h, const LavishSubpelJob *jobs,
+                                       const LavishDiamondResult *fullpel,
+                                       int njobs, int forced_stop, int allow_hp,
+                                       int iters_per_step, int mv_cost_type,
+                                       LavishSubpelResult *out, void *stream);
+
 /* ------------------------------------------------------------------------ */
 /* Per-call RTCD shims (host pointers)                                      */
 /* ------------------------------------------------------------------------ */

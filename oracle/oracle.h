@@ -200,6 +200,25 @@ void orc_diamond_batch(const uint8_t *src, int src_stride, const uint8_t *ref,
                        long njobs, int step_param, int mv_cost_type,
                        int skip_sad, OrcDiamondResult *out, int threads);
 
+/* ---- sub-pixel refinement (oracle_subpel.c); layouts = LavishSubpelJob /
+ * LavishSubpelResult.  MVs and limits in 1/8 pel. */
+typedef struct OrcSubpelJob {
+  int64_t src_off, ref_off;
+  int16_t start_row, start_col, ref_mv_row, ref_mv_col;
+  int16_t col_min, col_max, row_min, row_max;
+} OrcSubpelJob;
+typedef struct OrcSubpelResult {
+  int16_t best_row, best_col;
+  uint32_t besterr;
+  int32_t distortion;
+  uint32_t sse;
+} OrcSubpelResult;
+void orc_subpel_batch(const uint8_t *src, int src_stride, const uint8_t *ref,
+                      int ref_stride, int w, int h, const OrcSubpelJob *jobs,
+                      long njobs, int forced_stop, int allow_hp,
+                      int iters_per_step, int mv_cost_type,
+                      OrcSubpelResult *out, int threads);
+
 /* ---- C4: per-block TX-type RDO (oracle_rdo.c); layout = LavishRdoBlock */
 typedef struct OrcRdoBlock {
   int32_t best_type, eob, rate, satd;

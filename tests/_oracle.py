@@ -376,6 +376,25 @@ def diamond_batch(src, ref, stride, w, h, jobs, step_param=0, mv_cost_type=3, sk
     return out
 
 
+SUBPEL_RESULT = np.dtype([("best_row", "<i2"), ("best_col", "<i2"), ("besterr", "<u4"),
+                          ("distortion", "<i4"), ("sse", "<u4")], align=True)
+
+
+def subpel_batch(src, ref, stride, w, h, jobs, forced_stop=0, allow_hp=False, iters=1,
+                 mv_cost_type=3, threads=1):
+    """orc_subpel_batch over SUBPEL_JOB_DTYPE records (lavish_dsp.motion)."""
+    L = lib()
+    L.orc_subpel_batch.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_int,
+                                   ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_long,
+                                   ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                   ctypes.c_void_p, ctypes.c_int]
+    jobs = np.ascontiguousarray(jobs)
+    out = np.zeros(len(jobs), SUBPEL_RESULT)
+    L.orc_subpel_batch(P(src), stride, P(ref), stride, w, h, P(jobs), len(jobs), forced_stop,
+                       int(allow_hp), iters, mv_cost_type, P(out), threads)
+    return out
+
+
 # ------------------------------------------------------------- C4 RDO --
 RDO_DTYPE = np.dtype([("best_type", "<i4"), ("eob", "<i4"), ("rate", "<i4"), ("satd", "<i4"),
                       ("dist", "<i8"), ("sse", "<i8"), ("rdcost", "<i8")], align=True)
@@ -387,10 +406,9 @@ def rdo_plane(src, pred, tx_size, type_mask, bd, q, rdmult, threads=1, px=False)
     L = lib()
     fn = L.orc_rdo_plane_px if px else L.orc_rdo_plane
     fn.restype = ctypes.c_long
-    fn.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
-                                ctypes.c_int, ctypes.c_int, ctypes.c_uint, ctypes.c_int,
-                                ctypes.POINTER(OrcQuant), ctypes.c_int, ctypes.c_void_p,
-                                ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
+    fn.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                   ctypes.c_int, ctypes.c_uint, ctypes.c_int, ctypes.POINTER(OrcQuant),
+                   ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
     src = np.ascontiguousarray(src, dtype=np.uint16)
     pred = np.ascontiguousarray(pred, dtype=np.uint16)
     H, W = src.shape

