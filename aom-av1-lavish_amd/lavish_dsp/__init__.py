@@ -244,6 +244,8 @@ def txq_plane(residual, tx_size, type_mask, qp, bit_depth=8, quant_kind=QUANT_FP
     import torch
     assert residual.dtype == torch.int16 and residual.is_cuda
     assert residual.stride(1) == 1, "residual rows must be contiguous"
+    if not 0 <= tx_size < len(TX_SIZES):
+        raise ValueError("tx_size %d out of range" % tx_size)
     Hh, Ww = residual.shape
     stride = residual.stride(0) if stride is None else stride
     width = Ww if width is None else width
