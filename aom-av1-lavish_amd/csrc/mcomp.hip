@@ -22,6 +22,8 @@
 // is lower, since the mv cost is >= 0), so the walk and every tie are the
 // reference's.  The source block stays in VGPRs for the whole search;
 // reference pixels come from L2 / MALL (a 1080p padded reference is ~2.5 MB).
+#include <type_traits>
+
 #include "lavish_internal.h"
 
 namespace lavish {
@@ -408,11 +410,95 @@ __device__ int full_pixel_diamond(const Ctx& c, int lane, int srow, int scol, in
 
 __device__ __forceinline__ int rawpel(int x) { return (x + 3 + (x >= 0)) >> 3; }  // mv.h:28
 
+// ---------------------------------------------------------------- BIGDIA --
+// av1_init_motion_compensation_bigdia (mcomp.c:498-550): scale 0 has the 4
+// nearest points, scale s >= 1 8 points of radius r = 2^(s-1) / 2r.
+__device__ __forceinline__ void bigdia_site(int s, int i, int& dr, int& dc) {
+  if (s == 0) {
+    dr = (i == 1) ? 1 : (i == 3) ? -1 : 0;
+    dc = (i == 0) ? -1 : (i == 2) ? 1 : 0;
+    return;
+  }
+  const int r = 1 << (s - 1);
+  // (-r,-r) (0,-2r) (r,-r) (2r,0) (r,r) (0,2r) (-r,r) (-2r,0)
+  dr = (i == 0 || i == 6) ? -r : (i == 2 || i == 4) ? r : (i == 3) ? 2 * r : (i == 7) ? -2 * r : 0;
+  dc = (i == 0 || i == 2) ? -r : (i == 4 || i == 6) ? r : (i == 1) ? -2 * r : (i == 5) ? 2 * r : 0;
+}
+
+// fast_bigdia_search -> bigdia_search -> pattern_search (mcomp.c:1017-1245,
+// 1266-1316) with do_init_search 0: from scale 10 - max(8, step_param) down
+// to 0, all candidates of the scale around the centre, then the 3 points
+// around the winning direction until none improves.  (With a cost list the
+// reference finishes scale 0 in a separate block whose mv result is the
+// same for do_init_search 0; the list itself is not produced here.)
+// Lane group g evaluates candidate g; the keyed minimum is the reference's
+// sequential update order (update_mvs_and_sad, mcomp.c:858-877).
+template <int W, int H, bool SKIP>
+__device__ int fast_bigdia(const Ctx& c, int lane, int srow, int scol, int step_param, int& brow,
+                           int& bcol, int& steps) {
+  Search<W, H, SKIP> S;
+  S.load_src(c, lane);
+  const int g = lane >> 3;
+  const int search_step = min(max(kMaxSteps - 3, step_param), kMaxSteps - 1);
+  const int s0 = kMaxSteps - 1 - search_step;  // search_steps[] = {10, 9, ..., 0}
+  int br = min(max(srow, c.row_min), c.row_max);
+  int bc = min(max(scol, c.col_min), c.col_max);
+  uint32_t best = mvsad_cost(c, br, bc) +
+                  rdlane(S.group_sad(c, (int64_t)br * c.rs + bc, true), 0);
+  for (int s = s0; s >= 0; --s) {
+    const int n = s == 0 ? 4 : 8;
+    // one round: candidate idx (groups g < cnt) around (br, bc) at scale s;
+    // returns the winning group or -1
+    auto check = [&](int cnt, int idx) -> int {
+      const bool all_in = br - (1 << s) >= c.row_min && br + (1 << s) <= c.row_max &&
+                          bc - (1 << s) >= c.col_min && bc + (1 << s) <= c.col_max;
+      int dr, dc;
+      bigdia_site(s, idx, dr, dc);
+      const int r = br + dr, cc = bc + dc;
+      const bool valid = g < cnt && (all_in || (cc >= c.col_min && cc <= c.col_max &&
+                                                r >= c.row_min && r <= c.row_max));
+      const uint32_t mine = S.group_sad(c, (int64_t)r * c.rs + cc, valid);
+      const uint32_t key = valid ? ((mine + mvsad_cost(c, r, cc)) << 3) | (uint32_t)g : ~0u;
+      uint32_t kmin = rdlane(key, 0);
+#pragma unroll
+      for (int i = 1; i < 8; ++i) kmin = min(kmin, rdlane(key, 8 * i));
+      ++steps;
+      if (kmin >= (best << 3)) return -1;
+      best = kmin >> 3;
+      return (int)(kmin & 7);
+    };
+    int k = check(n, g < n ? g : 0);
+    if (k < 0) continue;
+    {
+      int dr, dc;
+      bigdia_site(s, k, dr, dc);
+      br += dr;
+      bc += dc;
+    }
+    while (true) {
+      // next_chkpts_indices: k - 1, k, k + 1 (cyclic)
+      const int idx = g == 0 ? (k == 0 ? n - 1 : k - 1) : g == 1 ? k : (k == n - 1 ? 0 : k + 1);
+      const int j = check(3, idx);
+      if (j < 0) break;
+      k = j == 0 ? (k == 0 ? n - 1 : k - 1) : j == 1 ? k : (k == n - 1 ? 0 : k + 1);
+      int dr, dc;
+      bigdia_site(s, k, dr, dc);
+      br += dr;
+      bc += dc;
+    }
+  }
+  brow = br;
+  bcol = bc;
+  return var_cost<W, H>(c, lane, br, bc);  // get_mvpred_var_cost
+}
+
+
 template <int W, int H>
 __global__ __launch_bounds__(256) void diamond_kernel(const uint8_t* __restrict__ src, int ss,
                                                       const uint8_t* __restrict__ ref, int rs,
                                                       const Job* __restrict__ jobs, int njobs,
                                                       int step_param, int cost_type, int skip,
+                                                      int method,
                                                       LavishDiamondResult* __restrict__ out) {
   // XCD-aware: consecutive job quads (neighbouring blocks) share an XCD's L2
   const int nwg = gridDim.x;  // multiple of 8
@@ -441,10 +527,19 @@ __global__ __launch_bounds__(256) void diamond_kernel(const uint8_t* __restrict_
   c.sad_lambda = sad_lambda(cost_type);
   c.sse_lambda = sse_lambda(cost_type);
   int br, bc, steps = 0, searches = 0, sme;
+  // method 0: DIAMOND (full_pixel_diamond), 1: FAST_BIGDIA (pattern_search)
+  auto search = [&](auto skip_tag) {
+    constexpr bool SK = decltype(skip_tag)::value;
+    if (method == 0)
+      return full_pixel_diamond<W, H, SK>(c, lane, jb.start_row, jb.start_col, step_param, br,
+                                          bc, steps, searches, win);
+    ++searches;
+    return fast_bigdia<W, H, SK>(c, lane, jb.start_row, jb.start_col, step_param, br, bc,
+                                 steps);
+  };
   // use_downsampled_sad applies to blocks at least 16 high (mcomp.c:132-133)
   if (skip && H >= 16) {
-    sme = full_pixel_diamond<W, H, true>(c, lane, jb.start_row, jb.start_col, step_param, br, bc,
-                                         steps, searches, win);
+    sme = search(std::true_type{});
     // quality check of the row-skipping search (mcomp.c:1840-1867)
     Search<W, H, false> F;
     F.load_src(c, lane);
@@ -454,12 +549,9 @@ __global__ __launch_bounds__(256) void diamond_kernel(const uint8_t* __restrict_
     K.load_src(c, lane);
     const int ssad = (int)rdlane(K.group_sad(c, off, true), 0);
     const int thresh = (W >> 2) * (H >> 2);
-    if (sad > thresh && abs(ssad - sad) * 10 >= max(sad, 1) * 9)
-      sme = full_pixel_diamond<W, H, false>(c, lane, jb.start_row, jb.start_col, step_param, br,
-                                            bc, steps, searches, win);
+    if (sad > thresh && abs(ssad - sad) * 10 >= max(sad, 1) * 9) sme = search(std::false_type{});
   } else {
-    sme = full_pixel_diamond<W, H, false>(c, lane, jb.start_row, jb.start_col, step_param, br, bc,
-                                          steps, searches, win);
+    sme = search(std::false_type{});
   }
   if (lane == 0) {
     LavishDiamondResult r;
@@ -474,12 +566,31 @@ __global__ __launch_bounds__(256) void diamond_kernel(const uint8_t* __restrict_
 
 template <int W, int H>
 void launch(const uint8_t* src, int ss, const uint8_t* ref, int rs, const LavishDiamondJob* jobs,
-            int njobs, int step_param, int cost_type, int skip, LavishDiamondResult* out,
-            hipStream_t s) {
+            int njobs, int step_param, int cost_type, int skip, int method,
+            LavishDiamondResult* out, hipStream_t s) {
   int nwg = (njobs + 3) / 4;
   nwg = (nwg + 7) & ~7;
   hipLaunchKernelGGL((diamond_kernel<W, H>), dim3(nwg), dim3(256), 0, s, src, ss, ref, rs,
-                     (const Job*)jobs, njobs, step_param, cost_type, skip, out);
+                     (const Job*)jobs, njobs, step_param, cost_type, skip, method, out);
+}
+
+int fullpel_batch(const uint8_t* src, int src_stride, const uint8_t* ref, int ref_stride, int w,
+                  int h, const LavishDiamondJob* jobs, int njobs, int step_param,
+                  int mv_cost_type, int use_downsampled_sad, int method,
+                  LavishDiamondResult* out, hipStream_t s) {
+  if (njobs <= 0) return 0;
+  if (step_param < 0 || step_param >= kMaxSteps) return -1;
+  if (mv_cost_type < 1 || mv_cost_type > 4) return -2;  // MV_COST_ENTROPY not supported
+#define LAVISH_DIA_CASE(W, H)                                                                 \
+  if (w == W && h == H) {                                                                     \
+    launch<W, H>(src, src_stride, ref, ref_stride, jobs, njobs, step_param, mv_cost_type,     \
+                 use_downsampled_sad, method, out, s);                                        \
+    LAVISH_CHECK(hipGetLastError());                                                          \
+    return 0;                                                                                 \
+  }
+  LAVISH_ENCODER_BLOCK_SIZES(LAVISH_DIA_CASE)
+#undef LAVISH_DIA_CASE
+  return -3;
 }
 
 }  // namespace
@@ -493,18 +604,16 @@ extern "C" int lavish_diamond_search_batch(const uint8_t* src, int src_stride, c
                                            int step_param, int mv_cost_type,
                                            int use_downsampled_sad, LavishDiamondResult* out,
                                            void* stream) {
-  if (njobs <= 0) return 0;
-  if (step_param < 0 || step_param >= kMaxSteps) return -1;
-  if (mv_cost_type < 1 || mv_cost_type > 4) return -2;  // MV_COST_ENTROPY not supported
-  hipStream_t s = (hipStream_t)stream;
-#define LAVISH_DIA_CASE(W, H)                                                                 \
-  if (w == W && h == H) {                                                                     \
-    launch<W, H>(src, src_stride, ref, ref_stride, jobs, njobs, step_param, mv_cost_type,     \
-                 use_downsampled_sad, out, s);                                                \
-    LAVISH_CHECK(hipGetLastError());                                                          \
-    return 0;                                                                                 \
-  }
-  LAVISH_ENCODER_BLOCK_SIZES(LAVISH_DIA_CASE)
-#undef LAVISH_DIA_CASE
-  return -3;
+  return fullpel_batch(src, src_stride, ref, ref_stride, w, h, jobs, njobs, step_param,
+                       mv_cost_type, use_downsampled_sad, 0, out, (hipStream_t)stream);
+}
+
+extern "C" int lavish_fast_bigdia_search_batch(const uint8_t* src, int src_stride,
+                                               const uint8_t* ref, int ref_stride, int w, int h,
+                                               const LavishDiamondJob* jobs, int njobs,
+                                               int step_param, int mv_cost_type,
+                                               int use_downsampled_sad,
+                                               LavishDiamondResult* out, void* stream) {
+  return fullpel_batch(src, src_stride, ref, ref_stride, w, h, jobs, njobs, step_param,
+                       mv_cost_type, use_downsampled_sad, 1, out, (hipStream_t)stream);
 }

@@ -28,6 +28,8 @@ _vp, _i32 = ctypes.c_void_p, ctypes.c_int32
 _lib.lavish_diamond_search_batch.argtypes = [_vp, _i32, _vp, _i32, _i32, _i32, _vp, _i32, _i32,
                                              _i32, _i32, _vp, _vp]
 _lib.lavish_diamond_search_batch.restype = _i32
+_lib.lavish_fast_bigdia_search_batch.argtypes = _lib.lavish_diamond_search_batch.argtypes
+_lib.lavish_fast_bigdia_search_batch.restype = _i32
 
 
 def block_mv_limits(mi_rows, mi_cols, mi_row, mi_col, mi_height, mi_width, border):
@@ -103,22 +105,23 @@ def to_device(arr, device="cuda"):
 
 
 def diamond_search_batch(src, ref, w, h, jobs, step_param=0, mv_cost_type=MV_COST_L1_HDRES,
-                         use_downsampled_sad=False, out=None, stream=None):
+                         use_downsampled_sad=False, out=None, stream=None, method="diamond"):
     """src: uint8 device tensor (padded plane, 2-D), ref: uint8 device tensor
     holding the reference planes (any shape, contiguous, same stride); jobs:
     device byte tensor of JOB_DTYPE records.  Returns a device byte tensor of
-    RESULT_DTYPE records (view with results_numpy)."""
+    RESULT_DTYPE records (view with results_numpy).  method "bigdia":
+    lavish_fast_bigdia_search_batch (search_method FAST_BIGDIA)."""
     import torch
     assert src.dtype == torch.uint8 and ref.dtype == torch.uint8
     assert src.is_contiguous() and ref.is_contiguous(), "planes must be C-contiguous"
     nj = jobs.numel() // JOB_DTYPE.itemsize
     if out is None:
         out = torch.empty(nj * RESULT_DTYPE.itemsize, dtype=torch.uint8, device=src.device)
-    rc = _lib.lavish_diamond_search_batch(_vp(src.data_ptr()), src.stride(0),
-                                          _vp(ref.data_ptr()), src.stride(0), w, h,
-                                          _vp(jobs.data_ptr()), nj, step_param, mv_cost_type,
-                                          int(use_downsampled_sad), _vp(out.data_ptr()),
-                                          _stream_ptr(stream))
+    fn = (_lib.lavish_fast_bigdia_search_batch if method == "bigdia"
+          else _lib.lavish_diamond_search_batch)
+    rc = fn(_vp(src.data_ptr()), src.stride(0), _vp(ref.data_ptr()), src.stride(0), w, h,
+            _vp(jobs.data_ptr()), nj, step_param, mv_cost_type, int(use_downsampled_sad),
+            _vp(out.data_ptr()), _stream_ptr(stream))
     if rc != 0:
         raise ValueError("lavish_diamond_search_batch rejected its arguments (rc=%d)" % rc)
     return out

@@ -331,6 +331,19 @@ int lavish_diamond_search_batch(const uint8_t *src, int src_stride,
                                 int use_downsampled_sad,
                                 LavishDiamondResult *out, void *stream);
 
+/* FAST_BIGDIA (search_method of the TPL model at speed >= 5 and of
+ * bsize-dependent full-pel searches): fast_bigdia_search -> bigdia_search ->
+ * pattern_search (av1/encoder/mcomp.c:498-550, 1017-1316) with
+ * do_init_search 0, then get_mvpred_var_cost; the downsampled-SAD recheck of
+ * av1_full_pixel_search (:1840-1873) as for DIAMOND.  Same jobs / results as
+ * lavish_diamond_search_batch (steps = candidate rounds, searches = passes). */
+int lavish_fast_bigdia_search_batch(const uint8_t *src, int src_stride,
+                                    const uint8_t *ref, int ref_stride, int w,
+                                    int h, const LavishDiamondJob *jobs,
+                                    int njobs, int step_param,
+                                    int mv_cost_type, int use_downsampled_sad,
+                                    LavishDiamondResult *out, void *stream);
+
 /* ---- sub-pixel refinement ------------------------
  * av1_find_best_sub_pixel_tree_pruned_more (av1/encoder/mcomp.c:2907-2981;
  * subpel_search_method SUBPEL_TREE_PRUNED_MORE, speed >= 4) without a cost

@@ -200,6 +200,12 @@ void orc_diamond_batch(const uint8_t *src, int src_stride, const uint8_t *ref,
                        long njobs, int step_param, int mv_cost_type,
                        int skip_sad, OrcDiamondResult *out, int threads);
 
+/* FAST_BIGDIA full-pel search (oracle_mcomp.c), same jobs / results */
+void orc_bigdia_batch(const uint8_t *src, int src_stride, const uint8_t *ref,
+                      int ref_stride, int w, int h, const OrcDiamondJob *jobs,
+                      long njobs, int step_param, int mv_cost_type,
+                      int skip_sad, OrcDiamondResult *out, int threads);
+
 /* ---- sub-pixel refinement (oracle_subpel.c); layouts = LavishSubpelJob /
  * LavishSubpelResult.  MVs and limits in 1/8 pel. */
 typedef struct OrcSubpelJob {

@@ -359,11 +359,13 @@ def block_error(coeff, dqcoeff, n, bd=None):
 
 # ------------------------------------------------------ C3 diamond search --
 def diamond_batch(src, ref, stride, w, h, jobs, step_param=0, mv_cost_type=3, skip=False,
-                  threads=1):
-    """orc_diamond_batch over JOB_DTYPE records (lavish_dsp.motion); src and
-    ref are the flat padded planes (ref holds all reference planes)."""
+                  threads=1, method="diamond"):
+    """orc_diamond_batch (method "bigdia": orc_bigdia_batch, FAST_BIGDIA) over
+    JOB_DTYPE records (lavish_dsp.motion); src and ref are the flat padded
+    planes (ref holds all reference planes)."""
     L = lib()
-    L.orc_diamond_batch.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_int,
+    fn = L.orc_bigdia_batch if method == "bigdia" else L.orc_diamond_batch
+    fn.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_int,
                                     ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_long,
                                     ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
                                     ctypes.c_int]
@@ -371,8 +373,8 @@ def diamond_batch(src, ref, stride, w, h, jobs, step_param=0, mv_cost_type=3, sk
     out = np.zeros(len(jobs), np.dtype([("best_row", "<i2"), ("best_col", "<i2"),
                                         ("bestsme", "<i4"), ("steps", "<i4"),
                                         ("searches", "<i4")], align=True))
-    L.orc_diamond_batch(P(src), stride, P(ref), stride, w, h, P(jobs), len(jobs), step_param,
-                        mv_cost_type, int(skip), P(out), threads)
+    fn(P(src), stride, P(ref), stride, w, h, P(jobs), len(jobs), step_param, mv_cost_type,
+       int(skip), P(out), threads)
     return out
 
 
