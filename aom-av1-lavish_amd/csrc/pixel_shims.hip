@@ -430,4 +430,19 @@ HBD_INV_SHIM(16, 32) HBD_INV_SHIM(32, 16) HBD_INV_SHIM(32, 32) HBD_INV_SHIM(32, 
 HBD_INV_SHIM(64, 32) HBD_INV_SHIM(64, 64) HBD_INV_SHIM(8, 32) HBD_INV_SHIM(32, 8)
 HBD_INV_SHIM(16, 64) HBD_INV_SHIM(64, 16)
 
+// ---- TX-pruning features (av1/common/av1_rtcd_defs.pl:469) ----
+void av1_get_horver_correlation_full_hip(const int16_t* diff, int stride, int w, int h,
+                                         float* hcorr, float* vcorr) {
+  Stage st(kStageCap);
+  const int16_t* d = st.block(diff, stride, w, h);
+  float* dout = (float*)st.take(2 * sizeof(float));
+  must(lavish_horver_correlation_batch(d, w, w, h, w, h, dout, dout + 1, st.s),
+       "lavish_horver_correlation_batch");
+  float r[2];
+  st.copy_out(r, dout, 2);
+  st.sync();
+  *hcorr = r[0];
+  *vcorr = r[1];
+}
+
 }  // extern "C"

@@ -474,3 +474,56 @@ def rdo_frame(src, pred, frame, qp, rdmult, bit_depth=10, reconstruct=True, stre
         if rc != 0:
             raise ValueError("lavish_rdo_reconstruct rejected its arguments (rc=%d)" % rc)
     return frame
+
+
+# ----------------------------------------------------- TX-pruning features --
+_lib.lavish_horver_correlation_batch.argtypes = [_vp, _i32, _i32, _i32, _i32, _i32, _vp, _vp, _vp]
+_lib.lavish_horver_correlation_batch.restype = _i32
+_lib.lavish_tx_prune_features_batch.argtypes = [_vp, _i32, _i32, _i32, _i32, _vp, _vp, _vp]
+_lib.lavish_tx_prune_features_batch.restype = _i32
+_lib.av1_get_horver_correlation_full_hip.argtypes = [_vp, _i32, _i32, _i32, _vp, _vp]
+_lib.av1_get_horver_correlation_full_hip.restype = None
+
+
+def horver_correlation_batch(residual, bw, bh, stream=None):
+    """lavish_horver_correlation_batch: (hcorr, vcorr) float32 device tensors
+    over the full bw x bh blocks of a device int16 residual plane."""
+    import torch
+    assert residual.dtype == torch.int16 and residual.stride(1) == 1
+    H, W = residual.shape
+    nb = (W // bw) * (H // bh)
+    hc = torch.empty(nb, dtype=torch.float32, device=residual.device)
+    vc = torch.empty(nb, dtype=torch.float32, device=residual.device)
+    rc = _lib.lavish_horver_correlation_batch(ctypes.c_void_p(residual.data_ptr()),
+                                              residual.stride(0), W, H, bw, bh,
+                                              ctypes.c_void_p(hc.data_ptr()),
+                                              ctypes.c_void_p(vc.data_ptr()), _stream_ptr(stream))
+    if rc != 0:
+        raise ValueError("lavish_horver_correlation_batch rejected its arguments (rc=%d)" % rc)
+    return hc, vc
+
+
+def tx_prune_features(residual, tx_size, stream=None):
+    """lavish_tx_prune_features_batch: (hfeatures, vfeatures) [block, 16]
+    float32 device tensors, prune_tx_2D's neural-net inputs."""
+    import torch
+    assert residual.dtype == torch.int16 and residual.stride(1) == 1
+    H, W = residual.shape
+    nb = (W // TX_W[tx_size]) * (H // TX_H[tx_size])
+    hf = torch.empty((nb, 16), dtype=torch.float32, device=residual.device)
+    vf = torch.empty((nb, 16), dtype=torch.float32, device=residual.device)
+    rc = _lib.lavish_tx_prune_features_batch(ctypes.c_void_p(residual.data_ptr()),
+                                             residual.stride(0), W, H, tx_size,
+                                             ctypes.c_void_p(hf.data_ptr()),
+                                             ctypes.c_void_p(vf.data_ptr()), _stream_ptr(stream))
+    if rc != 0:
+        raise ValueError("lavish_tx_prune_features_batch rejected its arguments (rc=%d)" % rc)
+    return hf, vf
+
+
+def av1_get_horver_correlation_full(diff, stride, w, h):
+    """Per-call RTCD shim (host int16 buffer): returns (hcorr, vcorr)."""
+    hc, vc = ctypes.c_float(), ctypes.c_float()
+    _lib.av1_get_horver_correlation_full_hip(_p(diff), stride, w, h, ctypes.byref(hc),
+                                             ctypes.byref(vc))
+    return hc.value, vc.value

@@ -390,6 +390,23 @@ int lavish_subpel_search_after_diamond(const uint8_t *src, int src_stride,
                                        int iters_per_step, int mv_cost_type,
                                        LavishSubpelResult *out, void *stream);
 
+/* ---- TX-type pruning features ---------------------
+ * Every full bw x bh block of an int16 residual plane (raster order):
+ * av1_get_horver_correlation_full (av1/encoder/rdopt.c:514-609) -> hcorr /
+ * vcorr[block] (bw, bh in 2..128). */
+int lavish_horver_correlation_batch(const int16_t *residual, int stride,
+                                    int width, int height, int bw, int bh,
+                                    float *hcorr, float *vcorr, void *stream);
+/* prune_tx_2D's two neural-net inputs (av1/encoder/tx_search.c:1516-1529)
+ * per tx_size block: hfeatures[block][16] = get_energy_distribution_finer's
+ * column projection (tx_search.c:1411-1473) in [0, n-1) and hcorr at n-1
+ * (n = w <= 8 ? w : w / 2); vfeatures likewise for rows; unused entries 0.
+ * tx sizes up to 32x32 (else -2).  Bit-exact single precision. */
+int lavish_tx_prune_features_batch(const int16_t *residual, int stride,
+                                   int width, int height, int tx_size,
+                                   float *hfeatures, float *vfeatures,
+                                   void *stream);
+
 /* ------------------------------------------------------------------------ */
 /* Per-call RTCD shims (host pointers)                                      */
 /* ------------------------------------------------------------------------ */
@@ -625,6 +642,9 @@ int64_t av1_block_error_hip(const int32_t *coeff, const int32_t *dqcoeff,
 int64_t av1_highbd_block_error_hip(const int32_t *coeff,
                                    const int32_t *dqcoeff,
                                    intptr_t block_size, int64_t *ssz, int bd);
+/* av1_get_horver_correlation_full (av1/common/av1_rtcd_defs.pl:469) */
+void av1_get_horver_correlation_full_hip(const int16_t *diff, int stride, int w,
+                                         int h, float *hcorr, float *vcorr);
 
 #ifdef __cplusplus
 }

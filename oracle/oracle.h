@@ -225,6 +225,15 @@ void orc_subpel_batch(const uint8_t *src, int src_stride, const uint8_t *ref,
                       int iters_per_step, int mv_cost_type,
                       OrcSubpelResult *out, int threads);
 
+/* ---- TX-type pruning features (oracle_txfeat.c) ---- */
+void orc_horver_correlation_full(const int16_t *diff, int stride, int width,
+                                 int height, float *hcorr, float *vcorr);
+void orc_energy_distribution_finer(const int16_t *diff, int stride, int bw,
+                                   int bh, float *hordist, float *verdist);
+long orc_tx_prune_features(const int16_t *residual, int stride, int width,
+                           int height, int bw, int bh, float *hfeatures,
+                           float *vfeatures);
+
 /* ---- C4: per-block TX-type RDO (oracle_rdo.c); layout = LavishRdoBlock */
 typedef struct OrcRdoBlock {
   int32_t best_type, eob, rate, satd;

@@ -422,3 +422,31 @@ def rdo_plane(src, pred, tx_size, type_mask, bd, q, rdmult, threads=1, px=False)
     fn(P(src), P(pred), W, W, H, tx_size, type_mask, bd, ctypes.byref(q), rdmult, P(out), P(qc),
        P(dq), threads)
     return out, qc, dq
+
+
+# ---------------------------------------------------- TX-pruning features --
+def horver_full(diff, stride, w, h):
+    """orc_horver_correlation_full on a host int16 buffer: (hcorr, vcorr)."""
+    L = lib()
+    L.orc_horver_correlation_full.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
+                                              ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]
+    hc, vc = ctypes.c_float(), ctypes.c_float()
+    diff = np.ascontiguousarray(diff, dtype=np.int16)
+    L.orc_horver_correlation_full(P(diff), stride, w, h, ctypes.byref(hc), ctypes.byref(vc))
+    return np.float32(hc.value), np.float32(vc.value)
+
+
+def tx_prune_features(res, bw, bh):
+    """orc_tx_prune_features over an int16 plane: (hfeatures, vfeatures) [block, 16]."""
+    L = lib()
+    L.orc_tx_prune_features.restype = ctypes.c_long
+    L.orc_tx_prune_features.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
+                                        ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                        ctypes.c_void_p, ctypes.c_void_p]
+    res = np.ascontiguousarray(res, dtype=np.int16)
+    H, W = res.shape
+    nb = (W // bw) * (H // bh)
+    hf = np.zeros((nb, 16), np.float32)
+    vf = np.zeros((nb, 16), np.float32)
+    L.orc_tx_prune_features(P(res), W, W, H, bw, bh, P(hf), P(vf))
+    return hf, vf
