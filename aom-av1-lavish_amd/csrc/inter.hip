@@ -1,0 +1,470 @@
+// inter.hip -- batched single-reference inter prediction for gfx950
+// ("its prediction output feeds C4").
+//
+// Reference (one block per call, one CPU thread):
+//   av1_enc_build_one_inter_predictor (av1/encoder/reconinter_enc.c:47-51)
+//   -> enc_calc_subpel_params / init_subpel_params (av1/common/reconinter.h:
+//      131-165): q10 position of the block + mv, clamped to the frame's
+//      border window, split into an integer pixel and a 1/16 phase
+//   -> av1_get_interp_filter_params_with_block_size (filter.h:253-259):
+//      4-tap kernels for block dimensions <= 4
+//   -> convolve_2d_facade_single (convolve.c:614-634, highbd :1106-1128):
+//      copy / av1_convolve_x_sr / _y_sr / _2d_sr with the single-prediction
+//      rounding of get_conv_params_no_round (convolve.h:63-95).
+//
+// Here a job is one (block, mv, filter pair); a thread owns CW adjacent
+// output columns x R rows of one job.  It reads each source row segment it
+// needs (CW + 7 pixels) with dword-aligned loads + v_alignbyte, runs the
+// horizontal pass in registers, keeps the R + 7 intermediate rows of its
+// columns in VGPRs and finishes the vertical pass there -- no LDS, no
+// barrier; adjacent threads read adjacent bytes, so a wave's loads coalesce
+// and the (w + 7) x (h + 7) source window of a block is fetched from HBM
+// about once (the overlap hits L2: consecutive jobs share an XCD).  12-tap
+// kernels (MULTITAP_SHARP2, temporal filtering only) take a direct,
+// per-pixel path.
+#include "lavish_internal.h"
+
+namespace lavish {
+namespace {
+
+struct IJob {
+  int64_t ref_off, dst_off;
+  int32_t pix_row, pix_col;
+  int16_t mv_row, mv_col;
+  uint8_t filter_x, filter_y, pad[2];
+};
+static_assert(sizeof(IJob) == sizeof(LavishInterPredJob) && sizeof(IJob) == 32, "job layout");
+
+// [kind][phase][tap]: 0 REGULAR 1 SMOOTH 2 SHARP 3 BILINEAR, 4 / 5 the
+// 4-tap REGULAR / SMOOTH kernels (8-tap layout) -- filter.h:111-243
+__constant__ int16_t kK8[6][16][8] = {
+  { { 0, 0, 0, 128, 0, 0, 0, 0 }, { 0, 2, -6, 126, 8, -2, 0, 0 },
+    { 0, 2, -10, 122, 18, -4, 0, 0 }, { 0, 2, -12, 116, 28, -8, 2, 0 },
+    { 0, 2, -14, 110, 38, -10, 2, 0 }, { 0, 2, -14, 102, 48, -12, 2, 0 },
+    { 0, 2, -16, 94, 58, -12, 2, 0 }, { 0, 2, -14, 84, 66, -12, 2, 0 },
+    { 0, 2, -14, 76, 76, -14, 2, 0 }, { 0, 2, -12, 66, 84, -14, 2, 0 },
+    { 0, 2, -12, 58, 94, -16, 2, 0 }, { 0, 2, -12, 48, 102, -14, 2, 0 },
+    { 0, 2, -10, 38, 110, -14, 2, 0 }, { 0, 2, -8, 28, 116, -12, 2, 0 },
+    { 0, 0, -4, 18, 122, -10, 2, 0 }, { 0, 0, -2, 8, 126, -6, 2, 0 } },
+  { { 0, 0, 0, 128, 0, 0, 0, 0 }, { 0, 2, 28, 62, 34, 2, 0, 0 },
+    { 0, 0, 26, 62, 36, 4, 0, 0 }, { 0, 0, 22, 62, 40, 4, 0, 0 },
+    { 0, 0, 20, 60, 42, 6, 0, 0 }, { 0, 0, 18, 58, 44, 8, 0, 0 },
+    { 0, 0, 16, 56, 46, 10, 0, 0 }, { 0, -2, 16, 54, 48, 12, 0, 0 },
+    { 0, -2, 14, 52, 52, 14, -2, 0 }, { 0, 0, 12, 48, 54, 16, -2, 0 },
+    { 0, 0, 10, 46, 56, 16, 0, 0 }, { 0, 0, 8, 44, 58, 18, 0, 0 },
+    { 0, 0, 6, 42, 60, 20, 0, 0 }, { 0, 0, 4, 40, 62, 22, 0, 0 },
+    { 0, 0, 4, 36, 62, 26, 0, 0 }, { 0, 0, 2, 34, 62, 28, 2, 0 } },
+  { { 0, 0, 0, 128, 0, 0, 0, 0 }, { -2, 2, -6, 126, 8, -2, 2, 0 },
+    { -2, 6, -12, 124, 16, -6, 4, -2 }, { -2, 8, -18, 120, 26, -10, 6, -2 },
+    { -4, 10, -22, 116, 38, -14, 6, -2 }, { -4, 10, -22, 108, 48, -18, 8, -2 },
+    { -4, 10, -24, 100, 60, -20, 8, -2 }, { -4, 10, -24, 90, 70, -22, 10, -2 },
+    { -4, 12, -24, 80, 80, -24, 12, -4 }, { -2, 10, -22, 70, 90, -24, 10, -4 },
+    { -2, 8, -20, 60, 100, -24, 10, -4 }, { -2, 8, -18, 48, 108, -22, 10, -4 },
+    { -2, 6, -14, 38, 116, -22, 10, -4 }, { -2, 6, -10, 26, 120, -18, 8, -2 },
+    { -2, 4, -6, 16, 124, -12, 6, -2 }, { 0, 2, -2, 8, 126, -6, 2, -2 } },
+  { { 0, 0, 0, 128, 0, 0, 0, 0 }, { 0, 0, 0, 120, 8, 0, 0, 0 },
+    { 0, 0, 0, 112, 16, 0, 0, 0 }, { 0, 0, 0, 104, 24, 0, 0, 0 },
+    { 0, 0, 0, 96, 32, 0, 0, 0 }, { 0, 0, 0, 88, 40, 0, 0, 0 },
+    { 0, 0, 0, 80, 48, 0, 0, 0 }, { 0, 0, 0, 72, 56, 0, 0, 0 },
+    { 0, 0, 0, 64, 64, 0, 0, 0 }, { 0, 0, 0, 56, 72, 0, 0, 0 },
+    { 0, 0, 0, 48, 80, 0, 0, 0 }, { 0, 0, 0, 40, 88, 0, 0, 0 },
+    { 0, 0, 0, 32, 96, 0, 0, 0 }, { 0, 0, 0, 24, 104, 0, 0, 0 },
+    { 0, 0, 0, 16, 112, 0, 0, 0 }, { 0, 0, 0, 8, 120, 0, 0, 0 } },
+  { { 0, 0, 0, 128, 0, 0, 0, 0 }, { 0, 0, -4, 126, 8, -2, 0, 0 },
+    { 0, 0, -8, 122, 18, -4, 0, 0 }, { 0, 0, -10, 116, 28, -6, 0, 0 },
+    { 0, 0, -12, 110, 38, -8, 0, 0 }, { 0, 0, -12, 102, 48, -10, 0, 0 },
+    { 0, 0, -14, 94, 58, -10, 0, 0 }, { 0, 0, -12, 84, 66, -10, 0, 0 },
+    { 0, 0, -12, 76, 76, -12, 0, 0 }, { 0, 0, -10, 66, 84, -12, 0, 0 },
+    { 0, 0, -10, 58, 94, -14, 0, 0 }, { 0, 0, -10, 48, 102, -12, 0, 0 },
+    { 0, 0, -8, 38, 110, -12, 0, 0 }, { 0, 0, -6, 28, 116, -10, 0, 0 },
+    { 0, 0, -4, 18, 122, -8, 0, 0 }, { 0, 0, -2, 8, 126, -4, 0, 0 } },
+  { { 0, 0, 0, 128, 0, 0, 0, 0 }, { 0, 0, 30, 62, 34, 2, 0, 0 },
+    { 0, 0, 26, 62, 36, 4, 0, 0 }, { 0, 0, 22, 62, 40, 4, 0, 0 },
+    { 0, 0, 20, 60, 42, 6, 0, 0 }, { 0, 0, 18, 58, 44, 8, 0, 0 },
+    { 0, 0, 16, 56, 46, 10, 0, 0 }, { 0, 0, 14, 54, 48, 12, 0, 0 },
+    { 0, 0, 12, 52, 52, 12, 0, 0 }, { 0, 0, 12, 48, 54, 14, 0, 0 },
+    { 0, 0, 10, 46, 56, 16, 0, 0 }, { 0, 0, 8, 44, 58, 18, 0, 0 },
+    { 0, 0, 6, 42, 60, 20, 0, 0 }, { 0, 0, 4, 40, 62, 22, 0, 0 },
+    { 0, 0, 4, 36, 62, 26, 0, 0 }, { 0, 0, 2, 34, 62, 30, 0, 0 } },
+};
+
+// MULTITAP_SHARP2
+__constant__ int16_t kK12[16][12] = {
+  { 0, 0, 0, 0, 0, 128, 0, 0, 0, 0, 0, 0 },
+  { 0, 1, -2, 3, -7, 127, 8, -4, 2, -1, 1, 0 },
+  { -1, 2, -3, 6, -13, 124, 18, -8, 4, -2, 2, -1 },
+  { -1, 3, -4, 8, -18, 120, 28, -12, 7, -4, 2, -1 },
+  { -1, 3, -6, 10, -21, 115, 38, -15, 8, -5, 3, -1 },
+  { -2, 4, -6, 12, -24, 108, 49, -18, 10, -6, 3, -2 },
+  { -2, 4, -7, 13, -25, 100, 60, -21, 11, -7, 4, -2 },
+  { -2, 4, -7, 13, -26, 91, 71, -24, 13, -7, 4, -2 },
+  { -2, 4, -7, 13, -25, 81, 81, -25, 13, -7, 4, -2 },
+  { -2, 4, -7, 13, -24, 71, 91, -26, 13, -7, 4, -2 },
+  { -2, 4, -7, 11, -21, 60, 100, -25, 13, -7, 4, -2 },
+  { -2, 3, -6, 10, -18, 49, 108, -24, 12, -6, 4, -2 },
+  { -1, 3, -5, 8, -15, 38, 115, -21, 10, -6, 3, -1 },
+  { -1, 2, -4, 7, -12, 28, 120, -18, 8, -4, 3, -1 },
+  { -1, 2, -2, 4, -8, 18, 124, -13, 6, -3, 2, -1 },
+  { 0, 1, -1, 2, -4, 8, 127, -7, 3, -2, 1, 0 },
+};
+
+struct IpArgs {
+  const void* ref;
+  int64_t rs;
+  int fw, fh, ssx, ssy, w, h;
+  const IJob* jobs;
+  const LavishSubpelResult* mvs;  // optional mv override
+  int njobs;
+  void* dst;
+  int64_t ds;
+  int bd, r0, r1;
+  // RTCD shims: the caller's own kernels and path (kCustom layout); the
+  // job's ref_off is then the block's integer position
+  const int16_t* custom;
+};
+enum { kCPath = 0, kCTx = 1, kCTy = 2, kCFx = 4, kCFy = 16, kCustomLen = 28 };
+
+typedef const __attribute__((address_space(1))) uint32_t* gptr;
+
+__device__ __forceinline__ int rpot(int v, int n) { return (v + ((1 << n) >> 1)) >> n; }
+__device__ __forceinline__ int clip_bd(int v, int mx) { return v < 0 ? 0 : v > mx ? mx : v; }
+
+// NP consecutive pixels starting at p (any alignment), from dword-aligned
+// loads; reads up to 4 bytes either side of the span (inside the border)
+template <int NP>
+__device__ __forceinline__ void load_px(const uint8_t* p, int (&o)[NP]) {
+  const uintptr_t a = (uintptr_t)p;
+  const gptr q = (gptr)(a & ~(uintptr_t)3);
+  const uint32_t sh = (uint32_t)(a & 3);
+  constexpr int NE = (NP + 3) / 4;
+  uint32_t d[NE + 1];
+#pragma unroll
+  for (int i = 0; i <= NE; ++i) d[i] = q[i];
+#pragma unroll
+  for (int j = 0; j < NP; ++j) {
+    const uint32_t e = __builtin_amdgcn_alignbyte(d[(j >> 2) + 1], d[j >> 2], sh);
+    o[j] = (int)((e >> (8 * (j & 3))) & 0xFFu);
+  }
+}
+template <int NP>
+__device__ __forceinline__ void load_px(const uint16_t* p, int (&o)[NP]) {
+  const uintptr_t a = (uintptr_t)p;
+  const gptr q = (gptr)(a & ~(uintptr_t)3);
+  const uint32_t sh = (uint32_t)(a & 2);
+  constexpr int NE = (NP + 1) / 2;
+  uint32_t d[NE + 1];
+#pragma unroll
+  for (int i = 0; i <= NE; ++i) d[i] = q[i];
+#pragma unroll
+  for (int j = 0; j < NP; ++j) {
+    const uint32_t e = __builtin_amdgcn_alignbyte(d[(j >> 1) + 1], d[j >> 1], sh);
+    o[j] = (int)((e >> (16 * (j & 1))) & 0xFFFFu);
+  }
+}
+
+template <int CW>
+__device__ __forceinline__ void store_px(uint8_t* p, const int (&v)[CW]) {
+  const uintptr_t a = (uintptr_t)p;
+  if constexpr (CW == 4) {
+    if ((a & 3) == 0) {
+      *(uint32_t*)p = (uint32_t)v[0] | ((uint32_t)v[1] << 8) | ((uint32_t)v[2] << 16) |
+                      ((uint32_t)v[3] << 24);
+      return;
+    }
+  } else {
+    if ((a & 1) == 0) {
+      *(uint16_t*)p = (uint16_t)(v[0] | (v[1] << 8));
+      return;
+    }
+  }
+#pragma unroll
+  for (int c = 0; c < CW; ++c) p[c] = (uint8_t)v[c];
+}
+template <int CW>
+__device__ __forceinline__ void store_px(uint16_t* p, const int (&v)[CW]) {
+  const uintptr_t a = (uintptr_t)p;
+  if ((a & 3) == 0) {
+#pragma unroll
+    for (int c = 0; c < CW; c += 2)
+      *(uint32_t*)(p + c) = (uint32_t)v[c] | ((uint32_t)v[c + 1] << 16);
+    return;
+  }
+#pragma unroll
+  for (int c = 0; c < CW; ++c) p[c] = (uint16_t)v[c];
+}
+
+template <typename T>
+__device__ __forceinline__ int px(const T* p, int64_t i) {
+  return (int)p[i];
+}
+
+// direct per-pixel evaluation for any tap count (12-tap kernels)
+template <typename T, int CW, int R>
+__device__ void generic_block(const T* src, int64_t rs, T* dst, int64_t ds, int path,
+                              const int16_t* fx, int tx, const int16_t* fy, int ty, int bd,
+                              int r0, int r1) {
+  const int mx = (1 << bd) - 1;
+  const int foh = tx / 2 - 1, fov = ty / 2 - 1;
+  for (int r = 0; r < R; ++r)
+    for (int c = 0; c < CW; ++c) {
+      int v;
+      if (path == 0) {
+        v = px(src, r * rs + c);
+      } else if (path == 1) {
+        int s = 0;
+        for (int k = 0; k < tx; ++k) s += fx[k] * px(src, r * rs + c - foh + k);
+        v = clip_bd(rpot(rpot(s, r0), 7 - r0), mx);
+      } else if (path == 2) {
+        int s = 0;
+        for (int k = 0; k < ty; ++k) s += fy[k] * px(src, (r - fov + k) * rs + c);
+        v = clip_bd(rpot(s, 7), mx);
+      } else {
+        const int ob = bd + 14 - r0;
+        int s = 1 << ob;
+        for (int k = 0; k < ty; ++k) {
+          int hs = 1 << (bd + 6);
+          for (int m = 0; m < tx; ++m) hs += fx[m] * px(src, (r - fov + k) * rs + c - foh + m);
+          s += fy[k] * (int)(int16_t)rpot(hs, r0);
+        }
+        const int res = rpot(s, r1) - ((1 << (ob - r1)) + (1 << (ob - r1 - 1)));
+        v = clip_bd(rpot(res, 14 - r0 - r1), mx);
+      }
+      dst[r * ds + c] = (T)v;
+    }
+}
+
+template <typename T, int CW, int R>
+__global__ __launch_bounds__(256) void inter_kernel(IpArgs a) {
+  const int ncg = a.w / CW;
+  const int tpj = ncg * (a.h / R);
+  // XCD-aware: consecutive jobs (neighbouring blocks, overlapping source
+  // windows) land on the same XCD's L2
+  const int nwg = gridDim.x;  // multiple of 8
+  const int wg = (blockIdx.x & 7) * (nwg >> 3) + (blockIdx.x >> 3);
+  const int64_t gid = (int64_t)wg * 256 + threadIdx.x;
+  const int64_t j = gid / tpj;
+  if (j >= a.njobs) return;
+  const int sub = (int)(gid - j * tpj);
+  const int rsi = sub / ncg, cg = sub - rsi * ncg;
+  const IJob jb = a.jobs[j];
+  const T* src;
+  int path, tx, ty;
+  const int16_t *fx, *fy;
+  if (a.custom) {
+    src = (const T*)a.ref + jb.ref_off;
+    path = a.custom[kCPath];
+    tx = a.custom[kCTx];
+    ty = a.custom[kCTy];
+    fx = a.custom + kCFx;
+    fy = a.custom + kCFy;
+  } else {
+    int mvr = jb.mv_row, mvc = jb.mv_col;
+    if (a.mvs) {
+      mvr = a.mvs[j].best_row;
+      mvc = a.mvs[j].best_col;
+    }
+    // init_subpel_params (unscaled): q4 -> q10 (+ SCALE_EXTRA_OFF), clamp
+    int pos_y = ((jb.pix_row << 4) + mvr * (1 << (1 - a.ssy))) * 64 + 32;
+    int pos_x = ((jb.pix_col << 4) + mvc * (1 << (1 - a.ssx))) * 64 + 32;
+    const int top = -(((288 >> a.ssy) - 4) << 10), left = -(((288 >> a.ssx) - 4) << 10);
+    pos_y = min(max(pos_y, top), (a.fh + 4) << 10);
+    pos_x = min(max(pos_x, left), (a.fw + 4) << 10);
+    const int sx = (pos_x & 1023) >> 6, sy = (pos_y & 1023) >> 6;
+    src = (const T*)a.ref + jb.ref_off + (int64_t)(pos_y >> 10) * a.rs + (pos_x >> 10);
+    path = (sx ? 1 : 0) + (sy ? 2 : 0);
+    // av1_get_interp_filter_params_with_block_size
+    const int f_x = jb.filter_x, f_y = jb.filter_y;
+    const int kx = a.w <= 4 ? (f_x == 1 ? 5 : f_x == 3 ? 3 : 4) : f_x;
+    const int ky = a.h <= 4 ? (f_y == 1 ? 5 : f_y == 3 ? 3 : 4) : f_y;
+    tx = f_x == 4 ? 12 : 8;
+    ty = f_y == 4 ? 12 : 8;
+    fx = f_x == 4 ? kK12[sx] : kK8[kx > 5 ? 0 : kx][sx];
+    fy = f_y == 4 ? kK12[sy] : kK8[ky > 5 ? 0 : ky][sy];
+  }
+  src += (int64_t)(rsi * R) * a.rs + cg * CW;
+  T* dst = (T*)a.dst + jb.dst_off + (int64_t)(rsi * R) * a.ds + cg * CW;
+  const int mx = (1 << a.bd) - 1;
+  const bool wide = ((path & 1) && tx != 8) || ((path & 2) && ty != 8);
+  if (wide) {
+    generic_block<T, CW, R>(src, a.rs, dst, a.ds, path, fx, tx, fy, ty, a.bd, a.r0, a.r1);
+    return;
+  }
+  int kx[8], ky[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    kx[k] = fx[k];
+    ky[k] = fy[k];
+  }
+  if (path == 0) {  // aom_convolve_copy
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      int p[CW];
+      load_px<CW>(src + r * a.rs, p);
+      store_px<CW>(dst + r * a.ds, p);
+    }
+  } else if (path == 1) {  // av1_convolve_x_sr
+    const int r0 = a.r0, bits = 7 - a.r0;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      int p[CW + 7], o[CW];
+      load_px<CW + 7>(src + r * a.rs - 3, p);
+#pragma unroll
+      for (int c = 0; c < CW; ++c) {
+        int s = 0;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) s += kx[k] * p[c + k];
+        o[c] = clip_bd(rpot(rpot(s, r0), bits), mx);
+      }
+      store_px<CW>(dst + r * a.ds, o);
+    }
+  } else if (path == 2) {  // av1_convolve_y_sr
+    int col[R + 7][CW];
+#pragma unroll
+    for (int i = 0; i < R + 7; ++i) load_px<CW>(src + (i - 3) * a.rs, col[i]);
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      int o[CW];
+#pragma unroll
+      for (int c = 0; c < CW; ++c) {
+        int s = 0;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) s += ky[k] * col[r + k][c];
+        o[c] = clip_bd(rpot(s, 7), mx);
+      }
+      store_px<CW>(dst + r * a.ds, o);
+    }
+  } else {  // av1_convolve_2d_sr
+    const int r0 = a.r0, r1 = a.r1, bits = 14 - r0 - r1;
+    const int hoff = 1 << (a.bd + 6);
+    const int ob = a.bd + 14 - r0;
+    const int voff = (1 << (ob - r1)) + (1 << (ob - r1 - 1));
+    int im[R + 7][CW];
+#pragma unroll
+    for (int i = 0; i < R + 7; ++i) {
+      int p[CW + 7];
+      load_px<CW + 7>(src + (i - 3) * a.rs - 3, p);
+#pragma unroll
+      for (int c = 0; c < CW; ++c) {
+        int s = hoff;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) s += kx[k] * p[c + k];
+        im[i][c] = (int)(int16_t)rpot(s, r0);
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      int o[CW];
+#pragma unroll
+      for (int c = 0; c < CW; ++c) {
+        int s = 1 << ob;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) s += ky[k] * im[r + k][c];
+        o[c] = clip_bd(rpot(rpot(s, r1) - voff, bits), mx);
+      }
+      store_px<CW>(dst + r * a.ds, o);
+    }
+  }
+}
+
+template <typename T, int CW>
+void launch_cw(const IpArgs& a, hipStream_t s) {
+  const int R = a.h < 8 ? a.h : 8;
+  const int64_t threads = (int64_t)a.njobs * (a.w / CW) * (a.h / R);
+  const int nwg = (int)(((threads + 255) / 256 + 7) & ~7LL);
+  if (R == 8)
+    hipLaunchKernelGGL((inter_kernel<T, CW, 8>), dim3(nwg), dim3(256), 0, s, a);
+  else if (R == 4)
+    hipLaunchKernelGGL((inter_kernel<T, CW, 4>), dim3(nwg), dim3(256), 0, s, a);
+  else
+    hipLaunchKernelGGL((inter_kernel<T, CW, 2>), dim3(nwg), dim3(256), 0, s, a);
+  LAVISH_CHECK(hipGetLastError());
+}
+
+template <typename T>
+void launch_t(const IpArgs& a, hipStream_t s) {
+  if (a.w == 2)
+    launch_cw<T, 2>(a, s);
+  else
+    launch_cw<T, 4>(a, s);
+}
+
+bool pow2_size(int v) { return v >= 2 && v <= 128 && (v & (v - 1)) == 0; }
+
+// get_conv_params_no_round(0, plane, NULL, 0, 0, bd)
+void conv_rounds(int bd, int& r0, int& r1) {
+  r0 = 3;
+  r1 = 14 - 3;
+  const int ibr = bd + 7 - r0 + 2;
+  if (ibr > 16) {
+    r0 += ibr - 16;
+    r1 -= ibr - 16;
+  }
+}
+
+}  // namespace
+
+int inter_pred_batch(const void* ref, int ref_stride, int ref_width, int ref_height, int ss_x,
+                     int ss_y, int w, int h, const LavishInterPredJob* jobs, int njobs,
+                     const LavishSubpelResult* mvs, void* dst, int dst_stride, int bd, int highbd,
+                     const int16_t* custom, int r0, int r1, hipStream_t s) {
+  if (!pow2_size(w) || !pow2_size(h)) return -3;
+  if (ss_x < 0 || ss_x > 1 || ss_y < 0 || ss_y > 1) return -1;
+  if (highbd ? (bd != 8 && bd != 10 && bd != 12) : bd != 8) return -1;
+  if (ref_width < 0 || ref_height < 0) return -4;
+  if (njobs < 0) return -4;
+  if (njobs == 0) return 0;
+  IpArgs a;
+  a.ref = ref;
+  a.rs = ref_stride;
+  a.fw = ref_width;
+  a.fh = ref_height;
+  a.ssx = ss_x;
+  a.ssy = ss_y;
+  a.w = w;
+  a.h = h;
+  a.jobs = (const IJob*)jobs;
+  a.mvs = mvs;
+  a.njobs = njobs;
+  a.dst = dst;
+  a.ds = dst_stride;
+  a.bd = bd;
+  if (custom) {
+    a.r0 = r0;
+    a.r1 = r1;
+  } else {
+    conv_rounds(bd, a.r0, a.r1);
+  }
+  a.custom = custom;
+  if (highbd)
+    launch_t<uint16_t>(a, s);
+  else
+    launch_t<uint8_t>(a, s);
+  return 0;
+}
+
+}  // namespace lavish
+
+using namespace lavish;
+
+extern "C" int lavish_build_inter_pred_batch(const void* ref, int ref_stride, int ref_width,
+                                             int ref_height, int ss_x, int ss_y, int w, int h,
+                                             const LavishInterPredJob* jobs, int njobs,
+                                             void* dst, int dst_stride, int bit_depth, int highbd,
+                                             void* stream) {
+  return inter_pred_batch(ref, ref_stride, ref_width, ref_height, ss_x, ss_y, w, h, jobs, njobs,
+                          nullptr, dst, dst_stride, bit_depth, highbd, nullptr, 0, 0,
+                          (hipStream_t)stream);
+}
+
+extern "C" int lavish_build_inter_pred_after_subpel(const void* ref, int ref_stride,
+                                                    int ref_width, int ref_height, int ss_x,
+                                                    int ss_y, int w, int h,
+                                                    const LavishInterPredJob* jobs,
+                                                    const LavishSubpelResult* mvs, int njobs,
+                                                    void* dst, int dst_stride, int bit_depth,
+                                                    int highbd, void* stream) {
+  if (!mvs) return -4;
+  return inter_pred_batch(ref, ref_stride, ref_width, ref_height, ss_x, ss_y, w, h, jobs, njobs,
+                          mvs, dst, dst_stride, bit_depth, highbd, nullptr, 0, 0,
+                          (hipStream_t)stream);
+}

@@ -50,6 +50,12 @@ int rdo_plane(const uint16_t* src, const uint16_t* pred, int stride, int width, 
               LavishRdoBlock* out, int32_t* qcoeff, int32_t* dqcoeff, hipStream_t s,
               int px = 0);
 
+// inter prediction batch (inter.hip); custom = an RTCD shim's own kernels
+int inter_pred_batch(const void* ref, int ref_stride, int ref_width, int ref_height, int ss_x,
+                     int ss_y, int w, int h, const LavishInterPredJob* jobs, int njobs,
+                     const LavishSubpelResult* mvs, void* dst, int dst_stride, int bd, int highbd,
+                     const int16_t* custom, int r0, int r1, hipStream_t s);
+
 // fork / join over the library's per-thread internal streams
 int fan_width();
 hipStream_t* fan_out(hipStream_t caller);

@@ -209,6 +209,46 @@ void check_lossless(const LavishTxfmParam* p) {
   }
 }
 
+// one block through the inter-prediction kernel with the caller's own
+// kernels (path: 0 copy, 1 x_sr, 2 y_sr, 3 2d_sr); only the source window
+// the C function reads is staged
+template <typename Pix>
+void conv_shim(const Pix* src, ptrdiff_t ss, Pix* dst, ptrdiff_t ds, int w, int h, int path,
+               const LavishInterpFilterParams* fpx, int subx, const LavishInterpFilterParams* fpy,
+               int suby, int r0, int r1, int bd) {
+  int16_t c[28] = {0};
+  int tx = 8, ty = 8;
+  if (path & 1) {
+    tx = fpx->taps;
+    if (tx > 12) lavish::set_error("convolve shim: taps > 12", hipErrorInvalidValue, __FILE__, __LINE__);
+    for (int k = 0; k < tx; ++k) c[4 + k] = fpx->filter_ptr[tx * (subx & 15) + k];
+  }
+  if (path & 2) {
+    ty = fpy->taps;
+    if (ty > 12) lavish::set_error("convolve shim: taps > 12", hipErrorInvalidValue, __FILE__, __LINE__);
+    for (int k = 0; k < ty; ++k) c[16 + k] = fpy->filter_ptr[ty * (suby & 15) + k];
+  }
+  c[0] = (int16_t)path;
+  c[1] = (int16_t)tx;
+  c[2] = (int16_t)ty;
+  const int foh = (path & 1) ? tx / 2 - 1 : 0, fov = (path & 2) ? ty / 2 - 1 : 0;
+  const int ww = w + ((path & 1) ? tx - 1 : 0), wh = h + ((path & 2) ? ty - 1 : 0);
+  Stage st(kStageCap);
+  const Pix* win = st.block(src - fov * ss - foh, ss, ww, wh);
+  st.take(64);  // slack for the kernel's dword-aligned over-read
+  LavishInterPredJob jb{};
+  jb.ref_off = (int64_t)fov * ww + foh;
+  const LavishInterPredJob* djob = st.copy_in(&jb, 1);
+  const int16_t* dc = st.copy_in(c, 28);
+  Pix* dout = (Pix*)st.take((size_t)w * h * sizeof(Pix));
+  must(inter_pred_batch(win, ww, 0, 0, 0, 0, w, h, djob, 1, nullptr, dout, w, bd,
+                        sizeof(Pix) == 2, dc, r0, r1, st.s),
+       "inter_pred_batch");
+  LAVISH_CHECK(hipMemcpy2DAsync(dst, (size_t)ds * sizeof(Pix), dout, (size_t)w * sizeof(Pix),
+                                (size_t)w * sizeof(Pix), h, hipMemcpyDeviceToHost, st.s));
+  st.sync();
+}
+
 }  // namespace
 }  // namespace lavish
 
@@ -443,6 +483,57 @@ void av1_get_horver_correlation_full_hip(const int16_t* diff, int stride, int w,
   st.sync();
   *hcorr = r[0];
   *vcorr = r[1];
+}
+
+void av1_convolve_2d_sr_hip(const uint8_t* src, int src_stride, uint8_t* dst, int dst_stride,
+                            int w, int h, const LavishInterpFilterParams* fpx,
+                            const LavishInterpFilterParams* fpy, const int subpel_x_qn,
+                            const int subpel_y_qn, LavishConvolveParams* cp) {
+  conv_shim<uint8_t>(src, src_stride, dst, dst_stride, w, h, 3, fpx, subpel_x_qn, fpy,
+                     subpel_y_qn, cp->round_0, cp->round_1, 8);
+}
+void av1_convolve_x_sr_hip(const uint8_t* src, int src_stride, uint8_t* dst, int dst_stride,
+                           int w, int h, const LavishInterpFilterParams* fpx,
+                           const int subpel_x_qn, LavishConvolveParams* cp) {
+  conv_shim<uint8_t>(src, src_stride, dst, dst_stride, w, h, 1, fpx, subpel_x_qn, nullptr, 0,
+                     cp->round_0, cp->round_1, 8);
+}
+void av1_convolve_y_sr_hip(const uint8_t* src, int src_stride, uint8_t* dst, int dst_stride,
+                           int w, int h, const LavishInterpFilterParams* fpy,
+                           const int subpel_y_qn) {
+  conv_shim<uint8_t>(src, src_stride, dst, dst_stride, w, h, 2, nullptr, 0, fpy, subpel_y_qn, 3,
+                     11, 8);
+}
+void av1_highbd_convolve_2d_sr_hip(const uint16_t* src, int src_stride, uint16_t* dst,
+                                   int dst_stride, int w, int h,
+                                   const LavishInterpFilterParams* fpx,
+                                   const LavishInterpFilterParams* fpy, const int subpel_x_qn,
+                                   const int subpel_y_qn, LavishConvolveParams* cp, int bd) {
+  conv_shim<uint16_t>(src, src_stride, dst, dst_stride, w, h, 3, fpx, subpel_x_qn, fpy,
+                      subpel_y_qn, cp->round_0, cp->round_1, bd);
+}
+void av1_highbd_convolve_x_sr_hip(const uint16_t* src, int src_stride, uint16_t* dst,
+                                  int dst_stride, int w, int h,
+                                  const LavishInterpFilterParams* fpx, const int subpel_x_qn,
+                                  LavishConvolveParams* cp, int bd) {
+  conv_shim<uint16_t>(src, src_stride, dst, dst_stride, w, h, 1, fpx, subpel_x_qn, nullptr, 0,
+                      cp->round_0, cp->round_1, bd);
+}
+void av1_highbd_convolve_y_sr_hip(const uint16_t* src, int src_stride, uint16_t* dst,
+                                  int dst_stride, int w, int h,
+                                  const LavishInterpFilterParams* fpy, const int subpel_y_qn,
+                                  int bd) {
+  conv_shim<uint16_t>(src, src_stride, dst, dst_stride, w, h, 2, nullptr, 0, fpy, subpel_y_qn,
+                      3, 11, bd);
+}
+void aom_convolve_copy_hip(const uint8_t* src, ptrdiff_t src_stride, uint8_t* dst,
+                           ptrdiff_t dst_stride, int w, int h) {
+  conv_shim<uint8_t>(src, src_stride, dst, dst_stride, w, h, 0, nullptr, 0, nullptr, 0, 3, 11, 8);
+}
+void aom_highbd_convolve_copy_hip(const uint16_t* src, ptrdiff_t src_stride, uint16_t* dst,
+                                  ptrdiff_t dst_stride, int w, int h) {
+  conv_shim<uint16_t>(src, src_stride, dst, dst_stride, w, h, 0, nullptr, 0, nullptr, 0, 3, 11,
+                      12);
 }
 
 }  // extern "C"

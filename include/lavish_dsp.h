@@ -390,6 +390,44 @@ int lavish_subpel_search_after_diamond(const uint8_t *src, int src_stride,
                                        int iters_per_step, int mv_cost_type,
                                        LavishSubpelResult *out, void *stream);
 
+/* ---- Inter prediction -----------------------------
+ * av1_enc_build_one_inter_predictor (av1/encoder/reconinter_enc.c:47-51) for
+ * a batch of single-reference translational blocks: init_subpel_params
+ * (av1/common/reconinter.h:131-165, unscaled, border clamp), the block-size
+ * filter choice (filter.h:253-259) and convolve_2d_facade_single
+ * (av1/common/convolve.c:614-634 / highbd :1106-1128).
+ *   ref: plane origin (buf0) of the reference, with the reference's
+ *        AOM_BORDER_IN_PIXELS >> ss border around it (per direction; 12-tap
+ *        MULTITAP_SHARP2 reads one more row / column at the clamp extremes,
+ *        as the C does); ref_width / height: the plane's size (the clamp
+ *        window).
+ *   w, h: 2..128 (powers of two); ss_x / ss_y: the plane's subsampling.
+ *   highbd 0: u8 planes (bit_depth 8); 1: u16 planes, bit_depth 8/10/12.
+ * dst[job.dst_off + y * dst_stride + x] receives the prediction. */
+typedef struct LavishInterPredJob {
+  int64_t ref_off;             /* element offset of this job's reference plane origin */
+  int64_t dst_off;             /* element offset of the block's first output pixel */
+  int32_t pix_row, pix_col;    /* block position in the plane (pixels) */
+  int16_t mv_row, mv_col;      /* MV, 1/8 luma pel */
+  uint8_t filter_x, filter_y;  /* InterpFilter: 0 REGULAR 1 SMOOTH 2 SHARP 3 BILINEAR 4 SHARP2 */
+  uint8_t pad[2];
+} LavishInterPredJob;
+
+int lavish_build_inter_pred_batch(const void *ref, int ref_stride, int ref_width,
+                                  int ref_height, int ss_x, int ss_y, int w, int h,
+                                  const LavishInterPredJob *jobs, int njobs,
+                                  void *dst, int dst_stride, int bit_depth,
+                                  int highbd, void *stream);
+/* The same with job j's mv taken from a sub-pel search result (chained on
+ * the device after lavish_subpel_search_batch / _after_diamond). */
+int lavish_build_inter_pred_after_subpel(const void *ref, int ref_stride,
+                                         int ref_width, int ref_height, int ss_x,
+                                         int ss_y, int w, int h,
+                                         const LavishInterPredJob *jobs,
+                                         const LavishSubpelResult *mvs, int njobs,
+                                         void *dst, int dst_stride, int bit_depth,
+                                         int highbd, void *stream);
+
 /* ---- TX-type pruning features ---------------------
  * Every full bw x bh block of an int16 residual plane (raster order):
  * av1_get_horver_correlation_full (av1/encoder/rdopt.c:514-609) -> hcorr /
@@ -645,6 +683,60 @@ int64_t av1_highbd_block_error_hip(const int32_t *coeff,
 /* av1_get_horver_correlation_full (av1/common/av1_rtcd_defs.pl:469) */
 void av1_get_horver_correlation_full_hip(const int16_t *diff, int stride, int w,
                                          int h, float *hcorr, float *vcorr);
+
+/* Convolution (av1/common/av1_rtcd_defs.pl:565-575, aom_dsp_rtcd_defs.pl:449,461).
+ * Layout mirrors of InterpFilterParams (av1/common/filter.h:105-109) and
+ * ConvolveParams (av1/common/convolve.h:21-32). */
+typedef struct LavishInterpFilterParams {
+  const int16_t *filter_ptr;
+  uint16_t taps;
+  uint8_t interp_filter;
+} LavishInterpFilterParams;
+typedef struct LavishConvolveParams {
+  int do_average;
+  uint16_t *dst;
+  int dst_stride;
+  int round_0;
+  int round_1;
+  int plane;
+  int is_compound;
+  int use_dist_wtd_comp_avg;
+  int fwd_offset;
+  int bck_offset;
+} LavishConvolveParams;
+void av1_convolve_2d_sr_hip(const uint8_t *src, int src_stride, uint8_t *dst,
+                            int dst_stride, int w, int h,
+                            const LavishInterpFilterParams *filter_params_x,
+                            const LavishInterpFilterParams *filter_params_y,
+                            const int subpel_x_qn, const int subpel_y_qn,
+                            LavishConvolveParams *conv_params);
+void av1_convolve_x_sr_hip(const uint8_t *src, int src_stride, uint8_t *dst,
+                           int dst_stride, int w, int h,
+                           const LavishInterpFilterParams *filter_params_x,
+                           const int subpel_x_qn, LavishConvolveParams *conv_params);
+void av1_convolve_y_sr_hip(const uint8_t *src, int src_stride, uint8_t *dst,
+                           int dst_stride, int w, int h,
+                           const LavishInterpFilterParams *filter_params_y,
+                           const int subpel_y_qn);
+void av1_highbd_convolve_2d_sr_hip(const uint16_t *src, int src_stride,
+                                   uint16_t *dst, int dst_stride, int w, int h,
+                                   const LavishInterpFilterParams *filter_params_x,
+                                   const LavishInterpFilterParams *filter_params_y,
+                                   const int subpel_x_qn, const int subpel_y_qn,
+                                   LavishConvolveParams *conv_params, int bd);
+void av1_highbd_convolve_x_sr_hip(const uint16_t *src, int src_stride,
+                                  uint16_t *dst, int dst_stride, int w, int h,
+                                  const LavishInterpFilterParams *filter_params_x,
+                                  const int subpel_x_qn,
+                                  LavishConvolveParams *conv_params, int bd);
+void av1_highbd_convolve_y_sr_hip(const uint16_t *src, int src_stride,
+                                  uint16_t *dst, int dst_stride, int w, int h,
+                                  const LavishInterpFilterParams *filter_params_y,
+                                  const int subpel_y_qn, int bd);
+void aom_convolve_copy_hip(const uint8_t *src, ptrdiff_t src_stride, uint8_t *dst,
+                           ptrdiff_t dst_stride, int w, int h);
+void aom_highbd_convolve_copy_hip(const uint16_t *src, ptrdiff_t src_stride,
+                                  uint16_t *dst, ptrdiff_t dst_stride, int w, int h);
 
 #ifdef __cplusplus
 }

@@ -264,6 +264,24 @@ long orc_txq_plane(const int16_t *residual, int stride, int width, int height,
                    const OrcQuant *q, int quant_b, int32_t *qcoeff,
                    int32_t *dqcoeff, uint16_t *eob, int threads);
 
+/* ---- inter prediction (8(f) rank 2): oracle_convolve.c ---- */
+#define FILTER_BITS_ORC 7
+typedef struct OrcInterPredJob {
+  int64_t ref_off, dst_off;
+  int32_t pix_row, pix_col;
+  int16_t mv_row, mv_col;
+  uint8_t filter_x, filter_y, pad[2];
+} OrcInterPredJob;
+int orc_interp_kernel(int interp_filter, int size, int subpel, int16_t *out);
+void orc_conv_rounds(int bd, int *round_0, int *round_1);
+void orc_convolve_block(const void *src, ptrdiff_t ss, void *dst, ptrdiff_t ds, int w, int h,
+                        int path, const int16_t *fx, int tx, const int16_t *fy, int ty,
+                        int round_0, int round_1, int bd, int hbd);
+long orc_build_inter_pred_batch(const void *ref, int ref_stride, int ref_width, int ref_height,
+                                int ss_x, int ss_y, int w, int h, const OrcInterPredJob *jobs,
+                                long njobs, const OrcSubpelResult *mvs, void *dst,
+                                int dst_stride, int bd, int hbd);
+
 #ifdef __cplusplus
 }
 #endif

@@ -450,3 +450,67 @@ def tx_prune_features(res, bw, bh):
     vf = np.zeros((nb, 16), np.float32)
     L.orc_tx_prune_features(P(res), W, W, H, bw, bh, P(hf), P(vf))
     return hf, vf
+
+
+# ------------------------------------------------- inter prediction --
+INTER_JOB = np.dtype([("ref_off", "<i8"), ("dst_off", "<i8"), ("pix_row", "<i4"),
+                      ("pix_col", "<i4"), ("mv_row", "<i2"), ("mv_col", "<i2"),
+                      ("filter_x", "u1"), ("filter_y", "u1"), ("pad", "u1", (2,))], align=True)
+
+
+def interp_kernel(interp_filter, size, subpel):
+    """orc_interp_kernel: the kernel row the oracle uses (taps, int16 array)."""
+    L = lib()
+    L.orc_interp_kernel.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
+    out = np.zeros(12, np.int16)
+    taps = L.orc_interp_kernel(interp_filter, size, subpel, P(out))
+    return out[:taps]
+
+
+def conv_rounds(bd):
+    L = lib()
+    r0, r1 = ctypes.c_int(), ctypes.c_int()
+    L.orc_conv_rounds(bd, ctypes.byref(r0), ctypes.byref(r1))
+    return r0.value, r1.value
+
+
+def convolve_block(src, src_off, ss, w, h, path, fx, fy, round_0, round_1, bd):
+    """orc_convolve_block on a numpy plane (uint8 / uint16); src_off = element
+    offset of the block's integer position.  Returns the (h, w) block."""
+    L = lib()
+    L.orc_convolve_block.argtypes = [ctypes.c_void_p, ctypes.c_ssize_t, ctypes.c_void_p,
+                                     ctypes.c_ssize_t, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                     ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p,
+                                     ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                     ctypes.c_int]
+    hb = src.dtype == np.uint16
+    out = np.zeros((h, w), src.dtype)
+    fx = np.ascontiguousarray(fx if fx is not None else np.zeros(8), np.int16)
+    fy = np.ascontiguousarray(fy if fy is not None else np.zeros(8), np.int16)
+    L.orc_convolve_block(ctypes.c_void_p(src.ctypes.data + src_off * src.itemsize), ss, P(out),
+                         w, w, h, path, P(fx), len(fx), P(fy), len(fy), round_0, round_1, bd,
+                         int(hb))
+    return out
+
+
+def build_inter_pred(ref, ref_origin, ref_width, ref_height, ss_x, ss_y, w, h, jobs, dst_shape,
+                     bd=8, mvs=None, dst_stride=None):
+    """orc_build_inter_pred_batch over INTER_JOB records; ref is a bordered
+    numpy plane whose frame origin is element offset ref_origin."""
+    L = lib()
+    L.orc_build_inter_pred_batch.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
+                                             ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                             ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
+                                             ctypes.c_long, ctypes.c_void_p, ctypes.c_void_p,
+                                             ctypes.c_int, ctypes.c_int, ctypes.c_int]
+    L.orc_build_inter_pred_batch.restype = ctypes.c_long
+    hb = ref.dtype == np.uint16
+    jobs = np.ascontiguousarray(jobs)
+    out = np.zeros(dst_shape, ref.dtype)
+    ds = out.shape[-1] if dst_stride is None else dst_stride
+    m = None if mvs is None else np.ascontiguousarray(mvs)
+    L.orc_build_inter_pred_batch(ctypes.c_void_p(ref.ctypes.data + ref_origin * ref.itemsize),
+                                 ref.strides[0] // ref.itemsize, ref_width, ref_height, ss_x,
+                                 ss_y, w, h, P(jobs), len(jobs),
+                                 None if m is None else P(m), P(out), ds, bd, int(hb))
+    return out
