@@ -233,7 +233,74 @@ __device__ void generic_block(const T* src, int64_t rs, T* dst, int64_t ds, int 
     }
 }
 
-template <typename T, int CW, int R>
+// 4 negated taps as packed signed bytes (every 8-tap kernel's negation fits
+// i8: the taps lie in [-24, 128])
+__device__ __forceinline__ int pack_neg4(const int16_t* f) {
+  return (int)((uint32_t)(uint8_t)(-f[0]) | ((uint32_t)(uint8_t)(-f[1]) << 8) |
+               ((uint32_t)(uint8_t)(-f[2]) << 16) | ((uint32_t)(uint8_t)(-f[3]) << 24));
+}
+
+// u8 prediction with the default rounding (round_0 3, round_1 11, bd 8)
+// through the 2-D form for every phase: with the phase-0 kernel (128 at the
+// centre) the 2-D rounding reduces exactly to the x-only / y-only / copy
+// results (im = 16 p + 2^11 or rpot(s, 3) + 2^11; the vertical offsets
+// cancel), so one branch-free path serves all four facade cases.
+// Horizontal taps run as v_dot4_i32_i8 on (p - 128) bytes against the
+// negated kernel: sum f p = 128 * 128 - dot(-f, p - 128).
+template <int R>
+__device__ __forceinline__ void u8_2d(const uint8_t* src, int64_t rs, uint8_t* dst, int64_t ds,
+                                      const int16_t* fx, const int16_t* fy) {
+  const int nlo = pack_neg4(fx), nhi = pack_neg4(fx + 4);
+  int ky[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) ky[k] = fy[k];
+  constexpr int kC1 = 16384 + (1 << 14) + 4;  // 128 * 128 + 2^(bd + 6) + rounding of >> 3
+  int im[R + 7][4];
+#pragma unroll
+  for (int i = 0; i < R + 7; ++i) {
+    const uintptr_t ad = (uintptr_t)(src + (i - 3) * rs - 3);
+    const gptr q = (gptr)(ad & ~(uintptr_t)3);
+    const uint32_t sh = (uint32_t)(ad & 3);
+    const uint32_t d0 = q[0], d1 = q[1], d2 = q[2], d3 = q[3];
+    const uint32_t e0 = __builtin_amdgcn_alignbyte(d1, d0, sh) ^ 0x80808080u;
+    const uint32_t e1 = __builtin_amdgcn_alignbyte(d2, d1, sh) ^ 0x80808080u;
+    const uint32_t e2 = __builtin_amdgcn_alignbyte(d3, d2, sh) ^ 0x80808080u;
+    const int w[8] = {(int)e0,
+                      (int)__builtin_amdgcn_alignbyte(e1, e0, 1),
+                      (int)__builtin_amdgcn_alignbyte(e1, e0, 2),
+                      (int)__builtin_amdgcn_alignbyte(e1, e0, 3),
+                      (int)e1,
+                      (int)__builtin_amdgcn_alignbyte(e2, e1, 1),
+                      (int)__builtin_amdgcn_alignbyte(e2, e1, 2),
+                      (int)__builtin_amdgcn_alignbyte(e2, e1, 3)};
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const int t = __builtin_amdgcn_sdot4(nhi, w[c + 4], __builtin_amdgcn_sdot4(nlo, w[c], 0, false),
+                                           false);
+      im[i][c] = (kC1 - t) >> 3;
+    }
+  }
+  // vertical: rpot(s, 11) - offsets folded into the accumulator's start
+  constexpr int kOb = 8 + 14 - 3;
+  constexpr int kVoff = (1 << (kOb - 11)) + (1 << (kOb - 12));
+  constexpr int kVinit = (1 << kOb) + (1 << 10) - (kVoff << 11);
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    int o[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      int s = kVinit;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) s += ky[k] * im[r + k][c];
+      o[c] = clip_bd(s >> 11, 255);
+    }
+    store_px<4>(dst + r * ds, o);
+  }
+}
+
+// FAST: the u8 batch path (default rounding, table kernels) -- only the
+// branch-free 2-D form and the 12-tap path are compiled in
+template <typename T, int CW, int R, bool FAST>
 __global__ __launch_bounds__(256) void inter_kernel(IpArgs a) {
   const int ncg = a.w / CW;
   const int tpj = ncg * (a.h / R);
@@ -241,10 +308,10 @@ __global__ __launch_bounds__(256) void inter_kernel(IpArgs a) {
   // windows) land on the same XCD's L2
   const int nwg = gridDim.x;  // multiple of 8
   const int wg = (blockIdx.x & 7) * (nwg >> 3) + (blockIdx.x >> 3);
-  const int64_t gid = (int64_t)wg * 256 + threadIdx.x;
-  const int64_t j = gid / tpj;
-  if (j >= a.njobs) return;
-  const int sub = (int)(gid - j * tpj);
+  const uint32_t gid = (uint32_t)wg * 256u + threadIdx.x;  // < 2^31 (host check)
+  const uint32_t j = gid / (uint32_t)tpj;
+  if (j >= (uint32_t)a.njobs) return;
+  const int sub = (int)(gid - j * (uint32_t)tpj);
   const int rsi = sub / ncg, cg = sub - rsi * ncg;
   const IJob jb = a.jobs[j];
   const T* src;
@@ -276,10 +343,13 @@ __global__ __launch_bounds__(256) void inter_kernel(IpArgs a) {
     const int f_x = jb.filter_x, f_y = jb.filter_y;
     const int kx = a.w <= 4 ? (f_x == 1 ? 5 : f_x == 3 ? 3 : 4) : f_x;
     const int ky = a.h <= 4 ? (f_y == 1 ? 5 : f_y == 3 ? 3 : 4) : f_y;
-    tx = f_x == 4 ? 12 : 8;
-    ty = f_y == 4 ? 12 : 8;
-    fx = f_x == 4 ? kK12[sx] : kK8[kx > 5 ? 0 : kx][sx];
-    fy = f_y == 4 ? kK12[sy] : kK8[ky > 5 ? 0 : ky][sy];
+    // a direction at phase 0 is not filtered: the 8-tap identity row stands
+    // in for it (the FAST path runs every job through the 2-D form)
+    const bool x12 = f_x == 4 && sx, y12 = f_y == 4 && sy;
+    tx = x12 ? 12 : 8;
+    ty = y12 ? 12 : 8;
+    fx = x12 ? kK12[sx] : kK8[kx > 5 ? 0 : kx][sx];
+    fy = y12 ? kK12[sy] : kK8[ky > 5 ? 0 : ky][sy];
   }
   src += (int64_t)(rsi * R) * a.rs + cg * CW;
   T* dst = (T*)a.dst + jb.dst_off + (int64_t)(rsi * R) * a.ds + cg * CW;
@@ -289,79 +359,84 @@ __global__ __launch_bounds__(256) void inter_kernel(IpArgs a) {
     generic_block<T, CW, R>(src, a.rs, dst, a.ds, path, fx, tx, fy, ty, a.bd, a.r0, a.r1);
     return;
   }
-  int kx[8], ky[8];
+  if constexpr (FAST) {
+    u8_2d<R>((const uint8_t*)src, a.rs, (uint8_t*)dst, a.ds, fx, fy);
+    return;
+  } else {
+    int kx[8], ky[8];
 #pragma unroll
-  for (int k = 0; k < 8; ++k) {
-    kx[k] = fx[k];
-    ky[k] = fy[k];
-  }
-  if (path == 0) {  // aom_convolve_copy
-#pragma unroll
-    for (int r = 0; r < R; ++r) {
-      int p[CW];
-      load_px<CW>(src + r * a.rs, p);
-      store_px<CW>(dst + r * a.ds, p);
+    for (int k = 0; k < 8; ++k) {
+      kx[k] = fx[k];
+      ky[k] = fy[k];
     }
-  } else if (path == 1) {  // av1_convolve_x_sr
-    const int r0 = a.r0, bits = 7 - a.r0;
+    if (path == 0) {  // aom_convolve_copy
 #pragma unroll
-    for (int r = 0; r < R; ++r) {
-      int p[CW + 7], o[CW];
-      load_px<CW + 7>(src + r * a.rs - 3, p);
-#pragma unroll
-      for (int c = 0; c < CW; ++c) {
-        int s = 0;
-#pragma unroll
-        for (int k = 0; k < 8; ++k) s += kx[k] * p[c + k];
-        o[c] = clip_bd(rpot(rpot(s, r0), bits), mx);
+      for (int r = 0; r < R; ++r) {
+        int p[CW];
+        load_px<CW>(src + r * a.rs, p);
+        store_px<CW>(dst + r * a.ds, p);
       }
-      store_px<CW>(dst + r * a.ds, o);
-    }
-  } else if (path == 2) {  // av1_convolve_y_sr
-    int col[R + 7][CW];
+    } else if (path == 1) {  // av1_convolve_x_sr
+      const int r0 = a.r0, bits = 7 - a.r0;
 #pragma unroll
-    for (int i = 0; i < R + 7; ++i) load_px<CW>(src + (i - 3) * a.rs, col[i]);
+      for (int r = 0; r < R; ++r) {
+        int p[CW + 7], o[CW];
+        load_px<CW + 7>(src + r * a.rs - 3, p);
 #pragma unroll
-    for (int r = 0; r < R; ++r) {
-      int o[CW];
+        for (int c = 0; c < CW; ++c) {
+          int s = 0;
 #pragma unroll
-      for (int c = 0; c < CW; ++c) {
-        int s = 0;
-#pragma unroll
-        for (int k = 0; k < 8; ++k) s += ky[k] * col[r + k][c];
-        o[c] = clip_bd(rpot(s, 7), mx);
+          for (int k = 0; k < 8; ++k) s += kx[k] * p[c + k];
+          o[c] = clip_bd(rpot(rpot(s, r0), bits), mx);
+        }
+        store_px<CW>(dst + r * a.ds, o);
       }
-      store_px<CW>(dst + r * a.ds, o);
-    }
-  } else {  // av1_convolve_2d_sr
-    const int r0 = a.r0, r1 = a.r1, bits = 14 - r0 - r1;
-    const int hoff = 1 << (a.bd + 6);
-    const int ob = a.bd + 14 - r0;
-    const int voff = (1 << (ob - r1)) + (1 << (ob - r1 - 1));
-    int im[R + 7][CW];
+    } else if (path == 2) {  // av1_convolve_y_sr
+      int col[R + 7][CW];
 #pragma unroll
-    for (int i = 0; i < R + 7; ++i) {
-      int p[CW + 7];
-      load_px<CW + 7>(src + (i - 3) * a.rs - 3, p);
+      for (int i = 0; i < R + 7; ++i) load_px<CW>(src + (i - 3) * a.rs, col[i]);
 #pragma unroll
-      for (int c = 0; c < CW; ++c) {
-        int s = hoff;
+      for (int r = 0; r < R; ++r) {
+        int o[CW];
 #pragma unroll
-        for (int k = 0; k < 8; ++k) s += kx[k] * p[c + k];
-        im[i][c] = (int)(int16_t)rpot(s, r0);
+        for (int c = 0; c < CW; ++c) {
+          int s = 0;
+#pragma unroll
+          for (int k = 0; k < 8; ++k) s += ky[k] * col[r + k][c];
+          o[c] = clip_bd(rpot(s, 7), mx);
+        }
+        store_px<CW>(dst + r * a.ds, o);
       }
-    }
+    } else {  // av1_convolve_2d_sr
+      const int r0 = a.r0, r1 = a.r1, bits = 14 - r0 - r1;
+      const int hoff = 1 << (a.bd + 6);
+      const int ob = a.bd + 14 - r0;
+      const int voff = (1 << (ob - r1)) + (1 << (ob - r1 - 1));
+      int im[R + 7][CW];
 #pragma unroll
-    for (int r = 0; r < R; ++r) {
-      int o[CW];
+      for (int i = 0; i < R + 7; ++i) {
+        int p[CW + 7];
+        load_px<CW + 7>(src + (i - 3) * a.rs - 3, p);
 #pragma unroll
-      for (int c = 0; c < CW; ++c) {
-        int s = 1 << ob;
+        for (int c = 0; c < CW; ++c) {
+          int s = hoff;
 #pragma unroll
-        for (int k = 0; k < 8; ++k) s += ky[k] * im[r + k][c];
-        o[c] = clip_bd(rpot(rpot(s, r1) - voff, bits), mx);
+          for (int k = 0; k < 8; ++k) s += kx[k] * p[c + k];
+          im[i][c] = (int)(int16_t)rpot(s, r0);
+        }
       }
-      store_px<CW>(dst + r * a.ds, o);
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        int o[CW];
+#pragma unroll
+        for (int c = 0; c < CW; ++c) {
+          int s = 1 << ob;
+#pragma unroll
+          for (int k = 0; k < 8; ++k) s += ky[k] * im[r + k][c];
+          o[c] = clip_bd(rpot(rpot(s, r1) - voff, bits), mx);
+        }
+        store_px<CW>(dst + r * a.ds, o);
+      }
     }
   }
 }
@@ -370,13 +445,27 @@ template <typename T, int CW>
 void launch_cw(const IpArgs& a, hipStream_t s) {
   const int R = a.h < 8 ? a.h : 8;
   const int64_t threads = (int64_t)a.njobs * (a.w / CW) * (a.h / R);
+  if (threads >= (1LL << 31) - 256 * 8) {
+    set_error("lavish_build_inter_pred_batch: job list too large for one launch",
+              hipErrorInvalidValue, __FILE__, __LINE__);
+    return;
+  }
   const int nwg = (int)(((threads + 255) / 256 + 7) & ~7LL);
-  if (R == 8)
-    hipLaunchKernelGGL((inter_kernel<T, CW, 8>), dim3(nwg), dim3(256), 0, s, a);
-  else if (R == 4)
-    hipLaunchKernelGGL((inter_kernel<T, CW, 4>), dim3(nwg), dim3(256), 0, s, a);
-  else
-    hipLaunchKernelGGL((inter_kernel<T, CW, 2>), dim3(nwg), dim3(256), 0, s, a);
+  constexpr bool kFastOk = sizeof(T) == 1 && CW == 4;
+  if (kFastOk && !a.custom) {
+    if (R == 8)
+      hipLaunchKernelGGL((inter_kernel<T, CW, 8, kFastOk>), dim3(nwg), dim3(256), 0, s, a);
+    else if (R == 4)
+      hipLaunchKernelGGL((inter_kernel<T, CW, 4, kFastOk>), dim3(nwg), dim3(256), 0, s, a);
+    else
+      hipLaunchKernelGGL((inter_kernel<T, CW, 2, kFastOk>), dim3(nwg), dim3(256), 0, s, a);
+  } else if (R == 8) {
+    hipLaunchKernelGGL((inter_kernel<T, CW, 8, false>), dim3(nwg), dim3(256), 0, s, a);
+  } else if (R == 4) {
+    hipLaunchKernelGGL((inter_kernel<T, CW, 4, false>), dim3(nwg), dim3(256), 0, s, a);
+  } else {
+    hipLaunchKernelGGL((inter_kernel<T, CW, 2, false>), dim3(nwg), dim3(256), 0, s, a);
+  }
   LAVISH_CHECK(hipGetLastError());
 }
 

@@ -51,7 +51,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--workload", choices=("rdo", "c2", "c3", "c3sub", "c4", "c4px", "c5"),
+    ap.add_argument("--workload", choices=("rdo", "c2", "c3", "c3sub", "c4", "c4px", "c5", "inter"),
                     default="rdo")
     ap.add_argument("--rdmult", type=int, default=2000)
     ap.add_argument("--width", type=int, default=1920)
@@ -300,10 +300,154 @@ def main_c4(args):
         dist.destroy_process_group()
 
 
+INTER_BORDER = 288  # AOM_BORDER_IN_PIXELS: the clamp window of init_subpel_params
+
+
+def inter_setup(W, H, nrefs, seed):
+    """Inter-prediction workload: nrefs bordered 8-bit references and one job
+    per 16x16 block x reference with a seeded sub-pel mv (+-32 px) and a
+    seeded dual-filter pair from {REGULAR, SMOOTH, SHARP}."""
+    import lavish_dsp.inter as I
+    import lavish_dsp.synth as synth
+    _, refs = synth.motion_planes(W, H, nrefs, INTER_BORDER, seed=seed)
+    plane = refs[0].size
+    org = INTER_BORDER * refs.shape[2] + INTER_BORDER
+    rng = np.random.default_rng(seed)
+    jobs = []
+    for k in range(nrefs):
+        n = (W // C3_BLOCK) * (H // C3_BLOCK)
+        j = I.plane_jobs(W, H, C3_BLOCK, C3_BLOCK, rng.integers(-256, 257, size=(n, 2)),
+                         rng.integers(0, 3, size=(n, 2)), ref_off=k * plane)
+        j["dst_off"] += k * W * H
+        jobs.append(j)
+    return refs, org, np.concatenate(jobs)
+
+
+def inter_bytes(W, H, nrefs, njobs):
+    """Algorithmic bytes of one step: every reference pixel read once and every
+    prediction pixel written once (u8), plus the 32 B job records; the
+    per-block source windows ((16 + 7)^2 per block) overlap and are L2 hits."""
+    return nrefs * 2 * W * H + 32 * njobs
+
+
+def cpu_baseline_inter(args):
+    """orc_build_inter_pred_batch (one thread) on a 1920x256 strip of the same
+    workload, repeated for ~cpu_seconds; SB64/s."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import _oracle as O
+    W, Hs = args.width, 256
+    refs, org, jobs = inter_setup(W, Hs, args.refs, 1234)
+    flat = refs.reshape(refs.shape[0] * refs.shape[1], refs.shape[2])
+    sb = sb64_count(W, Hs)
+    passes = 0
+    t0 = time.perf_counter()
+    while True:
+        O.build_inter_pred(flat, org, W, Hs, 0, 0, C3_BLOCK, C3_BLOCK, jobs,
+                           (args.refs * Hs, W))
+        passes += 1
+        dt = time.perf_counter() - t0
+        if dt >= args.cpu_seconds:
+            break
+    return {"value": round(passes * sb / dt, 2), "unit": "SB64/s", "cores": 1, "kind": "port",
+            "sample": "%d passes of a %dx%d strip (%d SB64, %d predictions) through the inter "
+                      "step, oracle C restatement (-O3, 1 thread), %.1f s"
+                      % (passes, W, Hs, sb, len(jobs), dt)}
+
+
+def main_inter(args):
+    """Single-reference inter prediction of every 16x16 block against every
+    reference (lavish_build_inter_pred_batch), one 1080p frame per step."""
+    import torch
+    import torch.distributed as dist
+    import lavish_dsp as L
+    import lavish_dsp.inter as I
+    import lavish_dsp.motion as M
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local_rank)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    W, H = args.width, args.height
+    refs, org, jobs_np = inter_setup(W, H, args.refs, 1234 + rank)
+    tref = torch.from_numpy(refs.reshape(-1, refs.shape[2])).cuda()
+    tjobs = M.to_device(jobs_np)
+    dst = torch.empty((args.refs * H, W), dtype=torch.uint8, device="cuda")
+    stream = torch.cuda.current_stream()
+
+    def step():
+        I.build_inter_pred_batch(tref, org, W, H, C3_BLOCK, C3_BLOCK, tjobs, dst=dst,
+                                 stream=stream)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+          for _ in range(args.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        ev[k][0].record(stream)
+        step()
+        ev[k][1].record(stream)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    status = L.status()
+    if status[0] != 0:
+        raise RuntimeError("HIP error during bench: %s" % (status,))
+    k_ms = sum(a.elapsed_time(b) for a, b in ev) / args.steps
+    nbytes = inter_bytes(W, H, args.refs, len(jobs_np))
+    sb = sb64_count(W, H)
+    line = {
+        "metric": METRIC,
+        "value": round(world * sb * args.steps / elapsed, 2),
+        "unit": "SB64/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u8",
+        "data": "synthetic (seeded 1080p content, lavish_dsp/synth.py; seeded mvs / filters)",
+        "config": {
+            "workload": "inter: %dx%d 8-bit; single-reference inter prediction "
+                        "(av1_enc_build_one_inter_predictor: border clamp, dual-filter 8-tap "
+                        "REGULAR/SMOOTH/SHARP, x/y/2d sub-pel convolution) of every %dx%d block "
+                        "x %d refs, %d predictions; %d SB64/frame"
+                        % (W, H, C3_BLOCK, C3_BLOCK, args.refs, len(jobs_np), sb),
+            "parallelism": "frame-per-rank x%d" % world,
+        },
+        "roofline": {"bound": "hbm", "kernel": "inter_kernel<u8,4,8> "
+                     "(lavish_build_inter_pred_batch)",
+                     "achieved": round(nbytes / (k_ms * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "traffic": None, "avg_launch_ms": round(k_ms, 4),
+                     "algorithmic_bytes_per_launch": nbytes},
+    }
+    line["roofline"]["frac"] = round(line["roofline"]["achieved"] / HBM_PEAK_GBS, 4)
+    if rank == 0 and world == 1 and not args.no_cpu:
+        line["cpu_baseline"] = cpu_baseline_inter(args)
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def main():
     args = parse()
     if args.workload in ("c4", "c4px", "c5"):
         return main_c4(args)
+    if args.workload == "inter":
+        return main_inter(args)
     import torch
     import torch.distributed as dist
     import lavish_dsp as L
