@@ -125,6 +125,7 @@ struct IpArgs {
 enum { kCPath = 0, kCTx = 1, kCTy = 2, kCFx = 4, kCFy = 16, kCustomLen = 28 };
 
 typedef const __attribute__((address_space(1))) uint32_t* gptr;
+typedef uint32_t u4a __attribute__((ext_vector_type(4), aligned(4)));
 
 __device__ __forceinline__ int rpot(int v, int n) { return (v + ((1 << n) >> 1)) >> n; }
 __device__ __forceinline__ int clip_bd(int v, int mx) { return v < 0 ? 0 : v > mx ? mx : v; }
@@ -261,7 +262,10 @@ __device__ __forceinline__ void u8_2d(const uint8_t* src, int64_t rs, uint8_t* d
     const uintptr_t ad = (uintptr_t)(src + (i - 3) * rs - 3);
     const gptr q = (gptr)(ad & ~(uintptr_t)3);
     const uint32_t sh = (uint32_t)(ad & 3);
-    const uint32_t d0 = q[0], d1 = q[1], d2 = q[2], d3 = q[3];
+    // one 16-byte load per row (4-byte aligned: the hardware's unaligned
+    // mode serves it; a quarter of the vector-memory instructions)
+    const u4a v = *(const __attribute__((address_space(1))) u4a*)q;
+    const uint32_t d0 = v.x, d1 = v.y, d2 = v.z, d3 = v.w;
     const uint32_t e0 = __builtin_amdgcn_alignbyte(d1, d0, sh) ^ 0x80808080u;
     const uint32_t e1 = __builtin_amdgcn_alignbyte(d2, d1, sh) ^ 0x80808080u;
     const uint32_t e2 = __builtin_amdgcn_alignbyte(d3, d2, sh) ^ 0x80808080u;
@@ -280,26 +284,57 @@ __device__ __forceinline__ void u8_2d(const uint8_t* src, int64_t rs, uint8_t* d
       im[i][c] = (kC1 - t) >> 3;
     }
   }
-  // vertical: rpot(s, 11) - offsets folded into the accumulator's start
+  // vertical: rpot(s, 11) - offsets folded into the accumulator's start;
+  // the im rows (int16 for u8 input) pair up as (2i, 2i+1) / (2i+1, 2i+2)
+  // for v_dot2_i32_i16 against the tap pairs
   constexpr int kOb = 8 + 14 - 3;
   constexpr int kVoff = (1 << (kOb - 11)) + (1 << (kOb - 12));
   constexpr int kVinit = (1 << kOb) + (1 << 10) - (kVoff << 11);
+  typedef short s2 __attribute__((ext_vector_type(2)));
+  s2 kp[4];
+#pragma unroll
+  for (int m = 0; m < 4; ++m) kp[m] = s2{(short)ky[2 * m], (short)ky[2 * m + 1]};
+  constexpr int NP = (R + 7) / 2 + 1;  // (2i, 2i+1) pairs covering rows 0 .. R + 6
+  uint32_t pe[NP][4];
+#pragma unroll
+  for (int i = 0; i < NP; ++i)
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const uint32_t lo = 2 * i < R + 7 ? (uint32_t)im[2 * i][c] : 0u;
+      const uint32_t hi = 2 * i + 1 < R + 7 ? (uint32_t)im[2 * i + 1][c] : 0u;
+      pe[i][c] = __builtin_amdgcn_perm(hi, lo, 0x05040100u);
+    }
+  // output rows as packed bytes, stored after the loop (one alignment test)
+  uint32_t ow[R];
 #pragma unroll
   for (int r = 0; r < R; ++r) {
-    int o[4];
+    uint32_t w = 0;
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
       int s = kVinit;
 #pragma unroll
-      for (int k = 0; k < 8; ++k) s += ky[k] * im[r + k][c];
-      o[c] = clip_bd(s >> 11, 255);
+      for (int m = 0; m < 4; ++m) {
+        const int i = (r >> 1) + m;
+        // odd rows pair (2i+1, 2i+2): the upper half of pair i + lower of i+1
+        const uint32_t pr =
+            (r & 1) ? __builtin_amdgcn_alignbyte(pe[i + 1][c], pe[i][c], 2) : pe[i][c];
+        s = __builtin_amdgcn_sdot2(kp[m], __builtin_bit_cast(s2, pr), s, false);
+      }
+      w |= (uint32_t)clip_bd(s >> 11, 255) << (8 * c);
     }
-    store_px<4>(dst + r * ds, o);
+    ow[r] = w;
+  }
+  if ((((uintptr_t)dst | (uintptr_t)ds) & 3) == 0) {
+#pragma unroll
+    for (int r = 0; r < R; ++r) *(uint32_t*)(dst + r * ds) = ow[r];
+  } else {
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) dst[r * ds + c] = (uint8_t)(ow[r] >> (8 * c));
   }
 }
 
-// FAST: the u8 batch path (default rounding, table kernels) -- only the
-// branch-free 2-D form and the 12-tap path are compiled in
 template <typename T, int CW, int R, bool FAST>
 __global__ __launch_bounds__(256) void inter_kernel(IpArgs a) {
   const int ncg = a.w / CW;
@@ -443,7 +478,12 @@ __global__ __launch_bounds__(256) void inter_kernel(IpArgs a) {
 
 template <typename T, int CW>
 void launch_cw(const IpArgs& a, hipStream_t s) {
-  const int R = a.h < 8 ? a.h : 8;
+  constexpr bool kFastOk = sizeof(T) == 1 && CW == 4;
+  const bool fast = kFastOk && !a.custom;
+  // rows per thread: 16 amortises the 7 extra horizontal rows better, 8 keeps
+  // more waves resident (LAVISH_INTER_RMAX=8 selects it, for measurement)
+  static const int rmax = getenv("LAVISH_INTER_RMAX") ? atoi(getenv("LAVISH_INTER_RMAX")) : 16;
+  const int R = a.h < 8 ? a.h : (fast && a.h >= 16 && rmax >= 16 ? 16 : 8);
   const int64_t threads = (int64_t)a.njobs * (a.w / CW) * (a.h / R);
   if (threads >= (1LL << 31) - 256 * 8) {
     set_error("lavish_build_inter_pred_batch: job list too large for one launch",
@@ -451,9 +491,10 @@ void launch_cw(const IpArgs& a, hipStream_t s) {
     return;
   }
   const int nwg = (int)(((threads + 255) / 256 + 7) & ~7LL);
-  constexpr bool kFastOk = sizeof(T) == 1 && CW == 4;
-  if (kFastOk && !a.custom) {
-    if (R == 8)
+  if (fast) {
+    if (R == 16)
+      hipLaunchKernelGGL((inter_kernel<T, CW, 16, kFastOk>), dim3(nwg), dim3(256), 0, s, a);
+    else if (R == 8)
       hipLaunchKernelGGL((inter_kernel<T, CW, 8, kFastOk>), dim3(nwg), dim3(256), 0, s, a);
     else if (R == 4)
       hipLaunchKernelGGL((inter_kernel<T, CW, 4, kFastOk>), dim3(nwg), dim3(256), 0, s, a);

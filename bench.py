@@ -405,6 +405,12 @@ def main_inter(args):
         raise RuntimeError("HIP error during bench: %s" % (status,))
     k_ms = sum(a.elapsed_time(b) for a, b in ev) / args.steps
     nbytes = inter_bytes(W, H, args.refs, len(jobs_np))
+    traffic = None
+    if os.path.exists(args.pmc_json) and (W, H, args.refs) == (1920, 1080, 7):
+        try:
+            traffic = json.load(open(args.pmc_json)).get("inter", {}).get("hbm_bytes_per_launch")
+        except (ValueError, OSError):
+            traffic = None
     sb = sb64_count(W, H)
     line = {
         "metric": METRIC,
@@ -427,10 +433,10 @@ def main_inter(args):
                         % (W, H, C3_BLOCK, C3_BLOCK, args.refs, len(jobs_np), sb),
             "parallelism": "frame-per-rank x%d" % world,
         },
-        "roofline": {"bound": "hbm", "kernel": "inter_kernel<u8,4,8> "
+        "roofline": {"bound": "hbm", "kernel": "inter_kernel<u8,4,16,FAST> "
                      "(lavish_build_inter_pred_batch)",
                      "achieved": round(nbytes / (k_ms * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBS,
-                     "unit": "GB/s", "traffic": None, "avg_launch_ms": round(k_ms, 4),
+                     "unit": "GB/s", "traffic": traffic, "avg_launch_ms": round(k_ms, 4),
                      "algorithmic_bytes_per_launch": nbytes},
     }
     line["roofline"]["frac"] = round(line["roofline"]["achieved"] / HBM_PEAK_GBS, 4)
