@@ -485,6 +485,16 @@ void av1_get_horver_correlation_full_hip(const int16_t* diff, int stride, int w,
   *vcorr = r[1];
 }
 
+void av1_nn_predict_hip(const float* input_nodes, const LavishNNConfig* cfg, int reduce_prec,
+                        float* output) {
+  Stage st(kStageCap);
+  const float* din = st.copy_in(input_nodes, (size_t)cfg->num_inputs);
+  float* dout = (float*)st.take((size_t)cfg->num_outputs * sizeof(float));
+  must(lavish_nn_predict_batch(din, cfg, reduce_prec, dout, 1, st.s), "lavish_nn_predict_batch");
+  st.copy_out(output, dout, (size_t)cfg->num_outputs);
+  st.sync();
+}
+
 void av1_convolve_2d_sr_hip(const uint8_t* src, int src_stride, uint8_t* dst, int dst_stride,
                             int w, int h, const LavishInterpFilterParams* fpx,
                             const LavishInterpFilterParams* fpy, const int subpel_x_qn,

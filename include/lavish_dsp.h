@@ -445,6 +445,43 @@ int lavish_tx_prune_features_batch(const int16_t *residual, int stride,
                                    float *hfeatures, float *vfeatures,
                                    void *stream);
 
+/* Layout of NN_CONFIG (av1/encoder/ml.h:24-34): a caller passes the
+ * reference's own models (e.g. av1_tx_type_nnconfig_map_hor[tx_size]).
+ * Models are uploaded once per distinct content. */
+typedef struct LavishNNConfig {
+  int num_inputs;
+  int num_outputs;
+  int num_hidden_layers;
+  int num_hidden_nodes[10];
+  const float *weights[11];
+  const float *bias[11];
+} LavishNNConfig;
+
+/* prune_tx_2D (av1/encoder/tx_search.c:1487-1641) for every full tx_size
+ * block of an int16 residual plane (raster order): features, the two nets
+ * (av1_nn_predict_c with reduce_prec), av1_nn_fast_softmax_16_c, the
+ * adaptive threshold of (tx_set_type, prune_2d_txfm_mode), the sorting
+ * network and the TX_TYPE_PRUNE_4/5 cumulative cut.
+ *   allowed_in[block] (or allowed_default for every block when NULL): the
+ *   incoming allowed_tx_mask; allowed_out[block]: the pruned mask;
+ *   txk_map[block][16]: the search order (TX_TYPE values, 255 unused),
+ *   identity where prune_tx_2D leaves it untouched (tx set other than
+ *   ALL16 / DTT9_IDTX_1DDCT, mode 0, or nn_hor / nn_ver NULL).
+ * Float results follow the C functions bit for bit.  -2: tx size or
+ * threshold outside the reference's tables; -3: model shape unsupported
+ * (outputs != 4, > 16 inputs, differing depths, > 128 nodes). */
+int lavish_prune_tx_2d_batch(const int16_t *residual, int stride, int width,
+                             int height, int tx_size, int tx_set_type,
+                             int prune_2d_txfm_mode, const LavishNNConfig *nn_hor,
+                             const LavishNNConfig *nn_ver,
+                             const uint16_t *allowed_in, uint16_t allowed_default,
+                             uint16_t *allowed_out, uint8_t *txk_map,
+                             void *stream);
+/* av1_nn_predict_c (av1/encoder/ml.c:31-70) for n input vectors
+ * (inputs[n][num_inputs] -> outputs[n][num_outputs], device memory). */
+int lavish_nn_predict_batch(const float *inputs, const LavishNNConfig *nn_config,
+                            int reduce_prec, float *outputs, int n, void *stream);
+
 /* ------------------------------------------------------------------------ */
 /* Per-call RTCD shims (host pointers)                                      */
 /* ------------------------------------------------------------------------ */
@@ -683,6 +720,10 @@ int64_t av1_highbd_block_error_hip(const int32_t *coeff,
 /* av1_get_horver_correlation_full (av1/common/av1_rtcd_defs.pl:469) */
 void av1_get_horver_correlation_full_hip(const int16_t *diff, int stride, int w,
                                          int h, float *hcorr, float *vcorr);
+
+/* av1_nn_predict (av1/common/av1_rtcd_defs.pl:472) */
+void av1_nn_predict_hip(const float *input_nodes, const LavishNNConfig *nn_config,
+                        int reduce_prec, float *output);
 
 /* Convolution (av1/common/av1_rtcd_defs.pl:565-575, aom_dsp_rtcd_defs.pl:449,461).
  * Layout mirrors of InterpFilterParams (av1/common/filter.h:105-109) and

@@ -282,6 +282,22 @@ long orc_build_inter_pred_batch(const void *ref, int ref_stride, int ref_width, 
                                 long njobs, const OrcSubpelResult *mvs, void *dst,
                                 int dst_stride, int bd, int hbd);
 
+/* ---- TX-type pruning (8(f) rank 4): oracle_txfeat.c ---- */
+typedef struct OrcNNConfig { /* layout of NN_CONFIG (av1/encoder/ml.h:24-34) */
+  int num_inputs, num_outputs, num_hidden_layers;
+  int num_hidden_nodes[10];
+  const float *weights[11];
+  const float *bias[11];
+} OrcNNConfig;
+void orc_nn_predict(const float *input_nodes, const OrcNNConfig *c, int reduce_prec,
+                    float *output);
+void orc_sort_fi32(float *k, int *v, int n);
+int orc_prune_aggressiveness(int tx_set_type, int prune_mode);
+long orc_prune_tx_2d(const int16_t *residual, int stride, int width, int height, int bw, int bh,
+                     int tx_set_type, int prune_mode, const float *thresholds,
+                     const OrcNNConfig *hor, const OrcNNConfig *ver, const uint16_t *allowed_in,
+                     uint16_t allowed_default, uint16_t *allowed_out, uint8_t *txk_map);
+
 #ifdef __cplusplus
 }
 #endif

@@ -514,3 +514,75 @@ def build_inter_pred(ref, ref_origin, ref_width, ref_height, ss_x, ss_y, w, h, j
                                  ss_y, w, h, P(jobs), len(jobs),
                                  None if m is None else P(m), P(out), ds, bd, int(hb))
     return out
+
+
+# ------------------------------------------------------ TX-type pruning --
+class OrcNNConfig(ctypes.Structure):
+    _fields_ = [("num_inputs", ctypes.c_int), ("num_outputs", ctypes.c_int),
+                ("num_hidden_layers", ctypes.c_int), ("num_hidden_nodes", ctypes.c_int * 10),
+                ("weights", ctypes.c_void_p * 11), ("bias", ctypes.c_void_p * 11)]
+
+
+def nn_config(cfg):
+    """An OrcNNConfig over a json model dict {num_inputs, num_outputs, hidden,
+    weights, bias} (arrays kept alive on the returned object)."""
+    c = OrcNNConfig()
+    c.num_inputs, c.num_outputs = cfg["num_inputs"], cfg["num_outputs"]
+    c.num_hidden_layers = len(cfg["hidden"])
+    for i, h in enumerate(cfg["hidden"]):
+        c.num_hidden_nodes[i] = h
+    keep = []
+    for i, (w, b) in enumerate(zip(cfg["weights"], cfg["bias"])):
+        wa, ba = np.asarray(w, np.float32), np.asarray(b, np.float32)
+        keep += [wa, ba]
+        c.weights[i] = wa.ctypes.data
+        c.bias[i] = ba.ctypes.data
+    c._keep = keep
+    return c
+
+
+def nn_predict(inp, cfg, reduce_prec=True):
+    L = lib()
+    L.orc_nn_predict.argtypes = [ctypes.c_void_p, ctypes.POINTER(OrcNNConfig), ctypes.c_int,
+                                 ctypes.c_void_p]
+    c = cfg if isinstance(cfg, OrcNNConfig) else nn_config(cfg)
+    x = np.ascontiguousarray(inp, np.float32)
+    out = np.zeros(c.num_outputs, np.float32)
+    L.orc_nn_predict(P(x), ctypes.byref(c), int(reduce_prec), P(out))
+    return out
+
+
+def sort_fi32(k, v, n):
+    L = lib()
+    L.orc_sort_fi32.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
+    k = np.ascontiguousarray(k, np.float32).copy()
+    v = np.ascontiguousarray(v, np.int32).copy()
+    L.orc_sort_fi32(P(k), P(v), n)
+    return k, v
+
+
+def prune_tx_2d(res, bw, bh, tx_set_type, prune_mode, thresholds, hor, ver, allowed_in=None,
+                allowed_default=0xFFFF):
+    """orc_prune_tx_2d over an int16 residual plane: (allowed_out[nblk],
+    txk_map[nblk, 16])."""
+    L = lib()
+    L.orc_prune_tx_2d.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                  ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                  ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                  ctypes.c_void_p, ctypes.c_uint16, ctypes.c_void_p,
+                                  ctypes.c_void_p]
+    L.orc_prune_tx_2d.restype = ctypes.c_long
+    H, W = res.shape
+    n = (W // bw) * (H // bh)
+    out = np.zeros(n, np.uint16)
+    maps = np.zeros((n, 16), np.uint8)
+    th = None if thresholds is None else np.ascontiguousarray(thresholds, np.float32)
+    hc = None if hor is None else (hor if isinstance(hor, OrcNNConfig) else nn_config(hor))
+    vc = None if ver is None else (ver if isinstance(ver, OrcNNConfig) else nn_config(ver))
+    ai = None if allowed_in is None else np.ascontiguousarray(allowed_in, np.uint16)
+    L.orc_prune_tx_2d(P(res), res.strides[0] // 2, W, H, bw, bh, tx_set_type, prune_mode,
+                      None if th is None else P(th),
+                      None if hc is None else ctypes.addressof(hc),
+                      None if vc is None else ctypes.addressof(vc),
+                      None if ai is None else P(ai), allowed_default, P(out), P(maps))
+    return out, maps
