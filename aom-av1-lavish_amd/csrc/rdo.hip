@@ -53,6 +53,10 @@ struct RdoArgs {
   // group); newcol[i] = 1 where order[i] starts a group
   int order[16];
   int newcol[16];
+  // decision modes, optional: per-block allowed_tx_mask and search order
+  // (txk_map, [block][16]) as prune_tx_2D leaves them
+  const uint16_t* block_mask;
+  const uint8_t* block_map;
   const int16_t* iscan_dct;       // DCT_DCT inverse scan (rate_estimator)
   int32_t* qcoeff;
   int32_t* dqcoeff;
@@ -109,6 +113,40 @@ __device__ __forceinline__ void rdo_types(const RdoArgs& a, const int32_t (&res)
     best_rd[k] = INT64_MAX;
     best_dist[k] = best_sse[k] = 0;
     best_type[k] = best_eob[k] = best_rate[k] = best_satd[k] = 0;
+  }
+  // per block (LDS, read at each decision): the allowed types that also
+  // appear in the block's search order, and each type's position in that
+  // order; identity without per-block data.  A zero mask means DCT_DCT only
+  // (get_tx_mask's rule, tx_search.c:1885-1888).
+  __shared__ uint8_t s_rank[T::P][16];
+  __shared__ uint16_t s_ok[T::P];
+  if constexpr (DEC) {
+    if (lane < T::P) {
+      uint32_t ok = 0xFFFFu;
+      if (lane < nvalid) {
+        const int blk = blk0 + lane;
+        if (a.block_mask) {
+          const uint32_t m = a.block_mask[blk];
+          ok = m ? m : 1u;
+        }
+        if (a.block_map) {
+          uint32_t present = 0;
+          for (int i = 0; i < 16; ++i) s_rank[lane][i] = 16;
+          for (int i = 0; i < 16; ++i) {
+            const int t = a.block_map[(size_t)blk * 16 + i];
+            if (t < 16 && !((present >> t) & 1)) {
+              present |= 1u << t;
+              s_rank[lane][t] = (uint8_t)i;
+            }
+          }
+          ok &= present;
+        } else {
+          for (int i = 0; i < 16; ++i) s_rank[lane][i] = (uint8_t)i;
+        }
+      }
+      s_ok[lane] = (uint16_t)ok;
+    }
+    wave_sync();
   }
 
   for (int oi = 0; oi < a.ntypes; ++oi) {
@@ -311,10 +349,13 @@ __device__ __forceinline__ void rdo_types(const RdoArgs& a, const int32_t (&res)
           dsse = bsse;
         }
         const int64_t rd = (((int64_t)st_rate[k] * a.rdmult + 256) >> 9) + dist * 128;
-        // the reference keeps the first type (ascending) of strictly
-        // smallest cost; types are visited grouped by vertical kind, so
-        // equal costs resolve to the lower type index
-        if (rd < best_rd[k] || (rd == best_rd[k] && t < best_type[k])) {
+        // the reference keeps the first type of strictly smallest cost in
+        // its search order (txk_map; ascending without one); types are
+        // visited here grouped by vertical kind, so equal costs resolve by
+        // that order's rank
+        if (((s_ok[bb] >> t) & 1) &&
+            (rd < best_rd[k] ||
+             (rd == best_rd[k] && s_rank[bb][t] < s_rank[bb][best_type[k]]))) {
           best_rd[k] = rd;
           best_dist[k] = dist;
           best_sse[k] = dsse;
@@ -601,7 +642,8 @@ int rdo_plane_px64(RdoArgs& a, int tx_size, int width, int height, hipStream_t s
 
 int rdo_plane(const uint16_t* src, const uint16_t* pred, int stride, int width, int height,
               int tx_size, uint32_t type_mask, int bd, const LavishQuantParams* qp, int rdmult,
-              LavishRdoBlock* out, int32_t* qcoeff, int32_t* dqcoeff, hipStream_t s, int px) {
+              LavishRdoBlock* out, int32_t* qcoeff, int32_t* dqcoeff, hipStream_t s, int px,
+              const uint16_t* block_mask, const uint8_t* block_map) {
   if (tx_size < 0 || tx_size >= 19) return -1;
   if (qp == nullptr || out == nullptr || qcoeff == nullptr || dqcoeff == nullptr) return -3;
   if (bd != 8 && bd != 10 && bd != 12) return -3;
@@ -622,8 +664,13 @@ int rdo_plane(const uint16_t* src, const uint16_t* pred, int stride, int width, 
   a.out = out;
   a.qcoeff = qcoeff;
   a.dqcoeff = dqcoeff;
+  a.block_mask = block_mask;
+  a.block_map = block_map;
   if (px) {
-    if (W > 32 || H > 32) return rdo_plane_px64(a, tx_size, width, height, s);
+    if (W > 32 || H > 32) {
+      if (block_mask || block_map) return -6;  // single-type path
+      return rdo_plane_px64(a, tx_size, width, height, s);
+    }
     return launch_size<2>(tx_size, a, s);
   }
   return launch_size<1>(tx_size, a, s);
@@ -962,4 +1009,15 @@ extern "C" int lavish_rdo_reconstruct(uint32_t size_mask, const LavishRdoBlock* 
                                       int bit_depth, uint8_t* sb_tx_size, void* stream) {
   return lavish::rdo_reconstruct(size_mask, records, dqcoeff, width, height, pred, recon, stride,
                                  bit_depth, sb_tx_size, (hipStream_t)stream);
+}
+
+extern "C" int lavish_rdo_plane_masked(const uint16_t* src, const uint16_t* pred, int stride,
+                                       int width, int height, int tx_size, uint32_t type_mask,
+                                       int bit_depth, const LavishQuantParams* qp, int rdmult,
+                                       const uint16_t* block_mask, const uint8_t* block_map,
+                                       int pixel_domain, LavishRdoBlock* out, int32_t* qcoeff,
+                                       int32_t* dqcoeff, void* stream) {
+  return lavish::rdo_plane(src, pred, stride, width, height, tx_size, type_mask, bit_depth, qp,
+                           rdmult, out, qcoeff, dqcoeff, (hipStream_t)stream, pixel_domain ? 1 : 0,
+                           block_mask, block_map);
 }

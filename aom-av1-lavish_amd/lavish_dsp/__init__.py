@@ -408,6 +408,34 @@ def rdo_plane(src, pred, tx_size, type_mask, qp, rdmult, bit_depth=10, out=None,
     return out
 
 
+_lib.lavish_rdo_plane_masked.argtypes = [_vp, _vp, _i32, _i32, _i32, _i32, ctypes.c_uint32, _i32,
+                                         ctypes.POINTER(QuantParams), _i32, _vp, _vp, _i32, _vp,
+                                         _vp, _vp, _vp]
+_lib.lavish_rdo_plane_masked.restype = _i32
+
+
+def rdo_plane_masked(src, pred, tx_size, type_mask, qp, rdmult, block_mask=None,
+                     block_map=None, bit_depth=10, px=False, out=None, stream=None):
+    """lavish_rdo_plane_masked: C4 with the per-block allowed_tx_mask (device
+    int16 / uint16 tensor [block]) and search order (device uint8 [block, 16])
+    that lavish_prune_tx_2d_batch produces."""
+    import torch
+    assert src.dtype == torch.int16 and pred.dtype == torch.int16
+    H, W = src.shape
+    if out is None:
+        out = rdo_out(src, tx_size)
+    rc = _lib.lavish_rdo_plane_masked(
+        ctypes.c_void_p(src.data_ptr()), ctypes.c_void_p(pred.data_ptr()), src.stride(0), W, H,
+        tx_size, type_mask, bit_depth, ctypes.byref(qp), rdmult,
+        None if block_mask is None else ctypes.c_void_p(block_mask.data_ptr()),
+        None if block_map is None else ctypes.c_void_p(block_map.data_ptr()), int(px),
+        ctypes.c_void_p(out["records"].data_ptr()), ctypes.c_void_p(out["qcoeff"].data_ptr()),
+        ctypes.c_void_p(out["dqcoeff"].data_ptr()), _stream_ptr(stream))
+    if rc != 0:
+        raise ValueError("lavish_rdo_plane_masked rejected its arguments (rc=%d)" % rc)
+    return out
+
+
 def rdo_records(out):
     return out["records"].cpu().numpy().view(RDO_DTYPE)
 

@@ -249,6 +249,19 @@ int lavish_rdo_plane(const uint16_t *src, const uint16_t *pred, int stride,
                      int bit_depth, const LavishQuantParams *qp, int rdmult,
                      LavishRdoBlock *out, int32_t *qcoeff, int32_t *dqcoeff,
                      void *stream);
+/* The same with the per-block allowed_tx_mask / search order that
+ * lavish_prune_tx_2d_batch produces (device arrays, either may be NULL):
+ * block b only considers types set in block_mask[b] (0 = DCT_DCT only,
+ * get_tx_mask's rule) that appear in block_map[b][0..15], and equal costs go
+ * to the type earlier in block_map[b] (search_tx_type's txk_map loop,
+ * tx_search.c:2148-2246).  type_mask is the evaluated superset.
+ * pixel_domain: 0 TX-domain distortion, 1 pixel-domain (sizes <= 32). */
+int lavish_rdo_plane_masked(const uint16_t *src, const uint16_t *pred, int stride,
+                            int width, int height, int tx_size, uint32_t type_mask,
+                            int bit_depth, const LavishQuantParams *qp, int rdmult,
+                            const uint16_t *block_mask, const uint8_t *block_map,
+                            int pixel_domain, LavishRdoBlock *out, int32_t *qcoeff,
+                            int32_t *dqcoeff, void *stream);
 
 /* Frame level: lavish_rdo_plane for every size set in size_mask (bit =
  * TX_SIZE) with type_masks[tx_size] and per-size outputs (arrays of 19

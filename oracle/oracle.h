@@ -248,6 +248,12 @@ long orc_rdo_plane_px(const uint16_t *src, const uint16_t *pred, int stride,
                       int width, int height, int tx_size, unsigned type_mask,
                       int bd, const OrcQuant *q, int rdmult, OrcRdoBlock *out,
                       int32_t *qcoeff, int32_t *dqcoeff, int threads);
+/* the same with search_tx_type's per-block allowed_tx_mask / txk_map */
+long orc_rdo_plane_masked(const uint16_t *src, const uint16_t *pred, int stride, int width,
+                          int height, int tx_size, unsigned type_mask, int bd, const OrcQuant *q,
+                          int rdmult, const uint16_t *block_mask, const uint8_t *block_map,
+                          int px, OrcRdoBlock *out, int32_t *qcoeff, int32_t *dqcoeff,
+                          int threads);
 void orc_rdo_reconstruct(int nsizes, const int *sizes,
                          const OrcRdoBlock *const *recs,
                          const int32_t *const *dqs, int width, int height,

@@ -52,6 +52,8 @@ typedef struct {
   const uint16_t *src, *pred;
   int stride, width, tx_size, bd, rdmult, row0, row1, ntypes, px;
   int types[16];
+  const uint16_t *block_mask; /* optional allowed_tx_mask per block */
+  const uint8_t *block_map;   /* optional txk_map per block ([16]) */
   const OrcQuant *q;
   OrcRdoBlock *out;
   int32_t *qcoeff, *dqcoeff;
@@ -84,8 +86,24 @@ static void *rdo_rows(void *arg) {
       OrcRdoBlock best;
       memset(&best, 0, sizeof(best));
       best.rdcost = INT64_MAX;
-      for (int ti = 0; ti < j->ntypes; ++ti) {
-        const int t = j->types[ti];
+      /* search_tx_type's loop (tx_search.c:2148-2157): txk_map order,
+       * skipping TX_TYPE_INVALID and types outside allowed_tx_mask
+       * (get_tx_mask: a zero mask becomes DCT_DCT, tx_search.c:1885-1888);
+       * only types of the call's type set are evaluated */
+      unsigned inset = 0;
+      for (int ti = 0; ti < j->ntypes; ++ti) inset |= 1u << j->types[ti];
+      unsigned allowed = j->block_mask ? j->block_mask[blk] : 0xFFFFu;
+      if (!allowed) allowed = 1;
+      int seq[16], nseq = 0;
+      for (int idx = 0; idx < 16; ++idx) {
+        const int t = j->block_map ? j->block_map[blk * 16 + idx] : idx;
+        if (t >= 16 || !((allowed >> t) & 1) || !((inset >> t) & 1)) continue;
+        int dup = 0;
+        for (int u = 0; u < nseq; ++u) dup |= seq[u] == t;
+        if (!dup) seq[nseq++] = t;
+      }
+      for (int ti = 0; ti < nseq; ++ti) {
+        const int t = seq[ti];
         orc_fwd_txfm2d(diff, coeff, W, t, j->tx_size, j->bd);
         uint16_t eob;
         orc_highbd_quantize_fp(coeff, n, j->q->zbin, j->q->round_fp, j->q->quant_fp,
@@ -147,7 +165,8 @@ static void *rdo_rows(void *arg) {
 static long rdo_plane(const uint16_t *src, const uint16_t *pred, int stride, int width,
                       int height, int tx_size, unsigned type_mask, int bd, const OrcQuant *q,
                       int rdmult, OrcRdoBlock *out, int32_t *qcoeff, int32_t *dqcoeff,
-                      int threads, int px) {
+                      int threads, int px, const uint16_t *block_mask,
+                      const uint8_t *block_map) {
   const int W = orc_tx_w(tx_size), H = orc_tx_h(tx_size);
   const int bh = height / H;
   RdoJob base;
@@ -164,6 +183,8 @@ static long rdo_plane(const uint16_t *src, const uint16_t *pred, int stride, int
   base.qcoeff = qcoeff;
   base.dqcoeff = dqcoeff;
   base.px = px;
+  base.block_mask = block_mask;
+  base.block_map = block_map;
   for (int t = 0; t < 16; ++t)
     if ((type_mask >> t) & 1) base.types[base.ntypes++] = t;
   if (threads < 1) threads = 1;
@@ -188,7 +209,7 @@ long orc_rdo_plane(const uint16_t *src, const uint16_t *pred, int stride, int wi
                    int rdmult, OrcRdoBlock *out, int32_t *qcoeff, int32_t *dqcoeff,
                    int threads) {
   return rdo_plane(src, pred, stride, width, height, tx_size, type_mask, bd, q, rdmult, out,
-                   qcoeff, dqcoeff, threads, 0);
+                   qcoeff, dqcoeff, threads, 0, NULL, NULL);
 }
 
 long orc_rdo_plane_px(const uint16_t *src, const uint16_t *pred, int stride, int width,
@@ -196,7 +217,16 @@ long orc_rdo_plane_px(const uint16_t *src, const uint16_t *pred, int stride, int
                       int rdmult, OrcRdoBlock *out, int32_t *qcoeff, int32_t *dqcoeff,
                       int threads) {
   return rdo_plane(src, pred, stride, width, height, tx_size, type_mask, bd, q, rdmult, out,
-                   qcoeff, dqcoeff, threads, 1);
+                   qcoeff, dqcoeff, threads, 1, NULL, NULL);
+}
+
+long orc_rdo_plane_masked(const uint16_t *src, const uint16_t *pred, int stride, int width,
+                          int height, int tx_size, unsigned type_mask, int bd, const OrcQuant *q,
+                          int rdmult, const uint16_t *block_mask, const uint8_t *block_map,
+                          int px, OrcRdoBlock *out, int32_t *qcoeff, int32_t *dqcoeff,
+                          int threads) {
+  return rdo_plane(src, pred, stride, width, height, tx_size, type_mask, bd, q, rdmult, out,
+                   qcoeff, dqcoeff, threads, px, block_mask, block_map);
 }
 
 /* Per 64x64 SB: the size (of `sizes`, largest area first) whose full blocks

@@ -424,6 +424,32 @@ def rdo_plane(src, pred, tx_size, type_mask, bd, q, rdmult, threads=1, px=False)
     return out, qc, dq
 
 
+def rdo_plane_masked(src, pred, tx_size, type_mask, bd, q, rdmult, block_mask=None,
+                     block_map=None, px=False, threads=1):
+    """orc_rdo_plane_masked: search_tx_type's txk_map / allowed_tx_mask loop."""
+    L = lib()
+    fn = L.orc_rdo_plane_masked
+    fn.restype = ctypes.c_long
+    fn.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                   ctypes.c_int, ctypes.c_uint, ctypes.c_int, ctypes.POINTER(OrcQuant),
+                   ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int,
+                   ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
+    src = np.ascontiguousarray(src, dtype=np.uint16)
+    pred = np.ascontiguousarray(pred, dtype=np.uint16)
+    H, W = src.shape
+    nb = (W // TX_W[tx_size]) * (H // TX_H[tx_size])
+    n = max_eob(tx_size)
+    out = np.zeros(nb, RDO_DTYPE)
+    qc = np.zeros((nb, n), np.int32)
+    dq = np.zeros((nb, n), np.int32)
+    bm = None if block_mask is None else np.ascontiguousarray(block_mask, np.uint16)
+    mp = None if block_map is None else np.ascontiguousarray(block_map, np.uint8)
+    fn(P(src), P(pred), W, W, H, tx_size, type_mask, bd, ctypes.byref(q), rdmult,
+       None if bm is None else P(bm), None if mp is None else P(mp), int(px), P(out), P(qc),
+       P(dq), threads)
+    return out, qc, dq
+
+
 # ---------------------------------------------------- TX-pruning features --
 def horver_full(diff, stride, w, h):
     """orc_horver_correlation_full on a host int16 buffer: (hcorr, vcorr)."""
