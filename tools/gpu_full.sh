@@ -14,7 +14,9 @@ tail -1 gpurun_out/smoke.log
 step bench timeout -k 10 300 python -u bench.py --steps 20 --warmup 3 --cpu-seconds 8 > gpurun_out/bench.log 2>&1
 grep -v amdgpu.ids gpurun_out/bench.log | tail -1 | cut -c1-400
 step bench_c4 timeout -k 10 300 python -u bench.py --workload c4 --steps 20 --warmup 3 --cpu-seconds 8 > gpurun_out/bench_c4.log 2>&1
+step bench_inter timeout -k 10 300 python -u bench.py --workload inter --steps 50 --warmup 5 --cpu-seconds 8 > gpurun_out/bench_inter.log 2>&1
 cd /tmp && export TMPDIR=/tmp
+step rocprof_inter timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/gpurun_out/prof_inter" -o kt -- python3 "$R/bench.py" --workload inter --steps 50 --warmup 5 --no-cpu > "$R/gpurun_out/prof_inter.log" 2>&1
 step rocprof timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/gpurun_out/prof" -o kt -- python3 "$R/bench.py" --steps 10 --warmup 2 --no-cpu > "$R/gpurun_out/prof.log" 2>&1
 step rocprof_c4 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/gpurun_out/prof_c4" -o kt -- python3 "$R/bench.py" --workload c4 --steps 10 --warmup 2 --no-cpu > "$R/gpurun_out/prof_c4.log" 2>&1
 for c in FETCH_SIZE WRITE_SIZE; do
