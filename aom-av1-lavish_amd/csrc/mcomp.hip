@@ -494,7 +494,7 @@ __device__ int fast_bigdia(const Ctx& c, int lane, int srow, int scol, int step_
 
 
 template <int W, int H>
-__global__ __launch_bounds__(256) void diamond_kernel(const uint8_t* __restrict__ src, int ss,
+__global__ __launch_bounds__(256, 7) void diamond_kernel(const uint8_t* __restrict__ src, int ss,
                                                       const uint8_t* __restrict__ ref, int rs,
                                                       const Job* __restrict__ jobs, int njobs,
                                                       int step_param, int cost_type, int skip,
