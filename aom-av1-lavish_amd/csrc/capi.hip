@@ -169,6 +169,49 @@ void* shim_scratch(size_t bytes) {
   return t_scratch.ptr;
 }
 
+void shim_reject(const char* what, int rc) {
+  {
+    std::lock_guard<std::mutex> lk(g_mu);
+    if (g_status == 0) {
+      g_status = rc < 0 ? rc : -rc;
+      snprintf(g_status_str, sizeof(g_status_str), "%s rejected its arguments (rc %d)", what, rc);
+    }
+  }
+  fprintf(stderr, "[lavish_hip] %s rejected its arguments (rc %d)\n", what, rc);
+  if (g_abort_on_error) abort();
+}
+
+void* StreamScratch::acquire(size_t bytes, hipStream_t s) {
+  int dev = 0;
+  LAVISH_CHECK(hipGetDevice(&dev));
+  if (device != dev) {  // one device per process; a switch starts afresh
+    ptr = nullptr;
+    cap = 0;
+    pending = false;
+    LAVISH_CHECK(hipEventCreateWithFlags(&done, hipEventDisableTiming));
+    device = dev;
+  }
+  if (bytes > cap) {
+    if (ptr) {
+      if (pending) LAVISH_CHECK(hipEventSynchronize(done));
+      LAVISH_CHECK(hipFree(ptr));
+    }
+    size_t c = (size_t)1 << 16;
+    while (c < bytes) c <<= 1;
+    LAVISH_CHECK(hipMalloc(&ptr, c));
+    cap = c;
+    pending = false;
+  } else if (pending) {
+    LAVISH_CHECK(hipStreamWaitEvent(s, done, 0));
+  }
+  return ptr;
+}
+
+void StreamScratch::release(hipStream_t s) {
+  LAVISH_CHECK(hipEventRecord(done, s));
+  pending = true;
+}
+
 // ------------------------------------------------------------ quantizer --
 static int16_t dc_q(int q, int delta, int bd) {
   int i = q + delta;

@@ -66,6 +66,25 @@ void fan_in(hipStream_t caller);
 void* shim_scratch(size_t bytes);
 hipStream_t shim_stream();
 
+// Argument rejection inside a per-call shim (which has no error channel):
+// recorded in the sticky status like a HIP failure, then abort unless
+// lavish_hip_set_abort_on_error(0).
+void shim_reject(const char* what, int rc);
+
+// Device scratch reused by calls that may be queued on different streams.
+// acquire() makes `s` wait for the event the previous user's release()
+// recorded, so the buffer is never rewritten while an earlier kernel (on any
+// stream) may still read it; growing it waits for that event on the host.
+struct StreamScratch {
+  int device = -1;
+  void* ptr = nullptr;
+  size_t cap = 0;
+  hipEvent_t done = nullptr;
+  bool pending = false;
+  void* acquire(size_t bytes, hipStream_t s);
+  void release(hipStream_t s);
+};
+
 // Wave-local memory ordering: lanes of one wave exchange data through LDS
 // with no workgroup barrier (each wave owns its tile); these fences only stop
 // the compiler from moving LDS accesses across the exchange point (LDS ops of

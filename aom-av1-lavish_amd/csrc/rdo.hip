@@ -395,14 +395,19 @@ __device__ __forceinline__ void rdo_types(const RdoArgs& a, const int32_t (&res)
   }
 
   if constexpr (DEC) {
-    // decision records (one lane per block) and the winner's coefficients
+    // decision records (one lane per block) and the winner's coefficients.
+    // A block none of whose allowed types is in the evaluated set (possible
+    // only with caller masks) has no candidate: record best_type
+    // TX_TYPE_INVALID (255), eob 0, rdcost INT64_MAX, zero coefficients.
+    __shared__ uint8_t s_dead[T::P];
 #pragma unroll
     for (int k = 0; k < T::RPT; ++k) {
       const int j = k * 64 + lane;
       const int b = j / KH, r = j % KH;
       if (b < T::P && b < nvalid && r == 0) {
+        const bool dead = best_rd[k] == INT64_MAX;
         LavishRdoBlock o;
-        o.best_type = best_type[k];
+        o.best_type = dead ? 255 : best_type[k];
         o.eob = best_eob[k];
         o.rate = best_rate[k];
         o.satd = best_satd[k];
@@ -410,12 +415,15 @@ __device__ __forceinline__ void rdo_types(const RdoArgs& a, const int32_t (&res)
         o.sse = best_sse[k];
         o.rdcost = best_rd[k];
         a.out[blk0 + b] = o;
+        s_dead[b] = dead;
       }
     }
+    wave_sync();
     const int total = nvalid * NC;
     const size_t gbase = (size_t)blk0 * NC;
     for (int i = lane * 4; i < total; i += 64 * 4) {
-      const v4i q4 = *reinterpret_cast<const v4i*>(&tb[i]);
+      v4i q4 = *reinterpret_cast<const v4i*>(&tb[i]);
+      if (s_dead[i / NC]) q4 = v4i{0, 0, 0, 0};
       __builtin_nontemporal_store(q4, reinterpret_cast<v4i*>(&a.qcoeff[gbase + i]));
       const int rc0 = i % NC;
       v4i d4;
@@ -722,6 +730,10 @@ __device__ __forceinline__ int max_eob_dev(int s) {
   return w * h;
 }
 
+__device__ __forceinline__ int64_t sat_add(int64_t a, int64_t b) {
+  return a > INT64_MAX - b ? INT64_MAX : a + b;
+}
+
 struct SbArgs {
   int nsizes;
   int sizes[19];                       // candidate order: largest area first
@@ -749,13 +761,15 @@ __global__ __launch_bounds__(256) void sb_decide_kernel(SbArgs a) {
     const int W = tx_w_dev(s), H = tx_h_dev(s);
     if (y1 % H || x1 % W) continue;
     const int bw = a.width / W, nx = x1 / W, nblk = nx * (y1 / H);
+    // costs are >= 0; a block without a candidate costs INT64_MAX, so the
+    // sums saturate there instead of wrapping
     int64_t sum = 0;
     for (int k = lane; k < nblk; k += 64) {
       const int y = k / nx, x = k - y * nx;
-      sum += a.rec[s][(sy * 64 / H + y) * bw + sx * 64 / W + x].rdcost;
+      sum = sat_add(sum, a.rec[s][(sy * 64 / H + y) * bw + sx * 64 / W + x].rdcost);
     }
 #pragma unroll
-    for (int m = 1; m < 64; m <<= 1) sum += __shfl_xor(sum, m);
+    for (int m = 1; m < 64; m <<= 1) sum = sat_add(sum, __shfl_xor(sum, m));
     if (sum < best) {
       best = sum;
       best_s = s;
@@ -781,25 +795,10 @@ __global__ void inv_jobs_kernel(int s, const LavishRdoBlock* rec, int nblocks, i
   jobs[blk] = j;
 }
 
-struct ReconScratch {
-  int device = -1;
-  LavishInvJob* jobs = nullptr;
-  size_t cap = 0;
-};
-thread_local ReconScratch t_rs;
-
-LavishInvJob* job_scratch(size_t n) {
-  int dev = 0;
-  LAVISH_CHECK(hipGetDevice(&dev));
-  if (t_rs.device != dev || n > t_rs.cap) {
-    // previous users of the buffer are ordered before us on the same stream
-    if (t_rs.jobs && t_rs.device == dev) LAVISH_CHECK(hipFree(t_rs.jobs));
-    t_rs.cap = n < 4096 ? 4096 : n;
-    LAVISH_CHECK(hipMalloc(&t_rs.jobs, t_rs.cap * sizeof(LavishInvJob)));
-    t_rs.device = dev;
-  }
-  return t_rs.jobs;
-}
+// inverse-transform job list of lavish_rdo_reconstruct: reused call after
+// call, possibly from different streams (e.g. per-band streams of a shard),
+// so reuse is ordered by StreamScratch's event
+thread_local StreamScratch t_rs;
 
 }  // namespace
 
@@ -874,14 +873,10 @@ __global__ __launch_bounds__(256) void px64_finish_kernel(const uint16_t* src, c
   rec[blk] = o;
 }
 
-struct Px64Scratch {
-  int device = -1;
-  uint16_t* plane = nullptr;
-  size_t cap = 0;
-  LavishInvJob* jobs = nullptr;
-  size_t jcap = 0;
-};
-thread_local Px64Scratch t_px;
+// per TX size: rdo_frame_px deals the 64-point sizes over concurrent fan-out
+// streams, so each size owns its scratch plane / job list, and reuse across
+// calls (any stream) waits for the previous user's event
+thread_local StreamScratch t_px_plane[19], t_px_jobs[19];
 
 }  // namespace
 
@@ -890,32 +885,23 @@ int rdo_plane_px64(RdoArgs& a, int tx_size, int width, int height, hipStream_t s
   int rc = launch_size<1>(tx_size, a, s);
   if (rc || a.nblocks == 0) return rc;
   const int W = tx_w(tx_size), H = tx_h(tx_size);
-  int dev = 0;
-  LAVISH_CHECK(hipGetDevice(&dev));
-  const size_t need = (size_t)a.stride * height;
-  if (t_px.device != dev || need > t_px.cap || (size_t)a.nblocks > t_px.jcap) {
-    // earlier users of the buffers are ordered before us on this thread's streams
-    LAVISH_CHECK(hipDeviceSynchronize());
-    if (t_px.plane && t_px.device == dev) LAVISH_CHECK(hipFree(t_px.plane));
-    if (t_px.jobs && t_px.device == dev) LAVISH_CHECK(hipFree(t_px.jobs));
-    t_px.cap = need > t_px.cap ? need : t_px.cap;
-    t_px.jcap = (size_t)a.nblocks > t_px.jcap ? (size_t)a.nblocks : t_px.jcap;
-    LAVISH_CHECK(hipMalloc(&t_px.plane, t_px.cap * sizeof(uint16_t)));
-    LAVISH_CHECK(hipMalloc(&t_px.jobs, t_px.jcap * sizeof(LavishInvJob)));
-    t_px.device = dev;
-  }
-  LAVISH_CHECK(hipMemcpy2DAsync(t_px.plane, (size_t)a.stride * 2, a.pred, (size_t)a.stride * 2,
+  uint16_t* plane = (uint16_t*)t_px_plane[tx_size].acquire(
+      (size_t)a.stride * height * sizeof(uint16_t), s);
+  LavishInvJob* jobs =
+      (LavishInvJob*)t_px_jobs[tx_size].acquire((size_t)a.nblocks * sizeof(LavishInvJob), s);
+  LAVISH_CHECK(hipMemcpy2DAsync(plane, (size_t)a.stride * 2, a.pred, (size_t)a.stride * 2,
                                 (size_t)width * 2, height, hipMemcpyDeviceToDevice, s));
   hipLaunchKernelGGL(px64_jobs_kernel, dim3((a.nblocks + 255) / 256), dim3(256), 0, s, a.out,
-                     a.nblocks, a.bw, W, H, max_eob(tx_size), a.stride, t_px.jobs);
+                     a.nblocks, a.bw, W, H, max_eob(tx_size), a.stride, jobs);
   LAVISH_CHECK(hipGetLastError());
-  rc = inv_txfm_add_batch(a.dqcoeff, tx_size, t_px.jobs, a.nblocks, t_px.plane, a.stride, a.bd,
-                          1, s);
+  rc = inv_txfm_add_batch(a.dqcoeff, tx_size, jobs, a.nblocks, plane, a.stride, a.bd, 1, s);
   if (rc) return rc;
   hipLaunchKernelGGL(px64_finish_kernel, dim3(a.nblocks), dim3(256), 0, s, a.src, a.pred,
-                     t_px.plane, a.stride, a.bw, W, H, tx_size == 4 ? 1 : 0, a.bd, a.rdmult,
+                     plane, a.stride, a.bw, W, H, tx_size == 4 ? 1 : 0, a.bd, a.rdmult,
                      a.out);
   LAVISH_CHECK(hipGetLastError());
+  t_px_plane[tx_size].release(s);
+  t_px_jobs[tx_size].release(s);
   return 0;
 }
 
@@ -950,7 +936,7 @@ int rdo_reconstruct(uint32_t size_mask, const LavishRdoBlock* const* rec,
     const int t = a.sizes[i];
     maxb = max(maxb, (size_t)(width / tx_w(t)) * (height / tx_h(t)));
   }
-  LavishInvJob* jobs = job_scratch(maxb);
+  LavishInvJob* jobs = (LavishInvJob*)t_rs.acquire(maxb * sizeof(LavishInvJob), s);
   for (int i = 0; i < a.nsizes; ++i) {
     const int t = a.sizes[i];
     const int bw = width / tx_w(t);
@@ -960,8 +946,12 @@ int rdo_reconstruct(uint32_t size_mask, const LavishRdoBlock* const* rec,
                        bw, stride, a.sbw, sb_tx_size, jobs);
     LAVISH_CHECK(hipGetLastError());
     const int rc = inv_txfm_add_batch(dqcoeff[t], t, jobs, nb, recon, stride, bd, 1, s);
-    if (rc) return rc;
+    if (rc) {
+      t_rs.release(s);
+      return rc;
+    }
   }
+  t_rs.release(s);
   return 0;
 }
 

@@ -421,7 +421,18 @@ def rdo_plane_masked(src, pred, tx_size, type_mask, qp, rdmult, block_mask=None,
     that lavish_prune_tx_2d_batch produces."""
     import torch
     assert src.dtype == torch.int16 and pred.dtype == torch.int16
+    assert src.is_cuda and pred.is_cuda and src.shape == pred.shape
+    assert src.stride(1) == 1 and pred.stride(0) == src.stride(0)
     H, W = src.shape
+    nb = (W // TX_W[tx_size]) * (H // TX_H[tx_size])
+    # the kernel reads block_mask[nb] (16-bit) and block_map[nb][16] (u8) on
+    # the device: anything else would read out of bounds or host memory
+    if block_mask is not None:
+        assert block_mask.is_cuda and block_mask.dtype in (torch.int16, torch.uint16)
+        assert block_mask.is_contiguous() and tuple(block_mask.shape) == (nb,)
+    if block_map is not None:
+        assert block_map.is_cuda and block_map.dtype == torch.uint8
+        assert block_map.is_contiguous() and tuple(block_map.shape) == (nb, 16)
     if out is None:
         out = rdo_out(src, tx_size)
     rc = _lib.lavish_rdo_plane_masked(
@@ -502,6 +513,22 @@ def rdo_frame(src, pred, frame, qp, rdmult, bit_depth=10, reconstruct=True, stre
         if rc != 0:
             raise ValueError("lavish_rdo_reconstruct rejected its arguments (rc=%d)" % rc)
     return frame
+
+
+def rdo_reconstruct(sizes, outs, pred, recon, sb_tx_size, bit_depth=10, stream=None):
+    """lavish_rdo_reconstruct over per-size rdo_plane outputs `outs[s]`: the
+    per-SB TX size into sb_tx_size and recon = pred + the chosen blocks'
+    inverse transforms."""
+    assert pred.stride(1) == 1 and recon.stride(0) == pred.stride(0)
+    H, W = pred.shape
+    rec = _P19(*[outs[s]["records"].data_ptr() if s in outs else 0 for s in range(19)])
+    dq = _P19(*[outs[s]["dqcoeff"].data_ptr() if s in outs else 0 for s in range(19)])
+    rc = _lib.lavish_rdo_reconstruct(sum(1 << s for s in sizes), rec, dq, W, H,
+                                     ctypes.c_void_p(pred.data_ptr()),
+                                     ctypes.c_void_p(recon.data_ptr()), pred.stride(0), bit_depth,
+                                     ctypes.c_void_p(sb_tx_size.data_ptr()), _stream_ptr(stream))
+    if rc != 0:
+        raise ValueError("lavish_rdo_reconstruct rejected its arguments (rc=%d)" % rc)
 
 
 # ----------------------------------------------------- TX-pruning features --

@@ -66,12 +66,13 @@ def sharded_frame(height, rank, world, process_band, group=None):
 def c4_band_processor(src, pred, qp, rdmult, bit_depth, frames):
     """process_band for the GPU path: lavish_rdo_frame + reconstruct on the
     rows [y0, y1) of device planes (views share the full planes' stride).
-    `frames` caches the RdoFrame output buffers per band shape."""
+    `frames` caches the RdoFrame output buffers per band (bands may run
+    concurrently on different streams, so no two share buffers)."""
     import lavish_dsp as L
 
     def run(y0, y1):
         s, p = src[y0:y1], pred[y0:y1]
-        key = (y1 - y0, s.shape[1])
+        key = (y0, y1, s.shape[1])
         if key not in frames:
             frames[key] = L.RdoFrame(s)
         fr = frames[key]

@@ -156,6 +156,14 @@ static void *rdo_rows(void *arg) {
           memcpy(j->dqcoeff + blk * n, dq, sizeof(int32_t) * n);
         }
       }
+      if (best.rdcost == INT64_MAX) {
+        /* no allowed type in the evaluated set (caller masks only): the
+         * build's defined "no candidate" result -- TX_TYPE_INVALID, eob 0,
+         * zero coefficients, rdcost INT64_MAX */
+        best.best_type = 255;
+        memset(j->qcoeff + blk * n, 0, sizeof(int32_t) * n);
+        memset(j->dqcoeff + blk * n, 0, sizeof(int32_t) * n);
+      }
       j->out[blk] = best;
     }
   }
@@ -247,10 +255,14 @@ void orc_rdo_reconstruct(int nsizes, const int *sizes, const OrcRdoBlock *const 
         const int y1 = height - sy * 64 < 64 ? height - sy * 64 : 64;
         const int x1 = width - sx * 64 < 64 ? width - sx * 64 : 64;
         if (y1 % H || x1 % W) continue;
+        /* costs are >= 0; sums saturate at INT64_MAX (a block without a
+         * candidate costs INT64_MAX) */
         int64_t sum = 0;
         for (int y = 0; y < y1; y += H)
-          for (int x = 0; x < x1; x += W)
-            sum += recs[i][((sy * 64 + y) / H) * (width / W) + (sx * 64 + x) / W].rdcost;
+          for (int x = 0; x < x1; x += W) {
+            const int64_t c = recs[i][((sy * 64 + y) / H) * (width / W) + (sx * 64 + x) / W].rdcost;
+            sum = sum > INT64_MAX - c ? INT64_MAX : sum + c;
+          }
         if (sum < best) {
           best = sum;
           best_s = s;

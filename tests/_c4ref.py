@@ -37,9 +37,10 @@ def oracle_frame(src, pred, bd, masks, rdmult, threads=8, px=False):
                 tot = 0
                 for y in range(0, y1, bh_):
                     for x in range(0, x1, bw_):
-                        tot += int(per[s][0]["rdcost"][((sy * 64 + y) // bh_) * nbx
-                                                       + (sx * 64 + x) // bw_])
-                if best is None or tot < best[0]:
+                        tot = min(tot + int(per[s][0]["rdcost"][((sy * 64 + y) // bh_) * nbx
+                                                                + (sx * 64 + x) // bw_]),
+                                  2 ** 63 - 1)  # saturating, as orc_rdo_reconstruct
+                if tot < (2 ** 63 - 1 if best is None else best[0]):
                     best = (tot, s)
             if best is not None:
                 choice[sy * sbw + sx] = best[1]

@@ -450,6 +450,30 @@ def rdo_plane_masked(src, pred, tx_size, type_mask, bd, q, rdmult, block_mask=No
     return out, qc, dq
 
 
+def rdo_reconstruct(sizes, recs, dqs, pred, bd):
+    """orc_rdo_reconstruct: per-SB TX size (lowest saturating sum of block
+    costs, ties to the larger size) and recon = pred + the chosen blocks'
+    inverse transforms.  recs / dqs are per entry of `sizes`.  Returns
+    (recon, sb_tx_size)."""
+    L = lib()
+    vp = ctypes.c_void_p
+    L.orc_rdo_reconstruct.argtypes = [ctypes.c_int, vp, vp, vp, ctypes.c_int, ctypes.c_int, vp,
+                                      vp, ctypes.c_int, ctypes.c_int, vp]
+    order = sorted(range(len(sizes)), key=lambda i: -TX_W[sizes[i]] * TX_H[sizes[i]])
+    sz = np.array([sizes[i] for i in order], np.int32)
+    recs = [np.ascontiguousarray(recs[i]) for i in order]
+    dqs = [np.ascontiguousarray(dqs[i], np.int32) for i in order]
+    rp = (vp * len(sz))(*[r.ctypes.data for r in recs])
+    dp = (vp * len(sz))(*[d.ctypes.data for d in dqs])
+    pred = np.ascontiguousarray(pred, dtype=np.uint16)
+    H, W = pred.shape
+    recon = np.empty_like(pred)
+    choice = np.zeros(((W + 63) // 64) * ((H + 63) // 64), np.uint8)
+    L.orc_rdo_reconstruct(len(sz), P(sz), ctypes.cast(rp, vp), ctypes.cast(dp, vp), W, H, P(pred),
+                          P(recon), W, bd, P(choice))
+    return recon, choice
+
+
 # ---------------------------------------------------- TX-pruning features --
 def horver_full(diff, stride, w, h):
     """orc_horver_correlation_full on a host int16 buffer: (hcorr, vcorr)."""

@@ -1,0 +1,121 @@
+"""GPU parity at the BASELINE.json configurations' full sizes (SURVEY.md
+8(d)), every job / block / superblock against the oracle:
+
+* C3: DIAMOND full-pel search of every 16x16 block of a 1920x1080 frame
+  against 7 references (56 280 jobs) with the 1080p speed features bench.py
+  times (downsampled SAD, the bench's mv cost);
+* C4: the 3840x2160 10-bit RDO step (all candidate sizes / types, per-SB TX
+  size, reconstruction) -- records, sb_tx_size and the reconstruction;
+* C5 at world 1: the SB-row band processor of lavish_dsp/shard.py over 3
+  bands on 3 streams equals the whole-frame step.
+"""
+import os
+
+import numpy as np
+import pytest
+
+import _oracle as O
+from _c4ref import oracle_frame_c
+
+pytestmark = pytest.mark.gpu
+
+THREADS = max(1, min(32, os.cpu_count() or 1))
+
+
+@pytest.fixture(scope="module")
+def L():
+    import torch
+    assert torch.cuda.is_available()
+    import lavish_dsp
+    return lavish_dsp
+
+
+def _bench():
+    import importlib.util
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    spec = importlib.util.spec_from_file_location("bench", os.path.join(root, "bench.py"))
+    b = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(b)
+    return b
+
+
+def test_c3_1080p_7refs_all_jobs(L):
+    import torch
+    import lavish_dsp.motion as M
+    import lavish_dsp.synth as synth
+    b = _bench()
+    W, H, R, border = 1920, 1080, 7, 160
+    src, refs = synth.motion_planes(W, H, R, border, seed=1234)
+    st = src.shape[1]
+    jobs = M.frame_jobs(W, H, st, border, src.size, b.C3_BLOCK, b.C3_BLOCK, R)
+    assert len(jobs) == 56280
+    got = M.results_numpy(M.diamond_search_batch(
+        torch.from_numpy(src).cuda(), torch.from_numpy(refs).cuda(), b.C3_BLOCK, b.C3_BLOCK,
+        M.to_device(jobs), 0, b.C3_COST, b.C3_SKIP))
+    exp = O.diamond_batch(src.reshape(-1), refs.reshape(-1), st, b.C3_BLOCK, b.C3_BLOCK, jobs, 0,
+                          b.C3_COST, b.C3_SKIP, threads=THREADS)
+    for f in ("best_row", "best_col", "bestsme", "steps"):  # the oracle has no search count
+        np.testing.assert_array_equal(got[f], exp[f], err_msg=f)
+    assert (np.abs(got["best_row"]) + np.abs(got["best_col"]) > 0).mean() > 0.5
+
+
+def _c4_planes(W, H):
+    import lavish_dsp.synth as synth
+    src = synth.frame(W, H, 10, 1234).astype(np.uint16)
+    pred = synth.shifted(synth.frame(W, H, 10, 1235), 3, -2).astype(np.uint16)
+    return src, pred
+
+
+def test_c4_4k_10bit_frame(L):
+    """bench.py --workload c4's frame and parameters."""
+    import torch
+    W, H, rdmult = 3840, 2160, 2000
+    src, pred = _c4_planes(W, H)
+    masks = dict(L.C4_TYPE_MASKS)
+    per, choice, recon = oracle_frame_c(src, pred, 10, masks, rdmult, threads=THREADS)
+    ts = torch.from_numpy(src.view(np.int16)).cuda()
+    tp = torch.from_numpy(pred.view(np.int16)).cuda()
+    fr = L.RdoFrame(ts)
+    L.rdo_frame(ts, tp, fr, L.build_quant_params(10, 128, L.QUANT_FP), rdmult, 10)
+    for s in masks:
+        got = L.rdo_records(fr.outs[s])
+        for f in ("best_type", "eob", "rate", "satd", "dist", "sse", "rdcost"):
+            np.testing.assert_array_equal(got[f], per[s][0][f], err_msg="%d %s" % (s, f))
+        np.testing.assert_array_equal(fr.outs[s]["qcoeff"].cpu().numpy(), per[s][1])
+        np.testing.assert_array_equal(fr.outs[s]["dqcoeff"].cpu().numpy(), per[s][2])
+    np.testing.assert_array_equal(fr.sb_tx_size.cpu().numpy(), choice)
+    np.testing.assert_array_equal(fr.recon.cpu().numpy().view(np.uint16), recon)
+    assert len(np.unique(choice)) > 1
+
+
+def test_c5_bands_world1_three_streams(L):
+    """shard.c4_band_processor on the 3 bands bands(H, 3) gives, each on its
+    own stream, the whole-frame step's reconstruction (SB rows are
+    independent for C4); the bands run concurrently, so the library's reused
+    device scratch must be ordered across streams."""
+    import torch
+    import lavish_dsp.shard as shard
+    W, H, rdmult = 1280, 720, 1700
+    src, pred = _c4_planes(W, H)
+    ts = torch.from_numpy(src.view(np.int16)).cuda()
+    tp = torch.from_numpy(pred.view(np.int16)).cuda()
+    qp = L.build_quant_params(10, 128, L.QUANT_FP)
+    whole = L.RdoFrame(ts)
+    L.rdo_frame(ts, tp, whole, qp, rdmult, 10)
+    torch.cuda.synchronize()
+    frames = {}
+    proc = shard.c4_band_processor(ts, tp, qp, rdmult, 10, frames)
+    streams = [torch.cuda.Stream() for _ in range(3)]
+    parts = []
+    for it in range(2):  # twice: the second pass reuses every cached buffer
+        parts = []
+        for (y0, y1), st in zip(shard.bands(H, 3), streams):
+            with torch.cuda.stream(st):
+                parts.append(proc(y0, y1).clone())
+        torch.cuda.synchronize()
+    full = torch.cat(parts, 0)
+    np.testing.assert_array_equal(full.cpu().numpy(), whole.recon.cpu().numpy())
+    # and through sharded_frame (world 1: one band, the whole frame)
+    one = shard.sharded_frame(H, 0, 1, proc)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(one.cpu().numpy(), whole.recon.cpu().numpy())

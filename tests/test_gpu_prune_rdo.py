@@ -62,8 +62,43 @@ def test_masked_random_orders(L, s, px):
     got = L.rdo_records(out)
     live = exp["rdcost"] != np.iinfo(np.int64).max  # blocks left with an allowed type
     assert live.mean() > 0.5
-    _cmp(got[live], exp[live], eq[live], ed[live], {"qcoeff": out["qcoeff"][torch.from_numpy(live).cuda()],
-                                                    "dqcoeff": out["dqcoeff"][torch.from_numpy(live).cuda()]})
+    # every block, including the ones with no candidate (tmask 0x0201 leaves
+    # many): TX_TYPE_INVALID, eob 0, INT64_MAX cost, zero coefficients
+    if s == 3:
+        assert (~live).sum() > 0
+    assert (exp["best_type"][~live] == 255).all() and (exp["eob"][~live] == 0).all()
+    _cmp(got, exp, eq, ed, out)
+
+
+def test_dead_blocks_reconstruct(L):
+    """Blocks without a candidate cost INT64_MAX: the SB sums saturate (no
+    wrap), so such an SB never picks that size, as in the oracle."""
+    import torch
+    bd = 10
+    src, pred = _planes(bd, 17)
+    sizes = {3: 0x0201, 2: 0xFFFF}
+    nb3 = (src.shape[1] // 32) * (src.shape[0] // 32)
+    masks = np.full(nb3, 0x0002, np.uint16)  # ADST_DCT only: never in {DCT, IDTX}
+    masks[::3] = 0
+    q = O.build_quant(bd, 128)
+    qp = L.build_quant_params(bd, 128, L.QUANT_FP)
+    ts = torch.from_numpy(src.view(np.int16)).cuda()
+    tp = torch.from_numpy(pred.view(np.int16)).cuda()
+    o3 = L.rdo_plane_masked(ts, tp, 3, sizes[3], qp, 1500,
+                            torch.from_numpy(masks.view(np.int16)).cuda(), None, bd)
+    o2 = L.rdo_plane(ts, tp, 2, sizes[2], qp, 1500, bd)
+    e3, q3, d3 = O.rdo_plane_masked(src, pred, 3, sizes[3], bd, q, 1500, masks, None, threads=8)
+    e2, q2, d2 = O.rdo_plane(src, pred, 2, sizes[2], bd, q, 1500, threads=8)
+    _cmp(L.rdo_records(o3), e3, q3, d3, o3)
+    recon = torch.empty_like(ts)
+    sbt = torch.empty(((src.shape[1] + 63) // 64) * ((src.shape[0] + 63) // 64), dtype=torch.uint8,
+                      device="cuda")
+    L.rdo_reconstruct([3, 2], {3: o3, 2: o2}, tp, recon, sbt, bd)
+    torch.cuda.synchronize()
+    er, esb = O.rdo_reconstruct([3, 2], [e3, e2], [d3, d2], pred, bd)
+    np.testing.assert_array_equal(sbt.cpu().numpy(), esb)
+    np.testing.assert_array_equal(recon.cpu().numpy().view(np.uint16), er)
+    assert (esb == 2).mean() > 0.5
 
 
 def test_masked_null_equals_plain(L):

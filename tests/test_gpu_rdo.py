@@ -196,3 +196,28 @@ def test_rdo_frame_px_and_reconstruct(L, bd):
         np.testing.assert_array_equal(fr.outs[s]["dqcoeff"].cpu().numpy(), per[s][2])
     np.testing.assert_array_equal(fr.sb_tx_size.cpu().numpy(), choice)
     np.testing.assert_array_equal(fr.recon.cpu().numpy().view(np.uint16), recon)
+
+
+def test_rdo_frame_px_every_64_point_size(L):
+    """All five 64-point sizes in one lavish_rdo_frame_px call: they run on
+    concurrent fan-out streams, each with its own scratch plane / job list
+    (rdo_plane_px64), and a second call reuses the scratch."""
+    import torch
+    bd = 10
+    src, pred = _planes(bd, 79, Wp=384, Hp=256)
+    masks = {4: 0x1, 11: 0x1, 12: 0x1, 17: 0x1, 18: 0x1, 3: 0x201, 2: 0xFFFF}
+    rdmult = 1900
+    q = O.build_quant(bd, 128)
+    ts = torch.from_numpy(src.view(np.int16)).cuda()
+    tp = torch.from_numpy(pred.view(np.int16)).cuda()
+    fr = L.RdoFrame(ts, type_masks=masks)
+    qp = L.build_quant_params(bd, 128, L.QUANT_FP)
+    for _ in range(2):
+        L.rdo_frame(ts, tp, fr, qp, rdmult, bd, px=True, reconstruct=False)
+    torch.cuda.synchronize()
+    for s, m in masks.items():
+        exp, eq, ed = O.rdo_plane(src, pred, s, m, bd, q, rdmult, threads=8, px=True)
+        got = L.rdo_records(fr.outs[s])
+        for f in ("best_type", "eob", "dist", "sse", "rdcost"):
+            np.testing.assert_array_equal(got[f], exp[f], err_msg="%d %s" % (s, f))
+        np.testing.assert_array_equal(fr.outs[s]["dqcoeff"].cpu().numpy(), ed)
