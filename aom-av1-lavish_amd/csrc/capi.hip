@@ -306,9 +306,9 @@ const int16_t* lavish_iscan(int tx_size, int tx_type) {
 static void fwd2d_shim(int tx_size, const int16_t* input, int32_t* output, int stride,
                        int tx_type) {
   const int W = tx_w(tx_size), H = tx_h(tx_size);
-  if (!tx_type_valid(tx_size, tx_type)) {
-    fprintf(stderr, "[lavish_hip] invalid tx_type %d for tx_size %d\n", tx_type, tx_size);
-    abort();
+  if (tx_size < 0 || tx_size >= 19 || !tx_type_valid(tx_size, tx_type)) {
+    shim_reject("av1_fwd_txfm2d (tx_size / tx_type)", -5);
+    return;
   }
   hipStream_t s = shim_stream();
   const int n = max_eob(tx_size);
@@ -324,8 +324,8 @@ static void fwd2d_shim(int tx_size, const int16_t* input, int32_t* output, int s
   const int rc = txq_plane(din, W, W, H, tx_size, 1u << tx_type, 8, LAVISH_QUANT_NONE, nullptr,
                            nullptr, nullptr, nullptr, dout, s);
   if (rc != 0) {
-    fprintf(stderr, "[lavish_hip] txq_plane rejected tx_size %d (rc %d)\n", tx_size, rc);
-    abort();
+    shim_reject("txq_plane", rc);
+    return;
   }
   LAVISH_CHECK(hipMemcpyAsync(output, dout, (size_t)n * sizeof(int32_t), hipMemcpyDeviceToHost,
                               s));
@@ -371,14 +371,33 @@ FWD2D_SHIM(8, 32, 15)
 FWD2D_SHIM(32, 8, 16)
 #undef FWD2D_SHIM
 
-// av1_lowbd_fwd_txfm_c -> av1_highbd_fwd_txfm (hybrid_fwd_txfm.c:244-313)
+// av1_lowbd_fwd_txfm_c -> av1_highbd_fwd_txfm (hybrid_fwd_txfm.c:244-313):
+// only the 4x4 case looks at `lossless` (highbd_fwd_txfm_4x4, :77-88), where
+// it takes the Walsh-Hadamard transform (wht.hip)
 void av1_lowbd_fwd_txfm_hip(const int16_t* src_diff, int32_t* coeff, int diff_stride,
                             LavishTxfmParam* p) {
-  if (p->lossless) {
-    fprintf(stderr, "[lavish_hip] lossless WHT is not offloaded (DESIGN.md)\n");
-    abort();
+  if (p->lossless && p->tx_size == 0) {
+    av1_fwht4x4_hip(src_diff, coeff, diff_stride);
+    return;
   }
   fwd2d_shim(p->tx_size, src_diff, coeff, diff_stride, p->tx_type);
+}
+
+// av1_quick_txfm (hybrid_fwd_txfm.c:315-336): the TPL model's transform --
+// aom_hadamard_{4x4..32x32} or the DCT_DCT forward transform
+void av1_quick_txfm_hip(int use_hadamard, uint8_t tx_size, LavishBitDepthInfo bd_info,
+                        const int16_t* src_diff, int src_stride, int32_t* coeff) {
+  (void)bd_info;  // feeds only the forward transform's disabled range checks
+  if (use_hadamard) {
+    switch (tx_size) {
+      case 0: aom_hadamard_4x4_hip(src_diff, src_stride, coeff); return;
+      case 1: aom_hadamard_8x8_hip(src_diff, src_stride, coeff); return;
+      case 2: aom_hadamard_16x16_hip(src_diff, src_stride, coeff); return;
+      case 3: aom_hadamard_32x32_hip(src_diff, src_stride, coeff); return;
+      default: shim_reject("av1_quick_txfm (hadamard size)", -2); return;
+    }
+  }
+  fwd2d_shim(tx_size, src_diff, coeff, src_stride, 0);
 }
 
 // Quantizer shims: the reference passes pointers into its 8-wide QUANTS

@@ -62,6 +62,10 @@ int fan_width();
 hipStream_t* fan_out(hipStream_t caller);
 void fan_in(hipStream_t caller);
 
+// av1_highbd_iwht4x4_add (av1/common/idct.c:34-40) on a host u16 4x4 block
+// (wht.hip): the lossless branch of the inverse-transform shims
+void iwht_host(const int32_t* input, uint16_t* dest, int stride, int eob, int bd);
+
 // per-thread scratch device buffer for the per-call (host pointer) shims
 void* shim_scratch(size_t bytes);
 hipStream_t shim_stream();

@@ -14,7 +14,10 @@
 //   subtract                aom_dsp/subtract.c:20-54
 //   sum_squares_2d_i16      aom_dsp/sum_squares.c:16-30
 //   hadamard / satd         aom_dsp/avg.c:102-348,509-516
-//   block_error             av1/encoder/rdopt.c:635-682
+//   hadamard_lp / satd_lp   aom_dsp/avg.c:207-316,518-524
+//   block_error (+_lp)      av1/encoder/rdopt.c:635-682
+//   sum_sse_2d_i16          aom_dsp/sum_squares.c:75-90
+//   get_blk_sse_sum         aom_dsp/blk_sse_sum.c:14-27
 #include "lavish_internal.h"
 
 namespace lavish {
@@ -254,10 +257,13 @@ __device__ __forceinline__ void had_small(const int16_t* src, int st, int32_t* c
   }
 }
 
-// jobs: src_off = element offset of the block, aux_off = coefficient offset
+// jobs: src_off = element offset of the block, aux_off = coefficient offset.
+// coeff16 != nullptr: aom_hadamard_lp_8x8 (avg.c:207-236), the lowbd 8x8
+// butterflies and transpose stored as int16.
 __global__ __launch_bounds__(64) void hadamard_small_kernel(int n, int highbd, const int16_t* src,
                                                             int stride, const LavishPixJob* jobs,
-                                                            int njobs, int32_t* coeff) {
+                                                            int njobs, int32_t* coeff,
+                                                            int16_t* coeff16) {
   const int j = blockIdx.x * 64 + threadIdx.x;
   if (j >= njobs) return;
   const LavishPixJob jb = jobs[j];
@@ -265,14 +271,21 @@ __global__ __launch_bounds__(64) void hadamard_small_kernel(int n, int highbd, c
   if (n == 4) had_small<4, false>(src + jb.src_off, stride, c);
   else if (highbd) had_small<8, true>(src + jb.src_off, stride, c);
   else had_small<8, false>(src + jb.src_off, stride, c);
-  for (int i = 0; i < n * n; ++i) coeff[jb.aux_off + i] = c[i];
+  if (coeff16) {
+    for (int i = 0; i < n * n; ++i) coeff16[jb.aux_off + i] = (int16_t)c[i];
+  } else {
+    for (int i = 0; i < n * n; ++i) coeff[jb.aux_off + i] = c[i];
+  }
 }
 
 // 16x16 / 32x32: one wave per job; 8x8 sub-blocks by lanes into LDS, then the
-// combine stages (avg.c:226-348) over all lanes.
+// combine stages (avg.c:226-348) over all lanes.  coeff16 != nullptr:
+// aom_hadamard_lp_16x16 (avg.c:289-316): every combine value truncated to
+// int16 and no AVX2 group swap.
 __global__ __launch_bounds__(64) void hadamard_big_kernel(int n, int highbd, const int16_t* src,
                                                           int stride, const LavishPixJob* jobs,
-                                                          int32_t* coeff) {
+                                                          int32_t* coeff, int16_t* coeff16) {
+  const bool lp = coeff16 != nullptr;
   __shared__ int32_t c[1024];
   const LavishPixJob jb = jobs[blockIdx.x];
   const int lane = threadIdx.x;
@@ -291,16 +304,22 @@ __global__ __launch_bounds__(64) void hadamard_big_kernel(int n, int highbd, con
     int32_t* cq = c + q * 256;
     const int i = lane;  // 64 lanes x one column of 4
     const int32_t a0 = cq[i], a1 = cq[64 + i], a2 = cq[128 + i], a3 = cq[192 + i];
-    const int32_t b0 = (a0 + a1) >> 1, b1 = (a0 - a1) >> 1;
-    const int32_t b2 = (a2 + a3) >> 1, b3 = (a2 - a3) >> 1;
+    int32_t b0 = (a0 + a1) >> 1, b1 = (a0 - a1) >> 1;
+    int32_t b2 = (a2 + a3) >> 1, b3 = (a2 - a3) >> 1;
+    if (lp) {
+      b0 = (int16_t)b0;
+      b1 = (int16_t)b1;
+      b2 = (int16_t)b2;
+      b3 = (int16_t)b3;
+    }
     __syncthreads();
-    cq[i] = b0 + b2;
-    cq[64 + i] = b1 + b3;
-    cq[128 + i] = b0 - b2;
-    cq[192 + i] = b1 - b3;
+    cq[i] = lp ? (int16_t)(b0 + b2) : b0 + b2;
+    cq[64 + i] = lp ? (int16_t)(b1 + b3) : b1 + b3;
+    cq[128 + i] = lp ? (int16_t)(b0 - b2) : b0 - b2;
+    cq[192 + i] = lp ? (int16_t)(b1 - b3) : b1 - b3;
     __syncthreads();
     // lowbd only: swap of 4-wide groups to match the AVX2 order (avg.c:281-287)
-    if (!highbd) {
+    if (!highbd && !lp) {
       const int row = lane >> 2, jj = lane & 3;
       const int32_t t = cq[row * 16 + 4 + jj];
       const int32_t u = cq[row * 16 + 8 + jj];
@@ -321,7 +340,11 @@ __global__ __launch_bounds__(64) void hadamard_big_kernel(int n, int highbd, con
     }
     __syncthreads();
   }
-  for (int i = lane; i < n * n; i += 64) coeff[jb.aux_off + i] = c[i];
+  if (lp) {
+    for (int i = lane; i < n * n; i += 64) coeff16[jb.aux_off + i] = (int16_t)c[i];
+  } else {
+    for (int i = lane; i < n * n; i += 64) coeff[jb.aux_off + i] = c[i];
+  }
 }
 
 // ---------------------------------------------------------------- SATD ----
@@ -333,7 +356,52 @@ __global__ __launch_bounds__(64) void satd_kernel(const int32_t* coeff, int leng
   if (threadIdx.x == 0) out[blockIdx.x] = (int)acc;
 }
 
+__global__ __launch_bounds__(64) void satd_lp_kernel(const int16_t* coeff, int length, int* out) {
+  const int16_t* c = coeff + (int64_t)blockIdx.x * length;
+  uint32_t acc = 0;
+  for (int i = threadIdx.x; i < length; i += 64) acc += (uint32_t)abs((int)c[i]);
+  acc = wave_sum32(acc);
+  if (threadIdx.x == 0) out[blockIdx.x] = (int)acc;
+}
+
+// ------------------------------------------------------- sum and sse ----
+// (sum, sse) of an int16 block: aom_sum_sse_2d_i16 (sum_squares.c:75-90) and
+// aom_get_blk_sse_sum (blk_sse_sum.c:14-27) -- v * v in int, int64 sums
+__global__ __launch_bounds__(64) void sum_sse_kernel(const int16_t* src, int stride, int w, int h,
+                                                     const LavishPixJob* jobs, int32_t* sum_out,
+                                                     int64_t* sse_out) {
+  const LavishPixJob jb = jobs[blockIdx.x];
+  int64_t ss = 0, sm = 0;
+  for (int i = threadIdx.x; i < w * h; i += 64) {
+    const int y = i / w, x = i - y * w;
+    const int v = src[jb.src_off + (int64_t)y * stride + x];
+    ss += v * v;
+    sm += v;
+  }
+  ss = wave_sum64(ss);
+  sm = wave_sum64(sm);
+  if (threadIdx.x == 0) {
+    if (sum_out) sum_out[blockIdx.x] = (int32_t)sm;
+    if (sse_out) sse_out[blockIdx.x] = ss;
+  }
+}
+
 // --------------------------------------------------------- block error ----
+// av1_block_error_lp (rdopt.c:650-660): int16 inputs, diff * diff in int
+// (wrapping) arithmetic, int64 sum
+__global__ __launch_bounds__(64) void block_error_lp_kernel(const int16_t* coeff,
+                                                            const int16_t* dqcoeff, int n,
+                                                            int64_t* err_out) {
+  const int64_t base = (int64_t)blockIdx.x * n;
+  int64_t err = 0;
+  for (int i = threadIdx.x; i < n; i += 64) {
+    const int32_t df = (int32_t)coeff[base + i] - dqcoeff[base + i];
+    err += (int32_t)((uint32_t)df * (uint32_t)df);
+  }
+  err = wave_sum64(err);
+  if (threadIdx.x == 0) err_out[blockIdx.x] = err;
+}
+
 __global__ __launch_bounds__(64) void block_error_kernel(const int32_t* coeff,
                                                          const int32_t* dqcoeff, int n, int bd,
                                                          int64_t* err_out, int64_t* ssz_out) {
@@ -444,12 +512,55 @@ int lavish_hadamard_batch(int n, int highbd, const int16_t* src_diff, int stride
   hipStream_t s = (hipStream_t)stream;
   if (n == 4 || n == 8)
     hipLaunchKernelGGL(hadamard_small_kernel, dim3((njobs + 63) / 64), dim3(64), 0, s, n, highbd,
-                       src_diff, stride, jobs, njobs, coeff);
+                       src_diff, stride, jobs, njobs, coeff, (int16_t*)nullptr);
   else if (n == 16 || n == 32)
     hipLaunchKernelGGL(hadamard_big_kernel, dim3(njobs), dim3(64), 0, s, n, highbd, src_diff,
-                       stride, jobs, coeff);
+                       stride, jobs, coeff, (int16_t*)nullptr);
   else
     return -1;
+  LCHK();
+  return 0;
+}
+
+int lavish_hadamard_lp_batch(int n, const int16_t* src_diff, int stride, const LavishPixJob* jobs,
+                             int njobs, int16_t* coeff, void* stream) {
+  if (njobs <= 0) return 0;
+  hipStream_t s = (hipStream_t)stream;
+  if (n == 8)
+    hipLaunchKernelGGL(hadamard_small_kernel, dim3((njobs + 63) / 64), dim3(64), 0, s, 8, 0,
+                       src_diff, stride, jobs, njobs, (int32_t*)nullptr, coeff);
+  else if (n == 16)
+    hipLaunchKernelGGL(hadamard_big_kernel, dim3(njobs), dim3(64), 0, s, 16, 0, src_diff, stride,
+                       jobs, (int32_t*)nullptr, coeff);
+  else
+    return -1;  // the reference has lp forms for 8x8 and 16x16 only
+  LCHK();
+  return 0;
+}
+
+int lavish_satd_lp_batch(const int16_t* coeff, int length, int nblocks, int* out, void* stream) {
+  if (nblocks <= 0) return 0;
+  hipLaunchKernelGGL(satd_lp_kernel, dim3(nblocks), dim3(64), 0, (hipStream_t)stream, coeff,
+                     length, out);
+  LCHK();
+  return 0;
+}
+
+int lavish_block_error_lp_batch(const int16_t* coeff, const int16_t* dqcoeff, int n, int nblocks,
+                                int64_t* err, void* stream) {
+  if (nblocks <= 0) return 0;
+  hipLaunchKernelGGL(block_error_lp_kernel, dim3(nblocks), dim3(64), 0, (hipStream_t)stream,
+                     coeff, dqcoeff, n, err);
+  LCHK();
+  return 0;
+}
+
+int lavish_sum_sse_batch(const int16_t* src, int stride, int w, int h, const LavishPixJob* jobs,
+                         int njobs, int32_t* sum, int64_t* sse, void* stream) {
+  if (njobs <= 0) return 0;
+  if (w <= 0 || h <= 0) return -1;
+  hipLaunchKernelGGL(sum_sse_kernel, dim3(njobs), dim3(64), 0, (hipStream_t)stream, src, stride,
+                     w, h, jobs, sum, sse);
   LCHK();
   return 0;
 }

@@ -53,10 +53,7 @@ struct Stage {
 constexpr size_t kStageCap = 4u << 20;  // 128x128 u16 x (src + 4 refs + second) + outputs
 
 void must(int rc, const char* what) {
-  if (rc != 0) {
-    fprintf(stderr, "[lavish_hip] %s rejected its arguments (rc %d)\n", what, rc);
-    abort();
-  }
+  if (rc != 0) shim_reject(what, rc);
 }
 
 template <typename Pix>
@@ -183,9 +180,9 @@ int64_t block_error_shim(const int32_t* coeff, const int32_t* dqcoeff, intptr_t 
 // kernel on a single job, copy the window back.
 template <typename Pix>
 void inv_shim(int tx_size, const int32_t* input, Pix* dst, int stride, int tx_type, int bd) {
-  if (!tx_type_valid(tx_size, tx_type)) {
-    fprintf(stderr, "[lavish_hip] invalid tx_type %d for tx_size %d\n", tx_type, tx_size);
-    abort();
+  if (tx_size < 0 || tx_size >= 19 || !tx_type_valid(tx_size, tx_type)) {
+    shim_reject("inverse transform (tx_size / tx_type)", -5);
+    return;
   }
   const int W = tx_w(tx_size), H = tx_h(tx_size), n = max_eob(tx_size);
   Stage st(kStageCap);
@@ -202,11 +199,21 @@ void inv_shim(int tx_size, const int32_t* input, Pix* dst, int stride, int tx_ty
   st.sync();
 }
 
-void check_lossless(const LavishTxfmParam* p) {
-  if (p->lossless) {
-    fprintf(stderr, "[lavish_hip] lossless (WHT) inverse transform is not implemented\n");
-    abort();
-  }
+// the lossless branch of av1_highbd_inv_txfm_add_4x4_c (idct.c:42-57): only
+// TX_4X4 looks at `lossless`; it adds the inverse Walsh-Hadamard transform
+// (av1_highbd_iwht4x4_add, eob > 1 -> the 16-coefficient form).  Returns 1
+// when it handled the block.
+template <typename Pix>
+int lossless_inv(const int32_t* input, Pix* dst, int stride, const LavishTxfmParam* p) {
+  if (!p->lossless || p->tx_size != 0) return 0;
+  uint16_t blk[16];
+  for (int r = 0; r < 4; ++r)
+    for (int c = 0; c < 4; ++c) blk[r * 4 + c] = dst[r * stride + c];
+  iwht_host(input, blk, 4, p->eob, p->bd);
+  // av1_inv_txfm_add_c (idct.c:281-302) copies back through (uint8_t)
+  for (int r = 0; r < 4; ++r)
+    for (int c = 0; c < 4; ++c) dst[r * stride + c] = (Pix)blk[r * 4 + c];
+  return 1;
 }
 
 // one block through the inter-prediction kernel with the caller's own
@@ -422,6 +429,88 @@ int aom_satd_hip(const int32_t* coeff, int length) {
   return r;
 }
 
+// aom_hadamard_lp_{8x8,16x16} and the dual form (two 8x8 side by side,
+// avg.c:238-245); aom_satd_lp; av1_block_error_lp
+static void hadamard_lp_shim(int n, int nblk, const int16_t* src, ptrdiff_t stride,
+                             int16_t* coeff) {
+  Stage st(kStageCap);
+  const int16_t* d = st.block(src, stride, n * nblk, n);
+  int16_t* dc = (int16_t*)st.take((size_t)nblk * n * n * sizeof(int16_t));
+  LavishPixJob jb[2] = {};
+  for (int k = 0; k < nblk; ++k) {
+    jb[k].src_off = (int64_t)k * n;
+    jb[k].aux_off = (int64_t)k * n * n;
+  }
+  const LavishPixJob* djob = st.copy_in(jb, nblk);
+  must(lavish_hadamard_lp_batch(n, d, n * nblk, djob, nblk, dc, st.s), "lavish_hadamard_lp_batch");
+  st.copy_out(coeff, dc, (size_t)nblk * n * n);
+  st.sync();
+}
+void aom_hadamard_lp_8x8_hip(const int16_t* s, ptrdiff_t st, int16_t* c) {
+  hadamard_lp_shim(8, 1, s, st, c);
+}
+void aom_hadamard_lp_16x16_hip(const int16_t* s, ptrdiff_t st, int16_t* c) {
+  hadamard_lp_shim(16, 1, s, st, c);
+}
+void aom_hadamard_lp_8x8_dual_hip(const int16_t* s, ptrdiff_t st, int16_t* c) {
+  hadamard_lp_shim(8, 2, s, st, c);
+}
+
+int aom_satd_lp_hip(const int16_t* coeff, int length) {
+  Stage st(kStageCap + (size_t)length * 2);
+  const int16_t* d = st.copy_in(coeff, length);
+  int* dout = (int*)st.take(64);
+  must(lavish_satd_lp_batch(d, length, 1, dout, st.s), "lavish_satd_lp_batch");
+  int r = 0;
+  st.copy_out(&r, dout, 1);
+  st.sync();
+  return r;
+}
+
+int64_t av1_block_error_lp_hip(const int16_t* coeff, const int16_t* dqcoeff, intptr_t n) {
+  Stage st(kStageCap + (size_t)n * 4);
+  const int16_t* c = st.copy_in(coeff, n);
+  const int16_t* dq = st.copy_in(dqcoeff, n);
+  int64_t* de = (int64_t*)st.take(64);
+  must(lavish_block_error_lp_batch(c, dq, (int)n, 1, de, st.s), "lavish_block_error_lp_batch");
+  int64_t e = 0;
+  st.copy_out(&e, de, 1);
+  st.sync();
+  return e;
+}
+
+// (sum, sse) of an int16 block through lavish_sum_sse_batch
+static void sum_sse_shim(const int16_t* src, int stride, int w, int h, int32_t* sum,
+                         int64_t* sse) {
+  Stage st(kStageCap + (size_t)w * h * 2);
+  const int16_t* d = st.block(src, stride, w, h);
+  LavishPixJob jb{};
+  const LavishPixJob* djob = st.copy_in(&jb, 1);
+  int32_t* dsum = (int32_t*)st.take(64);
+  int64_t* dsse = (int64_t*)st.take(64);
+  must(lavish_sum_sse_batch(d, w, w, h, djob, 1, dsum, dsse, st.s), "lavish_sum_sse_batch");
+  st.copy_out(sum, dsum, 1);
+  st.copy_out(sse, dsse, 1);
+  st.sync();
+}
+// aom_sum_sse_2d_i16 (sum_squares.c:75-90): *sum accumulates (the caller
+// initialises it), the return is the sum of squares
+uint64_t aom_sum_sse_2d_i16_hip(const int16_t* src, int src_stride, int width, int height,
+                                int* sum) {
+  int32_t s = 0;
+  int64_t ss = 0;
+  sum_sse_shim(src, src_stride, width, height, &s, &ss);
+  *sum += s;
+  return (uint64_t)ss;
+}
+// aom_get_blk_sse_sum (blk_sse_sum.c:14-27)
+void aom_get_blk_sse_sum_hip(const int16_t* data, int stride, int bw, int bh, int* x_sum,
+                             int64_t* x2_sum) {
+  int32_t s = 0;
+  sum_sse_shim(data, stride, bw, bh, &s, x2_sum);
+  *x_sum = s;
+}
+
 int64_t av1_block_error_hip(const int32_t* coeff, const int32_t* dqcoeff, intptr_t n,
                             int64_t* ssz) {
   return block_error_shim(coeff, dqcoeff, n, ssz, 0);
@@ -448,19 +537,20 @@ LAVISH_TX_SIZES_ALL(INV2D_SHIM)
 // av1_inv_txfm_add_c (idct.c:281-302): u8 destination, bd 8
 void av1_inv_txfm_add_hip(const int32_t* dqcoeff, uint8_t* dst, int stride,
                           const LavishTxfmParam* p) {
-  check_lossless(p);
+  if (lossless_inv<uint8_t>(dqcoeff, dst, stride, p)) return;
   inv_shim<uint8_t>(p->tx_size, dqcoeff, dst, stride, p->tx_type, 8);
 }
 // av1_highbd_inv_txfm_add_c (idct.c:212-279): tagged u16 destination
 void av1_highbd_inv_txfm_add_hip(const int32_t* input, uint8_t* dest, int stride,
                                  const LavishTxfmParam* p) {
-  check_lossless(p);
+  if (lossless_inv<uint16_t>(input, untag<uint16_t>(dest), stride, p)) return;
   inv_shim<uint16_t>(p->tx_size, input, untag<uint16_t>(dest), stride, p->tx_type, p->bd);
 }
 #define HBD_INV_SHIM(w, h)                                                                    \
   void av1_highbd_inv_txfm_add_##w##x##h##_hip(const int32_t* input, uint8_t* dest,           \
                                                int stride, const LavishTxfmParam* p) {        \
-    check_lossless(p);                                                                        \
+    if (w == 4 && h == 4 && lossless_inv<uint16_t>(input, untag<uint16_t>(dest), stride, p))  \
+      return;                                                                                 \
     inv_shim<uint16_t>(size_of(w, h), input, untag<uint16_t>(dest), stride, p->tx_type,      \
                        p->bd);                                                                \
   }

@@ -123,6 +123,15 @@ for _s, _name in enumerate(TX_SIZES):
     _FWD2D[_s] = f
 _lib.av1_lowbd_fwd_txfm_hip.argtypes = [_vp, _vp, _i32, ctypes.POINTER(TxfmParam)]
 
+
+class BitDepthInfo(ctypes.Structure):
+    """BitDepthInfo (av1/common/blockd.h:952-960)."""
+    _fields_ = [("bit_depth", ctypes.c_int), ("use_highbitdepth_buf", ctypes.c_int)]
+
+
+_lib.av1_quick_txfm_hip.argtypes = [_i32, ctypes.c_uint8, BitDepthInfo, _vp, _i32, _vp]
+_lib.av1_quick_txfm_hip.restype = None
+
 _QARGS = [_vp, ctypes.c_ssize_t, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]
 _QUANT_NAMES = ["av1_quantize_fp", "av1_quantize_fp_32x32", "av1_quantize_fp_64x64",
                 "aom_quantize_b", "aom_quantize_b_32x32", "aom_quantize_b_64x64",
@@ -183,6 +192,12 @@ for _s in _FWD2D:
 
 def av1_lowbd_fwd_txfm(src_diff, coeff, diff_stride, txfm_param):
     _lib.av1_lowbd_fwd_txfm_hip(_p(src_diff), _p(coeff), diff_stride, ctypes.byref(txfm_param))
+
+
+def av1_quick_txfm(use_hadamard, tx_size, bd_info, src_diff, src_stride, coeff):
+    """av1_quick_txfm (av1/encoder/hybrid_fwd_txfm.c:315-336)."""
+    _lib.av1_quick_txfm_hip(int(use_hadamard), tx_size, bd_info, _p(src_diff), src_stride,
+                            _p(coeff))
 
 
 def _quant(name):

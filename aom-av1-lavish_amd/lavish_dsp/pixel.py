@@ -94,6 +94,15 @@ for _n in ("4x4", "8x8", "16x16", "32x32"):
 for _n in ("8x8", "16x16", "32x32"):
     _proto("aom_highbd_hadamard_" + _n, None, [_vp, _ssz, _vp])
 _proto("aom_satd", ctypes.c_int, [_vp, _i32])
+for _n in ("8x8", "16x16", "8x8_dual"):
+    _proto("aom_hadamard_lp_" + _n, None, [_vp, _ssz, _vp])
+_proto("aom_satd_lp", ctypes.c_int, [_vp, _i32])
+_proto("av1_block_error_lp", ctypes.c_int64, [_vp, _vp, _ssz])
+_proto("aom_sum_sse_2d_i16", ctypes.c_uint64, [_vp, _i32, _i32, _i32, _vp])
+_proto("aom_get_blk_sse_sum", None, [_vp, _i32, _i32, _i32, _vp, _vp])
+_proto("av1_fwht4x4", None, [_vp, _vp, _i32])
+_proto("av1_highbd_iwht4x4_16_add", None, [_vp, _vp, _i32, _i32])
+_proto("av1_highbd_iwht4x4_1_add", None, [_vp, _vp, _i32, _i32])
 _proto("av1_block_error", ctypes.c_int64, [_vp, _vp, _ssz, _vp])
 _proto("av1_highbd_block_error", ctypes.c_int64, [_vp, _vp, _ssz, _vp, _i32])
 
@@ -202,6 +211,51 @@ def satd(coeff, length):
     return _PROTOS["aom_satd"](_ptr(coeff), length)
 
 
+def hadamard_lp(n, src_diff, stride, dual=False):
+    """aom_hadamard_lp_{8x8,16x16} / _8x8_dual: int16 coefficients."""
+    out = np.zeros(n * n * (2 if dual else 1), np.int16)
+    name = "aom_hadamard_lp_8x8_dual" if dual else "aom_hadamard_lp_%dx%d" % (n, n)
+    _PROTOS[name](_ptr(src_diff), stride, _ptr(out))
+    return out
+
+
+def satd_lp(coeff, length):
+    return _PROTOS["aom_satd_lp"](_ptr(np.ascontiguousarray(coeff, np.int16)), length)
+
+
+def block_error_lp(coeff, dqcoeff, n):
+    return _PROTOS["av1_block_error_lp"](_ptr(np.ascontiguousarray(coeff, np.int16)),
+                                         _ptr(np.ascontiguousarray(dqcoeff, np.int16)), n)
+
+
+def sum_sse_2d_i16(src, stride, w, h, sum_in=0):
+    """aom_sum_sse_2d_i16: (sse, *sum after the call)."""
+    sm = np.array([sum_in], np.int32)
+    v = _PROTOS["aom_sum_sse_2d_i16"](_ptr(src), stride, w, h, _ptr(sm))
+    return v, int(sm[0])
+
+
+def get_blk_sse_sum(src, stride, w, h):
+    """aom_get_blk_sse_sum: (x_sum, x2_sum)."""
+    sm = np.zeros(1, np.int32)
+    ss = np.zeros(1, np.int64)
+    _PROTOS["aom_get_blk_sse_sum"](_ptr(src), stride, w, h, _ptr(sm), _ptr(ss))
+    return int(sm[0]), int(ss[0])
+
+
+def fwht4x4(src_diff, stride):
+    out = np.zeros(16, np.int32)
+    _PROTOS["av1_fwht4x4"](_ptr(src_diff), _ptr(out), stride)
+    return out
+
+
+def iwht4x4_add(coeff, dst, stride, bd, full=True):
+    """av1_highbd_iwht4x4_16_add (full) / _1_add on a uint16 view (tagged
+    pointer, like the reference's callers)."""
+    name = "av1_highbd_iwht4x4_16_add" if full else "av1_highbd_iwht4x4_1_add"
+    _PROTOS[name](_ptr(np.ascontiguousarray(coeff, np.int32)), _ptr(dst, True), stride, bd)
+
+
 def block_error(coeff, dqcoeff, n, bd=None):
     """(error, ssz): av1_block_error (bd None) / av1_highbd_block_error."""
     ssz = np.zeros(1, np.int64)
@@ -223,7 +277,13 @@ for _n, _a in (
         ("lavish_sum_squares_batch", [_vp, _i32, _i32, _i32, _vp, _i32, _vp, _vp]),
         ("lavish_hadamard_batch", [_i32, _i32, _vp, _i32, _vp, _i32, _vp, _vp]),
         ("lavish_satd_batch", [_vp, _i32, _i32, _vp, _vp]),
-        ("lavish_block_error_batch", [_vp, _vp, _i32, _i32, _i32, _vp, _vp, _vp])):
+        ("lavish_block_error_batch", [_vp, _vp, _i32, _i32, _i32, _vp, _vp, _vp]),
+        ("lavish_hadamard_lp_batch", [_i32, _vp, _i32, _vp, _i32, _vp, _vp]),
+        ("lavish_satd_lp_batch", [_vp, _i32, _i32, _vp, _vp]),
+        ("lavish_block_error_lp_batch", [_vp, _vp, _i32, _i32, _vp, _vp]),
+        ("lavish_sum_sse_batch", [_vp, _i32, _i32, _i32, _vp, _i32, _vp, _vp, _vp]),
+        ("lavish_fwht4x4_batch", [_vp, _i32, _vp, _i32, _vp, _vp]),
+        ("lavish_iwht4x4_add_batch", [_vp, _vp, _i32, _vp, _i32, _i32, _i32, _vp])):
     getattr(_lib, _n).argtypes = _a
     getattr(_lib, _n).restype = _i32
 
@@ -324,3 +384,42 @@ def block_error_batch(coeff, dqcoeff, bit_depth=0, stream=None):
                                          _d(ssz), _stream_ptr(stream)),
            "lavish_block_error_batch")
     return err, ssz
+
+
+def sum_sse_batch(src, w, h, jobs, stream=None):
+    """(sum int32, sse int64) tensors of lavish_sum_sse_batch."""
+    import torch
+    nj = jobs.numel() // JOB_DTYPE.itemsize
+    sm = torch.empty(nj, dtype=torch.int32, device=src.device)
+    ss = torch.empty(nj, dtype=torch.int64, device=src.device)
+    _check(_lib.lavish_sum_sse_batch(_d(src), src.stride(0), w, h, _d(jobs), nj, _d(sm), _d(ss),
+                                     _stream_ptr(stream)), "lavish_sum_sse_batch")
+    return sm, ss
+
+
+def hadamard_lp_batch(n, src_diff, jobs, ncoeff_words, stream=None):
+    import torch
+    nj = jobs.numel() // JOB_DTYPE.itemsize
+    out = torch.zeros(ncoeff_words, dtype=torch.int16, device=src_diff.device)
+    _check(_lib.lavish_hadamard_lp_batch(n, _d(src_diff), src_diff.stride(0), _d(jobs), nj,
+                                         _d(out), _stream_ptr(stream)), "lavish_hadamard_lp_batch")
+    return out
+
+
+def fwht4x4_batch(src_diff, jobs, ncoeff_words, stream=None):
+    import torch
+    nj = jobs.numel() // JOB_DTYPE.itemsize
+    out = torch.zeros(ncoeff_words, dtype=torch.int32, device=src_diff.device)
+    _check(_lib.lavish_fwht4x4_batch(_d(src_diff), src_diff.stride(0), _d(jobs), nj, _d(out),
+                                     _stream_ptr(stream)), "lavish_fwht4x4_batch")
+    return out
+
+
+def iwht4x4_add_batch(dqcoeff, jobs, dst, bit_depth, stream=None):
+    """lavish_iwht4x4_add_batch; jobs: device tensor of lavish_dsp.INV_JOB_DTYPE
+    records; dst: uint8 (bd 8) or int16-viewed uint16 plane, updated in place."""
+    from . import INV_JOB_DTYPE
+    nj = jobs.numel() // INV_JOB_DTYPE.itemsize
+    _check(_lib.lavish_iwht4x4_add_batch(_d(dqcoeff), _d(jobs), nj, _d(dst), dst.stride(0),
+                                         bit_depth, int(dst.element_size() == 2),
+                                         _stream_ptr(stream)), "lavish_iwht4x4_add_batch")

@@ -205,6 +205,32 @@ int lavish_block_error_batch(const int32_t *coeff, const int32_t *dqcoeff,
                              int n, int nblocks, int bit_depth, int64_t *err,
                              int64_t *ssz, void *stream);
 
+/* aom_hadamard_lp_{8x8,16x16} (aom_dsp/avg.c:207-316): int16 coefficients
+ * (n = 8 or 16, else -1). */
+int lavish_hadamard_lp_batch(int n, const int16_t *src_diff, int stride,
+                             const LavishPixJob *jobs, int njobs,
+                             int16_t *coeff, void *stream);
+/* aom_satd_lp (aom_dsp/avg.c:518-524) of nblocks contiguous int16 blocks. */
+int lavish_satd_lp_batch(const int16_t *coeff, int length, int nblocks,
+                         int *out, void *stream);
+/* av1_block_error_lp (av1/encoder/rdopt.c:650-660). */
+int lavish_block_error_lp_batch(const int16_t *coeff, const int16_t *dqcoeff,
+                                int n, int nblocks, int64_t *err,
+                                void *stream);
+/* (sum, sum of squares) of a w x h int16 block at src + job.src_off:
+ * aom_sum_sse_2d_i16 (aom_dsp/sum_squares.c:75-90) and aom_get_blk_sse_sum
+ * (aom_dsp/blk_sse_sum.c:14-27).  Either output may be NULL. */
+int lavish_sum_sse_batch(const int16_t *src, int stride, int w, int h,
+                         const LavishPixJob *jobs, int njobs, int32_t *sum,
+                         int64_t *sse, void *stream);
+
+/* ---- lossless 4x4 Walsh-Hadamard ----------------------------------------
+ * av1_fwht4x4 (hybrid_fwd_txfm.c:24-76): src_diff + job.src_off (stride) ->
+ * 16 words at coeff + job.aux_off. */
+int lavish_fwht4x4_batch(const int16_t *src_diff, int stride,
+                         const LavishPixJob *jobs, int njobs, int32_t *coeff,
+                         void *stream);
+
 /* ---- inverse transform + reconstruction (a17) ---------------------------
  * av1_inverse_transform_block (av1/common/idct.c:304-322) for a list of
  * blocks of one tx_size: dst (u8 when highbd = 0, then bit_depth must be 8;
@@ -224,6 +250,12 @@ int lavish_inv_txfm_add_batch(const int32_t *dqcoeff, int tx_size,
                               const LavishInvJob *jobs, int njobs, void *dst,
                               int dst_stride, int bit_depth, int highbd,
                               void *stream);
+/* The lossless TX_4X4 inverse (av1_highbd_iwht4x4_add, idct.c:34-40): per
+ * job the 16-coefficient WHT when eob > 1, the DC-only form when eob == 1,
+ * nothing when eob == 0; same job / destination conventions. */
+int lavish_iwht4x4_add_batch(const int32_t *dqcoeff, const LavishInvJob *jobs,
+                             int njobs, void *dst, int dst_stride,
+                             int bit_depth, int highbd, void *stream);
 
 /* ---- C4: fused TX-type RDO ----------------------------------------------
  * For every full tx_size block of (src - pred) (u16 planes, bit_depth 8/10/12)
@@ -526,9 +558,27 @@ LAVISH_FWD2D(32, 8)
 #undef LAVISH_FWD2D
 
 /* av1_lowbd_fwd_txfm (av1/common/av1_rtcd_defs.pl:355,
- * av1/encoder/hybrid_fwd_txfm.c:244) */
+ * av1/encoder/hybrid_fwd_txfm.c:244); a lossless TX_4X4 takes av1_fwht4x4 */
 void av1_lowbd_fwd_txfm_hip(const int16_t *src_diff, int32_t *coeff,
                             int diff_stride, LavishTxfmParam *txfm_param);
+/* lossless Walsh-Hadamard (av1/common/av1_rtcd_defs.pl:351,217-218;
+ * hybrid_fwd_txfm.c:24-76, av1_inv_txfm2d.c:20-107); tagged u16 dest */
+void av1_fwht4x4_hip(const int16_t *input, int32_t *output, int stride);
+void av1_highbd_iwht4x4_16_add_hip(const int32_t *input, uint8_t *dest,
+                                   int dest_stride, int bd);
+void av1_highbd_iwht4x4_1_add_hip(const int32_t *input, uint8_t *dest,
+                                  int dest_stride, int bd);
+/* BitDepthInfo of av1/common/blockd.h:952-960 */
+typedef struct LavishBitDepthInfo {
+  int bit_depth;
+  int use_highbitdepth_buf;
+} LavishBitDepthInfo;
+/* av1_quick_txfm (av1/encoder/hybrid_fwd_txfm.c:315-336, the TPL model's
+ * transform): aom_hadamard_{4x4..32x32} when use_hadamard, else the DCT_DCT
+ * forward transform of tx_size. */
+void av1_quick_txfm_hip(int use_hadamard, uint8_t tx_size,
+                        LavishBitDepthInfo bd_info, const int16_t *src_diff,
+                        int src_stride, int32_t *coeff);
 
 /* quantizers (aom_dsp/aom_dsp_rtcd_defs.pl:655-694,
  * av1/common/av1_rtcd_defs.pl:334-344,428) */
@@ -724,6 +774,23 @@ void aom_highbd_hadamard_32x32_hip(const int16_t *src_diff,
                                    ptrdiff_t src_stride, int32_t *coeff);
 int aom_satd_hip(const int32_t *coeff, int length);
 
+/* aom_dsp_rtcd_defs.pl:1256-1263,1278 (int16 "low precision" forms) */
+void aom_hadamard_lp_8x8_hip(const int16_t *src_diff, ptrdiff_t src_stride,
+                             int16_t *coeff);
+void aom_hadamard_lp_16x16_hip(const int16_t *src_diff, ptrdiff_t src_stride,
+                               int16_t *coeff);
+void aom_hadamard_lp_8x8_dual_hip(const int16_t *src_diff, ptrdiff_t src_stride,
+                                  int16_t *coeff);
+int aom_satd_lp_hip(const int16_t *coeff, int length);
+/* aom_dsp_rtcd_defs.pl:770,731 */
+uint64_t aom_sum_sse_2d_i16_hip(const int16_t *src, int src_stride, int width,
+                                int height, int *sum);
+void aom_get_blk_sse_sum_hip(const int16_t *data, int stride, int bw, int bh,
+                             int *x_sum, int64_t *x2_sum);
+
+/* av1/common/av1_rtcd_defs.pl:331 */
+int64_t av1_block_error_lp_hip(const int16_t *coeff, const int16_t *dqcoeff,
+                               intptr_t block_size);
 /* av1/common/av1_rtcd_defs.pl:328,423 */
 int64_t av1_block_error_hip(const int32_t *coeff, const int32_t *dqcoeff,
                             intptr_t block_size, int64_t *ssz);

@@ -161,6 +161,12 @@ uint64_t orc_sum_squares_2d_i16(const int16_t *src, int stride, int w, int h);
 void orc_hadamard(int n, const int16_t *src_diff, ptrdiff_t src_stride,
                   int32_t *coeff);
 int orc_satd(const int32_t *coeff, int length);
+/* oracle_lp.c: int16 forms, (sum, sse), lossless WHT */
+void orc_hadamard_lp(int n, const int16_t *src, ptrdiff_t st, int16_t *coeff);
+int orc_satd_lp(const int16_t *coeff, int length);
+int64_t orc_block_error_lp(const int16_t *coeff, const int16_t *dqcoeff, intptr_t n);
+void orc_sum_sse(const int16_t *src, int stride, int w, int h, int *sum, int64_t *sse);
+void orc_iwht4x4_add(const int32_t *in, uint16_t *dst, int stride, int eob, int bd);
 int64_t orc_block_error(const int32_t *coeff, const int32_t *dqcoeff,
                         intptr_t block_size, int64_t *ssz);
 int64_t orc_highbd_block_error(const int32_t *coeff, const int32_t *dqcoeff,

@@ -96,6 +96,12 @@ def _declare(L):
     L.orc_sum_squares_2d_i16.argtypes = [vp, i32, i32, i32]
     L.orc_hadamard.argtypes = [i32, vp, ctypes.c_ssize_t, vp]
     L.orc_satd.argtypes = [vp, i32]
+    L.orc_hadamard_lp.argtypes = [i32, vp, ctypes.c_ssize_t, vp]
+    L.orc_satd_lp.argtypes = [vp, i32]
+    L.orc_block_error_lp.argtypes = [vp, vp, ctypes.c_ssize_t]
+    L.orc_block_error_lp.restype = i64
+    L.orc_sum_sse.argtypes = [vp, i32, i32, i32, vp, vp]
+    L.orc_iwht4x4_add.argtypes = [vp, vp, i32, i32, i32]
     L.orc_block_error.restype = i64
     L.orc_block_error.argtypes = [vp, vp, ctypes.c_ssize_t, vp]
     L.orc_highbd_block_error.restype = i64
@@ -346,6 +352,41 @@ def hadamard(n, src, stride, highbd=False):
 
 def satd(coeff, length):
     return lib().orc_satd(P(coeff), length)
+
+
+def hadamard_lp(n, src, stride):
+    out = np.zeros(n * n, np.int16)
+    lib().orc_hadamard_lp(n, P(np.ascontiguousarray(src, np.int16)), stride, P(out))
+    return out
+
+
+def satd_lp(coeff, length):
+    return lib().orc_satd_lp(P(np.ascontiguousarray(coeff, np.int16)), length)
+
+
+def block_error_lp(coeff, dqcoeff, n):
+    return lib().orc_block_error_lp(P(np.ascontiguousarray(coeff, np.int16)),
+                                    P(np.ascontiguousarray(dqcoeff, np.int16)), n)
+
+
+def sum_sse(src, stride, w, h):
+    """(sum, sse) of an int16 block (aom_sum_sse_2d_i16 / aom_get_blk_sse_sum)."""
+    sm, ss = ctypes.c_int(0), ctypes.c_int64(0)
+    lib().orc_sum_sse(P(np.ascontiguousarray(src, np.int16)), stride, w, h, ctypes.byref(sm),
+                      ctypes.byref(ss))
+    return sm.value, ss.value
+
+
+def fwht4x4(block, stride):
+    out = np.zeros(16, np.int32)
+    lib().orc_fwht4x4(P(np.ascontiguousarray(block, np.int16)), P(out), stride)
+    return out
+
+
+def iwht4x4_add(coeff, dst, eob, bd):
+    dst = np.ascontiguousarray(dst, np.uint16).copy()
+    lib().orc_iwht4x4_add(P(np.ascontiguousarray(coeff, np.int32)), P(dst), dst.shape[1], eob, bd)
+    return dst
 
 
 def block_error(coeff, dqcoeff, n, bd=None):

@@ -1,0 +1,558 @@
+#!/usr/bin/env python3
+"""Golden fixtures produced by EXECUTING THE REFERENCE'S OWN C FUNCTION BODIES
+(test infrastructure; runs only in the dev container, where /root/reference
+exists).
+
+tests/golden/cinterp.py interprets the reference's source text (C semantics
+kept exactly, see its header).  This script drives the reference functions on
+inputs drawn the way the reference's own tests draw them (ACMRandom seeded
+0xbaba over gtest's LCG, test/acm_random.h + gtest.cc:378-381) and writes the
+inputs and the reference outputs as small npz fixtures:
+
+  fix_txfm.npz    av1_fwd_txfm2d_{WxH}_c (av1/encoder/av1_fwd_txfm2d.c:56-312)
+                  for every valid (tx_size, tx_type) (IsTxSizeTypeValid,
+                  test/av1_txfm_test.h:89-100): the all-(2^bd - 1) block and
+                  Rand16() % 2^bd blocks of AV1FwdTxfm2dMatchTest
+                  (test/av1_fwd_txfm2d_test.cc:258-275) plus signed residual
+                  blocks, bd 8 and 10; the whole W*H output buffer
+  fix_qparams.npz av1_build_quantizer (av1/encoder/av1_quantize.c:602-686)
+                  y rows for bd 8/10/12 x quant_sharpness {0, 3, -3}
+  fix_quant.npz   av1_quantize_fp{,_32x32,_64x64}_c, aom_quantize_b{,_32x32,
+                  _64x64}_c, av1_highbd_quantize_fp_c, aom_highbd_quantize_b
+                  {,_32x32,_64x64}_c (av1/encoder/av1_quantize.c:36-264,
+                  565-577; aom_dsp/quantize.c:108-169,261-320,399-432) x qindex
+                  {0, 32, 128, 255} x bd {8, 10} with av1_build_quantizer's
+                  tables and the DCT_DCT scan of av1_scan_orders
+                  (av1/common/scan.c)
+  fix_inv.npz     av1_inv_txfm2d_add_{WxH}_c (av1/common/av1_inv_txfm2d.c:
+                  234-484) for every valid (tx_size, tx_type) x bd {8, 10, 12}
+  fix_wht.npz     av1_fwht4x4_c, av1_highbd_iwht4x4_{16,1}_add_c (lossless)
+  fix_pixel.npz   sad / sad_skip / x4d (aom_dsp/sad.c), variance / sub-pixel
+                  variance (aom_dsp/variance.c), their highbd 10-bit forms,
+                  hadamard / satd (aom_dsp/avg.c), block_error
+                  (av1/encoder/rdopt.c:635-682), subtract (aom_dsp/subtract.c),
+                  sse (aom_dsp/sse.c), sum_squares (aom_dsp/sum_squares.c)
+
+Usage: python tests/golden/gen_fixtures.py [section ...]
+"""
+import os
+import sys
+import time
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
+import cinterp as C  # noqa: E402
+
+REF = os.environ.get("LAVISH_REFERENCE", "/root/reference")
+
+TX_NAMES = ["4x4", "8x8", "16x16", "32x32", "64x64", "4x8", "8x4", "8x16", "16x8", "16x32",
+            "32x16", "32x64", "64x32", "4x16", "16x4", "8x32", "32x8", "16x64", "64x16"]
+TX_W = [4, 8, 16, 32, 64, 4, 8, 8, 16, 16, 32, 32, 64, 4, 16, 8, 32, 16, 64]
+TX_H = [4, 8, 16, 32, 64, 8, 4, 16, 8, 32, 16, 64, 32, 16, 4, 32, 8, 64, 16]
+
+
+def max_eob(s):
+    if s in (17, 18):
+        return 512
+    if TX_W[s] == 64 or TX_H[s] == 64:
+        return 1024
+    return TX_W[s] * TX_H[s]
+
+
+def valid_types(s):
+    """IsTxSizeTypeValid (test/av1_txfm_test.h:89-100)."""
+    m = max(TX_W[s], TX_H[s])
+    if m == 64:
+        return [0]
+    if m == 32:
+        return [0, 9]
+    return list(range(16))
+
+
+class ACMRandom:
+    """test/acm_random.h over testing::internal::Random (gtest.cc:378-381)."""
+
+    def __init__(self, seed=0xbaba):
+        self.state = seed
+
+    def generate(self, rng):
+        self.state = (1103515245 * self.state + 12345) % (1 << 31)
+        return self.state % rng
+
+    def rand16(self):
+        return (self.generate(1 << 31) >> 15) & 0xFFFF
+
+    def rand8(self):
+        return (self.generate(1 << 31) >> 23) & 0xFF
+
+
+COMMON = ["aom/aom_integer.h", "aom_ports/mem.h", "aom_dsp/aom_dsp_common.h",
+          "aom_dsp/txfm_common.h", "av1/common/enums.h", "av1/common/common.h",
+          "av1/common/common_data.h", "av1/common/av1_txfm.h", "av1/common/av1_txfm.c"]
+
+
+def tu_txfm():
+    return C.TU(REF, COMMON + ["av1/encoder/av1_fwd_txfm1d.h", "av1/encoder/av1_fwd_txfm1d_cfg.h",
+                               "av1/encoder/av1_fwd_txfm1d.c", "av1/encoder/av1_fwd_txfm2d.c",
+                               "av1/common/av1_inv_txfm1d.h", "av1/common/av1_inv_txfm1d_cfg.h",
+                               "av1/common/av1_inv_txfm1d.c", "av1/common/av1_inv_txfm2d.c",
+                               "av1/encoder/hybrid_fwd_txfm.c"],
+                C.reference_defines(REF))
+
+
+def tu_quant():
+    return C.TU(REF, ["aom/aom_integer.h", "aom/aom_codec.h", "aom_ports/mem.h",
+                      "aom_dsp/aom_dsp_common.h", "aom_dsp/txfm_common.h", "av1/common/enums.h",
+                      "av1/common/common.h", "av1/common/quant_common.h",
+                      "av1/common/quant_common.c", "aom_dsp/quantize.h", "aom_dsp/quantize.c",
+                      "av1/encoder/av1_quantize.h", "av1/encoder/av1_quantize.c",
+                      "av1/common/entropymode.h", "av1/common/scan.h", "av1/common/scan.c"],
+                C.reference_defines(REF))
+
+
+def check_errors(tu, needed):
+    missing = [n for n in needed if not tu.has_func(n)]
+    if missing:
+        for e in tu.errors:
+            print("  parse:", e)
+        raise SystemExit("reference functions not parsed: %s" % missing)
+
+
+# ----------------------------------------------------------------------------
+# forward transforms
+# ----------------------------------------------------------------------------
+def fwd_inputs(s, rnd):
+    """(blocks[K, H, W] int16, bds[K]) for one (tx_size, tx_type)."""
+    W, H = TX_W[s], TX_H[s]
+    blocks, bds = [], []
+    for bd in (8, 10):
+        blocks.append(np.full((H, W), (1 << bd) - 1, np.int16))  # the test's first input
+        bds.append(bd)
+        for _ in range(2):  # AV1FwdTxfm2dMatchTest: Rand16() % (1 << bd)
+            blocks.append(np.array([rnd.rand16() % (1 << bd) for _ in range(W * H)],
+                                   np.int16).reshape(H, W))
+            bds.append(bd)
+        for _ in range(2):  # signed residuals src - pred in [-(2^bd - 1), 2^bd - 1]
+            blocks.append(np.array([(rnd.rand16() % (1 << (bd + 1))) - ((1 << bd) - 1)
+                                    for _ in range(W * H)], np.int16).reshape(H, W))
+            bds.append(bd)
+    return np.stack(blocks), np.array(bds, np.int32)
+
+
+def gen_txfm(tu):
+    check_errors(tu, ["av1_fwd_txfm2d_%s_c" % n for n in TX_NAMES])
+    rnd = ACMRandom()
+    out = {}
+    for s in range(19):
+        W, H = TX_W[s], TX_H[s]
+        fn = tu.func("av1_fwd_txfm2d_%s_c" % TX_NAMES[s])
+        t0 = time.time()
+        for t in valid_types(s):
+            blocks, bds = fwd_inputs(s, rnd)
+            res = np.zeros((len(blocks), W * H), np.int32)
+            for k, (blk, bd) in enumerate(zip(blocks, bds)):
+                # stride W + 3: the reference reads `stride`-spaced rows
+                padded = np.zeros((H, W + 3), np.int16)
+                padded[:, :W] = blk
+                inp = tu.buffer("int16_t", padded.reshape(-1).tolist())
+                o = tu.buffer("int32_t", [0x5A5A5A5A] * (W * H))  # stale words stay visible
+                fn(inp, o, W + 3, t, int(bd))
+                res[k] = o.buf
+            out["in_%d_%d" % (s, t)] = blocks
+            out["bd_%d_%d" % (s, t)] = bds
+            out["out_%d_%d" % (s, t)] = res
+        print("  fwd %-5s %2d types %.1fs" % (TX_NAMES[s], len(valid_types(s)), time.time() - t0))
+    np.savez_compressed(os.path.join(HERE, "fix_txfm.npz"), **out)
+
+
+# ----------------------------------------------------------------------------
+# quantizer tables and quantizers
+# ----------------------------------------------------------------------------
+QFIELDS = ["y_quant", "y_quant_shift", "y_quant_fp", "y_round_fp", "y_zbin", "y_round"]
+
+
+def build_quantizer(tu, bd, sharpness):
+    """av1_build_quantizer(bd, 0, 0, 0, 0, 0, &quants, &deq, sharpness): the
+    y rows, {field: int16[256, 8]}."""
+    quants = tu.struct_obj("QUANTS")
+    deq = tu.struct_obj("Dequants")
+    tu.func("av1_build_quantizer")(bd, 0, 0, 0, 0, 0, quants, deq, sharpness)
+    st = quants.ty
+    obj = quants.buf[0]
+    res = {f: np.array(obj.vals[st.index[f]], np.int16).reshape(256, 8) for f in QFIELDS}
+    dst = deq.ty
+    res["y_dequant_QTX"] = np.array(deq.buf[0].vals[dst.index["y_dequant_QTX"]],
+                                    np.int16).reshape(256, 8)
+    return res
+
+
+def gen_qparams(tu):
+    check_errors(tu, ["av1_build_quantizer"])
+    out = {}
+    for bd in (8, 10, 12):
+        for sh in (0, 3, -3):
+            for f, v in build_quantizer(tu, bd, sh).items():
+                out["%s_bd%d_sh%d" % (f, bd, sh)] = v
+    np.savez_compressed(os.path.join(HERE, "fix_qparams.npz"), **out)
+
+
+def dct_scan(tu, s):
+    """av1_scan_orders[tx_size][DCT_DCT] (scan, iscan) as int16 arrays."""
+    so = tu.global_value("av1_scan_orders")  # flat [TX_SIZES_ALL * TX_TYPES] SCAN_ORDER
+    st = so[0].st
+    e = so[s * 16 + 0]
+    n = max_eob(s)
+    sp = e.vals[st.index["scan"]]
+    ip = e.vals[st.index["iscan"]]
+    return (np.array(sp.buf[sp.off:sp.off + n], np.int16),
+            np.array(ip.buf[ip.off:ip.off + n], np.int16))
+
+
+QUANT_CASES = [  # (name, tx_size, log_scale, highbd, kind)
+    ("av1_quantize_fp_c", 0, 0, False, "fp"), ("av1_quantize_fp_c", 2, 0, False, "fp"),
+    ("av1_quantize_fp_32x32_c", 3, 1, False, "fp"), ("av1_quantize_fp_32x32_c", 9, 1, False, "fp"),
+    ("av1_quantize_fp_64x64_c", 4, 2, False, "fp"),
+    ("aom_quantize_b_c", 0, 0, False, "b"), ("aom_quantize_b_c", 2, 0, False, "b"),
+    ("aom_quantize_b_32x32_c", 3, 1, False, "b"), ("aom_quantize_b_64x64_c", 4, 2, False, "b"),
+    ("av1_highbd_quantize_fp_c", 0, 0, True, "fp"), ("av1_highbd_quantize_fp_c", 2, 0, True, "fp"),
+    ("av1_highbd_quantize_fp_c", 3, 1, True, "fp"), ("av1_highbd_quantize_fp_c", 4, 2, True, "fp"),
+    ("aom_highbd_quantize_b_c", 0, 0, True, "b"), ("aom_highbd_quantize_b_c", 2, 0, True, "b"),
+    ("aom_highbd_quantize_b_32x32_c", 3, 1, True, "b"),
+    ("aom_highbd_quantize_b_64x64_c", 4, 2, True, "b"),
+]
+
+
+def quant_inputs(s, bd, rnd, fwd):
+    """Coefficient blocks: transforms of random residuals (the fix_txfm
+    outputs of that size), a random span, and the QuantizeTest extremes
+    (DC-only, all -8191 style fills scaled to the bit depth)."""
+    n = max_eob(s)
+    lim = 1 << (bd + 7)
+    blocks = []
+    for k in range(2):
+        blocks.append(fwd[k % len(fwd)][:n].astype(np.int64))
+    blocks.append(np.array([(rnd.rand16() * 65536 + rnd.rand16()) % (2 * lim) - lim
+                            for _ in range(n)], np.int64) // (1 + (np.arange(n) % 7)))
+    # decaying with frequency (smooth content): eobs land mid-block
+    blocks.append(np.array([((rnd.rand16() - 32768) * (lim >> 6)) // (32768 * (1 + (i % 32) + i // 32))
+                            for i in range(n)], np.int64))
+    dc = np.zeros(n, np.int64)
+    dc[0] = lim - 1
+    blocks.append(dc)
+    blocks.append(np.full(n, -(lim // 4) - 1, np.int64))
+    return np.stack(blocks).astype(np.int32)
+
+
+def gen_quant(tu, txfm_fix):
+    names = sorted({c[0] for c in QUANT_CASES})
+    check_errors(tu, names)
+    rnd = ACMRandom()
+    out = {}
+    for bd in (8, 10):
+        qrows = build_quantizer(tu, bd, 0)
+        for ci, (name, s, ls, hb, kind) in enumerate(QUANT_CASES):
+            if hb != (bd > 8):
+                continue
+            scan, iscan = dct_scan(tu, s)
+            n = max_eob(s)
+            fwd = txfm_fix["out_%d_0" % s]
+            fwd = [f for f, b in zip(fwd, txfm_fix["bd_%d_0" % s]) if b == bd]
+            coeffs = quant_inputs(s, bd, rnd, fwd)
+            for q in (0, 32, 128, 255):
+                if kind == "fp":
+                    z, r, qu, qs = (qrows["y_zbin"][q], qrows["y_round_fp"][q],
+                                    qrows["y_quant_fp"][q], qrows["y_quant_shift"][q])
+                else:
+                    z, r, qu, qs = (qrows["y_zbin"][q], qrows["y_round"][q],
+                                    qrows["y_quant"][q], qrows["y_quant_shift"][q])
+                dq = qrows["y_dequant_QTX"][q]
+                qc = np.zeros((len(coeffs), n), np.int32)
+                dqc = np.zeros((len(coeffs), n), np.int32)
+                eob = np.zeros(len(coeffs), np.int32)
+                for k, c in enumerate(coeffs):
+                    cp = tu.buffer("int32_t", c.tolist())
+                    qp = tu.buffer("int32_t", [77] * n)
+                    dp = tu.buffer("int32_t", [77] * n)
+                    ep = tu.buffer("uint16_t", 1)
+                    args = [cp, n, tu.buffer("int16_t", z.tolist()), tu.buffer("int16_t", r.tolist()),
+                            tu.buffer("int16_t", qu.tolist()), tu.buffer("int16_t", qs.tolist()),
+                            qp, dp, tu.buffer("int16_t", dq.tolist()), ep,
+                            tu.buffer("int16_t", scan.tolist()), tu.buffer("int16_t", iscan.tolist())]
+                    if name == "av1_highbd_quantize_fp_c":
+                        args.append(ls)
+                    tu.func(name)(*args)
+                    qc[k], dqc[k], eob[k] = qp.buf, dp.buf, ep.buf[0]
+                key = "%d_%d_q%d" % (ci, bd, q)
+                out["coeff_" + key] = coeffs
+                out["qcoeff_" + key] = qc
+                out["dqcoeff_" + key] = dqc
+                out["eob_" + key] = eob
+        print("  quant bd %d done" % bd)
+    out["cases"] = np.array([[s, ls, int(hb), int(kind == "b")] for _, s, ls, hb, kind in QUANT_CASES],
+                            np.int32)
+    out["case_names"] = np.array([c[0] for c in QUANT_CASES])
+    np.savez_compressed(os.path.join(HERE, "fix_quant.npz"), **out)
+
+
+# ----------------------------------------------------------------------------
+# inverse transforms
+# ----------------------------------------------------------------------------
+def gen_inv(tu, txfm_fix):
+    check_errors(tu, ["av1_inv_txfm2d_add_%s_c" % n for n in TX_NAMES])
+    rnd = ACMRandom(0xbaba + 1)
+    out = {}
+    for s in range(19):
+        W, H = TX_W[s], TX_H[s]
+        n = max_eob(s)
+        fn = tu.func("av1_inv_txfm2d_add_%s_c" % TX_NAMES[s])
+        t0 = time.time()
+        for t in valid_types(s):
+            fwd = txfm_fix["out_%d_%d" % (s, t)]
+            cases_in, cases_dst, cases_out, cases_bd = [], [], [], []
+            for bd in (8, 10, 12):
+                srcs = []
+                # a forward transform of a residual of this bit depth (dense),
+                # the same coarsely quantised (sparse), and large sparse values
+                # that exercise the per-stage clamps
+                f = fwd[3 if bd == 8 else 8][:n].astype(np.int64)
+                srcs.append(f << max(0, bd - 10))
+                srcs.append((f // 64) * 64)
+                sp = np.zeros(n, np.int64)
+                for _ in range(6):
+                    sp[rnd.generate(n)] = (rnd.rand16() - 32768) * (1 << (bd - 6))
+                srcs.append(sp)
+                for c in srcs:
+                    c = np.clip(c, -(1 << (bd + 8)), (1 << (bd + 8)) - 1).astype(np.int32)
+                    dst = np.array([rnd.rand16() % (1 << bd) for _ in range(H * (W + 5))],
+                                   np.uint16).reshape(H, W + 5)
+                    ip = tu.buffer("int32_t", c.tolist())
+                    op = tu.buffer("uint16_t", dst.reshape(-1).tolist())
+                    fn(ip, op, W + 5, t, bd)
+                    cases_in.append(c)
+                    cases_dst.append(dst)
+                    cases_out.append(np.array(op.buf, np.uint16).reshape(H, W + 5))
+                    cases_bd.append(bd)
+            out["in_%d_%d" % (s, t)] = np.stack(cases_in)
+            out["dst_%d_%d" % (s, t)] = np.stack(cases_dst)
+            out["out_%d_%d" % (s, t)] = np.stack(cases_out)
+            out["bd_%d_%d" % (s, t)] = np.array(cases_bd, np.int32)
+        print("  inv %-5s %2d types %.1fs" % (TX_NAMES[s], len(valid_types(s)), time.time() - t0))
+    np.savez_compressed(os.path.join(HERE, "fix_inv.npz"), **out)
+
+
+# ----------------------------------------------------------------------------
+# pixel-domain kernels
+# ----------------------------------------------------------------------------
+# @encoder_block_sizes (aom_dsp/aom_dsp_rtcd_defs.pl:42-58)
+BLOCK_SIZES = [(128, 128), (128, 64), (64, 128), (64, 64), (64, 32), (32, 64), (32, 32), (32, 16),
+               (16, 32), (16, 16), (16, 8), (8, 16), (8, 8), (8, 4), (4, 8), (4, 4), (4, 16),
+               (16, 4), (8, 32), (32, 8), (16, 64), (64, 16)]
+SUBPEL_OFFSETS = [(0, 0), (3, 0), (0, 5), (4, 4), (7, 2)]
+
+
+def tu_pixel():
+    return C.TU(REF, ["aom/aom_integer.h", "aom_ports/mem.h", "aom_dsp/aom_dsp_common.h",
+                      "aom_dsp/aom_filter.h", "aom_dsp/blend.h", "aom_dsp/variance.h",
+                      "aom_dsp/sad.c", "aom_dsp/variance.c", "aom_dsp/avg.c", "aom_dsp/sse.c",
+                      "aom_dsp/subtract.c", "aom_dsp/sum_squares.c", "aom_dsp/blk_sse_sum.c",
+                      "av1/encoder/rdopt.c"],
+                C.reference_defines(REF))
+
+
+def _pix(rnd, n, bd):
+    """Pixels: mostly uniform, one in eight near the extremes (saturation)."""
+    mx = (1 << bd) - 1
+    out = []
+    for _ in range(n):
+        r = rnd.rand16()
+        if r % 8 == 0:
+            out.append(mx - (r >> 12) if r & 0x100 else (r >> 12))
+        else:
+            out.append(r % (mx + 1))
+    return out
+
+
+def gen_pixel(tu):
+    rnd = ACMRandom(0xbaba + 2)
+    out = {}
+    u32 = lambda v: v & 0xFFFFFFFF
+    for (W, H) in BLOCK_SIZES:
+        key = "%dx%d" % (W, H)
+        t0 = time.time()
+        ss, rs = W + 9, 2 * W + 17
+        for bd in (8, 10):
+            hb = bd > 8
+            et = "uint16_t" if hb else "uint8_t"
+            src = np.array(_pix(rnd, (H + 1) * ss, bd)).reshape(H + 1, ss)
+            ref = np.array(_pix(rnd, (H + 1) * rs, bd)).reshape(H + 1, rs)
+            sp = tu.buffer(et, src.reshape(-1).tolist())
+            rp = tu.buffer(et, ref.reshape(-1).tolist())
+            a = tu.tagged(sp) if hb else sp
+            b = tu.tagged(rp) if hb else rp
+            pre = "aom_highbd_" if hb else "aom_"
+            k = "%s_bd%d" % (key, bd)
+            out["src_" + k] = src.astype(np.uint16)
+            out["ref_" + k] = ref.astype(np.uint16)
+            out["sad_" + k] = np.array([u32(tu.func("%ssad%dx%d_c" % (pre, W, H))(a, ss, b, rs))])
+            out["sadskip_" + k] = np.array([u32(tu.func("%ssad_skip_%dx%d_c" % (pre, W, H))(
+                a, ss, b, rs))])
+            # x4d: the 4 candidates at offsets 0, 1, 3, W + 2 of the reference row
+            refs = [C.Pointer(rp.buf, o, rp.ty) for o in (0, 1, 3, W + 2)]
+            arr = C.Pointer([tu.tagged(r) if hb else r for r in refs], 0, C.Ptr(C.UCHAR))
+            o4 = tu.buffer("uint32_t", 4)
+            tu.func("%ssad%dx%dx4d_c" % (pre, W, H))(a, ss, arr, rs, o4)
+            out["sadx4d_" + k] = np.array(o4.buf, np.int64)
+            vpre = "aom_highbd_10_" if hb else "aom_"
+            sse = tu.buffer("uint32_t", 1)
+            v = tu.func("%svariance%dx%d_c" % (vpre, W, H))(a, ss, b, rs, sse)
+            out["var_" + k] = np.array([u32(v), sse.buf[0]], np.int64)
+            sv = []
+            for xo, yo in SUBPEL_OFFSETS:
+                sse = tu.buffer("uint32_t", 1)
+                v = tu.func("%ssub_pixel_variance%dx%d_c" % (vpre, W, H))(a, ss, xo, yo, b, rs, sse)
+                sv.append([u32(v), sse.buf[0]])
+            out["subvar_" + k] = np.array(sv, np.int64)
+        print("  pixel %-7s %.1fs" % (key, time.time() - t0))
+    # hadamard / satd on residuals in [-(2^bd - 1), 2^bd - 1]
+    for n in (4, 8, 16, 32):
+        for bd in (8, 10):
+            st = n + 3
+            res = [(rnd.rand16() % (1 << (bd + 1))) - ((1 << bd) - 1) for _ in range(n * st)]
+            rp = tu.buffer("int16_t", res)
+            k = "%d_bd%d" % (n, bd)
+            out["hres_" + k] = np.array(res, np.int16).reshape(n, st)
+            if bd == 8:
+                co = tu.buffer("int32_t", n * n)
+                tu.func("aom_hadamard_%dx%d_c" % (n, n))(rp, st, co)
+                out["had_" + k] = np.array(co.buf, np.int32)
+                out["satd_" + k] = np.array([tu.func("aom_satd_c")(co, n * n)])
+                if n in (8, 16):
+                    cl = tu.buffer("int16_t", n * n)
+                    tu.func("aom_hadamard_lp_%dx%d_c" % (n, n))(rp, st, cl)
+                    out["hadlp_" + k] = np.array(cl.buf, np.int16)
+                    out["satdlp_" + k] = np.array([tu.func("aom_satd_lp_c")(cl, n * n)])
+            elif n >= 8:
+                co = tu.buffer("int32_t", n * n)
+                tu.func("aom_highbd_hadamard_%dx%d_c" % (n, n))(rp, st, co)
+                out["had_" + k] = np.array(co.buf, np.int32)
+                out["satd_" + k] = np.array([tu.func("aom_satd_c")(co, n * n)])
+    # block error (rdopt.c:635-682), lp and highbd
+    for n in (16, 64, 256, 1024, 4096):
+        c = [(rnd.rand16() - 32768) * 4 + (rnd.rand16() & 3) for _ in range(n)]
+        d = [x + ((rnd.rand16() % 2001) - 1000) for x in c]
+        cp, dp = tu.buffer("int32_t", c), tu.buffer("int32_t", d)
+        ssz = tu.buffer("int64_t", 1)
+        e = tu.func("av1_block_error_c")(cp, dp, n, ssz)
+        out["be_c_%d" % n], out["be_d_%d" % n] = np.array(c, np.int32), np.array(d, np.int32)
+        out["be_%d" % n] = np.array([e, ssz.buf[0]], np.int64)
+        for bd in (10, 12):
+            ssz = tu.buffer("int64_t", 1)
+            e = tu.func("av1_highbd_block_error_c")(cp, dp, n, ssz, bd)
+            out["behb_%d_bd%d" % (n, bd)] = np.array([e, ssz.buf[0]], np.int64)
+        cl = [(x >> 3) for x in c]
+        dl = [max(-32768, min(32767, x + ((rnd.rand16() % 201) - 100))) for x in cl]
+        out["belp_c_%d" % n], out["belp_d_%d" % n] = np.array(cl, np.int16), np.array(dl, np.int16)
+        out["belp_%d" % n] = np.array([tu.func("av1_block_error_lp_c")(
+            tu.buffer("int16_t", cl), tu.buffer("int16_t", dl), n)], np.int64)
+    # subtract / sse / sum_squares / sum_sse / blk_sse_sum over odd shapes
+    for (w, h) in ((4, 4), (8, 4), (16, 16), (7, 5), (64, 64), (32, 8), (128, 128)):
+        for bd in (8, 10):
+            hb = bd > 8
+            et = "uint16_t" if hb else "uint8_t"
+            sst, pst, dst = w + 5, w + 2, w + 7
+            src = np.array(_pix(rnd, h * sst, bd)).reshape(h, sst)
+            prd = np.array(_pix(rnd, h * pst, bd)).reshape(h, pst)
+            sp, pp = tu.buffer(et, src.reshape(-1).tolist()), tu.buffer(et, prd.reshape(-1).tolist())
+            a, b = (tu.tagged(sp), tu.tagged(pp)) if hb else (sp, pp)
+            k = "%dx%d_bd%d" % (w, h, bd)
+            out["s_src_" + k], out["s_pred_" + k] = src.astype(np.uint16), prd.astype(np.uint16)
+            dp = tu.buffer("int16_t", [0x7777] * (h * dst))
+            tu.func("aom_highbd_subtract_block_c" if hb else "aom_subtract_block_c")(
+                h, w, dp, dst, a, sst, b, pst)
+            out["sub_" + k] = np.array(dp.buf, np.int16).reshape(h, dst)
+            out["sse_" + k] = np.array([tu.func("aom_highbd_sse_c" if hb else "aom_sse_c")(
+                a, sst, b, pst, w, h)], np.int64)
+            res = np.array(dp.buf, np.int64)
+            rp = tu.buffer("int16_t", res.tolist())
+            out["sumsq_" + k] = np.array([tu.func("aom_sum_squares_2d_i16_c")(rp, dst, w, h)],
+                                         np.uint64)
+            sm = tu.buffer("int", 1)
+            v = tu.func("aom_sum_sse_2d_i16_c")(rp, dst, w, h, sm)
+            out["sumsse_" + k] = np.array([v, sm.buf[0]], np.int64)
+            xs, x2 = tu.buffer("int", 1), tu.buffer("int64_t", 1)
+            tu.func("aom_get_blk_sse_sum_c")(rp, dst, w, h, xs, x2)
+            out["blksse_" + k] = np.array([xs.buf[0], x2.buf[0]], np.int64)
+    np.savez_compressed(os.path.join(HERE, "fix_pixel.npz"), **out)
+
+
+def gen_wht(tu):
+    """av1_fwht4x4_c (hybrid_fwd_txfm.c:24-76) and av1_highbd_iwht4x4_{16,1}
+    _add_c (av1_inv_txfm2d.c:20-107) on lossless residuals / coefficients."""
+    check_errors(tu, ["av1_fwht4x4_c", "av1_highbd_iwht4x4_16_add_c", "av1_highbd_iwht4x4_1_add_c"])
+    rnd = ACMRandom(0xbaba + 3)
+    out = {}
+    ins, fo = [], []
+    for k in range(24):
+        bd = (8, 10, 12)[k % 3]
+        m = (1 << bd) - 1
+        blk = [((rnd.rand16() % (2 * m + 1)) - m) if k % 4 else (m if (i & 1) else -m)
+               for i in range(4 * 7)]
+        ip = tu.buffer("int16_t", blk)
+        op = tu.buffer("int32_t", 16)
+        tu.func("av1_fwht4x4_c")(ip, op, 7)
+        ins.append(np.array(blk, np.int16).reshape(4, 7))
+        fo.append(np.array(op.buf, np.int32))
+    out["fwht_in"], out["fwht_out"] = np.stack(ins), np.stack(fo)
+    cin, dst0, dst1, bds, o16, o1 = [], [], [], [], [], []
+    for k in range(24):
+        bd = (8, 10, 12)[k % 3]
+        c = fo[k].astype(np.int64) if k % 2 else np.array(
+            [(rnd.rand16() - 32768) << (bd - 8) for _ in range(16)], np.int64)
+        c = c.astype(np.int32)
+        d = np.array([rnd.rand16() % (1 << bd) for _ in range(4 * 6)], np.uint16).reshape(4, 6)
+        res = []
+        for fn in ("av1_highbd_iwht4x4_16_add_c", "av1_highbd_iwht4x4_1_add_c"):
+            dp = tu.buffer("uint16_t", d.reshape(-1).tolist())
+            tu.func(fn)(tu.buffer("int32_t", c.tolist()), tu.tagged(dp), 6, bd)
+            res.append(np.array(dp.buf, np.uint16).reshape(4, 6))
+        cin.append(c)
+        dst0.append(d)
+        bds.append(bd)
+        o16.append(res[0])
+        o1.append(res[1])
+    out["iwht_in"], out["iwht_dst"], out["iwht_bd"] = np.stack(cin), np.stack(dst0), np.array(bds)
+    out["iwht16_out"], out["iwht1_out"] = np.stack(o16), np.stack(o1)
+    np.savez_compressed(os.path.join(HERE, "fix_wht.npz"), **out)
+
+
+def main(argv):
+    sections = argv or ["txfm", "qparams", "quant", "inv", "pixel", "wht"]
+    t0 = time.time()
+    ttx = None
+    if "txfm" in sections or "inv" in sections or "wht" in sections:
+        ttx = tu_txfm()
+    if "txfm" in sections:
+        gen_txfm(ttx)
+    tq = None
+    if "qparams" in sections or "quant" in sections:
+        tq = tu_quant()
+    if "qparams" in sections:
+        gen_qparams(tq)
+    txfm_fix = None
+    if "quant" in sections or "inv" in sections:
+        txfm_fix = dict(np.load(os.path.join(HERE, "fix_txfm.npz")))
+    if "quant" in sections:
+        gen_quant(tq, txfm_fix)
+    if "inv" in sections:
+        gen_inv(ttx, txfm_fix)
+    if "pixel" in sections:
+        gen_pixel(tu_pixel())
+    if "wht" in sections:
+        gen_wht(ttx)
+    print("done in %.0fs" % (time.time() - t0))
+
+
+if __name__ == "__main__":
+    main(sys.argv[1:])

@@ -92,3 +92,25 @@ def test_product_does_not_reference_oracle():
             if f.endswith((".hip", ".h", ".py", ".cpp")) or f == "Makefile":
                 txt = open(os.path.join(dirpath, f), errors="ignore").read()
                 assert "oracle" not in txt.replace("oracle/ never", ""), os.path.join(dirpath, f)
+
+
+@pytest.mark.parametrize("bd", [8, 10, 12])
+@pytest.mark.parametrize("sharp", [0, 3, -3])
+def test_quant_params_match_reference_execution(bd, sharp):
+    """lavish_build_quant_params against av1_build_quantizer as the
+    reference's own code computes it (tests/golden/fix_qparams.npz, made by
+    executing av1/encoder/av1_quantize.c:602-686), every qindex."""
+    import lavish_dsp
+    F = dict(np.load(os.path.join(ROOT, "tests", "golden", "fix_qparams.npz")))
+    for q in range(256):
+        fp = lavish_dsp.build_quant_params(bd, q, lavish_dsp.QUANT_FP, sharp).as_dict()
+        b = lavish_dsp.build_quant_params(bd, q, lavish_dsp.QUANT_B, sharp).as_dict()
+        row = lambda f: F["%s_bd%d_sh%d" % (f, bd, sharp)][q, :2]
+        np.testing.assert_array_equal(fp["round"], row("y_round_fp"))
+        np.testing.assert_array_equal(fp["quant"], row("y_quant_fp"))
+        np.testing.assert_array_equal(b["round"], row("y_round"))
+        np.testing.assert_array_equal(b["quant"], row("y_quant"))
+        for d in (fp, b):
+            np.testing.assert_array_equal(d["zbin"], row("y_zbin"))
+            np.testing.assert_array_equal(d["quant_shift"], row("y_quant_shift"))
+            np.testing.assert_array_equal(d["dequant"], row("y_dequant_QTX"))

@@ -1,0 +1,198 @@
+"""The oracle (oracle/*.c) against fixtures produced by executing the
+reference's own C function bodies (tests/golden/gen_fixtures.py through
+tests/golden/cinterp.py): forward 2-D transforms of every valid (size, type),
+av1_build_quantizer's tables, the fp / b quantizers (lowbd and highbd, every
+log_scale), and the inverse 2-D transforms + add at bd 8 / 10 / 12 -- all
+bit-exact.  This is what pins the 2-D composition (shifts, flips, rect
+scaling, 64-point zero + repack), the quantizers and the inverse to the
+reference rather than to a reading of it."""
+import os
+
+import numpy as np
+import pytest
+
+import _oracle as O
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+GOLD = os.path.join(HERE, "golden")
+
+
+def _load(name):
+    return dict(np.load(os.path.join(GOLD, name)))
+
+
+@pytest.fixture(scope="module")
+def FT():
+    return _load("fix_txfm.npz")
+
+
+@pytest.fixture(scope="module")
+def FQ():
+    return _load("fix_quant.npz")
+
+
+@pytest.fixture(scope="module")
+def FI():
+    return _load("fix_inv.npz")
+
+
+def _pairs():
+    return [(s, t) for s in range(19) for t in range(16) if O.type_valid(s, t)]
+
+
+def test_fixture_coverage(FT, FI):
+    """Every valid (tx_size, tx_type) -- 159 combinations -- is present."""
+    p = _pairs()
+    assert len(p) == 159
+    for s, t in p:
+        assert "out_%d_%d" % (s, t) in FT and "out_%d_%d" % (s, t) in FI
+
+
+@pytest.mark.parametrize("s", range(19))
+def test_fwd_txfm2d_vs_reference(FT, s):
+    for t in range(16):
+        if not O.type_valid(s, t):
+            continue
+        ins, outs, bds = FT["in_%d_%d" % (s, t)], FT["out_%d_%d" % (s, t)], FT["bd_%d_%d" % (s, t)]
+        for blk, exp, bd in zip(ins, outs, bds):
+            got = O.fwd_txfm2d(blk, t, s, int(bd))
+            np.testing.assert_array_equal(got, exp, err_msg="size %d type %d bd %d" % (s, t, bd))
+
+
+@pytest.mark.parametrize("bd", [8, 10, 12])
+@pytest.mark.parametrize("sharp", [0, 3, -3])
+def test_build_quantizer_vs_reference(bd, sharp):
+    F = _load("fix_qparams.npz")
+    for q in range(256):
+        a = O.quant_arrays(O.build_quant(bd, q, sharp))
+        for mine, ref in (("quant", "y_quant"), ("quant_shift", "y_quant_shift"),
+                          ("zbin", "y_zbin"), ("round", "y_round"), ("quant_fp", "y_quant_fp"),
+                          ("round_fp", "y_round_fp"), ("dequant", "y_dequant_QTX")):
+            np.testing.assert_array_equal(a[mine], F["%s_bd%d_sh%d" % (ref, bd, sharp)][q, :2],
+                                          err_msg="%s q %d" % (mine, q))
+
+
+def quant_cases(FQ):
+    for ci, (s, ls, hb, isb) in enumerate(FQ["cases"]):
+        for bd in ((10,) if hb else (8,)):
+            for q in (0, 32, 128, 255):
+                yield ci, int(s), int(ls), bool(hb), bool(isb), bd, q
+
+
+def test_quantizers_vs_reference(FQ):
+    n_checked = 0
+    for ci, s, ls, hb, isb, bd, q in quant_cases(FQ):
+        key = "%d_%d_q%d" % (ci, bd, q)
+        qq = O.build_quant(bd, q)
+        n = O.max_eob(s)
+        for k, c in enumerate(FQ["coeff_" + key]):
+            qc, dq, eob = O.quantize("b" if isb else "fp", c, n, qq, O.scan(s, 0), O.iscan(s, 0),
+                                     ls, highbd=hb)
+            msg = "%s size %d q %d block %d" % (FQ["case_names"][ci], s, q, k)
+            np.testing.assert_array_equal(qc, FQ["qcoeff_" + key][k], err_msg=msg)
+            np.testing.assert_array_equal(dq, FQ["dqcoeff_" + key][k], err_msg=msg)
+            assert eob == FQ["eob_" + key][k], msg
+            n_checked += 1
+    assert n_checked > 300
+
+
+@pytest.mark.parametrize("s", range(19))
+def test_inv_txfm2d_add_vs_reference(FI, s):
+    W = O.TX_W[s]
+    for t in range(16):
+        if not O.type_valid(s, t):
+            continue
+        key = "%d_%d" % (s, t)
+        for c, dst, exp, bd in zip(FI["in_" + key], FI["dst_" + key], FI["out_" + key],
+                                   FI["bd_" + key]):
+            got = O.inv_txfm2d_add(c, dst, t, s, int(bd))
+            np.testing.assert_array_equal(got, exp, err_msg="size %d type %d bd %d" % (s, t, bd))
+            assert W + 5 == dst.shape[1]
+
+
+# ---------------------------------------------------------------- pixel --
+BLOCK_SIZES = [(128, 128), (128, 64), (64, 128), (64, 64), (64, 32), (32, 64), (32, 32), (32, 16),
+               (16, 32), (16, 16), (16, 8), (8, 16), (8, 8), (8, 4), (4, 8), (4, 4), (4, 16),
+               (16, 4), (8, 32), (32, 8), (16, 64), (64, 16)]
+SUBPEL_OFFSETS = [(0, 0), (3, 0), (0, 5), (4, 4), (7, 2)]
+
+
+@pytest.fixture(scope="module")
+def FP():
+    return _load("fix_pixel.npz")
+
+
+def pixel_planes(FP, W, H, bd):
+    k = "%dx%d_bd%d" % (W, H, bd)
+    dt = np.uint8 if bd == 8 else np.uint16
+    return k, FP["src_" + k].astype(dt), FP["ref_" + k].astype(dt)
+
+
+@pytest.mark.parametrize("W,H", BLOCK_SIZES)
+@pytest.mark.parametrize("bd", [8, 10])
+def test_sad_variance_vs_reference(FP, W, H, bd):
+    k, a, b = pixel_planes(FP, W, H, bd)
+    hb = bd > 8
+    ss, rs = a.shape[1], b.shape[1]
+    assert O.sad(a, ss, b, rs, W, H, highbd=hb) == FP["sad_" + k][0]
+    assert O.sad(a, ss, b, rs, W, H, highbd=hb, skip=True) == FP["sadskip_" + k][0]
+    flat = b.reshape(-1)
+    got4 = [O.sad(a, ss, flat[o:], rs, W, H, highbd=hb) for o in (0, 1, 3, W + 2)]
+    np.testing.assert_array_equal(got4, FP["sadx4d_" + k])
+    assert list(O.variance(a, ss, b, rs, W, H, bd, hb)) == list(FP["var_" + k])
+    got = [O.sub_pixel_variance(a, ss, xo, yo, b, rs, W, H, bd, hb) for xo, yo in SUBPEL_OFFSETS]
+    np.testing.assert_array_equal(np.array(got, np.int64), FP["subvar_" + k])
+
+
+def test_hadamard_satd_vs_reference(FP):
+    for n in (4, 8, 16, 32):
+        for bd in (8, 10):
+            k = "%d_bd%d" % (n, bd)
+            if "had_" + k not in FP:
+                continue
+            res = FP["hres_" + k]
+            got = O.hadamard(n, res, res.shape[1], highbd=bd > 8)
+            np.testing.assert_array_equal(got, FP["had_" + k], err_msg=k)
+            assert O.satd(got, n * n) == FP["satd_" + k][0]
+            if "hadlp_" + k in FP:
+                lp = O.hadamard_lp(n, res, res.shape[1])
+                np.testing.assert_array_equal(lp, FP["hadlp_" + k], err_msg=k)
+                assert O.satd_lp(lp, n * n) == FP["satdlp_" + k][0]
+
+
+def test_block_error_vs_reference(FP):
+    for n in (16, 64, 256, 1024, 4096):
+        c, d = FP["be_c_%d" % n], FP["be_d_%d" % n]
+        assert list(O.block_error(c, d, n)) == list(FP["be_%d" % n])
+        for bd in (10, 12):
+            assert list(O.block_error(c, d, n, bd)) == list(FP["behb_%d_bd%d" % (n, bd)])
+        assert O.block_error_lp(FP["belp_c_%d" % n], FP["belp_d_%d" % n], n) == FP["belp_%d" % n][0]
+
+
+def test_subtract_sse_sums_vs_reference(FP):
+    for (w, h) in ((4, 4), (8, 4), (16, 16), (7, 5), (64, 64), (32, 8), (128, 128)):
+        for bd in (8, 10):
+            k = "%dx%d_bd%d" % (w, h, bd)
+            dt = np.uint8 if bd == 8 else np.uint16
+            src, prd = FP["s_src_" + k].astype(dt), FP["s_pred_" + k].astype(dt)
+            exp = FP["sub_" + k]
+            diff = np.full(exp.shape, 0x7777, np.int16)
+            O.subtract_block(h, w, diff, diff.shape[1], src, src.shape[1], prd, prd.shape[1],
+                             highbd=bd > 8)
+            np.testing.assert_array_equal(diff, exp, err_msg=k)
+            assert O.sse(src, src.shape[1], prd, prd.shape[1], w, h, highbd=bd > 8) == \
+                FP["sse_" + k][0]
+            assert O.sum_squares_2d_i16(exp, exp.shape[1], w, h) == FP["sumsq_" + k][0]
+            sm, ss = O.sum_sse(exp, exp.shape[1], w, h)
+            assert [ss, sm] == list(FP["sumsse_" + k])
+            assert [sm, ss] == list(FP["blksse_" + k])
+
+
+def test_wht_vs_reference():
+    F = _load("fix_wht.npz")
+    for blk, exp in zip(F["fwht_in"], F["fwht_out"]):
+        np.testing.assert_array_equal(O.fwht4x4(blk, blk.shape[1]), exp)
+    for c, d, bd, e16, e1 in zip(F["iwht_in"], F["iwht_dst"], F["iwht_bd"], F["iwht16_out"],
+                                 F["iwht1_out"]):
+        np.testing.assert_array_equal(O.iwht4x4_add(c, d, 16, int(bd)), e16)
+        np.testing.assert_array_equal(O.iwht4x4_add(c, d, 1, int(bd)), e1)
