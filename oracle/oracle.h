@@ -172,7 +172,15 @@ int64_t orc_block_error(const int32_t *coeff, const int32_t *dqcoeff,
 int64_t orc_highbd_block_error(const int32_t *coeff, const int32_t *dqcoeff,
                                intptr_t block_size, int64_t *ssz, int bd);
 
-/* ---- C3: DIAMOND full-pixel motion search (oracle_mcomp.c) ---- */
+/* ---- C3: full-pixel motion search (oracle_mcomp.c) ---- */
+/* MV_COST_PARAMS (av1/encoder/mcomp.h:40-50): mvcost[k] point at the centre
+ * entry of MV_VALS-entry tables (indices -MV_MAX..MV_MAX). */
+typedef struct OrcMvCost {
+  int mv_cost_type; /* MV_COST_TYPE: 0 ENTROPY 1 L1_LOWRES 2 L1_MIDRES 3 L1_HDRES 4 NONE */
+  int sad_per_bit, error_per_bit;
+  const int32_t *mvjcost;
+  const int32_t *mvcost[2];
+} OrcMvCost;
 typedef struct OrcMsParams {
   const uint8_t *src; /* block origin */
   int src_stride;
@@ -181,11 +189,18 @@ typedef struct OrcMsParams {
   int w, h;
   int col_min, col_max, row_min, row_max; /* FullMvLimits */
   int ref_mv_row, ref_mv_col;             /* MV (1/8 pel) for the mv cost */
-  int mv_cost_type; /* MV_COST_TYPE: 1 L1_LOWRES 2 L1_MIDRES 3 L1_HDRES 4 NONE */
+  int mv_cost_type; /* MV_COST_TYPE */
   int skip_sad;     /* use_downsampled_sad: sdf = aom_sad_skip */
+  const OrcMvCost *cost; /* tables for MV_COST_ENTROPY (NULL otherwise) */
 } OrcMsParams;
-/* av1_full_pixel_search with search_method DIAMOND (no mesh): returns the
- * var cost, writes the best FULLPEL_MV and the number of diamond steps. */
+/* search methods (SEARCH_METHODS, av1/encoder/mcomp_structs.h) */
+enum { ORC_DIAMOND = 0, ORC_FAST_BIGDIA = 1, ORC_BIGDIA = 2 };
+/* av1_full_pixel_search (no mesh) with DIAMOND / FAST_BIGDIA / BIGDIA:
+ * returns the var cost, writes the best FULLPEL_MV, the step count and,
+ * when cost_list != NULL, the reference's 5-entry cost list. */
+int orc_full_pixel_search(const OrcMsParams *p, int method, int start_row, int start_col,
+                          int step_param, int *cost_list, int *best_row, int *best_col,
+                          int *steps);
 int orc_full_pixel_search_diamond(const OrcMsParams *p, int start_row,
                                   int start_col, int step_param, int *best_row,
                                   int *best_col, int *steps);
@@ -211,6 +226,14 @@ void orc_bigdia_batch(const uint8_t *src, int src_stride, const uint8_t *ref,
                       int ref_stride, int w, int h, const OrcDiamondJob *jobs,
                       long njobs, int step_param, int mv_cost_type,
                       int skip_sad, OrcDiamondResult *out, int threads);
+
+/* any method, any mv cost (cost->mv_cost_type), optional cost lists
+ * (cost_lists[job][5]) */
+void orc_full_pixel_search_batch(const uint8_t *src, int src_stride, const uint8_t *ref,
+                                 int ref_stride, int w, int h, const OrcDiamondJob *jobs,
+                                 long njobs, int method, int step_param, const OrcMvCost *cost,
+                                 int skip_sad, int32_t *cost_lists, OrcDiamondResult *out,
+                                 int threads);
 
 /* ---- sub-pixel refinement (oracle_subpel.c); layouts = LavishSubpelJob /
  * LavishSubpelResult.  MVs and limits in 1/8 pel. */

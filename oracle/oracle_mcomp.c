@@ -1,16 +1,24 @@
 /* oracle_mcomp.c -- TEST INFRASTRUCTURE ONLY (see oracle.h).
  *
- * CPU restatement of the DIAMOND full-pixel motion search of the reference:
- *   av1_init_dsmotion_compensation   av1/encoder/mcomp.c:369-404 (level 0)
- *   mvsad_err_cost / mv_err_cost     av1/encoder/mcomp.c:257-360 (L1 / none)
- *   diamond_search_sad               av1/encoder/mcomp.c:1318-1477
- *   full_pixel_diamond               av1/encoder/mcomp.c:1479-1526
- *   downsampled-SAD quality recheck  av1/encoder/mcomp.c:1840-1867
- *   FAST_BIGDIA (pattern_search)     av1/encoder/mcomp.c:498-550,1017-1316
+ * CPU restatement of the full-pixel motion search of the reference:
+ *   av1_init_dsmotion_compensation     av1/encoder/mcomp.c:369-404 (level 0)
+ *   av1_init_motion_compensation_bigdia av1/encoder/mcomp.c:498-550
+ *   mv_cost / mv_err_cost / mvsad_err_cost (entropy, L1, none)
+ *                                      av1/encoder/mcomp.c:255-360
+ *   av1_get_mv_joint                   av1/encoder/encodemv.h:49-55
+ *   diamond_search_sad                 av1/encoder/mcomp.c:1318-1477
+ *   full_pixel_diamond                 av1/encoder/mcomp.c:1479-1526
+ *   pattern_search (BIGDIA do_init_search 1, FAST_BIGDIA 0, cost lists)
+ *                                      av1/encoder/mcomp.c:858-1245,1266-1316
+ *   calc_int_sad_list                  av1/encoder/mcomp.c:789-838
+ *   av1_full_pixel_search: method switch, downsampled-SAD quality recheck
+ *                                      av1/encoder/mcomp.c:1755-1873
  * with sdf/sdx4df = aom_sad / aom_sad_skip and vf = aom_variance of the
- * block size (oracle_dsp.c).  MV_COST_ENTROPY (needs the entropy context's
- * mv cost tables) and mesh refinement are not restated.
+ * block size (oracle_dsp.c).  Mesh refinement is not restated (off at the
+ * configurations here).  Pinned by tests/golden/fix_mcomp.npz, made by
+ * executing the reference's own av1_full_pixel_search.
  */
+#include <limits.h>
 #include <stdlib.h>
 
 #include "oracle.h"
@@ -26,22 +34,37 @@ static int sse_lambda(int type) {
 
 static int rawpel(int x) { return (x + 3 + (x >= 0)) >> 3; } /* mv.h:28 */
 
+/* mv_cost (mcomp.c:268-272) of a 1/8-pel diff */
+static int mv_rate(const OrcMvCost *c, int dr, int dc) {
+  const int joint = (dc != 0) | ((dr != 0) << 1);
+  return c->mvjcost[joint] + c->mvcost[0][dr] + c->mvcost[1][dc];
+}
+
 static unsigned mvsad_cost(const OrcMsParams *p, int row, int col) {
-  if (p->mv_cost_type < 1 || p->mv_cost_type > 3) return 0;
   const int dr = (row - rawpel(p->ref_mv_row)) * 8;
   const int dc = (col - rawpel(p->ref_mv_col)) * 8;
+  if (p->mv_cost_type == 0) /* ROUND_POWER_OF_TWO(unsigned, AV1_PROB_COST_SHIFT) */
+    return ((unsigned)mv_rate(p->cost, dr, dc) * (unsigned)p->cost->sad_per_bit + 256u) >> 9;
+  if (p->mv_cost_type < 1 || p->mv_cost_type > 3) return 0;
   return (unsigned)((sad_lambda(p->mv_cost_type) * (abs(dr) + abs(dc))) >> 3);
 }
 
 static int mv_cost(const OrcMsParams *p, int row, int col) {
-  if (p->mv_cost_type < 1 || p->mv_cost_type > 3) return 0;
   const int dr = row * 8 - p->ref_mv_row, dc = col * 8 - p->ref_mv_col;
+  if (p->mv_cost_type == 0) /* ROUND_POWER_OF_TWO_64(., 7 + 9 - 6 + 4) */
+    return (int)(((int64_t)mv_rate(p->cost, dr, dc) * p->cost->error_per_bit + 8192) >> 14);
+  if (p->mv_cost_type < 1 || p->mv_cost_type > 3) return 0;
   return (sse_lambda(p->mv_cost_type) * (abs(dr) + abs(dc))) >> 3;
 }
 
 static int in_range(const OrcMsParams *p, int row, int col) {
   return col >= p->col_min && col <= p->col_max && row >= p->row_min &&
          row <= p->row_max;
+}
+
+static int bounds_ok(const OrcMsParams *p, int row, int col, int r) {
+  return row - r >= p->row_min && row + r <= p->row_max && col - r >= p->col_min &&
+         col + r <= p->col_max;
 }
 
 static unsigned block_sad(const OrcMsParams *p, int row, int col, int skip) {
@@ -55,6 +78,25 @@ static int var_cost(const OrcMsParams *p, int row, int col) {
   const uint8_t *r = p->ref + (ptrdiff_t)row * p->ref_stride + col;
   const int v = (int)orc_variance(p->src, p->src_stride, r, p->ref_stride, p->w, p->h, &sse);
   return v + mv_cost(p, row, col);
+}
+
+/* calc_int_sad_list (mcomp.c:789-838): neighbours left, bottom, right, top */
+static void int_sad_list(const OrcMsParams *p, int br, int bc, int skip, int *cl,
+                         int has_sad) {
+  static const int nr[4] = { 0, 1, 0, -1 }, nc[4] = { -1, 0, 1, 0 };
+  if (!has_sad) {
+    cl[0] = (int)block_sad(p, br, bc, skip);
+    const int all = bounds_ok(p, br, bc, 1);
+    for (int i = 0; i < 4; ++i) {
+      if (!all && !in_range(p, br + nr[i], bc + nc[i]))
+        cl[i + 1] = INT_MAX;
+      else
+        cl[i + 1] = (int)block_sad(p, br + nr[i], bc + nc[i], skip);
+    }
+  }
+  cl[0] += (int)mvsad_cost(p, br, bc);
+  for (int i = 0; i < 4; ++i)
+    if (cl[i + 1] != INT_MAX) cl[i + 1] += (int)mvsad_cost(p, br + nr[i], bc + nc[i]);
 }
 
 /* diamond_search_sad without second_pred / mask: returns bestsad, writes
@@ -73,8 +115,7 @@ static unsigned diamond(const OrcMsParams *p, int srow, int scol, int search_ste
   for (int step = tot - 1; step >= 0; --step) {
     const int rad = 1 << step; /* cfg->radius[step] at level 0 */
     int best_site = 0;
-    const int all_in = row - rad >= p->row_min && row + rad <= p->row_max &&
-                       col - rad >= p->col_min && col + rad <= p->col_max;
+    const int all_in = bounds_ok(p, row, col, rad);
     for (int i = 1; i <= 8; ++i) {
       const int r = row + kDr[i] * rad, c = col + kDc[i] * rad;
       if (!all_in && !in_range(p, r, c)) continue;
@@ -102,7 +143,7 @@ static unsigned diamond(const OrcMsParams *p, int srow, int scol, int search_ste
 }
 
 static int full_pixel_diamond(const OrcMsParams *p, int srow, int scol, int step_param, int skip,
-                              int *brow, int *bcol, int *steps) {
+                              int *cl, int *brow, int *bcol, int *steps) {
   int n, num00 = 0;
   diamond(p, srow, scol, step_param, skip, brow, bcol, &n, steps);
   int bestsme = var_cost(p, *brow, *bcol);
@@ -122,37 +163,11 @@ static int full_pixel_diamond(const OrcMsParams *p, int srow, int scol, int step
       num00 = 0;
     }
   }
+  if (cl) int_sad_list(p, *brow, *bcol, skip, cl, 0);
   return bestsme;
 }
 
-int orc_full_pixel_search_diamond(const OrcMsParams *p, int start_row, int start_col,
-                                  int step_param, int *best_row, int *best_col,
-                                  int *steps) {
-  *steps = 0;
-  /* use_downsampled_sad only for blocks >= 16 high (mcomp.c:132-133) */
-  const int skip = p->skip_sad && p->h >= 16;
-  int var = full_pixel_diamond(p, start_row, start_col, step_param, skip, best_row, best_col,
-                               steps);
-  if (skip) {
-    const uint8_t *r = p->ref + (ptrdiff_t)*best_row * p->ref_stride + *best_col;
-    const int sad = (int)orc_sad(p->src, p->src_stride, r, p->ref_stride, p->w, p->h);
-    const int ssad = (int)orc_sad_skip(p->src, p->src_stride, r, p->ref_stride, p->w, p->h);
-    const int thresh = (p->w >> 2) * (p->h >> 2); /* 1 << (mi_w_log2 + mi_h_log2) */
-    const int big = sad > 1 ? sad : 1;
-    if (sad > thresh && abs(ssad - sad) * 10 >= big * 9)
-      var = full_pixel_diamond(p, start_row, start_col, step_param, 0, best_row, best_col,
-                               steps);
-  }
-  return var;
-}
-
-/* ---- FAST_BIGDIA: fast_bigdia_search -> bigdia_search -> pattern_search
- * (mcomp.c:1017-1245, 1266-1316) with do_init_search 0, sites of
- * av1_init_motion_compensation_bigdia (mcomp.c:498-550), candidate updates
- * update_mvs_and_sad (mcomp.c:858-877) in site order.  Written in the
- * reference's cost_list == NULL form; with a cost list the reference finishes
- * scale 0 in a separate block whose mv result is identical for
- * do_init_search 0.  *steps counts candidate rounds (full or 3-point). */
+/* ---- pattern_search over the BIGDIA sites (mcomp.c:1017-1245) ---- */
 static void bigdia_site(int s, int i, int *dr, int *dc) {
   static const int k0r[4] = { 0, 1, 0, -1 }, k0c[4] = { -1, 0, 1, 0 };
   static const int kr[8] = { -1, 0, 1, 2, 1, 0, -1, -2 }, kc[8] = { -1, -2, -1, 0, 1, 2, 1, 0 };
@@ -165,95 +180,209 @@ static void bigdia_site(int s, int i, int *dr, int *dc) {
     *dc = kc[i] * r;
   }
 }
+static int ncand(int s) { return s == 0 ? 4 : 8; }
 
-/* update_mvs_and_sad without raw / second-best tracking */
-static int bd_update(const OrcMsParams *p, unsigned thissad, int r, int c, unsigned *best) {
-  if (thissad >= *best) return 0;
-  const unsigned sad = thissad + mvsad_cost(p, r, c);
-  if (sad < *best) {
-    *best = sad;
+typedef struct {
+  const OrcMsParams *p;
+  int skip;
+  unsigned best, raw_best;
+  int *cl;
+  int *steps;
+} PState;
+
+/* update_mvs_and_sad (mcomp.c:858-877) */
+static int upd(PState *st, unsigned thissad, int r, int c) {
+  if (thissad >= st->best) return 0;
+  const unsigned sad = thissad + mvsad_cost(st->p, r, c);
+  if (sad < st->best) {
+    st->raw_best = thissad;
+    st->best = sad;
     return 1;
   }
   return 0;
 }
 
-static int fast_bigdia(const OrcMsParams *p, int srow, int scol, int step_param, int skip,
-                       int *brow, int *bcol, int *steps) {
-  int search_step = step_param > MAX_STEPS - 3 ? step_param : MAX_STEPS - 3;
+/* calc_sad4 / calc_sad_update_bestmv over candidates [0, n) of scale s
+ * around (br, bc); cost list entries get the raw SADs (sad4: all four; the
+ * bounds-checked form: in-range ones only).  Returns the best site or -1. */
+static int scan_all(PState *st, int s, int br, int bc, int *cl) {
+  const OrcMsParams *p = st->p;
+  int best_site = -1;
+  const int all = bounds_ok(p, br, bc, 1 << s);
+  for (int i = 0; i < ncand(s); ++i) {
+    int dr, dc;
+    bigdia_site(s, i, &dr, &dc);
+    if (!all && !in_range(p, br + dr, bc + dc)) continue;
+    const unsigned sad = block_sad(p, br + dr, bc + dc, st->skip);
+    if (cl) cl[i + 1] = (int)sad;
+    if (upd(st, sad, br + dr, bc + dc)) best_site = i;
+  }
+  ++*st->steps;
+  return best_site;
+}
+
+/* calc_sad3_update_bestmv / _with_indices: returns j of idx[j] or -1 */
+static int scan3(PState *st, int s, int br, int bc, const int *idx, int *cl) {
+  const OrcMsParams *p = st->p;
+  int best_site = -1;
+  const int all = bounds_ok(p, br, bc, 1 << s);
+  for (int j = 0; j < 3; ++j) {
+    int dr, dc;
+    bigdia_site(s, idx[j], &dr, &dc);
+    if (!all && !in_range(p, br + dr, bc + dc)) {
+      if (cl) cl[idx[j] + 1] = INT_MAX;
+      continue;
+    }
+    const unsigned sad = block_sad(p, br + dr, bc + dc, st->skip);
+    if (cl) cl[idx[j] + 1] = (int)sad;
+    if (upd(st, sad, br + dr, bc + dc)) best_site = j;
+  }
+  ++*st->steps;
+  return best_site;
+}
+
+static void next3(int k, int n, int *idx) {
+  idx[0] = (k == 0) ? n - 1 : k - 1;
+  idx[1] = k;
+  idx[2] = (k == n - 1) ? 0 : k + 1;
+}
+
+static int pattern_search(const OrcMsParams *p, int srow, int scol, int search_step,
+                          int do_init, int skip, int *cl, int *brow, int *bcol, int *steps) {
+  PState st = { p, skip, UINT_MAX, UINT_MAX, cl, steps };
   if (search_step > MAX_STEPS - 1) search_step = MAX_STEPS - 1;
-  int s = MAX_STEPS - 1 - search_step; /* search_steps[search_step] */
+  int best_init_s = MAX_STEPS - 1 - search_step; /* search_steps[search_step] */
   if (scol < p->col_min) scol = p->col_min;
   if (scol > p->col_max) scol = p->col_max;
   if (srow < p->row_min) srow = p->row_min;
   if (srow > p->row_max) srow = p->row_max;
-  int br = srow, bc = scol, k = -1;
-  unsigned best = block_sad(p, br, bc, skip) + mvsad_cost(p, br, bc);
-  int best_site = -1;
-  for (; s >= 0; s--) {
-    const int n = s == 0 ? 4 : 8;
-    const int all_in = br - (1 << s) >= p->row_min && br + (1 << s) <= p->row_max &&
-                       bc - (1 << s) >= p->col_min && bc + (1 << s) <= p->col_max;
-    for (int i = 0; i < n; ++i) { /* calc_sad4_update_bestmv / calc_sad_update_bestmv */
-      int dr, dc;
-      bigdia_site(s, i, &dr, &dc);
-      if (!all_in && !in_range(p, br + dr, bc + dc)) continue;
-      if (bd_update(p, block_sad(p, br + dr, bc + dc, skip), br + dr, bc + dc, &best))
-        best_site = i;
+  int br = srow, bc = scol, k = -1, s;
+  if (cl) cl[0] = cl[1] = cl[2] = cl[3] = cl[4] = INT_MAX;
+  int costlist_has_sad = 0;
+  st.raw_best = block_sad(p, br, bc, skip);
+  st.best = st.raw_best + mvsad_cost(p, br, bc);
+  if (do_init) {
+    s = best_init_s;
+    best_init_s = -1;
+    for (int t = 0; t <= s; ++t) { /* every scale around the fixed start */
+      const int bs = scan_all(&st, t, br, bc, NULL);
+      if (bs == -1) continue;
+      best_init_s = t;
+      k = bs;
     }
-    ++*steps;
-    if (best_site == -1) continue;
-    {
+    if (best_init_s != -1) {
       int dr, dc;
-      bigdia_site(s, best_site, &dr, &dc);
+      bigdia_site(best_init_s, k, &dr, &dc);
       br += dr;
       bc += dc;
-      k = best_site;
     }
-    do {
-      int idx[3];
-      best_site = -1;
-      idx[0] = (k == 0) ? n - 1 : k - 1;
-      idx[1] = k;
-      idx[2] = (k == n - 1) ? 0 : k + 1;
-      const int in3 = br - (1 << s) >= p->row_min && br + (1 << s) <= p->row_max &&
-                      bc - (1 << s) >= p->col_min && bc + (1 << s) <= p->col_max;
-      for (int j = 0; j < 3; ++j) { /* calc_sad3_update_bestmv / _with_indices */
+  }
+  if (best_init_s != -1) {
+    const int last_s = cl != NULL; /* num_candidates[0] == 4 for BIGDIA */
+    int best_site = -1;
+    s = best_init_s;
+    for (; s >= last_s; s--) {
+      if (!do_init || s != best_init_s) {
+        best_site = scan_all(&st, s, br, bc, NULL);
+        if (best_site == -1) continue;
         int dr, dc;
-        bigdia_site(s, idx[j], &dr, &dc);
-        if (!in3 && !in_range(p, br + dr, bc + dc)) continue;
-        if (bd_update(p, block_sad(p, br + dr, bc + dc, skip), br + dr, bc + dc, &best))
-          best_site = j;
-      }
-      ++*steps;
-      if (best_site != -1) {
-        k = idx[best_site];
-        int dr, dc;
-        bigdia_site(s, k, &dr, &dc);
+        bigdia_site(s, best_site, &dr, &dc);
         br += dr;
         bc += dc;
+        k = best_site;
       }
-    } while (best_site != -1);
+      do {
+        int idx[3];
+        next3(k, ncand(s), idx);
+        best_site = scan3(&st, s, br, bc, idx, NULL);
+        if (best_site != -1) {
+          k = idx[best_site];
+          int dr, dc;
+          bigdia_site(s, k, &dr, &dc);
+          br += dr;
+          bc += dc;
+        }
+      } while (best_site != -1);
+    }
+    if (s == 0) { /* only with a cost list (last_s == 1) */
+      cl[0] = (int)st.raw_best;
+      costlist_has_sad = 1;
+      if (!do_init || s != best_init_s) {
+        best_site = scan_all(&st, 0, br, bc, cl);
+        if (best_site != -1) {
+          int dr, dc;
+          bigdia_site(0, best_site, &dr, &dc);
+          br += dr;
+          bc += dc;
+          k = best_site;
+        }
+      }
+      while (best_site != -1) {
+        int idx[3];
+        next3(k, 4, idx);
+        cl[1] = cl[2] = cl[3] = cl[4] = INT_MAX;
+        cl[((k + 2) % 4) + 1] = cl[0];
+        cl[0] = (int)st.raw_best;
+        best_site = scan3(&st, 0, br, bc, idx, cl);
+        if (best_site != -1) {
+          k = idx[best_site];
+          int dr, dc;
+          bigdia_site(0, k, &dr, &dc);
+          br += dr;
+          bc += dc;
+        }
+      }
+    }
   }
   *brow = br;
   *bcol = bc;
+  if (cl) int_sad_list(p, br, bc, skip, cl, costlist_has_sad);
   return var_cost(p, br, bc); /* get_mvpred_var_cost */
+}
+
+/* av1_full_pixel_search (mcomp.c:1755-1873) without mesh search */
+int orc_full_pixel_search(const OrcMsParams *p, int method, int start_row, int start_col,
+                          int step_param, int *cl, int *best_row, int *best_col, int *steps) {
+  /* use_downsampled_sad only for blocks >= 16 high (mcomp.c:132-133) */
+  int skip = p->skip_sad && p->h >= 16;
+  for (;;) {
+    if (cl) cl[0] = cl[1] = cl[2] = cl[3] = cl[4] = INT_MAX;
+    int var;
+    if (method == ORC_DIAMOND) {
+      var = full_pixel_diamond(p, start_row, start_col, step_param, skip, cl, best_row, best_col,
+                               steps);
+    } else {
+      /* fast_bigdia_search: AOMMAX(MAX_MVSEARCH_STEPS - 3, step_param), do_init 0;
+       * bigdia_search: step_param, do_init 1 */
+      const int fast = method == ORC_FAST_BIGDIA;
+      const int ss = fast ? (step_param > MAX_STEPS - 3 ? step_param : MAX_STEPS - 3) : step_param;
+      var = pattern_search(p, start_row, start_col, ss, !fast, skip, cl, best_row, best_col,
+                           steps);
+    }
+    if (!skip) return var;
+    /* quality check of the row-skipping search (mcomp.c:1840-1867) */
+    const uint8_t *r = p->ref + (ptrdiff_t)*best_row * p->ref_stride + *best_col;
+    const int sad = (int)orc_sad(p->src, p->src_stride, r, p->ref_stride, p->w, p->h);
+    const int ssad = (int)orc_sad_skip(p->src, p->src_stride, r, p->ref_stride, p->w, p->h);
+    const int thresh = (p->w >> 2) * (p->h >> 2); /* 1 << (mi_w_log2 + mi_h_log2) */
+    const int big = sad > 1 ? sad : 1;
+    if (!(sad > thresh && abs(ssad - sad) * 10 >= big * 9)) return var;
+    skip = 0; /* redo the whole search with the full SAD */
+  }
+}
+
+int orc_full_pixel_search_diamond(const OrcMsParams *p, int start_row, int start_col,
+                                  int step_param, int *best_row, int *best_col, int *steps) {
+  *steps = 0;
+  return orc_full_pixel_search(p, ORC_DIAMOND, start_row, start_col, step_param, NULL, best_row,
+                               best_col, steps);
 }
 
 int orc_full_pixel_search_bigdia(const OrcMsParams *p, int start_row, int start_col,
                                  int step_param, int *best_row, int *best_col, int *steps) {
   *steps = 0;
-  const int skip = p->skip_sad && p->h >= 16;
-  int var = fast_bigdia(p, start_row, start_col, step_param, skip, best_row, best_col, steps);
-  if (skip) { /* av1_full_pixel_search quality recheck, mcomp.c:1840-1873 */
-    const uint8_t *r = p->ref + (ptrdiff_t)*best_row * p->ref_stride + *best_col;
-    const int sad = (int)orc_sad(p->src, p->src_stride, r, p->ref_stride, p->w, p->h);
-    const int ssad = (int)orc_sad_skip(p->src, p->src_stride, r, p->ref_stride, p->w, p->h);
-    const int thresh = (p->w >> 2) * (p->h >> 2);
-    const int big = sad > 1 ? sad : 1;
-    if (sad > thresh && abs(ssad - sad) * 10 >= big * 9)
-      var = fast_bigdia(p, start_row, start_col, step_param, 0, best_row, best_col, steps);
-  }
-  return var;
+  return orc_full_pixel_search(p, ORC_FAST_BIGDIA, start_row, start_col, step_param, NULL,
+                               best_row, best_col, steps);
 }
 
 /* ---- batch driver (pthreads over job ranges) ---- */
@@ -261,9 +390,11 @@ int orc_full_pixel_search_bigdia(const OrcMsParams *p, int start_row, int start_
 
 typedef struct {
   const uint8_t *src, *ref;
-  int ss, rs, w, h, step_param, cost, skip, method;
+  int ss, rs, w, h, step_param, skip, method;
+  const OrcMvCost *cost;
   const OrcDiamondJob *jobs;
   OrcDiamondResult *out;
+  int32_t *cls;
   long lo, hi;
 } BatchArg;
 
@@ -273,13 +404,11 @@ static void *batch_worker(void *v) {
     const OrcDiamondJob *jb = &a->jobs[j];
     OrcMsParams p = { a->src + jb->src_off, a->ss, a->ref + jb->ref_off, a->rs, a->w, a->h,
                       jb->col_min, jb->col_max, jb->row_min, jb->row_max, jb->ref_mv_row,
-                      jb->ref_mv_col, a->cost, a->skip };
-    int br, bc, steps;
-    a->out[j].bestsme =
-        a->method ? orc_full_pixel_search_bigdia(&p, jb->start_row, jb->start_col, a->step_param,
-                                                 &br, &bc, &steps)
-                  : orc_full_pixel_search_diamond(&p, jb->start_row, jb->start_col,
-                                                  a->step_param, &br, &bc, &steps);
+                      jb->ref_mv_col, a->cost->mv_cost_type, a->skip, a->cost };
+    int br, bc, steps = 0;
+    a->out[j].bestsme = orc_full_pixel_search(&p, a->method, jb->start_row, jb->start_col,
+                                              a->step_param, a->cls ? a->cls + 5 * j : NULL,
+                                              &br, &bc, &steps);
     a->out[j].best_row = (int16_t)br;
     a->out[j].best_col = (int16_t)bc;
     a->out[j].steps = steps;
@@ -288,17 +417,18 @@ static void *batch_worker(void *v) {
   return NULL;
 }
 
-static void fullpel_batch(const uint8_t *src, int src_stride, const uint8_t *ref,
-                          int ref_stride, int w, int h, const OrcDiamondJob *jobs, long njobs,
-                          int step_param, int mv_cost_type, int skip_sad, int method,
-                          OrcDiamondResult *out, int threads) {
+void orc_full_pixel_search_batch(const uint8_t *src, int src_stride, const uint8_t *ref,
+                                 int ref_stride, int w, int h, const OrcDiamondJob *jobs,
+                                 long njobs, int method, int step_param, const OrcMvCost *cost,
+                                 int skip_sad, int32_t *cost_lists, OrcDiamondResult *out,
+                                 int threads) {
   if (threads < 1) threads = 1;
   if (threads > 64) threads = 64;
   pthread_t tid[64];
   BatchArg args[64];
   for (int t = 0; t < threads; ++t) {
-    args[t] = (BatchArg){ src, ref, src_stride, ref_stride, w, h, step_param, mv_cost_type,
-                          skip_sad, method, jobs, out, njobs * t / threads,
+    args[t] = (BatchArg){ src, ref, src_stride, ref_stride, w, h, step_param, skip_sad, method,
+                          cost, jobs, out, cost_lists, njobs * t / threads,
                           njobs * (t + 1) / threads };
     if (threads > 1) pthread_create(&tid[t], NULL, batch_worker, &args[t]);
     else batch_worker(&args[t]);
@@ -310,13 +440,15 @@ static void fullpel_batch(const uint8_t *src, int src_stride, const uint8_t *ref
 void orc_diamond_batch(const uint8_t *src, int src_stride, const uint8_t *ref, int ref_stride,
                        int w, int h, const OrcDiamondJob *jobs, long njobs, int step_param,
                        int mv_cost_type, int skip_sad, OrcDiamondResult *out, int threads) {
-  fullpel_batch(src, src_stride, ref, ref_stride, w, h, jobs, njobs, step_param, mv_cost_type,
-                skip_sad, 0, out, threads);
+  const OrcMvCost c = { mv_cost_type, 0, 0, NULL, { NULL, NULL } };
+  orc_full_pixel_search_batch(src, src_stride, ref, ref_stride, w, h, jobs, njobs, ORC_DIAMOND,
+                              step_param, &c, skip_sad, NULL, out, threads);
 }
 
 void orc_bigdia_batch(const uint8_t *src, int src_stride, const uint8_t *ref, int ref_stride,
                       int w, int h, const OrcDiamondJob *jobs, long njobs, int step_param,
                       int mv_cost_type, int skip_sad, OrcDiamondResult *out, int threads) {
-  fullpel_batch(src, src_stride, ref, ref_stride, w, h, jobs, njobs, step_param, mv_cost_type,
-                skip_sad, 1, out, threads);
+  const OrcMvCost c = { mv_cost_type, 0, 0, NULL, { NULL, NULL } };
+  orc_full_pixel_search_batch(src, src_stride, ref, ref_stride, w, h, jobs, njobs,
+                              ORC_FAST_BIGDIA, step_param, &c, skip_sad, NULL, out, threads);
 }

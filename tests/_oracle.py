@@ -419,6 +419,48 @@ def diamond_batch(src, ref, stride, w, h, jobs, step_param=0, mv_cost_type=3, sk
     return out
 
 
+class OrcMvCost(ctypes.Structure):
+    _fields_ = [("mv_cost_type", ctypes.c_int), ("sad_per_bit", ctypes.c_int),
+                ("error_per_bit", ctypes.c_int), ("mvjcost", ctypes.c_void_p),
+                ("mvcost", ctypes.c_void_p * 2)]
+
+
+FP_METHODS = {"diamond": 0, "fast_bigdia": 1, "bigdia": 2}
+
+
+def full_pixel_search_batch(src, ref, stride, w, h, jobs, method="diamond", step_param=0,
+                            mv_cost_type=3, sad_per_bit=0, error_per_bit=0, mvjcost=None,
+                            mvcost=None, skip=False, cost_list=False, threads=1):
+    """orc_full_pixel_search_batch: av1_full_pixel_search with any of the
+    DIAMOND / FAST_BIGDIA / BIGDIA methods and any mv cost.  mvjcost int32[4],
+    mvcost int32[2][MV_VALS] (centred at MV_MAX) for MV_COST_ENTROPY.
+    Returns (results, cost_lists int32[n][5] or None)."""
+    L = lib()
+    fn = L.orc_full_pixel_search_batch
+    fn.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
+                   ctypes.c_int, ctypes.c_void_p, ctypes.c_long, ctypes.c_int, ctypes.c_int,
+                   ctypes.POINTER(OrcMvCost), ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
+                   ctypes.c_int]
+    jobs = np.ascontiguousarray(jobs)
+    keep = []
+    c = OrcMvCost(mv_cost_type, sad_per_bit, error_per_bit)
+    if mvjcost is not None:
+        mj = np.ascontiguousarray(mvjcost, np.int32)
+        mc = np.ascontiguousarray(mvcost, np.int32)
+        keep += [mj, mc]
+        mid = (mc.shape[1] - 1) // 2
+        c.mvjcost = mj.ctypes.data
+        c.mvcost[0] = mc.ctypes.data + 4 * mid
+        c.mvcost[1] = mc.ctypes.data + 4 * (mc.shape[1] + mid)
+    out = np.zeros(len(jobs), np.dtype([("best_row", "<i2"), ("best_col", "<i2"),
+                                        ("bestsme", "<i4"), ("steps", "<i4"),
+                                        ("searches", "<i4")], align=True))
+    cls = np.full((len(jobs), 5), 0x7FFFFFFF, np.int32) if cost_list else None
+    fn(P(src), stride, P(ref), stride, w, h, P(jobs), len(jobs), FP_METHODS[method], step_param,
+       ctypes.byref(c), int(skip), P(cls) if cost_list else None, P(out), threads)
+    return out, cls
+
+
 SUBPEL_RESULT = np.dtype([("best_row", "<i2"), ("best_col", "<i2"), ("besterr", "<u4"),
                           ("distortion", "<i4"), ("sse", "<u4")], align=True)
 

@@ -100,6 +100,8 @@ class Struct(CType):
         self.name = name
         self.fields = None  # [(name, type)]
         self.index = {}
+        self.is_union = False
+        self.packed_unknown = False
 
     def __repr__(self):
         return "struct %s" % self.name
@@ -136,6 +138,10 @@ BUILTIN_TYPEDEFS = {
     "int32_t": INT, "uint32_t": UINT, "int64_t": LONG, "uint64_t": ULONG,
     "intptr_t": LONG, "uintptr_t": ULONG, "size_t": ULONG, "ptrdiff_t": LONG,
     "ssize_t": LONG, "FILE": Struct("FILE"),
+    # libc / pthread types the headers mention (system headers are not part of
+    # the reference): opaque scalars, never used by the interpreted code paths
+    "pthread_mutex_t": LONG, "pthread_cond_t": LONG, "pthread_t": ULONG, "va_list": LONG,
+    "jmp_buf": LONG, "pthread_attr_t": LONG, "sem_t": LONG,
 }
 
 
@@ -194,6 +200,12 @@ def sizeof(t):
             raise CError("sizeof incomplete array")
         return t.n * sizeof(t.of)
     if isinstance(t, Struct):
+        if t.packed_unknown:
+            raise CError("sizeof a struct with bitfields")
+        if t.is_union:
+            al = max([alignof(ft) for _, ft in t.fields] or [1])
+            sz = max([sizeof(ft) for _, ft in t.fields] or [0])
+            return (sz + al - 1) // al * al
         off, al = 0, 1
         for _, ft in t.fields:
             a = alignof(ft)
@@ -229,11 +241,13 @@ def scalar_of(t):
 # =============================================================================
 class SObj:
     """A struct object: one cell per field (array fields hold their own flat
-    list, struct fields an SObj)."""
-    __slots__ = ("st", "vals")
+    list, struct fields an SObj).  A union keeps one cell per member plus the
+    index of the member last accessed; accessing another member first
+    re-materialises it from that one's bytes (little-endian layout)."""
+    __slots__ = ("st", "vals", "cur")
 
     def __init__(self, st, vals):
-        self.st, self.vals = st, vals
+        self.st, self.vals, self.cur = st, vals, 0
 
 
 def new_storage(t):
@@ -264,8 +278,80 @@ def new_obj(t):
 
 def copy_obj(v):
     if isinstance(v, SObj):
-        return SObj(v.st, [list(x) if isinstance(x, list) else copy_obj(x) for x in v.vals])
+        o = SObj(v.st, [list(x) if isinstance(x, list) else copy_obj(x) for x in v.vals])
+        o.cur = v.cur
+        return o
     return v
+
+
+def to_bytes(v, t):
+    """Little-endian object representation (ints, floats, structs, arrays)."""
+    import struct as _s
+    if isinstance(t, Int):
+        return (v & t.mask).to_bytes(t.bits // 8, "little")
+    if isinstance(t, Flt):
+        return _s.pack("<f" if t.bits == 32 else "<d", v)
+    if isinstance(t, Arr):
+        es = slots(t.of)
+        return b"".join(to_bytes(v[k * es:(k + 1) * es] if isinstance(t.of, Arr) else v[k], t.of)
+                        for k in range(t.n))
+    if isinstance(t, Struct):
+        if t.is_union:
+            k = v.cur
+            b = to_bytes(v.vals[k], t.fields[k][1])
+            return b + bytes(sizeof(t) - len(b))
+        out = bytearray()
+        for (fn, ft), fv in zip(t.fields, v.vals):
+            a = alignof(ft)
+            out += bytes((-len(out)) % a)
+            out += to_bytes(fv, ft)
+        out += bytes((-len(out)) % alignof(t))
+        return bytes(out)
+    raise CError("object representation of %r" % (t,))
+
+
+def from_bytes(b, t):
+    import struct as _s
+    if isinstance(t, Int):
+        return t.wrap(int.from_bytes(b[:t.bits // 8], "little"))
+    if isinstance(t, Flt):
+        return _s.unpack("<f" if t.bits == 32 else "<d", b[:t.bits // 8])[0]
+    if isinstance(t, Arr):
+        es = sizeof(t.of)
+        out = []
+        for k in range(t.n):
+            x = from_bytes(b[k * es:(k + 1) * es], t.of)
+            if isinstance(t.of, Arr):
+                out.extend(x)
+            else:
+                out.append(x)
+        return out
+    if isinstance(t, Struct):
+        o = new_obj(t)
+        if t.is_union:
+            o.vals[0] = from_bytes(b, t.fields[0][1])
+            o.cur = 0
+            return o
+        off = 0
+        for k, (fn, ft) in enumerate(t.fields):
+            a = alignof(ft)
+            off += (-off) % a
+            o.vals[k] = from_bytes(b[off:off + sizeof(ft)], ft)
+            off += sizeof(ft)
+        return o
+    raise CError("object representation of %r" % (t,))
+
+
+def union_member(obj, idx):
+    """Make member idx of a union object current (re-interpreting the bytes
+    of the member last accessed)."""
+    if obj.cur != idx:
+        st = obj.st
+        raw = to_bytes(obj.vals[obj.cur], st.fields[obj.cur][1])
+        raw = raw + bytes(max(0, sizeof(st.fields[idx][1]) - len(raw)))
+        obj.vals[idx] = from_bytes(raw, st.fields[idx][1])
+        obj.cur = idx
+    return obj
 
 
 class Pointer:
@@ -386,16 +472,58 @@ class Preprocessor:
     hide sets against recursive expansion.  #include is ignored: the TU lists
     its files explicitly, in dependency order."""
 
-    def __init__(self, defines):
+    RTCD_DEFS = {"config/aom_dsp_rtcd.h": "aom_dsp/aom_dsp_rtcd_defs.pl",
+                 "config/av1_rtcd.h": "av1/common/av1_rtcd_defs.pl",
+                 "config/aom_scale_rtcd.h": "aom_scale/aom_scale_rtcd.pl"}
+
+    def __init__(self, defines, root=None):
         self.macros = {}
+        self.root = root
+        self.done_rtcd = set()
         for k, v in defines.items():
             self.macros[k] = Macro(k, None, tokenize(str(v)))
 
-    def process(self, text, fname):
+    def include(self, rest, fname):
+        """Tokens of a quoted #include found under the reference root (its
+        guards make repeats empty); generated config/* headers and <system>
+        headers are skipped (their content is reference_defines / the rtcd
+        name fallback)."""
+        m = re.match(r'"([^"]+)"', rest)
+        if not m or self.root is None:
+            return []
+        if m.group(1) in self.RTCD_DEFS:
+            # a generated rtcd header: its prelude is the `print <<EOF` block
+            # of the *_rtcd_defs.pl it is generated from (build/cmake/rtcd.pl
+            # copies it verbatim); the prototypes that follow are not needed
+            # (calls resolve to the _c functions)
+            if m.group(1) in self.done_rtcd:
+                return []
+            self.done_rtcd.add(m.group(1))
+            with open(os.path.join(self.root, self.RTCD_DEFS[m.group(1)])) as fh:
+                pl = fh.read()
+            pre = re.search(r"print <<EOF\n(.*?)\nEOF", pl, re.S)
+            return self.process(pre.group(1), m.group(1), expand=False) if pre else []
+        if m.group(1).startswith("config/"):
+            return []
+        for base in (self.root, os.path.join(self.root, os.path.dirname(fname))):
+            path = os.path.join(base, m.group(1))
+            if os.path.isfile(path):
+                rel = os.path.relpath(path, self.root)
+                with open(path) as fh:
+                    return self.process(fh.read(), rel, expand=False)
+        return []
+
+    def process(self, text, fname, expand=True):
         text = strip_comments(text)
         # join continuation lines, keeping line numbers for the next line
         lines = text.split("\n")
         toks = []
+        done = [0]  # toks[:done] are already macro-expanded
+
+        def pending_expand(ts):
+            out = ts[:done[0]] + (self.expand(ts[done[0]:]) if expand or True else ts[done[0]:])
+            done[0] = len(out)
+            return out
         stack = []  # (parent_active, taken)
         active = True
         ln = 0
@@ -440,15 +568,25 @@ class Preprocessor:
                 elif not active:
                     continue
                 elif kw == "define":
+                    # what precedes is expanded with the macros as they stand
+                    # (a function-local #define ... #undef pair, e.g.
+                    # UPDATE_SEARCH_STEP in mcomp.c, must apply in between)
+                    toks = pending_expand(toks)
                     self.define(rest, fname, start)
                 elif kw == "undef":
+                    toks = pending_expand(toks)
                     self.macros.pop(rest.split()[0], None)
                 elif kw == "error":
                     raise CError("%s:%d: #error %s" % (fname, start, rest))
+                elif kw == "include":
+                    # expand what precedes with the macros defined so far
+                    toks = pending_expand(toks) + self.include(rest, fname)
+                    done[0] = len(toks)
                 continue
             if active and s:
                 toks.extend(tokenize(line, fname, start))
-        return self.expand(toks)
+        toks = pending_expand(toks)
+        return toks
 
     def define(self, rest, fname, ln):
         m = re.match(r"(\w+)", rest)
@@ -581,6 +719,8 @@ QUAL_KW = {"const", "volatile", "restrict", "__restrict", "__restrict__", "stati
 
 
 class Parser:
+    _anon = 0
+
     def __init__(self, toks, scope):
         self.t = toks
         self.i = 0
@@ -690,10 +830,12 @@ class Parser:
         name = None
         if self.peek().k == "id":
             name = self.next().v
-        key = name or ("<anon%d>" % id(self))
+        Parser._anon += 1
+        key = (kind + " " + name) if name else ("<anon%d>" % Parser._anon)
         st = self.sc.structs.get(key)
         if st is None:
             st = Struct(key)
+            st.is_union = kind == "union"
             if name:
                 self.sc.structs[key] = st
         if self.accept("{"):
@@ -701,17 +843,23 @@ class Parser:
             while not self.accept("}"):
                 base, _ = self.decl_specs()
                 while True:
-                    if self.peek().v == ":":
-                        raise CError("bitfields unsupported")
+                    if self.peek().v == ":":  # unnamed bitfield (padding)
+                        self.next()
+                        self.sc.const_eval(self.cond_expr())
+                        if not self.accept(","):
+                            break
+                        continue
                     fname, ftype = self.declarator(base)
                     if self.accept(":"):
-                        raise CError("bitfields unsupported")
+                        # a bitfield: an integer of that width (stores wrap
+                        # to it); layout is not modelled (no sizeof use)
+                        width = self.sc.const_eval(self.cond_expr())
+                        ftype = Int(width, ftype.signed, "%s:%d" % (ftype.name, width))
+                        st.packed_unknown = True
                     fields.append((fname, ftype))
                     if not self.accept(","):
                         break
                 self.expect(";")
-            if kind == "union":
-                raise CError("unions unsupported")
             st.fields = fields
             st.index = {f: k for k, (f, _) in enumerate(fields)}
         return st
@@ -1179,7 +1327,7 @@ class TU:
         self.compiled = {}
         self.addr = AddrMap()
         self.errors = []
-        self.pp = Preprocessor(defines)
+        self.pp = Preprocessor(defines, root)
         for f in files:
             with open(os.path.join(root, f)) as fh:
                 toks = self.pp.process(fh.read(), f)
@@ -1201,7 +1349,8 @@ class TU:
                 elif v in (")", "]"):
                     depth -= 1
                 elif v == "{":
-                    if depth == 0 and toks[j - 1].v == ")" and "=" not in [t.v for t in toks[i:j]]:
+                    if depth == 0 and toks[j - 1].v == ")" and "=" not in [t.v for t in toks[i:j]] \
+                            and not self._attr_paren(toks, j - 1):
                         # function body: match braces
                         d = 0
                         k = j
@@ -1237,6 +1386,23 @@ class TU:
                 self.errors.append((fname, chunk[0].where, str(e)))
             except (IndexError, KeyError, AttributeError, TypeError, ValueError) as e:
                 self.errors.append((fname, chunk[0].where, repr(e)))
+
+    @staticmethod
+    def _attr_paren(toks, close):
+        """True when the ')' at toks[close] ends an __attribute__((...))."""
+        d = 0
+        k = close
+        while k >= 0:
+            if toks[k].v == ")":
+                d += 1
+            elif toks[k].v == "(":
+                d -= 1
+                if d == 0:
+                    break
+            k -= 1
+        while k > 0 and toks[k - 1].v == "(":
+            k -= 1
+        return k > 0 and toks[k - 1].v in ("__attribute__", "__declspec")
 
     def parse_external(self, chunk):
         p = Parser(chunk + [Tok("eof", "<eof>")], self)
@@ -1525,14 +1691,12 @@ class TU:
                 raise CError("subscript of %r" % (bt,))
             el = bt.to
             es = slots(el)
-            if isinstance(el, Arr):
-                def loc(fr):
-                    p = bf(fr)
-                    return p.buf, p.off + xf(fr) * es
-            else:
-                def loc(fr):
-                    p = bf(fr)
-                    return p.buf, p.off + xf(fr) * es if es != 1 else p.off + xf(fr)
+            def loc(fr):
+                p = bf(fr)
+                o = p.off + xf(fr) * es
+                if o < 0 or p.buf is None:
+                    raise CError("out-of-bounds / wild access at offset %d" % o)
+                return p.buf, o
             return loc, el
         if k == "un" and e[1] == "*":
             pf, pt = self.rvalue(fs, e[2])
@@ -1545,6 +1709,8 @@ class TU:
                     p = self.addr.to_ptr(p.off, p.ty)
                     if p.buf is None:
                         raise CError("dereference of a wild pointer")
+                if p.off < 0:
+                    raise CError("out-of-bounds access at offset %d" % p.off)
                 return p.buf, p.off
             return loc, pt.to
         if k in ("member", "arrow"):
@@ -1559,6 +1725,10 @@ class TU:
                 raise CError("member of %r" % (stt,))
             idx = stt.index[e[2]]
             ft = stt.fields[idx][1]
+            if stt.is_union:
+                if isinstance(ft, Arr):
+                    return (lambda fr: (union_member(getobj(fr), idx).vals[idx], 0)), ft
+                return (lambda fr: (union_member(getobj(fr), idx).vals, idx)), ft
             if isinstance(ft, Arr):
                 return (lambda fr: (getobj(fr).vals[idx], 0)), ft
             return (lambda fr: (getobj(fr).vals, idx)), ft
@@ -1872,6 +2042,15 @@ class TU:
                         holder[0] = self.compiled.get(rn) or self.compile_func(rn)
                     return holder[0]([cv(a(fr)) for cv, a in zip(convs, fl)])
                 return f, ft.ret
+        if callee[0] == "id" and fs.lookup(callee[1]) is None and \
+                self.global_type(callee[1]) is None and self.resolve_name(callee[1]) is None:
+            # no definition: an error only if this call is ever executed
+            nm = callee[1]
+            ret = self.func_decls[nm].ret if nm in self.func_decls else INT
+
+            def missing(fr):
+                raise CError("call to undefined function %s" % nm)
+            return missing, ret
         pf, pt = self.rvalue(fs, callee)
         ft = pt.to if isinstance(pt, Ptr) else pt
         if not isinstance(ft, Func):

@@ -527,8 +527,170 @@ def gen_wht(tu):
     np.savez_compressed(os.path.join(HERE, "fix_wht.npz"), **out)
 
 
+# ----------------------------------------------------------------------------
+# motion search (C3 and its RDO-path variants)
+# ----------------------------------------------------------------------------
+MV_MAX = 16383
+MV_VALS = 2 * MV_MAX + 1
+
+
+def nmv_cost_tables():
+    """av1_build_nmv_cost_table (av1/encoder/encodemv.c:294-300) over the
+    default nmv context (av1/common/entropymv.c:15) at low and high mv
+    precision: (mvjcost[4], mvcost[2][MV_VALS]) each, centred at MV_MAX."""
+    tu = C.TU(REF, ["av1/encoder/cost.c", "av1/common/entropymv.c", "av1/encoder/encodemv.c"],
+              C.reference_defines(REF))
+    check_errors(tu, ["av1_build_nmv_cost_table"])
+    cell, _, t = tu.global_cell("default_nmv_context")
+    ctx = C.Pointer(cell, 0, t)
+    out = {}
+    for prec, nm in ((tu.enums["MV_SUBPEL_LOW_PRECISION"], "lp"),
+                     (tu.enums["MV_SUBPEL_HIGH_PRECISION"], "hp")):
+        mj = tu.buffer("int", 4)
+        c0, c1 = tu.buffer("int", MV_VALS), tu.buffer("int", MV_VALS)
+        arr = C.Pointer([C.Pointer(c0.buf, MV_MAX, c0.ty), C.Pointer(c1.buf, MV_MAX, c1.ty)], 0,
+                        C.Ptr(C.INT))
+        tu.func("av1_build_nmv_cost_table")(mj, arr, ctx, prec)
+        out["mvjcost_" + nm] = np.array(mj.buf, np.int32)
+        out["mvcost_" + nm] = np.stack([np.array(c0.buf, np.int32), np.array(c1.buf, np.int32)])
+    return out
+
+
+def _set(obj, **kw):
+    for k, v in kw.items():
+        obj.vals[obj.st.index[k]] = v
+
+
+def _get(obj, k):
+    return obj.vals[obj.st.index[k]]
+
+
+MS_BLOCKS = [(16, 16, 10), (8, 8, 6), (32, 32, 5), (64, 64, 3), (16, 8, 4), (8, 32, 3),
+             (32, 16, 3), (128, 128, 1), (4, 4, 3)]
+MS_CASES = [  # (method name, do-we-pass-a-cost-list, cost type, downsampled sad, step_param)
+    ("DIAMOND", 1, "MV_COST_ENTROPY", 1, 0), ("DIAMOND", 0, "MV_COST_ENTROPY", 0, 0),
+    ("DIAMOND", 1, "MV_COST_L1_HDRES", 1, 0), ("DIAMOND", 0, "MV_COST_NONE", 0, 3),
+    ("BIGDIA", 1, "MV_COST_ENTROPY", 1, 0), ("BIGDIA", 0, "MV_COST_ENTROPY", 0, 2),
+    ("BIGDIA", 1, "MV_COST_ENTROPY", 0, 5),
+    ("FAST_BIGDIA", 1, "MV_COST_ENTROPY", 0, 0), ("FAST_BIGDIA", 0, "MV_COST_NONE", 0, 6),
+    ("FAST_BIGDIA", 1, "MV_COST_L1_HDRES", 1, 8),
+]
+
+
+def gen_mcomp():
+    """av1_full_pixel_search (av1/encoder/mcomp.c:1755-1895) over the DIAMOND,
+    BIGDIA (do_init_search 1) and FAST_BIGDIA (do_init_search 0) methods with
+    the entropy / L1 / none mv costs, with and without the downsampled-SAD
+    speed feature and a cost list, on a small synthetic frame pair; plus the
+    default-context mv cost tables and the mv limits of av1_set_mv_limits /
+    av1_set_mv_search_range."""
+    sys.path.insert(0, os.path.join(os.path.dirname(HERE), "..", "aom-av1-lavish_amd"))
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(HERE)), "aom-av1-lavish_amd"))
+    import lavish_dsp.synth as synth
+    out = nmv_cost_tables()
+    tu = C.TU(REF, ["aom_dsp/sad.c", "aom_dsp/variance.c", "av1/encoder/mcomp.c"],
+              C.reference_defines(REF))
+    check_errors(tu, ["av1_full_pixel_search", "av1_init_dsmotion_compensation",
+                      "av1_init_motion_compensation_bigdia", "av1_set_mv_search_range"])
+    E = tu.enums
+    W, H, BORDER, NREF = 160, 128, 160, 2
+    src_np, refs_np = synth.motion_planes(W, H, NREF, BORDER, seed=4321)
+    stride = src_np.shape[1]
+    out["src"], out["refs"] = src_np, refs_np
+    out["geom"] = np.array([W, H, BORDER, NREF], np.int32)
+    src_buf = tu.buffer("uint8_t", src_np.reshape(-1).tolist())
+    ref_bufs = [tu.buffer("uint8_t", r.reshape(-1).tolist()) for r in refs_np]
+    org = BORDER * stride + BORDER
+    cfgs = {}
+    for m in ("DIAMOND", "BIGDIA", "FAST_BIGDIA"):
+        cfg = tu.struct_obj("search_site_config")
+        if m == "DIAMOND":
+            tu.func("av1_init_dsmotion_compensation")(cfg, stride, 0)
+        else:
+            tu.func("av1_init_motion_compensation_bigdia")(cfg, stride, 0)
+        cfgs[m] = cfg
+    mj = tu.buffer("int", out["mvjcost_lp"].tolist())
+    mc = [tu.buffer("int", out["mvcost_lp"][k].tolist()) for k in range(2)]
+    mc = [C.Pointer(c.buf, MV_MAX, c.ty) for c in mc]
+    mi_params = tu.struct_obj("CommonModeInfoParams")
+    _set(mi_params.buf[0], mi_rows=((H + 7) & ~7) // 4, mi_cols=((W + 7) & ~7) // 4)
+    rnd = ACMRandom(0xbaba + 4)
+    jobs = []
+    for (bw, bh, nblk) in MS_BLOCKS:
+        fn = tu.func
+        vtab = tu.struct_obj("aom_variance_fn_ptr_t")
+        sz = "%dx%d" % (bw, bh)
+        _set(vtab.buf[0], sdf=fn("aom_sad%s" % sz), sdsf=fn("aom_sad_skip_%s" % sz),
+             vf=fn("aom_variance%s" % sz), sdx4df=fn("aom_sad%sx4d" % sz),
+             sdx3df=fn("aom_sad%sx3d" % sz), sdsx4df=fn("aom_sad_skip_%sx4d" % sz))
+        bsize = E["BLOCK_%dX%d" % (bw, bh)]
+        for ci, (mname, use_cl, ctype, skip, step_param) in enumerate(MS_CASES):
+            for b in range(nblk):
+                by = rnd.generate(H // bh) * bh
+                bx = rnd.generate(W // bw) * bw
+                k = rnd.generate(NREF)
+                ref_mv = [(0, 0), (13, -21), (-40, 33), (24, 8), (-3, -77)][rnd.generate(5)]
+                lim = tu.struct_obj("FullMvLimits")
+                tu.func("av1_set_mv_limits")(mi_params, lim, by // 4, bx // 4, bh // 4, bw // 4,
+                                             BORDER)
+                rmv = tu.struct_obj("MV")
+                _set(rmv.buf[0], row=ref_mv[0], col=ref_mv[1])
+                tu.func("av1_set_mv_search_range")(lim, rmv)
+                L = lim.buf[0]
+                lims = [_get(L, f) for f in ("col_min", "col_max", "row_min", "row_max")]
+                start = ((ref_mv[0] + 4) >> 3, (ref_mv[1] + 4) >> 3) if b % 3 else \
+                    (rnd.generate(41) - 20, rnd.generate(41) - 20)
+                # buffers
+                sbuf = tu.struct_obj("struct buf_2d")
+                _set(sbuf.buf[0], buf=C.Pointer(src_buf.buf, org + by * stride + bx, C.UCHAR),
+                     stride=stride, width=bw, height=bh)
+                rbuf = tu.struct_obj("struct buf_2d")
+                _set(rbuf.buf[0], buf=C.Pointer(ref_bufs[k].buf, org + by * stride + bx, C.UCHAR),
+                     stride=stride, width=W, height=H)
+                ms = tu.struct_obj("FULLPEL_MOTION_SEARCH_PARAMS")
+                P = ms.buf[0]
+                _set(P, bsize=bsize, vfp=vtab, search_method=E[mname], search_sites=cfgs[mname],
+                     run_mesh_search=0, prune_mesh_search=0, mesh_search_mv_diff_threshold=4,
+                     force_mesh_thresh=0, fine_search_interval=0, is_intra_mode=0,
+                     fast_obmc_search=0)
+                msb = _get(P, "ms_buffers")
+                _set(msb, ref=rbuf, src=sbuf, second_pred=None, mask=None, mask_stride=0,
+                     inv_mask=0, wsrc=None, obmc_mask=None)
+                _set(P, mv_limits=C.copy_obj(L))
+                mcp = _get(P, "mv_cost_params")
+                fref = tu.func("get_fullmv_from_mv")(rmv)
+                _set(mcp, ref_mv=rmv, full_ref_mv=fref, mv_cost_type=E[ctype], mvjcost=mj,
+                     error_per_bit=31 + 7 * (b % 3), sad_per_bit=3 + (b % 4))
+                _get(mcp, "mvcost")[0], _get(mcp, "mvcost")[1] = mc[0], mc[1]
+                pre = "sds" if (skip and bh >= 16) else "sd"
+                vt = vtab.buf[0]
+                _set(P, sdf=_get(vt, "sdsf" if pre == "sds" else "sdf"),
+                     sdx4df=_get(vt, "sdsx4df" if pre == "sds" else "sdx4df"),
+                     sdx3df=_get(vt, "sdsx4df" if pre == "sds" else "sdx3df"))
+                smv = C.new_obj(tu.ctype("FULLPEL_MV"))
+                _set(smv, row=start[0], col=start[1])
+                best = tu.struct_obj("FULLPEL_MV")
+                cl = tu.buffer("int", [0x7FFFFFFF] * 5) if use_cl else None
+                var = tu.func("av1_full_pixel_search")(smv, ms, step_param, cl, best, None)
+                bm = best.buf[0]
+                jobs.append([bw, bh, ci, by, bx, k, ref_mv[0], ref_mv[1], start[0], start[1]] +
+                            lims + [_get(mcp, "error_per_bit"), _get(mcp, "sad_per_bit"),
+                                    _get(bm, "row"), _get(bm, "col"), var] +
+                            (list(cl.buf) if use_cl else [0x7FFFFFFF] * 5))
+        print("  mcomp %-7s %d jobs" % (sz, len(jobs)))
+    out["jobs"] = np.array(jobs, np.int64)
+    out["job_fields"] = np.array(["bw", "bh", "case", "by", "bx", "ref", "ref_mv_row",
+                                  "ref_mv_col", "start_row", "start_col", "col_min", "col_max",
+                                  "row_min", "row_max", "error_per_bit", "sad_per_bit",
+                                  "best_row", "best_col", "var", "cl0", "cl1", "cl2", "cl3",
+                                  "cl4"])
+    out["cases"] = np.array([[["DIAMOND", "BIGDIA", "FAST_BIGDIA"].index(m), cl,
+                              E[ct], sk, sp] for m, cl, ct, sk, sp in MS_CASES], np.int32)
+    np.savez_compressed(os.path.join(HERE, "fix_mcomp.npz"), **out)
+
+
 def main(argv):
-    sections = argv or ["txfm", "qparams", "quant", "inv", "pixel", "wht"]
+    sections = argv or ["txfm", "qparams", "quant", "inv", "pixel", "wht", "mcomp"]
     t0 = time.time()
     ttx = None
     if "txfm" in sections or "inv" in sections or "wht" in sections:
@@ -551,6 +713,8 @@ def main(argv):
         gen_pixel(tu_pixel())
     if "wht" in sections:
         gen_wht(ttx)
+    if "mcomp" in sections:
+        gen_mcomp()
     print("done in %.0fs" % (time.time() - t0))
 
 

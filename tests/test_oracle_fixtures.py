@@ -196,3 +196,59 @@ def test_wht_vs_reference():
                                  F["iwht1_out"]):
         np.testing.assert_array_equal(O.iwht4x4_add(c, d, 16, int(bd)), e16)
         np.testing.assert_array_equal(O.iwht4x4_add(c, d, 1, int(bd)), e1)
+
+
+# -------------------------------------------------------- motion search --
+MS_METHODS = ["diamond", "bigdia", "fast_bigdia"]   # fixture "cases" column 0
+MS_JOB = np.dtype([("src_off", "<i8"), ("ref_off", "<i8"), ("start_row", "<i2"),
+                   ("start_col", "<i2"), ("ref_mv_row", "<i2"), ("ref_mv_col", "<i2"),
+                   ("col_min", "<i2"), ("col_max", "<i2"), ("row_min", "<i2"),
+                   ("row_max", "<i2")], align=True)
+
+
+def mcomp_groups(F):
+    """Fixture jobs grouped by (case, block size, lambdas) -- the parameters
+    one batch call shares -- as (case row, bw, bh, epb, spb, JOB records,
+    expected rows)."""
+    J = {n: i for i, n in enumerate(F["job_fields"])}
+    jobs = F["jobs"]
+    W, H, BORDER, NREF = (int(v) for v in F["geom"])
+    stride = F["src"].shape[1]
+    plane = F["refs"][0].size
+    org = BORDER * stride + BORDER
+    key = lambda r: tuple(int(r[J[k]]) for k in ("case", "bw", "bh", "error_per_bit",
+                                                   "sad_per_bit"))
+    groups = {}
+    for r in jobs:
+        groups.setdefault(key(r), []).append(r)
+    for (ci, bw, bh, epb, spb), rows in sorted(groups.items()):
+        rows = np.array(rows)
+        rec = np.zeros(len(rows), MS_JOB)
+        off = org + rows[:, J["by"]] * stride + rows[:, J["bx"]]
+        rec["src_off"], rec["ref_off"] = off, off + rows[:, J["ref"]] * plane
+        for f in ("start_row", "start_col", "ref_mv_row", "ref_mv_col", "col_min", "col_max",
+                  "row_min", "row_max"):
+            rec[f] = rows[:, J[f]]
+        yield F["cases"][ci], bw, bh, epb, spb, rec, rows, J
+
+
+def test_full_pixel_search_vs_reference():
+    """orc_full_pixel_search_batch against av1_full_pixel_search executed from
+    the reference (DIAMOND / BIGDIA / FAST_BIGDIA, entropy / L1 / none mv
+    cost, downsampled SAD with its quality recheck, cost lists)."""
+    F = _load("fix_mcomp.npz")
+    stride = F["src"].shape[1]
+    n = 0
+    for case, bw, bh, epb, spb, rec, rows, J in mcomp_groups(F):
+        m, use_cl, ctype, skip, sp = (int(v) for v in case)
+        res, cl = O.full_pixel_search_batch(
+            F["src"], F["refs"], stride, bw, bh, rec, MS_METHODS[m], sp, ctype, spb, epb,
+            F["mvjcost_lp"], F["mvcost_lp"], skip=bool(skip), cost_list=bool(use_cl))
+        msg = "case %s %dx%d" % (list(case), bw, bh)
+        np.testing.assert_array_equal(res["best_row"], rows[:, J["best_row"]], err_msg=msg)
+        np.testing.assert_array_equal(res["best_col"], rows[:, J["best_col"]], err_msg=msg)
+        np.testing.assert_array_equal(res["bestsme"], rows[:, J["var"]], err_msg=msg)
+        if use_cl:
+            np.testing.assert_array_equal(cl, rows[:, J["cl0"]:J["cl4"] + 1], err_msg=msg)
+        n += len(rows)
+    assert n == len(F["jobs"])
