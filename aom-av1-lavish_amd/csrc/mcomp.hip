@@ -83,19 +83,33 @@ struct Ctx {
   int ref_mv_row, ref_mv_col, full_ref_row, full_ref_col;
   int cost_type;
   int sad_lambda, sse_lambda;  // per cost_type, hoisted out of the walk
+  int sad_per_bit, error_per_bit;  // MV_COST_ENTROPY
+  const int32_t* mvjcost;
+  const int32_t* mvcost0;  // centred at MV_MAX
+  const int32_t* mvcost1;
 };
 
 __device__ __forceinline__ int sad_lambda(int t) { return t == 1 ? 32 : t == 2 ? 15 : t == 3 ? 8 : 0; }
 __device__ __forceinline__ int sse_lambda(int t) { return t == 1 ? 2 : t == 2 ? 0 : t == 3 ? 1 : 0; }
 
-// mvsad_err_cost (mcomp.c:329-350) for the L1 types; 0 for MV_COST_NONE
+// mv_cost (mcomp.c:269-273) of a 1/8-pel diff: joint + row + col rates
+__device__ __forceinline__ int mv_rate(const Ctx& c, int dr, int dc) {
+  const int joint = (dc != 0) | ((dr != 0) << 1);  // av1_get_mv_joint
+  return c.mvjcost[joint] + c.mvcost0[dr] + c.mvcost1[dc];
+}
+
+// mvsad_err_cost (mcomp.c:329-350); the L1 lambdas are 0 for MV_COST_NONE
 __device__ __forceinline__ uint32_t mvsad_cost(const Ctx& c, int row, int col) {
   const int dr = (row - c.full_ref_row) * 8, dc = (col - c.full_ref_col) * 8;
+  if (c.cost_type == 0)  // ROUND_POWER_OF_TWO(., AV1_PROB_COST_SHIFT)
+    return ((uint32_t)mv_rate(c, dr, dc) * (uint32_t)c.sad_per_bit + 256u) >> 9;
   return (uint32_t)((c.sad_lambda * (abs(dr) + abs(dc))) >> 3);
 }
-// mv_err_cost (mcomp.c:287-314) for the L1 types
+// mv_err_cost (mcomp.c:290-314)
 __device__ __forceinline__ int mv_cost(const Ctx& c, int row, int col) {
   const int dr = row * 8 - c.ref_mv_row, dc = col * 8 - c.ref_mv_col;
+  if (c.cost_type == 0)  // RDDIV_BITS + AV1_PROB_COST_SHIFT - RD_EPB_SHIFT + 4 = 14
+    return (int)(((int64_t)mv_rate(c, dr, dc) * c.error_per_bit + 8192) >> 14);
   return (c.sse_lambda * (abs(dr) + abs(dc))) >> 3;
 }
 
@@ -147,6 +161,34 @@ __device__ int var_cost(const Ctx& c, int lane, int row, int col) {
     var_acc(a[0], b[0], sum, sse);
   }
   return var_finish<W, H>(c, sum, sse, row, col);
+}
+
+// sdf and sdsf (aom_sad / aom_sad_skip) at a full-pel mv in one pass: the
+// whole wave walks the block one word per lane; the skip SAD is twice the
+// SAD of the even rows
+template <int W, int H>
+__device__ void sad_and_skip(const Ctx& c, int lane, int row, int col, int& sad, int& ssad) {
+  constexpr int DW = W / 4;
+  uint32_t all = 0, even = 0;
+  const uint8_t* rb = c.ref + (int64_t)row * c.rs + col;
+  for (int i = lane; i < H * DW; i += 64) {
+    const int y = i / DW, x = i - y * DW;
+    uint32_t a[1], b[1];
+    load_row<1>(c.src + (int64_t)y * c.ss + 4 * x, a);
+    load_row<1>(rb + (int64_t)y * c.rs + 4 * x, b);
+    const uint32_t d = sad4(a[0], b[0], 0);
+    all += d;
+    even += (y & 1) ? 0u : d;
+  }
+  const uint32_t ga = group_sum8(all), ge = group_sum8(even);
+  uint32_t ta = rdlane(ga, 0), te = rdlane(ge, 0);
+#pragma unroll
+  for (int i = 1; i < 8; ++i) {
+    ta += rdlane(ga, 8 * i);
+    te += rdlane(ge, 8 * i);
+  }
+  sad = (int)ta;
+  ssad = (int)(2 * te);
 }
 
 typedef __attribute__((address_space(3))) uint32_t* lds_u32;
@@ -378,10 +420,45 @@ struct Search {
   }
 };
 
+// cl[i] = v for a wave-uniform but dynamic i, without a private-array index
+__device__ __forceinline__ void set_cl(int (&cl)[5], int i, int v) {
+#pragma unroll
+  for (int t = 0; t < 5; ++t) cl[t] = i == t ? v : cl[t];
+}
+
+// calc_int_sad_list (mcomp.c:789-841): cost list around (br, bc) -- centre,
+// left, bottom, right, top -- raw SADs (recomputed unless the pattern search
+// left them in cl) plus mvsad_err_cost; INT_MAX for out-of-range neighbours.
+// Groups 0..4 evaluate the five points at once.
+template <int W, int H, bool SKIP>
+__device__ void int_sad_list(const Search<W, H, SKIP>& S, const Ctx& c, int lane, int br, int bc,
+                             bool has_sad, int (&cl)[5]) {
+  const int g = lane >> 3;
+  if (!has_sad) {
+    const int dr = g == 2 ? 1 : g == 4 ? -1 : 0;
+    const int dc = g == 1 ? -1 : g == 3 ? 1 : 0;
+    const int r = br + dr, cc = bc + dc;
+    const bool all_in = br - 1 >= c.row_min && br + 1 <= c.row_max && bc - 1 >= c.col_min &&
+                        bc + 1 <= c.col_max;
+    const bool valid = g < 5 && (all_in || (cc >= c.col_min && cc <= c.col_max &&
+                                            r >= c.row_min && r <= c.row_max));
+    const uint32_t sad = S.group_sad(c, (int64_t)r * c.rs + cc, valid);
+    const uint32_t v = valid ? sad : 0x7FFFFFFFu;
+#pragma unroll
+    for (int i = 0; i < 5; ++i) cl[i] = (int)rdlane(v, 8 * i);
+  }
+  cl[0] += (int)mvsad_cost(c, br, bc);
+  if (cl[1] != INT_MAX) cl[1] += (int)mvsad_cost(c, br, bc - 1);
+  if (cl[2] != INT_MAX) cl[2] += (int)mvsad_cost(c, br + 1, bc);
+  if (cl[3] != INT_MAX) cl[3] += (int)mvsad_cost(c, br, bc + 1);
+  if (cl[4] != INT_MAX) cl[4] += (int)mvsad_cost(c, br - 1, bc);
+}
+
 // full_pixel_diamond (mcomp.c:1479-1526)
 template <int W, int H, bool SKIP>
 __device__ int full_pixel_diamond(const Ctx& c, int lane, int srow, int scol, int step_param,
-                                  int& brow, int& bcol, int& steps, int& searches, lds_u32 win) {
+                                  int& brow, int& bcol, int& steps, int& searches, lds_u32 win,
+                                  bool want_cl, int (&cl)[5]) {
   Search<W, H, SKIP> S;
   S.load_src(c, lane, win);
   int n, num00 = 0;
@@ -405,6 +482,7 @@ __device__ int full_pixel_diamond(const Ctx& c, int lane, int srow, int scol, in
       num00 = 0;
     }
   }
+  if (want_cl) int_sad_list(S, c, lane, brow, bcol, false, cl);
   return bestsme;
 }
 
@@ -425,81 +503,144 @@ __device__ __forceinline__ void bigdia_site(int s, int i, int& dr, int& dc) {
   dc = (i == 0 || i == 2) ? -r : (i == 4 || i == 6) ? r : (i == 1) ? -2 * r : (i == 5) ? 2 * r : 0;
 }
 
-// fast_bigdia_search -> bigdia_search -> pattern_search (mcomp.c:1017-1245,
-// 1266-1316) with do_init_search 0: from scale 10 - max(8, step_param) down
-// to 0, all candidates of the scale around the centre, then the 3 points
-// around the winning direction until none improves.  (With a cost list the
-// reference finishes scale 0 in a separate block whose mv result is the
-// same for do_init_search 0; the list itself is not produced here.)
+// pattern_search (mcomp.c:1017-1245) over the BIGDIA sites: with
+// do_init_search every scale up to the start scale around the start point
+// first (bigdia_search), else straight from the start scale (fast_bigdia /
+// fast_dia / vfast_dia); per scale all candidates, then the 3 points around
+// the winning direction until none improves.  With a cost list the last
+// scale runs in the reference's separate block that keeps the raw SADs of
+// the final neighbourhood (:1166-1221), then calc_int_sad_list.
 // Lane group g evaluates candidate g; the keyed minimum is the reference's
-// sequential update order (update_mvs_and_sad, mcomp.c:858-877).
+// sequential update order (update_mvs_and_sad, mcomp.c:858-877), whose raw
+// SAD is kept as raw_bestsad.
 template <int W, int H, bool SKIP>
-__device__ int fast_bigdia(const Ctx& c, int lane, int srow, int scol, int step_param, int& brow,
-                           int& bcol, int& steps) {
+__device__ int pattern(const Ctx& c, int lane, int srow, int scol, int search_step, bool do_init,
+                       bool want_cl, int (&cl)[5], int& brow, int& bcol, int& steps) {
   Search<W, H, SKIP> S;
   S.load_src(c, lane);
   const int g = lane >> 3;
-  const int search_step = min(max(kMaxSteps - 3, step_param), kMaxSteps - 1);
-  const int s0 = kMaxSteps - 1 - search_step;  // search_steps[] = {10, 9, ..., 0}
+  search_step = min(search_step, kMaxSteps - 1);
+  int best_init_s = kMaxSteps - 1 - search_step;  // search_steps[] = {10, 9, ..., 0}
   int br = min(max(srow, c.row_min), c.row_max);
   int bc = min(max(scol, c.col_min), c.col_max);
-  uint32_t best = mvsad_cost(c, br, bc) +
-                  rdlane(S.group_sad(c, (int64_t)br * c.rs + bc, true), 0);
-  for (int s = s0; s >= 0; --s) {
-    const int n = s == 0 ? 4 : 8;
-    // one round: candidate idx (groups g < cnt) around (br, bc) at scale s;
-    // returns the winning group or -1
-    auto check = [&](int cnt, int idx) -> int {
-      const bool all_in = br - (1 << s) >= c.row_min && br + (1 << s) <= c.row_max &&
-                          bc - (1 << s) >= c.col_min && bc + (1 << s) <= c.col_max;
-      int dr, dc;
-      bigdia_site(s, idx, dr, dc);
-      const int r = br + dr, cc = bc + dc;
-      const bool valid = g < cnt && (all_in || (cc >= c.col_min && cc <= c.col_max &&
-                                                r >= c.row_min && r <= c.row_max));
-      const uint32_t mine = S.group_sad(c, (int64_t)r * c.rs + cc, valid);
-      const uint32_t key = valid ? ((mine + mvsad_cost(c, r, cc)) << 3) | (uint32_t)g : ~0u;
-      uint32_t kmin = rdlane(key, 0);
+  if (want_cl) cl[0] = cl[1] = cl[2] = cl[3] = cl[4] = INT_MAX;
+  bool has_sad = false;
+  uint32_t raw = rdlane(S.group_sad(c, (int64_t)br * c.rs + bc, true), 0);
+  uint32_t best = raw + mvsad_cost(c, br, bc);
+  // one round: candidate idx (groups g < cnt) of scale s around (br, bc);
+  // returns the winning group or -1.  clmode 1: raw SADs of the valid
+  // candidates into cl (calc_sad4 / calc_sad_update_bestmv); 2: also INT_MAX
+  // for invalid ones (calc_sad3 / _with_indices)
+  auto check = [&](int s, int cnt, int idx, int clmode) -> int {
+    const bool all_in = br - (1 << s) >= c.row_min && br + (1 << s) <= c.row_max &&
+                        bc - (1 << s) >= c.col_min && bc + (1 << s) <= c.col_max;
+    int dr, dc;
+    bigdia_site(s, idx, dr, dc);
+    const int r = br + dr, cc = bc + dc;
+    const bool valid = g < cnt && (all_in || (cc >= c.col_min && cc <= c.col_max &&
+                                              r >= c.row_min && r <= c.row_max));
+    const uint32_t mine = S.group_sad(c, (int64_t)r * c.rs + cc, valid);
+    const uint32_t key = valid ? ((mine + mvsad_cost(c, r, cc)) << 3) | (uint32_t)g : ~0u;
+    uint32_t kmin = rdlane(key, 0);
 #pragma unroll
-      for (int i = 1; i < 8; ++i) kmin = min(kmin, rdlane(key, 8 * i));
-      ++steps;
-      if (kmin >= (best << 3)) return -1;
-      best = kmin >> 3;
-      return (int)(kmin & 7);
-    };
-    int k = check(n, g < n ? g : 0);
-    if (k < 0) continue;
-    {
-      int dr, dc;
-      bigdia_site(s, k, dr, dc);
-      br += dr;
-      bc += dc;
+    for (int i = 1; i < 8; ++i) kmin = min(kmin, rdlane(key, 8 * i));
+    ++steps;
+    if (clmode) {
+      const uint32_t tag = valid ? (mine << 1) | 1u : 0u;  // SADs < 2^22
+      for (int i = 0; i < cnt; ++i) {
+        const uint32_t t = rdlane(tag, 8 * i);
+        const int ix = (int)rdlane((uint32_t)idx, 8 * i);
+        if (t & 1u) set_cl(cl, ix + 1, (int)(t >> 1));
+        else if (clmode == 2) set_cl(cl, ix + 1, INT_MAX);
+      }
     }
-    while (true) {
-      // next_chkpts_indices: k - 1, k, k + 1 (cyclic)
-      const int idx = g == 0 ? (k == 0 ? n - 1 : k - 1) : g == 1 ? k : (k == n - 1 ? 0 : k + 1);
-      const int j = check(3, idx);
-      if (j < 0) break;
-      k = j == 0 ? (k == 0 ? n - 1 : k - 1) : j == 1 ? k : (k == n - 1 ? 0 : k + 1);
-      int dr, dc;
-      bigdia_site(s, k, dr, dc);
-      br += dr;
-      bc += dc;
+    if (kmin >= (best << 3)) return -1;
+    best = kmin >> 3;
+    raw = rdlane(mine, 8 * (int)(kmin & 7));
+    return (int)(kmin & 7);
+  };
+  auto move = [&](int s, int k) {
+    int dr, dc;
+    bigdia_site(s, k, dr, dc);
+    br += dr;
+    bc += dc;
+  };
+  // next_chkpts_indices: k - 1, k, k + 1 (cyclic over n)
+  auto around = [](int j, int k, int n) {
+    return j == 0 ? (k == 0 ? n - 1 : k - 1) : j == 1 ? k : (k == n - 1 ? 0 : k + 1);
+  };
+  int k = -1;
+  if (do_init) {
+    const int smax = best_init_s;
+    best_init_s = -1;
+    for (int t = 0; t <= smax; ++t) {
+      const int w = check(t, t == 0 ? 4 : 8, g, 0);
+      if (w < 0) continue;
+      best_init_s = t;
+      k = w;
+    }
+    if (best_init_s != -1) move(best_init_s, k);
+  }
+  if (best_init_s != -1) {
+    const int last_s = want_cl ? 1 : 0;  // num_candidates[0] == 4 for BIGDIA
+    int best_site = -1;
+    int s = best_init_s;
+    for (; s >= last_s; --s) {
+      const int n = s == 0 ? 4 : 8;
+      if (!do_init || s != best_init_s) {
+        best_site = check(s, n, g, 0);
+        if (best_site < 0) continue;
+        move(s, best_site);
+        k = best_site;
+      }
+      do {
+        best_site = check(s, 3, around(g, k, n), 0);
+        if (best_site >= 0) {
+          k = around(best_site, k, n);
+          move(s, k);
+        }
+      } while (best_site >= 0);
+    }
+    if (s == 0 && want_cl) {
+      cl[0] = (int)raw;
+      has_sad = true;
+      if (!do_init || s != best_init_s) {
+        best_site = check(0, 4, g, 1);
+        if (best_site >= 0) {
+          move(0, best_site);
+          k = best_site;
+        }
+      }
+      while (best_site >= 0) {
+        cl[1] = cl[2] = cl[3] = cl[4] = INT_MAX;
+        set_cl(cl, ((k + 2) & 3) + 1, cl[0]);
+        cl[0] = (int)raw;
+        best_site = check(0, 3, around(g, k, 4), 2);
+        if (best_site >= 0) {
+          k = around(best_site, k, 4);
+          move(0, k);
+        }
+      }
     }
   }
   brow = br;
   bcol = bc;
+  if (want_cl) int_sad_list(S, c, lane, br, bc, has_sad, cl);
   return var_cost<W, H>(c, lane, br, bc);  // get_mvpred_var_cost
 }
 
+// search_method values of SEARCH_METHODS (av1/encoder/mcomp_structs.h:56-86)
+enum { kDiamond = 0, kBigdia = 5, kFastDiamond = 8, kFastBigdia = 9, kVfastDiamond = 10 };
 
-template <int W, int H>
+// PAT: the BIGDIA-site pattern searches (method 5 / 8 / 9 / 10), else DIAMOND
+template <int W, int H, bool PAT>
 __global__ __launch_bounds__(256, 7) void diamond_kernel(const uint8_t* __restrict__ src, int ss,
                                                       const uint8_t* __restrict__ ref, int rs,
                                                       const Job* __restrict__ jobs, int njobs,
-                                                      int step_param, int cost_type, int skip,
-                                                      int method,
-                                                      LavishDiamondResult* __restrict__ out) {
+                                                      int step_param, LavishMvCostParams cost,
+                                                      int skip, int method,
+                                                      LavishDiamondResult* __restrict__ out,
+                                                      int32_t* __restrict__ cost_lists) {
   // XCD-aware: consecutive job quads (neighbouring blocks) share an XCD's L2
   const int nwg = gridDim.x;  // multiple of 8
   const int wg = (blockIdx.x & 7) * (nwg >> 3) + (blockIdx.x >> 3);
@@ -507,8 +648,9 @@ __global__ __launch_bounds__(256, 7) void diamond_kernel(const uint8_t* __restri
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int j = wg * 4 + wave;
   if (j >= njobs) return;
-  __shared__ uint32_t win_s[4 * Win<W, H>::SIZE];
-  const lds_u32 win = Win<W, H>::kOn ? (lds_u32)(win_s + wave * Win<W, H>::SIZE) : nullptr;
+  constexpr int WS = PAT ? 1 : Win<W, H>::SIZE;  // the window serves DIAMOND only
+  __shared__ uint32_t win_s[4 * WS];
+  const lds_u32 win = (!PAT && Win<W, H>::kOn) ? (lds_u32)(win_s + wave * WS) : nullptr;
   const Job jb = jobs[j];
   Ctx c;
   c.src = src + jb.src_off;
@@ -523,31 +665,39 @@ __global__ __launch_bounds__(256, 7) void diamond_kernel(const uint8_t* __restri
   c.ref_mv_col = jb.ref_mv_col;
   c.full_ref_row = rawpel(jb.ref_mv_row);
   c.full_ref_col = rawpel(jb.ref_mv_col);
-  c.cost_type = cost_type;
-  c.sad_lambda = sad_lambda(cost_type);
-  c.sse_lambda = sse_lambda(cost_type);
+  c.cost_type = cost.mv_cost_type;
+  c.sad_lambda = sad_lambda(cost.mv_cost_type);
+  c.sse_lambda = sse_lambda(cost.mv_cost_type);
+  c.sad_per_bit = cost.sad_per_bit;
+  c.error_per_bit = cost.error_per_bit;
+  c.mvjcost = cost.mvjcost;
+  c.mvcost0 = cost.mvcost[0];
+  c.mvcost1 = cost.mvcost[1];
+  const bool want_cl = cost_lists != nullptr;
+  int cl[5] = {INT_MAX, INT_MAX, INT_MAX, INT_MAX, INT_MAX};
   int br, bc, steps = 0, searches = 0, sme;
-  // method 0: DIAMOND (full_pixel_diamond), 1: FAST_BIGDIA (pattern_search)
   auto search = [&](auto skip_tag) {
     constexpr bool SK = decltype(skip_tag)::value;
-    if (method == 0)
+    if constexpr (!PAT) {
       return full_pixel_diamond<W, H, SK>(c, lane, jb.start_row, jb.start_col, step_param, br,
-                                          bc, steps, searches, win);
-    ++searches;
-    return fast_bigdia<W, H, SK>(c, lane, jb.start_row, jb.start_col, step_param, br, bc,
-                                 steps);
+                                          bc, steps, searches, win, want_cl, cl);
+    } else {
+      ++searches;
+      // bigdia_search (do_init 1) / fast_dia / vfast_dia / fast_bigdia (mcomp.c:1266-1316)
+      const int step = method == kBigdia        ? step_param
+                       : method == kFastDiamond ? max(kMaxSteps - 2, step_param)
+                       : method == kVfastDiamond ? max(kMaxSteps - 1, step_param)
+                                                 : max(kMaxSteps - 3, step_param);
+      return pattern<W, H, SK>(c, lane, jb.start_row, jb.start_col, step, method == kBigdia,
+                               want_cl, cl, br, bc, steps);
+    }
   };
   // use_downsampled_sad applies to blocks at least 16 high (mcomp.c:132-133)
   if (skip && H >= 16) {
     sme = search(std::true_type{});
     // quality check of the row-skipping search (mcomp.c:1840-1867)
-    Search<W, H, false> F;
-    F.load_src(c, lane);
-    const int64_t off = (int64_t)br * rs + bc;
-    const int sad = (int)rdlane(F.group_sad(c, off, true), 0);
-    Search<W, H, true> K;
-    K.load_src(c, lane);
-    const int ssad = (int)rdlane(K.group_sad(c, off, true), 0);
+    int sad, ssad;
+    sad_and_skip<W, H>(c, lane, br, bc, sad, ssad);
     const int thresh = (W >> 2) * (H >> 2);
     if (sad > thresh && abs(ssad - sad) * 10 >= max(sad, 1) * 9) sme = search(std::false_type{});
   } else {
@@ -562,29 +712,47 @@ __global__ __launch_bounds__(256, 7) void diamond_kernel(const uint8_t* __restri
     r.searches = searches;
     out[j] = r;
   }
+  if (want_cl && lane < 5) {
+    const int v = lane == 0 ? cl[0] : lane == 1 ? cl[1] : lane == 2 ? cl[2] : lane == 3 ? cl[3] : cl[4];
+    cost_lists[5 * (int64_t)j + lane] = v;
+  }
 }
 
 template <int W, int H>
 void launch(const uint8_t* src, int ss, const uint8_t* ref, int rs, const LavishDiamondJob* jobs,
-            int njobs, int step_param, int cost_type, int skip, int method,
-            LavishDiamondResult* out, hipStream_t s) {
+            int njobs, int step_param, const LavishMvCostParams& cost, int skip, int method,
+            LavishDiamondResult* out, int32_t* cost_lists, hipStream_t s) {
   int nwg = (njobs + 3) / 4;
   nwg = (nwg + 7) & ~7;
-  hipLaunchKernelGGL((diamond_kernel<W, H>), dim3(nwg), dim3(256), 0, s, src, ss, ref, rs,
-                     (const Job*)jobs, njobs, step_param, cost_type, skip, method, out);
+  if (method == kDiamond)
+    hipLaunchKernelGGL((diamond_kernel<W, H, false>), dim3(nwg), dim3(256), 0, s, src, ss, ref,
+                       rs, (const Job*)jobs, njobs, step_param, cost, skip, method, out,
+                       cost_lists);
+  else
+    hipLaunchKernelGGL((diamond_kernel<W, H, true>), dim3(nwg), dim3(256), 0, s, src, ss, ref,
+                       rs, (const Job*)jobs, njobs, step_param, cost, skip, method, out,
+                       cost_lists);
 }
 
+}  // namespace
+
 int fullpel_batch(const uint8_t* src, int src_stride, const uint8_t* ref, int ref_stride, int w,
-                  int h, const LavishDiamondJob* jobs, int njobs, int step_param,
-                  int mv_cost_type, int use_downsampled_sad, int method,
-                  LavishDiamondResult* out, hipStream_t s) {
+                  int h, const LavishDiamondJob* jobs, int njobs, int method, int step_param,
+                  const LavishMvCostParams* cost, int use_downsampled_sad,
+                  LavishDiamondResult* out, int32_t* cost_lists, hipStream_t s) {
   if (njobs <= 0) return 0;
   if (step_param < 0 || step_param >= kMaxSteps) return -1;
-  if (mv_cost_type < 1 || mv_cost_type > 4) return -2;  // MV_COST_ENTROPY not supported
+  if (cost == nullptr || cost->mv_cost_type < 0 || cost->mv_cost_type > 4) return -2;
+  if (cost->mv_cost_type == 0 &&
+      (cost->mvjcost == nullptr || cost->mvcost[0] == nullptr || cost->mvcost[1] == nullptr))
+    return -2;
+  if (method != kDiamond && method != kBigdia && method != kFastDiamond &&
+      method != kFastBigdia && method != kVfastDiamond)
+    return -4;
 #define LAVISH_DIA_CASE(W, H)                                                                 \
   if (w == W && h == H) {                                                                     \
-    launch<W, H>(src, src_stride, ref, ref_stride, jobs, njobs, step_param, mv_cost_type,     \
-                 use_downsampled_sad, method, out, s);                                        \
+    launch<W, H>(src, src_stride, ref, ref_stride, jobs, njobs, step_param, *cost,            \
+                 use_downsampled_sad, method, out, cost_lists, s);                            \
     LAVISH_CHECK(hipGetLastError());                                                          \
     return 0;                                                                                 \
   }
@@ -593,10 +761,28 @@ int fullpel_batch(const uint8_t* src, int src_stride, const uint8_t* ref, int re
   return -3;
 }
 
-}  // namespace
 }  // namespace lavish
 
 using namespace lavish;
+
+static LavishMvCostParams l1_cost(int mv_cost_type) {
+  LavishMvCostParams c = {};
+  // the L1 entry points never took MV_COST_ENTROPY (it needs the tables)
+  c.mv_cost_type = mv_cost_type == 0 ? -1 : mv_cost_type;
+  return c;
+}
+
+extern "C" int lavish_full_pixel_search_batch(const uint8_t* src, int src_stride,
+                                              const uint8_t* ref, int ref_stride, int w, int h,
+                                              const LavishDiamondJob* jobs, int njobs,
+                                              int search_method, int step_param,
+                                              const LavishMvCostParams* cost,
+                                              int use_downsampled_sad, LavishDiamondResult* out,
+                                              int32_t* cost_lists, void* stream) {
+  return fullpel_batch(src, src_stride, ref, ref_stride, w, h, jobs, njobs, search_method,
+                       step_param, cost, use_downsampled_sad, out, cost_lists,
+                       (hipStream_t)stream);
+}
 
 extern "C" int lavish_diamond_search_batch(const uint8_t* src, int src_stride, const uint8_t* ref,
                                            int ref_stride, int w, int h,
@@ -604,8 +790,9 @@ extern "C" int lavish_diamond_search_batch(const uint8_t* src, int src_stride, c
                                            int step_param, int mv_cost_type,
                                            int use_downsampled_sad, LavishDiamondResult* out,
                                            void* stream) {
-  return fullpel_batch(src, src_stride, ref, ref_stride, w, h, jobs, njobs, step_param,
-                       mv_cost_type, use_downsampled_sad, 0, out, (hipStream_t)stream);
+  const LavishMvCostParams c = l1_cost(mv_cost_type);
+  return fullpel_batch(src, src_stride, ref, ref_stride, w, h, jobs, njobs, kDiamond, step_param,
+                       &c, use_downsampled_sad, out, nullptr, (hipStream_t)stream);
 }
 
 extern "C" int lavish_fast_bigdia_search_batch(const uint8_t* src, int src_stride,
@@ -614,6 +801,7 @@ extern "C" int lavish_fast_bigdia_search_batch(const uint8_t* src, int src_strid
                                                int step_param, int mv_cost_type,
                                                int use_downsampled_sad,
                                                LavishDiamondResult* out, void* stream) {
-  return fullpel_batch(src, src_stride, ref, ref_stride, w, h, jobs, njobs, step_param,
-                       mv_cost_type, use_downsampled_sad, 1, out, (hipStream_t)stream);
+  const LavishMvCostParams c = l1_cost(mv_cost_type);
+  return fullpel_batch(src, src_stride, ref, ref_stride, w, h, jobs, njobs, kFastBigdia,
+                       step_param, &c, use_downsampled_sad, out, nullptr, (hipStream_t)stream);
 }

@@ -18,7 +18,11 @@ RESULT_DTYPE = np.dtype([("best_row", "<i2"), ("best_col", "<i2"), ("bestsme", "
                          ("steps", "<i4"), ("searches", "<i4")], align=True)
 assert JOB_DTYPE.itemsize == 32 and RESULT_DTYPE.itemsize == 16
 
-MV_COST_L1_LOWRES, MV_COST_L1_MIDRES, MV_COST_L1_HDRES, MV_COST_NONE = 1, 2, 3, 4
+MV_COST_ENTROPY, MV_COST_L1_LOWRES, MV_COST_L1_MIDRES, MV_COST_L1_HDRES, MV_COST_NONE = range(5)
+# SEARCH_METHODS (av1/encoder/mcomp_structs.h:56-86) the full-pel search takes
+SEARCH_METHODS = {"diamond": 0, "bigdia": 5, "fast_diamond": 8, "fast_bigdia": 9,
+                  "vfast_diamond": 10}
+MV_MAX = (1 << 14) - 1
 MI_SIZE = 4
 AOM_INTERP_EXTEND = 4
 MAX_FULL_PEL_VAL = (1 << 10) - 1   # mcomp.h: (1 << (MAX_MVSEARCH_STEPS - 1)) - 1
@@ -30,6 +34,45 @@ _lib.lavish_diamond_search_batch.argtypes = [_vp, _i32, _vp, _i32, _i32, _i32, _
 _lib.lavish_diamond_search_batch.restype = _i32
 _lib.lavish_fast_bigdia_search_batch.argtypes = _lib.lavish_diamond_search_batch.argtypes
 _lib.lavish_fast_bigdia_search_batch.restype = _i32
+
+
+class MvCostParams(ctypes.Structure):
+    """LavishMvCostParams: MV_COST_PARAMS with device table pointers."""
+    _fields_ = [("mv_cost_type", ctypes.c_int32), ("sad_per_bit", ctypes.c_int32),
+                ("error_per_bit", ctypes.c_int32), ("reserved", ctypes.c_int32),
+                ("mvjcost", ctypes.c_void_p), ("mvcost", ctypes.c_void_p * 2)]
+
+
+_lib.lavish_full_pixel_search_batch.argtypes = [_vp, _i32, _vp, _i32, _i32, _i32, _vp, _i32,
+                                                _i32, _i32, ctypes.POINTER(MvCostParams), _i32,
+                                                _vp, _vp, _vp]
+_lib.lavish_full_pixel_search_batch.restype = _i32
+
+
+class MvCosts:
+    """Device copy of an nmv cost context (x->mv_costs): mvjcost int32[4] and
+    mvcost int32[2][2 * MV_MAX + 1] as av1_build_nmv_cost_table lays them
+    out; cost_params() makes the LavishMvCostParams for a search."""
+
+    def __init__(self, mvjcost, mvcost, device="cuda"):
+        import torch
+        mvcost = np.ascontiguousarray(mvcost, np.int32)
+        if mvcost.shape != (2, 2 * MV_MAX + 1) or np.shape(mvjcost) != (4,):
+            raise ValueError("mvjcost[4] and mvcost[2][%d] expected" % (2 * MV_MAX + 1))
+        self.mvjcost = torch.from_numpy(np.ascontiguousarray(mvjcost, np.int32)).to(device)
+        self.mvcost = torch.from_numpy(mvcost).to(device)
+
+    def cost_params(self, sad_per_bit, error_per_bit, mv_cost_type=MV_COST_ENTROPY):
+        c = MvCostParams(mv_cost_type, sad_per_bit, error_per_bit, 0)
+        c.mvjcost = self.mvjcost.data_ptr()
+        row = self.mvcost.stride(0) * 4
+        c.mvcost[0] = self.mvcost.data_ptr() + 4 * MV_MAX
+        c.mvcost[1] = self.mvcost.data_ptr() + row + 4 * MV_MAX
+        return c
+
+
+def l1_cost_params(mv_cost_type=MV_COST_L1_HDRES):
+    return MvCostParams(mv_cost_type, 0, 0, 0)
 
 
 def block_mv_limits(mi_rows, mi_cols, mi_row, mi_col, mi_height, mi_width, border):
@@ -125,6 +168,31 @@ def diamond_search_batch(src, ref, w, h, jobs, step_param=0, mv_cost_type=MV_COS
     if rc != 0:
         raise ValueError("lavish_diamond_search_batch rejected its arguments (rc=%d)" % rc)
     return out
+
+
+def full_pixel_search_batch(src, ref, w, h, jobs, cost, method="diamond", step_param=0,
+                            use_downsampled_sad=False, cost_list=False, out=None,
+                            cost_lists=None, stream=None):
+    """lavish_full_pixel_search_batch (av1_full_pixel_search): planes and jobs
+    as diamond_search_batch, cost a MvCostParams (MvCosts.cost_params or
+    l1_cost_params).  Returns (RESULT_DTYPE byte tensor, int32 [n, 5] cost
+    lists or None)."""
+    import torch
+    assert src.dtype == torch.uint8 and ref.dtype == torch.uint8
+    assert src.is_contiguous() and ref.is_contiguous(), "planes must be C-contiguous"
+    nj = jobs.numel() // JOB_DTYPE.itemsize
+    if out is None:
+        out = torch.empty(nj * RESULT_DTYPE.itemsize, dtype=torch.uint8, device=src.device)
+    if cost_list and cost_lists is None:
+        cost_lists = torch.empty((nj, 5), dtype=torch.int32, device=src.device)
+    rc = _lib.lavish_full_pixel_search_batch(
+        _vp(src.data_ptr()), src.stride(0), _vp(ref.data_ptr()), src.stride(0), w, h,
+        _vp(jobs.data_ptr()), nj, SEARCH_METHODS[method], step_param, ctypes.byref(cost),
+        int(use_downsampled_sad), _vp(out.data_ptr()),
+        _vp(cost_lists.data_ptr()) if cost_list else None, _stream_ptr(stream))
+    if rc != 0:
+        raise ValueError("lavish_full_pixel_search_batch rejected its arguments (rc=%d)" % rc)
+    return out, (cost_lists if cost_list else None)
 
 
 def results_numpy(out):

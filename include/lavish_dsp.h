@@ -389,6 +389,41 @@ int lavish_fast_bigdia_search_batch(const uint8_t *src, int src_stride,
                                     int mv_cost_type, int use_downsampled_sad,
                                     LavishDiamondResult *out, void *stream);
 
+/* MV_COST_PARAMS (av1/encoder/mcomp.h:69-85) for any mv_cost_type.  The
+ * tables are DEVICE pointers: mvjcost[MV_JOINTS] and mvcost[0] / [1] at the
+ * centre (index MV_MAX = 16383) of 2 * MV_MAX + 1 entries each, as
+ * x->mv_costs->mv_cost_stack is addressed (av1/encoder/block.h); needed for
+ * MV_COST_ENTROPY only.  sad_per_bit / error_per_bit: x->sadperbit /
+ * x->errorperbit (av1_set_error_per_bit / av1_set_sad_per_bit). */
+typedef struct LavishMvCostParams {
+  int32_t mv_cost_type; /* MV_COST_TYPE: 0 ENTROPY, 1..3 L1_{LOW,MID,HD}RES, 4 NONE */
+  int32_t sad_per_bit;
+  int32_t error_per_bit;
+  int32_t reserved;
+  const int32_t *mvjcost;
+  const int32_t *mvcost[2];
+} LavishMvCostParams;
+
+/* av1_full_pixel_search (av1/encoder/mcomp.c:1755-1873, no mesh refinement)
+ * for search_method (SEARCH_METHODS, mcomp_structs.h:56-86) DIAMOND 0,
+ * BIGDIA 5 (pattern_search with do_init_search), FAST_DIAMOND 8,
+ * FAST_BIGDIA 9, VFAST_DIAMOND 10 (BIGDIA sites, do_init_search 0, start
+ * scale clamps of :1291-1316), any mv cost (cost: HOST pointer to the
+ * parameters), the downsampled-SAD recheck, and -- when cost_lists (device,
+ * int32 [njobs][5]) is not NULL -- the cost list the reference returns for
+ * the sub-pel search (calc_int_sad_list: centre, left, bottom, right, top;
+ * INT_MAX where out of range); passing a cost list changes the BIGDIA-family
+ * walk exactly as in the reference (last_s).  Returns 0, -1 bad step_param,
+ * -2 bad cost parameters, -3 unsupported w x h, -4 unsupported method. */
+int lavish_full_pixel_search_batch(const uint8_t *src, int src_stride,
+                                   const uint8_t *ref, int ref_stride, int w,
+                                   int h, const LavishDiamondJob *jobs,
+                                   int njobs, int search_method, int step_param,
+                                   const LavishMvCostParams *cost,
+                                   int use_downsampled_sad,
+                                   LavishDiamondResult *out, int32_t *cost_lists,
+                                   void *stream);
+
 /* ---- sub-pixel refinement ------------------------
  * av1_find_best_sub_pixel_tree_pruned_more (av1/encoder/mcomp.c:2907-2981;
  * subpel_search_method SUBPEL_TREE_PRUNED_MORE, speed >= 4) without a cost

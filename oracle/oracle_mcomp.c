@@ -352,11 +352,15 @@ int orc_full_pixel_search(const OrcMsParams *p, int method, int start_row, int s
       var = full_pixel_diamond(p, start_row, start_col, step_param, skip, cl, best_row, best_col,
                                steps);
     } else {
-      /* fast_bigdia_search: AOMMAX(MAX_MVSEARCH_STEPS - 3, step_param), do_init 0;
-       * bigdia_search: step_param, do_init 1 */
-      const int fast = method == ORC_FAST_BIGDIA;
-      const int ss = fast ? (step_param > MAX_STEPS - 3 ? step_param : MAX_STEPS - 3) : step_param;
-      var = pattern_search(p, start_row, start_col, ss, !fast, skip, cl, best_row, best_col,
+      /* bigdia_search: step_param, do_init 1; fast_dia / vfast_dia /
+       * fast_bigdia: AOMMAX(MAX_MVSEARCH_STEPS - 2 / 1 / 3, step_param),
+       * do_init 0 (mcomp.c:1266-1316) */
+      const int floor = method == ORC_FAST_DIAMOND ? MAX_STEPS - 2
+                        : method == ORC_VFAST_DIAMOND ? MAX_STEPS - 1
+                        : MAX_STEPS - 3;
+      const int init = method == ORC_BIGDIA;
+      const int ss = init ? step_param : (step_param > floor ? step_param : floor);
+      var = pattern_search(p, start_row, start_col, ss, init, skip, cl, best_row, best_col,
                            steps);
     }
     if (!skip) return var;

@@ -1,0 +1,66 @@
+"""GPU parity of lavish_full_pixel_search_batch against av1_full_pixel_search
+executed from the reference (tests/golden/fix_mcomp.npz, made by
+tests/golden/gen_fixtures.py): DIAMOND, BIGDIA (do_init_search 1) and
+FAST_BIGDIA, MV_COST_ENTROPY with the default-context nmv cost tables, L1 and
+none, with and without the downsampled-SAD speed feature (and its quality
+recheck) and with and without a cost list -- best mv, returned var cost and
+the five cost-list entries bit-exact.  No oracle in the loop."""
+import os
+
+import numpy as np
+import pytest
+
+from _mcomp_fix import MS_METHODS, mcomp_groups
+
+pytestmark = pytest.mark.gpu
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+@pytest.fixture(scope="module")
+def F():
+    return dict(np.load(os.path.join(GOLD, "fix_mcomp.npz")))
+
+
+def test_full_pixel_search_vs_reference(F):
+    import torch
+    assert torch.cuda.is_available()
+    from lavish_dsp import motion as M
+    src = torch.from_numpy(F["src"]).cuda()
+    refs = torch.from_numpy(np.ascontiguousarray(F["refs"])).cuda()
+    costs = M.MvCosts(F["mvjcost_lp"], F["mvcost_lp"])
+    n = 0
+    for case, bw, bh, epb, spb, rec, rows, J in mcomp_groups(F):
+        m, use_cl, ctype, skip, sp = (int(v) for v in case)
+        cp = costs.cost_params(spb, epb, ctype)
+        out, cl = M.full_pixel_search_batch(src, refs, bw, bh, M.to_device(rec), cp,
+                                            MS_METHODS[m], sp, bool(skip), bool(use_cl))
+        torch.cuda.synchronize()
+        res = M.results_numpy(out)
+        msg = "case %s %dx%d" % ([int(v) for v in case], bw, bh)
+        np.testing.assert_array_equal(res["best_row"], rows[:, J["best_row"]], err_msg=msg)
+        np.testing.assert_array_equal(res["best_col"], rows[:, J["best_col"]], err_msg=msg)
+        np.testing.assert_array_equal(res["bestsme"], rows[:, J["var"]], err_msg=msg)
+        if use_cl:
+            np.testing.assert_array_equal(cl.cpu().numpy(), rows[:, J["cl0"]:J["cl4"] + 1],
+                                          err_msg=msg)
+        n += len(rows)
+    assert n == len(F["jobs"])
+
+
+def test_full_pixel_search_rejects(F):
+    """Entropy cost without tables, unknown search methods and bad step
+    params are refused (no launch)."""
+    import torch
+    from lavish_dsp import motion as M
+    src = torch.zeros((64, 64), dtype=torch.uint8, device="cuda")
+    jobs = M.to_device(np.zeros(1, M.JOB_DTYPE))
+    with pytest.raises(ValueError, match="rc=-2"):
+        M.full_pixel_search_batch(src, src, 8, 8, jobs, M.MvCostParams(0, 4, 40, 0))
+    import ctypes
+    # CLAMPED_DIAMOND (3) is not served: refused before any launch
+    rc = M._lib.lavish_full_pixel_search_batch(None, 64, None, 64, 8, 8, None, 1, 3, 0,
+                                               ctypes.byref(M.l1_cost_params()), 0, None, None,
+                                               None)
+    assert rc == -4
+    with pytest.raises(ValueError, match="rc=-1"):
+        M.full_pixel_search_batch(src, src, 8, 8, jobs, M.l1_cost_params(), step_param=11)
