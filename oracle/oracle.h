@@ -254,6 +254,14 @@ void orc_subpel_batch(const uint8_t *src, int src_stride, const uint8_t *ref,
                       long njobs, int forced_stop, int allow_hp,
                       int iters_per_step, int mv_cost_type,
                       OrcSubpelResult *out, int threads);
+/* any subpel method (1 SUBPEL_TREE_PRUNED, 2 SUBPEL_TREE_PRUNED_MORE), any
+ * mv cost, optional full-pel cost lists (cost_lists[job][5], the full-pel
+ * search's) */
+void orc_subpel_search_batch(const uint8_t *src, int src_stride, const uint8_t *ref,
+                             int ref_stride, int w, int h, const OrcSubpelJob *jobs, long njobs,
+                             int subpel_method, int forced_stop, int allow_hp,
+                             int iters_per_step, const OrcMvCost *cost,
+                             const int32_t *cost_lists, OrcSubpelResult *out, int threads);
 
 /* ---- TX-type pruning features (oracle_txfeat.c) ---- */
 void orc_horver_correlation_full(const int16_t *diff, int stride, int width,

@@ -1,9 +1,12 @@
 /* oracle_subpel.c -- TEST INFRASTRUCTURE ONLY (see oracle.h).
  *
  * CPU restatement of the sub-pixel motion refinement the encoder runs after
- * the full-pel search at speed >= 4:
- *   av1_find_best_sub_pixel_tree_pruned_more  av1/encoder/mcomp.c:2907-2981
- *     (cost_list NULL, last_mv_search_list NULL, unscaled reference)
+ * the full-pel search:
+ *   av1_find_best_sub_pixel_tree_pruned_more  av1/encoder/mcomp.c:2907-2990
+ *   av1_find_best_sub_pixel_tree_pruned       av1/encoder/mcomp.c:2992-3126
+ *     (last_mv_search_list NULL, unscaled reference), with the full-pel
+ *     search's cost list: is_cost_list_wellbehaved / get_cost_surf_min
+ *     (:2857-2876) for pruned_more, the whichdir quadrant for pruned
  *   setup_center_error                        mcomp.c:2781-2838 (vf at the
  *                                             full-pel start, no second_pred)
  *   two_level_checks_fast                     mcomp.c:2675-2686
@@ -12,7 +15,7 @@
  *   check_better_fast / estimated_pref_error  mcomp.c:2496-2523, 2368-2397
  *     (svf = aom_sub_pixel_variance: the bilinear estimate)
  *   get_best_diag_step                        mcomp.c:2555-2562
- *   mv_err_cost_ (L1 types / none)            mcomp.c:290-323
+ *   mv_err_cost_ (entropy / L1 / none)        mcomp.c:290-323
  *   av1_is_subpelmv_in_range                  mcomp.h:375-379
  * 8-bit planes.  MVs in 1/8 pel; the reference block at mv is at
  * ref + (row >> 3) * stride + (col >> 3) with offsets (col & 7, row & 7).
@@ -27,15 +30,22 @@ typedef struct {
   const uint8_t *src, *ref;
   int ss, rs, w, h, cost_type;
   const OrcSubpelJob *jb;
+  const OrcMvCost *cost; /* MV_COST_ENTROPY tables and error_per_bit */
 } SpCtx;
 
 static int sp_lambda(int t) { return t == 1 ? 2 : t == 2 ? 0 : t == 3 ? 1 : 0; }
 
-/* mv_err_cost_ for MV_COST_L1_* / MV_COST_NONE (mcomp.c:290-323) */
+/* mv_err_cost_ (mcomp.c:290-323) */
 static int sp_mv_cost(const SpCtx *c, int row, int col) {
+  const int dr = row - c->jb->ref_mv_row, dc = col - c->jb->ref_mv_col;
+  if (c->cost_type == 0) {
+    const OrcMvCost *m = c->cost;
+    const int joint = (dc != 0) | ((dr != 0) << 1);
+    const int rate = m->mvjcost[joint] + m->mvcost[0][dr] + m->mvcost[1][dc];
+    return (int)(((int64_t)rate * m->error_per_bit + 8192) >> 14);
+  }
   if (c->cost_type < 1 || c->cost_type > 3) return 0;
-  const int dr = abs(row - c->jb->ref_mv_row), dc = abs(col - c->jb->ref_mv_col);
-  return (sp_lambda(c->cost_type) * (dr + dc)) >> 3;
+  return (sp_lambda(c->cost_type) * (abs(dr) + abs(dc))) >> 3;
 }
 
 static int sp_in_range(const SpCtx *c, int row, int col) {
@@ -95,12 +105,19 @@ static void sp_two_level(const SpCtx *c, int tr, int tc, int hstep, int iters, S
   }
 }
 
-/* forced_stop: 0 EIGHTH_PEL, 1 QUARTER_PEL, 2 HALF_PEL, 3 FULL_PEL */
-static void sp_search(const SpCtx *c, int forced_stop, int allow_hp, int iters,
-                      OrcSubpelResult *out) {
+static int div_round(int n, int d) { /* divide_and_round, mcomp.c:2853-2855 */
+  return ((n < 0) ^ (d < 0)) ? ((n - d / 2) / d) : ((n + d / 2) / d);
+}
+
+/* forced_stop: 0 EIGHTH_PEL, 1 QUARTER_PEL, 2 HALF_PEL, 3 FULL_PEL;
+ * method 1 SUBPEL_TREE_PRUNED, 2 SUBPEL_TREE_PRUNED_MORE; cl NULL or the
+ * full-pel cost list */
+static void sp_search(const SpCtx *c, int method, int forced_stop, int allow_hp, int iters,
+                      const int32_t *cl, OrcSubpelResult *out) {
   SpBest b;
-  b.row = c->jb->start_row;
-  b.col = c->jb->start_col;
+  const int sr = c->jb->start_row, sc = c->jb->start_col;
+  b.row = sr;
+  b.col = sc;
   /* setup_center_error: vf at the (full-pel) start */
   unsigned sse;
   const uint8_t *r = c->ref + c->jb->ref_off + (ptrdiff_t)(b.row >> 3) * c->rs + (b.col >> 3);
@@ -110,7 +127,24 @@ static void sp_search(const SpCtx *c, int forced_stop, int allow_hp, int iters,
   b.besterr = v + (unsigned)sp_mv_cost(c, b.row, b.col);
   if (forced_stop != 3) {
     int hstep = 4; /* INIT_SUBPEL_STEP_SIZE */
-    sp_two_level(c, c->jb->start_row, c->jb->start_col, hstep, iters, &b);
+    const int cl_ok = cl && cl[0] != INT_MAX && cl[1] != INT_MAX && cl[2] != INT_MAX &&
+                      cl[3] != INT_MAX && cl[4] != INT_MAX;
+    if (method == 2 && cl_ok && cl[0] < cl[1] && cl[0] < cl[2] && cl[0] < cl[3] &&
+        cl[0] < cl[4]) {
+      /* get_cost_surf_min(bits 1), one check at the modelled minimum */
+      const int ic = div_round(cl[1] - cl[3], cl[1] - 2 * cl[0] + cl[3]);
+      const int ir = div_round(cl[4] - cl[2], cl[4] - 2 * cl[0] + cl[2]);
+      if (ir != 0 || ic != 0) sp_check(c, sr + ir * hstep, sc + ic * hstep, &b);
+    } else if (method == 1 && cl_ok) {
+      /* whichdir: the quadrant of the cheaper full-pel neighbours */
+      const int dc = cl[1] < cl[3] ? -hstep : hstep; /* left : right */
+      const int dr = cl[2] < cl[4] ? hstep : -hstep; /* bottom : top */
+      sp_check(c, sr, sc + dc, &b);
+      sp_check(c, sr + dr, sc, &b);
+      sp_check(c, sr + dr, sc + dc, &b);
+    } else {
+      sp_two_level(c, sr, sc, hstep, iters, &b);
+    }
     if (forced_stop < 2) {
       hstep >>= 1;
       sp_two_level(c, b.row, b.col, hstep, iters, &b);
@@ -131,7 +165,8 @@ typedef struct {
   SpCtx base;
   const OrcSubpelJob *jobs;
   OrcSubpelResult *out;
-  int forced_stop, allow_hp, iters;
+  const int32_t *cls;
+  int method, forced_stop, allow_hp, iters;
   long lo, hi;
 } SpArg;
 
@@ -140,23 +175,28 @@ static void *sp_worker(void *v) {
   for (long j = a->lo; j < a->hi; ++j) {
     SpCtx c = a->base;
     c.jb = &a->jobs[j];
-    sp_search(&c, a->forced_stop, a->allow_hp, a->iters, &a->out[j]);
+    sp_search(&c, a->method, a->forced_stop, a->allow_hp, a->iters,
+              a->cls ? a->cls + 5 * j : NULL, &a->out[j]);
   }
   return NULL;
 }
 
-void orc_subpel_batch(const uint8_t *src, int src_stride, const uint8_t *ref, int ref_stride,
-                      int w, int h, const OrcSubpelJob *jobs, long njobs, int forced_stop,
-                      int allow_hp, int iters_per_step, int mv_cost_type, OrcSubpelResult *out,
-                      int threads) {
+void orc_subpel_search_batch(const uint8_t *src, int src_stride, const uint8_t *ref,
+                             int ref_stride, int w, int h, const OrcSubpelJob *jobs, long njobs,
+                             int subpel_method, int forced_stop, int allow_hp,
+                             int iters_per_step, const OrcMvCost *cost,
+                             const int32_t *cost_lists, OrcSubpelResult *out, int threads) {
   if (threads < 1) threads = 1;
   if (threads > 64) threads = 64;
   pthread_t tid[64];
   SpArg args[64];
   for (int t = 0; t < threads; ++t) {
-    args[t].base = (SpCtx){ src, ref, src_stride, ref_stride, w, h, mv_cost_type, NULL };
+    args[t].base =
+        (SpCtx){ src, ref, src_stride, ref_stride, w, h, cost->mv_cost_type, NULL, cost };
     args[t].jobs = jobs;
     args[t].out = out;
+    args[t].cls = cost_lists;
+    args[t].method = subpel_method;
     args[t].forced_stop = forced_stop;
     args[t].allow_hp = allow_hp;
     args[t].iters = iters_per_step;
@@ -167,4 +207,13 @@ void orc_subpel_batch(const uint8_t *src, int src_stride, const uint8_t *ref, in
   }
   if (threads > 1)
     for (int t = 0; t < threads; ++t) pthread_join(tid[t], NULL);
+}
+
+void orc_subpel_batch(const uint8_t *src, int src_stride, const uint8_t *ref, int ref_stride,
+                      int w, int h, const OrcSubpelJob *jobs, long njobs, int forced_stop,
+                      int allow_hp, int iters_per_step, int mv_cost_type, OrcSubpelResult *out,
+                      int threads) {
+  const OrcMvCost c = { mv_cost_type, 0, 0, NULL, { NULL, NULL } };
+  orc_subpel_search_batch(src, src_stride, ref, ref_stride, w, h, jobs, njobs, 2, forced_stop,
+                          allow_hp, iters_per_step, &c, NULL, out, threads);
 }

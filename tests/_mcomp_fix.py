@@ -34,3 +34,29 @@ def mcomp_groups(F):
                   "row_min", "row_max"):
             rec[f] = rows[:, J[f]]
         yield F["cases"][ci], bw, bh, epb, spb, rec, rows, J
+
+
+def subpel_groups(F, mc):
+    """fix_subpel.npz jobs grouped by (case, block size, error_per_bit), as
+    (case row, bw, bh, epb, JOB records (start = full-pel best x 8, subpel
+    limits), cost lists int32 [n][5], expected rows, field index); mc: the
+    fix_mcomp.npz dict (planes and geometry)."""
+    J = {n: i for i, n in enumerate(F["job_fields"])}
+    W, H, BORDER, NREF = (int(v) for v in mc["geom"])
+    stride = mc["src"].shape[1]
+    plane = mc["refs"][0].size
+    org = BORDER * stride + BORDER
+    groups = {}
+    for r in F["jobs"]:
+        key = tuple(int(r[J[k]]) for k in ("case", "bw", "bh", "error_per_bit"))
+        groups.setdefault(key, []).append(r)
+    for (ci, bw, bh, epb), rows in sorted(groups.items()):
+        rows = np.array(rows)
+        rec = np.zeros(len(rows), MS_JOB)
+        off = org + rows[:, J["by"]] * stride + rows[:, J["bx"]]
+        rec["src_off"], rec["ref_off"] = off, off + rows[:, J["ref"]] * plane
+        for f in ("start_row", "start_col", "ref_mv_row", "ref_mv_col", "col_min", "col_max",
+                  "row_min", "row_max"):
+            rec[f] = rows[:, J[f]]
+        cls = np.ascontiguousarray(rows[:, J["cl0"]:J["cl4"] + 1].astype(np.int32))
+        yield F["cases"][ci], bw, bh, epb, rec, cls, rows, J

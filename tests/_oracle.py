@@ -461,6 +461,35 @@ def full_pixel_search_batch(src, ref, stride, w, h, jobs, method="diamond", step
     return out, cls
 
 
+def subpel_search_batch(src, ref, stride, w, h, jobs, method=2, forced_stop=0, allow_hp=False,
+                        iters=1, mv_cost_type=3, error_per_bit=0, mvjcost=None, mvcost=None,
+                        cost_lists=None, threads=1):
+    """orc_subpel_search_batch: SUBPEL_TREE_PRUNED (method 1) /
+    _PRUNED_MORE (2) with any mv cost and optional full-pel cost lists."""
+    L = lib()
+    fn = L.orc_subpel_search_batch
+    fn.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
+                   ctypes.c_int, ctypes.c_void_p, ctypes.c_long, ctypes.c_int, ctypes.c_int,
+                   ctypes.c_int, ctypes.c_int, ctypes.POINTER(OrcMvCost), ctypes.c_void_p,
+                   ctypes.c_void_p, ctypes.c_int]
+    jobs = np.ascontiguousarray(jobs)
+    c = OrcMvCost(mv_cost_type, 0, error_per_bit)
+    keep = []
+    if mvjcost is not None:
+        mj = np.ascontiguousarray(mvjcost, np.int32)
+        mc = np.ascontiguousarray(mvcost, np.int32)
+        keep += [mj, mc]
+        mid = (mc.shape[1] - 1) // 2
+        c.mvjcost = mj.ctypes.data
+        c.mvcost[0] = mc.ctypes.data + 4 * mid
+        c.mvcost[1] = mc.ctypes.data + 4 * (mc.shape[1] + mid)
+    out = np.zeros(len(jobs), SUBPEL_RESULT)
+    cl = None if cost_lists is None else np.ascontiguousarray(cost_lists, np.int32)
+    fn(P(src), stride, P(ref), stride, w, h, P(jobs), len(jobs), method, forced_stop,
+       int(allow_hp), iters, ctypes.byref(c), None if cl is None else P(cl), P(out), threads)
+    return out
+
+
 SUBPEL_RESULT = np.dtype([("best_row", "<i2"), ("best_col", "<i2"), ("besterr", "<u4"),
                           ("distortion", "<i4"), ("sse", "<u4")], align=True)
 

@@ -222,3 +222,25 @@ def test_full_pixel_search_vs_reference():
             np.testing.assert_array_equal(cl, rows[:, J["cl0"]:J["cl4"] + 1], err_msg=msg)
         n += len(rows)
     assert n == len(F["jobs"])
+
+
+def test_subpel_search_vs_reference():
+    """orc_subpel_search_batch against av1_find_best_sub_pixel_tree_pruned
+    (_more) executed from the reference, from full-pel results with their
+    cost lists (tests/golden/fix_subpel.npz)."""
+    from _mcomp_fix import subpel_groups
+    F, mc = _load("fix_subpel.npz"), _load("fix_mcomp.npz")
+    stride = mc["src"].shape[1]
+    n = 0
+    for case, bw, bh, epb, rec, cls, rows, J in subpel_groups(F, mc):
+        meth, hp, fstop, iters, ctype, use_cl = (int(v) for v in case)
+        tab = "hp" if hp else "lp"
+        res = O.subpel_search_batch(mc["src"], mc["refs"], stride, bw, bh, rec, meth, fstop,
+                                    bool(hp), iters, ctype, epb, mc["mvjcost_" + tab],
+                                    mc["mvcost_" + tab], cls if use_cl else None)
+        msg = "case %s %dx%d" % (list(case), bw, bh)
+        for f in ("best_row", "best_col", "besterr", "distortion", "sse"):
+            np.testing.assert_array_equal(res[f].astype(np.int64), rows[:, J[f]],
+                                          err_msg=msg + " " + f)
+        n += len(rows)
+    assert n == len(F["jobs"])
