@@ -1,17 +1,22 @@
 // subpel.hip -- batched sub-pixel motion refinement for gfx950 (SURVEY.md
 // 8(f) rank 2).
 //
-// Reference (one block, one reference, one CPU thread), the speed >= 4
-// subpel_search_method SUBPEL_TREE_PRUNED_MORE without a cost list:
-//   av1_find_best_sub_pixel_tree_pruned_more (av1/encoder/mcomp.c:2907-2981)
+// Reference (one block, one reference, one CPU thread), subpel_search_method
+// SUBPEL_TREE_PRUNED_MORE (speed >= 4) or SUBPEL_TREE_PRUNED:
+//   av1_find_best_sub_pixel_tree_pruned_more (av1/encoder/mcomp.c:2907-2990)
+//   av1_find_best_sub_pixel_tree_pruned (:2992-3126)
 //   -> setup_center_error (:2781-2838, vf at the full-pel start)
+//   -> with the full-pel search's cost list: get_cost_surf_min (:2870, one
+//      check at the modelled minimum when is_cost_list_wellbehaved) for
+//      pruned_more, the whichdir quadrant (3 checks) for pruned
 //   -> two_level_checks_fast (:2675) per half / quarter / (hp) eighth step:
 //      first_level_check_fast (:2566: left, right, up, down, then the
 //      diagonal toward the cheaper sides) and, with iters_per_step > 1,
 //      second_level_check_fast (:2608)
 //   -> check_better_fast (:2496): in-range test, estimated_pref_error =
 //      svf = aom_sub_pixel_variance (bilinear, aom_dsp/variance.c:73-145) +
-//      mv_err_cost_ (:290-323), "strictly better" update.
+//      mv_err_cost_ (:290-323, entropy / L1 / none), "strictly better"
+//      update.
 //
 // Here one wave64 owns one (block, reference) job.  Every check of a round
 // whose candidates are known in advance (the 4 cardinal points, the 2-3
@@ -77,10 +82,22 @@ struct SpCtx {
   int ref_mv_row, ref_mv_col;
   int col_min, col_max, row_min, row_max;
   int lambda;  // mv_err_cost_ L1 lambda (0: MV_COST_NONE)
+  bool entropy;
+  int error_per_bit;
+  const int32_t* mvjcost;
+  const int32_t* mvcost0;  // centred at MV_MAX
+  const int32_t* mvcost1;
 };
 
+// mv_err_cost_ (mcomp.c:290-323) at a wave-uniform mv
 __device__ __forceinline__ int mv_cost(const SpCtx& c, int row, int col) {
-  return (c.lambda * (abs(row - c.ref_mv_row) + abs(col - c.ref_mv_col))) >> 3;
+  const int dr = row - c.ref_mv_row, dc = col - c.ref_mv_col;
+  if (c.entropy) {
+    const int joint = (dc != 0) | ((dr != 0) << 1);  // av1_get_mv_joint
+    const int rate = c.mvjcost[joint] + c.mvcost0[dr] + c.mvcost1[dc];
+    return (int)(((int64_t)rate * c.error_per_bit + 8192) >> 14);
+  }
+  return (c.lambda * (abs(dr) + abs(dc))) >> 3;
 }
 __device__ __forceinline__ bool in_range(const SpCtx& c, int row, int col) {
   return col >= c.col_min && col <= c.col_max && row >= c.row_min && row <= c.row_max;
@@ -130,6 +147,11 @@ __device__ __forceinline__ void seg_err(const SpCtx& c, const uint32_t (&sv)[Sp<
       seg4(c, base, y, x, sw, f0, f1, g0, g1, sum, sse);
     }
   }
+}
+
+// divide_and_round (mcomp.c:2853-2855)
+__device__ __forceinline__ int div_round(int n, int d) {
+  return ((n < 0) ^ (d < 0)) ? ((n - d / 2) / d) : ((n + d / 2) / d);
 }
 
 struct Best {
@@ -216,8 +238,10 @@ __global__ __launch_bounds__(256) void subpel_kernel(const uint8_t* __restrict__
                                                      const uint8_t* __restrict__ ref, int rs,
                                                      const SJob* __restrict__ jobs, int njobs,
                                                      const LavishDiamondResult* __restrict__ fp,
-                                                     int forced_stop, int allow_hp, int iters,
-                                                     int lambda, LavishSubpelResult* out) {
+                                                     int method, int forced_stop, int allow_hp,
+                                                     int iters, LavishMvCostParams cost,
+                                                     const int32_t* __restrict__ cost_lists,
+                                                     LavishSubpelResult* out) {
   using S = Sp<W, H>;
   // XCD-aware: consecutive job quads share an XCD's L2
   const int nwg = gridDim.x;  // multiple of 8
@@ -237,7 +261,13 @@ __global__ __launch_bounds__(256) void subpel_kernel(const uint8_t* __restrict__
   c.col_max = jb.col_max;
   c.row_min = jb.row_min;
   c.row_max = jb.row_max;
-  c.lambda = lambda;
+  // mv_err_cost_ lambdas: SSE_LAMBDA_LOWRES 2, MIDRES 0, HDRES 1; NONE 0
+  c.lambda = cost.mv_cost_type == 1 ? 2 : cost.mv_cost_type == 3 ? 1 : 0;
+  c.entropy = cost.mv_cost_type == 0;
+  c.error_per_bit = cost.error_per_bit;
+  c.mvjcost = cost.mvjcost;
+  c.mvcost0 = cost.mvcost[0];
+  c.mvcost1 = cost.mvcost[1];
   // source words of this lane's segments
   uint32_t sv[S::NS];
 #pragma unroll
@@ -272,7 +302,35 @@ __global__ __launch_bounds__(256) void subpel_kernel(const uint8_t* __restrict__
   }
   if (forced_stop != 3) {  // FULL_PEL
     int hstep = 4;         // INIT_SUBPEL_STEP_SIZE: half pel
-    two_level<W, H>(c, sv, lane, start_row, start_col, hstep, iters, b);
+    int cl[5] = {INT_MAX, INT_MAX, INT_MAX, INT_MAX, INT_MAX};
+    if (cost_lists) {
+#pragma unroll
+      for (int i = 0; i < 5; ++i) cl[i] = cost_lists[5 * (int64_t)j + i];
+    }
+    const bool cl_ok = cl[0] != INT_MAX && cl[1] != INT_MAX && cl[2] != INT_MAX &&
+                       cl[3] != INT_MAX && cl[4] != INT_MAX;
+    if (method == 2 && cl_ok && cl[0] < cl[1] && cl[0] < cl[2] && cl[0] < cl[3] &&
+        cl[0] < cl[4]) {
+      // get_cost_surf_min (bits 1): |ic|, |ir| <= 1
+      const int ic = div_round(cl[1] - cl[3], cl[1] - 2 * cl[0] + cl[3]);
+      const int ir = div_round(cl[4] - cl[2], cl[4] - 2 * cl[0] + cl[2]);
+      if (ir != 0 || ic != 0) {
+        const int r[1] = {start_row + ir * hstep};
+        const int cc[1] = {start_col + ic * hstep};
+        uint32_t d1[1];
+        check_n<W, H, 1>(c, sv, lane, r, cc, b, d1);
+      }
+    } else if (method == 1 && cl_ok) {
+      // whichdir: left / right by cl[1] < cl[3], bottom / top by cl[2] < cl[4]
+      const int dc = cl[1] < cl[3] ? -hstep : hstep;
+      const int dr = cl[2] < cl[4] ? hstep : -hstep;
+      const int r[3] = {start_row, start_row + dr, start_row + dr};
+      const int cc[3] = {start_col + dc, start_col, start_col + dc};
+      uint32_t d3[3];
+      check_n<W, H, 3>(c, sv, lane, r, cc, b, d3);
+    } else {
+      two_level<W, H>(c, sv, lane, start_row, start_col, hstep, iters, b);
+    }
     if (forced_stop < 2) {  // below HALF_PEL
       hstep >>= 1;
       two_level<W, H>(c, sv, lane, b.row, b.col, hstep, iters, b);
@@ -295,34 +353,46 @@ __global__ __launch_bounds__(256) void subpel_kernel(const uint8_t* __restrict__
 
 template <int W, int H>
 void launch(const uint8_t* src, int ss, const uint8_t* ref, int rs, const LavishSubpelJob* jobs,
-            int njobs, const LavishDiamondResult* fp, int forced_stop, int allow_hp, int iters,
-            int lambda, LavishSubpelResult* out, hipStream_t s) {
+            int njobs, const LavishDiamondResult* fp, int method, int forced_stop, int allow_hp,
+            int iters, const LavishMvCostParams& cost, const int32_t* cost_lists,
+            LavishSubpelResult* out, hipStream_t s) {
   int nwg = (njobs + 3) / 4;
   nwg = (nwg + 7) & ~7;
   hipLaunchKernelGGL((subpel_kernel<W, H>), dim3(nwg), dim3(256), 0, s, src, ss, ref, rs,
-                     (const SJob*)jobs, njobs, fp, forced_stop, allow_hp, iters, lambda, out);
+                     (const SJob*)jobs, njobs, fp, method, forced_stop, allow_hp, iters, cost,
+                     cost_lists, out);
 }
 
 int subpel_batch(const uint8_t* src, int src_stride, const uint8_t* ref, int ref_stride, int w,
                  int h, const LavishSubpelJob* jobs, int njobs, const LavishDiamondResult* fp,
-                 int forced_stop, int allow_hp, int iters_per_step, int mv_cost_type,
+                 int method, int forced_stop, int allow_hp, int iters_per_step,
+                 const LavishMvCostParams* cost, const int32_t* cost_lists,
                  LavishSubpelResult* out, hipStream_t s) {
   if (njobs <= 0) return 0;
   if (forced_stop < 0 || forced_stop > 3) return -1;
-  if (mv_cost_type < 1 || mv_cost_type > 4) return -2;  // MV_COST_ENTROPY not supported
+  if (cost == nullptr || cost->mv_cost_type < 0 || cost->mv_cost_type > 4) return -2;
+  if (cost->mv_cost_type == 0 &&
+      (cost->mvjcost == nullptr || cost->mvcost[0] == nullptr || cost->mvcost[1] == nullptr))
+    return -2;
   if (iters_per_step < 1 || iters_per_step > 2) return -4;
-  // mv_err_cost_ lambdas: SSE_LAMBDA_LOWRES 2, MIDRES 0, HDRES 1; NONE 0
-  const int lambda = mv_cost_type == 1 ? 2 : mv_cost_type == 3 ? 1 : 0;
+  if (method != 1 && method != 2) return -6;  // SUBPEL_TREE_PRUNED / _PRUNED_MORE
 #define LAVISH_SP_CASE(W, H)                                                                   \
   if (w == W && h == H) {                                                                      \
-    launch<W, H>(src, src_stride, ref, ref_stride, jobs, njobs, fp, forced_stop, allow_hp,     \
-                 iters_per_step, lambda, out, s);                                              \
+    launch<W, H>(src, src_stride, ref, ref_stride, jobs, njobs, fp, method, forced_stop,       \
+                 allow_hp, iters_per_step, *cost, cost_lists, out, s);                         \
     LAVISH_CHECK(hipGetLastError());                                                           \
     return 0;                                                                                  \
   }
   LAVISH_ENCODER_BLOCK_SIZES(LAVISH_SP_CASE)
 #undef LAVISH_SP_CASE
   return -3;
+}
+
+LavishMvCostParams l1_cost(int mv_cost_type) {
+  LavishMvCostParams c = {};
+  // the L1 entry points never took MV_COST_ENTROPY (it needs the tables)
+  c.mv_cost_type = mv_cost_type == 0 ? -1 : mv_cost_type;
+  return c;
 }
 
 }  // namespace
@@ -336,8 +406,10 @@ extern "C" int lavish_subpel_search_batch(const uint8_t* src, int src_stride, co
                                           int forced_stop, int allow_hp, int iters_per_step,
                                           int mv_cost_type, LavishSubpelResult* out,
                                           void* stream) {
-  return subpel_batch(src, src_stride, ref, ref_stride, w, h, jobs, njobs, nullptr, forced_stop,
-                      allow_hp, iters_per_step, mv_cost_type, out, (hipStream_t)stream);
+  const LavishMvCostParams c = l1_cost(mv_cost_type);
+  return subpel_batch(src, src_stride, ref, ref_stride, w, h, jobs, njobs, nullptr, 2,
+                      forced_stop, allow_hp, iters_per_step, &c, nullptr, out,
+                      (hipStream_t)stream);
 }
 
 extern "C" int lavish_subpel_search_after_diamond(const uint8_t* src, int src_stride,
@@ -348,6 +420,19 @@ extern "C" int lavish_subpel_search_after_diamond(const uint8_t* src, int src_st
                                                   int iters_per_step, int mv_cost_type,
                                                   LavishSubpelResult* out, void* stream) {
   if (fullpel == nullptr) return -5;
-  return subpel_batch(src, src_stride, ref, ref_stride, w, h, jobs, njobs, fullpel, forced_stop,
-                      allow_hp, iters_per_step, mv_cost_type, out, (hipStream_t)stream);
+  const LavishMvCostParams c = l1_cost(mv_cost_type);
+  return subpel_batch(src, src_stride, ref, ref_stride, w, h, jobs, njobs, fullpel, 2,
+                      forced_stop, allow_hp, iters_per_step, &c, nullptr, out,
+                      (hipStream_t)stream);
+}
+
+extern "C" int lavish_find_best_sub_pixel_tree_batch(
+    const uint8_t* src, int src_stride, const uint8_t* ref, int ref_stride, int w, int h,
+    const LavishSubpelJob* jobs, const LavishDiamondResult* fullpel, int njobs,
+    int subpel_search_method, int forced_stop, int allow_hp, int iters_per_step,
+    const LavishMvCostParams* cost, const int32_t* cost_lists, LavishSubpelResult* out,
+    void* stream) {
+  return subpel_batch(src, src_stride, ref, ref_stride, w, h, jobs, njobs, fullpel,
+                      subpel_search_method, forced_stop, allow_hp, iters_per_step, cost,
+                      cost_lists, out, (hipStream_t)stream);
 }

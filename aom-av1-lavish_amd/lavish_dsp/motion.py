@@ -68,7 +68,36 @@ class MvCosts:
         row = self.mvcost.stride(0) * 4
         c.mvcost[0] = self.mvcost.data_ptr() + 4 * MV_MAX
         c.mvcost[1] = self.mvcost.data_ptr() + row + 4 * MV_MAX
+        c._owner = self  # the device tables live as long as the parameters
         return c
+
+
+def default_mv_cost_tables(allow_hp=False):
+    """(mvjcost[4], mvcost[2][2 * MV_MAX + 1]) of av1_build_nmv_cost_table over
+    the default nmv context at the frame's mv precision (package data made by
+    tests/golden/gen_fixtures.py nmv from the reference's own function)."""
+    import os
+    d = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "data",
+                             "nmv_cost_default.npz"))
+    t = "hp" if allow_hp else "lp"
+    return d["mvjcost_" + t], d["mvcost_" + t]
+
+
+def sad_per_bit(qindex, bit_depth=8):
+    """av1_set_sad_per_bit (av1/encoder/rd.c:336-346, 507-513):
+    (int)(0.0418 * q + 2.4107), q = av1_convert_qindex_to_q = ac_quant / 4."""
+    from . import build_quant_params
+    q = int(build_quant_params(bit_depth, qindex).dequant[1]) / 4.0
+    if bit_depth == 10:
+        q /= 4.0
+    elif bit_depth == 12:
+        q /= 16.0
+    return int(0.0418 * q + 2.4107)
+
+
+def error_per_bit(rdmult):
+    """av1_set_error_per_bit (av1/encoder/rd.h:305-307)."""
+    return max(rdmult >> 6, 1)
 
 
 def l1_cost_params(mv_cost_type=MV_COST_L1_HDRES):
@@ -281,6 +310,43 @@ def subpel_after_diamond(src, ref, w, h, jobs, fullpel, forced_stop=EIGHTH_PEL, 
         iters_per_step, mv_cost_type, _vp(out.data_ptr()), _stream_ptr(stream))
     if rc != 0:
         raise ValueError("lavish_subpel_search_after_diamond rejected its arguments (rc=%d)" % rc)
+    return out
+
+
+SUBPEL_METHODS = {"pruned": 1, "pruned_more": 2}   # SUBPEL_SEARCH_METHODS
+_lib.lavish_find_best_sub_pixel_tree_batch.argtypes = [
+    _vp, _i32, _vp, _i32, _i32, _i32, _vp, _vp, _i32, _i32, _i32, _i32, _i32,
+    ctypes.POINTER(MvCostParams), _vp, _vp, _vp]
+_lib.lavish_find_best_sub_pixel_tree_batch.restype = _i32
+
+
+def find_best_sub_pixel_tree_batch(src, ref, w, h, jobs, cost, method="pruned_more",
+                                   forced_stop=EIGHTH_PEL, allow_hp=False, iters_per_step=1,
+                                   fullpel=None, cost_lists=None, out=None, stream=None):
+    """lavish_find_best_sub_pixel_tree_batch: av1_find_best_sub_pixel_tree_pruned
+    (_more) with any mv cost (MvCostParams) and the full-pel cost lists
+    (device int32 [n, 5] or None); fullpel: device RESULT_DTYPE bytes to start
+    from (or None: the jobs' start fields)."""
+    import torch
+    assert src.dtype == torch.uint8 and ref.dtype == torch.uint8
+    assert src.is_contiguous() and ref.is_contiguous(), "planes must be C-contiguous"
+    nj = jobs.numel() // SUBPEL_JOB_DTYPE.itemsize
+    if fullpel is not None:
+        assert fullpel.numel() >= nj * RESULT_DTYPE.itemsize
+    if cost_lists is not None:
+        assert cost_lists.dtype == torch.int32 and cost_lists.numel() >= 5 * nj
+    if out is None:
+        out = torch.empty(nj * SUBPEL_RESULT_DTYPE.itemsize, dtype=torch.uint8,
+                          device=src.device)
+    rc = _lib.lavish_find_best_sub_pixel_tree_batch(
+        _vp(src.data_ptr()), src.stride(0), _vp(ref.data_ptr()), src.stride(0), w, h,
+        _vp(jobs.data_ptr()), None if fullpel is None else _vp(fullpel.data_ptr()), nj,
+        SUBPEL_METHODS[method], forced_stop, int(allow_hp), iters_per_step, ctypes.byref(cost),
+        None if cost_lists is None else _vp(cost_lists.data_ptr()), _vp(out.data_ptr()),
+        _stream_ptr(stream))
+    if rc != 0:
+        raise ValueError("lavish_find_best_sub_pixel_tree_batch rejected its arguments (rc=%d)"
+                         % rc)
     return out
 
 

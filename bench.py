@@ -12,8 +12,10 @@ The default workload ("rdo") is the metric's "fwd_txfm+quant+SAD" loop:
       (av1/encoder/tx_search.c:2148-2312) for the frame (lavish_txq_frame);
   C3  DIAMOND full-pixel motion search of every 16x16 block against 7
       reference frames (av1_full_pixel_search, av1/encoder/mcomp.c:1755),
-      with the 1080p speed features (use_downsampled_sad, MV_COST_L1_HDRES)
-      (lavish_diamond_search_batch),
+      as the RDO path runs it at 1080p speed 6: use_downsampled_sad,
+      MV_COST_ENTROPY over the default-context nmv cost tables with
+      sadperbit / errorperbit of the qindex / rdmult, and the cost list the
+      sub-pel search consumes (lavish_full_pixel_search_batch),
 
 by default back to back on the caller stream (C2 forks its per-size kernels
 over internal streams), so each leg's event-timed duration is its kernel
@@ -99,19 +101,22 @@ def algorithmic_bytes(L, s, width, height):
     return nb * (2 * W * H + nt * (8 * n + 2))
 
 
-def c3_algorithmic_bytes(res, njobs, bw, bh, skip):
+def c3_algorithmic_bytes(res, njobs, bw, bh, skip, cost_list=False):
     """C3 bytes: per (block, ref) the source block once,
     8 candidate blocks per executed diamond step (the x4d contract; skip rows
-    halve it), the source + reference block for every var cost, 16 B out."""
+    halve it), the source + reference block for every var cost, 16 B out;
+    with a cost list the 5 SADs of calc_int_sad_list and 20 B more out."""
     rows = bh // 2 if skip and bh >= 16 else bh
     steps = int(res["steps"].astype("int64").sum())
     searches = int(res["searches"].astype("int64").sum())
-    return njobs * (bw * bh + 16) + steps * 8 * rows * bw + searches * 2 * bw * bh
+    cl = njobs * (5 * rows * bw + 20) if cost_list else 0
+    return njobs * (bw * bh + 16) + steps * 8 * rows * bw + searches * 2 * bw * bh + cl
 
 
 C3_BLOCK = 16
-C3_COST = 3     # MV_COST_L1_HDRES
+C3_COST = 0     # MV_COST_ENTROPY (the RDO path's x->mv_cost_type)
 C3_SKIP = True  # use_downsampled_sad (>= 720p, speed_features.c:205-209)
+C3_CL = True    # cost list: subpel_search_method != SUBPEL_TREE (cond_cost_list)
 # sub-pixel refinement after the full-pel search (c3sub): SUBPEL_TREE_PRUNED_MORE
 # (speed >= 4), subpel_force_stop EIGHTH_PEL, iters_per_step 1 (speed >= 2),
 # allow_high_precision_mv = qindex < HIGH_PRECISION_MV_QTHRESH (128)
@@ -140,6 +145,9 @@ def cpu_baseline(args):
     src, refs = synth.motion_planes(W, Hs, args.refs, args.border)
     st = src.shape[1]
     jobs = M.frame_jobs(W, Hs, st, args.border, src.size, C3_BLOCK, C3_BLOCK, args.refs)
+    allow_hp = args.qindex < 128
+    mvj, mvc = M.default_mv_cost_tables(allow_hp)
+    spb, epb = M.sad_per_bit(args.qindex), M.error_per_bit(args.rdmult)
     sb = sb64_count(W, Hs)
     passes = 0
     t0 = time.perf_counter()
@@ -148,13 +156,14 @@ def cpu_baseline(args):
             for s in sizes:
                 O.txq_plane(res, s, L.valid_type_mask(s), q, threads=threads)
         if do_c3:
-            fp = O.diamond_batch(src.reshape(-1), refs.reshape(-1), st, C3_BLOCK, C3_BLOCK, jobs,
-                                 0, C3_COST, C3_SKIP, threads=threads)
+            fp, cl = O.full_pixel_search_batch(
+                src.reshape(-1), refs.reshape(-1), st, C3_BLOCK, C3_BLOCK, jobs, "diamond", 0,
+                C3_COST, spb, epb, mvj, mvc, skip=C3_SKIP, cost_list=C3_CL, threads=threads)
         if do_sub:
             sj = M.subpel_jobs(W, Hs, args.border, C3_BLOCK, C3_BLOCK, jobs, fp)
-            O.subpel_batch(src.reshape(-1), refs.reshape(-1), st, C3_BLOCK, C3_BLOCK, sj,
-                           SUB_FORCED_STOP, args.qindex < 128, SUB_ITERS, C3_COST,
-                           threads=threads)
+            O.subpel_search_batch(src.reshape(-1), refs.reshape(-1), st, C3_BLOCK, C3_BLOCK, sj,
+                                  2, SUB_FORCED_STOP, allow_hp, SUB_ITERS, C3_COST, epb, mvj,
+                                  mvc, cl, threads=threads)
         passes += 1
         dt = time.perf_counter() - t0
         if dt >= args.cpu_seconds:
@@ -539,6 +548,11 @@ def main():
     tjobs = M.to_device(jobs_np)
     c3_out = torch.empty(len(jobs_np) * M.RESULT_DTYPE.itemsize, dtype=torch.uint8,
                          device="cuda")
+    c3_cl = torch.empty((len(jobs_np), 5), dtype=torch.int32, device="cuda")
+    allow_hp = args.qindex < 128
+    mv_costs = M.MvCosts(*M.default_mv_cost_tables(allow_hp))
+    c3_cost = mv_costs.cost_params(M.sad_per_bit(args.qindex), M.error_per_bit(args.rdmult),
+                                   C3_COST)
     torch.cuda.synchronize()
 
     if do_sub:
@@ -548,12 +562,13 @@ def main():
                               device="cuda")
 
     def c3(on):
-        M.diamond_search_batch(tsrc, trefs, C3_BLOCK, C3_BLOCK, tjobs, 0, C3_COST, C3_SKIP,
-                               out=c3_out, stream=on)
-        if do_sub:  # chained on the device: starts = the full-pel results
-            M.subpel_after_diamond(tsrc, trefs, C3_BLOCK, C3_BLOCK, sub_jobs, c3_out,
-                                   SUB_FORCED_STOP, args.qindex < 128, SUB_ITERS, C3_COST,
-                                   out=sub_out, stream=on)
+        M.full_pixel_search_batch(tsrc, trefs, C3_BLOCK, C3_BLOCK, tjobs, c3_cost, "diamond", 0,
+                                  C3_SKIP, C3_CL, out=c3_out, cost_lists=c3_cl, stream=on)
+        if do_sub:  # chained on the device: starts + cost lists = the full-pel results
+            M.find_best_sub_pixel_tree_batch(tsrc, trefs, C3_BLOCK, C3_BLOCK, sub_jobs, c3_cost,
+                                             "pruned_more", SUB_FORCED_STOP, allow_hp, SUB_ITERS,
+                                             fullpel=c3_out, cost_lists=c3_cl, out=sub_out,
+                                             stream=on)
 
     overlap = do_c2 and do_c3 and args.overlap
     side = torch.cuda.Stream() if overlap else stream
@@ -615,7 +630,7 @@ def main():
     c2_ms = sum(ev[k][3].elapsed_time(ev[k][4]) for k in range(K)) / K if do_c2 else 0.0
     c2_bytes = sum(algorithmic_bytes(L, s, W, H) for s in sizes)
     c3_res = M.results_numpy(c3_out) if do_c3 else None
-    c3_bytes = c3_algorithmic_bytes(c3_res, len(jobs_np), C3_BLOCK, C3_BLOCK, C3_SKIP) \
+    c3_bytes = c3_algorithmic_bytes(c3_res, len(jobs_np), C3_BLOCK, C3_BLOCK, C3_SKIP, C3_CL) \
         if do_c3 else 0
 
     traffic = None
@@ -633,7 +648,8 @@ def main():
                 "unit": "GB/s", "traffic": traffic, "avg_launch_ms": round(c2_ms, 4),
                 "algorithmic_bytes_per_launch": c2_bytes}
     else:
-        roof = {"bound": "hbm", "kernel": "diamond_kernel<16,16> (lavish_diamond_search_batch)",
+        roof = {"bound": "hbm",
+                "kernel": "diamond_kernel<16,16,false> (lavish_full_pixel_search_batch)",
                 "achieved": round(c3_bytes / (c3_ms * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBS,
                 "unit": "GB/s", "traffic": None, "avg_launch_ms": round(c3_ms, 4),
                 "algorithmic_bytes_per_launch": c3_bytes}
@@ -647,10 +663,12 @@ def main():
                     "valid TX type" % args.qindex)
     if do_c3:
         legs.append("C3 DIAMOND full-pel search of every %dx%d block x %d refs (downsampled SAD, "
-                    "MV_COST_L1_HDRES, step_param 0)" % (C3_BLOCK, C3_BLOCK, args.refs))
+                    "MV_COST_ENTROPY default nmv context, sadperbit %d, errorperbit %d, "
+                    "cost list, step_param 0)" % (C3_BLOCK, C3_BLOCK, args.refs,
+                                                  c3_cost.sad_per_bit, c3_cost.error_per_bit))
     if do_sub:
         legs.append("sub-pel refinement SUBPEL_TREE_PRUNED_MORE to %s pel (bilinear svf, "
-                    "iters_per_step %d) chained on the device"
+                    "cost-list surface minimum, iters_per_step %d) chained on the device"
                     % ("1/8" if args.qindex < 128 else "1/4", SUB_ITERS))
     line = {
         "metric": METRIC,

@@ -470,6 +470,23 @@ int lavish_subpel_search_after_diamond(const uint8_t *src, int src_stride,
                                        int iters_per_step, int mv_cost_type,
                                        LavishSubpelResult *out, void *stream);
 
+/* The general form: subpel_search_method (SUBPEL_SEARCH_METHODS,
+ * mcomp_structs.h) 1 SUBPEL_TREE_PRUNED (av1_find_best_sub_pixel_tree_pruned,
+ * mcomp.c:2992-3126) or 2 SUBPEL_TREE_PRUNED_MORE (:2907-2990); any mv cost
+ * (cost: HOST pointer, tables on the device, as for
+ * lavish_full_pixel_search_batch -- the hp tables when allow_hp); cost_lists
+ * (device int32 [njobs][5] or NULL): the full-pel search's cost lists, which
+ * steer the first (half-pel) step exactly as in the reference.  fullpel
+ * (device, or NULL to use the jobs' start fields): start = its best x 8.
+ * Returns 0, -1 bad forced_stop, -2 bad cost parameters, -3 unsupported
+ * w x h, -4 bad iters_per_step, -6 unsupported method. */
+int lavish_find_best_sub_pixel_tree_batch(
+    const uint8_t *src, int src_stride, const uint8_t *ref, int ref_stride, int w,
+    int h, const LavishSubpelJob *jobs, const LavishDiamondResult *fullpel,
+    int njobs, int subpel_search_method, int forced_stop, int allow_hp,
+    int iters_per_step, const LavishMvCostParams *cost, const int32_t *cost_lists,
+    LavishSubpelResult *out, void *stream);
+
 /* ---- Inter prediction -----------------------------
  * av1_enc_build_one_inter_predictor (av1/encoder/reconinter_enc.c:47-51) for
  * a batch of single-reference translational blocks: init_subpel_params

@@ -556,6 +556,19 @@ def nmv_cost_tables():
     return out
 
 
+PKG_DATA = os.path.join(os.path.dirname(os.path.dirname(HERE)), "aom-av1-lavish_amd", "lavish_dsp",
+                        "data")
+
+
+def gen_nmv():
+    """The default-context mv cost tables as package data
+    (lavish_dsp/data/nmv_cost_default.npz): what av1_fill_mv_costs hands the
+    motion search on a frame coded from the default entropy context, used by
+    bench.py as the MV_COST_ENTROPY input."""
+    os.makedirs(PKG_DATA, exist_ok=True)
+    np.savez_compressed(os.path.join(PKG_DATA, "nmv_cost_default.npz"), **nmv_cost_tables())
+
+
 def _set(obj, **kw):
     for k, v in kw.items():
         obj.vals[obj.st.index[k]] = v
@@ -804,7 +817,8 @@ def gen_subpel():
 
 
 def main(argv):
-    sections = argv or ["txfm", "qparams", "quant", "inv", "pixel", "wht", "mcomp", "subpel"]
+    sections = argv or ["txfm", "qparams", "quant", "inv", "pixel", "wht", "nmv", "mcomp",
+                        "subpel"]
     t0 = time.time()
     ttx = None
     if "txfm" in sections or "inv" in sections or "wht" in sections:
@@ -827,6 +841,8 @@ def main(argv):
         gen_pixel(tu_pixel())
     if "wht" in sections:
         gen_wht(ttx)
+    if "nmv" in sections:
+        gen_nmv()
     if "mcomp" in sections:
         gen_mcomp()
     if "subpel" in sections:

@@ -3,7 +3,8 @@
 
 * C3: DIAMOND full-pel search of every 16x16 block of a 1920x1080 frame
   against 7 references (56 280 jobs) with the 1080p speed features bench.py
-  times (downsampled SAD, the bench's mv cost);
+  times (downsampled SAD, entropy mv cost, cost lists) and the sub-pel
+  refinement chained after it;
 * C4: the 3840x2160 10-bit RDO step (all candidate sizes / types, per-SB TX
   size, reconstruction) -- records, sb_tx_size and the reconstruction;
 * C5 at world 1: the SB-row band processor of lavish_dsp/shard.py over 3
@@ -40,23 +41,47 @@ def _bench():
 
 
 def test_c3_1080p_7refs_all_jobs(L):
+    """The bench's C3 leg (DIAMOND, downsampled SAD, MV_COST_ENTROPY over the
+    default nmv tables, cost lists) and its c3sub continuation (pruned_more
+    from the device results and cost lists) on all 56 280 jobs."""
     import torch
     import lavish_dsp.motion as M
     import lavish_dsp.synth as synth
     b = _bench()
-    W, H, R, border = 1920, 1080, 7, 160
+    W, H, R, border, qindex, rdmult = 1920, 1080, 7, 160, 128, 2000
     src, refs = synth.motion_planes(W, H, R, border, seed=1234)
     st = src.shape[1]
     jobs = M.frame_jobs(W, H, st, border, src.size, b.C3_BLOCK, b.C3_BLOCK, R)
     assert len(jobs) == 56280
-    got = M.results_numpy(M.diamond_search_batch(
-        torch.from_numpy(src).cuda(), torch.from_numpy(refs).cuda(), b.C3_BLOCK, b.C3_BLOCK,
-        M.to_device(jobs), 0, b.C3_COST, b.C3_SKIP))
-    exp = O.diamond_batch(src.reshape(-1), refs.reshape(-1), st, b.C3_BLOCK, b.C3_BLOCK, jobs, 0,
-                          b.C3_COST, b.C3_SKIP, threads=THREADS)
+    allow_hp = qindex < 128
+    mvj, mvc = M.default_mv_cost_tables(allow_hp)
+    spb, epb = M.sad_per_bit(qindex), M.error_per_bit(rdmult)
+    cp = M.MvCosts(mvj, mvc).cost_params(spb, epb, b.C3_COST)
+    tsrc, trefs = torch.from_numpy(src).cuda(), torch.from_numpy(refs).cuda()
+    fp, cl = M.full_pixel_search_batch(tsrc, trefs, b.C3_BLOCK, b.C3_BLOCK, M.to_device(jobs), cp,
+                                       "diamond", 0, b.C3_SKIP, b.C3_CL)
+    sj = M.subpel_jobs(W, H, border, b.C3_BLOCK, b.C3_BLOCK, jobs,
+                       np.zeros(len(jobs), M.RESULT_DTYPE))
+    sub = M.find_best_sub_pixel_tree_batch(tsrc, trefs, b.C3_BLOCK, b.C3_BLOCK, M.to_device(sj),
+                                           cp, "pruned_more", b.SUB_FORCED_STOP, allow_hp,
+                                           b.SUB_ITERS, fullpel=fp, cost_lists=cl)
+    torch.cuda.synchronize()
+    got, got_cl = M.results_numpy(fp), cl.cpu().numpy()
+    exp, exp_cl = O.full_pixel_search_batch(src.reshape(-1), refs.reshape(-1), st, b.C3_BLOCK,
+                                            b.C3_BLOCK, jobs, "diamond", 0, b.C3_COST, spb, epb,
+                                            mvj, mvc, skip=b.C3_SKIP, cost_list=b.C3_CL,
+                                            threads=THREADS)
     for f in ("best_row", "best_col", "bestsme", "steps"):  # the oracle has no search count
         np.testing.assert_array_equal(got[f], exp[f], err_msg=f)
+    np.testing.assert_array_equal(got_cl, exp_cl)
     assert (np.abs(got["best_row"]) + np.abs(got["best_col"]) > 0).mean() > 0.5
+    sj_exp = M.subpel_jobs(W, H, border, b.C3_BLOCK, b.C3_BLOCK, jobs, exp)
+    sexp = O.subpel_search_batch(src.reshape(-1), refs.reshape(-1), st, b.C3_BLOCK, b.C3_BLOCK,
+                                 sj_exp, 2, b.SUB_FORCED_STOP, allow_hp, b.SUB_ITERS, b.C3_COST,
+                                 epb, mvj, mvc, exp_cl, threads=THREADS)
+    sgot = M.subpel_results_numpy(sub)
+    for f in ("best_row", "best_col", "besterr", "distortion", "sse"):
+        np.testing.assert_array_equal(sgot[f], sexp[f], err_msg="subpel " + f)
 
 
 def _c4_planes(W, H):

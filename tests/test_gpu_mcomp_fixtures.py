@@ -64,3 +64,74 @@ def test_full_pixel_search_rejects(F):
     assert rc == -4
     with pytest.raises(ValueError, match="rc=-1"):
         M.full_pixel_search_batch(src, src, 8, 8, jobs, M.l1_cost_params(), step_param=11)
+
+
+def test_subpel_search_vs_reference(F):
+    """lavish_find_best_sub_pixel_tree_batch against
+    av1_find_best_sub_pixel_tree_pruned / _pruned_more executed from the
+    reference (tests/golden/fix_subpel.npz): entropy (hp / lp tables), L1 and
+    none mv costs, with and without the full-pel cost list, forced_stop and
+    iters_per_step variants -- best mv, besterr, distortion, sse bit-exact."""
+    import torch
+    from lavish_dsp import motion as M
+    from _mcomp_fix import subpel_groups
+    S = dict(np.load(os.path.join(GOLD, "fix_subpel.npz")))
+    src = torch.from_numpy(F["src"]).cuda()
+    refs = torch.from_numpy(np.ascontiguousarray(F["refs"])).cuda()
+    costs = {t: M.MvCosts(F["mvjcost_" + t], F["mvcost_" + t]) for t in ("lp", "hp")}
+    n = 0
+    for case, bw, bh, epb, rec, cls, rows, J in subpel_groups(S, F):
+        meth, hp, fstop, iters, ctype, use_cl = (int(v) for v in case)
+        cp = costs["hp" if hp else "lp"].cost_params(0, epb, ctype)
+        out = M.find_best_sub_pixel_tree_batch(
+            src, refs, bw, bh, M.to_device(rec), cp, {1: "pruned", 2: "pruned_more"}[meth],
+            fstop, bool(hp), iters, cost_lists=torch.from_numpy(cls).cuda() if use_cl else None)
+        torch.cuda.synchronize()
+        res = M.subpel_results_numpy(out)
+        msg = "case %s %dx%d" % ([int(v) for v in case], bw, bh)
+        for f in ("best_row", "best_col", "besterr", "distortion", "sse"):
+            np.testing.assert_array_equal(res[f].astype(np.int64), rows[:, J[f]],
+                                          err_msg=msg + " " + f)
+        n += len(rows)
+    assert n == len(S["jobs"])
+
+
+def test_fullpel_then_subpel_chain(F):
+    """The RDO path's chain on the device: full-pel DIAMOND with entropy cost
+    and cost list, then pruned_more from its results and cost lists -- equal to
+    the same two steps run from the fixture's full-pel answers."""
+    import torch
+    from lavish_dsp import motion as M
+    from _mcomp_fix import MS_METHODS, mcomp_groups
+    src = torch.from_numpy(F["src"]).cuda()
+    refs = torch.from_numpy(np.ascontiguousarray(F["refs"])).cuda()
+    costs = M.MvCosts(F["mvjcost_lp"], F["mvcost_lp"])
+    checked = 0
+    for case, bw, bh, epb, spb, rec, rows, J in mcomp_groups(F):
+        m, use_cl, ctype, skip, sp = (int(v) for v in case)
+        if not use_cl or ctype != 0:
+            continue
+        cp = costs.cost_params(spb, epb, 0)
+        fp, cl = M.full_pixel_search_batch(src, refs, bw, bh, M.to_device(rec), cp,
+                                           MS_METHODS[m], sp, bool(skip), True)
+        # sub-pel jobs: SubpelMvLimits from the block's x->mv_limits and ref_mv
+        W, H, BORDER, _ = (int(v) for v in F["geom"])
+        srec = rec.copy()
+        for i, r in enumerate(rows):
+            lim = M.block_mv_limits(((H + 7) & ~7) // 4, ((W + 7) & ~7) // 4, r[J["by"]] // 4,
+                                    r[J["bx"]] // 4, bh // 4, bw // 4, BORDER)
+            (srec["col_min"][i], srec["col_max"][i], srec["row_min"][i],
+             srec["row_max"][i]) = M.subpel_limits(lim, (r[J["ref_mv_row"]], r[J["ref_mv_col"]]))
+        chained = M.find_best_sub_pixel_tree_batch(src, refs, bw, bh, M.to_device(srec), cp,
+                                                   fullpel=fp, cost_lists=cl)
+        srec["start_row"] = rows[:, J["best_row"]] * 8
+        srec["start_col"] = rows[:, J["best_col"]] * 8
+        ref_cl = torch.from_numpy(np.ascontiguousarray(
+            rows[:, J["cl0"]:J["cl4"] + 1].astype(np.int32))).cuda()
+        direct = M.find_best_sub_pixel_tree_batch(src, refs, bw, bh, M.to_device(srec), cp,
+                                                  cost_lists=ref_cl)
+        torch.cuda.synchronize()
+        a, b = M.subpel_results_numpy(chained), M.subpel_results_numpy(direct)
+        np.testing.assert_array_equal(a, b)
+        checked += len(rows)
+    assert checked > 50
