@@ -50,7 +50,9 @@ __device__ __forceinline__ void load_row(const uint8_t* p, uint32_t (&out)[DW]) 
   uint32_t w[DW + 1];
 #pragma unroll
   for (int i = 0; i < DW; ++i) w[i] = q[i];
-  w[DW] = sh ? q[DW] : 0u;  // only lanes whose row is unaligned issue it
+  // the next word only matters when the row is unaligned; an aligned row
+  // re-reads its last word instead (no branch, no byte past the row)
+  w[DW] = q[sh ? DW : DW - 1];
 #pragma unroll
   for (int i = 0; i < DW; ++i) out[i] = __builtin_amdgcn_alignbyte(w[i + 1], w[i], sh);
 }
@@ -66,6 +68,27 @@ __device__ __forceinline__ uint32_t group_sum8(uint32_t v) {
 
 __device__ __forceinline__ uint32_t rdlane(uint32_t v, int l) {
   return (uint32_t)__builtin_amdgcn_readlane((int)v, l);
+}
+
+// Minimum / sum over the 8 lane groups of a value uniform within each group,
+// returned as a scalar: row_ror:8 pairs the two groups of a 16-lane row, the
+// gfx950 permlane16 / permlane32 swaps the rows -- 3 VALU steps instead of 8
+// readlanes and a scalar chain.
+__device__ __forceinline__ uint32_t groups_min(uint32_t v) {
+  v = min(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x128, 0xF, 0xF, false));
+  const auto p = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+  v = min((uint32_t)p[0], (uint32_t)p[1]);
+  const auto q = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+  v = min((uint32_t)q[0], (uint32_t)q[1]);
+  return (uint32_t)__builtin_amdgcn_readfirstlane((int)v);
+}
+__device__ __forceinline__ uint32_t groups_sum(uint32_t v) {
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x128, 0xF, 0xF, false);
+  const auto p = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+  v = (uint32_t)p[0] + (uint32_t)p[1];
+  const auto q = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+  v = (uint32_t)q[0] + (uint32_t)q[1];
+  return (uint32_t)__builtin_amdgcn_readfirstlane((int)v);
 }
 
 struct Job {
@@ -135,13 +158,7 @@ __device__ __forceinline__ void var_acc(uint32_t a, uint32_t b, int& sum, uint32
 
 template <int W, int H>
 __device__ __forceinline__ int var_finish(const Ctx& c, int sum, uint32_t sse, int row, int col) {
-  const uint32_t gs = group_sum8((uint32_t)sum), gq = group_sum8(sse);
-  uint32_t ts = rdlane(gs, 0), tq = rdlane(gq, 0);
-#pragma unroll
-  for (int i = 1; i < 8; ++i) {
-    ts += rdlane(gs, 8 * i);
-    tq += rdlane(gq, 8 * i);
-  }
+  const uint32_t ts = groups_sum(group_sum8((uint32_t)sum)), tq = groups_sum(group_sum8(sse));
   const uint32_t var = tq - (uint32_t)(((int64_t)(int)ts * (int)ts) / (W * H));
   return (int)var + mv_cost(c, row, col);
 }
@@ -180,13 +197,7 @@ __device__ void sad_and_skip(const Ctx& c, int lane, int row, int col, int& sad,
     all += d;
     even += (y & 1) ? 0u : d;
   }
-  const uint32_t ga = group_sum8(all), ge = group_sum8(even);
-  uint32_t ta = rdlane(ga, 0), te = rdlane(ge, 0);
-#pragma unroll
-  for (int i = 1; i < 8; ++i) {
-    ta += rdlane(ga, 8 * i);
-    te += rdlane(ge, 8 * i);
-  }
+  const uint32_t ta = groups_sum(group_sum8(all)), te = groups_sum(group_sum8(even));
   sad = (int)ta;
   ssad = (int)(2 * te);
 }
@@ -211,6 +222,12 @@ struct Win {
   static constexpr int SIZE = kOn ? ROWS * DW : 1;
 };
 
+// diamond site i + 1 (i = 0..7) of av1_init_dsmotion_compensation in units
+// of the radius: (-1,0) (1,0) (0,-1) (0,1) (-1,-1) (1,1) (-1,1) (1,-1),
+// packed as 2-bit (d + 1) fields
+__device__ __forceinline__ int site_dr(int i) { return ((0x8858 >> (2 * i)) & 3) - 1; }
+__device__ __forceinline__ int site_dc(int i) { return ((0x2885 >> (2 * i)) & 3) - 1; }
+
 template <int W, int H, bool SKIP>
 struct Search {
   using G = Geo<W, H, SKIP>;
@@ -225,6 +242,12 @@ struct Search {
   static constexpr bool kVarWin = WN::kOn && VN <= 4;
   uint32_t sv[kVarWin ? VN : 1];
   bool inwin;               // the last diamond() ended inside its window
+  bool wfilled;             // win holds the window at (wr0, wc0)
+  // every diamond_search_sad run of a full_pixel_diamond starts at the same
+  // clamped start_mv: its SAD is read once
+  bool have_c0;
+  int c0row, c0col;
+  uint32_t c0sad;
   int l;  // lane within the group
   lds_u32 win;              // this wave's window (WN::SIZE dwords), or null
   int wr0, wc0;             // window origin (mv units: block top-left at ref + wr0*rs + wc0)
@@ -234,6 +257,8 @@ struct Search {
     l = lane & 7;
     win = w;
     inwin = false;
+    wfilled = false;
+    have_c0 = false;
     if constexpr (kVarWin) {
 #pragma unroll
       for (int v = 0; v < VN; ++v) {
@@ -254,46 +279,52 @@ struct Search {
     }
   }
 
-  // group-partial SAD of the block at ref + off, reduced over the 8 lanes
-  __device__ __forceinline__ uint32_t group_sad(const Ctx& c, int64_t off, bool valid) const {
+  // group-partial SAD of the block at ref + off, reduced over the 8 lanes.
+  // Lanes whose candidate is not valid read the block at `safe` (in range)
+  // instead: no divergent branch around the loads; callers mask the result.
+  __device__ __forceinline__ uint32_t group_sad(const Ctx& c, int64_t off, bool valid,
+                                                int64_t safe) const {
+    off = valid ? off : safe;
     uint32_t acc = 0;
-    if (valid) {
-      if constexpr (kCache) {
+    if constexpr (kCache) {
 #pragma unroll
-        for (int k = 0; k < G::RPL; ++k) {
-          const int row = l + 8 * k;
-          if (row < G::RH) {
-            uint32_t r[G::DW];
-            load_row<G::DW>(c.ref + off + (int64_t)row * G::YS * c.rs, r);
+      for (int k = 0; k < G::RPL; ++k) {
+        const int row = l + 8 * k;
+        if (row < G::RH) {
+          uint32_t r[G::DW];
+          load_row<G::DW>(c.ref + off + (int64_t)row * G::YS * c.rs, r);
 #pragma unroll
-            for (int i = 0; i < G::DW; ++i) acc = sad4(s[k][i], r[i], acc);
-          }
+          for (int i = 0; i < G::DW; ++i) acc = sad4(s[k][i], r[i], acc);
         }
-      } else {
-        // rows in 32-byte chunks, not unrolled (keeps code and VGPRs small)
-        constexpr int CH = G::DW < 8 ? G::DW : 8;
+      }
+    } else {
+      // rows in 32-byte chunks, not unrolled (keeps code and VGPRs small)
+      constexpr int CH = G::DW < 8 ? G::DW : 8;
 #pragma unroll 1
-        for (int k = 0; k < G::RPL; ++k) {
-          const int row = l + 8 * k;
-          const uint8_t* rp = c.ref + off + (int64_t)row * G::YS * c.rs;
-          const uint8_t* sp = c.src + (int64_t)row * G::YS * c.ss;
+      for (int k = 0; k < G::RPL; ++k) {
+        const int row = l + 8 * k;
+        const uint8_t* rp = c.ref + off + (int64_t)row * G::YS * c.rs;
+        const uint8_t* sp = c.src + (int64_t)row * G::YS * c.ss;
 #pragma unroll 1
-          for (int x = 0; x < G::DW; x += CH) {
-            uint32_t r[CH], q[CH];
-            load_row<CH>(rp + 4 * x, r);
-            load_row<CH>(sp + 4 * x, q);
+        for (int x = 0; x < G::DW; x += CH) {
+          uint32_t r[CH], q[CH];
+          load_row<CH>(rp + 4 * x, r);
+          load_row<CH>(sp + 4 * x, q);
 #pragma unroll
-            for (int i = 0; i < CH; ++i) acc = sad4(q[i], r[i], acc);
-          }
+          for (int i = 0; i < CH; ++i) acc = sad4(q[i], r[i], acc);
         }
       }
     }
     acc = group_sum8(acc);
     return SKIP ? 2 * acc : acc;
   }
+  __device__ __forceinline__ uint32_t group_sad(const Ctx& c, int64_t off) const {
+    return group_sad(c, off, true, off);
+  }
 
   // copy the window around (row, col): rows outside [row_min, row_max + H)
-  // (never touched by a valid candidate) are not read
+  // (never touched by a valid candidate) repeat the nearest row inside; all
+  // loads are issued before the first store
   __device__ __forceinline__ void fill(const Ctx& c, int lane, int row, int col) {
     typedef const __attribute__((address_space(1))) uint32_t* gptr;
     wr0 = row - WN::R;
@@ -302,41 +333,47 @@ struct Search {
     const int rlo = max(0, c.row_min - wr0), rhi = min(WN::ROWS, c.row_max + H - wr0);
     typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
     typedef __attribute__((address_space(3))) u32x4* lptr4;
+    constexpr int N = WN::ROWS * WN::Q, NI = (N + 63) / 64;
+    u32x4 v[NI];
 #pragma unroll
-    for (int i0 = 0; i0 < WN::ROWS * WN::Q; i0 += 64) {
-      const int i = i0 + lane;
+    for (int it = 0; it < NI; ++it) {
+      const int i = min(64 * it + lane, N - 1);
       const int wr = i / WN::Q, d = i - wr * WN::Q;
-      if (i < WN::ROWS * WN::Q && wr >= rlo && wr < rhi) {
-        // dword-aligned 16-byte load (any dword alignment is a single access)
-        const uintptr_t ra = ((wbase + (int64_t)wr * c.rs) & ~(uintptr_t)3) + 16 * d;
-        const gptr q = (gptr)ra;
-        u32x4 v = {q[0], q[1], q[2], q[3]};
-        ((lptr4)win)[i] = v;
-      }
+      const int sr = min(max(wr, rlo), rhi - 1);
+      // dword-aligned 16-byte load (any dword alignment is a single access)
+      const uintptr_t ra = ((wbase + (int64_t)sr * c.rs) & ~(uintptr_t)3) + 16 * d;
+      const gptr q = (gptr)ra;
+      v[it] = u32x4{q[0], q[1], q[2], q[3]};
+    }
+#pragma unroll
+    for (int it = 0; it < NI; ++it) {
+      const int i = 64 * it + lane;
+      if (i < N) ((lptr4)win)[i] = v[it];
     }
     wave_sync();
   }
 
   // group SAD of the candidate at (r, cc) from the window
+  // (lanes whose candidate is not valid read the window centre instead)
   __device__ __forceinline__ uint32_t group_sad_win(const Ctx& c, int r, int cc,
                                                     bool valid) const {
+    r = valid ? r : wr0 + WN::R;
+    cc = valid ? cc : wc0 + WN::R;
     uint32_t acc = 0;
-    if (valid) {
 #pragma unroll
-      for (int k = 0; k < G::RPL; ++k) {
-        const int row = l + 8 * k;
-        if (row < G::RH) {
-          const int wr = r - wr0 + row * G::YS;
-          const int x = cc - wc0 + (int)((wbase + (int64_t)wr * c.rs) & 3);
-          const lds_u32 p = win + wr * WN::DW + (x >> 2);
-          const uint32_t sh = (uint32_t)(x & 3);
-          uint32_t w[G::DW + 1];
+    for (int k = 0; k < G::RPL; ++k) {
+      const int row = l + 8 * k;
+      if (row < G::RH) {
+        const int wr = r - wr0 + row * G::YS;
+        const int x = cc - wc0 + (int)((wbase + (int64_t)wr * c.rs) & 3);
+        const lds_u32 p = win + wr * WN::DW + (x >> 2);
+        const uint32_t sh = (uint32_t)(x & 3);
+        uint32_t w[G::DW + 1];
 #pragma unroll
-          for (int i = 0; i <= G::DW; ++i) w[i] = p[i];
+        for (int i = 0; i <= G::DW; ++i) w[i] = p[i];
 #pragma unroll
-          for (int i = 0; i < G::DW; ++i)
-            acc = sad4(s[k][i], __builtin_amdgcn_alignbyte(w[i + 1], w[i], sh), acc);
-        }
+        for (int i = 0; i < G::DW; ++i)
+          acc = sad4(s[k][i], __builtin_amdgcn_alignbyte(w[i + 1], w[i], sh), acc);
       }
     }
     acc = group_sum8(acc);
@@ -369,46 +406,49 @@ struct Search {
   }
 
   // diamond_search_sad (no second_pred): returns bestsad
-  __device__ uint32_t diamond(const Ctx& c, int lane, int srow, int scol, int search_step,
-                              int& brow, int& bcol, int& num00, int& steps) {
+  __device__ __forceinline__ uint32_t diamond(const Ctx& c, int lane, int srow, int scol,
+                                              int search_step, int& brow, int& bcol,
+                                              int& num00, int& steps) {
     const int g = lane >> 3;
     // site g + 1 of av1_init_dsmotion_compensation (row, col) in units of radius
-    const int sdr = (g == 0 || g == 4 || g == 6) ? -1 : (g == 1 || g == 5 || g == 7) ? 1 : 0;
-    const int sdc = (g == 2 || g == 4 || g == 7) ? -1 : (g == 3 || g == 5 || g == 6) ? 1 : 0;
+    const int sdr = site_dr(g), sdc = site_dc(g);
     srow = min(max(srow, c.row_min), c.row_max);
     scol = min(max(scol, c.col_min), c.col_max);
     int row = srow, col = scol, off_center = 0, center = 0;
-    uint32_t best = mvsad_cost(c, row, col) +
-                    rdlane(group_sad(c, (int64_t)row * c.rs + col, true), 0);
+    if (!have_c0 || c0row != srow || c0col != scol) {
+      c0sad = rdlane(group_sad(c, (int64_t)srow * c.rs + scol), 0);
+      have_c0 = true;
+      c0row = srow;
+      c0col = scol;
+    }
+    uint32_t best = mvsad_cost(c, row, col) + c0sad;
     const int tot = kMaxSteps - search_step;
     inwin = false;
     for (int step = tot - 1; step >= 0; --step) {
       const int rad = 1 << step;
       if constexpr (WN::kOn && kCache) {
         if (!inwin && rad <= WN::MAXRAD && win != nullptr) {
-          fill(c, lane, row, col);
+          // a later run reaching radius 8 at the same point finds its window
+          if (!wfilled || wr0 != row - WN::R || wc0 != col - WN::R) fill(c, lane, row, col);
+          wfilled = true;
           inwin = true;
         }
       }
-      const bool all_in = row - rad >= c.row_min && row + rad <= c.row_max &&
-                          col - rad >= c.col_min && col + rad <= c.col_max;
+      // (all_in of the reference only skips this test when it holds)
       const int r = row + sdr * rad, cc = col + sdc * rad;
-      const bool valid = all_in || (cc >= c.col_min && cc <= c.col_max && r >= c.row_min &&
-                                    r <= c.row_max);
+      const bool valid = cc >= c.col_min && cc <= c.col_max && r >= c.row_min && r <= c.row_max;
       const uint32_t mine = inwin ? group_sad_win(c, r, cc, valid)
-                                  : group_sad(c, (int64_t)r * c.rs + cc, valid);
+                                  : group_sad(c, (int64_t)r * c.rs + cc, valid,
+                                              (int64_t)row * c.rs + col);
       // key = cost * 8 + site (costs < 2^26 for blocks <= 128x128)
       const uint32_t key = valid ? ((mine + mvsad_cost(c, r, cc)) << 3) | (uint32_t)g : ~0u;
-      uint32_t kmin = rdlane(key, 0);
-#pragma unroll
-      for (int i = 1; i < 8; ++i) kmin = min(kmin, rdlane(key, 8 * i));
-      const int best_site = kmin < (best << 3) ? (int)(kmin & 7) + 1 : 0;
-      if (best_site) best = kmin >> 3;
+      const uint32_t kmin = groups_min(key);
       ++steps;
-      if (best_site) {
-        const int i = best_site - 1;
-        row += ((i == 0 || i == 4 || i == 6) ? -1 : (i == 1 || i == 5 || i == 7) ? 1 : 0) * rad;
-        col += ((i == 2 || i == 4 || i == 7) ? -1 : (i == 3 || i == 5 || i == 6) ? 1 : 0) * rad;
+      if (kmin < (best << 3)) {
+        best = kmin >> 3;
+        const int i = (int)(kmin & 7);
+        row += site_dr(i) * rad;
+        col += site_dc(i) * rad;
         off_center = 1;
       }
       if (!off_center) ++center;
@@ -438,11 +478,11 @@ __device__ void int_sad_list(const Search<W, H, SKIP>& S, const Ctx& c, int lane
     const int dr = g == 2 ? 1 : g == 4 ? -1 : 0;
     const int dc = g == 1 ? -1 : g == 3 ? 1 : 0;
     const int r = br + dr, cc = bc + dc;
-    const bool all_in = br - 1 >= c.row_min && br + 1 <= c.row_max && bc - 1 >= c.col_min &&
-                        bc + 1 <= c.col_max;
-    const bool valid = g < 5 && (all_in || (cc >= c.col_min && cc <= c.col_max &&
-                                            r >= c.row_min && r <= c.row_max));
-    const uint32_t sad = S.group_sad(c, (int64_t)r * c.rs + cc, valid);
+    // (check_bounds of the reference only skips this test when it holds)
+    const bool valid =
+        g < 5 && cc >= c.col_min && cc <= c.col_max && r >= c.row_min && r <= c.row_max;
+    const uint32_t sad =
+        S.group_sad(c, (int64_t)r * c.rs + cc, valid, (int64_t)br * c.rs + bc);
     const uint32_t v = valid ? sad : 0x7FFFFFFFu;
 #pragma unroll
     for (int i = 0; i < 5; ++i) cl[i] = (int)rdlane(v, 8 * i);
@@ -525,25 +565,23 @@ __device__ int pattern(const Ctx& c, int lane, int srow, int scol, int search_st
   int bc = min(max(scol, c.col_min), c.col_max);
   if (want_cl) cl[0] = cl[1] = cl[2] = cl[3] = cl[4] = INT_MAX;
   bool has_sad = false;
-  uint32_t raw = rdlane(S.group_sad(c, (int64_t)br * c.rs + bc, true), 0);
+  uint32_t raw = rdlane(S.group_sad(c, (int64_t)br * c.rs + bc), 0);
   uint32_t best = raw + mvsad_cost(c, br, bc);
   // one round: candidate idx (groups g < cnt) of scale s around (br, bc);
   // returns the winning group or -1.  clmode 1: raw SADs of the valid
   // candidates into cl (calc_sad4 / calc_sad_update_bestmv); 2: also INT_MAX
   // for invalid ones (calc_sad3 / _with_indices)
   auto check = [&](int s, int cnt, int idx, int clmode) -> int {
-    const bool all_in = br - (1 << s) >= c.row_min && br + (1 << s) <= c.row_max &&
-                        bc - (1 << s) >= c.col_min && bc + (1 << s) <= c.col_max;
     int dr, dc;
     bigdia_site(s, idx, dr, dc);
     const int r = br + dr, cc = bc + dc;
-    const bool valid = g < cnt && (all_in || (cc >= c.col_min && cc <= c.col_max &&
-                                              r >= c.row_min && r <= c.row_max));
-    const uint32_t mine = S.group_sad(c, (int64_t)r * c.rs + cc, valid);
+    // (check_bounds only skips this test when it holds)
+    const bool valid =
+        g < cnt && cc >= c.col_min && cc <= c.col_max && r >= c.row_min && r <= c.row_max;
+    const uint32_t mine =
+        S.group_sad(c, (int64_t)r * c.rs + cc, valid, (int64_t)br * c.rs + bc);
     const uint32_t key = valid ? ((mine + mvsad_cost(c, r, cc)) << 3) | (uint32_t)g : ~0u;
-    uint32_t kmin = rdlane(key, 0);
-#pragma unroll
-    for (int i = 1; i < 8; ++i) kmin = min(kmin, rdlane(key, 8 * i));
+    uint32_t kmin = groups_min(key);
     ++steps;
     if (clmode) {
       const uint32_t tag = valid ? (mine << 1) | 1u : 0u;  // SADs < 2^22
