@@ -124,8 +124,8 @@ __device__ __forceinline__ int mv_rate(const Ctx& c, int dr, int dc) {
 // mvsad_err_cost (mcomp.c:329-350); the L1 lambdas are 0 for MV_COST_NONE
 __device__ __forceinline__ uint32_t mvsad_cost(const Ctx& c, int row, int col) {
   const int dr = (row - c.full_ref_row) * 8, dc = (col - c.full_ref_col) * 8;
-  if (c.cost_type == 0)  // ROUND_POWER_OF_TWO(., AV1_PROB_COST_SHIFT)
-    return ((uint32_t)mv_rate(c, dr, dc) * (uint32_t)c.sad_per_bit + 256u) >> 9;
+  if (c.cost_type == 0)  // ROUND_POWER_OF_TWO(., AV1_PROB_COST_SHIFT); rates < 2^24
+    return (__umul24((uint32_t)mv_rate(c, dr, dc), (uint32_t)c.sad_per_bit) + 256u) >> 9;
   return (uint32_t)((c.sad_lambda * (abs(dr) + abs(dc))) >> 3);
 }
 // mv_err_cost (mcomp.c:290-314)
@@ -364,8 +364,8 @@ struct Search {
     for (int k = 0; k < G::RPL; ++k) {
       const int row = l + 8 * k;
       if (row < G::RH) {
-        const int wr = r - wr0 + row * G::YS;
-        const int x = cc - wc0 + (int)((wbase + (int64_t)wr * c.rs) & 3);
+        const int wr = r - wr0 + row * G::YS;  // >= 0
+        const int x = cc - wc0 + (int)(((uint32_t)wbase + __umul24(wr, c.rs & 3)) & 3);
         const lds_u32 p = win + wr * WN::DW + (x >> 2);
         const uint32_t sh = (uint32_t)(x & 3);
         uint32_t w[G::DW + 1];
@@ -393,7 +393,7 @@ struct Search {
           if (i < H * (W / 4)) {
             const int y = i / (W / 4), x4 = i % (W / 4);
             const int wr = row - wr0 + y;
-            const int xb = col - wc0 + 4 * x4 + (int)((wbase + (int64_t)wr * c.rs) & 3);
+            const int xb = col - wc0 + 4 * x4 + (int)(((uint32_t)wbase + __umul24(wr, c.rs & 3)) & 3);
             const lds_u32 p = win + wr * WN::DW + (xb >> 2);
             var_acc(sv[v], __builtin_amdgcn_alignbyte(p[1], p[0], (uint32_t)(xb & 3)), sum,
                     sse);
@@ -437,11 +437,14 @@ struct Search {
       // (all_in of the reference only skips this test when it holds)
       const int r = row + sdr * rad, cc = col + sdc * rad;
       const bool valid = cc >= c.col_min && cc <= c.col_max && r >= c.row_min && r <= c.row_max;
+      // the mv cost first (its table reads overlap the SAD); |r|, |cc| < 2048
+      // keep every index inside the cost tables, valid or not
+      const uint32_t mvs = mvsad_cost(c, r, cc);
       const uint32_t mine = inwin ? group_sad_win(c, r, cc, valid)
-                                  : group_sad(c, (int64_t)r * c.rs + cc, valid,
-                                              (int64_t)row * c.rs + col);
+                                  : group_sad(c, __mul24(r, c.rs) + cc, valid,
+                                              __mul24(row, c.rs) + col);
       // key = cost * 8 + site (costs < 2^26 for blocks <= 128x128)
-      const uint32_t key = valid ? ((mine + mvsad_cost(c, r, cc)) << 3) | (uint32_t)g : ~0u;
+      const uint32_t key = valid ? ((mine + mvs) << 3) | (uint32_t)g : ~0u;
       const uint32_t kmin = groups_min(key);
       ++steps;
       if (kmin < (best << 3)) {
@@ -672,7 +675,7 @@ enum { kDiamond = 0, kBigdia = 5, kFastDiamond = 8, kFastBigdia = 9, kVfastDiamo
 
 // PAT: the BIGDIA-site pattern searches (method 5 / 8 / 9 / 10), else DIAMOND
 template <int W, int H, bool PAT>
-__global__ __launch_bounds__(256, 7) void diamond_kernel(const uint8_t* __restrict__ src, int ss,
+__global__ __launch_bounds__(256, (W <= 16 && H <= 16) ? 8 : 7) void diamond_kernel(const uint8_t* __restrict__ src, int ss,
                                                       const uint8_t* __restrict__ ref, int rs,
                                                       const Job* __restrict__ jobs, int njobs,
                                                       int step_param, LavishMvCostParams cost,
