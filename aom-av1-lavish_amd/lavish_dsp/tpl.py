@@ -1,0 +1,153 @@
+"""The TPL model's per-block inter leg on the MI355X backend (SURVEY.md 8(f)
+rank 1): lavish_tpl_block_batch, and tpl_frame, which chains the whole leg on
+the device for every 16x16 block x reference of a frame:
+
+  av1_full_pixel_search (motion_estimation, av1/encoder/tpl_model.c:249-300:
+    tpl_sf.search_method, step_param = reduce_first_step_size, the frame's
+    mv costs, a cost list)            -> lavish_full_pixel_search_batch
+  find_fractional_mv_step (MV_COST_NONE, tpl_sf.subpel_force_stop, 2-tap)
+                                      -> lavish_find_best_sub_pixel_tree_batch
+  the inter predictor (EIGHTTAP_REGULAR, av1_enc_build_one_inter_predictor)
+                                      -> lavish_build_inter_pred_after_subpel
+  tpl_get_satd_cost per reference, the cheapest one, txfm_quant_rdcost
+                                      -> lavish_tpl_block_batch
+
+Intra candidates and the reference's per-block start-mv selection
+(prune_starting_mv / compare_sad over neighbouring tpl stats, which depends
+on already-finished blocks) stay with the caller: the start / center mv of
+each (block, reference) comes in the motion jobs."""
+import ctypes
+
+import numpy as np
+
+from . import QuantParams, _lib, _stream_ptr
+from . import inter as I
+from . import motion as M
+
+TPL_BLOCK_DTYPE = np.dtype([("best_ref", "<i4"), ("inter_cost", "<i4"), ("rate_cost", "<i4"),
+                            ("eob", "<i4"), ("recon_error", "<i8"), ("sse", "<i8")])
+assert TPL_BLOCK_DTYPE.itemsize == 32
+
+_vp, _i32, _i64 = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64
+_lib.lavish_tpl_block_batch.argtypes = [_vp, _i32, _vp, _i64, _i32, _i32, _i32, _i32, _i32, _i32,
+                                        ctypes.POINTER(QuantParams), _vp, _vp, _i32, _vp, _vp]
+_lib.lavish_tpl_block_batch.restype = _i32
+
+TPL_BSIZE = 16  # set_tpl_stats_block_size (tpl_model.c:137-145)
+
+
+def tpl_block_batch(src, preds, bsize, bit_depth, qp, width=None, height=None, out=None,
+                    recon=None, ref_costs=None, stream=None):
+    """lavish_tpl_block_batch.  src: 2-D device tensor whose [0, 0] is the
+    frame origin (a view into a padded plane is fine: its row stride is
+    used); preds: [nrefs, H, W] device tensor (or a 2-D one for a single
+    reference); qp: QuantParams for LAVISH_QUANT_FP; ref_costs: None, True
+    (allocate) or an int32 [nblocks, nrefs] device tensor.  Returns (records
+    byte tensor, recon tensor, costs or None)."""
+    import torch
+    assert src.dtype in (torch.uint8, torch.uint16, torch.int16) and preds.dtype == src.dtype
+    assert (src.dtype == torch.uint8) == (bit_depth == 8), "8-bit planes are uint8, else u16"
+    assert src.stride(1) == 1 and preds.stride(-1) == 1
+    if preds.dim() == 2:
+        preds = preds.unsqueeze(0)
+    nrefs = preds.shape[0]
+    H = src.shape[0] if height is None else height
+    W = src.shape[1] if width is None else width
+    nb = (W // bsize) * (H // bsize)
+    if out is None:
+        out = torch.empty(nb * TPL_BLOCK_DTYPE.itemsize, dtype=torch.uint8, device=src.device)
+    if recon is None:
+        recon = torch.empty((H, W), dtype=src.dtype, device=src.device)
+    costs = ref_costs
+    if ref_costs is True:
+        costs = torch.empty((nb, nrefs), dtype=torch.int32, device=src.device)
+    if costs is not None:
+        assert costs.dtype == torch.int32 and costs.numel() >= nb * nrefs
+    pp = preds.stride(0) if nrefs > 1 else 0
+    rc = _lib.lavish_tpl_block_batch(
+        _vp(src.data_ptr()), src.stride(0), _vp(preds.data_ptr()), pp, preds.stride(1), nrefs,
+        W, H, bsize, bit_depth, ctypes.byref(qp), _vp(out.data_ptr()), _vp(recon.data_ptr()),
+        recon.stride(0), _vp(costs.data_ptr()) if costs is not None else None,
+        _stream_ptr(stream))
+    if rc != 0:
+        raise ValueError("lavish_tpl_block_batch rejected its arguments (rc=%d)" % rc)
+    return out, recon, costs
+
+
+def records_numpy(out):
+    return out.cpu().numpy().view(TPL_BLOCK_DTYPE)
+
+
+class TplFrame:
+    """Device state of one TPL frame leg (8-bit): padded source / reference
+    planes (border >= AOM_BORDER_IN_PIXELS for the predictor), the motion jobs
+    of every (block, reference), and the intermediate buffers, so that step()
+    launches only kernels."""
+
+    def __init__(self, src_np, refs_np, width, height, border, qindex, rdmult,
+                 search_method="fast_bigdia", step_param=6, forced_stop=M.FULL_PEL,
+                 subpel_method="pruned_more", start_mvs=None, device="cuda"):
+        import torch
+        from . import build_quant_params, QUANT_FP
+        assert border >= I.AOM_BORDER_IN_PIXELS
+        self.W, self.H, self.border = width, height, border
+        self.nrefs = refs_np.shape[0]
+        self.stride = src_np.shape[1]
+        bs = TPL_BSIZE
+        self.src = torch.from_numpy(src_np).to(device)
+        self.refs = torch.from_numpy(refs_np).to(device)
+        org = border * self.stride + border
+        self.org = org
+        jobs = M.frame_jobs(width, height, self.stride, border, src_np.size, bs, bs, self.nrefs)
+        if start_mvs is not None:
+            jobs["start_row"], jobs["start_col"] = start_mvs[:, 0], start_mvs[:, 1]
+        self.jobs_np = jobs
+        self.jobs = M.to_device(jobs)
+        sj = M.subpel_jobs(width, height, border, bs, bs, jobs, np.zeros(len(jobs), M.RESULT_DTYPE))
+        self.sub_jobs = M.to_device(sj)
+        # inter prediction jobs: job j = (ref k, block) -> pred plane k, same position
+        nb = (width // bs) * (height // bs)
+        ij = []
+        for k in range(self.nrefs):
+            pj = I.plane_jobs(width, height, bs, bs, (0, 0), ref_off=k * src_np.size,
+                              dst_stride=width)
+            pj["dst_off"] += k * width * height
+            ij.append(pj)
+        self.inter_jobs = M.to_device(np.concatenate(ij))
+        self.nb = nb
+        allow_hp = qindex < 128
+        self.allow_hp = allow_hp
+        self.mv_costs = M.MvCosts(*M.default_mv_cost_tables(allow_hp), device=device)
+        self.cost = self.mv_costs.cost_params(M.sad_per_bit(qindex), M.error_per_bit(rdmult),
+                                              M.MV_COST_ENTROPY)
+        self.cost_none = M.l1_cost_params(M.MV_COST_NONE)
+        self.search_method, self.step_param = search_method, step_param
+        self.forced_stop, self.subpel_method = forced_stop, subpel_method
+        self.qp = build_quant_params(8, qindex, QUANT_FP)
+        n = len(jobs)
+        self.fp = torch.empty(n * M.RESULT_DTYPE.itemsize, dtype=torch.uint8, device=device)
+        self.cl = torch.empty((n, 5), dtype=torch.int32, device=device)
+        self.sub = torch.empty(n * M.SUBPEL_RESULT_DTYPE.itemsize, dtype=torch.uint8,
+                               device=device)
+        self.preds = torch.empty((self.nrefs, height, width), dtype=torch.uint8, device=device)
+        self.out = torch.empty(nb * TPL_BLOCK_DTYPE.itemsize, dtype=torch.uint8, device=device)
+        self.recon = torch.empty((height, width), dtype=torch.uint8, device=device)
+        self.costs = torch.empty((nb, self.nrefs), dtype=torch.int32, device=device)
+        self.src_view = self.src[border:border + height, border:border + width]
+
+    def step(self, stream=None, ref_costs=True):
+        bs = TPL_BSIZE
+        M.full_pixel_search_batch(self.src, self.refs, bs, bs, self.jobs, self.cost,
+                                  self.search_method, self.step_param, False, True, out=self.fp,
+                                  cost_lists=self.cl, stream=stream)
+        M.find_best_sub_pixel_tree_batch(self.src, self.refs, bs, bs, self.sub_jobs,
+                                         self.cost_none, self.subpel_method, self.forced_stop,
+                                         self.allow_hp, 1, fullpel=self.fp, cost_lists=self.cl,
+                                         out=self.sub, stream=stream)
+        I.build_inter_pred_batch(self.refs.view(-1, self.stride), self.org, self.W, self.H, bs, bs,
+                                 self.inter_jobs, dst=self.preds.view(-1, self.W),
+                                 dst_stride=self.W, bit_depth=8, mvs=self.sub, stream=stream)
+        tpl_block_batch(self.src_view, self.preds, bs, 8, self.qp, out=self.out,
+                        recon=self.recon, ref_costs=self.costs if ref_costs else None,
+                        stream=stream)
+        return self.out

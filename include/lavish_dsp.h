@@ -525,6 +525,38 @@ int lavish_build_inter_pred_after_subpel(const void *ref, int ref_stride,
                                          void *dst, int dst_stride, int bit_depth,
                                          int highbd, void *stream);
 
+/* ---- TPL block transform leg ----------------------
+ * For every full bsize x bsize block of a width x height frame (raster
+ * order; bsize 8 / 16 / 32 with TX = the block, tpl_model.c uses 16): the
+ * inter cost of each of nrefs predictions (tpl_get_satd_cost,
+ * av1/encoder/tpl_model.c:199-210: subtract, av1_quick_txfm DCT_DCT,
+ * aom_satd), the cheapest reference (lowest cost, earlier reference on
+ * ties), and on its prediction txfm_quant_rdcost (:225-247):
+ * get_quantize_error (:98-135, quantize_fp with qp built for
+ * LAVISH_QUANT_FP, block error and sse >> (TX_32X32 ? 0 : 2), each >= 1),
+ * rate_estimator (:212-223) and recon = prediction + the inverse transform.
+ *   src: plane origin, src_stride elements; preds: reference k's
+ *   prediction plane at preds + k * pred_plane elements (same geometry);
+ *   recon: output plane.  8-bit: uint8_t planes; 10 / 12-bit: uint16_t.
+ *   ref_costs (device, optional): int32 [nblocks][nrefs] inter costs.
+ * Returns 0, or -1 bad bsize, -2 bad bit_depth, -3 NULL argument, -4 bad
+ * nrefs / preds, -5 bad geometry. */
+typedef struct LavishTplBlock {
+  int32_t best_ref;    /* index of the cheapest prediction */
+  int32_t inter_cost;  /* its satd cost */
+  int32_t rate_cost;   /* rate_estimator, << AV1_PROB_COST_SHIFT */
+  int32_t eob;
+  int64_t recon_error; /* get_quantize_error's recon_error */
+  int64_t sse;         /* and sse */
+} LavishTplBlock;
+
+int lavish_tpl_block_batch(const void *src, int src_stride, const void *preds,
+                           int64_t pred_plane, int pred_stride, int nrefs,
+                           int width, int height, int bsize, int bit_depth,
+                           const LavishQuantParams *qp, LavishTplBlock *out,
+                           void *recon, int recon_stride, int32_t *ref_costs,
+                           void *stream);
+
 /* ---- TX-type pruning features ---------------------
  * Every full bw x bh block of an int16 residual plane (raster order):
  * av1_get_horver_correlation_full (av1/encoder/rdopt.c:514-609) -> hcorr /

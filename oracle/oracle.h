@@ -342,6 +342,16 @@ long orc_prune_tx_2d(const int16_t *residual, int stride, int width, int height,
                      const OrcNNConfig *hor, const OrcNNConfig *ver, const uint16_t *allowed_in,
                      uint16_t allowed_default, uint16_t *allowed_out, uint8_t *txk_map);
 
+/* ---- TPL block transform leg (oracle_tpl.c); layout = LavishTplBlock ---- */
+typedef struct OrcTplBlock {
+  int32_t best_ref, inter_cost, rate_cost, eob;
+  int64_t recon_error, sse;
+} OrcTplBlock;
+void orc_tpl_block_batch(const void *src, int src_stride, const void *preds, long pred_plane,
+                         int pred_stride, int nrefs, int width, int height, int bsize, int bd,
+                         const OrcQuant *q, OrcTplBlock *out, void *recon, int recon_stride,
+                         int32_t *ref_costs, int threads);
+
 #ifdef __cplusplus
 }
 #endif

@@ -748,3 +748,31 @@ def prune_tx_2d(res, bw, bh, tx_set_type, prune_mode, thresholds, hor, ver, allo
                       None if vc is None else ctypes.addressof(vc),
                       None if ai is None else P(ai), allowed_default, P(out), P(maps))
     return out, maps
+
+
+# ------------------------------------------------------------ TPL block leg --
+TPL_BLOCK = np.dtype([("best_ref", "<i4"), ("inter_cost", "<i4"), ("rate_cost", "<i4"),
+                      ("eob", "<i4"), ("recon_error", "<i8"), ("sse", "<i8")])
+
+
+def tpl_block_batch(src, preds, bsize, bd, qindex, threads=1):
+    """orc_tpl_block_batch: src [H, W] (uint8 at bd 8, uint16 above), preds
+    [nrefs, H, W] of the same type.  Returns (records, recon, ref_costs)."""
+    L = lib()
+    fn = L.orc_tpl_block_batch
+    fn.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_long, ctypes.c_int,
+                   ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                   ctypes.POINTER(OrcQuant), ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int,
+                   ctypes.c_void_p, ctypes.c_int]
+    src = np.ascontiguousarray(src)
+    preds = np.ascontiguousarray(preds)
+    H, W = src.shape
+    nrefs = preds.shape[0]
+    nb = (W // bsize) * (H // bsize)
+    out = np.zeros(nb, TPL_BLOCK)
+    recon = np.zeros_like(src)
+    costs = np.zeros((nb, nrefs), np.int32)
+    q = build_quant(bd, qindex)
+    fn(P(src), W, P(preds), preds[0].size, W, nrefs, W, H, bsize, bd, ctypes.byref(q), P(out),
+       P(recon), W, P(costs), threads)
+    return out, recon, costs
