@@ -53,7 +53,8 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--workload", choices=("rdo", "c2", "c3", "c3sub", "c4", "c4px", "c5", "inter"),
+    ap.add_argument("--workload", choices=("rdo", "c2", "c3", "c3sub", "c4", "c4px", "c5", "inter",
+                                           "tpl"),
                     default="rdo")
     ap.add_argument("--rdmult", type=int, default=2000)
     ap.add_argument("--width", type=int, default=1920)
@@ -510,12 +511,185 @@ def main_inter(args):
         dist.destroy_process_group()
 
 
+TPL_BORDER = 288  # AOM_BORDER_IN_PIXELS: the predictor's clamp reads stay inside
+
+
+def tpl_block_bytes(W, H, nrefs, bs=16):
+    """TPL block-leg bytes per frame (lavish_tpl_block_batch): the source and
+    every reference's prediction read once (u8), the reconstruction written,
+    a 32-byte record and nrefs int32 costs per block."""
+    nb = (W // bs) * (H // bs)
+    return W * H * (nrefs + 2) + nb * (32 + 4 * nrefs)
+
+
+def cpu_baseline_tpl(args):
+    """The oracle chain (full-pel, sub-pel, prediction, block leg) on a 1920x256
+    strip with the bench's parameters, repeated for ~cpu_seconds."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import _oracle as O
+    import lavish_dsp.inter as I
+    import lavish_dsp.motion as M
+    import lavish_dsp.synth as synth
+    threads = host_cores()
+    W, Hs, R, border = args.width, 256, args.refs, TPL_BORDER
+    src, refs = synth.motion_planes(W, Hs, R, border)
+    st = src.shape[1]
+    jobs = M.frame_jobs(W, Hs, st, border, src.size, 16, 16, R)
+    allow_hp = args.qindex < 128
+    mvj, mvc = M.default_mv_cost_tables(allow_hp)
+    spb, epb = M.sad_per_bit(args.qindex), M.error_per_bit(args.rdmult)
+    ij = np.concatenate([I.plane_jobs(W, Hs, 16, 16, (0, 0), ref_off=k * src.size, dst_stride=W)
+                         for k in range(R)])
+    n1 = len(ij) // R
+    for k in range(R):
+        ij["dst_off"][k * n1:(k + 1) * n1] += k * W * Hs
+    org = border * st + border
+    sb = sb64_count(W, Hs)
+    passes = 0
+    t0 = time.perf_counter()
+    while True:
+        fp, cl = O.full_pixel_search_batch(src.reshape(-1), refs.reshape(-1), st, 16, 16, jobs,
+                                           "fast_bigdia", 6, 0, spb, epb, mvj, mvc,
+                                           cost_list=True, threads=threads)
+        sj = M.subpel_jobs(W, Hs, border, 16, 16, jobs, fp)
+        sub = O.subpel_search_batch(src.reshape(-1), refs.reshape(-1), st, 16, 16, sj, 2,
+                                    M.FULL_PEL, allow_hp, 1, M.MV_COST_NONE, 0, None, None, cl,
+                                    threads=threads)
+        preds = O.build_inter_pred(refs.reshape(-1, st), org, W, Hs, 0, 0, 16, 16, ij,
+                                   (R, Hs, W), mvs=sub, dst_stride=W)
+        O.tpl_block_batch(src[border:border + Hs, border:border + W], preds, 16, 8, args.qindex,
+                          threads=threads)
+        passes += 1
+        dt = time.perf_counter() - t0
+        if dt >= args.cpu_seconds:
+            break
+    return {"value": round(passes * sb / dt, 2), "unit": "SB64/s", "cores": threads,
+            "kind": "port",
+            "sample": "%d passes of a %dx%d strip (%d SB64) through the tpl step (full-pel, "
+                      "sub-pel, prediction, block leg), oracle C restatement (-O3, %d pthreads), "
+                      "%.1f s" % (passes, W, Hs, sb, threads, dt)}
+
+
+def main_tpl(args):
+    """The TPL model's inter leg for one 1080p frame per step (TplFrame.step:
+    FAST_BIGDIA full-pel with entropy costs and cost lists, sub-pel stop at
+    full pel with MV_COST_NONE, EIGHTTAP_REGULAR predictions, then the block
+    leg: per-reference satd, best reference, quantize error, rate, recon) --
+    the cpu-used=6 tpl speed features (speed_features.c:1101,1213-1216)."""
+    import torch
+    import torch.distributed as dist
+    import lavish_dsp as L
+    import lavish_dsp.motion as M
+    import lavish_dsp.synth as synth
+    import lavish_dsp.tpl as T
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local_rank)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    W, H, R = args.width, args.height, args.refs
+    src, refs = synth.motion_planes(W, H, R, TPL_BORDER, seed=1234 + rank)
+    tf = T.TplFrame(src, refs, W, H, TPL_BORDER, args.qindex, args.rdmult)
+    stream = torch.cuda.current_stream()
+    bs = T.TPL_BSIZE
+
+    def step(ev=None):
+        mark = (lambda i: ev[i].record(stream)) if ev is not None else (lambda i: None)
+        mark(0)
+        M.full_pixel_search_batch(tf.src, tf.refs, bs, bs, tf.jobs, tf.cost, tf.search_method,
+                                  tf.step_param, False, True, out=tf.fp, cost_lists=tf.cl,
+                                  stream=stream)
+        mark(1)
+        M.find_best_sub_pixel_tree_batch(tf.src, tf.refs, bs, bs, tf.sub_jobs, tf.cost_none,
+                                         tf.subpel_method, tf.forced_stop, tf.allow_hp, 1,
+                                         fullpel=tf.fp, cost_lists=tf.cl, out=tf.sub,
+                                         stream=stream)
+        mark(2)
+        import lavish_dsp.inter as I
+        I.build_inter_pred_batch(tf.refs.view(-1, tf.stride), tf.org, W, H, bs, bs,
+                                 tf.inter_jobs, dst=tf.preds.view(-1, W), dst_stride=W,
+                                 bit_depth=8, mvs=tf.sub, stream=stream)
+        mark(3)
+        T.tpl_block_batch(tf.src_view, tf.preds, bs, 8, tf.qp, out=tf.out, recon=tf.recon,
+                          ref_costs=tf.costs, stream=stream)
+        mark(4)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    ev = [[torch.cuda.Event(enable_timing=True) for _ in range(5)] for _ in range(args.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        step(ev[k])
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    status = L.status()
+    if status[0] != 0:
+        raise RuntimeError("HIP error during bench: %s" % (status,))
+    K = args.steps
+    legs = [sum(ev[k][i].elapsed_time(ev[k][i + 1]) for k in range(K)) / K for i in range(4)]
+    names = ["fullpel_fast_bigdia", "subpel", "inter_pred", "tpl_block"]
+    blk_bytes = tpl_block_bytes(W, H, R)
+    sb = sb64_count(W, H)
+    recs = T.records_numpy(tf.out)
+    line = {
+        "metric": METRIC,
+        "value": round(world * sb * args.steps / elapsed, 2),
+        "unit": "SB64/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "int32",
+        "data": "synthetic (seeded 1080p content, lavish_dsp/synth.py)",
+        "config": {
+            "workload": "tpl: %dx%d 8-bit frame per step; TPL inter leg of every 16x16 block x %d "
+                        "refs: FAST_BIGDIA full-pel (step_param 6, MV_COST_ENTROPY default nmv "
+                        "context, cost list) -> sub-pel forced stop FULL_PEL (MV_COST_NONE) -> "
+                        "EIGHTTAP_REGULAR prediction -> tpl_get_satd_cost per ref, best ref, "
+                        "get_quantize_error (quantize_fp qindex %d) + rate_estimator + recon; "
+                        "%d SB64/frame" % (W, H, R, args.qindex, sb),
+            "parallelism": "frame-per-rank x%d" % world,
+        },
+        "roofline": {"bound": "hbm", "kernel": "tpl_kernel<16,0,u8> (lavish_tpl_block_batch)",
+                     "achieved": round(blk_bytes / (legs[3] * 1e-3) / 1e9, 1),
+                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "traffic": None,
+                     "avg_launch_ms": round(legs[3], 4),
+                     "algorithmic_bytes_per_launch": blk_bytes},
+        "legs_ms": {n: round(v, 4) for n, v in zip(names, legs)},
+        "tpl": {"blocks": int(len(recs)), "mean_eob": round(float(recs["eob"].mean()), 2),
+                "refs_chosen": int(len(set(recs["best_ref"].tolist())))},
+    }
+    line["roofline"]["frac"] = round(line["roofline"]["achieved"] / HBM_PEAK_GBS, 4)
+    if rank == 0 and world == 1 and not args.no_cpu:
+        line["cpu_baseline"] = cpu_baseline_tpl(args)
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def main():
     args = parse()
     if args.workload in ("c4", "c4px", "c5"):
         return main_c4(args)
     if args.workload == "inter":
         return main_inter(args)
+    if args.workload == "tpl":
+        return main_tpl(args)
     import torch
     import torch.distributed as dist
     import lavish_dsp as L

@@ -816,9 +816,91 @@ def gen_subpel():
     np.savez_compressed(os.path.join(HERE, "fix_subpel.npz"), **out)
 
 
+def gen_tpl():
+    """tpl_get_satd_cost and txfm_quant_rdcost (av1/encoder/tpl_model.c:199-247,
+    with get_quantize_error :98-135 and rate_estimator :212-223) on random
+    src / prediction blocks: 8x8 / 16x16 / 32x32, bd 8 / 10 / 12, several
+    qindex -- satd, rate, recon_error, sse and the reconstruction the
+    reference writes into the prediction."""
+    tu = C.TU(REF, ["av1/encoder/tpl_model.c", "av1/encoder/encodemb.c",
+                    "av1/encoder/hybrid_fwd_txfm.c", "av1/encoder/av1_fwd_txfm2d.c",
+                    "av1/encoder/av1_fwd_txfm1d.c", "av1/common/av1_txfm.c", "aom_dsp/avg.c",
+                    "av1/common/quant_common.c", "aom_dsp/quantize.c",
+                    "av1/encoder/av1_quantize.c", "av1/encoder/rdopt.c", "av1/common/idct.c",
+                    "av1/common/av1_inv_txfm2d.c", "av1/common/av1_inv_txfm1d.c",
+                    "aom_dsp/subtract.c", "av1/common/scan.c"], C.reference_defines(REF))
+    check_errors(tu, ["tpl_get_satd_cost", "txfm_quant_rdcost", "av1_build_quantizer"])
+    E = tu.enums
+    rnd = ACMRandom(0xbaba + 6)
+    out = {}
+    for bd in (8, 10, 12):
+        quants = tu.struct_obj("QUANTS")
+        deq = tu.struct_obj("Dequants")
+        # av1_build_quantizer(bd, y_dc_delta_q, u/v deltas..., quants, deq, sharpness)
+        tu.func("av1_build_quantizer")(bd, 0, 0, 0, 0, 0, quants, deq, 0)
+        for n in (8, 16, 32):
+            ts = E["TX_%dX%d" % (n, n)]
+            recs, srcs, preds, recons, qs = [], [], [], [], []
+            for qindex in (0, 40, 128, 255):
+                for k in range(3):
+                    m = (1 << bd) - 1
+                    amp = (4, 40, m)[k] << (0 if k == 2 else bd - 8)
+                    src = [rnd.rand16() % (m + 1) for _ in range(n * n)]
+                    prd = [min(m, max(0, v + (rnd.rand16() % (2 * amp + 1)) - amp)) for v in src]
+                    hb = bd > 8
+                    ty = "uint16_t" if hb else "uint8_t"
+                    sb = tu.buffer(ty, src)
+                    db = tu.buffer(ty, prd)
+                    sp = tu.tagged(sb) if hb else sb
+                    dp = tu.tagged(db) if hb else db
+                    xd_bd = tu.struct_obj("BitDepthInfo")
+                    _set(xd_bd.buf[0], bit_depth=bd, use_highbitdepth_buf=int(hb))
+                    diff = tu.buffer("int16_t", n * n)
+                    coeff = tu.buffer("tran_low_t", n * n)
+                    satd = tu.func("tpl_get_satd_cost")(C.copy_obj(xd_bd.buf[0]), diff, n, sp, n,
+                                                        dp, n, coeff, n, n, ts)
+                    # MACROBLOCK with plane 0 quantizer tables and xd
+                    x = tu.struct_obj("MACROBLOCK")
+                    X = x.buf[0]
+                    p0 = _get(X, "plane")[0]
+                    Q, D = quants.buf[0], deq.buf[0]
+                    for fld, src_t, nm in (("quant_fp_QTX", Q, "y_quant_fp"),
+                                           ("round_fp_QTX", Q, "y_round_fp"),
+                                           ("quant_QTX", Q, "y_quant"),
+                                           ("quant_shift_QTX", Q, "y_quant_shift"),
+                                           ("zbin_QTX", Q, "y_zbin"), ("round_QTX", Q, "y_round"),
+                                           ("dequant_QTX", D, "y_dequant_QTX")):
+                        arr = _get(src_t, nm)  # [QINDEX_RANGE][8], flat
+                        _set(p0, **{fld: C.Pointer(arr, 8 * qindex, tu.ctype("int16_t"))})
+                    xd = _get(X, "e_mbd")
+                    mbmi = tu.struct_obj("MB_MODE_INFO")
+                    ybuf = tu.struct_obj("YV12_BUFFER_CONFIG")
+                    _set(ybuf.buf[0], flags=8 if hb else 0)  # YV12_FLAG_HIGHBITDEPTH
+                    _set(xd, bd=bd, mi=C.Pointer([mbmi], 0, C.Ptr(tu.ctype("MB_MODE_INFO"))),
+                         cur_buf=ybuf)
+                    rate, rerr, sse = (tu.buffer("int", 1), tu.buffer("int64_t", 1),
+                                       tu.buffer("int64_t", 1))
+                    qc, dq = tu.buffer("tran_low_t", n * n), tu.buffer("tran_low_t", n * n)
+                    tu.func("txfm_quant_rdcost")(x, diff, n, sp, n, dp, n, coeff, qc, dq, n, n,
+                                                 ts, rate, rerr, sse)
+                    recs.append([satd, rate.buf[0], rerr.buf[0], sse.buf[0]])
+                    srcs.append(src)
+                    preds.append(prd)
+                    recons.append(list(db.buf))
+                    qs.append(qindex)
+            k = "%d_bd%d" % (n, bd)
+            out["rec_" + k] = np.array(recs, np.int64)
+            out["src_" + k] = np.array(srcs, np.int32).reshape(-1, n, n)
+            out["pred_" + k] = np.array(preds, np.int32).reshape(-1, n, n)
+            out["recon_" + k] = np.array(recons, np.int32).reshape(-1, n, n)
+            out["q_" + k] = np.array(qs, np.int32)
+            print("  tpl %s" % k)
+    np.savez_compressed(os.path.join(HERE, "fix_tpl.npz"), **out)
+
+
 def main(argv):
     sections = argv or ["txfm", "qparams", "quant", "inv", "pixel", "wht", "nmv", "mcomp",
-                        "subpel"]
+                        "subpel", "tpl"]
     t0 = time.time()
     ttx = None
     if "txfm" in sections or "inv" in sections or "wht" in sections:
@@ -847,6 +929,8 @@ def main(argv):
         gen_mcomp()
     if "subpel" in sections:
         gen_subpel()
+    if "tpl" in sections:
+        gen_tpl()
     print("done in %.0fs" % (time.time() - t0))
 
 

@@ -127,3 +127,30 @@ def test_tpl_frame_chain_vs_oracle(T):
         np.testing.assert_array_equal(got[f], exp[f], err_msg=f)
     np.testing.assert_array_equal(grec, erec)
     assert len(set(got["best_ref"])) > 1
+
+
+@pytest.mark.parametrize("n", [8, 16, 32])
+@pytest.mark.parametrize("bd", [8, 10, 12])
+def test_tpl_block_batch_vs_reference(T, n, bd):
+    """lavish_tpl_block_batch against tpl_get_satd_cost + txfm_quant_rdcost
+    executed from the reference (tests/golden/fix_tpl.npz), the blocks of one
+    qindex side by side in a plane.  No oracle in the loop."""
+    import os
+    F = dict(np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden",
+                                  "fix_tpl.npz")))
+    k = "%d_bd%d" % (n, bd)
+    dt = np.uint8 if bd == 8 else np.uint16
+    qs = F["q_" + k]
+    for q in sorted(set(qs.tolist())):
+        idx = np.nonzero(qs == q)[0]
+        src = np.concatenate([F["src_" + k][i] for i in idx], axis=1).astype(dt)
+        pred = np.concatenate([F["pred_" + k][i] for i in idx], axis=1).astype(dt)[None]
+        got, grec, gcost = _run(T, src, pred, n, bd, int(q))
+        exp = F["rec_" + k][idx]
+        msg = "%s q %d" % (k, q)
+        np.testing.assert_array_equal(got["inter_cost"], exp[:, 0], err_msg=msg)
+        np.testing.assert_array_equal(got["rate_cost"], exp[:, 1], err_msg=msg)
+        np.testing.assert_array_equal(got["recon_error"], exp[:, 2], err_msg=msg)
+        np.testing.assert_array_equal(got["sse"], exp[:, 3], err_msg=msg)
+        np.testing.assert_array_equal(
+            grec, np.concatenate([F["recon_" + k][i] for i in idx], axis=1).astype(dt), err_msg=msg)

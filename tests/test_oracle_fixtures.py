@@ -244,3 +244,23 @@ def test_subpel_search_vs_reference():
                                           err_msg=msg + " " + f)
         n += len(rows)
     assert n == len(F["jobs"])
+
+
+@pytest.mark.parametrize("n", [8, 16, 32])
+@pytest.mark.parametrize("bd", [8, 10, 12])
+def test_tpl_block_vs_reference(n, bd):
+    """orc_tpl_block_batch (one prediction) against tpl_get_satd_cost +
+    txfm_quant_rdcost executed from the reference (tests/golden/fix_tpl.npz):
+    satd, rate, recon_error, sse and the reconstruction."""
+    F = _load("fix_tpl.npz")
+    k = "%d_bd%d" % (n, bd)
+    dt = np.uint8 if bd == 8 else np.uint16
+    for i, (rec, q) in enumerate(zip(F["rec_" + k], F["q_" + k])):
+        src = F["src_" + k][i].astype(dt)
+        pred = F["pred_" + k][i].astype(dt)[None]
+        got, recon, costs = O.tpl_block_batch(src, pred, n, bd, int(q))
+        msg = "%s block %d q %d" % (k, i, q)
+        assert [got["inter_cost"][0], got["rate_cost"][0], got["recon_error"][0],
+                got["sse"][0]] == list(rec), msg
+        assert costs[0, 0] == rec[0], msg
+        np.testing.assert_array_equal(recon, F["recon_" + k][i].astype(dt), err_msg=msg)

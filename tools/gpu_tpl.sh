@@ -1,0 +1,8 @@
+#!/bin/bash
+# TPL leg: bench line + kernel-trace stats
+cd "$GRAFT_REPO_ROOT"
+mkdir -p gpurun_out
+timeout -k 10 300 python -u bench.py --workload tpl --steps 20 --warmup 5 > gpurun_out/bench_tpl.log 2>&1; rc=$?; echo "bench rc=$rc"; [ $rc -ne 0 ] && { tail -5 gpurun_out/bench_tpl.log; exit $rc; }
+grep '^{' gpurun_out/bench_tpl.log | cut -c1-300
+cd /tmp && export TMPDIR=/tmp
+timeout -k 10 180 rocprofv3 --kernel-trace --stats --output-format csv -d "$GRAFT_REPO_ROOT/gpurun_out/prof_tpl" -o k -- python3 "$GRAFT_REPO_ROOT/bench.py" --workload tpl --steps 10 --warmup 2 --no-cpu > "$GRAFT_REPO_ROOT/gpurun_out/prof_tpl.log" 2>&1; echo "prof rc=$?"
