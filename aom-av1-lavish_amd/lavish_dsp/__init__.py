@@ -124,6 +124,56 @@ for _s, _name in enumerate(TX_SIZES):
 _lib.av1_lowbd_fwd_txfm_hip.argtypes = [_vp, _vp, _i32, ctypes.POINTER(TxfmParam)]
 
 
+class PlaneQuant(ctypes.Structure):
+    """LavishPlaneQuant: MACROBLOCK_PLANE's *_QTX tables ([0] DC, [1] AC)."""
+    _fields_ = [(n, ctypes.c_int16 * 2) for n in
+                ("zbin", "round_fp", "quant_fp", "round", "quant", "quant_shift", "dequant")]
+
+
+_lib.lavish_build_plane_quant.argtypes = [_i32, _i32, _i32, _i32, ctypes.POINTER(PlaneQuant)]
+_lib.lavish_build_plane_quant.restype = _i32
+_lib.lavish_av1_quant_batch.argtypes = [_vp, _i32, _i32, _i32, _i32, ctypes.POINTER(PlaneQuant),
+                                        _i32, _i32, ctypes.c_uint32, _i32, _vp, _vp, _vp, _vp,
+                                        _vp, _vp]
+_lib.lavish_av1_quant_batch.restype = _i32
+# xform_quant_idx of lavish_av1_quant_batch (AV1_XFORM_QUANT) + the satd gate
+AV1_QUANT_FP, AV1_QUANT_B, AV1_QUANT_DC, AV1_QUANT_SKIP, AV1_QUANT_SATD_GATE = range(5)
+
+
+def build_plane_quant(bit_depth, qindex, quant_sharpness=0, y_dc_delta_q=0):
+    q = PlaneQuant()
+    if _lib.lavish_build_plane_quant(bit_depth, qindex, quant_sharpness, y_dc_delta_q,
+                                     ctypes.byref(q)) != 0:
+        raise ValueError("lavish_build_plane_quant(%d, %d) failed" % (bit_depth, qindex))
+    return q
+
+
+def av1_quant_batch(coeff, tx_size, tx_type, bit_depth, pq, mode, skip_trellis=0,
+                    threshold=0xFFFFFFFF, qstep=0, dc_only=None, stream=None):
+    """lavish_av1_quant_batch over a device int32 [nblocks, n] coefficient
+    tensor (n = max_eob(tx_size)); returns (qcoeff, dqcoeff, eob, flags)."""
+    import torch
+    n = max_eob(tx_size)
+    assert coeff.dtype == torch.int32 and coeff.is_contiguous() and coeff.shape[-1] == n
+    nb = coeff.numel() // n
+    qc, dq = torch.empty_like(coeff), torch.empty_like(coeff)
+    eob = torch.empty(nb, dtype=torch.int16, device=coeff.device)
+    flags = torch.empty(nb, dtype=torch.uint8, device=coeff.device)
+    if dc_only is not None:
+        assert dc_only.dtype == torch.uint8 and dc_only.numel() >= nb and dc_only.is_cuda
+    rc = _lib.lavish_av1_quant_batch(_p_t(coeff), nb, tx_size, tx_type, bit_depth,
+                                     ctypes.byref(pq), mode, skip_trellis, threshold, qstep,
+                                     _p_t(dc_only) if dc_only is not None else None, _p_t(qc),
+                                     _p_t(dq), _p_t(eob), _p_t(flags), _stream_ptr(stream))
+    if rc != 0:
+        raise ValueError("lavish_av1_quant_batch rejected its arguments (rc=%d)" % rc)
+    return qc, dq, eob, flags
+
+
+def _p_t(t):
+    return ctypes.c_void_p(t.data_ptr())
+
+
 class BitDepthInfo(ctypes.Structure):
     """BitDepthInfo (av1/common/blockd.h:952-960)."""
     _fields_ = [("bit_depth", ctypes.c_int), ("use_highbitdepth_buf", ctypes.c_int)]

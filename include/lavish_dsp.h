@@ -137,6 +137,47 @@ int lavish_quantize_batch(const int32_t *coeff, int n, int nblocks,
                           const LavishQuantParams *qp, int32_t *qcoeff,
                           int32_t *dqcoeff, uint16_t *eob, void *stream);
 
+/* ---- av1_quant: quantizer selection ------------------
+ * The tables av1_quant reads from MACROBLOCK_PLANE (*_QTX, [0] DC, [1] AC;
+ * av1/encoder/block.h), as av1_build_quantizer fills them. */
+typedef struct LavishPlaneQuant {
+  int16_t zbin[2], round_fp[2], quant_fp[2], round[2], quant[2], quant_shift[2],
+      dequant[2];
+} LavishPlaneQuant;
+int lavish_build_plane_quant(int bit_depth, int qindex, int quant_sharpness,
+                             int y_dc_delta_q, LavishPlaneQuant *out);
+
+/* xform_quant_idx (AV1_XFORM_QUANT, av1/encoder/encodemb.h) plus the
+ * search_tx_type selection */
+enum {
+  LAVISH_AV1_QUANT_FP = 0,   /* av1_quantize_fp_facade / highbd */
+  LAVISH_AV1_QUANT_B = 1,    /* av1_quantize_b_facade / highbd */
+  LAVISH_AV1_QUANT_DC = 2,   /* av1_quantize_dc_facade / highbd */
+  LAVISH_AV1_QUANT_SKIP = 3, /* AV1_XFORM_QUANT_SKIP_QUANT: outputs untouched */
+  /* search_tx_type (tx_search.c:2140-2169): skip_trellis ? B : FP, then per
+   * block skip_trellis_opt_based_on_satd (:1923-1955) -> B without trellis
+   * when the satd gate fires, else FP with trellis */
+  LAVISH_AV1_QUANT_SATD_GATE = 4
+};
+
+/* av1_quant (av1/encoder/encodemb.c:308-341) over nblocks contiguous blocks
+ * of n = av1_get_max_eob(tx_size) coefficients (device): the facade of `mode`
+ * (is_hbd = bit_depth > 8, log_scale of tx_size, scan of (tx_size, tx_type),
+ * no quantization matrix) -> qcoeff / dqcoeff [nblocks][n], eob[nblocks].
+ * SATD_GATE mode: skip_trellis, coeff_opt_satd_threshold
+ * (coeff_opt_thresholds[1], UINT_MAX = off), qstep (dequant_QTX[1] >>
+ * (hbd ? bd - 5 : 3)) and the optional per-block dc_only flags as the
+ * reference passes them.  flags (device, nullable) [nblocks]: bit 0 =
+ * use_optimize_b (the caller's trellis, av1_optimize_b, is still due for
+ * these), bits 1-2 = the quantizer used.  Returns 0 or negative on bad
+ * arguments. */
+int lavish_av1_quant_batch(const int32_t *coeff, int nblocks, int tx_size,
+                           int tx_type, int bit_depth, const LavishPlaneQuant *pq,
+                           int mode, int skip_trellis,
+                           unsigned coeff_opt_satd_threshold, int qstep,
+                           const uint8_t *dc_only, int32_t *qcoeff, int32_t *dqcoeff,
+                           uint16_t *eob, uint8_t *flags, void *stream);
+
 /* ---- pixel-domain batch kernels ----------------------------------------- */
 /* One job = one block.  Offsets are in ELEMENTS (u8 or u16 samples / int16
  * residual words) from the plane base pointers passed to the call.  Which

@@ -352,6 +352,13 @@ void orc_tpl_block_batch(const void *src, int src_stride, const void *preds, lon
                          const OrcQuant *q, OrcTplBlock *out, void *recon, int recon_stride,
                          int32_t *ref_costs, int threads);
 
+/* ---- av1_quant selection (oracle_qfacade.c): mode 0 FP, 1 B, 2 DC, 3 skip
+ * quant, 4 search_tx_type's satd gate; returns use_optimize_b | kind << 1 -- */
+int orc_av1_quant_block(const int32_t *coeff, int tx_size, int tx_type, int bd,
+                        const OrcQuant *q, int mode, int skip_trellis, unsigned threshold,
+                        int qstep, int dc_only, int32_t *qcoeff, int32_t *dqcoeff,
+                        uint16_t *eob);
+
 #ifdef __cplusplus
 }
 #endif

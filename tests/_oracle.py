@@ -776,3 +776,20 @@ def tpl_block_batch(src, preds, bsize, bd, qindex, threads=1):
     fn(P(src), W, P(preds), preds[0].size, W, nrefs, W, H, bsize, bd, ctypes.byref(q), P(out),
        P(recon), W, P(costs), threads)
     return out, recon, costs
+
+
+def av1_quant_block(coeff, tx_size, tx_type, bd, qindex, mode, skip_trellis=0,
+                    threshold=0xFFFFFFFF, qstep=0, dc_only=0):
+    """orc_av1_quant_block -> (flags, qcoeff, dqcoeff, eob)."""
+    L = lib()
+    fn = L.orc_av1_quant_block
+    fn.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                   ctypes.POINTER(OrcQuant), ctypes.c_int, ctypes.c_int, ctypes.c_uint,
+                   ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
+    c = np.ascontiguousarray(coeff, np.int32)
+    qc, dq = np.zeros(len(c), np.int32), np.zeros(len(c), np.int32)
+    eob = np.zeros(1, np.uint16)
+    q = build_quant(bd, qindex)
+    flags = fn(P(c), tx_size, tx_type, bd, ctypes.byref(q), mode, skip_trellis, threshold, qstep,
+               dc_only, P(qc), P(dq), P(eob))
+    return flags, qc, dq, int(eob[0])

@@ -2092,6 +2092,9 @@ class TU:
             return (lambda fr: None), VOID
         if name in ("fprintf", "printf", "fflush"):
             return (lambda fr: 0), INT
+        if name in ("__builtin_expect",):  # LIKELY / UNLIKELY (aom_ports/mem.h)
+            (af, at), _ = A
+            return af, at
         if name in ("__builtin_clz",):
             (af, _), = A
             return (lambda fr: 32 - (af(fr) & 0xFFFFFFFF).bit_length()), INT

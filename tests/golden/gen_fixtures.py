@@ -898,9 +898,105 @@ def gen_tpl():
     np.savez_compressed(os.path.join(HERE, "fix_tpl.npz"), **out)
 
 
+QF_SIZES = [0, 1, 2, 3, 4, 6, 9, 12, 17]    # TX_4X4 8X8 16X16 32X32 64X64 8X4 16X32 64X32 16X64
+QF_GATES = [(0, 86), (0, 142), (0, 0), (0, 0xFFFFFFFF), (1, 86)]   # (skip_trellis, threshold)
+
+
+def gen_qfacade(txfm_fix):
+    """skip_trellis_opt_based_on_satd (av1/encoder/tx_search.c:1923-1955) and
+    av1_quant (av1/encoder/encodemb.c:308-341) as search_tx_type drives them
+    (:2140-2169), on forward-transform outputs of fix_txfm.npz scaled to
+    several magnitudes: bd 8 / 10 / 12, qindex 20 / 120 / 240, thresholds of
+    coeff_opt_thresholds incl. UINT_MAX and skip_trellis; plus the DC facade."""
+    tu = C.TU(REF, ["av1/encoder/tx_search.c", "av1/encoder/encodemb.c", "aom_dsp/avg.c",
+                    "av1/encoder/av1_quantize.c", "aom_dsp/quantize.c",
+                    "av1/common/quant_common.c", "av1/common/scan.c",
+                    "av1/encoder/encodetxb.c", "av1/common/idct.c"], C.reference_defines(REF))
+    check_errors(tu, ["skip_trellis_opt_based_on_satd", "av1_quant", "av1_setup_quant",
+                      "av1_build_quantizer"])
+    E = tu.enums
+    rnd = ACMRandom(0xbaba + 7)
+    rows = []
+    coeffs, qcs, dqcs = [], [], []
+    for bd in (8, 10, 12):
+        quants = tu.struct_obj("QUANTS")
+        deq = tu.struct_obj("Dequants")
+        tu.func("av1_build_quantizer")(bd, 0, 0, 0, 0, 0, quants, deq, 0)
+        for s in QF_SIZES:
+            n = 1024 if s in (4, 11, 12) else (512 if s in (17, 18) else TX_W[s] * TX_H[s])
+            t = 0
+            src = txfm_fix["out_%d_%d" % (s, t)]
+            for qindex in (20, 120, 240):
+                for gi, (skip_trellis, thr) in enumerate(QF_GATES + [(None, None)]):
+                    b = rnd.generate(len(src))
+                    scale = (1, 4, 16)[rnd.generate(3)]
+                    base = src[b].astype(np.int64)
+                    if s in (4, 11, 12, 17):  # 64-point: the kept 32x32 / 32x16 quadrant
+                        base = base[:n]
+                    c = np.clip(base // scale << (bd - 8), -(1 << (bd + 7)), (1 << (bd + 7)) - 1)
+                    dc_only = int(rnd.generate(4) == 0)
+                    if dc_only:
+                        c[1:] = 0
+                    x = tu.struct_obj("MACROBLOCK")
+                    X = x.buf[0]
+                    p0 = _get(X, "plane")[0]
+                    cb = tu.buffer("tran_low_t", c.tolist())
+                    qb, db = tu.buffer("tran_low_t", n), tu.buffer("tran_low_t", n)
+                    eb = tu.buffer("uint16_t", 1)
+                    ec = tu.buffer("uint8_t", 1)
+                    Q, D = quants.buf[0], deq.buf[0]
+                    for fld, srct, nm in (("quant_fp_QTX", Q, "y_quant_fp"),
+                                          ("round_fp_QTX", Q, "y_round_fp"),
+                                          ("quant_QTX", Q, "y_quant"),
+                                          ("quant_shift_QTX", Q, "y_quant_shift"),
+                                          ("zbin_QTX", Q, "y_zbin"), ("round_QTX", Q, "y_round"),
+                                          ("dequant_QTX", D, "y_dequant_QTX")):
+                        _set(p0, **{fld: C.Pointer(_get(srct, nm), 8 * qindex,
+                                                   tu.ctype("int16_t"))})
+                    _set(p0, coeff=cb, qcoeff=qb, dqcoeff=db, eobs=eb, txb_entropy_ctx=ec)
+                    _set(_get(X, "e_mbd"), bd=bd)
+                    _set(X, seg_skip_block=0)
+                    qp = tu.struct_obj("QUANT_PARAM")
+                    tp = tu.struct_obj("TxfmParam")
+                    _set(tp.buf[0], tx_type=t, tx_size=s, is_hbd=int(bd > 8), bd=bd)
+                    deqv = _get(D, "y_dequant_QTX")[8 * qindex + 1]
+                    qstep = deqv >> ((bd - 5) if bd > 8 else 3)
+                    if skip_trellis is None:  # the DC facade
+                        tu.func("av1_setup_quant")(s, 0, E["AV1_XFORM_QUANT_DC"], 0, qp)
+                        mode, flag = 2, 2 << 1
+                    else:
+                        tu.func("av1_setup_quant")(s, int(not skip_trellis),
+                                                   E["AV1_XFORM_QUANT_B"] if skip_trellis
+                                                   else E["AV1_XFORM_QUANT_FP"], 0, qp)
+                        tu.func("skip_trellis_opt_based_on_satd")(x, qp, 0, 0, s, 0, qstep, thr,
+                                                                  skip_trellis, dc_only)
+                        P_ = qp.buf[0]
+                        mode = 4
+                        flag = _get(P_, "use_optimize_b") | (_get(P_, "xform_quant_idx") << 1)
+                    tu.func("av1_quant")(x, 0, 0, tp, qp)
+                    rows.append([bd, s, t, qindex, mode, skip_trellis or 0,
+                                 thr if thr is not None else 0, qstep, dc_only, flag, eb.buf[0],
+                                 len(coeffs)])
+                    pad = np.zeros(1024, np.int32)
+                    pad[:n] = c
+                    coeffs.append(pad)
+                    q = np.zeros(1024, np.int32)
+                    q[:n] = qb.buf
+                    qcs.append(q)
+                    d = np.zeros(1024, np.int32)
+                    d[:n] = db.buf
+                    dqcs.append(d)
+            print("  qfacade bd %d size %d: %d blocks" % (bd, s, len(rows)))
+    out = {"rows": np.array(rows, np.int64), "coeff": np.stack(coeffs),
+           "qcoeff": np.stack(qcs), "dqcoeff": np.stack(dqcs),
+           "row_fields": np.array(["bd", "tx_size", "tx_type", "qindex", "mode", "skip_trellis",
+                                   "threshold", "qstep", "dc_only", "flags", "eob", "index"])}
+    np.savez_compressed(os.path.join(HERE, "fix_qfacade.npz"), **out)
+
+
 def main(argv):
     sections = argv or ["txfm", "qparams", "quant", "inv", "pixel", "wht", "nmv", "mcomp",
-                        "subpel", "tpl"]
+                        "subpel", "tpl", "qfacade"]
     t0 = time.time()
     ttx = None
     if "txfm" in sections or "inv" in sections or "wht" in sections:
@@ -931,6 +1027,8 @@ def main(argv):
         gen_subpel()
     if "tpl" in sections:
         gen_tpl()
+    if "qfacade" in sections:
+        gen_qfacade(dict(np.load(os.path.join(HERE, "fix_txfm.npz"))))
     print("done in %.0fs" % (time.time() - t0))
 
 

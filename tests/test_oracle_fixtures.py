@@ -264,3 +264,26 @@ def test_tpl_block_vs_reference(n, bd):
                 got["sse"][0]] == list(rec), msg
         assert costs[0, 0] == rec[0], msg
         np.testing.assert_array_equal(recon, F["recon_" + k][i].astype(dt), err_msg=msg)
+
+
+def test_av1_quant_selection_vs_reference():
+    """orc_av1_quant_block against skip_trellis_opt_based_on_satd + av1_quant
+    executed from the reference (tests/golden/fix_qfacade.npz): the quantizer
+    chosen, use_optimize_b, qcoeff, dqcoeff and eob."""
+    F = _load("fix_qfacade.npz")
+    J = {n: i for i, n in enumerate(F["row_fields"])}
+    kinds = set()
+    for r in F["rows"]:
+        g = lambda k: int(r[J[k]])
+        n = O.max_eob(g("tx_size"))
+        i = g("index")
+        flags, qc, dq, eob = O.av1_quant_block(F["coeff"][i][:n], g("tx_size"), g("tx_type"),
+                                               g("bd"), g("qindex"), g("mode"), g("skip_trellis"),
+                                               g("threshold"), g("qstep"), g("dc_only"))
+        msg = str({k: g(k) for k in J})
+        assert flags == g("flags"), msg
+        assert eob == g("eob"), msg
+        np.testing.assert_array_equal(qc, F["qcoeff"][i][:n], err_msg=msg)
+        np.testing.assert_array_equal(dq, F["dqcoeff"][i][:n], err_msg=msg)
+        kinds.add(flags)
+    assert {0 << 1 | 1, 1 << 1, 2 << 1} <= kinds  # FP+trellis, B, DC all exercised
