@@ -558,7 +558,8 @@ __device__ __forceinline__ void bigdia_site(int s, int i, int& dr, int& dc) {
 // SAD is kept as raw_bestsad.
 template <int W, int H, bool SKIP>
 __device__ int pattern(const Ctx& c, int lane, int srow, int scol, int search_step, bool do_init,
-                       bool want_cl, int (&cl)[5], int& brow, int& bcol, int& steps) {
+                       bool want_cl, int (&cl)[5], int& brow, int& bcol, int& steps,
+                       int& nsad) {
   Search<W, H, SKIP> S;
   S.load_src(c, lane);
   const int g = lane >> 3;
@@ -570,6 +571,7 @@ __device__ int pattern(const Ctx& c, int lane, int srow, int scol, int search_st
   bool has_sad = false;
   uint32_t raw = rdlane(S.group_sad(c, (int64_t)br * c.rs + bc), 0);
   uint32_t best = raw + mvsad_cost(c, br, bc);
+  ++nsad;
   // one round: candidate idx (groups g < cnt) of scale s around (br, bc);
   // returns the winning group or -1.  clmode 1: raw SADs of the valid
   // candidates into cl (calc_sad4 / calc_sad_update_bestmv); 2: also INT_MAX
@@ -586,6 +588,7 @@ __device__ int pattern(const Ctx& c, int lane, int srow, int scol, int search_st
     const uint32_t key = valid ? ((mine + mvsad_cost(c, r, cc)) << 3) | (uint32_t)g : ~0u;
     uint32_t kmin = groups_min(key);
     ++steps;
+    nsad += __popcll(__ballot(valid)) >> 3;  // candidate blocks read this round
     if (clmode) {
       const uint32_t tag = valid ? (mine << 1) | 1u : 0u;  // SADs < 2^22
       for (int i = 0; i < cnt; ++i) {
@@ -666,7 +669,11 @@ __device__ int pattern(const Ctx& c, int lane, int srow, int scol, int search_st
   }
   brow = br;
   bcol = bc;
-  if (want_cl) int_sad_list(S, c, lane, br, bc, has_sad, cl);
+  if (want_cl) {
+    int_sad_list(S, c, lane, br, bc, has_sad, cl);
+    if (!has_sad) nsad += 1 + (cl[1] != INT_MAX) + (cl[2] != INT_MAX) + (cl[3] != INT_MAX) +
+                          (cl[4] != INT_MAX);
+  }
   return var_cost<W, H>(c, lane, br, bc);  // get_mvpred_var_cost
 }
 
@@ -723,14 +730,13 @@ __global__ __launch_bounds__(256, (W <= 16 && H <= 16) ? 8 : 7) void diamond_ker
       return full_pixel_diamond<W, H, SK>(c, lane, jb.start_row, jb.start_col, step_param, br,
                                           bc, steps, searches, win, want_cl, cl);
     } else {
-      ++searches;
-      // bigdia_search (do_init 1) / fast_dia / vfast_dia / fast_bigdia (mcomp.c:1266-1316)
+      // searches: the SAD blocks read (start, candidates, cost list) (do_init 1) / fast_dia / vfast_dia / fast_bigdia (mcomp.c:1266-1316)
       const int step = method == kBigdia        ? step_param
                        : method == kFastDiamond ? max(kMaxSteps - 2, step_param)
                        : method == kVfastDiamond ? max(kMaxSteps - 1, step_param)
                                                  : max(kMaxSteps - 3, step_param);
       return pattern<W, H, SK>(c, lane, jb.start_row, jb.start_col, step, method == kBigdia,
-                               want_cl, cl, br, bc, steps);
+                               want_cl, cl, br, bc, steps, searches);
     }
   };
   // use_downsampled_sad applies to blocks at least 16 high (mcomp.c:132-133)

@@ -640,6 +640,12 @@ def main_tpl(args):
     legs = [sum(ev[k][i].elapsed_time(ev[k][i + 1]) for k in range(K)) / K for i in range(4)]
     names = ["fullpel_fast_bigdia", "subpel", "inter_pred", "tpl_block"]
     blk_bytes = tpl_block_bytes(W, H, R)
+    fp_res = M.results_numpy(tf.fp)
+    # full-pel leg bytes: per job the source block, the var cost's 2 blocks,
+    # 16 + 20 B out; every SAD block it read (results' `searches` field for
+    # the pattern methods: start, in-range candidates, cost list)
+    nj = len(fp_res)
+    fp_bytes = nj * (3 * bs * bs + 36) + int(fp_res["searches"].astype(np.int64).sum()) * bs * bs
     sb = sb64_count(W, H)
     recs = T.records_numpy(tf.out)
     line = {
@@ -664,14 +670,25 @@ def main_tpl(args):
                         "%d SB64/frame" % (W, H, R, args.qindex, sb),
             "parallelism": "frame-per-rank x%d" % world,
         },
-        "roofline": {"bound": "hbm", "kernel": "tpl_kernel<16,0,u8> (lavish_tpl_block_batch)",
-                     "achieved": round(blk_bytes / (legs[3] * 1e-3) / 1e9, 1),
-                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "traffic": None,
-                     "avg_launch_ms": round(legs[3], 4),
-                     "algorithmic_bytes_per_launch": blk_bytes},
+        "roofline": ({"bound": "hbm",
+                      "kernel": "diamond_kernel<16,16,true> (FAST_BIGDIA, "
+                                "lavish_full_pixel_search_batch)",
+                      "achieved": round(fp_bytes / (legs[0] * 1e-3) / 1e9, 1),
+                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "traffic": None,
+                      "avg_launch_ms": round(legs[0], 4),
+                      "algorithmic_bytes_per_launch": fp_bytes}
+                     if legs[0] >= legs[3] else
+                     {"bound": "hbm", "kernel": "tpl_kernel<16,0,u8> (lavish_tpl_block_batch)",
+                      "achieved": round(blk_bytes / (legs[3] * 1e-3) / 1e9, 1),
+                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "traffic": None,
+                      "avg_launch_ms": round(legs[3], 4),
+                      "algorithmic_bytes_per_launch": blk_bytes}),
         "legs_ms": {n: round(v, 4) for n, v in zip(names, legs)},
         "tpl": {"blocks": int(len(recs)), "mean_eob": round(float(recs["eob"].mean()), 2),
-                "refs_chosen": int(len(set(recs["best_ref"].tolist())))},
+                "refs_chosen": int(len(set(recs["best_ref"].tolist()))),
+                "fullpel_sad_blocks_per_job": round(float(fp_res["searches"].mean()), 2),
+                "block_leg": {"ms": round(legs[3], 4), "algorithmic_bytes": blk_bytes,
+                              "achieved_GBps": round(blk_bytes / (legs[3] * 1e-3) / 1e9, 1)}},
     }
     line["roofline"]["frac"] = round(line["roofline"]["achieved"] / HBM_PEAK_GBS, 4)
     if rank == 0 and world == 1 and not args.no_cpu:

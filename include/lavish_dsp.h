@@ -401,8 +401,10 @@ typedef struct LavishDiamondJob {
 typedef struct LavishDiamondResult {
   int16_t best_row, best_col; /* FULLPEL_MV */
   int32_t bestsme;  /* returned var cost: aom_variance + mv_err_cost */
-  int32_t steps;    /* 8-site diamond steps evaluated */
-  int32_t searches; /* diamond_search_sad runs */
+  int32_t steps;    /* DIAMOND: 8-site steps; pattern methods: candidate rounds */
+  int32_t searches; /* DIAMOND: diamond_search_sad runs; pattern methods
+                       (lavish_full_pixel_search_batch, BIGDIA family): the
+                       SAD blocks read (start, in-range candidates, cost list) */
 } LavishDiamondResult;
 
 /* mv_cost_type: MV_COST_TYPE (av1/encoder/mcomp.h:31-38) 1 L1_LOWRES,
