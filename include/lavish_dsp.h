@@ -178,6 +178,52 @@ int lavish_av1_quant_batch(const int32_t *coeff, int nblocks, int tx_size,
                            const uint8_t *dc_only, int32_t *qcoeff, int32_t *dqcoeff,
                            uint16_t *eob, uint8_t *flags, void *stream);
 
+/* ---- coefficient rate ---------------------------- */
+/* MACROBLOCK::coeff_costs, field for field (CoeffCosts, av1/encoder/block.h:
+ * 172-211): LV_MAP_COEFF_COST per [txs_ctx][plane_type] and LV_MAP_EOB_COST
+ * per [eob_multi_size][plane_type], as av1_fill_coeff_costs leaves them (the
+ * caller copies x->coeff_costs to the device once per frame / cdf update). */
+typedef struct LavishCoeffCost {
+  int32_t txb_skip_cost[13][2];  /* TXB_SKIP_CONTEXTS */
+  int32_t base_eob_cost[4][3];   /* SIG_COEF_CONTEXTS_EOB */
+  int32_t base_cost[42][8];      /* SIG_COEF_CONTEXTS */
+  int32_t eob_extra_cost[9][2];  /* EOB_COEF_CONTEXTS */
+  int32_t dc_sign_cost[3][2];    /* DC_SIGN_CONTEXTS */
+  int32_t lps_cost[21][26];      /* LEVEL_CONTEXTS x (COEFF_BASE_RANGE + 1) * 2 */
+} LavishCoeffCost;
+typedef struct LavishEobCost {
+  int32_t eob_cost[2][11];
+} LavishEobCost;
+typedef struct LavishCoeffCosts {
+  LavishCoeffCost coeff_costs[5][2]; /* [TX_SIZES][PLANE_TYPES] */
+  LavishEobCost eob_costs[7][2];
+} LavishCoeffCosts;
+/* TXB_CTX (av1/common/txb_common.h:22-25) */
+typedef struct LavishTxbCtx {
+  int32_t txb_skip_ctx; /* 0..12 */
+  int32_t dc_sign_ctx;  /* 0..2 */
+} LavishTxbCtx;
+
+enum {
+  LAVISH_COEFF_RATE_EXACT = 0,    /* av1_cost_coeffs_txb (txb_rdopt.c:599-624) */
+  LAVISH_COEFF_RATE_LAPLACIAN = 1 /* av1_cost_coeffs_txb_laplacian, adjust_eob 0 */
+};
+
+/* Replaces av1_cost_coeffs_txb / av1_cost_coeffs_txb_laplacian (av1/encoder/
+ * txb_rdopt.c:599-660; cost_coeffs, tx_search.c:1903-1921, is the caller) for
+ * nblocks blocks of one (tx_size, tx_type, plane): qcoeff [nblocks][n], n =
+ * av1_get_max_eob(tx_size), raster order as the quantizer writes it (the kept
+ * 32x32 quadrant for 64-point sizes); eob [nblocks] = p->eobs (the scan
+ * position after the last nonzero coefficient, as the quantizers return it);
+ * costs / txb_ctx (nullable: all {0, 0}) / rate [nblocks] on the device;
+ * tx_type_cost = get_tx_type_cost's value (txb_rdopt.c:263-294; a
+ * MACROBLOCK-level table lookup the caller owns), added for plane 0 when
+ * eob > 0.  Returns 0 or negative on bad arguments. */
+int lavish_cost_coeffs_txb_batch(const LavishCoeffCosts *costs, const int32_t *qcoeff,
+                                 const uint16_t *eob, int nblocks, int plane, int tx_size,
+                                 int tx_type, const LavishTxbCtx *txb_ctx, int tx_type_cost,
+                                 int mode, int32_t *rate, void *stream);
+
 /* ---- pixel-domain batch kernels ----------------------------------------- */
 /* One job = one block.  Offsets are in ELEMENTS (u8 or u16 samples / int16
  * residual words) from the plane base pointers passed to the call.  Which

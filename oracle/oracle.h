@@ -359,6 +359,32 @@ int orc_av1_quant_block(const int32_t *coeff, int tx_size, int tx_type, int bd,
                         int qstep, int dc_only, int32_t *qcoeff, int32_t *dqcoeff,
                         uint16_t *eob);
 
+/* ---- coefficient rate (oracle_costcoeffs.c): av1_cost_coeffs_txb and
+ * av1_cost_coeffs_txb_laplacian(adjust_eob 0); the cost tables are
+ * MACROBLOCK::coeff_costs (CoeffCosts, av1/encoder/block.h:172-211) ---- */
+typedef struct {
+  int32_t txb_skip_cost[13][2];
+  int32_t base_eob_cost[4][3];
+  int32_t base_cost[42][8];
+  int32_t eob_extra_cost[9][2];
+  int32_t dc_sign_cost[3][2];
+  int32_t lps_cost[21][26];
+} OrcCoeffCost;
+typedef struct {
+  int32_t eob_cost[2][11];
+} OrcEobCost;
+typedef struct {
+  OrcCoeffCost coeff_costs[5][2];
+  OrcEobCost eob_costs[7][2];
+} OrcCoeffCosts;
+int orc_cost_coeffs_txb(const OrcCoeffCosts *cc, const int32_t *qcoeff, int eob, int plane,
+                        int tx_size, int tx_type, int txb_skip_ctx, int dc_sign_ctx,
+                        int tx_type_cost, int laplacian);
+void orc_cost_coeffs_txb_batch(const OrcCoeffCosts *cc, const int32_t *qcoeff, int n_stride,
+                               const uint16_t *eob, int nblocks, int plane, int tx_size,
+                               int tx_type, const int32_t *txb_ctx, int tx_type_cost,
+                               int laplacian, int32_t *rate);
+
 #ifdef __cplusplus
 }
 #endif

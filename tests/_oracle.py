@@ -793,3 +793,43 @@ def av1_quant_block(coeff, tx_size, tx_type, bd, qindex, mode, skip_trellis=0,
     flags = fn(P(c), tx_size, tx_type, bd, ctypes.byref(q), mode, skip_trellis, threshold, qstep,
                dc_only, P(qc), P(dq), P(eob))
     return flags, qc, dq, int(eob[0])
+
+
+CC_COEFF_COST = 944   # int32 cells of one LV_MAP_COEFF_COST
+CC_EOB_COST = 22      # int32 cells of one LV_MAP_EOB_COST
+
+
+def coeff_costs_blob(coeff_costs, eob_costs):
+    """CoeffCosts (av1/encoder/block.h:806-811) as one flat int32 array:
+    coeff_costs[5][2] (LV_MAP_COEFF_COST) then eob_costs[7][2]."""
+    a = np.ascontiguousarray(coeff_costs, np.int32).reshape(-1)
+    b = np.ascontiguousarray(eob_costs, np.int32).reshape(-1)
+    assert a.size == 10 * CC_COEFF_COST and b.size == 14 * CC_EOB_COST
+    return np.concatenate([a, b])
+
+
+def cost_coeffs_txb(blob, qcoeff, eob, plane, tx_size, tx_type, txb_skip_ctx=0, dc_sign_ctx=0,
+                    tx_type_cost=0, laplacian=False):
+    """orc_cost_coeffs_txb: av1_cost_coeffs_txb / _laplacian(adjust_eob 0)."""
+    fn = lib().orc_cost_coeffs_txb
+    fn.argtypes = [ctypes.c_void_p, ctypes.c_void_p] + [ctypes.c_int] * 8
+    fn.restype = ctypes.c_int
+    q = np.ascontiguousarray(qcoeff, np.int32)
+    return fn(P(blob), P(q), eob, plane, tx_size, tx_type, txb_skip_ctx, dc_sign_ctx,
+              tx_type_cost, int(laplacian))
+
+
+def cost_coeffs_txb_batch(blob, qcoeff, eob, plane, tx_size, tx_type, txb_ctx=None,
+                          tx_type_cost=0, laplacian=False):
+    """orc_cost_coeffs_txb_batch over qcoeff [nblocks, n] -> int32 rates."""
+    fn = lib().orc_cost_coeffs_txb_batch
+    fn.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p,
+                   ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
+                   ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
+    q = np.ascontiguousarray(qcoeff, np.int32)
+    e = np.ascontiguousarray(eob, np.uint16)
+    ctx = None if txb_ctx is None else np.ascontiguousarray(txb_ctx, np.int32)
+    out = np.zeros(q.shape[0], np.int32)
+    fn(P(blob), P(q), q.shape[1], P(e), q.shape[0], plane, tx_size, tx_type,
+       P(ctx) if ctx is not None else None, tx_type_cost, int(laplacian), P(out))
+    return out

@@ -994,9 +994,116 @@ def gen_qfacade(txfm_fix):
     np.savez_compressed(os.path.join(HERE, "fix_qfacade.npz"), **out)
 
 
+CC_TYPES = {16: [0, 3, 6, 9, 10, 11, 12, 15], 32: [0, 9], 64: [0]}   # by max(W, H)
+CC_COEFF_COST = 944   # int32 cells of one LV_MAP_COEFF_COST (av1/encoder/block.h:172-195)
+CC_EOB_COST = 22      # LV_MAP_EOB_COST (block.h:199-202)
+
+
+def cc_scan(tu, s, t):
+    """av1_scan_orders[tx_size][tx_type].scan (av1/common/scan.c)."""
+    so = tu.global_value("av1_scan_orders")
+    e = so[s * 16 + t]
+    sp = e.vals[e.st.index["scan"]]
+    n = max_eob(s)
+    return np.array(sp.buf[sp.off:sp.off + n], np.int64)
+
+
+def cc_block(rnd, scan, eob):
+    """One qcoeff block (raster) whose last nonzero coefficient in scan order
+    sits at scan index eob - 1: levels 0 / 1 / 2 / 3..14 / 15..400 (the
+    Golomb tail, past the levels' 127 clamp) at decreasing odds."""
+    q = np.zeros(len(scan), np.int32)
+    for j in range(eob):
+        r = rnd.generate(100)
+        if r < 45:
+            lv = 0
+        elif r < 70:
+            lv = 1
+        elif r < 80:
+            lv = 2
+        elif r < 94:
+            lv = 3 + rnd.generate(12)
+        else:
+            lv = 15 + rnd.generate(386)
+        if j == eob - 1 and lv == 0:
+            lv = 1 + rnd.generate(20)
+        q[scan[j]] = -lv if rnd.generate(2) else lv
+    return q
+
+
+def gen_costcoeffs():
+    """av1_cost_coeffs_txb and av1_cost_coeffs_txb_laplacian(adjust_eob 0)
+    (av1/encoder/txb_rdopt.c:451-660) for every tx_size over tx types of all
+    three classes, luma (inter, the tx-type cost of get_tx_type_cost
+    :263-294) and chroma, eob 0 / 1 / 2 / random / max, random
+    txb_skip_ctx / dc_sign_ctx, with random LV_MAP_COEFF_COST /
+    LV_MAP_EOB_COST / inter_tx_type_costs tables."""
+    tu = C.TU(REF, ["av1/encoder/txb_rdopt.c", "av1/encoder/encodetxb.c",
+                    "av1/common/txb_common.c", "av1/common/scan.c"], C.reference_defines(REF))
+    check_errors(tu, ["av1_cost_coeffs_txb", "av1_cost_coeffs_txb_laplacian"])
+    E = tu.enums
+    rnd = ACMRandom(0xbaba + 8)
+    x = tu.struct_obj("MACROBLOCK")
+    X = x.buf[0]
+    ccs = _get(X, "coeff_costs")
+    cc_tabs = np.array([rnd.generate(4000) for _ in range(10 * CC_COEFF_COST)], np.int32)
+    eob_tabs = np.array([rnd.generate(4000) for _ in range(14 * CC_EOB_COST)], np.int32)
+    k = 0
+    for obj in _get(ccs, "coeff_costs"):
+        for fld in ("txb_skip_cost", "base_eob_cost", "base_cost", "eob_extra_cost",
+                    "dc_sign_cost", "lps_cost"):
+            cell = _get(obj, fld)
+            cell[:] = cc_tabs[k:k + len(cell)].tolist()
+            k += len(cell)
+    assert k == len(cc_tabs)
+    k = 0
+    for obj in _get(ccs, "eob_costs"):
+        cell = _get(obj, "eob_cost")
+        cell[:] = eob_tabs[k:k + len(cell)].tolist()
+        k += len(cell)
+    assert k == len(eob_tabs)
+    mc = _get(X, "mode_costs")
+    itx = _get(mc, "inter_tx_type_costs")
+    itx[:] = [rnd.generate(3000) for _ in range(len(itx))]
+    mbmi = tu.struct_obj("MB_MODE_INFO")
+    _get(mbmi.buf[0], "ref_frame")[0] = E["LAST_FRAME"]
+    xd = _get(X, "e_mbd")
+    _set(xd, mi=tu.buffer("MB_MODE_INFO *", [mbmi]))
+    xd_p = C.Pointer(X.vals, X.st.index["e_mbd"], tu.ctype("MACROBLOCKD"))
+    rows, blocks = [], []
+    for s in range(19):
+        n = max_eob(s)
+        for t in CC_TYPES[max(TX_W[s], TX_H[s], 16)]:
+            scan = cc_scan(tu, s, t)
+            for plane in (0, 1):
+                for eob in (0, 1, 2, 3 + rnd.generate(max(1, n // 8)), 1 + rnd.generate(n), n):
+                    eob = min(eob, n)
+                    q = cc_block(rnd, scan, eob)
+                    p0 = _get(X, "plane")[plane]
+                    _set(p0, qcoeff=tu.buffer("tran_low_t", q.tolist()),
+                         eobs=tu.buffer("uint16_t", [eob]))
+                    ctx = tu.struct_obj("TXB_CTX")
+                    skip_ctx, dc_ctx = rnd.generate(13), rnd.generate(3)
+                    _set(ctx.buf[0], txb_skip_ctx=skip_ctx, dc_sign_ctx=dc_ctx)
+                    rate = tu.func("av1_cost_coeffs_txb")(x, plane, 0, s, t, ctx, 0)
+                    lap = tu.func("av1_cost_coeffs_txb_laplacian")(x, plane, 0, s, t, ctx, 0, 0)
+                    ttc = tu.func("get_tx_type_cost")(x, xd_p, plane, s, t, 0)
+                    rows.append([s, t, plane, eob, skip_ctx, dc_ctx, ttc, rate, lap, len(blocks)])
+                    pad = np.zeros(1024, np.int32)
+                    pad[:n] = q
+                    blocks.append(pad)
+        print("  costcoeffs size %d: %d blocks" % (s, len(rows)))
+    out = {"rows": np.array(rows, np.int64), "qcoeff": np.stack(blocks),
+           "coeff_costs": cc_tabs, "eob_costs": eob_tabs,
+           "row_fields": np.array(["tx_size", "tx_type", "plane", "eob", "txb_skip_ctx",
+                                   "dc_sign_ctx", "tx_type_cost", "rate", "rate_laplacian",
+                                   "index"])}
+    np.savez_compressed(os.path.join(HERE, "fix_costcoeffs.npz"), **out)
+
+
 def main(argv):
     sections = argv or ["txfm", "qparams", "quant", "inv", "pixel", "wht", "nmv", "mcomp",
-                        "subpel", "tpl", "qfacade"]
+                        "subpel", "tpl", "qfacade", "costcoeffs"]
     t0 = time.time()
     ttx = None
     if "txfm" in sections or "inv" in sections or "wht" in sections:
@@ -1029,6 +1136,8 @@ def main(argv):
         gen_tpl()
     if "qfacade" in sections:
         gen_qfacade(dict(np.load(os.path.join(HERE, "fix_txfm.npz"))))
+    if "costcoeffs" in sections:
+        gen_costcoeffs()
     print("done in %.0fs" % (time.time() - t0))
 
 

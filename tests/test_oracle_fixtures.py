@@ -287,3 +287,27 @@ def test_av1_quant_selection_vs_reference():
         np.testing.assert_array_equal(dq, F["dqcoeff"][i][:n], err_msg=msg)
         kinds.add(flags)
     assert {0 << 1 | 1, 1 << 1, 2 << 1} <= kinds  # FP+trellis, B, DC all exercised
+
+
+def test_cost_coeffs_txb_matches_reference():
+    """orc_cost_coeffs_txb against av1_cost_coeffs_txb and
+    av1_cost_coeffs_txb_laplacian executed from the reference
+    (tests/golden/fix_costcoeffs.npz): every tx size, tx types of the 2D /
+    horizontal / vertical classes, luma and chroma, eob 0 / 1 / 2 / random /
+    max, Golomb-range levels, random cost tables."""
+    F = _load("fix_costcoeffs.npz")
+    J = {n: i for i, n in enumerate(F["row_fields"])}
+    blob = O.coeff_costs_blob(F["coeff_costs"], F["eob_costs"])
+    classes = set()
+    for r in F["rows"]:
+        g = lambda k: int(r[J[k]])
+        n = O.max_eob(g("tx_size"))
+        q = F["qcoeff"][g("index")][:n]
+        args = (blob, q, g("eob"), g("plane"), g("tx_size"), g("tx_type"), g("txb_skip_ctx"),
+                g("dc_sign_ctx"), g("tx_type_cost"))
+        msg = str({k: g(k) for k in J})
+        assert O.cost_coeffs_txb(*args) == g("rate"), msg
+        assert O.cost_coeffs_txb(*args, laplacian=True) == g("rate_laplacian"), msg
+        classes.add(0 if g("tx_type") < 10 else 1 + (g("tx_type") & 1))
+    assert classes == {0, 1, 2}
+    assert (F["rows"][:, J["tx_size"]] == np.arange(19)[:, None]).any(axis=1).all()
