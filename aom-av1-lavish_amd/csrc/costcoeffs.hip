@@ -25,16 +25,13 @@
 // tables and the inverse scan are staged in LDS once per workgroup, which
 // then strides over the batch.  No scatter, no workgroup barrier in the loop
 // (each wave owns its blocks' level maps).
+#include "coeffcost_dev.h"
 #include "lavish_internal.h"
 
 namespace lavish {
 namespace {
 
-// int32 cells of LV_MAP_COEFF_COST (av1/encoder/block.h:172-195) and the
-// field offsets inside it
-constexpr int kCostCells = 944, kEobCells = 22;
-constexpr int kSkip = 0, kBaseEob = 26, kBase = 38, kEobExtra = 374, kDcSign = 392, kLps = 398;
-static_assert(kLps + 21 * 26 == kCostCells, "LV_MAP_COEFF_COST layout");
+using namespace cc;
 static_assert(sizeof(LavishCoeffCost) == kCostCells * 4, "LavishCoeffCost layout");
 static_assert(sizeof(LavishEobCost) == kEobCells * 4, "LavishEobCost layout");
 
@@ -56,73 +53,6 @@ struct CcArgs {
   int wlt, wgt;     // tx_size_wide < / > tx_size_high (av1_nz_map_ctx_offset)
   int tx_type_cost;
 };
-
-__device__ __forceinline__ int min3(int v) { return min(v, 3); }
-
-// get_nz_mag + get_nz_map_ctx_from_stats (txb_common.h:150-224)
-__device__ __forceinline__ int lower_ctx(const CcArgs& a, const uint8_t* lv, int stride, int pos,
-                                         int col, int row) {
-  const uint8_t* l = lv + col * stride + row;
-  int mag = min3(l[stride]) + min3(l[1]);
-  if (a.cls == 0) {
-    mag += min3(l[stride + 1]) + min3(l[2 * stride]) + min3(l[2]);
-  } else if (a.cls == 2) {
-    mag += min3(l[2]) + min3(l[3]) + min3(l[4]);
-  } else {
-    mag += min3(l[2 * stride]) + min3(l[3 * stride]) + min3(l[4 * stride]);
-  }
-  const int ctx = min((mag + 1) >> 1, 4);
-  if (a.cls == 0) {
-    if (pos == 0) return 0;
-    // the av1_nz_map_ctx_offset entry (the algorithm of txb_common.h:199-209)
-    int off;
-    if (a.wlt && row < 2) off = 11;
-    else if (a.wgt && col < 2) off = 16;
-    else if (row + col < 2) off = 1;
-    else if (row + col < 4) off = 6;
-    else off = 21;
-    return ctx + off;
-  }
-  const int idx = a.cls == 1 ? col : row;  // nz_map_ctx_offset_1d
-  return ctx + 26 + (idx == 0 ? 0 : (idx == 1 ? 5 : 10));
-}
-
-// get_br_ctx (txb_common.h:103-135)
-__device__ __forceinline__ int br_ctx(const CcArgs& a, const uint8_t* lv, int stride, int pos,
-                                      int col, int row) {
-  const uint8_t* l = lv + col * stride + row;
-  int mag = l[1] + l[stride];
-  bool near;
-  if (a.cls == 0) {
-    mag += l[stride + 1];
-    near = row < 2 && col < 2;
-  } else if (a.cls == 1) {
-    mag += l[2 * stride];
-    near = col == 0;
-  } else {
-    mag += l[2];
-    near = row == 0;
-  }
-  mag = min((mag + 1) >> 1, 6);
-  return pos == 0 ? mag : mag + (near ? 7 : 14);
-}
-
-// get_br_ctx_eob (txb_common.h:90-101)
-__device__ __forceinline__ int br_ctx_eob(const CcArgs& a, int pos, int col, int row) {
-  if (pos == 0) return 0;
-  const bool near = a.cls == 0 ? (row < 2 && col < 2) : (a.cls == 1 ? col == 0 : row == 0);
-  return near ? 7 : 14;
-}
-
-// get_br_cost + get_golomb_cost (txb_rdopt_utils.h:86-104)
-__device__ __forceinline__ int br_cost(const int32_t* tab, int ctx, int level) {
-  int c = tab[kLps + ctx * 26 + min(level - 3, 12)];
-  if (level >= 15) {
-    const int len = 32 - __clz(level - 14);  // get_msb(r) + 1
-    c += (2 * len - 1) << 9;
-  }
-  return c;
-}
 
 template <int LOGN, bool LAP>
 __global__ __launch_bounds__(256) void cost_coeffs_kernel(CcArgs a) {
@@ -189,43 +119,21 @@ __global__ __launch_bounds__(256) void cost_coeffs_kernel(CcArgs a) {
         const int i = (int16_t)(iv >> (16 * e));
         if (i >= eob) continue;
         const int v = vs[e];
-        const int level = abs(v);
         if (LAP) {
+          const int level = abs(v);
           cost += i == eob - 1 ? (level - 1) << 11 : kCostLut[min(level, 14)];
           continue;
         }
-        const int pos = pos0 + e, row = row0 + e;
-        if (i == eob - 1) {
-          const int ctx = i == 0 ? 0 : (i <= (N >> 3) ? 1 : (i <= (N >> 2) ? 2 : 3));
-          cost += tab[kBaseEob + ctx * 3 + min3(level) - 1];
-          if (level > 2) cost += br_cost(tab, br_ctx_eob(a, pos, col, row), level);
-        } else {
-          cost += tab[kBase + lower_ctx(a, lv, stride, pos, col, row) * 8 + min3(level)];
-          if (level > 2) cost += br_cost(tab, br_ctx(a, lv, stride, pos, col, row), level);
-        }
-        if (level) cost += i ? 512 : tab[kDcSign + dcctx * 2 + (v < 0)];
+        cost += coeff_term(tab, a.cls, a.wlt, a.wgt, lv, stride, N, pos0 + e, col, row0 + e, i,
+                           eob, v, dcctx);
       }
     }
 #pragma unroll
     for (int m = 1; m < G; m <<= 1) cost += __shfl_xor(cost, m);
     if (valid && g == 0) {
       const int skctx = a.ctx ? a.ctx[b].txb_skip_ctx : 0;
-      int r;
-      if (eob == 0) {
-        r = tab[kSkip + skctx * 2 + 1];
-      } else {
-        // get_eob_cost: av1_get_eob_pos_token (encodetxb.c:117-131) as a
-        // bit length, av1_eob_group_start / av1_eob_offset_bits in closed form
-        const int t = eob < 3 ? eob : 33 - __clz(eob - 1);
-        const int bits = t >= 3 ? t - 2 : 0;
-        r = tab[kSkip + skctx * 2] + a.tx_type_cost + cost +
-            tab[kCostCells + (a.cls ? 11 : 0) + t - 1];
-        if (bits > 0) {
-          const int extra = eob - (t >= 2 ? (1 << (t - 2)) + 1 : t);
-          r += tab[kEobExtra + (t - 3) * 2 + ((extra >> (bits - 1)) & 1)] + (bits - 1) * 512;
-        }
-        if (LAP) r += (512 + 739) * (eob - 1);  // const_term + loge_par
-      }
+      int r = txb_rate(tab, a.cls, skctx, eob, a.tx_type_cost, cost);
+      if (LAP && eob > 0) r += (512 + 739) * (eob - 1);  // const_term + loge_par
       a.rate[b] = r;
     }
     if (!LAP) wave_sync();
@@ -267,7 +175,7 @@ extern "C" int lavish_cost_coeffs_txb_batch(const LavishCoeffCosts* costs, const
   a.w = w;
   a.h = h;
   a.bhl = ilog2(h);
-  a.cls = tx_type < 10 ? 0 : ((tx_type & 1) ? 1 : 2);
+  a.cls = cc::tx_class(tx_type);
   a.wlt = txw < txh;
   a.wgt = txw > txh;
   a.tx_type_cost = plane == 0 ? tx_type_cost : 0;  // get_tx_type_cost: 0 for plane > 0

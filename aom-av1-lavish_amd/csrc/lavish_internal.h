@@ -45,11 +45,18 @@ int txq_plane_64(const int16_t* residual, int stride, int width, int height, int
 // inverse transform batch (inv.hip)
 int inv_txfm_add_batch(const int32_t* dq, int tx_size, const LavishInvJob* jobs, int njobs,
                        void* dst, int stride, int bd, int highbd, hipStream_t s);
+// the coefficient-rate decision (lavish_rdo_plane_rate): device CoeffCosts,
+// per-block TXB_CTX (nullable) and get_tx_type_cost per tx type (host, nullable)
+struct RateCfg {
+  const LavishCoeffCosts* costs;
+  const LavishTxbCtx* txb_ctx;
+  const int32_t* tx_type_costs;
+};
 int rdo_plane(const uint16_t* src, const uint16_t* pred, int stride, int width, int height,
               int tx_size, uint32_t type_mask, int bd, const LavishQuantParams* qp, int rdmult,
               LavishRdoBlock* out, int32_t* qcoeff, int32_t* dqcoeff, hipStream_t s,
               int px = 0, const uint16_t* block_mask = nullptr,
-              const uint8_t* block_map = nullptr);
+              const uint8_t* block_map = nullptr, const RateCfg* rate = nullptr);
 
 // inter prediction batch (inter.hip); custom = an RTCD shim's own kernels
 int inter_pred_batch(const void* ref, int ref_stride, int ref_width, int ref_height, int ss_x,

@@ -30,6 +30,7 @@
 // size including the 64-point ones (tools/range_analysis.py).
 #include <type_traits>
 
+#include "coeffcost_dev.h"
 #include "lavish_internal.h"
 #include "quant_dev.h"
 
@@ -58,6 +59,15 @@ struct RdoArgs {
   const uint16_t* block_mask;
   const uint8_t* block_map;
   const int16_t* iscan_dct;       // DCT_DCT inverse scan (rate_estimator)
+  // MODE 3: the coefficient rate (av1_cost_coeffs_txb) replaces
+  // rate_estimator: the size's luma LV_MAP_COEFF_COST / LV_MAP_EOB_COST,
+  // per-block TXB_CTX (nullable: {0, 0}), get_tx_type_cost per tx type, and
+  // the av1_nz_map_ctx_offset shape of the unadjusted size
+  const int32_t* cc_cost;
+  const int32_t* cc_eob;
+  const LavishTxbCtx* txb_ctx;
+  int tx_type_cost[16];
+  int nz_wlt, nz_wgt;
   int32_t* qcoeff;
   int32_t* dqcoeff;
   uint16_t* eob;
@@ -105,6 +115,8 @@ __device__ __forceinline__ void rdo_types(const RdoArgs& a, const int32_t (&res)
   constexpr int NC = T::NC, KW = T::KW, KH = T::KH, T1S = T::T1S;
   constexpr int LS = C::log_scale;
   constexpr bool DEC = MODE >= 1;  // decision modes (1: TX-domain, 2: pixel-domain distortion)
+  constexpr bool RATE = MODE == 3;  // TX-domain distortion, coefficient rate
+  constexpr int LST = KH + 4, LVB = (KW + 4) * LST;  // padded |level| map per block
   // per (row-pass slot k) running best of the block that slot belongs to
   int64_t best_rd[T::RPT], best_dist[T::RPT], best_sse[T::RPT];
   int best_type[T::RPT], best_eob[T::RPT], best_rate[T::RPT], best_satd[T::RPT];
@@ -146,6 +158,16 @@ __device__ __forceinline__ void rdo_types(const RdoArgs& a, const int32_t (&res)
       }
       s_ok[lane] = (uint16_t)ok;
     }
+    wave_sync();
+  }
+  // MODE 3: the cost tables and the blocks' |level| maps (pads stay zero:
+  // only in-block bytes are rewritten per type)
+  __shared__ int32_t s_cc[RATE ? cc::kTabCells : 1];
+  __shared__ __attribute__((aligned(4))) uint8_t s_lv[RATE ? T::P * LVB : 4];
+  if constexpr (RATE) {
+    for (int i = lane; i < cc::kCostCells; i += 64) s_cc[i] = a.cc_cost[i];
+    if (lane < cc::kEobCells) s_cc[cc::kCostCells + lane] = a.cc_eob[lane];
+    for (int i = lane; i < T::P * LVB / 4; i += 64) reinterpret_cast<uint32_t*>(s_lv)[i] = 0u;
     wave_sync();
   }
 
@@ -237,22 +259,48 @@ __device__ __forceinline__ void rdo_types(const RdoArgs& a, const int32_t (&res)
         if (r == 0 && live && bb < nvalid && a.eob != nullptr)
           a.eob[(size_t)ti * a.nblocks + blk0 + bb] = (uint16_t)last;
       } else {
-        // rate_estimator: positions of the DCT_DCT scan below eob
         int rate = 0;
+        if constexpr (RATE) {
+          // av1_cost_coeffs_txb (txb_rdopt.c:599-624) on this type's
+          // quantized block: its |level| map, then each row lane's terms
+          uint8_t* lvb = s_lv + bb * LVB;
+          if (live) {
 #pragma unroll
-        for (int c = 0; c < KW; ++c) {
-          const int rc = c * KH + r;
-          const uint32_t al = (uint32_t)abs(q[c]);
-          if (a.iscan_dct[rc] < last) rate += get_msb(al + 1) + 1 + (al > 0);
+            for (int c = 0; c < KW; ++c) lvb[c * LST + r] = (uint8_t)min(abs(q[c]), 127);
+          }
+          wave_sync();
+          const int cls = cc::tx_class(t);
+          const bool has_ctx = a.txb_ctx != nullptr && live && bb < nvalid;
+          const LavishTxbCtx tc = has_ctx ? a.txb_ctx[blk0 + bb] : LavishTxbCtx{0, 0};
+#pragma unroll
+          for (int c = 0; c < KW; ++c) {
+            const int rc = c * KH + r;
+            const int i = iscan[rc];
+            if (i < last)
+              rate += cc::coeff_term(s_cc, cls, a.nz_wlt, a.nz_wgt, lvb, LST, NC, rc, c, r, i,
+                                     last, q[c], tc.dc_sign_ctx);
+          }
+#pragma unroll
+          for (int m = 1; m < KH; m <<= 1) rate += __shfl_xor(rate, m);
+          rate = cc::txb_rate(s_cc, cls, tc.txb_skip_ctx, last, a.tx_type_cost[t], rate);
+        } else {
+          // rate_estimator: positions of the DCT_DCT scan below eob
+#pragma unroll
+          for (int c = 0; c < KW; ++c) {
+            const int rc = c * KH + r;
+            const uint32_t al = (uint32_t)abs(q[c]);
+            if (a.iscan_dct[rc] < last) rate += get_msb(al + 1) + 1 + (al > 0);
+          }
+#pragma unroll
+          for (int m = 1; m < KH; m <<= 1) rate += __shfl_xor(rate, m);
+          rate = (rate + 1) << 9;  // AV1_PROB_COST_SHIFT
         }
 #pragma unroll
         for (int m = 1; m < KH; m <<= 1) {
-          rate += __shfl_xor(rate, m);
           satd += __shfl_xor(satd, m);
           err += __shfl_xor(err, m);
           sse += __shfl_xor(sse, m);
         }
-        rate = (rate + 1) << 9;  // AV1_PROB_COST_SHIFT
         // av1_highbd_block_error rounding, then the TX-domain shift
         const int sh = 2 * (a.bd - 8);
         if (sh > 0) {
@@ -439,7 +487,9 @@ __device__ __forceinline__ void rdo_types(const RdoArgs& a, const int32_t (&res)
 // one wave = one tile of P blocks; 64-thread workgroups (LDS per tile is up
 // to ~20 KB for the 64-point sizes).  MODE 0: per-type coefficients (the
 // txq_plane contract), 1: decision with TX-domain distortion, 2: decision
-// with pixel-domain distortion (sizes <= 32x32; BDI = bit-depth index).
+// with pixel-domain distortion (sizes <= 32x32; BDI = bit-depth index), 3:
+// mode 1 ranked by the coefficient rate (av1_cost_coeffs_txb) instead of
+// rate_estimator.
 template <int W, int H, int MODE, int BDI>
 __global__ __launch_bounds__(64) void rdo_kernel(RdoArgs a) {
   using T = RTile<W, H>;
@@ -551,7 +601,7 @@ void launch_rdo(const RdoArgs& a, hipStream_t s) {
 
 template <int MODE>
 int launch_size(int tx_size, const RdoArgs& a, hipStream_t s) {
-  if constexpr (MODE <= 1) {
+  if constexpr (MODE <= 1 || MODE == 3) {
     switch (tx_size) {
       case 4: launch_rdo<64, 64, MODE>(a, s); return 0;
       case 11: launch_rdo<32, 64, MODE>(a, s); return 0;
@@ -651,7 +701,7 @@ int rdo_plane_px64(RdoArgs& a, int tx_size, int width, int height, hipStream_t s
 int rdo_plane(const uint16_t* src, const uint16_t* pred, int stride, int width, int height,
               int tx_size, uint32_t type_mask, int bd, const LavishQuantParams* qp, int rdmult,
               LavishRdoBlock* out, int32_t* qcoeff, int32_t* dqcoeff, hipStream_t s, int px,
-              const uint16_t* block_mask, const uint8_t* block_map) {
+              const uint16_t* block_mask, const uint8_t* block_map, const RateCfg* rate) {
   if (tx_size < 0 || tx_size >= 19) return -1;
   if (qp == nullptr || out == nullptr || qcoeff == nullptr || dqcoeff == nullptr) return -3;
   if (bd != 8 && bd != 10 && bd != 12) return -3;
@@ -674,6 +724,23 @@ int rdo_plane(const uint16_t* src, const uint16_t* pred, int stride, int width, 
   a.dqcoeff = dqcoeff;
   a.block_mask = block_mask;
   a.block_map = block_map;
+  if (rate != nullptr) {
+    if (px) return -7;  // the coefficient rate is built for TX-domain distortion
+    if (rate->costs == nullptr) return -3;
+    const int txw = W, txh = H;
+    const int w = txw > 32 ? 32 : txw, h = txh > 32 ? 32 : txh;
+    const int mn = txw < txh ? txw : txh, mx = txw < txh ? txh : txw;
+    const int lg_mn = 31 - __builtin_clz(mn), lg_mx = 31 - __builtin_clz(mx);
+    const int txs_ctx = (lg_mn - 2 + lg_mx - 2 + 1) >> 1;        // get_txsize_entropy_ctx
+    const int eob_multi = 31 - __builtin_clz(w * h) - 4;         // txsize_log2_minus4
+    a.cc_cost = &rate->costs->coeff_costs[txs_ctx][0].txb_skip_cost[0][0];
+    a.cc_eob = &rate->costs->eob_costs[eob_multi][0].eob_cost[0][0];
+    a.txb_ctx = rate->txb_ctx;
+    for (int t = 0; t < 16; ++t) a.tx_type_cost[t] = rate->tx_type_costs ? rate->tx_type_costs[t] : 0;
+    a.nz_wlt = txw < txh;
+    a.nz_wgt = txw > txh;
+    return launch_size<3>(tx_size, a, s);
+  }
   if (px) {
     if (W > 32 || H > 32) {
       if (block_mask || block_map) return -6;  // single-type path
@@ -1010,4 +1077,17 @@ extern "C" int lavish_rdo_plane_masked(const uint16_t* src, const uint16_t* pred
   return lavish::rdo_plane(src, pred, stride, width, height, tx_size, type_mask, bit_depth, qp,
                            rdmult, out, qcoeff, dqcoeff, (hipStream_t)stream, pixel_domain ? 1 : 0,
                            block_mask, block_map);
+}
+
+extern "C" int lavish_rdo_plane_rate(const uint16_t* src, const uint16_t* pred, int stride,
+                                     int width, int height, int tx_size, uint32_t type_mask,
+                                     int bit_depth, const LavishQuantParams* qp, int rdmult,
+                                     const LavishCoeffCosts* costs, const LavishTxbCtx* txb_ctx,
+                                     const int32_t* tx_type_costs, const uint16_t* block_mask,
+                                     const uint8_t* block_map, LavishRdoBlock* out,
+                                     int32_t* qcoeff, int32_t* dqcoeff, void* stream) {
+  const lavish::RateCfg rc{costs, txb_ctx, tx_type_costs};
+  return lavish::rdo_plane(src, pred, stride, width, height, tx_size, type_mask, bit_depth, qp,
+                           rdmult, out, qcoeff, dqcoeff, (hipStream_t)stream, 0, block_mask,
+                           block_map, &rc);
 }

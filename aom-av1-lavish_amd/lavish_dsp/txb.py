@@ -67,3 +67,49 @@ def cost_coeffs_txb_batch(costs, qcoeff, eob, tx_size, tx_type, plane=0, txb_ctx
     if rc != 0:
         raise ValueError("lavish_cost_coeffs_txb_batch rejected its arguments (rc=%d)" % rc)
     return out
+
+
+_lib.lavish_rdo_plane_rate.argtypes = [_vp, _vp, _i32, _i32, _i32, _i32, ctypes.c_uint32, _i32,
+                                       _vp, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]
+_lib.lavish_rdo_plane_rate.restype = _i32
+
+
+def rdo_plane_rate(src, pred, tx_size, type_mask, qp, rdmult, costs, txb_ctx=None,
+                   tx_type_costs=None, block_mask=None, block_map=None, bit_depth=10, out=None,
+                   stream=None):
+    """lavish_rdo_plane_rate: C4 (TX-domain distortion) ranked by the
+    coefficient rate.  costs: CoeffCosts; txb_ctx: None or device int32
+    [nblocks, 2]; tx_type_costs: None or 16 ints (get_tx_type_cost per type);
+    masks as rdo_plane_masked."""
+    import torch
+    from . import TX_H, TX_W, rdo_out
+    assert src.dtype == torch.int16 and pred.dtype == torch.int16
+    assert src.is_cuda and pred.is_cuda and src.shape == pred.shape
+    assert src.stride(1) == 1 and pred.stride(0) == src.stride(0)
+    H, W = src.shape
+    nb = (W // TX_W[tx_size]) * (H // TX_H[tx_size])
+    if txb_ctx is not None:
+        assert txb_ctx.is_cuda and txb_ctx.dtype == torch.int32 and txb_ctx.is_contiguous()
+        assert tuple(txb_ctx.shape) == (nb, 2)
+    if block_mask is not None:
+        assert block_mask.is_cuda and block_mask.dtype in (torch.int16, torch.uint16)
+        assert block_mask.is_contiguous() and tuple(block_mask.shape) == (nb,)
+    if block_map is not None:
+        assert block_map.is_cuda and block_map.dtype == torch.uint8
+        assert block_map.is_contiguous() and tuple(block_map.shape) == (nb, 16)
+    ttc = None
+    if tx_type_costs is not None:
+        ttc = np.ascontiguousarray(tx_type_costs, np.int32)
+        assert ttc.shape == (16,)
+    if out is None:
+        out = rdo_out(src, tx_size)
+    p = lambda t: None if t is None else _vp(t.data_ptr())
+    rc = _lib.lavish_rdo_plane_rate(
+        _vp(src.data_ptr()), _vp(pred.data_ptr()), src.stride(0), W, H, tx_size, type_mask,
+        bit_depth, ctypes.byref(qp), rdmult, _vp(costs.t.data_ptr()), p(txb_ctx),
+        None if ttc is None else ttc.ctypes.data_as(_vp), p(block_mask), p(block_map),
+        _vp(out["records"].data_ptr()), _vp(out["qcoeff"].data_ptr()),
+        _vp(out["dqcoeff"].data_ptr()), _stream_ptr(stream))
+    if rc != 0:
+        raise ValueError("lavish_rdo_plane_rate rejected its arguments (rc=%d)" % rc)
+    return out

@@ -381,6 +381,20 @@ int lavish_rdo_plane_masked(const uint16_t *src, const uint16_t *pred, int strid
                             const uint16_t *block_mask, const uint8_t *block_map,
                             int pixel_domain, LavishRdoBlock *out, int32_t *qcoeff,
                             int32_t *dqcoeff, void *stream);
+/* The TX-domain decision ranked by the coefficient rate: per type, rate =
+ * av1_cost_coeffs_txb (txb_rdopt.c:599-624, the cost_coeffs of
+ * search_tx_type, tx_search.c:1903-1921,2172-2176) on the FP-quantized block
+ * instead of rate_estimator, with the luma tables of the device CoeffCosts
+ * `costs`, per-block TXB_CTX txb_ctx (device, nullable: {0, 0}) and
+ * tx_type_costs[16] = get_tx_type_cost per tx type for this tx_size (host,
+ * nullable: 0).  Records' rate is that rate.  Masks as above. */
+int lavish_rdo_plane_rate(const uint16_t *src, const uint16_t *pred, int stride,
+                          int width, int height, int tx_size, uint32_t type_mask,
+                          int bit_depth, const LavishQuantParams *qp, int rdmult,
+                          const LavishCoeffCosts *costs, const LavishTxbCtx *txb_ctx,
+                          const int32_t *tx_type_costs, const uint16_t *block_mask,
+                          const uint8_t *block_map, LavishRdoBlock *out,
+                          int32_t *qcoeff, int32_t *dqcoeff, void *stream);
 
 /* Frame level: lavish_rdo_plane for every size set in size_mask (bit =
  * TX_SIZE) with type_masks[tx_size] and per-size outputs (arrays of 19

@@ -384,6 +384,15 @@ void orc_cost_coeffs_txb_batch(const OrcCoeffCosts *cc, const int32_t *qcoeff, i
                                const uint16_t *eob, int nblocks, int plane, int tx_size,
                                int tx_type, const int32_t *txb_ctx, int tx_type_cost,
                                int laplacian, int32_t *rate);
+/* C4 ranked by the coefficient rate (oracle_rdo.c): orc_rdo_plane_masked's
+ * TX-domain decision with rate = orc_cost_coeffs_txb; txb_ctx [nblocks][2]
+ * and tx_type_costs[16] nullable */
+long orc_rdo_plane_rate(const uint16_t *src, const uint16_t *pred, int stride, int width,
+                        int height, int tx_size, unsigned type_mask, int bd, const OrcQuant *q,
+                        int rdmult, const OrcCoeffCosts *cc, const int32_t *txb_ctx,
+                        const int32_t *tx_type_costs, const uint16_t *block_mask,
+                        const uint8_t *block_map, OrcRdoBlock *out, int32_t *qcoeff,
+                        int32_t *dqcoeff, int threads);
 
 #ifdef __cplusplus
 }

@@ -57,6 +57,11 @@ typedef struct {
   const OrcQuant *q;
   OrcRdoBlock *out;
   int32_t *qcoeff, *dqcoeff;
+  /* optional: the coefficient rate (av1_cost_coeffs_txb) instead of
+   * rate_estimator, with per-block TXB_CTX pairs and per-type tx-type costs */
+  const OrcCoeffCosts *cc;
+  const int32_t *txb_ctx;
+  const int32_t *tx_type_costs;
 } RdoJob;
 
 static void *rdo_rows(void *arg) {
@@ -142,7 +147,14 @@ static void *rdo_rows(void *arg) {
           }
           sse = block_sse;
         }
-        const int rate = rate_estimator(qc, eob, j->tx_size);
+        /* search_tx_type's cost_coeffs (tx_search.c:2172-2176) when tables are
+         * given, else the TPL rate_estimator proxy */
+        const int rate =
+            j->cc ? orc_cost_coeffs_txb(j->cc, qc, eob, 0, j->tx_size, t,
+                                        j->txb_ctx ? j->txb_ctx[2 * blk] : 0,
+                                        j->txb_ctx ? j->txb_ctx[2 * blk + 1] : 0,
+                                        j->tx_type_costs ? j->tx_type_costs[t] : 0, 0)
+                  : rate_estimator(qc, eob, j->tx_size);
         const int64_t rd = ((((int64_t)rate) * j->rdmult + 256) >> 9) + dist * 128;
         if (rd < best.rdcost) {
           best.best_type = t;
@@ -174,7 +186,8 @@ static long rdo_plane(const uint16_t *src, const uint16_t *pred, int stride, int
                       int height, int tx_size, unsigned type_mask, int bd, const OrcQuant *q,
                       int rdmult, OrcRdoBlock *out, int32_t *qcoeff, int32_t *dqcoeff,
                       int threads, int px, const uint16_t *block_mask,
-                      const uint8_t *block_map) {
+                      const uint8_t *block_map, const OrcCoeffCosts *cc,
+                      const int32_t *txb_ctx, const int32_t *tx_type_costs) {
   const int W = orc_tx_w(tx_size), H = orc_tx_h(tx_size);
   const int bh = height / H;
   RdoJob base;
@@ -193,6 +206,9 @@ static long rdo_plane(const uint16_t *src, const uint16_t *pred, int stride, int
   base.px = px;
   base.block_mask = block_mask;
   base.block_map = block_map;
+  base.cc = cc;
+  base.txb_ctx = txb_ctx;
+  base.tx_type_costs = tx_type_costs;
   for (int t = 0; t < 16; ++t)
     if ((type_mask >> t) & 1) base.types[base.ntypes++] = t;
   if (threads < 1) threads = 1;
@@ -217,7 +233,7 @@ long orc_rdo_plane(const uint16_t *src, const uint16_t *pred, int stride, int wi
                    int rdmult, OrcRdoBlock *out, int32_t *qcoeff, int32_t *dqcoeff,
                    int threads) {
   return rdo_plane(src, pred, stride, width, height, tx_size, type_mask, bd, q, rdmult, out,
-                   qcoeff, dqcoeff, threads, 0, NULL, NULL);
+                   qcoeff, dqcoeff, threads, 0, NULL, NULL, NULL, NULL, NULL);
 }
 
 long orc_rdo_plane_px(const uint16_t *src, const uint16_t *pred, int stride, int width,
@@ -225,7 +241,7 @@ long orc_rdo_plane_px(const uint16_t *src, const uint16_t *pred, int stride, int
                       int rdmult, OrcRdoBlock *out, int32_t *qcoeff, int32_t *dqcoeff,
                       int threads) {
   return rdo_plane(src, pred, stride, width, height, tx_size, type_mask, bd, q, rdmult, out,
-                   qcoeff, dqcoeff, threads, 1, NULL, NULL);
+                   qcoeff, dqcoeff, threads, 1, NULL, NULL, NULL, NULL, NULL);
 }
 
 long orc_rdo_plane_masked(const uint16_t *src, const uint16_t *pred, int stride, int width,
@@ -234,7 +250,18 @@ long orc_rdo_plane_masked(const uint16_t *src, const uint16_t *pred, int stride,
                           int px, OrcRdoBlock *out, int32_t *qcoeff, int32_t *dqcoeff,
                           int threads) {
   return rdo_plane(src, pred, stride, width, height, tx_size, type_mask, bd, q, rdmult, out,
-                   qcoeff, dqcoeff, threads, px, block_mask, block_map);
+                   qcoeff, dqcoeff, threads, px, block_mask, block_map, NULL, NULL, NULL);
+}
+
+long orc_rdo_plane_rate(const uint16_t *src, const uint16_t *pred, int stride, int width,
+                        int height, int tx_size, unsigned type_mask, int bd, const OrcQuant *q,
+                        int rdmult, const OrcCoeffCosts *cc, const int32_t *txb_ctx,
+                        const int32_t *tx_type_costs, const uint16_t *block_mask,
+                        const uint8_t *block_map, OrcRdoBlock *out, int32_t *qcoeff,
+                        int32_t *dqcoeff, int threads) {
+  return rdo_plane(src, pred, stride, width, height, tx_size, type_mask, bd, q, rdmult, out,
+                   qcoeff, dqcoeff, threads, 0, block_mask, block_map, cc, txb_ctx,
+                   tx_type_costs);
 }
 
 /* Per 64x64 SB: the size (of `sizes`, largest area first) whose full blocks

@@ -833,3 +833,29 @@ def cost_coeffs_txb_batch(blob, qcoeff, eob, plane, tx_size, tx_type, txb_ctx=No
     fn(P(blob), P(q), q.shape[1], P(e), q.shape[0], plane, tx_size, tx_type,
        P(ctx) if ctx is not None else None, tx_type_cost, int(laplacian), P(out))
     return out
+
+
+def rdo_plane_rate(src, pred, tx_size, type_mask, bd, q, rdmult, blob, txb_ctx=None,
+                   tx_type_costs=None, block_mask=None, block_map=None, threads=1):
+    """orc_rdo_plane_rate: the TX-domain C4 decision with rate =
+    orc_cost_coeffs_txb (search_tx_type's cost_coeffs)."""
+    fn = lib().orc_rdo_plane_rate
+    fn.restype = ctypes.c_long
+    fn.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                   ctypes.c_int, ctypes.c_uint, ctypes.c_int, ctypes.POINTER(OrcQuant),
+                   ctypes.c_int] + [ctypes.c_void_p] * 8 + [ctypes.c_int]
+    src = np.ascontiguousarray(src, dtype=np.uint16)
+    pred = np.ascontiguousarray(pred, dtype=np.uint16)
+    H, W = src.shape
+    nb = (W // TX_W[tx_size]) * (H // TX_H[tx_size])
+    n = max_eob(tx_size)
+    out = np.zeros(nb, RDO_DTYPE)
+    qc = np.zeros((nb, n), np.int32)
+    dq = np.zeros((nb, n), np.int32)
+    arr = lambda a, t: None if a is None else np.ascontiguousarray(a, t)
+    ctx, ttc = arr(txb_ctx, np.int32), arr(tx_type_costs, np.int32)
+    bm, mp = arr(block_mask, np.uint16), arr(block_map, np.uint8)
+    pp = lambda a: None if a is None else P(a)
+    fn(P(src), P(pred), W, W, H, tx_size, type_mask, bd, ctypes.byref(q), rdmult, P(blob),
+       pp(ctx), pp(ttc), pp(bm), pp(mp), P(out), P(qc), P(dq), threads)
+    return out, qc, dq

@@ -311,3 +311,25 @@ def test_cost_coeffs_txb_matches_reference():
         classes.add(0 if g("tx_type") < 10 else 1 + (g("tx_type") & 1))
     assert classes == {0, 1, 2}
     assert (F["rows"][:, J["tx_size"]] == np.arange(19)[:, None]).any(axis=1).all()
+
+
+def test_rdo_rate_oracle_records_are_cost_coeffs():
+    """orc_rdo_plane_rate's record rate is orc_cost_coeffs_txb (pinned above)
+    of the winning type's qcoeff / eob, and its rd cost is RDCOST of it."""
+    import _c4ref
+    bd = 10
+    src, pred = _c4ref.planes(bd, 3, 128, 64)
+    rng = np.random.default_rng(0)
+    blob = rng.integers(30, 4000, 10 * O.CC_COEFF_COST + 14 * O.CC_EOB_COST).astype(np.int32)
+    ttc = rng.integers(0, 3000, 16).astype(np.int32)
+    q = O.build_quant(bd, 128)
+    for s, tmask in ((0, 0xFFFF), (2, 0xFFFF), (7, 0xFFFF), (3, 0x201)):
+        nb = (128 // O.TX_W[s]) * (64 // O.TX_H[s])
+        ctx = np.stack([rng.integers(0, 13, nb), rng.integers(0, 3, nb)], 1).astype(np.int32)
+        rec, qc, _ = O.rdo_plane_rate(src, pred, s, tmask, bd, q, 1500, blob, ctx, ttc, threads=4)
+        for b in range(nb):
+            t = int(rec["best_type"][b])
+            r = O.cost_coeffs_txb(blob, qc[b], int(rec["eob"][b]), 0, s, t, int(ctx[b, 0]),
+                                  int(ctx[b, 1]), int(ttc[t]))
+            assert r == rec["rate"][b]
+            assert rec["rdcost"][b] == ((r * 1500 + 256) >> 9) + int(rec["dist"][b]) * 128
