@@ -29,21 +29,12 @@ __host__ __device__ __forceinline__ int tx_class(int tx_type) {
 
 __device__ __forceinline__ int min3(int v) { return v < 3 ? v : 3; }
 
-// get_nz_mag + get_nz_map_ctx_from_stats (txb_common.h:150-224); wlt / wgt =
-// tx_size_wide < / > tx_size_high of the (unadjusted) size, the rule that
-// generates av1_nz_map_ctx_offset (txb_common.h:199-209)
-__device__ __forceinline__ int lower_ctx(int cls, int wlt, int wgt, const uint8_t* lv, int stride,
-                                         int pos, int col, int row) {
-  const uint8_t* l = lv + col * stride + row;
-  int mag = min3(l[stride]) + min3(l[1]);
-  if (cls == 0) {
-    mag += min3(l[stride + 1]) + min3(l[2 * stride]) + min3(l[2]);
-  } else if (cls == 2) {
-    mag += min3(l[2]) + min3(l[3]) + min3(l[4]);
-  } else {
-    mag += min3(l[2 * stride]) + min3(l[3 * stride]) + min3(l[4 * stride]);
-  }
-  const int ctx = min((mag + 1) >> 1, 4);
+// get_nz_map_ctx_from_stats (txb_common.h:189-224) on the get_nz_mag sum;
+// wlt / wgt = tx_size_wide < / > tx_size_high of the (unadjusted) size, the
+// rule that generates av1_nz_map_ctx_offset (txb_common.h:199-209)
+__device__ __forceinline__ int nz_ctx(int cls, int wlt, int wgt, int stats, int pos, int col,
+                                      int row) {
+  const int ctx = min((stats + 1) >> 1, 4);
   if (cls == 0) {
     if (pos == 0) return 0;
     int off;
@@ -58,24 +49,34 @@ __device__ __forceinline__ int lower_ctx(int cls, int wlt, int wgt, const uint8_
   return ctx + 26 + (idx == 0 ? 0 : (idx == 1 ? 5 : 10));
 }
 
-// get_br_ctx (txb_common.h:103-135)
+// get_br_ctx's context from its neighbour sum (txb_common.h:103-135)
+__device__ __forceinline__ int br_ctx_mag(int cls, int mag, int pos, int col, int row) {
+  mag = min((mag + 1) >> 1, 6);
+  const bool near = cls == 0 ? (row < 2 && col < 2) : (cls == 1 ? col == 0 : row == 0);
+  return pos == 0 ? mag : mag + (near ? 7 : 14);
+}
+
+// get_nz_mag (txb_common.h:150-173) + get_nz_map_ctx_from_stats over the map
+__device__ __forceinline__ int lower_ctx(int cls, int wlt, int wgt, const uint8_t* lv, int stride,
+                                         int pos, int col, int row) {
+  const uint8_t* l = lv + col * stride + row;
+  int mag = min3(l[stride]) + min3(l[1]);
+  if (cls == 0) {
+    mag += min3(l[stride + 1]) + min3(l[2 * stride]) + min3(l[2]);
+  } else if (cls == 2) {
+    mag += min3(l[2]) + min3(l[3]) + min3(l[4]);
+  } else {
+    mag += min3(l[2 * stride]) + min3(l[3 * stride]) + min3(l[4 * stride]);
+  }
+  return nz_ctx(cls, wlt, wgt, mag, pos, col, row);
+}
+
+// get_br_ctx (txb_common.h:103-135) over the map
 __device__ __forceinline__ int br_ctx(int cls, const uint8_t* lv, int stride, int pos, int col,
                                       int row) {
   const uint8_t* l = lv + col * stride + row;
-  int mag = l[1] + l[stride];
-  bool near;
-  if (cls == 0) {
-    mag += l[stride + 1];
-    near = row < 2 && col < 2;
-  } else if (cls == 1) {
-    mag += l[2 * stride];
-    near = col == 0;
-  } else {
-    mag += l[2];
-    near = row == 0;
-  }
-  mag = min((mag + 1) >> 1, 6);
-  return pos == 0 ? mag : mag + (near ? 7 : 14);
+  const int third = cls == 0 ? l[stride + 1] : (cls == 1 ? l[2 * stride] : l[2]);
+  return br_ctx_mag(cls, l[1] + l[stride] + third, pos, col, row);
 }
 
 // get_br_ctx_eob (txb_common.h:90-101)
@@ -109,6 +110,27 @@ __device__ __forceinline__ int coeff_term(const int32_t* tab, int cls, int wlt, 
   } else {
     cost = tab[kBase + lower_ctx(cls, wlt, wgt, lv, stride, pos, col, row) * 8 + min3(level)];
     if (level > 2) cost += br_cost(tab, br_ctx(cls, lv, stride, pos, col, row), level);
+  }
+  if (level) cost += i ? 512 : tab[kDcSign + dc_sign_ctx * 2 + (v < 0)];
+  return cost;
+}
+
+// coeff_term with the neighbour sums already formed (no level map): nzmag =
+// get_nz_mag's clipped sum, brmag = get_br_ctx's raw sum.  Levels clipped to
+// 15 (MAX_BASE_BR_RANGE) give the same contexts: get_nz_mag clips each to 3
+// and get_br_ctx saturates once its sum reaches 11.
+__device__ __forceinline__ int coeff_term_mag(const int32_t* tab, int cls, int wlt, int wgt,
+                                              int n, int pos, int col, int row, int i, int eob,
+                                              int v, int dc_sign_ctx, int nzmag, int brmag) {
+  const int level = abs(v);
+  int cost;
+  if (i == eob - 1) {
+    const int ctx = i == 0 ? 0 : (i <= (n >> 3) ? 1 : (i <= (n >> 2) ? 2 : 3));
+    cost = tab[kBaseEob + ctx * 3 + min3(level) - 1];
+    if (level > 2) cost += br_cost(tab, br_ctx_eob(cls, pos, col, row), level);
+  } else {
+    cost = tab[kBase + nz_ctx(cls, wlt, wgt, nzmag, pos, col, row) * 8 + min3(level)];
+    if (level > 2) cost += br_cost(tab, br_ctx_mag(cls, brmag, pos, col, row), level);
   }
   if (level) cost += i ? 512 : tab[kDcSign + dc_sign_ctx * 2 + (v < 0)];
   return cost;

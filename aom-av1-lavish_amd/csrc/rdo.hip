@@ -116,7 +116,6 @@ __device__ __forceinline__ void rdo_types(const RdoArgs& a, const int32_t (&res)
   constexpr int LS = C::log_scale;
   constexpr bool DEC = MODE >= 1;  // decision modes (1: TX-domain, 2: pixel-domain distortion)
   constexpr bool RATE = MODE == 3;  // TX-domain distortion, coefficient rate
-  constexpr int LST = KH + 4, LVB = (KW + 4) * LST;  // padded |level| map per block
   // per (row-pass slot k) running best of the block that slot belongs to
   int64_t best_rd[T::RPT], best_dist[T::RPT], best_sse[T::RPT];
   int best_type[T::RPT], best_eob[T::RPT], best_rate[T::RPT], best_satd[T::RPT];
@@ -160,14 +159,11 @@ __device__ __forceinline__ void rdo_types(const RdoArgs& a, const int32_t (&res)
     }
     wave_sync();
   }
-  // MODE 3: the cost tables and the blocks' |level| maps (pads stay zero:
-  // only in-block bytes are rewritten per type)
+  // MODE 3: the cost tables
   __shared__ int32_t s_cc[RATE ? cc::kTabCells : 1];
-  __shared__ __attribute__((aligned(4))) uint8_t s_lv[RATE ? T::P * LVB : 4];
   if constexpr (RATE) {
     for (int i = lane; i < cc::kCostCells; i += 64) s_cc[i] = a.cc_cost[i];
     if (lane < cc::kEobCells) s_cc[cc::kCostCells + lane] = a.cc_eob[lane];
-    for (int i = lane; i < T::P * LVB / 4; i += 64) reinterpret_cast<uint32_t*>(s_lv)[i] = 0u;
     wave_sync();
   }
 
@@ -262,23 +258,53 @@ __device__ __forceinline__ void rdo_types(const RdoArgs& a, const int32_t (&res)
         int rate = 0;
         if constexpr (RATE) {
           // av1_cost_coeffs_txb (txb_rdopt.c:599-624) on this type's
-          // quantized block: its |level| map, then each row lane's terms
-          uint8_t* lvb = s_lv + bb * LVB;
-          if (live) {
-#pragma unroll
-            for (int c = 0; c < KW; ++c) lvb[c * LST + r] = (uint8_t)min(abs(q[c]), 127);
-          }
-          wave_sync();
+          // quantized block.  Lane = row r of its block, so the |level| map
+          // neighbours of get_nz_mag / get_br_ctx are this lane's own
+          // columns c+1.. and the same columns of rows r+1.. (lanes below):
+          // levels clipped to 15 as nibbles, 8 per word, shifted down the
+          // wave a word at a time; rows past the block read as the zero pad.
+          constexpr int NW = (KW + 7) / 8;
           const int cls = cc::tx_class(t);
+          const int nrow = cls == 2 ? 4 : 2;  // rows below that a context reads
+          uint32_t pk[5][NW];
+#pragma unroll
+          for (int w = 0; w < NW; ++w) pk[0][w] = 0u;
+#pragma unroll
+          for (int c = 0; c < KW; ++c)
+            pk[0][c >> 3] |= (uint32_t)min(abs(q[c]), 15) << (4 * (c & 7));
+#pragma unroll
+          for (int d = 1; d <= 4; ++d) {
+#pragma unroll
+            for (int w = 0; w < NW; ++w) {
+              const uint32_t x = d <= nrow ? (uint32_t)__shfl_down((int)pk[0][w], d) : 0u;
+              pk[d][w] = r + d < KH ? x : 0u;
+            }
+          }
+          auto nib = [&](int d, int c) -> int {
+            return c < KW ? (int)((pk[d][c >> 3] >> (4 * (c & 7))) & 15u) : 0;
+          };
           const bool has_ctx = a.txb_ctx != nullptr && live && bb < nvalid;
           const LavishTxbCtx tc = has_ctx ? a.txb_ctx[blk0 + bb] : LavishTxbCtx{0, 0};
 #pragma unroll
           for (int c = 0; c < KW; ++c) {
             const int rc = c * KH + r;
             const int i = iscan[rc];
-            if (i < last)
-              rate += cc::coeff_term(s_cc, cls, a.nz_wlt, a.nz_wgt, lvb, LST, NC, rc, c, r, i,
-                                     last, q[c], tc.dc_sign_ctx);
+            if (i < last) {
+              const int right = nib(0, c + 1), below = nib(1, c);
+              int nzmag = cc::min3(right) + cc::min3(below), third;
+              if (cls == 0) {
+                third = nib(1, c + 1);
+                nzmag += cc::min3(third) + cc::min3(nib(0, c + 2)) + cc::min3(nib(2, c));
+              } else if (cls == 1) {
+                third = nib(0, c + 2);
+                nzmag += cc::min3(third) + cc::min3(nib(0, c + 3)) + cc::min3(nib(0, c + 4));
+              } else {
+                third = nib(2, c);
+                nzmag += cc::min3(third) + cc::min3(nib(3, c)) + cc::min3(nib(4, c));
+              }
+              rate += cc::coeff_term_mag(s_cc, cls, a.nz_wlt, a.nz_wgt, NC, rc, c, r, i, last,
+                                         q[c], tc.dc_sign_ctx, nzmag, right + below + third);
+            }
           }
 #pragma unroll
           for (int m = 1; m < KH; m <<= 1) rate += __shfl_xor(rate, m);

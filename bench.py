@@ -54,7 +54,7 @@ def parse():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--workload", choices=("rdo", "c2", "c3", "c3sub", "c4", "c4px", "c5", "inter",
-                                           "tpl"),
+                                           "tpl", "rate"),
                     default="rdo")
     ap.add_argument("--rdmult", type=int, default=2000)
     ap.add_argument("--width", type=int, default=1920)
@@ -699,6 +699,150 @@ def main_tpl(args):
         dist.destroy_process_group()
 
 
+def rate_tables(seed=2024):
+    """Seeded CoeffCosts cells in av1_fill_coeff_costs' magnitude and
+    get_tx_type_cost per type (the timing does not depend on the values)."""
+    from lavish_dsp import txb
+    rng = np.random.default_rng(seed)
+    return (rng.integers(30, 4000, txb.COEFF_COSTS_CELLS).astype(np.int32),
+            rng.integers(0, 3000, 16).astype(np.int32))
+
+
+def cpu_baseline_rate(args):
+    """Oracle C4 ranked by the coefficient rate (orc_rdo_plane_rate for every
+    candidate size / type) on a 3840x128 10-bit strip, ~cpu_seconds."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import _c4ref
+    import _oracle as O
+    import lavish_dsp as L
+    threads = host_cores()
+    src, pred = _c4ref.planes(10, 1234, Wp=3840, Hp=128)
+    blob, ttc = rate_tables()
+    q = O.build_quant(10, args.qindex)
+    sb = sb64_count(3840, 128)
+    passes = 0
+    t0 = time.perf_counter()
+    while True:
+        for s, m in L.C4_TYPE_MASKS.items():
+            O.rdo_plane_rate(src, pred, s, m, 10, q, args.rdmult, blob, None, ttc,
+                             threads=threads)
+        passes += 1
+        dt = time.perf_counter() - t0
+        if dt >= args.cpu_seconds:
+            break
+    return {"value": round(passes * sb / dt, 2), "unit": "SB64/s", "cores": threads,
+            "kind": "port",
+            "sample": "%d passes of a 3840x128 10-bit strip (%d SB64) through the rate step "
+                      "(RDO of all candidate sizes / types ranked by av1_cost_coeffs_txb), "
+                      "oracle C restatement (-O3, %d pthreads), %.1f s"
+                      % (passes, sb, threads, dt)}
+
+
+def main_rate(args):
+    """The coefficient rate on a 4K 10-bit frame.
+    Step = C4's decision of every candidate size / type (the c4 type sets)
+    ranked by av1_cost_coeffs_txb (lavish_rdo_plane_rate, rdo_kernel mode
+    3), sizes back to back on the current stream.  Beside it, timed the same
+    way: the same decision with rate_estimator (lavish_rdo_plane_masked,
+    mode 1), and the standalone lavish_cost_coeffs_txb_batch over every
+    block of each size's DCT_DCT quantization (lavish_txq_plane)."""
+    import torch
+    import lavish_dsp as L
+    import lavish_dsp.synth as synth
+    from lavish_dsp import txb
+    torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0")))
+    W = args.width if args.width != 1920 else 3840
+    H = args.height if args.height != 1080 else 2160
+    src_np = synth.frame(W, H, 10, 1234).astype(np.uint16)
+    pred_np = synth.shifted(synth.frame(W, H, 10, 1235), 3, -2).astype(np.uint16)
+    src = torch.from_numpy(src_np.view(np.int16)).cuda()
+    pred = torch.from_numpy(pred_np.view(np.int16)).cuda()
+    qp = L.build_quant_params(10, args.qindex, L.QUANT_FP)
+    blob, ttc = rate_tables()
+    costs = txb.CoeffCosts(blob)
+    sizes = dict(L.C4_TYPE_MASKS)
+    outs = {s: L.rdo_out(src, s) for s in sizes}
+    stream = torch.cuda.current_stream()
+
+    def timed(fn, steps, warmup):
+        for _ in range(warmup):
+            fn()
+        torch.cuda.synchronize()
+        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+              for _ in range(steps)]
+        t0 = time.perf_counter()
+        for k in range(steps):
+            ev[k][0].record(stream)
+            fn()
+            ev[k][1].record(stream)
+        torch.cuda.synchronize()
+        return time.perf_counter() - t0, sum(a.elapsed_time(b) for a, b in ev) / steps
+
+    def step_rate():
+        for s, m in sizes.items():
+            txb.rdo_plane_rate(src, pred, s, m, qp, args.rdmult, costs, None, ttc,
+                               bit_depth=10, out=outs[s])
+
+    def step_est():
+        for s, m in sizes.items():
+            L.rdo_plane_masked(src, pred, s, m, qp, args.rdmult, bit_depth=10, out=outs[s])
+
+    elapsed, step_ms = timed(step_rate, args.steps, args.warmup)
+    _, est_ms = timed(step_est, args.steps, args.warmup)
+    # standalone coefficient rate over each size's DCT_DCT quantization
+    res = (src.to(torch.int32) - pred.to(torch.int32)).to(torch.int16).contiguous()
+    cc = {}
+    for s in sizes:
+        tq = L.txq_plane(res, s, 1, qp, bit_depth=10)
+        qc, eob = tq["qcoeff"][0].contiguous(), tq["eob"][0].contiguous()
+        rate = torch.empty(qc.shape[0], dtype=torch.int32, device="cuda")
+        _, ms = timed(lambda: txb.cost_coeffs_txb_batch(costs, qc, eob, s, 0, out=rate),
+                      args.steps, args.warmup)
+        nb, n = qc.shape
+        nbytes = nb * (4 * n + 2 + 4)  # qcoeff, eob in, rate out
+        cc[L.TX_SIZES[s]] = {"blocks": nb, "ms": round(ms, 4), "algorithmic_bytes": nbytes,
+                             "achieved_GBps": round(nbytes / (ms * 1e-3) / 1e9, 1),
+                             "mean_eob": round(float(eob.view(torch.uint16).float().mean()), 1)}
+    status = L.status()
+    if status[0] != 0:
+        raise RuntimeError("HIP error during bench: %s" % (status,))
+    sb = sb64_count(W, H)
+    nbytes = c4_algorithmic_bytes(L, W, H) - 8 * W * H  # no reconstruction in this step
+    line = {
+        "metric": METRIC,
+        "value": round(sb * args.steps / elapsed, 2),
+        "unit": "SB64/s",
+        "n_gpus": 1,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "int32",
+        "data": "synthetic (seeded 4K 10-bit content, lavish_dsp/synth.py; seeded CoeffCosts)",
+        "config": {
+            "workload": "rate: %dx%d 10-bit frame per step; TX-type RDO (subtract, fwd txfm, "
+                        "highbd quantize_fp, TX-domain block error, av1_cost_coeffs_txb rate, "
+                        "RDCOST) of 64x64 DCT, 32x32 DCT+IDTX, 16x16/8x8/4x4 all types; "
+                        "qindex %d, rdmult %d; %d SB64/frame" % (W, H, args.qindex,
+                                                                args.rdmult, sb),
+            "parallelism": "frame-per-rank x1"},
+        "roofline": {"bound": "hbm", "kernel": "rdo_kernel<W,H,3> x5 sizes "
+                     "(lavish_rdo_plane_rate)",
+                     "achieved": round(nbytes / (step_ms * 1e-3) / 1e9, 1),
+                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "traffic": None,
+                     "avg_launch_ms": round(step_ms, 4),
+                     "algorithmic_bytes_per_launch": nbytes},
+        "rate_estimator_ms": round(est_ms, 4),
+        "cost_coeffs": cc,
+    }
+    line["roofline"]["frac"] = round(line["roofline"]["achieved"] / HBM_PEAK_GBS, 4)
+    if not args.no_cpu:
+        line["cpu_baseline"] = cpu_baseline_rate(args)
+    print(json.dumps(line), flush=True)
+
+
 def main():
     args = parse()
     if args.workload in ("c4", "c4px", "c5"):
@@ -707,6 +851,8 @@ def main():
         return main_inter(args)
     if args.workload == "tpl":
         return main_tpl(args)
+    if args.workload == "rate":
+        return main_rate(args)
     import torch
     import torch.distributed as dist
     import lavish_dsp as L
