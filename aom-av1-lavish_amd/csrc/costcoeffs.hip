@@ -181,8 +181,11 @@ extern "C" int lavish_cost_coeffs_txb_batch(const LavishCoeffCosts* costs, const
   a.tx_type_cost = plane == 0 ? tx_type_cost : 0;  // get_tx_type_cost: 0 for plane > 0
   const int logn = ilog2(w * h);
   const int c = (w * h) / 4, gl = c < 64 ? c : 64, bpwg = 4 * (64 / gl);
+  // 8 workgroups per CU at most: each stages the tables once and then
+  // strides over the batch (small blocks would otherwise re-stage ~4 KB of
+  // tables per few KB of coefficients)
   int grid = (nblocks + bpwg - 1) / bpwg;
-  if (grid > 4096) grid = 4096;
+  if (grid > 2048) grid = 2048;
   hipStream_t s = (hipStream_t)stream;
   const bool lap = mode == LAVISH_COEFF_RATE_LAPLACIAN;
 #define LAVISH_CC(L)                                                                      \
