@@ -113,3 +113,41 @@ def rdo_plane_rate(src, pred, tx_size, type_mask, qp, rdmult, costs, txb_ctx=Non
     if rc != 0:
         raise ValueError("lavish_rdo_plane_rate rejected its arguments (rc=%d)" % rc)
     return out
+
+
+_lib.lavish_optimize_b_batch.argtypes = [_vp, _vp, _vp, _vp, _vp, _i32, _i32, _i32, _i32, _i32,
+                                         _i32, _i32, _i32, _vp, _vp, _i32, _vp, _vp, _vp]
+_lib.lavish_optimize_b_batch.restype = _i32
+
+
+def optimize_b_batch(costs, tcoeff, qcoeff, dqcoeff, eob, tx_size, tx_type, bit_depth, rdmult,
+                     dequant, plane=0, is_inter=1, sharpness=0, txb_ctx=None, tx_type_cost=0,
+                     rate=None, entropy_ctx=None, stream=None):
+    """lavish_optimize_b_batch (av1_optimize_b): qcoeff / dqcoeff / eob are
+    updated in place (device int32 [nblocks, n], int16 / uint16 [nblocks]);
+    dequant = (dc, ac) dequantizer values.  Returns (rate, entropy_ctx)."""
+    import torch
+    n = max_eob(tx_size)
+    for t in (tcoeff, qcoeff, dqcoeff):
+        assert t.dtype == torch.int32 and t.is_contiguous() and t.shape[-1] == n and t.is_cuda
+    nb = qcoeff.numel() // n
+    assert tcoeff.numel() == qcoeff.numel() == dqcoeff.numel()
+    assert eob.dtype in (torch.int16, torch.uint16) and eob.numel() >= nb and eob.is_cuda
+    if txb_ctx is not None:
+        assert txb_ctx.dtype == torch.int32 and txb_ctx.is_contiguous()
+        assert txb_ctx.numel() >= 2 * nb and txb_ctx.is_cuda
+    if rate is None:
+        rate = torch.empty(nb, dtype=torch.int32, device=qcoeff.device)
+    if entropy_ctx is None:
+        entropy_ctx = torch.empty(nb, dtype=torch.uint8, device=qcoeff.device)
+    dq = np.ascontiguousarray(dequant, np.int16)
+    assert dq.shape == (2,)
+    rc = _lib.lavish_optimize_b_batch(
+        _vp(costs.t.data_ptr()), _vp(tcoeff.data_ptr()), _vp(qcoeff.data_ptr()),
+        _vp(dqcoeff.data_ptr()), _vp(eob.data_ptr()), nb, plane, tx_size, tx_type, bit_depth,
+        is_inter, rdmult, sharpness, dq.ctypes.data_as(_vp),
+        _vp(txb_ctx.data_ptr()) if txb_ctx is not None else None, tx_type_cost,
+        _vp(rate.data_ptr()), _vp(entropy_ctx.data_ptr()), _stream_ptr(stream))
+    if rc != 0:
+        raise ValueError("lavish_optimize_b_batch rejected its arguments (rc=%d)" % rc)
+    return rate, entropy_ctx

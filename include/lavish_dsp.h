@@ -224,6 +224,26 @@ int lavish_cost_coeffs_txb_batch(const LavishCoeffCosts *costs, const int32_t *q
                                  int tx_type, const LavishTxbCtx *txb_ctx, int tx_type_cost,
                                  int mode, int32_t *rate, void *stream);
 
+/* Replaces av1_optimize_b (av1/encoder/encodemb.c:87-103) -> av1_optimize_txb
+ * (txb_rdopt.c:326-449), the trellis search_tx_type runs on FP-quantized
+ * blocks flagged use_optimize_b, for nblocks blocks of one (tx_size,
+ * tx_type, plane), no quantization matrix.  Device arrays [nblocks][n] (n =
+ * av1_get_max_eob): tcoeff (p->coeff) in; qcoeff / dqcoeff updated in place;
+ * eob [nblocks] in / out; txb_ctx nullable ({0, 0}); rate [nblocks] out
+ * (rate_cost, incl. the skip / non-skip and tx-type cost); entropy_ctx
+ * [nblocks] out, nullable (p->txb_entropy_ctx = av1_get_txb_entropy_context).
+ * rdmult = x->rdmult, is_inter = is_inter_block, sharpness =
+ * oxcf.algo_cfg.sharpness, dequant = p->dequant_QTX[0..1] (host).  eob 0:
+ * rate = txb_skip_cost[ctx][1] (the early exit; segments with
+ * optimize_seg_arr 0 or lossless are the caller's to skip).  Returns 0 or
+ * negative on bad arguments. */
+int lavish_optimize_b_batch(const LavishCoeffCosts *costs, const int32_t *tcoeff,
+                            int32_t *qcoeff, int32_t *dqcoeff, uint16_t *eob, int nblocks,
+                            int plane, int tx_size, int tx_type, int bit_depth, int is_inter,
+                            int rdmult, int sharpness, const int16_t *dequant,
+                            const LavishTxbCtx *txb_ctx, int tx_type_cost, int32_t *rate,
+                            uint8_t *entropy_ctx, void *stream);
+
 /* ---- pixel-domain batch kernels ----------------------------------------- */
 /* One job = one block.  Offsets are in ELEMENTS (u8 or u16 samples / int16
  * residual words) from the plane base pointers passed to the call.  Which

@@ -394,6 +394,14 @@ long orc_rdo_plane_rate(const uint16_t *src, const uint16_t *pred, int stride, i
                         const uint8_t *block_map, OrcRdoBlock *out, int32_t *qcoeff,
                         int32_t *dqcoeff, int threads);
 
+/* ---- coefficient trellis (oracle_trellis.c): av1_optimize_b without a
+ * quantization matrix; qcoeff / dqcoeff updated in place; returns the new eob */
+int orc_optimize_b(const OrcCoeffCosts *cc, const int32_t *tcoeff, int32_t *qcoeff,
+                   int32_t *dqcoeff, int eob, int plane, int tx_size, int tx_type, int bd,
+                   int is_inter, int x_rdmult, int sharpness, const int16_t dequant[2],
+                   int txb_skip_ctx, int dc_sign_ctx, int tx_type_cost, int *rate_cost,
+                   uint8_t *entropy_ctx);
+
 #ifdef __cplusplus
 }
 #endif

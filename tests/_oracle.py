@@ -859,3 +859,21 @@ def rdo_plane_rate(src, pred, tx_size, type_mask, bd, q, rdmult, blob, txb_ctx=N
     fn(P(src), P(pred), W, W, H, tx_size, type_mask, bd, ctypes.byref(q), rdmult, P(blob),
        pp(ctx), pp(ttc), pp(bm), pp(mp), P(out), P(qc), P(dq), threads)
     return out, qc, dq
+
+
+def optimize_b(blob, tcoeff, qcoeff, dqcoeff, eob, plane, tx_size, tx_type, bd, is_inter,
+               x_rdmult, sharpness, dequant, txb_skip_ctx=0, dc_sign_ctx=0, tx_type_cost=0):
+    """orc_optimize_b -> (eob, rate, entropy_ctx, qcoeff, dqcoeff) (copies)."""
+    fn = lib().orc_optimize_b
+    fn.argtypes = [ctypes.c_void_p] * 4 + [ctypes.c_int] * 8 + [ctypes.c_void_p] + \
+        [ctypes.c_int] * 3 + [ctypes.c_void_p, ctypes.c_void_p]
+    fn.restype = ctypes.c_int
+    t = np.ascontiguousarray(tcoeff, np.int32)
+    q = np.array(qcoeff, np.int32)
+    d = np.array(dqcoeff, np.int32)
+    dqv = np.ascontiguousarray(dequant, np.int16)
+    rate = np.zeros(1, np.int32)
+    ec = np.zeros(1, np.uint8)
+    e = fn(P(blob), P(t), P(q), P(d), eob, plane, tx_size, tx_type, bd, is_inter, x_rdmult,
+           sharpness, P(dqv), txb_skip_ctx, dc_sign_ctx, tx_type_cost, P(rate), P(ec))
+    return e, int(rate[0]), int(ec[0]), q, d

@@ -142,6 +142,7 @@ BUILTIN_TYPEDEFS = {
     # the reference): opaque scalars, never used by the interpreted code paths
     "pthread_mutex_t": LONG, "pthread_cond_t": LONG, "pthread_t": ULONG, "va_list": LONG,
     "jmp_buf": LONG, "pthread_attr_t": LONG, "sem_t": LONG,
+    "float_t": FLOAT, "double_t": DOUBLE,  # <math.h> (FLT_EVAL_METHOD 0)
 }
 
 

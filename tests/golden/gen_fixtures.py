@@ -1101,9 +1101,129 @@ def gen_costcoeffs():
     np.savez_compressed(os.path.join(HERE, "fix_costcoeffs.npz"), **out)
 
 
+TR_SIZES = [0, 1, 2, 3, 4, 5, 6, 9, 13, 14, 17]  # 4x4 8x8 16x16 32x32 64x64 4x8 8x4 16x32 4x16 16x4 16x64
+TR_TYPES = {16: [0, 3, 9, 10, 11, 14], 32: [0, 9], 64: [0]}
+
+
+def gen_trellis(txfm_fix):
+    """av1_optimize_b (av1/encoder/encodemb.c:87-103) -> av1_optimize_txb
+    (av1/encoder/txb_rdopt.c:326-449) on av1_quant's FP output (the
+    use_optimize_b path of search_tx_type), from forward-transform outputs of
+    fix_txfm.npz scaled to several magnitudes: bd 8 / 10, qindex 40 / 120 /
+    200, sharpness 0 / 1, luma inter / luma intra / chroma, tx types of the
+    three classes, random TXB_CTX and random LV_MAP cost / tx-type cost
+    tables.  Outputs: the rate, the new eob, qcoeff / dqcoeff and the
+    txb_entropy_ctx."""
+    tu = C.TU(REF, ["av1/encoder/encoder.h", "av1/encoder/txb_rdopt.c",
+                    "av1/encoder/encodetxb.c", "av1/common/txb_common.c", "av1/common/scan.c",
+                    "av1/encoder/encodemb.c", "av1/encoder/av1_quantize.c", "aom_dsp/quantize.c",
+                    "av1/common/quant_common.c", "av1/common/idct.c"], C.reference_defines(REF))
+    check_errors(tu, ["av1_optimize_b", "av1_optimize_txb", "av1_quant", "av1_setup_quant",
+                      "av1_build_quantizer"])
+    E = tu.enums
+    rnd = ACMRandom(0xbaba + 9)
+    cc_tabs = np.array([rnd.generate(4000) for _ in range(10 * CC_COEFF_COST)], np.int32)
+    eob_tabs = np.array([rnd.generate(4000) for _ in range(14 * CC_EOB_COST)], np.int32)
+    cpi = tu.struct_obj("AV1_COMP")
+    CP = cpi.buf[0]
+    _get(CP, "optimize_seg_arr")[0] = 1
+    x = tu.struct_obj("MACROBLOCK")
+    X = x.buf[0]
+    ccs = _get(X, "coeff_costs")
+    k = 0
+    for obj in _get(ccs, "coeff_costs"):
+        for fld in ("txb_skip_cost", "base_eob_cost", "base_cost", "eob_extra_cost",
+                    "dc_sign_cost", "lps_cost"):
+            cell = _get(obj, fld)
+            cell[:] = cc_tabs[k:k + len(cell)].tolist()
+            k += len(cell)
+    k = 0
+    for obj in _get(ccs, "eob_costs"):
+        cell = _get(obj, "eob_cost")
+        cell[:] = eob_tabs[k:k + len(cell)].tolist()
+        k += len(cell)
+    mc = _get(X, "mode_costs")
+    itx = _get(mc, "inter_tx_type_costs")
+    itx[:] = [rnd.generate(3000) for _ in range(len(itx))]
+    atx = _get(mc, "intra_tx_type_costs")
+    atx[:] = [rnd.generate(3000) for _ in range(len(atx))]
+    mbmi = tu.struct_obj("MB_MODE_INFO")
+    xd = _get(X, "e_mbd")
+    _set(xd, mi=tu.buffer("MB_MODE_INFO *", [mbmi]))
+    xd_p = C.Pointer(X.vals, X.st.index["e_mbd"], tu.ctype("MACROBLOCKD"))
+    rows, cin, qin, dqin, qout, dqout = [], [], [], [], [], []
+    for bd in (8, 10):
+        quants = tu.struct_obj("QUANTS")
+        deq = tu.struct_obj("Dequants")
+        tu.func("av1_build_quantizer")(bd, 0, 0, 0, 0, 0, quants, deq, 0)
+        Q, D = quants.buf[0], deq.buf[0]
+        _set(xd, bd=bd)
+        for s in TR_SIZES:
+            n = max_eob(s)
+            for t in TR_TYPES[max(TX_W[s], TX_H[s], 16)]:
+                src = txfm_fix["out_%d_%d" % (s, t)]
+                for qindex in (40, 120, 200):
+                    for plane, inter in ((0, 1), (0, 0), (1, 1)):
+                        b = rnd.generate(len(src))
+                        scale = (1, 4, 16, 64)[rnd.generate(4)]
+                        c = np.clip(src[b].astype(np.int64)[:n] // scale << (bd - 8),
+                                    -(1 << (bd + 7)), (1 << (bd + 7)) - 1)
+                        sharp = rnd.generate(2)
+                        rdmult = 200 + rnd.generate((3000, 60000)[rnd.generate(2)])
+                        p0 = _get(X, "plane")[plane]
+                        for fld, srct, nm in (("quant_fp_QTX", Q, "y_quant_fp"),
+                                              ("round_fp_QTX", Q, "y_round_fp"),
+                                              ("quant_QTX", Q, "y_quant"),
+                                              ("quant_shift_QTX", Q, "y_quant_shift"),
+                                              ("zbin_QTX", Q, "y_zbin"), ("round_QTX", Q, "y_round"),
+                                              ("dequant_QTX", D, "y_dequant_QTX")):
+                            _set(p0, **{fld: C.Pointer(_get(srct, nm), 8 * qindex,
+                                                       tu.ctype("int16_t"))})
+                        cb = tu.buffer("tran_low_t", c.tolist())
+                        qb, db = tu.buffer("tran_low_t", n), tu.buffer("tran_low_t", n)
+                        eb = tu.buffer("uint16_t", 1)
+                        ec = tu.buffer("uint8_t", 1)
+                        _set(p0, coeff=cb, qcoeff=qb, dqcoeff=db, eobs=eb, txb_entropy_ctx=ec)
+                        _set(X, seg_skip_block=0, rdmult=rdmult)
+                        M = mbmi.buf[0]
+                        _get(M, "ref_frame")[0] = E["LAST_FRAME"] if inter else E["INTRA_FRAME"]
+                        _set(M, mode=E["DC_PRED"], segment_id=0)
+                        _set(_get(_get(CP, "oxcf"), "algo_cfg"), sharpness=sharp)
+                        qp = tu.struct_obj("QUANT_PARAM")
+                        tp = tu.struct_obj("TxfmParam")
+                        _set(tp.buf[0], tx_type=t, tx_size=s, is_hbd=int(bd > 8), bd=bd)
+                        tu.func("av1_setup_quant")(s, 1, E["AV1_XFORM_QUANT_FP"], 0, qp)
+                        tu.func("av1_quant")(x, plane, 0, tp, qp)
+                        eob_in = eb.buf[0]
+                        q_in, dq_in = list(qb.buf), list(db.buf)
+                        ctx = tu.struct_obj("TXB_CTX")
+                        skip_ctx, dc_ctx = rnd.generate(13), rnd.generate(3)
+                        _set(ctx.buf[0], txb_skip_ctx=skip_ctx, dc_sign_ctx=dc_ctx)
+                        rate = tu.buffer("int", 1)
+                        eob_out = tu.func("av1_optimize_b")(cpi, x, plane, 0, s, t, ctx, rate)
+                        ttc = tu.func("get_tx_type_cost")(x, xd_p, plane, s, t, 0)
+                        rows.append([bd, s, t, qindex, plane, inter, sharp, rdmult, skip_ctx,
+                                     dc_ctx, ttc, eob_in, eob_out, rate.buf[0], ec.buf[0],
+                                     len(cin)])
+                        for lst, v in ((cin, c), (qin, q_in), (dqin, dq_in), (qout, qb.buf),
+                                       (dqout, db.buf)):
+                            pad = np.zeros(1024, np.int32)
+                            pad[:n] = v
+                            lst.append(pad)
+            print("  trellis bd %d size %d: %d blocks" % (bd, s, len(rows)))
+    out = {"rows": np.array(rows, np.int64), "coeff": np.stack(cin), "qcoeff_in": np.stack(qin),
+           "dqcoeff_in": np.stack(dqin), "qcoeff": np.stack(qout), "dqcoeff": np.stack(dqout),
+           "coeff_costs": cc_tabs, "eob_costs": eob_tabs,
+           "row_fields": np.array(["bd", "tx_size", "tx_type", "qindex", "plane", "is_inter",
+                                   "sharpness", "rdmult", "txb_skip_ctx", "dc_sign_ctx",
+                                   "tx_type_cost", "eob_in", "eob", "rate", "entropy_ctx",
+                                   "index"])}
+    np.savez_compressed(os.path.join(HERE, "fix_trellis.npz"), **out)
+
+
 def main(argv):
     sections = argv or ["txfm", "qparams", "quant", "inv", "pixel", "wht", "nmv", "mcomp",
-                        "subpel", "tpl", "qfacade", "costcoeffs"]
+                        "subpel", "tpl", "qfacade", "costcoeffs", "trellis"]
     t0 = time.time()
     ttx = None
     if "txfm" in sections or "inv" in sections or "wht" in sections:
@@ -1138,6 +1258,8 @@ def main(argv):
         gen_qfacade(dict(np.load(os.path.join(HERE, "fix_txfm.npz"))))
     if "costcoeffs" in sections:
         gen_costcoeffs()
+    if "trellis" in sections:
+        gen_trellis(dict(np.load(os.path.join(HERE, "fix_txfm.npz"))))
     print("done in %.0fs" % (time.time() - t0))
 
 

@@ -333,3 +333,31 @@ def test_rdo_rate_oracle_records_are_cost_coeffs():
                                   int(ctx[b, 1]), int(ttc[t]))
             assert r == rec["rate"][b]
             assert rec["rdcost"][b] == ((r * 1500 + 256) >> 9) + int(rec["dist"][b]) * 128
+
+
+def test_optimize_b_matches_reference():
+    """orc_optimize_b against av1_optimize_b executed from the reference
+    (tests/golden/fix_trellis.npz) on av1_quant's FP output: rate, eob,
+    txb_entropy_ctx, qcoeff and dqcoeff, every row."""
+    F = _load("fix_trellis.npz")
+    J = {n: i for i, n in enumerate(F["row_fields"])}
+    blob = O.coeff_costs_blob(F["coeff_costs"], F["eob_costs"])
+    changed = skipped = 0
+    for r in F["rows"]:
+        g = lambda k: int(r[J[k]])
+        n = O.max_eob(g("tx_size"))
+        i = g("index")
+        q = O.quant_arrays(O.build_quant(g("bd"), g("qindex")))
+        dqv = q["dequant"]
+        e, rate, ec, qc, dq = O.optimize_b(
+            blob, F["coeff"][i][:n], F["qcoeff_in"][i][:n], F["dqcoeff_in"][i][:n],
+            g("eob_in"), g("plane"), g("tx_size"), g("tx_type"), g("bd"), g("is_inter"),
+            g("rdmult"), g("sharpness"), dqv, g("txb_skip_ctx"), g("dc_sign_ctx"),
+            g("tx_type_cost"))
+        msg = str({k: g(k) for k in J})
+        assert (e, rate, ec) == (g("eob"), g("rate"), g("entropy_ctx")), msg
+        np.testing.assert_array_equal(qc, F["qcoeff"][i][:n], err_msg=msg)
+        np.testing.assert_array_equal(dq, F["dqcoeff"][i][:n], err_msg=msg)
+        changed += int((qc != F["qcoeff_in"][i][:n]).any())
+        skipped += int(g("eob") == 0 and g("eob_in") > 0)
+    assert changed > 100 and skipped > 10
