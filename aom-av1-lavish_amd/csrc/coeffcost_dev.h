@@ -79,6 +79,40 @@ __device__ __forceinline__ int br_ctx(int cls, const uint8_t* lv, int stride, in
   return br_ctx_mag(cls, l[1] + l[stride] + third, pos, col, row);
 }
 
+// The neighbour offsets of get_nz_mag / get_br_ctx for one tx class, fixed
+// per block: lower_ctx_off / br_ctx_off read through them with no per-
+// coefficient class branch.  (The class-branching forms above, inlined into
+// the trellis walk, were miscompiled by the ROCm 7.2 compiler for the
+// vertical class: the l[2] address register of the br_ctx load was left
+// undefined on that path.)
+struct NbrOff {
+  int nz0, nz1, nz2;  // get_nz_mag's three class-dependent neighbours
+  int br;             // get_br_ctx's third neighbour
+};
+__host__ __device__ __forceinline__ NbrOff nbr_off(int cls, int stride) {
+  NbrOff o;
+  if (cls == 0) {
+    o.nz0 = stride + 1; o.nz1 = 2 * stride; o.nz2 = 2; o.br = stride + 1;
+  } else if (cls == 2) {
+    o.nz0 = 2; o.nz1 = 3; o.nz2 = 4; o.br = 2;
+  } else {
+    o.nz0 = 2 * stride; o.nz1 = 3 * stride; o.nz2 = 4 * stride; o.br = 2 * stride;
+  }
+  return o;
+}
+__device__ __forceinline__ int lower_ctx_off(const NbrOff& o, int cls, int wlt, int wgt,
+                                             const uint8_t* lv, int stride, int pos, int col,
+                                             int row) {
+  const uint8_t* l = lv + col * stride + row;
+  const int mag = min3(l[stride]) + min3(l[1]) + min3(l[o.nz0]) + min3(l[o.nz1]) + min3(l[o.nz2]);
+  return nz_ctx(cls, wlt, wgt, mag, pos, col, row);
+}
+__device__ __forceinline__ int br_ctx_off(const NbrOff& o, int cls, const uint8_t* lv, int stride,
+                                          int pos, int col, int row) {
+  const uint8_t* l = lv + col * stride + row;
+  return br_ctx_mag(cls, l[1] + l[stride] + l[o.br], pos, col, row);
+}
+
 // get_br_ctx_eob (txb_common.h:90-101)
 __device__ __forceinline__ int br_ctx_eob(int cls, int pos, int col, int row) {
   if (pos == 0) return 0;

@@ -56,6 +56,7 @@ struct Walk {
   int32_t* dqc;
   int64_t rdmult;
   int n, h, bhl, stride, cls, wlt, wgt, shift, sharpness, dqv_dc, dqv_ac, dc_sign_ctx;
+  NbrOff nb;  // the class's neighbour offsets in the level map
 
   // RDCOST (av1/encoder/rd.h:31-33)
   __device__ __forceinline__ int64_t rd(int64_t r, int64_t d) const {
@@ -72,7 +73,7 @@ struct Walk {
     lv[col_of(ci) * stride + row_of(ci)] = (uint8_t)min(v, 127);
   }
   __device__ __forceinline__ int lower(int ci) const {
-    return lower_ctx(cls, wlt, wgt, lv, stride, ci, col_of(ci), row_of(ci));
+    return lower_ctx_off(nb, cls, wlt, wgt, lv, stride, ci, col_of(ci), row_of(ci));
   }
   // get_lower_levels_ctx_eob (txb_common.h:229-234)
   __device__ __forceinline__ int eob_ctx(int si) const {
@@ -96,7 +97,7 @@ struct Walk {
     int c = tab[kBase + ctx * 8 + min3(a)];
     if (a) {
       c += sign_cost(ci, sign);
-      if (a > 2) c += br_cost(tab, br_ctx(cls, lv, stride, ci, col_of(ci), row_of(ci)), a);
+      if (a > 2) c += br_cost(tab, br_ctx_off(nb, cls, lv, stride, ci, col_of(ci), row_of(ci)), a);
     }
     return c;
   }
@@ -167,7 +168,7 @@ struct Walk {
     int cost = tab[kBase + ctx * 8 + min3(a)] + 512;
     int diff = a <= 3 ? tab[kBase + ctx * 8 + a + 4] : 0;
     if (a > 2) {
-      const int* lps = tab + kLps + br_ctx(cls, lv, stride, ci, col_of(ci), row_of(ci)) * 26;
+      const int* lps = tab + kLps + br_ctx_off(nb, cls, lv, stride, ci, col_of(ci), row_of(ci)) * 26;
       const int br = min(a - 3, 12);
       cost += lps[br];
       if (a <= 15) diff += lps[br + 13];
@@ -313,6 +314,7 @@ __global__ __launch_bounds__(64) void trellis_kernel(TrArgs a) {
   w.bhl = a.bhl;
   w.stride = a.h + 4;
   w.cls = a.cls;
+  w.nb = nbr_off(a.cls, w.stride);
   w.wlt = a.wlt;
   w.wgt = a.wgt;
   w.shift = a.shift;

@@ -96,4 +96,5 @@ def test_optimize_b_vs_oracle(s, t, bd, sharp):
         np.testing.assert_array_equal(gq[b], oq)
         np.testing.assert_array_equal(gd[b], od)
         changed += int((oq != q0[b]).any())
-    assert changed > 0
+    if sharp == 0:  # (at sharpness 2 small blocks are often left as quantized)
+        assert changed > 0
