@@ -12,8 +12,8 @@
 // Here one wave64 owns one (block, reference) job and runs that sequential
 // walk.  A step's 8 candidate sites are evaluated at once: lane group
 // g = lane / 8 takes site g + 1, its 8 lanes split the block's rows, each
-// lane accumulates v_sad_u8 over 4-byte words (rows assembled with
-// v_alignbyte from dword-aligned loads), and three DPP adds leave the
+// lane accumulates v_sad_u8 over 4-byte words (each row one byte-addressed
+// 16-byte load), and three DPP adds leave the
 // group's SAD in every lane.  Each group then forms the key
 // (sad + mvsad_cost) * 8 + site for its site and the wave takes the minimum
 // over the 8 groups (8 readlanes + s_min): the reference's sequential
@@ -35,26 +35,40 @@ __device__ __forceinline__ uint32_t sad4(uint32_t a, uint32_t b, uint32_t acc) {
   return __builtin_amdgcn_sad_u8(a, b, acc);
 }
 
-// DW consecutive 4-byte words starting at an arbitrary byte address, from
-// dword-aligned loads (DW words + one more, merged into dwordx4 loads) and
-// v_alignbyte.  The extra word is the next one only when the address is
-// unaligned (else the last one again), so no byte outside the row is read.
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+// DW consecutive 4-byte words starting at an arbitrary byte address.  The
+// queues run with unaligned access enabled (SH_MEM_CONFIG alignment mode;
+// probed on the box by tools/microbench/unaligned.hip), so one dwordx4 /
+// dwordx2 load per 16 / 8 bytes at the byte address returns the row
+// directly: one vector-memory instruction per 16-byte row instead of a
+// dwordx4 + dword pair and four v_alignbyte.
 template <int DW>
 __device__ __forceinline__ void load_row(const uint8_t* p, uint32_t (&out)[DW]) {
-  const uintptr_t a = (uintptr_t)p;
   // global address space: global_load (not flat: no LDS-aperture check and
   // no lgkmcnt dependency)
-  typedef const __attribute__((address_space(1))) uint32_t* gptr;
-  const gptr q = (gptr)(a & ~(uintptr_t)3);
-  const uint32_t sh = (uint32_t)(a & 3);
-  uint32_t w[DW + 1];
+  if constexpr (DW % 4 == 0) {
+    typedef const __attribute__((address_space(1))) u32x4* gptr4;
+    const gptr4 q = (gptr4)p;
 #pragma unroll
-  for (int i = 0; i < DW; ++i) w[i] = q[i];
-  // the next word only matters when the row is unaligned; an aligned row
-  // re-reads its last word instead (no branch, no byte past the row)
-  w[DW] = q[sh ? DW : DW - 1];
+    for (int i = 0; i < DW / 4; ++i) {
+      const u32x4 v = q[i];
+      out[4 * i] = v.x;
+      out[4 * i + 1] = v.y;
+      out[4 * i + 2] = v.z;
+      out[4 * i + 3] = v.w;
+    }
+  } else if constexpr (DW == 2) {
+    typedef const __attribute__((address_space(1))) u32x2* gptr2;
+    const u32x2 v = *(gptr2)p;
+    out[0] = v.x;
+    out[1] = v.y;
+  } else {
+    typedef const __attribute__((address_space(1))) uint32_t* gptr;
 #pragma unroll
-  for (int i = 0; i < DW; ++i) out[i] = __builtin_amdgcn_alignbyte(w[i + 1], w[i], sh);
+    for (int i = 0; i < DW; ++i) out[i] = ((gptr)p)[i];
+  }
 }
 
 // sum over the 8-lane group (every lane of the group gets it): quad_perm
@@ -203,6 +217,7 @@ __device__ void sad_and_skip(const Ctx& c, int lane, int row, int col, int& sad,
 }
 
 typedef __attribute__((address_space(3))) uint32_t* lds_u32;
+typedef __attribute__((address_space(3))) uint8_t* lds_u8;
 
 // LDS window of the reference for the small-radius tail of a search: once the
 // radius drops to <= 8 the walk can move at most 8+4+2+1 = 15 pixels, so every
@@ -366,14 +381,27 @@ struct Search {
       if (row < G::RH) {
         const int wr = r - wr0 + row * G::YS;  // >= 0
         const int x = cc - wc0 + (int)(((uint32_t)wbase + __umul24(wr, c.rs & 3)) & 3);
-        const lds_u32 p = win + wr * WN::DW + (x >> 2);
-        const uint32_t sh = (uint32_t)(x & 3);
-        uint32_t w[G::DW + 1];
+        // byte-addressed (unaligned) LDS reads, 16 / 8 / 4 bytes at a time
+        const lds_u8 p = (lds_u8)win + (wr * WN::DW * 4 + x);
+        uint32_t w[G::DW];
+        if constexpr (G::DW % 4 == 0) {
 #pragma unroll
-        for (int i = 0; i <= G::DW; ++i) w[i] = p[i];
+          for (int i = 0; i < G::DW / 4; ++i) {
+            const u32x4 v = ((const __attribute__((address_space(3))) u32x4*)p)[i];
+            w[4 * i] = v.x;
+            w[4 * i + 1] = v.y;
+            w[4 * i + 2] = v.z;
+            w[4 * i + 3] = v.w;
+          }
+        } else if constexpr (G::DW == 2) {
+          const u32x2 v = *(const __attribute__((address_space(3))) u32x2*)p;
+          w[0] = v.x;
+          w[1] = v.y;
+        } else {
+          w[0] = *(const __attribute__((address_space(3))) uint32_t*)p;
+        }
 #pragma unroll
-        for (int i = 0; i < G::DW; ++i)
-          acc = sad4(s[k][i], __builtin_amdgcn_alignbyte(w[i + 1], w[i], sh), acc);
+        for (int i = 0; i < G::DW; ++i) acc = sad4(s[k][i], w[i], acc);
       }
     }
     acc = group_sum8(acc);
@@ -394,9 +422,8 @@ struct Search {
             const int y = i / (W / 4), x4 = i % (W / 4);
             const int wr = row - wr0 + y;
             const int xb = col - wc0 + 4 * x4 + (int)(((uint32_t)wbase + __umul24(wr, c.rs & 3)) & 3);
-            const lds_u32 p = win + wr * WN::DW + (xb >> 2);
-            var_acc(sv[v], __builtin_amdgcn_alignbyte(p[1], p[0], (uint32_t)(xb & 3)), sum,
-                    sse);
+            const lds_u8 p = (lds_u8)win + (wr * WN::DW * 4 + xb);
+            var_acc(sv[v], *(const __attribute__((address_space(3))) uint32_t*)p, sum, sse);
           }
         }
         return var_finish<W, H>(c, sum, sse, row, col);
