@@ -61,6 +61,135 @@ __global__ __launch_bounds__(64) void sad_kernel(const Pix* src, int ss, const P
   }
 }
 
+// ----------------------------------------------- 8-bit SAD / variance ----
+// The u8 forms of sad_kernel / var_kernel (modes 0-2, kinds 0-2 and 4) on
+// 4-byte words: a job's rows are cut into chunks of C = min(4, w / 4) words,
+// each lane takes whole chunks with byte-addressed loads (16 / 8 / 4 bytes;
+// the queues allow unaligned access), and a wave holds 64 / LPJ jobs of LPJ
+// = min(64, chunks) lanes each, so a 4x4 job uses 4 lanes, not a wave.
+//   SAD: v_sad_u8 per word (the avg mode first takes v_lerp_u8 of ref and
+//        second_pred, ROUND_POWER_OF_TWO(a + b, 1) per byte);
+//   variance: sum = sad(a, 0) - sad(b, 0), sse = a.a + b.b - 2 a.b with
+//        v_dot4_u32_u8 (exact mod 2^32; the true sse < 2^32 for 8-bit).
+struct U8Shape {
+  int lw4;   // log2(w / 4)
+  int lc;    // log2(words per chunk)
+  int lcpr;  // log2(chunks per row)
+  int lpj;   // lanes per job (power of two, <= 64)
+  int chunks;
+};
+
+__device__ __forceinline__ void load_words(const uint8_t* p, int c, uint32_t (&w)[4]) {
+  typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+  typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+  if (c == 4) {
+    const u32x4 v = *(const __attribute__((address_space(1))) u32x4*)p;
+    w[0] = v.x; w[1] = v.y; w[2] = v.z; w[3] = v.w;
+  } else if (c == 2) {
+    const u32x2 v = *(const __attribute__((address_space(1))) u32x2*)p;
+    w[0] = v.x; w[1] = v.y; w[2] = 0; w[3] = 0;
+  } else {
+    w[0] = *(const __attribute__((address_space(1))) uint32_t*)p;
+    w[1] = 0; w[2] = 0; w[3] = 0;
+  }
+}
+
+// sum over the LPJ-lane group of a job (every lane of the group gets it)
+__device__ __forceinline__ uint32_t group_sum(uint32_t v, int lpj) {
+  for (int m = 1; m < lpj; m <<= 1) v += __shfl_xor(v, m);
+  return v;
+}
+
+__global__ __launch_bounds__(256) void sad_u8_kernel(const uint8_t* __restrict__ src, int ss,
+                                                     const uint8_t* __restrict__ ref, int rs,
+                                                     U8Shape sh, const LavishPixJob* __restrict__ jobs,
+                                                     int njobs, int nrefs, int mode,
+                                                     const uint8_t* __restrict__ second, int w,
+                                                     uint32_t* __restrict__ out) {
+  const int t = blockIdx.x * 256 + threadIdx.x;
+  const int j = t >> __builtin_ctz(sh.lpj);
+  const int q = t & (sh.lpj - 1);
+  const bool live = j < njobs;
+  const LavishPixJob jb = jobs[live ? j : njobs - 1];
+  const int rstep = mode == 1 ? 2 : 1;
+  const int c = 1 << sh.lc;
+  for (int k = 0; k < nrefs; ++k) {
+    uint32_t acc = 0;
+    for (int i = q; i < sh.chunks; i += sh.lpj) {
+      const int y = i >> sh.lcpr, x = (i & ((1 << sh.lcpr) - 1)) << (sh.lc + 2);
+      uint32_t a[4], b[4];
+      load_words(src + jb.src_off + (int64_t)y * rstep * ss + x, c, a);
+      load_words(ref + jb.ref_off[k] + (int64_t)y * rstep * rs + x, c, b);
+      if (mode == 2) {
+        uint32_t p[4];
+        load_words(second + jb.aux_off + (int64_t)y * w + x, c, p);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) b[u] = __builtin_amdgcn_lerp(b[u], p[u], 0x01010101u);
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) acc = __builtin_amdgcn_sad_u8(a[u], b[u], acc);
+    }
+    acc = group_sum(acc, sh.lpj);
+    if (live && q == 0) out[(int64_t)j * nrefs + k] = mode == 1 ? 2 * acc : acc;
+  }
+}
+
+__global__ __launch_bounds__(256) void var_u8_kernel(const uint8_t* __restrict__ a, int as,
+                                                     const uint8_t* __restrict__ b, int bs,
+                                                     U8Shape sh, int w, int h,
+                                                     const LavishPixJob* __restrict__ jobs,
+                                                     int njobs, int kind,
+                                                     uint32_t* __restrict__ var_out,
+                                                     uint32_t* __restrict__ sse_out,
+                                                     int32_t* __restrict__ sum_out,
+                                                     int64_t* __restrict__ sse64_out) {
+  const int t = blockIdx.x * 256 + threadIdx.x;
+  const int j = t >> __builtin_ctz(sh.lpj);
+  const int q = t & (sh.lpj - 1);
+  const bool live = j < njobs;
+  const LavishPixJob jb = jobs[live ? j : njobs - 1];
+  const int c = 1 << sh.lc;
+  uint32_t sa = 0, sb = 0, aa = 0, bb = 0, ab = 0;
+  for (int i = q; i < sh.chunks; i += sh.lpj) {
+    const int y = i >> sh.lcpr, x = (i & ((1 << sh.lcpr) - 1)) << (sh.lc + 2);
+    uint32_t va[4], vb[4];
+    load_words(a + jb.src_off + (int64_t)y * as + x, c, va);
+    load_words(b + jb.ref_off[0] + (int64_t)y * bs + x, c, vb);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      sa = __builtin_amdgcn_sad_u8(va[u], 0u, sa);
+      sb = __builtin_amdgcn_sad_u8(vb[u], 0u, sb);
+      aa = __builtin_amdgcn_udot4(va[u], va[u], aa, false);
+      bb = __builtin_amdgcn_udot4(vb[u], vb[u], bb, false);
+      ab = __builtin_amdgcn_udot4(va[u], vb[u], ab, false);
+    }
+  }
+  const int sum = (int)group_sum(sa, sh.lpj) - (int)group_sum(sb, sh.lpj);
+  const uint32_t sse = group_sum(aa, sh.lpj) + group_sum(bb, sh.lpj) - 2u * group_sum(ab, sh.lpj);
+  if (!live || q != 0) return;
+  if (kind == 4) {
+    sse64_out[j] = (int64_t)sse;
+    return;
+  }
+  if (sse_out) sse_out[j] = sse;
+  if (sum_out) sum_out[j] = sum;
+  if (var_out) var_out[j] = kind == 1 ? sse : sse - (uint32_t)(((int64_t)sum * sum) / (w * h));
+}
+
+static int ilog2(int v) { return 31 - __builtin_clz(v); }
+
+// the u8 word-chunk layout of a w x h block with `rows` rows read; false when
+// w or rows is not a power of two >= 4 / >= 1
+static bool u8_shape(int w, int rows, U8Shape& sh) {
+  if (w < 4 || (w & (w - 1)) || rows < 1 || (rows & (rows - 1))) return false;
+  sh.lw4 = ilog2(w / 4);
+  sh.lc = sh.lw4 < 2 ? sh.lw4 : 2;
+  sh.lcpr = sh.lw4 - sh.lc;
+  sh.chunks = rows << sh.lcpr;
+  sh.lpj = sh.chunks < 64 ? sh.chunks : 64;
+  return true;
+}
+
 // ------------------------------------------------------------ variance ----
 // d = a - b with a = the first rtcd pointer (src; the bilinear-filtered one
 // for sub-pixel variance) at job.src_off and b = the second at job.ref_off[0].  kind 0: variance, 1: mse (returns sse), 2: get_var
@@ -447,6 +576,15 @@ int lavish_sad_batch(const void* src, int src_stride, const void* ref, int ref_s
   if (njobs <= 0) return 0;
   if (nrefs < 1 || nrefs > 4 || mode < 0 || mode > 2 || (mode == 2 && !second_pred)) return -1;
   hipStream_t s = (hipStream_t)stream;
+  U8Shape sh;
+  if (!highbd && u8_shape(w, mode == 1 ? h / 2 : h, sh)) {
+    const int blocks = (int)(((int64_t)njobs * sh.lpj + 255) / 256);
+    hipLaunchKernelGGL(sad_u8_kernel, dim3(blocks), dim3(256), 0, s, (const uint8_t*)src,
+                       src_stride, (const uint8_t*)ref, ref_stride, sh, jobs, njobs, nrefs, mode,
+                       (const uint8_t*)second_pred, w, sad_out);
+    LCHK();
+    return 0;
+  }
   if (highbd)
     hipLaunchKernelGGL(sad_kernel<uint16_t>, dim3(njobs), dim3(64), 0, s, (const uint16_t*)src,
                        src_stride, (const uint16_t*)ref, ref_stride, w, h, jobs, nrefs, mode,
@@ -466,6 +604,15 @@ int lavish_variance_batch(const void* a, int a_stride, const void* b, int b_stri
   if (njobs <= 0) return 0;
   if (kind < 0 || kind > 5 || (kind == 5 && !second_pred)) return -1;
   hipStream_t s = (hipStream_t)stream;
+  U8Shape sh;
+  if (!highbd && kind != 3 && kind != 5 && u8_shape(w, h, sh)) {
+    const int blocks = (int)(((int64_t)njobs * sh.lpj + 255) / 256);
+    hipLaunchKernelGGL(var_u8_kernel, dim3(blocks), dim3(256), 0, s, (const uint8_t*)a, a_stride,
+                       (const uint8_t*)b, b_stride, sh, w, h, jobs, njobs, kind, var_out,
+                       sse_out, sum_out, sse64_out);
+    LCHK();
+    return 0;
+  }
   if (highbd)
     hipLaunchKernelGGL(var_kernel<uint16_t>, dim3(njobs), dim3(64), 0, s, (const uint16_t*)a,
                        a_stride, (const uint16_t*)b, b_stride, w, h, jobs, kind, bit_depth,

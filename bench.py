@@ -34,6 +34,7 @@ launch duration, from HIP events on the launch stream) and `cpu_baseline`
 (the oracle's C restatement on the host cores, rank 0 at N=1, bounded sample).
 """
 import argparse
+import ctypes
 import json
 
 import numpy as np
@@ -54,7 +55,7 @@ def parse():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--workload", choices=("rdo", "c2", "c3", "c3sub", "c4", "c4px", "c5", "inter",
-                                           "tpl", "rate"),
+                                           "tpl", "rate", "pixel"),
                     default="rdo")
     ap.add_argument("--rdmult", type=int, default=2000)
     ap.add_argument("--width", type=int, default=1920)
@@ -511,6 +512,160 @@ def main_inter(args):
         dist.destroy_process_group()
 
 
+PIX_RADIUS = 16  # candidate offsets of the pixel workload: within +-16 px
+
+
+def pixel_setup(W, H, nrefs, border, seed):
+    """Pixel workload: the motion planes and one LavishPixJob per 16x16 block
+    x reference: src = the block, ref_off[0..3] = four seeded candidate
+    positions within +-PIX_RADIUS px in that reference (an x4d call)."""
+    import lavish_dsp.pixel as P
+    import lavish_dsp.synth as synth
+    src, refs = synth.motion_planes(W, H, nrefs, border, seed=seed)
+    st = src.shape[1]
+    nbx, nby = W // C3_BLOCK, H // C3_BLOCK
+    ys = np.repeat(np.arange(nby) * C3_BLOCK, nbx)
+    xs = np.tile(np.arange(nbx) * C3_BLOCK, nby)
+    org = (ys + border) * st + xs + border
+    rng = np.random.default_rng(seed)
+    jobs = np.zeros(nrefs * len(org), P.JOB_DTYPE)
+    jobs["src_off"] = np.tile(org, nrefs)
+    d = rng.integers(-PIX_RADIUS, PIX_RADIUS + 1, size=(len(jobs), 4, 2))
+    plane = np.repeat(np.arange(nrefs) * refs[0].size, len(org))
+    jobs["ref_off"] = (plane + np.tile(org, nrefs))[:, None] + d[..., 0] * st + d[..., 1]
+    return src, refs, st, jobs
+
+
+def pixel_bytes(njobs, bw=16, bh=16):
+    """Algorithmic bytes of one step: per job the x4d SAD reads the source
+    block and 4 candidate blocks (5 * w * h) and writes 16 B; the variance
+    reads 2 * w * h and writes 8 B; 56 B job record read by each call."""
+    return njobs * (5 * bw * bh + 16 + 2 * bw * bh + 8 + 2 * 56)
+
+
+def cpu_baseline_pixel(args):
+    """orc_pixel_batch (the oracle's orc_sad x 4 + orc_variance per job) on a
+    1920x256 strip of the same workload on all host cores, ~cpu_seconds."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import _oracle as O
+    W, Hs = args.width, 256
+    src, refs, st, jobs = pixel_setup(W, Hs, args.refs, args.border, 1234)
+    threads = host_cores()
+    sb = sb64_count(W, Hs)
+    passes = 0
+    t0 = time.perf_counter()
+    while True:
+        O.pixel_batch(src.reshape(-1), st, refs.reshape(-1), st, C3_BLOCK, C3_BLOCK, jobs,
+                      threads=threads)
+        passes += 1
+        dt = time.perf_counter() - t0
+        if dt >= args.cpu_seconds:
+            break
+    return {"value": round(passes * sb / dt, 2), "unit": "SB64/s", "cores": threads,
+            "kind": "port",
+            "sample": "%d passes of a %dx%d strip (%d SB64, %d jobs) through the pixel step, "
+                      "oracle C restatement (-O3, %d pthreads), %.1f s"
+                      % (passes, W, Hs, sb, len(jobs), threads, dt)}
+
+
+def main_pixel(args):
+    """The pixel batch kernels on a 1080p frame: aom_sad16x16x4d of every
+    16x16 block x reference at 4 seeded candidates (lavish_sad_batch, nrefs
+    4) then aom_variance16x16 at candidate 0 (lavish_variance_batch)."""
+    import torch
+    import torch.distributed as dist
+    import lavish_dsp as L
+    import lavish_dsp.pixel as P
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local_rank)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    W, H = args.width, args.height
+    src, refs, st, jobs_np = pixel_setup(W, H, args.refs, args.border, 1234 + rank)
+    tsrc = torch.from_numpy(src).cuda()
+    trefs = torch.from_numpy(refs.reshape(-1, st)).cuda()  # the refs stacked, one stride
+    tjobs = P.jobs_tensor(jobs_np, "cuda")
+    nj = len(jobs_np)
+    sad = torch.empty((nj, 4), dtype=torch.int32, device="cuda")
+    var = torch.empty(nj, dtype=torch.int32, device="cuda")
+    sse = torch.empty(nj, dtype=torch.int32, device="cuda")
+    stream = torch.cuda.current_stream()
+    vp = lambda t: ctypes.c_void_p(t.data_ptr())
+    sp = ctypes.c_void_p(stream.cuda_stream)
+
+    def step():  # the C ABI directly: no wrapper-side conversions in the timed region
+        rc = P._lib.lavish_sad_batch(vp(tsrc), st, vp(trefs), st, C3_BLOCK, C3_BLOCK, vp(tjobs),
+                                     nj, 4, 0, None, 0, vp(sad), sp)
+        rc |= P._lib.lavish_variance_batch(vp(tsrc), st, vp(trefs), st, C3_BLOCK, C3_BLOCK,
+                                           vp(tjobs), nj, 0, 8, 0, None, vp(var), vp(sse), None,
+                                           None, sp)
+        assert rc == 0
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+          for _ in range(args.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        ev[k][0].record(stream)
+        step()
+        ev[k][1].record(stream)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    status = L.status()
+    if status[0] != 0:
+        raise RuntimeError("HIP error during bench: %s" % (status,))
+    k_ms = sum(a.elapsed_time(b) for a, b in ev) / args.steps
+    nbytes = pixel_bytes(len(jobs_np))
+    sb = sb64_count(W, H)
+    line = {
+        "metric": METRIC,
+        "value": round(world * sb * args.steps / elapsed, 2),
+        "unit": "SB64/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u8",
+        "data": "synthetic (seeded 1080p content, lavish_dsp/synth.py; seeded candidates)",
+        "config": {
+            "workload": "pixel: %dx%d 8-bit; aom_sad16x16x4d (4 candidates within +-%d px) + "
+                        "aom_variance16x16 of every 16x16 block x %d refs, %d jobs; %d SB64/frame"
+                        % (W, H, PIX_RADIUS, args.refs, len(jobs_np), sb),
+            "parallelism": "frame-per-rank x%d" % world,
+        },
+        "roofline": {"bound": "hbm", "kernel": "sad_u8_kernel + var_u8_kernel "
+                     "(lavish_sad_batch + lavish_variance_batch)",
+                     "achieved": round(nbytes / (k_ms * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "traffic": None, "avg_launch_ms": round(k_ms, 4),
+                     "algorithmic_bytes_per_launch": nbytes,
+                     "note": "overlapping candidate blocks are L2 hits: algorithmic bytes "
+                             "exceed the HBM bytes"},
+    }
+    line["roofline"]["frac"] = round(line["roofline"]["achieved"] / HBM_PEAK_GBS, 4)
+    if rank == 0 and world == 1 and not args.no_cpu:
+        line["cpu_baseline"] = cpu_baseline_pixel(args)
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
 TPL_BORDER = 288  # AOM_BORDER_IN_PIXELS: the predictor's clamp reads stay inside
 
 
@@ -849,6 +1004,8 @@ def main():
         return main_c4(args)
     if args.workload == "inter":
         return main_inter(args)
+    if args.workload == "pixel":
+        return main_pixel(args)
     if args.workload == "tpl":
         return main_tpl(args)
     if args.workload == "rate":

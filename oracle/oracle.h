@@ -402,7 +402,14 @@ int orc_optimize_b(const OrcCoeffCosts *cc, const int32_t *tcoeff, int32_t *qcoe
                    int txb_skip_ctx, int dc_sign_ctx, int tx_type_cost, int *rate_cost,
                    uint8_t *entropy_ctx);
 
+/* oracle_pixbatch.c: 4-candidate SAD + variance (candidate 0) per job
+ * (LavishPixJob layout), 8-bit, over `threads` pthreads */
+void orc_pixel_batch(const uint8_t *src, int ss, const uint8_t *ref, int rs, int w, int h,
+                     const void *jobs, long njobs, uint32_t *sad, uint32_t *var, uint32_t *sse,
+                     int threads);
+
 #ifdef __cplusplus
 }
 #endif
+
 #endif  // LAVISH_ORACLE_H_

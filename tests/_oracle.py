@@ -877,3 +877,18 @@ def optimize_b(blob, tcoeff, qcoeff, dqcoeff, eob, plane, tx_size, tx_type, bd, 
     e = fn(P(blob), P(t), P(q), P(d), eob, plane, tx_size, tx_type, bd, is_inter, x_rdmult,
            sharpness, P(dqv), txb_skip_ctx, dc_sign_ctx, tx_type_cost, P(rate), P(ec))
     return e, int(rate[0]), int(ec[0]), q, d
+
+
+def pixel_batch(src, ss, ref, rs, w, h, jobs, threads=1):
+    """orc_pixel_batch: (sad [n, 4], var [n], sse [n]) of 8-bit jobs (JOB_DTYPE)."""
+    fn = lib().orc_pixel_batch
+    fn.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p] + [ctypes.c_int] * 3 + \
+        [ctypes.c_void_p, ctypes.c_long] + [ctypes.c_void_p] * 3 + [ctypes.c_int]
+    fn.restype = None
+    n = len(jobs)
+    sad = np.zeros((n, 4), np.uint32)
+    var = np.zeros(n, np.uint32)
+    sse = np.zeros(n, np.uint32)
+    jobs = np.ascontiguousarray(jobs)
+    fn(P(src), ss, P(ref), rs, w, h, P(jobs), n, P(sad), P(var), P(sse), threads)
+    return sad, var, sse

@@ -144,3 +144,22 @@ def test_c5_bands_world1_three_streams(L):
     one = shard.sharded_frame(H, 0, 1, proc)
     torch.cuda.synchronize()
     np.testing.assert_array_equal(one.cpu().numpy(), whole.recon.cpu().numpy())
+
+
+def test_pixel_1080p_7refs_all_jobs(L):
+    """bench.py --workload pixel: aom_sad16x16x4d + aom_variance16x16 of every
+    16x16 block x 7 refs at the seeded candidates, against orc_pixel_batch."""
+    import torch
+    import lavish_dsp.pixel as P
+    b = _bench()
+    src, refs, st, jobs = b.pixel_setup(1920, 1080, 7, 160, 1234)
+    tsrc = torch.from_numpy(src).cuda()
+    trefs = torch.from_numpy(refs.reshape(-1, st)).cuda()
+    tj = P.jobs_tensor(jobs, "cuda")
+    sad = P.sad_batch(tsrc, trefs, 16, 16, tj, nrefs=4).cpu().numpy()
+    vb = P.variance_batch(tsrc, trefs, 16, 16, tj, kind=0)
+    esad, evar, esse = O.pixel_batch(src.reshape(-1), st, refs.reshape(-1), st, 16, 16, jobs,
+                                     threads=THREADS)
+    np.testing.assert_array_equal(sad, esad)
+    np.testing.assert_array_equal(vb["var"].cpu().numpy(), evar)
+    np.testing.assert_array_equal(vb["sse"].cpu().numpy(), esse)
