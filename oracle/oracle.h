@@ -408,6 +408,18 @@ void orc_pixel_batch(const uint8_t *src, int ss, const uint8_t *ref, int rs, int
                      const void *jobs, long njobs, uint32_t *sad, uint32_t *var, uint32_t *sse,
                      int threads);
 
+/* oracle_warp.c: av1_get_shear_params (out: alpha, beta, gamma, delta;
+ * returns validity) and av1_warp_affine_c / av1_highbd_warp_affine_c */
+typedef struct {
+  int do_average, round_0, round_1, is_compound, use_dist_wtd_comp_avg, fwd_offset, bck_offset;
+} OrcConvParams;
+int orc_get_shear_params(const int32_t mat[6], int16_t out[4]);
+void orc_warp_affine(const int32_t mat[6], const void *ref, int width, int height, int stride,
+                     void *pred, int p_col, int p_row, int p_width, int p_height, int p_stride,
+                     int ss_x, int ss_y, int bd, int hbd, const OrcConvParams *cp,
+                     uint16_t *conv_dst, int dst_stride, int alpha, int beta, int gamma,
+                     int delta);
+
 #ifdef __cplusplus
 }
 #endif

@@ -892,3 +892,34 @@ def pixel_batch(src, ss, ref, rs, w, h, jobs, threads=1):
     jobs = np.ascontiguousarray(jobs)
     fn(P(src), ss, P(ref), rs, w, h, P(jobs), n, P(sad), P(var), P(sse), threads)
     return sad, var, sse
+
+
+class OrcConvParams(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_int) for n in ("do_average", "round_0", "round_1", "is_compound",
+                                             "use_dist_wtd_comp_avg", "fwd_offset", "bck_offset")]
+
+
+def get_shear_params(mat):
+    """orc_get_shear_params -> (valid, (alpha, beta, gamma, delta))."""
+    fn = lib().orc_get_shear_params
+    fn.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+    fn.restype = ctypes.c_int
+    m = np.ascontiguousarray(mat[:6], np.int32)
+    out = np.zeros(4, np.int16)
+    ok = fn(P(m), P(out))
+    return ok, tuple(int(v) for v in out)
+
+
+def warp_affine(mat, ref, width, height, stride, pred, p_col, p_row, p_width, p_height,
+                p_stride, ss_x, ss_y, bd, hbd, cp, conv_dst, dst_stride, params):
+    """orc_warp_affine in place on pred (u8 / u16) and conv_dst (u16 or None);
+    cp: dict of OrcConvParams fields; params: (alpha, beta, gamma, delta)."""
+    fn = lib().orc_warp_affine
+    fn.argtypes = [ctypes.c_void_p, ctypes.c_void_p] + [ctypes.c_int] * 3 + [ctypes.c_void_p] + \
+        [ctypes.c_int] * 9 + [ctypes.c_void_p, ctypes.c_void_p] + [ctypes.c_int] * 5
+    fn.restype = None
+    m = np.ascontiguousarray(mat[:6], np.int32)
+    c = OrcConvParams(**cp)
+    fn(P(m), P(ref), width, height, stride, P(pred), p_col, p_row, p_width, p_height, p_stride,
+       ss_x, ss_y, bd, hbd, ctypes.byref(c), P(conv_dst) if conv_dst is not None else None,
+       dst_stride, *params)

@@ -1221,9 +1221,137 @@ def gen_trellis(txfm_fix):
     np.savez_compressed(os.path.join(HERE, "fix_trellis.npz"), **out)
 
 
+# ----------------------------------------------------------------------------
+# affine warp (av1/common/warped_motion.c)
+# ----------------------------------------------------------------------------
+WARP_SHAPES = [(4, 4), (8, 8), (16, 8), (4, 16), (32, 32), (12, 20)]
+QUANT_DIST = [(9, 7), (11, 5), (12, 4), (13, 3)]  # quant_dist_lookup_table (common_data.h:421)
+
+
+def random_warped_param(rnd, bits):
+    """random_warped_param (test/warp_filter_test_util.cc:22-30)."""
+    if (rnd.rand8() & 7) == 0:
+        return 0
+    v = 1 + (rnd.rand16() & ((1 << bits) - 1))
+    return -v if rnd.rand8() & 1 else v
+
+
+def warped_model(rnd):
+    """generate_warped_model (test/warp_filter_test_util.cc:32-98) with every
+    is_*_zero flag 0: (mat[6], (alpha, beta, gamma, delta))."""
+    def rps(v, n):  # ROUND_POWER_OF_TWO_SIGNED
+        return -((-v + ((1 << n) >> 1)) >> n) if v < 0 else (v + ((1 << n) >> 1)) >> n
+
+    def cl16(v):
+        return max(-32768, min(32767, v))
+
+    def cdiv(a, b):  # C integer division (truncation)
+        q = abs(a) // abs(b)
+        return q if (a >= 0) == (b > 0) else -q
+    while True:
+        r8 = rnd.rand8() & 3
+        m = [random_warped_param(rnd, 22), random_warped_param(rnd, 22),
+             random_warped_param(rnd, 13) + (1 << 16), random_warped_param(rnd, 13), 0, 0]
+        if r8 == 2:
+            m[4], m[5] = -m[3], m[2]
+        else:
+            m[4] = random_warped_param(rnd, 13)
+            m[5] = random_warped_param(rnd, 13) + (1 << 16)
+        alpha = cl16(m[2] - (1 << 16))
+        beta = cl16(m[3])
+        gamma = cl16(cdiv(m[4] * (1 << 16), m[2]))
+        delta = cl16(m[5] - cdiv(m[3] * m[4] + m[2] // 2, m[2]) - (1 << 16))
+        if 4 * abs(alpha) + 7 * abs(beta) >= (1 << 16) or 4 * abs(gamma) + 4 * abs(delta) >= (1 << 16):
+            continue
+        return m, tuple(rps(v, 6) * 64 for v in (alpha, beta, gamma, delta))
+
+
+def gen_warp():
+    """av1_warp_affine_c / av1_highbd_warp_affine_c (warped_motion.c:264-388,
+    538-666) for bd 8 / 10 / 12, subsampling 0 / 1, the shapes of WARP_SHAPES,
+    and the four conv-param forms the reference's AV1WarpFilterTest drives
+    (test/warp_filter_test_util.cc:177-260): single prediction
+    (get_conv_params), compound first pass (no_round, do_average 0: the
+    CONV_BUF_TYPE output), compound average and distance-weighted average
+    (do_average 1 over that buffer); plus av1_get_shear_params (:218-247) of
+    every model."""
+    tu = C.TU(REF, ["aom/aom_integer.h", "aom_ports/mem.h", "aom_dsp/aom_dsp_common.h",
+                    "av1/common/enums.h", "av1/common/mv.h", "av1/common/convolve.h",
+                    "av1/common/warped_motion.h", "av1/common/warped_motion.c"],
+              C.reference_defines(REF))
+    check_errors(tu, ["av1_warp_affine_c", "av1_highbd_warp_affine_c", "av1_get_shear_params"])
+    rnd = ACMRandom(0xbaba + 11)
+    W, H, RS = 64, 48, 69           # reference plane (the function clamps to it)
+    PS = DS = 40                    # pred / conv-buffer strides
+    rows, refs, preds_in, preds, dsts_in, dsts, shear = [], [], [], [], [], [], []
+    for bd in (8, 10, 12):
+        hb = bd > 8
+        et = "uint16_t" if hb else "uint8_t"
+        for ci, (pw, ph) in enumerate(WARP_SHAPES):
+            for ssx, ssy in ((0, 0), (1, 1), (1, 0)):
+                t0 = time.time()
+                ref = np.array(_pix(rnd, H * RS, bd)).reshape(H, RS)
+                rp = tu.buffer(et, ref.reshape(-1).tolist())
+                mat, prm = warped_model(rnd)
+                # av1_get_shear_params on the same matrix
+                wm = tu.struct_obj("WarpedMotionParams")
+                wmat = _get(wm.buf[0], "wmmat")
+                for i in range(6):
+                    wmat[i] = mat[i]
+                ok = tu.func("av1_get_shear_params")(wm)
+                shear.append([ok] + mat + [_get(wm.buf[0], k) for k in ("alpha", "beta", "gamma",
+                                                                        "delta")])
+                p_col, p_row = 8 + (rnd.rand8() & 15), 8 + (rnd.rand8() & 15)
+                dst = [rnd.rand16() & ((1 << (bd + 4)) - 1) for _ in range(ph * DS)]
+                pin = _pix(rnd, ph * PS, bd)
+                dbuf = tu.buffer("CONV_BUF_TYPE", dst)
+                for mode in range(4):  # single, compound first pass, average, dist-wtd
+                    cp = tu.struct_obj("ConvolveParams")
+                    intbuf = bd + 7 - 3 + 2
+                    r0 = 3 + (intbuf - 16 if intbuf > 16 else 0)
+                    comp = int(mode > 0)
+                    r1 = 7 if comp else 14 - r0
+                    jj = rnd.generate(4)
+                    ii = rnd.generate(2)
+                    fwd, bck = (QUANT_DIST[jj][ii], QUANT_DIST[jj][1 - ii]) if mode == 3 else (0, 0)
+                    _set(cp.buf[0], do_average=int(mode >= 2), dst=dbuf if comp else
+                         C.Pointer(None, 0, tu.ctype("CONV_BUF_TYPE")), dst_stride=DS,
+                         round_0=r0, round_1=r1, plane=0, is_compound=comp,
+                         use_dist_wtd_comp_avg=int(mode == 3), fwd_offset=fwd, bck_offset=bck)
+                    pbuf = tu.buffer(et, pin)
+                    d_in = list(dbuf.buf)
+                    a = prm
+                    if hb:
+                        tu.func("av1_highbd_warp_affine_c")(
+                            tu.buffer("int32_t", mat), rp, W, H, RS, pbuf, p_col, p_row, pw, ph,
+                            PS, ssx, ssy, bd, cp, *a)
+                    else:
+                        tu.func("av1_warp_affine_c")(
+                            tu.buffer("int32_t", mat), rp, W, H, RS, pbuf, p_col, p_row, pw, ph,
+                            PS, ssx, ssy, cp, *a)
+                    rows.append([bd, pw, ph, ssx, ssy, p_col, p_row, mode, r0, r1, fwd, bck]
+                                + mat + list(prm) + [len(refs)])
+                    preds_in.append(np.array(pin, np.uint16))
+                    preds.append(np.array(pbuf.buf, np.uint16))
+                    dsts_in.append(np.array(d_in, np.uint16))
+                    dsts.append(np.array(dbuf.buf, np.uint16))
+                refs.append(ref.astype(np.uint16))
+                print("  warp bd %d %dx%d ss %d%d %.1fs" % (bd, pw, ph, ssx, ssy, time.time() - t0))
+    pad = lambda lst, n: np.stack([np.pad(a, (0, n - a.size)) for a in lst])
+    out = {"rows": np.array(rows, np.int64), "refs": np.stack(refs),
+           "pred_in": pad(preds_in, 32 * PS), "pred": pad(preds, 32 * PS),
+           "dst_in": pad(dsts_in, 32 * DS), "dst": pad(dsts, 32 * DS),
+           "shear": np.array(shear, np.int64), "geom": np.array([W, H, RS, PS, DS], np.int64),
+           "row_fields": np.array(["bd", "p_width", "p_height", "ss_x", "ss_y", "p_col", "p_row",
+                                   "mode", "round_0", "round_1", "fwd_offset", "bck_offset",
+                                   "m0", "m1", "m2", "m3", "m4", "m5", "alpha", "beta", "gamma",
+                                   "delta", "ref_index"])}
+    np.savez_compressed(os.path.join(HERE, "fix_warp.npz"), **out)
+
+
 def main(argv):
     sections = argv or ["txfm", "qparams", "quant", "inv", "pixel", "wht", "nmv", "mcomp",
-                        "subpel", "tpl", "qfacade", "costcoeffs", "trellis"]
+                        "subpel", "tpl", "qfacade", "costcoeffs", "trellis", "warp"]
     t0 = time.time()
     ttx = None
     if "txfm" in sections or "inv" in sections or "wht" in sections:
@@ -1260,6 +1388,8 @@ def main(argv):
         gen_costcoeffs()
     if "trellis" in sections:
         gen_trellis(dict(np.load(os.path.join(HERE, "fix_txfm.npz"))))
+    if "warp" in sections:
+        gen_warp()
     print("done in %.0fs" % (time.time() - t0))
 
 

@@ -84,6 +84,22 @@ def test_qlookup_header_matches_reference():
         assert [int(v) for v in re.findall(r"-?\d+", body)] == TABLES[key]
 
 
+def test_warp_tables_match_reference():
+    """kWarpedFilter / kDivLut of the product's and the oracle's warp_tables.h
+    against av1_warped_filter / div_lut parsed from the reference
+    (av1/common/warped_motion.c:29-166, tests/golden/ref_tables.json)."""
+    for path in (os.path.join(ROOT, "aom-av1-lavish_amd", "csrc", "warp_tables.h"),
+                 os.path.join(ROOT, "oracle", "warp_tables.h")):
+        src = open(path).read()
+        body = src[src.index("kWarpedFilter[193][8]"):]
+        body = body[body.index("{") + 1:body.index("};")]
+        vals = [int(v) for v in re.findall(r"-?\d+", body)]
+        assert vals == [v for row in TABLES["warped_filter"] for v in row]
+        body = src[src.index("kDivLut[257]"):]
+        body = body[body.index("{") + 1:body.index("};")]
+        assert [int(v) for v in re.findall(r"-?\d+", body)] == TABLES["div_lut"]
+
+
 def test_product_does_not_reference_oracle():
     """The product tree must not include, link or load anything in oracle/."""
     pk = os.path.join(ROOT, "aom-av1-lavish_amd")

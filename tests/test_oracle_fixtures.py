@@ -361,3 +361,45 @@ def test_optimize_b_matches_reference():
         changed += int((qc != F["qcoeff_in"][i][:n]).any())
         skipped += int(g("eob") == 0 and g("eob_in") > 0)
     assert changed > 100 and skipped > 10
+
+
+def _warp_case(F, r, J):
+    """Inputs of one fix_warp row as the oracle's arguments."""
+    g = lambda k: int(r[J[k]])
+    W, H, RS, PS, DS = (int(v) for v in F["geom"])
+    bd = g("bd")
+    hb = bd > 8
+    ref = F["refs"][g("ref_index")].astype(np.uint16 if hb else np.uint8)
+    mat = [g("m%d" % i) for i in range(6)]
+    cp = dict(do_average=int(g("mode") >= 2), round_0=g("round_0"), round_1=g("round_1"),
+              is_compound=int(g("mode") > 0), use_dist_wtd_comp_avg=int(g("mode") == 3),
+              fwd_offset=g("fwd_offset"), bck_offset=g("bck_offset"))
+    prm = tuple(g(k) for k in ("alpha", "beta", "gamma", "delta"))
+    return g, W, H, RS, PS, DS, bd, hb, ref, mat, cp, prm
+
+
+def test_warp_affine_matches_reference():
+    """orc_warp_affine against av1_warp_affine_c / av1_highbd_warp_affine_c
+    executed from the reference (tests/golden/fix_warp.npz): the prediction
+    and the compound buffer of every row (bd 8/10/12, subsampling, cropped
+    shapes, single / compound / average / distance-weighted)."""
+    F = _load("fix_warp.npz")
+    J = {n: i for i, n in enumerate(F["row_fields"])}
+    changed = 0
+    for k, r in enumerate(F["rows"]):
+        g, W, H, RS, PS, DS, bd, hb, ref, mat, cp, prm = _warp_case(F, r, J)
+        pred = F["pred_in"][k].astype(np.uint16 if hb else np.uint8).copy()
+        dst = F["dst_in"][k].copy()
+        O.warp_affine(mat, ref, W, H, RS, pred, g("p_col"), g("p_row"), g("p_width"),
+                      g("p_height"), PS, g("ss_x"), g("ss_y"), bd, int(hb), cp, dst, DS, prm)
+        np.testing.assert_array_equal(pred.astype(np.uint16), F["pred"][k], err_msg=str(k))
+        np.testing.assert_array_equal(dst, F["dst"][k], err_msg=str(k))
+        changed += int((F["pred"][k] != F["pred_in"][k]).any() or (F["dst"][k] != F["dst_in"][k]).any())
+    assert changed == len(F["rows"])
+
+
+def test_get_shear_params_matches_reference():
+    F = _load("fix_warp.npz")
+    for row in F["shear"]:
+        ok, prm = O.get_shear_params(row[1:7])
+        assert (ok,) + prm == tuple(int(v) for v in (row[0], *row[7:11])), row
