@@ -55,7 +55,7 @@ def parse():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--workload", choices=("rdo", "c2", "c3", "c3sub", "c4", "c4px", "c5", "inter",
-                                           "tpl", "rate", "pixel"),
+                                           "tpl", "rate", "pixel", "warp"),
                     default="rdo")
     ap.add_argument("--rdmult", type=int, default=2000)
     ap.add_argument("--width", type=int, default=1920)
@@ -666,6 +666,170 @@ def main_pixel(args):
         dist.destroy_process_group()
 
 
+
+def warp_setup(W, H, nrefs, seed):
+    """Warp workload: nrefs 8-bit references (the seeded motion planes without
+    their border: the warp clamps to the plane) and one LavishWarpJob per
+    16x16 block x reference: a seeded valid affine model (AFFINE or ROTZOOM,
+    the reference test's parameter ranges) whose projection of the block
+    centre lands within +-16 px of the block, and its av1_get_shear_params."""
+    import lavish_dsp.synth as synth
+    import lavish_dsp.warp as Wp
+    border = 160
+    _, refs = synth.motion_planes(W, H, nrefs, border, seed=seed)
+    refs = np.ascontiguousarray(refs[:, border:border + H, border:border + W])
+    rng = np.random.default_rng(seed)
+    nbx, nby = W // C3_BLOCK, H // C3_BLOCK
+    jobs = np.zeros(nrefs * nbx * nby, Wp.JOB_DTYPE)
+    n = 0
+    for k in range(nrefs):
+        for by in range(nby):
+            for bx in range(nbx):
+                while True:
+                    m = [0, 0, (1 << 16) + int(rng.integers(-3000, 3001)),
+                         int(rng.integers(-3000, 3001)), 0, 0]
+                    if rng.integers(0, 3) == 0:
+                        m[4], m[5] = -m[3], m[2]
+                    else:
+                        m[4] = int(rng.integers(-3000, 3001))
+                        m[5] = (1 << 16) + int(rng.integers(-3000, 3001))
+                    cx, cy = bx * C3_BLOCK + 8, by * C3_BLOCK + 8
+                    dx, dy = rng.integers(-16, 17, 2)
+                    m[0] = int(((cx + dx) << 16) - (m[2] * cx + m[3] * cy))
+                    m[1] = int(((cy + dy) << 16) - (m[4] * cx + m[5] * cy))
+                    ok, prm = Wp.get_shear_params(m)
+                    if ok:
+                        break
+                j = jobs[n]
+                j["mat"] = m
+                j["alpha"], j["beta"], j["gamma"], j["delta"] = prm
+                j["p_col"], j["p_row"] = bx * C3_BLOCK, by * C3_BLOCK
+                j["p_width"] = j["p_height"] = C3_BLOCK
+                j["ref_off"] = k * W * H
+                j["pred_off"] = k * W * H + by * C3_BLOCK * W + bx * C3_BLOCK
+                n += 1
+    return refs, jobs
+
+
+def warp_bytes(njobs, bw=16, bh=16):
+    """Algorithmic bytes of one step: per block the prediction written (w*h)
+    and the reference samples it covers read once (w*h; the 15 x 15 windows
+    of neighbouring 8x8 units overlap and are L2 hits), plus the 72 B job."""
+    return njobs * (2 * bw * bh + 72)
+
+
+def cpu_baseline_warp(args):
+    """orc_warp_batch (the oracle's av1_warp_affine_c restatement) on a
+    1920x256 strip of the same workload on all host cores, ~cpu_seconds."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import _oracle as O
+    W, Hs = args.width, 256
+    refs, jobs = warp_setup(W, Hs, args.refs, 1234)
+    pred = np.zeros_like(refs)
+    threads = host_cores()
+    sb = sb64_count(W, Hs)
+    cp = dict(do_average=0, round_0=3, round_1=11, is_compound=0, use_dist_wtd_comp_avg=0,
+              fwd_offset=0, bck_offset=0)
+    passes = 0
+    t0 = time.perf_counter()
+    while True:
+        O.warp_batch(refs.reshape(-1, W), W, Hs, W, pred.reshape(-1, W), W, jobs, cp,
+                     threads=threads)
+        passes += 1
+        dt = time.perf_counter() - t0
+        if dt >= args.cpu_seconds:
+            break
+    return {"value": round(passes * sb / dt, 2), "unit": "SB64/s", "cores": threads,
+            "kind": "port",
+            "sample": "%d passes of a %dx%d strip (%d SB64, %d blocks) through the warp step, "
+                      "oracle C restatement (-O3, %d pthreads), %.1f s"
+                      % (passes, W, Hs, sb, len(jobs), threads, dt)}
+
+
+def main_warp(args):
+    """Affine warp prediction (av1_warp_affine_c, single prediction, 8-bit)
+    of every 16x16 block of a 1080p frame against every reference with its
+    own local model (lavish_warp_affine_batch), one frame per step."""
+    import torch
+    import torch.distributed as dist
+    import lavish_dsp as L
+    import lavish_dsp.warp as Wp
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local_rank)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    W, H = args.width, args.height
+    refs, jobs_np = warp_setup(W, H, args.refs, 1234 + rank)
+    tref = torch.from_numpy(refs.reshape(-1, W)).cuda()
+    pred = torch.empty_like(tref)
+    tjobs = torch.from_numpy(jobs_np.view(np.uint8)).cuda()
+    cp = Wp.conv_params(3, 11)
+    stream = torch.cuda.current_stream()
+
+    def step():
+        Wp.warp_affine_batch(tref, W, H, W, pred, W, tjobs, len(jobs_np), cp, 8, stream=stream)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+          for _ in range(args.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        ev[k][0].record(stream)
+        step()
+        ev[k][1].record(stream)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    status = L.status()
+    if status[0] != 0:
+        raise RuntimeError("HIP error during bench: %s" % (status,))
+    k_ms = sum(a.elapsed_time(b) for a, b in ev) / args.steps
+    nbytes = warp_bytes(len(jobs_np))
+    sb = sb64_count(W, H)
+    line = {
+        "metric": METRIC,
+        "value": round(world * sb * args.steps / elapsed, 2),
+        "unit": "SB64/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u8",
+        "data": "synthetic (seeded 1080p content, lavish_dsp/synth.py; seeded affine models)",
+        "config": {
+            "workload": "warp: %dx%d 8-bit; av1_warp_affine (single prediction) of every %dx%d "
+                        "block x %d refs with its own local affine model, %d blocks; "
+                        "%d SB64/frame" % (W, H, C3_BLOCK, C3_BLOCK, args.refs, len(jobs_np), sb),
+            "parallelism": "frame-per-rank x%d" % world,
+        },
+        "roofline": {"bound": "hbm", "kernel": "warp_kernel<u8> (lavish_warp_affine_batch)",
+                     "achieved": round(nbytes / (k_ms * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "traffic": None, "avg_launch_ms": round(k_ms, 4),
+                     "algorithmic_bytes_per_launch": nbytes},
+    }
+    line["roofline"]["frac"] = round(line["roofline"]["achieved"] / HBM_PEAK_GBS, 4)
+    if rank == 0 and world == 1 and not args.no_cpu:
+        line["cpu_baseline"] = cpu_baseline_warp(args)
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
 TPL_BORDER = 288  # AOM_BORDER_IN_PIXELS: the predictor's clamp reads stay inside
 
 
@@ -1006,6 +1170,8 @@ def main():
         return main_inter(args)
     if args.workload == "pixel":
         return main_pixel(args)
+    if args.workload == "warp":
+        return main_warp(args)
     if args.workload == "tpl":
         return main_tpl(args)
     if args.workload == "rate":

@@ -1066,6 +1066,49 @@ void aom_convolve_copy_hip(const uint8_t *src, ptrdiff_t src_stride, uint8_t *ds
 void aom_highbd_convolve_copy_hip(const uint16_t *src, ptrdiff_t src_stride,
                                   uint16_t *dst, ptrdiff_t dst_stride, int w, int h);
 
+
+/* ---- affine warp --------------------------------
+ * Replaces av1_warp_affine_c (av1/common/warped_motion.c:538-666) and
+ * av1_highbd_warp_affine_c (:264-388) for a batch of prediction blocks of
+ * one reference plane.  A job is one block: its warp matrix (wmmat[0..5])
+ * and shear parameters (av1_get_shear_params), the block position p_col /
+ * p_row / p_width / p_height in the predicted plane, the element offset of
+ * the reference plane origin (ref_off: several planes may be stacked) and of
+ * the block's top-left in pred / conv_dst.  conv_params: round_0, round_1,
+ * is_compound, do_average, use_dist_wtd_comp_avg, fwd_offset, bck_offset as
+ * the reference reads them (its dst / dst_stride are replaced by conv_dst /
+ * dst_stride).  Device pointers; asynchronous on `stream`.  highbd: u16
+ * samples (bit_depth 8/10/12), else u8 (bit_depth 8).  Returns 0, or < 0 on
+ * rejected arguments. */
+typedef struct LavishWarpJob {
+  int32_t mat[6];
+  int16_t alpha, beta, gamma, delta;
+  int32_t p_col, p_row, p_width, p_height;
+  int64_t ref_off;
+  int64_t pred_off;
+  int64_t dst_off;
+} LavishWarpJob;
+int lavish_warp_affine_batch(const void *ref, int width, int height, int stride, void *pred,
+                             int p_stride, uint16_t *conv_dst, int dst_stride,
+                             const LavishWarpJob *jobs, int njobs, int subsampling_x,
+                             int subsampling_y, int bit_depth, int highbd,
+                             const LavishConvolveParams *conv_params, void *stream);
+/* av1_get_shear_params (warped_motion.c:218-247) on a host matrix: out =
+ * alpha, beta, gamma, delta; returns 1 when the model is usable by the warp
+ * filter, else 0. */
+int lavish_get_shear_params(const int32_t *mat, int16_t *out);
+/* av1/common/av1_rtcd_defs.pl:548,544 (per-call shims, host buffers) */
+void av1_warp_affine_hip(const int32_t *mat, const uint8_t *ref, int width, int height,
+                         int stride, uint8_t *pred, int p_col, int p_row, int p_width,
+                         int p_height, int p_stride, int subsampling_x, int subsampling_y,
+                         LavishConvolveParams *conv_params, int16_t alpha, int16_t beta,
+                         int16_t gamma, int16_t delta);
+void av1_highbd_warp_affine_hip(const int32_t *mat, const uint16_t *ref, int width,
+                                int height, int stride, uint16_t *pred, int p_col, int p_row,
+                                int p_width, int p_height, int p_stride, int subsampling_x,
+                                int subsampling_y, int bd, LavishConvolveParams *conv_params,
+                                int16_t alpha, int16_t beta, int16_t gamma, int16_t delta);
+
 #ifdef __cplusplus
 }
 #endif

@@ -419,6 +419,9 @@ void orc_warp_affine(const int32_t mat[6], const void *ref, int width, int heigh
                      int ss_x, int ss_y, int bd, int hbd, const OrcConvParams *cp,
                      uint16_t *conv_dst, int dst_stride, int alpha, int beta, int gamma,
                      int delta);
+void orc_warp_batch(const void *ref, int width, int height, int stride, void *pred,
+                    int p_stride, uint16_t *dst, int dst_stride, const void *jobs, long njobs,
+                    int ss_x, int ss_y, int bd, int hbd, const OrcConvParams *cp, int threads);
 
 #ifdef __cplusplus
 }

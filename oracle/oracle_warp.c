@@ -139,3 +139,70 @@ void orc_warp_affine(const int32_t mat[6], const void *ref, int width, int heigh
     }
   }
 }
+
+/* Batch driver for the `warp` bench workload's CPU baseline: jobs in the
+ * LavishWarpJob layout (one block each), one conv form, over pthreads. */
+#include <pthread.h>
+
+typedef struct {
+  int32_t mat[6];
+  int16_t alpha, beta, gamma, delta;
+  int32_t p_col, p_row, p_width, p_height;
+  int64_t ref_off, pred_off, dst_off;
+} WarpJob;
+
+typedef struct {
+  const void *ref;
+  void *pred;
+  uint16_t *dst;
+  const WarpJob *jobs;
+  const OrcConvParams *cp;
+  int width, height, stride, p_stride, dst_stride, ss_x, ss_y, bd, hbd;
+  long lo, hi;
+} WarpArg;
+
+static void *warp_worker(void *p) {
+  const WarpArg *a = (const WarpArg *)p;
+  const int es = a->hbd ? 2 : 1;
+  for (long j = a->lo; j < a->hi; ++j) {
+    const WarpJob *jb = &a->jobs[j];
+    orc_warp_affine(jb->mat, (const char *)a->ref + jb->ref_off * es, a->width, a->height,
+                    a->stride, (char *)a->pred + jb->pred_off * es, jb->p_col, jb->p_row,
+                    jb->p_width, jb->p_height, a->p_stride, a->ss_x, a->ss_y, a->bd, a->hbd,
+                    a->cp, a->dst ? a->dst + jb->dst_off : NULL, a->dst_stride, jb->alpha,
+                    jb->beta, jb->gamma, jb->delta);
+  }
+  return NULL;
+}
+
+void orc_warp_batch(const void *ref, int width, int height, int stride, void *pred,
+                    int p_stride, uint16_t *dst, int dst_stride, const void *jobs, long njobs,
+                    int ss_x, int ss_y, int bd, int hbd, const OrcConvParams *cp, int threads) {
+  if (threads < 1) threads = 1;
+  if (threads > 256) threads = 256;
+  pthread_t tid[256];
+  WarpArg args[256];
+  for (int t = 0; t < threads; ++t) {
+    WarpArg *a = &args[t];
+    a->ref = ref;
+    a->pred = pred;
+    a->dst = dst;
+    a->jobs = (const WarpJob *)jobs;
+    a->cp = cp;
+    a->width = width;
+    a->height = height;
+    a->stride = stride;
+    a->p_stride = p_stride;
+    a->dst_stride = dst_stride;
+    a->ss_x = ss_x;
+    a->ss_y = ss_y;
+    a->bd = bd;
+    a->hbd = hbd;
+    a->lo = njobs * t / threads;
+    a->hi = njobs * (t + 1) / threads;
+    if (threads > 1) pthread_create(&tid[t], NULL, warp_worker, a);
+    else warp_worker(a);
+  }
+  if (threads > 1)
+    for (int t = 0; t < threads; ++t) pthread_join(tid[t], NULL);
+}

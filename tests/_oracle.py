@@ -923,3 +923,19 @@ def warp_affine(mat, ref, width, height, stride, pred, p_col, p_row, p_width, p_
     fn(P(m), P(ref), width, height, stride, P(pred), p_col, p_row, p_width, p_height, p_stride,
        ss_x, ss_y, bd, hbd, ctypes.byref(c), P(conv_dst) if conv_dst is not None else None,
        dst_stride, *params)
+
+
+def warp_batch(ref, width, height, stride, pred, p_stride, jobs, cp, bd=8, dst=None,
+               dst_stride=0, ss_x=0, ss_y=0, threads=1):
+    """orc_warp_batch in place on pred / dst (jobs: lavish_dsp.warp.JOB_DTYPE)."""
+    fn = lib().orc_warp_batch
+    fn.argtypes = [ctypes.c_void_p] + [ctypes.c_int] * 3 + [ctypes.c_void_p, ctypes.c_int,
+                                                            ctypes.c_void_p, ctypes.c_int,
+                                                            ctypes.c_void_p, ctypes.c_long] + \
+        [ctypes.c_int] * 4 + [ctypes.c_void_p, ctypes.c_int]
+    fn.restype = None
+    c = OrcConvParams(**cp)
+    jobs = np.ascontiguousarray(jobs)
+    fn(P(ref), width, height, stride, P(pred), p_stride, P(dst) if dst is not None else None,
+       dst_stride, P(jobs), len(jobs), ss_x, ss_y, bd, int(ref.dtype == np.uint16),
+       ctypes.byref(c), threads)

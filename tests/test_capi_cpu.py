@@ -130,3 +130,21 @@ def test_quant_params_match_reference_execution(bd, sharp):
             np.testing.assert_array_equal(d["zbin"], row("y_zbin"))
             np.testing.assert_array_equal(d["quant_shift"], row("y_quant_shift"))
             np.testing.assert_array_equal(d["dequant"], row("y_dequant_QTX"))
+
+
+def test_shear_params_host_matches_reference():
+    """lavish_get_shear_params (host code of the product, no GPU) against
+    av1_get_shear_params executed from the reference (fix_warp.npz)."""
+    lib = ctypes.CDLL(os.path.join(ROOT, "aom-av1-lavish_amd", "liblavish_hip.so"))
+    lib.lavish_get_shear_params.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+    lib.lavish_get_shear_params.restype = ctypes.c_int
+    F = np.load(os.path.join(ROOT, "tests", "golden", "fix_warp.npz"))
+    n_ok = 0
+    for row in F["shear"]:
+        m = np.ascontiguousarray(row[1:7], np.int32)
+        out = np.zeros(4, np.int16)
+        ok = lib.lavish_get_shear_params(m.ctypes.data_as(ctypes.c_void_p),
+                                         out.ctypes.data_as(ctypes.c_void_p))
+        assert (ok,) + tuple(int(v) for v in out) == tuple(int(v) for v in (row[0], *row[7:11]))
+        n_ok += ok
+    assert n_ok > len(F["shear"]) // 2

@@ -163,3 +163,22 @@ def test_pixel_1080p_7refs_all_jobs(L):
     np.testing.assert_array_equal(sad, esad)
     np.testing.assert_array_equal(vb["var"].cpu().numpy(), evar)
     np.testing.assert_array_equal(vb["sse"].cpu().numpy(), esse)
+
+
+def test_warp_1080p_7refs_all_blocks(L):
+    """bench.py --workload warp: av1_warp_affine of every 16x16 block x 7 refs
+    with its own local model, against orc_warp_batch."""
+    import torch
+    import lavish_dsp.warp as Wp
+    b = _bench()
+    W, H = 1920, 1080
+    refs, jobs = b.warp_setup(W, H, 7, 1234)
+    tref = torch.from_numpy(refs.reshape(-1, W)).cuda()
+    pred = torch.zeros_like(tref)
+    Wp.warp_affine_batch(tref, W, H, W, pred, W, torch.from_numpy(jobs.view(np.uint8)).cuda(),
+                         len(jobs), Wp.conv_params(3, 11), 8)
+    exp = np.zeros_like(refs)
+    O.warp_batch(refs.reshape(-1, W), W, H, W, exp.reshape(-1, W), W, jobs,
+                 dict(do_average=0, round_0=3, round_1=11, is_compound=0,
+                      use_dist_wtd_comp_avg=0, fwd_offset=0, bck_offset=0), threads=THREADS)
+    np.testing.assert_array_equal(pred.cpu().numpy(), exp.reshape(-1, W))
