@@ -419,6 +419,12 @@ void orc_warp_affine(const int32_t mat[6], const void *ref, int width, int heigh
                      int ss_x, int ss_y, int bd, int hbd, const OrcConvParams *cp,
                      uint16_t *conv_dst, int dst_stride, int alpha, int beta, int gamma,
                      int delta);
+/* oracle_compound.c: the av1_dist_wtd_convolve_* family (path 0 copy, 1 x,
+ * 2 y, 3 2d), lowbd / highbd */
+void orc_dist_wtd_convolve(int path, const void *src, int src_stride, void *dst, int dst_stride,
+                           int w, int h, const int16_t *fx, int tx, const int16_t *fy, int ty,
+                           const OrcConvParams *cp, uint16_t *conv, int conv_stride, int bd,
+                           int hbd);
 void orc_warp_batch(const void *ref, int width, int height, int stride, void *pred,
                     int p_stride, uint16_t *dst, int dst_stride, const void *jobs, long njobs,
                     int ss_x, int ss_y, int bd, int hbd, const OrcConvParams *cp, int threads);

@@ -939,3 +939,20 @@ def warp_batch(ref, width, height, stride, pred, p_stride, jobs, cp, bd=8, dst=N
     fn(P(ref), width, height, stride, P(pred), p_stride, P(dst) if dst is not None else None,
        dst_stride, P(jobs), len(jobs), ss_x, ss_y, bd, int(ref.dtype == np.uint16),
        ctypes.byref(c), threads)
+
+
+def dist_wtd_convolve(path, src, src_stride, dst, dst_stride, w, h, fx, fy, cp, conv,
+                      conv_stride, bd, hbd, src_off=0):
+    """orc_dist_wtd_convolve in place on dst / conv; src_off: element offset
+    of the block's integer position in the flat src array."""
+    fn = lib().orc_dist_wtd_convolve
+    fn.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p] + \
+        [ctypes.c_int] * 3 + [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_int,
+                              ctypes.c_void_p, ctypes.c_void_p] + [ctypes.c_int] * 3
+    fn.restype = None
+    fxa = np.ascontiguousarray(fx, np.int16)
+    fya = np.ascontiguousarray(fy, np.int16)
+    c = OrcConvParams(**cp)
+    base = src.ctypes.data + src_off * src.itemsize
+    fn(path, ctypes.c_void_p(base), src_stride, P(dst), dst_stride, w, h, P(fxa), len(fxa),
+       P(fya), len(fya), ctypes.byref(c), P(conv), conv_stride, bd, hbd)

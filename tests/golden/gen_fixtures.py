@@ -1349,9 +1349,95 @@ def gen_warp():
     np.savez_compressed(os.path.join(HERE, "fix_warp.npz"), **out)
 
 
+# ----------------------------------------------------------------------------
+# compound convolutions (av1/common/convolve.c)
+# ----------------------------------------------------------------------------
+def gen_compound():
+    """av1_dist_wtd_convolve_{2d_copy,x,y,2d}_c and their highbd forms
+    (av1/common/convolve.c:291-489,790-988) -- the four paths of
+    convolve_2d_facade_compound (:590-612) -- for bd 8 / 10 / 12, block sizes
+    4x4 .. 32x16, filters REGULAR / SMOOTH / SHARP / BILINEAR (the 4-tap
+    kernels for 4-wide / 4-high blocks, av1_get_interp_filter_params_with_
+    block_size), and the conv-param forms: compound first pass (do_average
+    0) and the plain / distance-weighted averages (do_average 1) over that
+    buffer (get_conv_params_no_round)."""
+    tu = C.TU(REF, ["aom/aom_integer.h", "aom_ports/mem.h", "aom_dsp/aom_dsp_common.h",
+                    "aom_dsp/aom_filter.h", "av1/common/enums.h", "av1/common/filter.h",
+                    "av1/common/convolve.h", "av1/common/convolve.c"],
+              C.reference_defines(REF))
+    names = ["av1_dist_wtd_convolve_2d_copy_c", "av1_dist_wtd_convolve_x_c",
+             "av1_dist_wtd_convolve_y_c", "av1_dist_wtd_convolve_2d_c",
+             "av1_highbd_dist_wtd_convolve_2d_copy_c", "av1_highbd_dist_wtd_convolve_x_c",
+             "av1_highbd_dist_wtd_convolve_y_c", "av1_highbd_dist_wtd_convolve_2d_c",
+             "av1_get_interp_filter_params_with_block_size"]
+    check_errors(tu, names)
+    rnd = ACMRandom(0xbaba + 12)
+    SS, DS, CS = 48, 40, 40  # src / dst / conv-buffer strides
+    rows, srcs, dsts, dsts_in, convs, convs_in = [], [], [], [], [], []
+    for bd in (8, 10, 12):
+        hb = bd > 8
+        et = "uint16_t" if hb else "uint8_t"
+        pre = "av1_highbd_" if hb else "av1_"
+        for (w, h) in ((4, 4), (8, 8), (16, 8), (4, 16), (32, 16), (8, 32)):
+            t0 = time.time()
+            for path in range(4):
+                for mode in range(3):  # first pass, average, dist-wtd average
+                    fxi, fyi = rnd.generate(4), rnd.generate(4)
+                    sx = 0 if path in (0, 2) else 1 + rnd.generate(15)
+                    sy = 0 if path in (0, 1) else 1 + rnd.generate(15)
+                    src = np.array(_pix(rnd, (h + 12) * SS, bd)).reshape(h + 12, SS)
+                    sp = tu.buffer(et, src.reshape(-1).tolist())
+                    blk = C.Pointer(sp.buf, 5 * SS + 5, sp.ty)  # room for the taps
+                    d_in = _pix(rnd, h * DS, bd)
+                    c_in = [rnd.rand16() & ((1 << (bd + 4)) - 1) for _ in range(h * CS)]
+                    dp = tu.buffer(et, d_in)
+                    cb = tu.buffer("CONV_BUF_TYPE", c_in)
+                    cp = tu.struct_obj("ConvolveParams")
+                    intbuf = bd + 7 - 3 + 2
+                    r0 = 3 + (intbuf - 16 if intbuf > 16 else 0)
+                    jj, ii = rnd.generate(4), rnd.generate(2)
+                    fwd, bck = (QUANT_DIST[jj][ii], QUANT_DIST[jj][1 - ii]) if mode == 2 else (0, 0)
+                    _set(cp.buf[0], do_average=int(mode > 0), dst=cb, dst_stride=CS, round_0=r0,
+                         round_1=7, plane=0, is_compound=1, use_dist_wtd_comp_avg=int(mode == 2),
+                         fwd_offset=fwd, bck_offset=bck)
+                    fpx = tu.func("av1_get_interp_filter_params_with_block_size")(fxi, w)
+                    fpy = tu.func("av1_get_interp_filter_params_with_block_size")(fyi, h)
+                    a = [blk, SS, dp, DS, w, h]
+                    if path == 0:
+                        a += [cp]
+                    elif path == 1:
+                        a += [fpx, sx, cp]
+                    elif path == 2:
+                        a += [fpy, sy, cp]
+                    else:
+                        a += [fpx, fpy, sx, sy, cp]
+                    if hb:
+                        a.append(bd)
+                    fn = ["dist_wtd_convolve_2d_copy_c", "dist_wtd_convolve_x_c",
+                          "dist_wtd_convolve_y_c", "dist_wtd_convolve_2d_c"][path]
+                    tu.func(pre + fn)(*a)
+                    rows.append([bd, w, h, path, mode, fxi, fyi, sx, sy, r0, 7, fwd, bck,
+                                 len(srcs)])
+                    srcs.append(src.astype(np.uint16))
+                    pad = lambda v, n: np.pad(np.array(v, np.uint16), (0, n - len(v)))
+                    dsts_in.append(pad(d_in, 32 * DS))
+                    dsts.append(pad(dp.buf, 32 * DS))
+                    convs_in.append(pad(c_in, 32 * CS))
+                    convs.append(pad(cb.buf, 32 * CS))
+            print("  compound bd %d %dx%d %.1fs" % (bd, w, h, time.time() - t0))
+    pad_src = lambda a: np.pad(a, ((0, 44 - a.shape[0]), (0, 0)))
+    out = {"rows": np.array(rows, np.int64), "src": np.stack([pad_src(a) for a in srcs]),
+           "dst_in": np.stack(dsts_in), "dst": np.stack(dsts), "conv_in": np.stack(convs_in),
+           "conv": np.stack(convs), "geom": np.array([SS, DS, CS, 5], np.int64),
+           "row_fields": np.array(["bd", "w", "h", "path", "mode", "filter_x", "filter_y",
+                                   "subpel_x", "subpel_y", "round_0", "round_1", "fwd_offset",
+                                   "bck_offset", "src_index"])}
+    np.savez_compressed(os.path.join(HERE, "fix_compound.npz"), **out)
+
+
 def main(argv):
     sections = argv or ["txfm", "qparams", "quant", "inv", "pixel", "wht", "nmv", "mcomp",
-                        "subpel", "tpl", "qfacade", "costcoeffs", "trellis", "warp"]
+                        "subpel", "tpl", "qfacade", "costcoeffs", "trellis", "warp", "compound"]
     t0 = time.time()
     ttx = None
     if "txfm" in sections or "inv" in sections or "wht" in sections:
@@ -1390,6 +1476,8 @@ def main(argv):
         gen_trellis(dict(np.load(os.path.join(HERE, "fix_txfm.npz"))))
     if "warp" in sections:
         gen_warp()
+    if "compound" in sections:
+        gen_compound()
     print("done in %.0fs" % (time.time() - t0))
 
 

@@ -403,3 +403,28 @@ def test_get_shear_params_matches_reference():
     for row in F["shear"]:
         ok, prm = O.get_shear_params(row[1:7])
         assert (ok,) + prm == tuple(int(v) for v in (row[0], *row[7:11])), row
+
+
+def test_dist_wtd_convolve_matches_reference():
+    """orc_dist_wtd_convolve against av1_dist_wtd_convolve_{2d_copy,x,y,2d}_c
+    and the highbd forms executed from the reference (fix_compound.npz): the
+    CONV_BUF and the averaged prediction of every row."""
+    F = _load("fix_compound.npz")
+    J = {n: i for i, n in enumerate(F["row_fields"])}
+    SS, DS, CS, org = (int(v) for v in F["geom"])
+    for k, r in enumerate(F["rows"]):
+        g = lambda n: int(r[J[n]])
+        bd, w, h = g("bd"), g("w"), g("h")
+        hb = bd > 8
+        src = np.ascontiguousarray(F["src"][g("src_index")].astype(np.uint16 if hb else np.uint8))
+        dst = F["dst_in"][k].astype(np.uint16 if hb else np.uint8).copy()
+        conv = F["conv_in"][k].copy()
+        fx = O.interp_kernel(g("filter_x"), w, g("subpel_x"))
+        fy = O.interp_kernel(g("filter_y"), h, g("subpel_y"))
+        cp = dict(do_average=int(g("mode") > 0), round_0=g("round_0"), round_1=g("round_1"),
+                  is_compound=1, use_dist_wtd_comp_avg=int(g("mode") == 2),
+                  fwd_offset=g("fwd_offset"), bck_offset=g("bck_offset"))
+        O.dist_wtd_convolve(g("path"), src, SS, dst, DS, w, h, fx, fy, cp, conv, CS, bd, int(hb),
+                            src_off=org * SS + org)
+        np.testing.assert_array_equal(conv, F["conv"][k], err_msg=str(k))
+        np.testing.assert_array_equal(dst.astype(np.uint16), F["dst"][k], err_msg=str(k))
