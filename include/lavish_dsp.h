@@ -1109,6 +1109,69 @@ void av1_highbd_warp_affine_hip(const int32_t *mat, const uint16_t *ref, int wid
                                 int subsampling_y, int bd, LavishConvolveParams *conv_params,
                                 int16_t alpha, int16_t beta, int16_t gamma, int16_t delta);
 
+
+/* ---- compound (CONV_BUF) convolutions -----------
+ * Replaces av1_dist_wtd_convolve_{2d_copy,x,y,2d}_c and the highbd forms
+ * (av1/common/convolve.c:291-489,790-988) for a batch of w x h blocks
+ * sharing the x / y filters (InterpFilterParams as the caller holds them:
+ * host filter_ptr, taps <= 12) and the conv params (round_0, round_1,
+ * do_average, use_dist_wtd_comp_avg, fwd_offset, bck_offset; its dst /
+ * dst_stride are replaced by conv_dst / conv_stride).  Per block: the source
+ * position (element offset of the block's integer position), the prediction
+ * and CONV_BUF offsets and the sub-pel phases (1/16 pel), which choose the
+ * path as convolve_2d_facade_compound does.  w, h <= 128.  Device pointers;
+ * asynchronous on `stream`. */
+typedef struct LavishCompoundJob {
+  int64_t src_off;
+  int64_t dst_off;
+  int64_t conv_off;
+  int32_t subpel_x_qn, subpel_y_qn;
+} LavishCompoundJob;
+int lavish_dist_wtd_convolve_batch(const void *src, int src_stride, void *dst, int dst_stride,
+                                   uint16_t *conv_dst, int conv_stride, int w, int h,
+                                   const LavishCompoundJob *jobs, int njobs,
+                                   const LavishInterpFilterParams *filter_params_x,
+                                   const LavishInterpFilterParams *filter_params_y,
+                                   const LavishConvolveParams *conv_params, int bit_depth,
+                                   int highbd, void *stream);
+/* av1/common/av1_rtcd_defs.pl:568-579 (per-call shims, host buffers) */
+void av1_dist_wtd_convolve_2d_hip(const uint8_t *src, int src_stride, uint8_t *dst,
+                                  int dst_stride, int w, int h,
+                                  const LavishInterpFilterParams *filter_params_x,
+                                  const LavishInterpFilterParams *filter_params_y,
+                                  const int subpel_x_qn, const int subpel_y_qn,
+                                  LavishConvolveParams *conv_params);
+void av1_dist_wtd_convolve_2d_copy_hip(const uint8_t *src, int src_stride, uint8_t *dst,
+                                       int dst_stride, int w, int h,
+                                       LavishConvolveParams *conv_params);
+void av1_dist_wtd_convolve_x_hip(const uint8_t *src, int src_stride, uint8_t *dst,
+                                 int dst_stride, int w, int h,
+                                 const LavishInterpFilterParams *filter_params_x,
+                                 const int subpel_x_qn, LavishConvolveParams *conv_params);
+void av1_dist_wtd_convolve_y_hip(const uint8_t *src, int src_stride, uint8_t *dst,
+                                 int dst_stride, int w, int h,
+                                 const LavishInterpFilterParams *filter_params_y,
+                                 const int subpel_y_qn, LavishConvolveParams *conv_params);
+void av1_highbd_dist_wtd_convolve_2d_hip(const uint16_t *src, int src_stride, uint16_t *dst,
+                                         int dst_stride, int w, int h,
+                                         const LavishInterpFilterParams *filter_params_x,
+                                         const LavishInterpFilterParams *filter_params_y,
+                                         const int subpel_x_qn, const int subpel_y_qn,
+                                         LavishConvolveParams *conv_params, int bd);
+void av1_highbd_dist_wtd_convolve_x_hip(const uint16_t *src, int src_stride, uint16_t *dst,
+                                        int dst_stride, int w, int h,
+                                        const LavishInterpFilterParams *filter_params_x,
+                                        const int subpel_x_qn,
+                                        LavishConvolveParams *conv_params, int bd);
+void av1_highbd_dist_wtd_convolve_y_hip(const uint16_t *src, int src_stride, uint16_t *dst,
+                                        int dst_stride, int w, int h,
+                                        const LavishInterpFilterParams *filter_params_y,
+                                        const int subpel_y_qn,
+                                        LavishConvolveParams *conv_params, int bd);
+void av1_highbd_dist_wtd_convolve_2d_copy_hip(const uint16_t *src, int src_stride,
+                                              uint16_t *dst, int dst_stride, int w, int h,
+                                              LavishConvolveParams *conv_params, int bd);
+
 #ifdef __cplusplus
 }
 #endif
