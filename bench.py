@@ -17,13 +17,13 @@ The default workload ("rdo") is the metric's "fwd_txfm+quant+SAD" loop:
       sadperbit / errorperbit of the qindex / rdmult, and the cost list the
       sub-pel search consumes (lavish_full_pixel_search_batch),
 
-by default back to back on the caller stream (C2 forks its per-size kernels
-over internal streams), so each leg's event-timed duration is its kernel
-duration (what rocprof reports).  The legs are independent (the residual is
-given): --overlap runs C3 on a second stream beside C2 -- C3 is bound by the
-vector-memory address path and latency, C2 by HBM writes -- which shortens
-the step by ~7 % while stretching each leg.  --workload c2 / c3 times one
-leg alone.
+by default side by side: the legs are independent (the residual is given),
+so C3 runs on a second stream beside C2 -- C3 is bound by the vector-memory
+address path, C2 by HBM writes -- which shortens the step ~10 % (measured
+0.967 -> 0.872 ms).  The per-kernel roofline and legs_ms come from a serial
+pass after the timed region (isolated legs); legs_overlapped_ms keeps the
+stretched spans of the timed region.  --serial times the legs back to back
+on one stream; --workload c2 / c3 times one leg alone.
 
 Multi-GPU: one process per GPU (torchrun), each rank processes its own frame
 (independent units, no data-path collective): weak scaling.  Timing: barrier +
@@ -55,7 +55,7 @@ def parse():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--workload", choices=("rdo", "c2", "c3", "c3sub", "c4", "c4px", "c5", "inter",
-                                           "tpl", "rate", "pixel", "warp"),
+                                           "tpl", "rate", "pixel", "warp", "compound"),
                     default="rdo")
     ap.add_argument("--rdmult", type=int, default=2000)
     ap.add_argument("--width", type=int, default=1920)
@@ -67,9 +67,10 @@ def parse():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-c4", action="store_true",
                     help="skip the c4 sub-object (4K 10-bit RDO step) of the default line")
-    ap.add_argument("--overlap", action="store_true",
-                    help="run the C3 leg on a second stream beside the C2 leg (default: C3 "
-                         "then C2 on one stream)")
+    ap.add_argument("--serial", action="store_true",
+                    help="run the C3 and C2 legs back to back on one stream (default: C3 on a "
+                         "second stream beside C2)")
+    ap.add_argument("--overlap", action="store_true", help=argparse.SUPPRESS)  # the default
     ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
     return ap.parse_args()
 
@@ -830,6 +831,176 @@ def main_warp(args):
     if world > 1:
         dist.destroy_process_group()
 
+
+def compound_setup(W, H, nrefs, seed):
+    """Compound workload: the 8-bit motion planes (no border kept: candidates
+    stay >= 8 px inside) and, per 16x16 block, a pair of references (k, k+1
+    mod nrefs for every k) with seeded integer + sub-pel motion (+-16 px,
+    1/16 pel): pass 1 jobs read ref k into the CONV_BUF, pass 2 jobs read
+    ref k+1 and average (distance-weighted) into the prediction."""
+    import lavish_dsp.compound as Cm
+    import lavish_dsp.synth as synth
+    border = 160
+    _, refs = synth.motion_planes(W, H, nrefs, border, seed=seed)
+    st = refs.shape[2]
+    rng = np.random.default_rng(seed)
+    nbx, nby = W // C3_BLOCK, H // C3_BLOCK
+    ys = np.repeat(np.arange(nby) * C3_BLOCK, nbx)
+    xs = np.tile(np.arange(nbx) * C3_BLOCK, nby)
+    n = len(ys)
+    passes = []
+    for p in range(2):
+        jobs = np.zeros(nrefs * n, Cm.JOB_DTYPE)
+        for k in range(nrefs):
+            sl = slice(k * n, (k + 1) * n)
+            r = (k + p) % nrefs
+            d = rng.integers(-16, 17, (n, 2))
+            jobs["src_off"][sl] = r * refs[0].size + (ys + border + d[:, 0]) * st + xs + border + d[:, 1]
+            jobs["dst_off"][sl] = k * W * H + ys * W + xs
+            jobs["conv_off"][sl] = k * W * H + ys * W + xs
+        jobs["subpel_x_qn"] = rng.integers(0, 16, len(jobs))
+        jobs["subpel_y_qn"] = rng.integers(0, 16, len(jobs))
+        passes.append(jobs)
+    return refs, st, passes
+
+
+def compound_tables():
+    """EIGHTTAP_REGULAR kernels for 16-wide blocks (av1/common/filter.h)."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import _oracle as O
+    return np.stack([O.interp_kernel(0, 16, p) for p in range(16)])
+
+
+COMPOUND_CP = [dict(do_average=0, round_0=3, round_1=7, is_compound=1, use_dist_wtd_comp_avg=0,
+                    fwd_offset=0, bck_offset=0),
+               dict(do_average=1, round_0=3, round_1=7, is_compound=1, use_dist_wtd_comp_avg=1,
+                    fwd_offset=9, bck_offset=7)]
+
+
+def cpu_baseline_compound(args):
+    """orc_dist_wtd_batch (the oracle's av1_dist_wtd_convolve_* restatement,
+    both passes) on a 1920x256 strip of the same workload, all host cores."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import _oracle as O
+    W, Hs = args.width, 256
+    refs, st, passes = compound_setup(W, Hs, args.refs, 1234)
+    tab = compound_tables()
+    dst = np.zeros(args.refs * W * Hs, np.uint8)
+    conv = np.zeros(args.refs * W * Hs, np.uint16)
+    threads = host_cores()
+    sb = sb64_count(W, Hs)
+    n = 0
+    t0 = time.perf_counter()
+    while True:
+        for p in range(2):
+            O.dist_wtd_batch(refs.reshape(-1), st, dst, W, conv, W, C3_BLOCK, C3_BLOCK,
+                             passes[p], tab, tab, COMPOUND_CP[p], threads=threads)
+        n += 1
+        dt = time.perf_counter() - t0
+        if dt >= args.cpu_seconds:
+            break
+    return {"value": round(n * sb / dt, 2), "unit": "SB64/s", "cores": threads, "kind": "port",
+            "sample": "%d passes of a %dx%d strip (%d SB64, 2 x %d blocks) through the compound "
+                      "step, oracle C restatement (-O3, %d pthreads), %.1f s"
+                      % (n, W, Hs, sb, len(passes[0]), threads, dt)}
+
+
+def main_compound(args):
+    """Compound inter prediction of every 16x16 block x reference pair of a
+    1080p frame: lavish_dist_wtd_convolve_batch twice (first prediction into
+    the CONV_BUF, then the distance-weighted average into the prediction)."""
+    import torch
+    import torch.distributed as dist
+    import lavish_dsp as L
+    import lavish_dsp.compound as Cm
+    from lavish_dsp.inter import ConvolveParams
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local_rank)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    W, H = args.width, args.height
+    refs, st, passes = compound_setup(W, H, args.refs, 1234 + rank)
+    tref = torch.from_numpy(refs.reshape(-1)).cuda()
+    dst = torch.empty(args.refs * W * H, dtype=torch.uint8, device="cuda")
+    conv = torch.empty(args.refs * W * H, dtype=torch.int16, device="cuda")
+    tjobs = [torch.from_numpy(p.view(np.uint8)).cuda() for p in passes]
+    fp, tab = Cm.filter_params(compound_tables())
+    cps = [ConvolveParams(c["do_average"], None, 0, c["round_0"], c["round_1"], 0, 1,
+                          c["use_dist_wtd_comp_avg"], c["fwd_offset"], c["bck_offset"])
+           for c in COMPOUND_CP]
+    stream = torch.cuda.current_stream()
+    nj = len(passes[0])
+
+    def step():
+        for p in range(2):
+            Cm.dist_wtd_convolve_batch(tref, st, dst, W, conv, W, C3_BLOCK, C3_BLOCK, tjobs[p], nj,
+                                       fp, fp, cps[p], 8, stream=stream)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+          for _ in range(args.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        ev[k][0].record(stream)
+        step()
+        ev[k][1].record(stream)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    status = L.status()
+    if status[0] != 0:
+        raise RuntimeError("HIP error during bench: %s" % (status,))
+    k_ms = sum(a.elapsed_time(b) for a, b in ev) / args.steps
+    # per block and pass: the source window read once, the CONV_BUF written
+    # (pass 1) or read + the prediction written (pass 2), the 32 B job
+    nbytes = nj * (2 * 256 + 2 * 512 + 512 + 256 + 2 * 32)
+    sb = sb64_count(W, H)
+    line = {
+        "metric": METRIC,
+        "value": round(world * sb * args.steps / elapsed, 2),
+        "unit": "SB64/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u8",
+        "data": "synthetic (seeded 1080p content, lavish_dsp/synth.py; seeded mvs)",
+        "config": {
+            "workload": "compound: %dx%d 8-bit; av1_dist_wtd_convolve (facade path per block, "
+                        "EIGHTTAP_REGULAR) of every %dx%d block x %d reference pairs: first "
+                        "prediction into the CONV_BUF, distance-weighted average into the "
+                        "prediction; %d SB64/frame" % (W, H, C3_BLOCK, C3_BLOCK, args.refs, sb),
+            "parallelism": "frame-per-rank x%d" % world,
+        },
+        "roofline": {"bound": "hbm", "kernel": "compound_kernel<u8> x 2 "
+                     "(lavish_dist_wtd_convolve_batch)",
+                     "achieved": round(nbytes / (k_ms * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "traffic": None, "avg_launch_ms": round(k_ms / 2, 4),
+                     "algorithmic_bytes_per_launch": nbytes // 2},
+    }
+    line["roofline"]["frac"] = round(line["roofline"]["achieved"] / HBM_PEAK_GBS, 4)
+    if rank == 0 and world == 1 and not args.no_cpu:
+        line["cpu_baseline"] = cpu_baseline_compound(args)
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
 TPL_BORDER = 288  # AOM_BORDER_IN_PIXELS: the predictor's clamp reads stay inside
 
 
@@ -1172,6 +1343,8 @@ def main():
         return main_pixel(args)
     if args.workload == "warp":
         return main_warp(args)
+    if args.workload == "compound":
+        return main_compound(args)
     if args.workload == "tpl":
         return main_tpl(args)
     if args.workload == "rate":
@@ -1230,17 +1403,20 @@ def main():
                                              fullpel=c3_out, cost_lists=c3_cl, out=sub_out,
                                              stream=on)
 
-    overlap = do_c2 and do_c3 and args.overlap
-    side = torch.cuda.Stream() if overlap else stream
+    overlap = do_c2 and do_c3 and not args.serial
+    side_stream = torch.cuda.Stream()
     fork = torch.cuda.Event()
     join = torch.cuda.Event()
 
-    def step(ev=None):
+    def step(ev=None, ovl=None):
         """One frame.  ev = (start, c3 start, c3 end, c2 start, c2 end, end),
-        each leg's pair recorded on the stream that leg runs on."""
+        each leg's pair recorded on the stream that leg runs on; ovl: run C3 on
+        the side stream beside C2 (default: the run's mode)."""
+        ovl = overlap if ovl is None else ovl
+        side = side_stream if ovl else stream
         if ev is not None:
             ev[0].record(stream)
-        if overlap:  # the legs are independent: C3 (TA / latency bound) beside C2 (HBM writes)
+        if ovl:  # the legs are independent: C3 (TA / latency bound) beside C2 (HBM writes)
             fork.record(stream)
             side.wait_event(fork)
         if do_c3:
@@ -1255,7 +1431,7 @@ def main():
             L.txq_frame(res, frame, qp, stream=stream)
             if ev is not None:
                 ev[4].record(stream)
-        if overlap:
+        if ovl:
             join.record(side)
             stream.wait_event(join)
         if ev is not None:
@@ -1288,6 +1464,20 @@ def main():
     step_ms = sum(ev[k][0].elapsed_time(ev[k][5]) for k in range(K)) / K
     c3_ms = sum(ev[k][1].elapsed_time(ev[k][2]) for k in range(K)) / K if do_c3 else 0.0
     c2_ms = sum(ev[k][3].elapsed_time(ev[k][4]) for k in range(K)) / K if do_c2 else 0.0
+    legs_overlapped = None
+    if overlap:
+        # the legs share the GPU in the timed region, which stretches each; the
+        # per-kernel roofline is taken from a serial pass after it (isolated
+        # legs, same inputs), not from the overlapped leg spans
+        legs_overlapped = {"c2_txq_frame": round(c2_ms, 4), "c3_diamond": round(c3_ms, 4)}
+        KS = max(5, K // 2)
+        evs = [tuple(torch.cuda.Event(enable_timing=True) for _ in range(6)) for _ in range(KS)]
+        step(ovl=False)
+        for k in range(KS):
+            step(evs[k], ovl=False)
+        torch.cuda.synchronize()
+        c3_ms = sum(evs[k][1].elapsed_time(evs[k][2]) for k in range(KS)) / KS
+        c2_ms = sum(evs[k][3].elapsed_time(evs[k][4]) for k in range(KS)) / KS
     c2_bytes = sum(algorithmic_bytes(L, s, W, H) for s in sizes)
     c3_res = M.results_numpy(c3_out) if do_c3 else None
     c3_bytes = c3_algorithmic_bytes(c3_res, len(jobs_np), C3_BLOCK, C3_BLOCK, C3_SKIP, C3_CL) \
@@ -1352,8 +1542,12 @@ def main():
         },
         "roofline": roof,
         "legs_ms": {"c2_txq_frame": round(c2_ms, 4), "c3_diamond": round(c3_ms, 4),
-                    "step_event_ms": round(step_ms, 4)},
+                    "step_event_ms": round(step_ms, 4),
+                    "legs": "isolated (serial pass after the timed region)" if overlap
+                            else "as timed"},
     }
+    if legs_overlapped is not None:
+        line["legs_overlapped_ms"] = legs_overlapped
     if do_c3:
         line["c3"] = {"jobs": len(jobs_np),
                       "steps_per_job": round(float(c3_res["steps"].mean()), 2),

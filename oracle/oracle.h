@@ -425,6 +425,10 @@ void orc_dist_wtd_convolve(int path, const void *src, int src_stride, void *dst,
                            int w, int h, const int16_t *fx, int tx, const int16_t *fy, int ty,
                            const OrcConvParams *cp, uint16_t *conv, int conv_stride, int bd,
                            int hbd);
+void orc_dist_wtd_batch(const void *src, int src_stride, void *dst, int dst_stride,
+                        uint16_t *conv, int conv_stride, int w, int h, const void *jobs,
+                        long njobs, const int16_t *fx, int tx, const int16_t *fy, int ty,
+                        const OrcConvParams *cp, int bd, int hbd, int threads);
 void orc_warp_batch(const void *ref, int width, int height, int stride, void *pred,
                     int p_stride, uint16_t *dst, int dst_stride, const void *jobs, long njobs,
                     int ss_x, int ss_y, int bd, int hbd, const OrcConvParams *cp, int threads);

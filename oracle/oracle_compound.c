@@ -34,6 +34,18 @@ void orc_dist_wtd_convolve(int path, const void *src, int src_stride, void *dst,
   const int round_bits = 2 * FB - r0 - r1;
   const int fo_x = tx / 2 - 1, fo_y = ty / 2 - 1;
   const int pmax = (1 << bd) - 1;
+  /* path 3: the (h + ty - 1) x w horizontally filtered rows first (int16,
+   * as im_block) */
+  int16_t im[(128 + 11) * 128];
+  if (path == 3)
+    for (int y = 0; y < h + ty - 1; ++y) {
+      const long row = (long)(y - fo_y) * src_stride;
+      for (int x = 0; x < w; ++x) {
+        int32_t hs = 1 << (bd + FB - 1);
+        for (int m = 0; m < tx; ++m) hs += fx[m] * pget(src, row + x - fo_x + m, hbd);
+        im[y * w + x] = (int16_t)rpot(hs, r0);
+      }
+    }
   for (int y = 0; y < h; ++y) {
     for (int x = 0; x < w; ++x) {
       int32_t res;
@@ -49,14 +61,9 @@ void orc_dist_wtd_convolve(int path, const void *src, int src_stride, void *dst,
           s += fy[k] * pget(src, (long)(y - fo_y + k) * src_stride + x, hbd);
         res = rpot(s * (1 << (FB - r0)), r1) + round_offset;
       } else {
-        /* the intermediate rows y - fo_y .. y - fo_y + ty - 1 at column x */
+        /* the intermediate rows y .. y + ty - 1 (source rows y - fo_y ..) */
         int32_t s = 1 << offset_bits;
-        for (int k = 0; k < ty; ++k) {
-          const long row = (long)(y - fo_y + k) * src_stride;
-          int32_t hs = 1 << (bd + FB - 1);
-          for (int m = 0; m < tx; ++m) hs += fx[m] * pget(src, row + x - fo_x + m, hbd);
-          s += fy[k] * (int16_t)rpot(hs, r0);
-        }
+        for (int k = 0; k < ty; ++k) s += fy[k] * im[(y + k) * w + x];
         res = (uint16_t)rpot(s, r1);
       }
       uint16_t *c = conv + (long)y * conv_stride + x;
@@ -74,4 +81,74 @@ void orc_dist_wtd_convolve(int path, const void *src, int src_stride, void *dst,
       else ((uint8_t *)dst)[(long)y * dst_stride + x] = (uint8_t)v;
     }
   }
+}
+
+/* Batch driver for the `compound` bench workload's CPU baseline: jobs in the
+ * LavishCompoundJob layout, the x / y kernel tables [16][taps] shared, the
+ * path per job from its sub-pel phases, over pthreads. */
+#include <pthread.h>
+
+typedef struct {
+  int64_t src_off, dst_off, conv_off;
+  int32_t sx, sy;
+} CompJob;
+
+typedef struct {
+  const void *src;
+  void *dst;
+  uint16_t *conv;
+  const CompJob *jobs;
+  const int16_t *fx, *fy;
+  const OrcConvParams *cp;
+  int src_stride, dst_stride, conv_stride, w, h, tx, ty, bd, hbd;
+  long lo, hi;
+} CompArg;
+
+static void *comp_worker(void *p) {
+  const CompArg *a = (const CompArg *)p;
+  const int es = a->hbd ? 2 : 1;
+  for (long j = a->lo; j < a->hi; ++j) {
+    const CompJob *jb = &a->jobs[j];
+    const int sx = jb->sx & 15, sy = jb->sy & 15;
+    orc_dist_wtd_convolve((sx != 0) + 2 * (sy != 0), (const char *)a->src + jb->src_off * es,
+                          a->src_stride, (char *)a->dst + jb->dst_off * es, a->dst_stride, a->w,
+                          a->h, a->fx + sx * a->tx, a->tx, a->fy + sy * a->ty, a->ty, a->cp,
+                          a->conv + jb->conv_off, a->conv_stride, a->bd, a->hbd);
+  }
+  return NULL;
+}
+
+void orc_dist_wtd_batch(const void *src, int src_stride, void *dst, int dst_stride,
+                        uint16_t *conv, int conv_stride, int w, int h, const void *jobs,
+                        long njobs, const int16_t *fx, int tx, const int16_t *fy, int ty,
+                        const OrcConvParams *cp, int bd, int hbd, int threads) {
+  if (threads < 1) threads = 1;
+  if (threads > 256) threads = 256;
+  pthread_t tid[256];
+  CompArg args[256];
+  for (int t = 0; t < threads; ++t) {
+    CompArg *a = &args[t];
+    a->src = src;
+    a->dst = dst;
+    a->conv = conv;
+    a->jobs = (const CompJob *)jobs;
+    a->fx = fx;
+    a->fy = fy;
+    a->cp = cp;
+    a->src_stride = src_stride;
+    a->dst_stride = dst_stride;
+    a->conv_stride = conv_stride;
+    a->w = w;
+    a->h = h;
+    a->tx = tx;
+    a->ty = ty;
+    a->bd = bd;
+    a->hbd = hbd;
+    a->lo = njobs * t / threads;
+    a->hi = njobs * (t + 1) / threads;
+    if (threads > 1) pthread_create(&tid[t], NULL, comp_worker, a);
+    else comp_worker(a);
+  }
+  if (threads > 1)
+    for (int t = 0; t < threads; ++t) pthread_join(tid[t], NULL);
 }

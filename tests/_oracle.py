@@ -956,3 +956,21 @@ def dist_wtd_convolve(path, src, src_stride, dst, dst_stride, w, h, fx, fy, cp, 
     base = src.ctypes.data + src_off * src.itemsize
     fn(path, ctypes.c_void_p(base), src_stride, P(dst), dst_stride, w, h, P(fxa), len(fxa),
        P(fya), len(fya), ctypes.byref(c), P(conv), conv_stride, bd, hbd)
+
+
+def dist_wtd_batch(src, src_stride, dst, dst_stride, conv, conv_stride, w, h, jobs, fx_table,
+                   fy_table, cp, bd=8, threads=1):
+    """orc_dist_wtd_batch in place on dst / conv (jobs: lavish_dsp.compound.JOB_DTYPE,
+    fx_table / fy_table: int16 [16, taps])."""
+    fn = lib().orc_dist_wtd_batch
+    fn.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p] + \
+        [ctypes.c_int] * 3 + [ctypes.c_void_p, ctypes.c_long, ctypes.c_void_p, ctypes.c_int,
+                              ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p] + [ctypes.c_int] * 3
+    fn.restype = None
+    fx = np.ascontiguousarray(fx_table, np.int16)
+    fy = np.ascontiguousarray(fy_table, np.int16)
+    c = OrcConvParams(**cp)
+    jobs = np.ascontiguousarray(jobs)
+    fn(P(src), src_stride, P(dst), dst_stride, P(conv), conv_stride, w, h, P(jobs), len(jobs),
+       P(fx), fx.shape[1], P(fy), fy.shape[1], ctypes.byref(c), bd, int(src.dtype == np.uint16),
+       threads)
