@@ -71,6 +71,28 @@ __device__ __forceinline__ void load_row(const uint8_t* p, uint32_t (&out)[DW]) 
   }
 }
 
+// The same DW words from dword-aligned loads (DW words + one more, merged into
+// dwordx4 loads) and v_alignbyte: the pattern searches keep this form -- their
+// candidates sit a few pixels apart, so a wave's lanes hit the same lines at
+// different byte offsets, the shape where byte-addressed 16-byte loads cost
+// the address path most (profiles/r02_ta_rate.txt, "grp8"); measured on the
+// TPL FAST_BIGDIA leg: 0.191 ms aligned vs 0.218 ms byte-addressed.
+template <int DW>
+__device__ __forceinline__ void load_row_aligned(const uint8_t* p, uint32_t (&out)[DW]) {
+  const uintptr_t a = (uintptr_t)p;
+  typedef const __attribute__((address_space(1))) uint32_t* gptr;
+  const gptr q = (gptr)(a & ~(uintptr_t)3);
+  const uint32_t sh = (uint32_t)(a & 3);
+  uint32_t w[DW + 1];
+#pragma unroll
+  for (int i = 0; i < DW; ++i) w[i] = q[i];
+  // the next word only matters when the row is unaligned; an aligned row
+  // re-reads its last word instead (no branch, no byte past the row)
+  w[DW] = q[sh ? DW : DW - 1];
+#pragma unroll
+  for (int i = 0; i < DW; ++i) out[i] = __builtin_amdgcn_alignbyte(w[i + 1], w[i], sh);
+}
+
 // sum over the 8-lane group (every lane of the group gets it): quad_perm
 // [1,0,3,2], quad_perm [2,3,0,1], row_half_mirror
 __device__ __forceinline__ uint32_t group_sum8(uint32_t v) {
@@ -243,7 +265,10 @@ struct Win {
 __device__ __forceinline__ int site_dr(int i) { return ((0x8858 >> (2 * i)) & 3) - 1; }
 __device__ __forceinline__ int site_dc(int i) { return ((0x2885 >> (2 * i)) & 3) - 1; }
 
-template <int W, int H, bool SKIP>
+// UA: candidate rows as byte-addressed loads (DIAMOND: its global-memory
+// steps are the large-radius ones) or aligned loads + v_alignbyte (the
+// pattern searches, see load_row_aligned)
+template <int W, int H, bool SKIP, bool UA = true>
 struct Search {
   using G = Geo<W, H, SKIP>;
   using WN = Win<W, H>;
@@ -307,7 +332,8 @@ struct Search {
         const int row = l + 8 * k;
         if (row < G::RH) {
           uint32_t r[G::DW];
-          load_row<G::DW>(c.ref + off + (int64_t)row * G::YS * c.rs, r);
+          if constexpr (UA) load_row<G::DW>(c.ref + off + (int64_t)row * G::YS * c.rs, r);
+          else load_row_aligned<G::DW>(c.ref + off + (int64_t)row * G::YS * c.rs, r);
 #pragma unroll
           for (int i = 0; i < G::DW; ++i) acc = sad4(s[k][i], r[i], acc);
         }
@@ -500,8 +526,8 @@ __device__ __forceinline__ void set_cl(int (&cl)[5], int i, int v) {
 // left, bottom, right, top -- raw SADs (recomputed unless the pattern search
 // left them in cl) plus mvsad_err_cost; INT_MAX for out-of-range neighbours.
 // Groups 0..4 evaluate the five points at once.
-template <int W, int H, bool SKIP>
-__device__ void int_sad_list(const Search<W, H, SKIP>& S, const Ctx& c, int lane, int br, int bc,
+template <class S_t>
+__device__ void int_sad_list(const S_t& S, const Ctx& c, int lane, int br, int bc,
                              bool has_sad, int (&cl)[5]) {
   const int g = lane >> 3;
   if (!has_sad) {
@@ -587,7 +613,7 @@ template <int W, int H, bool SKIP>
 __device__ int pattern(const Ctx& c, int lane, int srow, int scol, int search_step, bool do_init,
                        bool want_cl, int (&cl)[5], int& brow, int& bcol, int& steps,
                        int& nsad) {
-  Search<W, H, SKIP> S;
+  Search<W, H, SKIP, false> S;
   S.load_src(c, lane);
   const int g = lane >> 3;
   search_step = min(search_step, kMaxSteps - 1);
