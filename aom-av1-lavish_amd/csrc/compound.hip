@@ -10,11 +10,12 @@
 // (fwd / bck offsets, DIST_PRECISION_BITS) -- removes the offset, rounds and
 // clips into the prediction.
 //
-// One workgroup per block: for the 2-D path its threads first filter the
-// (h + taps - 1) x w intermediate rows into LDS (int16, as the reference
-// stores them), then every thread takes output pixels (rows coalesced across
-// threads) and applies the vertical taps / the single 1-D pass / the copy
-// and the write-out.  The kernel rows of the caller's filters
+// One workgroup per block (blocks of <= 256 pixels share one 2 or 4 ways,
+// each with its slice of the dynamic LDS): for the 2-D path its threads
+// first filter the (h + taps - 1) x w intermediate rows into LDS (int16, as
+// the reference stores them), then every thread takes output pixels (rows
+// coalesced across threads) and applies the vertical taps / the single 1-D
+// pass / the copy and the write-out.  The kernel rows of the caller's filters
 // (InterpFilterParams, up to 12 taps x 16 phases) travel as kernel
 // arguments.
 #include <algorithm>
@@ -35,40 +36,50 @@ struct CompArgs {
   const LavishCompoundJob* jobs;
   int src_stride, dst_stride, conv_stride, w, h, njobs, bd;
   int tx, ty;                           // tap counts
+  int lw, bpw, any2d;                   // log2(w), blocks per workgroup, 2-D path possible
   int16_t fx[16][kMaxTaps], fy[16][kMaxTaps];
   int r0, r1, offset_bits, round_offset, round_bits, do_average, dist_wtd, fwd, bck;
 };
 
+// a.bpw blocks per 256-thread workgroup (small blocks share one), each with
+// 256 / bpw threads and its own slice of the dynamic LDS intermediate
 template <typename Pix>
 __global__ __launch_bounds__(256) void compound_kernel(CompArgs a) {
-  __shared__ int16_t im[(kMaxH + kMaxTaps - 1) * kMaxW];
+  extern __shared__ int16_t im_all[];
   const int nwg = gridDim.x;  // multiple of 8: consecutive blocks share an XCD's L2
-  const int j = (blockIdx.x & 7) * (nwg >> 3) + (blockIdx.x >> 3);
-  if (j >= a.njobs) return;
-  const LavishCompoundJob& jb = a.jobs[j];
+  const int wg = (blockIdx.x & 7) * (nwg >> 3) + (blockIdx.x >> 3);
+  const int tpb = 256 / a.bpw;  // threads per block
+  const int sub = threadIdx.x / tpb, t = threadIdx.x - sub * tpb;
+  const int j = wg * a.bpw + sub;
+  const bool live = j < a.njobs;
+  const LavishCompoundJob& jb = a.jobs[live ? j : a.njobs - 1];
   const int sx = jb.subpel_x_qn & 15, sy = jb.subpel_y_qn & 15;
   const int path = (sx != 0) + 2 * (sy != 0);
   const Pix* src = (const Pix*)a.src + jb.src_off;
   Pix* dst = (Pix*)a.dst + jb.dst_off;
   uint16_t* conv = a.conv + jb.conv_off;
-  const int w = a.w, h = a.h;
+  const int w = a.w, lw = a.lw;
   const int fo_x = a.tx / 2 - 1, fo_y = a.ty / 2 - 1;
   const int16_t* fx = a.fx[sx];
   const int16_t* fy = a.fy[sy];
-  if (path == 3) {  // horizontal pass of the 2-D form into LDS
-    const int ih = h + a.ty - 1;
-    for (int e = threadIdx.x; e < ih * w; e += 256) {
-      const int y = e / w, x = e - y * w;
-      const Pix* row = src + (int64_t)(y - fo_y) * a.src_stride + x - fo_x;
-      int32_t s = 1 << (a.bd + kFBits - 1);
-      for (int k = 0; k < a.tx; ++k) s += fx[k] * (int)row[k];
-      im[e] = (int16_t)((s + ((1 << a.r0) >> 1)) >> a.r0);
+  int16_t* im = im_all + sub * (a.h + a.ty - 1) * w;
+  if (a.any2d) {  // horizontal pass of the 2-D form into LDS (w is a power of two)
+    if (path == 3) {
+      const int ih = a.h + a.ty - 1;
+      for (int e = t; e < ih * w; e += tpb) {
+        const int y = e >> lw, x = e & (w - 1);
+        const Pix* row = src + (int64_t)(y - fo_y) * a.src_stride + x - fo_x;
+        int32_t s = 1 << (a.bd + kFBits - 1);
+        for (int k = 0; k < a.tx; ++k) s += fx[k] * (int)row[k];
+        im[e] = (int16_t)((s + ((1 << a.r0) >> 1)) >> a.r0);
+      }
     }
     __syncthreads();
   }
+  if (!live) return;
   const int pmax = (1 << a.bd) - 1;
-  for (int e = threadIdx.x; e < h * w; e += 256) {
-    const int y = e / w, x = e - y * w;
+  for (int e = t; e < a.h * w; e += tpb) {
+    const int y = e >> lw, x = e & (w - 1);
     int32_t res;
     if (path == 0) {
       res = (uint16_t)(((int)src[(int64_t)y * a.src_stride + x] << a.round_bits) +
@@ -86,7 +97,7 @@ __global__ __launch_bounds__(256) void compound_kernel(CompArgs a) {
       res = ((s + ((1 << a.r1) >> 1)) >> a.r1) + a.round_offset;
     } else {
       int32_t s = 1 << a.offset_bits;
-      for (int k = 0; k < a.ty; ++k) s += fy[k] * (int)im[(y + k) * w + x];
+      for (int k = 0; k < a.ty; ++k) s += fy[k] * (int)im[((y + k) << lw) + x];
       res = (uint16_t)((s + ((1 << a.r1) >> 1)) >> a.r1);
     }
     uint16_t* c = conv + (int64_t)y * a.conv_stride + x;
@@ -94,10 +105,10 @@ __global__ __launch_bounds__(256) void compound_kernel(CompArgs a) {
       *c = (uint16_t)res;
       continue;
     }
-    int32_t t = *c;
-    t = a.dist_wtd ? (t * a.fwd + res * a.bck) >> 4 : (t + res) >> 1;
-    t -= a.round_offset;
-    const int v = (t + ((1 << a.round_bits) >> 1)) >> a.round_bits;
+    int32_t tt = *c;
+    tt = a.dist_wtd ? (tt * a.fwd + res * a.bck) >> 4 : (tt + res) >> 1;
+    tt -= a.round_offset;
+    const int v = (tt + ((1 << a.round_bits) >> 1)) >> a.round_bits;
     dst[(int64_t)y * a.dst_stride + x] = (Pix)min(max(v, 0), pmax);
   }
 }
@@ -110,7 +121,7 @@ int compound_batch(const void* src, int src_stride, void* dst, int dst_stride, u
                    const LavishConvolveParams* cp, int bd, int highbd, hipStream_t s) {
   if (njobs <= 0) return 0;
   if (!src || !conv || !jobs || !cp || !fpx || !fpy || (cp->do_average && !dst)) return -1;
-  if (w < 1 || h < 1 || w > kMaxW || h > kMaxH) return -2;
+  if (w < 2 || h < 1 || w > kMaxW || h > kMaxH || (w & (w - 1))) return -2;
   if (highbd ? (bd != 8 && bd != 10 && bd != 12) : bd != 8) return -3;
   if (fpx->taps < 2 || fpx->taps > kMaxTaps || fpy->taps < 2 || fpy->taps > kMaxTaps ||
       (fpx->taps & 1) || (fpy->taps & 1) || !fpx->filter_ptr || !fpy->filter_ptr)
@@ -147,11 +158,17 @@ int compound_batch(const void* src, int src_stride, void* dst, int dst_stride, u
   a.dist_wtd = cp->use_dist_wtd_comp_avg;
   a.fwd = cp->fwd_offset;
   a.bck = cp->bck_offset;
-  const int nwg = (njobs + 7) & ~7;
+  a.lw = 31 - __builtin_clz(w);
+  // blocks of <= 256 pixels share a workgroup 4 ways, <= 1024 2 ways
+  a.bpw = w * h <= 256 ? 4 : (w * h <= 1024 ? 2 : 1);
+  a.any2d = 1;  // the per-block path is decided on the device
+  const size_t lds = (size_t)a.bpw * (h + a.ty - 1) * w * sizeof(int16_t);
+  int nwg = (njobs + a.bpw - 1) / a.bpw;
+  nwg = (nwg + 7) & ~7;
   if (highbd)
-    hipLaunchKernelGGL(compound_kernel<uint16_t>, dim3(nwg), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(compound_kernel<uint16_t>, dim3(nwg), dim3(256), lds, s, a);
   else
-    hipLaunchKernelGGL(compound_kernel<uint8_t>, dim3(nwg), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(compound_kernel<uint8_t>, dim3(nwg), dim3(256), lds, s, a);
   LAVISH_CHECK(hipGetLastError());
   return 0;
 }
