@@ -176,7 +176,132 @@ __global__ __launch_bounds__(256) void var_u8_kernel(const uint8_t* __restrict__
   if (var_out) var_out[j] = kind == 1 ? sse : sse - (uint32_t)(((int64_t)sum * sum) / (w * h));
 }
 
+// ---------------------------------------------- u16 (highbd) SAD / variance ----
+// The same word-chunk layout over u16 samples (a 4-byte word = 2 samples,
+// chunks of up to 8 samples = one 16-byte load): SAD on v_sad_u16; variance
+// with exact 64-bit per-lane sums, then highbd_variance64's rounding for
+// 10 / 12 bits (aom_dsp/variance.c:321-408) as var_kernel does it.
+__device__ __forceinline__ void load_words16(const uint16_t* p, int c, uint32_t (&w)[4]) {
+  load_words((const uint8_t*)p, c, w);
+}
+
+__global__ __launch_bounds__(256) void sad_u16_kernel(const uint16_t* __restrict__ src, int ss,
+                                                      const uint16_t* __restrict__ ref, int rs,
+                                                      U8Shape sh, const LavishPixJob* __restrict__ jobs,
+                                                      int njobs, int nrefs, int mode,
+                                                      const uint16_t* __restrict__ second, int w,
+                                                      uint32_t* __restrict__ out) {
+  const int t = blockIdx.x * 256 + threadIdx.x;
+  const int j = t >> __builtin_ctz(sh.lpj);
+  const int q = t & (sh.lpj - 1);
+  const bool live = j < njobs;
+  const LavishPixJob jb = jobs[live ? j : njobs - 1];
+  const int rstep = mode == 1 ? 2 : 1;
+  const int c = 1 << sh.lc;  // words per chunk (2 samples each)
+  for (int k = 0; k < nrefs; ++k) {
+    uint32_t acc = 0;
+    for (int i = q; i < sh.chunks; i += sh.lpj) {
+      const int y = i >> sh.lcpr, x = (i & ((1 << sh.lcpr) - 1)) << (sh.lc + 1);
+      uint32_t a[4], b[4];
+      load_words16(src + jb.src_off + (int64_t)y * rstep * ss + x, c, a);
+      load_words16(ref + jb.ref_off[k] + (int64_t)y * rstep * rs + x, c, b);
+      if (mode == 2) {
+        uint32_t p[4];
+        load_words16(second + jb.aux_off + (int64_t)y * w + x, c, p);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const uint32_t lo = ((b[u] & 0xFFFF) + (p[u] & 0xFFFF) + 1) >> 1;
+          const uint32_t hi = ((b[u] >> 16) + (p[u] >> 16) + 1) >> 1;
+          b[u] = lo | (hi << 16);
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) acc = __builtin_amdgcn_sad_u16(a[u], b[u], acc);
+    }
+    acc = group_sum(acc, sh.lpj);
+    if (live && q == 0) out[(int64_t)j * nrefs + k] = mode == 1 ? 2 * acc : acc;
+  }
+}
+
+__global__ __launch_bounds__(256) void var_u16_kernel(const uint16_t* __restrict__ a, int as,
+                                                      const uint16_t* __restrict__ b, int bs,
+                                                      U8Shape sh, int w, int h,
+                                                      const LavishPixJob* __restrict__ jobs,
+                                                      int njobs, int kind, int bd,
+                                                      uint32_t* __restrict__ var_out,
+                                                      uint32_t* __restrict__ sse_out,
+                                                      int32_t* __restrict__ sum_out,
+                                                      int64_t* __restrict__ sse64_out) {
+  const int t = blockIdx.x * 256 + threadIdx.x;
+  const int j = t >> __builtin_ctz(sh.lpj);
+  const int q = t & (sh.lpj - 1);
+  const bool live = j < njobs;
+  const LavishPixJob jb = jobs[live ? j : njobs - 1];
+  const int c = 1 << sh.lc;
+  int64_t sum = 0;
+  uint64_t sse = 0;
+  for (int i = q; i < sh.chunks; i += sh.lpj) {
+    const int y = i >> sh.lcpr, x = (i & ((1 << sh.lcpr) - 1)) << (sh.lc + 1);
+    uint32_t va[4], vb[4];
+    load_words16(a + jb.src_off + (int64_t)y * as + x, c, va);
+    load_words16(b + jb.ref_off[0] + (int64_t)y * bs + x, c, vb);
+    int s = 0;
+    uint32_t q2 = 0;  // <= 8 squares of 12-bit differences: < 2^28
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int d0 = (int)(va[u] & 0xFFFF) - (int)(vb[u] & 0xFFFF);
+      const int d1 = (int)(va[u] >> 16) - (int)(vb[u] >> 16);
+      s += d0 + d1;
+      q2 += (uint32_t)(d0 * d0) + (uint32_t)(d1 * d1);
+    }
+    sum += s;
+    sse += q2;
+  }
+  for (int m = 1; m < sh.lpj; m <<= 1) {
+    sum += __shfl_xor(sum, m);
+    sse += (uint64_t)__shfl_xor((int64_t)sse, m);
+  }
+  if (!live || q != 0) return;
+  if (kind == 4) {
+    sse64_out[j] = (int64_t)sse;
+    return;
+  }
+  uint32_t s32;
+  int sm;
+  if (bd == 8) {
+    s32 = (uint32_t)sse;
+    sm = (int)sum;
+  } else {
+    const int ss_ = bd == 10 ? 4 : 8, sh2 = bd == 10 ? 2 : 4;
+    s32 = (uint32_t)((sse + ((1ull << ss_) >> 1)) >> ss_);
+    sm = (int)((sum + ((1ll << sh2) >> 1)) >> sh2);
+  }
+  if (sse_out) sse_out[j] = s32;
+  if (sum_out) sum_out[j] = sm;
+  if (var_out) {
+    if (kind == 1) {
+      var_out[j] = s32;
+    } else if (bd == 8) {
+      var_out[j] = s32 - (uint32_t)(((int64_t)sm * sm) / (w * h));
+    } else {
+      const int64_t v = (int64_t)s32 - (((int64_t)sm * sm) / (w * h));
+      var_out[j] = v >= 0 ? (uint32_t)v : 0;
+    }
+  }
+}
+
 static int ilog2(int v) { return 31 - __builtin_clz(v); }
+
+// the u16 word-chunk layout (2 samples per word, chunks of <= 8 samples)
+static bool u16_shape(int w, int rows, U8Shape& sh) {
+  if (w < 2 || (w & (w - 1)) || rows < 1 || (rows & (rows - 1))) return false;
+  sh.lw4 = ilog2(w / 2);  // log2(words per row)
+  sh.lc = sh.lw4 < 2 ? sh.lw4 : 2;
+  sh.lcpr = sh.lw4 - sh.lc;
+  sh.chunks = rows << sh.lcpr;
+  sh.lpj = sh.chunks < 64 ? sh.chunks : 64;
+  return true;
+}
 
 // the u8 word-chunk layout of a w x h block with `rows` rows read; false when
 // w or rows is not a power of two >= 4 / >= 1
@@ -585,6 +710,14 @@ int lavish_sad_batch(const void* src, int src_stride, const void* ref, int ref_s
     LCHK();
     return 0;
   }
+  if (highbd && u16_shape(w, mode == 1 ? h / 2 : h, sh)) {
+    const int blocks = (int)(((int64_t)njobs * sh.lpj + 255) / 256);
+    hipLaunchKernelGGL(sad_u16_kernel, dim3(blocks), dim3(256), 0, s, (const uint16_t*)src,
+                       src_stride, (const uint16_t*)ref, ref_stride, sh, jobs, njobs, nrefs, mode,
+                       (const uint16_t*)second_pred, w, sad_out);
+    LCHK();
+    return 0;
+  }
   if (highbd)
     hipLaunchKernelGGL(sad_kernel<uint16_t>, dim3(njobs), dim3(64), 0, s, (const uint16_t*)src,
                        src_stride, (const uint16_t*)ref, ref_stride, w, h, jobs, nrefs, mode,
@@ -610,6 +743,14 @@ int lavish_variance_batch(const void* a, int a_stride, const void* b, int b_stri
     hipLaunchKernelGGL(var_u8_kernel, dim3(blocks), dim3(256), 0, s, (const uint8_t*)a, a_stride,
                        (const uint8_t*)b, b_stride, sh, w, h, jobs, njobs, kind, var_out,
                        sse_out, sum_out, sse64_out);
+    LCHK();
+    return 0;
+  }
+  if (highbd && kind != 3 && kind != 5 && u16_shape(w, h, sh)) {
+    const int blocks = (int)(((int64_t)njobs * sh.lpj + 255) / 256);
+    hipLaunchKernelGGL(var_u16_kernel, dim3(blocks), dim3(256), 0, s, (const uint16_t*)a,
+                       a_stride, (const uint16_t*)b, b_stride, sh, w, h, jobs, njobs, kind,
+                       bit_depth, var_out, sse_out, sum_out, sse64_out);
     LCHK();
     return 0;
   }
