@@ -233,6 +233,48 @@ __device__ void two_level(const SpCtx& c, const uint32_t (&sv)[Sp<W, H>::NS], in
   }
 }
 
+// one SUBPEL_TREE level with the bilinear error (USE_2_TAPS_ORIG):
+// first_level_check_fast (mcomp.c:2566-2606) around the current best, then
+// with iters_per_step > 1 and a moved best second_level_check_v2
+// (:2728-2779): row / column bias points away from a losing diagonal, the
+// diagonal bias point only when one of them improved
+template <int W, int H>
+__device__ void tree_level(const SpCtx& c, const uint32_t (&sv)[Sp<W, H>::NS], int lane,
+                           int hstep, int iters, Best& b) {
+  const int tr = b.row, tc = b.col;
+  uint32_t cst[4];
+  {
+    const int r[4] = {tr, tr, tr - hstep, tr + hstep};
+    const int cl[4] = {tc - hstep, tc + hstep, tc, tc};
+    check_n<W, H, 4>(c, sv, lane, r, cl, b, cst);
+  }
+  int dr = cst[2] <= cst[3] ? -hstep : hstep;
+  int dc = cst[0] <= cst[1] ? -hstep : hstep;
+  uint32_t d1[1];
+  {
+    const int r[1] = {tr + dr};
+    const int cl[1] = {tc + dc};
+    check_n<W, H, 1>(c, sv, lane, r, cl, b, d1);
+  }
+  if (iters <= 1) return;
+  const int br = b.row, bc = b.col;
+  if (br == tr && bc == tc) return;
+  if (tr == br) dr = -dr;
+  else if (tc == bc) dc = -dc;
+  const uint32_t before = b.besterr;
+  {
+    const int r[2] = {br + dr, br};
+    const int cl[2] = {bc, bc + dc};
+    uint32_t d2[2];
+    check_n<W, H, 2>(c, sv, lane, r, cl, b, d2);
+  }
+  if (b.besterr != before) {
+    const int r[1] = {br + dr};
+    const int cl[1] = {bc + dc};
+    check_n<W, H, 1>(c, sv, lane, r, cl, b, d1);
+  }
+}
+
 template <int W, int H>
 __global__ __launch_bounds__(256) void subpel_kernel(const uint8_t* __restrict__ src, int ss,
                                                      const uint8_t* __restrict__ ref, int rs,
@@ -300,7 +342,11 @@ __global__ __launch_bounds__(256) void subpel_kernel(const uint8_t* __restrict__
     b.sse1 = tq;
     b.besterr = var + (uint32_t)mv_cost(c, b.row, b.col);
   }
-  if (forced_stop != 3) {  // FULL_PEL
+  if (method == 0) {  // av1_find_best_sub_pixel_tree (mcomp.c:3128-3194), no repeat list
+    const int round = min(3 - forced_stop, 3 - (allow_hp ? 0 : 1));
+    int hstep = 4;
+    for (int it = 0; it < round; ++it, hstep >>= 1) tree_level<W, H>(c, sv, lane, hstep, iters, b);
+  } else if (forced_stop != 3) {  // FULL_PEL
     int hstep = 4;         // INIT_SUBPEL_STEP_SIZE: half pel
     int cl[5] = {INT_MAX, INT_MAX, INT_MAX, INT_MAX, INT_MAX};
     if (cost_lists) {
@@ -375,7 +421,7 @@ int subpel_batch(const uint8_t* src, int src_stride, const uint8_t* ref, int ref
       (cost->mvjcost == nullptr || cost->mvcost[0] == nullptr || cost->mvcost[1] == nullptr))
     return -2;
   if (iters_per_step < 1 || iters_per_step > 2) return -4;
-  if (method != 1 && method != 2) return -6;  // SUBPEL_TREE_PRUNED / _PRUNED_MORE
+  if (method < 0 || method > 2) return -6;  // SUBPEL_TREE (bilinear) / _PRUNED / _PRUNED_MORE
 #define LAVISH_SP_CASE(W, H)                                                                   \
   if (w == W && h == H) {                                                                      \
     launch<W, H>(src, src_stride, ref, ref_stride, jobs, njobs, fp, method, forced_stop,       \

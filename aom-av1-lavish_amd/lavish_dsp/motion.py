@@ -313,7 +313,7 @@ def subpel_after_diamond(src, ref, w, h, jobs, fullpel, forced_stop=EIGHTH_PEL, 
     return out
 
 
-SUBPEL_METHODS = {"pruned": 1, "pruned_more": 2}   # SUBPEL_SEARCH_METHODS
+SUBPEL_METHODS = {"tree": 0, "pruned": 1, "pruned_more": 2}   # SUBPEL_SEARCH_METHODS
 _lib.lavish_find_best_sub_pixel_tree_batch.argtypes = [
     _vp, _i32, _vp, _i32, _i32, _i32, _vp, _vp, _i32, _i32, _i32, _i32, _i32,
     ctypes.POINTER(MvCostParams), _vp, _vp, _vp]
@@ -323,8 +323,8 @@ _lib.lavish_find_best_sub_pixel_tree_batch.restype = _i32
 def find_best_sub_pixel_tree_batch(src, ref, w, h, jobs, cost, method="pruned_more",
                                    forced_stop=EIGHTH_PEL, allow_hp=False, iters_per_step=1,
                                    fullpel=None, cost_lists=None, out=None, stream=None):
-    """lavish_find_best_sub_pixel_tree_batch: av1_find_best_sub_pixel_tree_pruned
-    (_more) with any mv cost (MvCostParams) and the full-pel cost lists
+    """lavish_find_best_sub_pixel_tree_batch: av1_find_best_sub_pixel_tree
+    ("tree", bilinear error), _pruned or _pruned_more with any mv cost (MvCostParams) and the full-pel cost lists
     (device int32 [n, 5] or None); fullpel: device RESULT_DTYPE bytes to start
     from (or None: the jobs' start fields)."""
     import torch

@@ -594,7 +594,10 @@ int lavish_subpel_search_after_diamond(const uint8_t *src, int src_stride,
                                        LavishSubpelResult *out, void *stream);
 
 /* The general form: subpel_search_method (SUBPEL_SEARCH_METHODS,
- * mcomp_structs.h) 1 SUBPEL_TREE_PRUNED (av1_find_best_sub_pixel_tree_pruned,
+ * mcomp_structs.h) 0 SUBPEL_TREE (av1_find_best_sub_pixel_tree,
+ * mcomp.c:3128-3200, with subpel_search_type USE_2_TAPS_ORIG: the svf error,
+ * first_level_check_fast + second_level_check_v2 per level; no cost list),
+ * 1 SUBPEL_TREE_PRUNED (av1_find_best_sub_pixel_tree_pruned,
  * mcomp.c:2992-3126) or 2 SUBPEL_TREE_PRUNED_MORE (:2907-2990); any mv cost
  * (cost: HOST pointer, tables on the device, as for
  * lavish_full_pixel_search_batch -- the hp tables when allow_hp); cost_lists

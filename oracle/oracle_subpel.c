@@ -105,12 +105,38 @@ static void sp_two_level(const SpCtx *c, int tr, int tc, int hstep, int iters, S
   }
 }
 
+/* one SUBPEL_TREE level with the bilinear error (USE_2_TAPS_ORIG):
+ * first_level_check_fast (mcomp.c:2566-2606) around the current best, then
+ * with iters_per_step > 1 and a moved best second_level_check_v2
+ * (:2728-2779): the row / column bias points away from the diagonal step when
+ * the diagonal did not win, and the diagonal bias point only if one of them
+ * improved */
+static void sp_tree_level(const SpCtx *c, int hstep, int iters, SpBest *b) {
+  const int tr = b->row, tc = b->col;
+  const unsigned left = sp_check(c, tr, tc - hstep, b);
+  const unsigned right = sp_check(c, tr, tc + hstep, b);
+  const unsigned up = sp_check(c, tr - hstep, tc, b);
+  const unsigned down = sp_check(c, tr + hstep, tc, b);
+  int dr = up <= down ? -hstep : hstep, dc = left <= right ? -hstep : hstep;
+  sp_check(c, tr + dr, tc + dc, b);
+  if (iters <= 1) return;
+  const int br = b->row, bc = b->col;
+  if (br == tr && bc == tc) return;
+  if (tr == br) dr = -dr;
+  else if (tc == bc) dc = -dc;
+  const unsigned before = b->besterr;
+  sp_check(c, br + dr, bc, b);
+  sp_check(c, br, bc + dc, b);
+  if (b->besterr != before) sp_check(c, br + dr, bc + dc, b);
+}
+
 static int div_round(int n, int d) { /* divide_and_round, mcomp.c:2853-2855 */
   return ((n < 0) ^ (d < 0)) ? ((n - d / 2) / d) : ((n + d / 2) / d);
 }
 
 /* forced_stop: 0 EIGHTH_PEL, 1 QUARTER_PEL, 2 HALF_PEL, 3 FULL_PEL;
- * method 1 SUBPEL_TREE_PRUNED, 2 SUBPEL_TREE_PRUNED_MORE; cl NULL or the
+ * method 0 SUBPEL_TREE (bilinear error, USE_2_TAPS_ORIG), 1 SUBPEL_TREE_PRUNED,
+ * 2 SUBPEL_TREE_PRUNED_MORE; cl NULL or the
  * full-pel cost list */
 static void sp_search(const SpCtx *c, int method, int forced_stop, int allow_hp, int iters,
                       const int32_t *cl, OrcSubpelResult *out) {
@@ -125,7 +151,11 @@ static void sp_search(const SpCtx *c, int method, int forced_stop, int allow_hp,
   b.distortion = (int)v;
   b.sse1 = sse;
   b.besterr = v + (unsigned)sp_mv_cost(c, b.row, b.col);
-  if (forced_stop != 3) {
+  if (method == 0) { /* av1_find_best_sub_pixel_tree (mcomp.c:3128-3194), no repeat list */
+    const int round = (3 - forced_stop) < (3 - !allow_hp) ? 3 - forced_stop : 3 - !allow_hp;
+    int hstep = 4;
+    for (int it = 0; it < round; ++it, hstep >>= 1) sp_tree_level(c, hstep, iters, &b);
+  } else if (forced_stop != 3) {
     int hstep = 4; /* INIT_SUBPEL_STEP_SIZE */
     const int cl_ok = cl && cl[0] != INT_MAX && cl[1] != INT_MAX && cl[2] != INT_MAX &&
                       cl[3] != INT_MAX && cl[4] != INT_MAX;

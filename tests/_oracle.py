@@ -464,8 +464,9 @@ def full_pixel_search_batch(src, ref, stride, w, h, jobs, method="diamond", step
 def subpel_search_batch(src, ref, stride, w, h, jobs, method=2, forced_stop=0, allow_hp=False,
                         iters=1, mv_cost_type=3, error_per_bit=0, mvjcost=None, mvcost=None,
                         cost_lists=None, threads=1):
-    """orc_subpel_search_batch: SUBPEL_TREE_PRUNED (method 1) /
-    _PRUNED_MORE (2) with any mv cost and optional full-pel cost lists."""
+    """orc_subpel_search_batch: SUBPEL_TREE (method 0, bilinear error),
+    SUBPEL_TREE_PRUNED (1) / _PRUNED_MORE (2) with any mv cost and optional
+    full-pel cost lists."""
     L = lib()
     fn = L.orc_subpel_search_batch
     fn.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_int,

@@ -710,6 +710,9 @@ SP_CASES = [  # (subpel method, allow_hp, forced_stop, iters_per_step, cost type
     ("PRUNED", 1, "EIGHTH_PEL", 1, "MV_COST_ENTROPY", 1),
     ("PRUNED", 0, "HALF_PEL", 2, "MV_COST_ENTROPY", 1),
     ("PRUNED", 1, "EIGHTH_PEL", 2, "MV_COST_NONE", 0),
+    ("TREE", 1, "EIGHTH_PEL", 2, "MV_COST_ENTROPY", 0),
+    ("TREE", 0, "QUARTER_PEL", 1, "MV_COST_L1_HDRES", 0),
+    ("TREE", 1, "EIGHTH_PEL", 1, "MV_COST_NONE", 0),
 ]
 SP_SIZES = {(16, 16): 6, (8, 8): 5, (32, 32): 4, (64, 64): 2, (16, 8): 3, (8, 32): 2,
             (32, 16): 2, (128, 128): 1, (4, 4): 3}
@@ -723,7 +726,8 @@ def gen_subpel():
     F = dict(np.load(os.path.join(HERE, "fix_mcomp.npz")))
     tu = C.TU(REF, ["aom_dsp/variance.c", "av1/encoder/mcomp.c"], C.reference_defines(REF))
     check_errors(tu, ["av1_find_best_sub_pixel_tree_pruned_more",
-                      "av1_find_best_sub_pixel_tree_pruned", "av1_set_subpel_mv_search_range"])
+                      "av1_find_best_sub_pixel_tree_pruned", "av1_find_best_sub_pixel_tree",
+                      "av1_set_subpel_mv_search_range"])
     E = tu.enums
     W, H, BORDER, NREF = (int(v) for v in F["geom"])
     src_np, refs_np = F["src"], F["refs"]
@@ -790,7 +794,9 @@ def gen_subpel():
                 rbuf = tu.struct_obj("struct buf_2d")
                 _set(rbuf.buf[0], buf=C.Pointer(ref_bufs[k].buf, org + by * stride + bx, C.UCHAR),
                      stride=stride, width=W, height=H)
-                _set(vp, vfp=vtab, subpel_search_type=E["USE_2_TAPS"], w=bw, h=bh)
+                # SUBPEL_TREE takes the svf (bilinear) error only with USE_2_TAPS_ORIG
+                _set(vp, vfp=vtab, subpel_search_type=E["USE_2_TAPS_ORIG" if meth == "TREE"
+                                                         else "USE_2_TAPS"], w=bw, h=bh)
                 _set(_get(vp, "ms_buffers"), ref=rbuf, src=sbuf, second_pred=None, mask=None,
                      mask_stride=0, inv_mask=0, wsrc=None, obmc_mask=None)
                 smv = C.new_obj(tu.ctype("MV"))
@@ -798,7 +804,7 @@ def gen_subpel():
                 _set(smv, row=start[0], col=start[1])
                 best = tu.struct_obj("MV")
                 dist, sse = tu.buffer("int", 1), tu.buffer("unsigned int", 1)
-                f = "av1_find_best_sub_pixel_tree_" + meth.lower()
+                f = "av1_find_best_sub_pixel_tree" + ("" if meth == "TREE" else "_" + meth.lower())
                 err = tu.func(f)(xd, None, ms, smv, best, dist, sse, None)
                 bm = best.buf[0]
                 jobs.append([bw, bh, ci, by, bx, k, ref_mv[0], ref_mv[1], start[0], start[1]] +
@@ -811,7 +817,8 @@ def gen_subpel():
                                   "row_min", "row_max", "error_per_bit", "best_row", "best_col",
                                   "besterr", "distortion", "sse", "cl0", "cl1", "cl2", "cl3",
                                   "cl4"])
-    out["cases"] = np.array([[{"PRUNED": 1, "PRUNED_MORE": 2}[m], hp, E[fs], it, E[ct], cl]
+    out["cases"] = np.array([[{"TREE": 0, "PRUNED": 1, "PRUNED_MORE": 2}[m], hp, E[fs], it, E[ct],
+                              cl]
                              for m, hp, fs, it, ct, cl in SP_CASES], np.int32)
     np.savez_compressed(os.path.join(HERE, "fix_subpel.npz"), **out)
 

@@ -68,7 +68,7 @@ def test_full_pixel_search_rejects(F):
 
 def test_subpel_search_vs_reference(F):
     """lavish_find_best_sub_pixel_tree_batch against
-    av1_find_best_sub_pixel_tree_pruned / _pruned_more executed from the
+    av1_find_best_sub_pixel_tree (USE_2_TAPS_ORIG) / _pruned / _pruned_more executed from the
     reference (tests/golden/fix_subpel.npz): entropy (hp / lp tables), L1 and
     none mv costs, with and without the full-pel cost list, forced_stop and
     iters_per_step variants -- best mv, besterr, distortion, sse bit-exact."""
@@ -84,7 +84,7 @@ def test_subpel_search_vs_reference(F):
         meth, hp, fstop, iters, ctype, use_cl = (int(v) for v in case)
         cp = costs["hp" if hp else "lp"].cost_params(0, epb, ctype)
         out = M.find_best_sub_pixel_tree_batch(
-            src, refs, bw, bh, M.to_device(rec), cp, {1: "pruned", 2: "pruned_more"}[meth],
+            src, refs, bw, bh, M.to_device(rec), cp, {0: "tree", 1: "pruned", 2: "pruned_more"}[meth],
             fstop, bool(hp), iters, cost_lists=torch.from_numpy(cls).cuda() if use_cl else None)
         torch.cuda.synchronize()
         res = M.subpel_results_numpy(out)

@@ -75,3 +75,28 @@ def test_subpel_after_diamond_matches(planes):
     b = M.subpel_results_numpy(M.subpel_after_diamond(ts, tr, 16, 16, M.to_device(blank), fp, 0,
                                                       False))
     np.testing.assert_array_equal(a, b)
+
+
+@pytest.mark.parametrize("bw,bh", [(16, 16), (8, 8), (64, 64), (4, 4), (128, 128), (32, 8)])
+@pytest.mark.parametrize("fs,hp,iters", [(0, True, 2), (0, False, 1), (1, False, 2)])
+def test_subpel_tree_vs_oracle(planes, bw, bh, fs, hp, iters):
+    """SUBPEL_TREE (av1_find_best_sub_pixel_tree with USE_2_TAPS_ORIG) on the
+    general entry point against the oracle, L1 cost around a nonzero ref mv."""
+    import torch
+    import lavish_dsp.motion as M
+    W, H, src, refs = planes
+    stride = src.shape[1]
+    ref_mv = (13, -21)
+    jobs = M.frame_jobs(W, H, stride, BORDER, src.size, bw, bh, refs.shape[0], ref_mv)
+    ts, tr = torch.from_numpy(src).cuda(), torch.from_numpy(refs).cuda()
+    full = M.results_numpy(M.diamond_search_batch(ts, tr, bw, bh, M.to_device(jobs), 0, 3,
+                                                  bh >= 16))
+    sj = M.subpel_jobs(W, H, BORDER, bw, bh, jobs, full, ref_mv)
+    got = M.subpel_results_numpy(M.find_best_sub_pixel_tree_batch(
+        ts, tr, bw, bh, M.to_device(sj), M.l1_cost_params(), "tree", fs, hp, iters))
+    exp = O.subpel_search_batch(src.reshape(-1), refs.reshape(-1), stride, bw, bh, sj, 0, fs,
+                                hp, iters, 3, threads=8)
+    for f in ("best_row", "best_col", "besterr", "distortion", "sse"):
+        np.testing.assert_array_equal(got[f], exp[f], err_msg=f)
+    moved = (got["best_row"] != sj["start_row"]) | (got["best_col"] != sj["start_col"])
+    assert moved.mean() > 0.1
