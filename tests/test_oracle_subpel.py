@@ -65,3 +65,30 @@ def test_subpel_properties(setup, fs, hp, iters):
         assert (res["best_row"] == sj["start_row"]).all()
     else:
         assert ((res["best_row"] != sj["start_row"]) | (res["best_col"] != sj["start_col"])).any()
+
+
+@pytest.mark.parametrize("fs,hp,iters", [(0, True, 2), (0, False, 1), (2, False, 2)])
+def test_subpel_tree_properties(setup, fs, hp, iters):
+    """SUBPEL_TREE (method 0, USE_2_TAPS_ORIG) keeps the same invariants; its
+    control flow is pinned by the fix_subpel.npz TREE cases."""
+    import ctypes
+    M, src, refs, stride, sj = setup
+    L = O.lib()
+    L.orc_sub_pixel_variance.restype = ctypes.c_uint
+    L.orc_sub_pixel_variance.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
+                                         ctypes.c_int, ctypes.c_void_p, ctypes.c_int,
+                                         ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
+    res = O.subpel_search_batch(src.reshape(-1), refs.reshape(-1), stride, 16, 16, sj, 0, fs, hp,
+                                iters, 3, threads=8)
+    pm = O.subpel_search_batch(src.reshape(-1), refs.reshape(-1), stride, 16, 16, sj, 2, fs, hp,
+                               iters, 3, threads=8)
+    step = {0: 1 if hp else 2, 1: 2, 2: 4}[fs]
+    for k in range(0, len(sj), 7):
+        jb, r = sj[k], res[k]
+        row, col = int(r["best_row"]), int(r["best_col"])
+        assert row % step == 0 and col % step == 0
+        assert jb["row_min"] <= row <= jb["row_max"] and jb["col_min"] <= col <= jb["col_max"]
+        cost, var = _svf_cost(src, refs, stride, jb, row, col, 1)
+        assert int(r["besterr"]) == cost and int(r["distortion"]) == var
+    # the extra second-level checks: not worse than PRUNED_MORE in aggregate on this content
+    assert res["besterr"].astype(np.int64).sum() <= pm["besterr"].astype(np.int64).sum()
