@@ -22,6 +22,9 @@
 
 #include "lavish_internal.h"
 
+// the tap loops' unroll pragmas only take effect in the T8 instances
+#pragma clang diagnostic ignored "-Wpass-failed"
+
 namespace lavish {
 namespace {
 
@@ -43,7 +46,9 @@ struct CompArgs {
 
 // a.bpw blocks per 256-thread workgroup (small blocks share one), each with
 // 256 / bpw threads and its own slice of the dynamic LDS intermediate
-template <typename Pix>
+// T8: both filters have 8 taps (every block wider and taller than 4): the tap
+// loops unroll, so a pixel's 8 loads are in flight together
+template <typename Pix, bool T8>
 __global__ __launch_bounds__(256) void compound_kernel(CompArgs a) {
   extern __shared__ int16_t im_all[];
   const int nwg = gridDim.x;  // multiple of 8: consecutive blocks share an XCD's L2
@@ -59,18 +64,20 @@ __global__ __launch_bounds__(256) void compound_kernel(CompArgs a) {
   Pix* dst = (Pix*)a.dst + jb.dst_off;
   uint16_t* conv = a.conv + jb.conv_off;
   const int w = a.w, lw = a.lw;
-  const int fo_x = a.tx / 2 - 1, fo_y = a.ty / 2 - 1;
+  const int ntx = T8 ? 8 : a.tx, nty = T8 ? 8 : a.ty;
+  const int fo_x = ntx / 2 - 1, fo_y = nty / 2 - 1;
   const int16_t* fx = a.fx[sx];
   const int16_t* fy = a.fy[sy];
   int16_t* im = im_all + sub * (a.h + a.ty - 1) * w;
   if (a.any2d) {  // horizontal pass of the 2-D form into LDS (w is a power of two)
     if (path == 3) {
-      const int ih = a.h + a.ty - 1;
+      const int ih = a.h + nty - 1;
       for (int e = t; e < ih * w; e += tpb) {
         const int y = e >> lw, x = e & (w - 1);
         const Pix* row = src + (int64_t)(y - fo_y) * a.src_stride + x - fo_x;
         int32_t s = 1 << (a.bd + kFBits - 1);
-        for (int k = 0; k < a.tx; ++k) s += fx[k] * (int)row[k];
+#pragma unroll
+        for (int k = 0; k < ntx; ++k) s += fx[k] * (int)row[k];
         im[e] = (int16_t)((s + ((1 << a.r0) >> 1)) >> a.r0);
       }
     }
@@ -87,17 +94,20 @@ __global__ __launch_bounds__(256) void compound_kernel(CompArgs a) {
     } else if (path == 1) {
       const Pix* row = src + (int64_t)y * a.src_stride + x - fo_x;
       int32_t s = 0;
-      for (int k = 0; k < a.tx; ++k) s += fx[k] * (int)row[k];
+#pragma unroll
+      for (int k = 0; k < ntx; ++k) s += fx[k] * (int)row[k];
       res = (1 << (kFBits - a.r1)) * ((s + ((1 << a.r0) >> 1)) >> a.r0) + a.round_offset;
     } else if (path == 2) {
       const Pix* col = src + (int64_t)(y - fo_y) * a.src_stride + x;
       int32_t s = 0;
-      for (int k = 0; k < a.ty; ++k) s += fy[k] * (int)col[(int64_t)k * a.src_stride];
+#pragma unroll
+      for (int k = 0; k < nty; ++k) s += fy[k] * (int)col[(int64_t)k * a.src_stride];
       s *= 1 << (kFBits - a.r0);
       res = ((s + ((1 << a.r1) >> 1)) >> a.r1) + a.round_offset;
     } else {
       int32_t s = 1 << a.offset_bits;
-      for (int k = 0; k < a.ty; ++k) s += fy[k] * (int)im[((y + k) << lw) + x];
+#pragma unroll
+      for (int k = 0; k < nty; ++k) s += fy[k] * (int)im[((y + k) << lw) + x];
       res = (uint16_t)((s + ((1 << a.r1) >> 1)) >> a.r1);
     }
     uint16_t* c = conv + (int64_t)y * a.conv_stride + x;
@@ -165,10 +175,14 @@ int compound_batch(const void* src, int src_stride, void* dst, int dst_stride, u
   const size_t lds = (size_t)a.bpw * (h + a.ty - 1) * w * sizeof(int16_t);
   int nwg = (njobs + a.bpw - 1) / a.bpw;
   nwg = (nwg + 7) & ~7;
-  if (highbd)
-    hipLaunchKernelGGL(compound_kernel<uint16_t>, dim3(nwg), dim3(256), lds, s, a);
-  else
-    hipLaunchKernelGGL(compound_kernel<uint8_t>, dim3(nwg), dim3(256), lds, s, a);
+  const bool t8 = a.tx == 8 && a.ty == 8;
+  if (highbd) {
+    if (t8) hipLaunchKernelGGL((compound_kernel<uint16_t, true>), dim3(nwg), dim3(256), lds, s, a);
+    else hipLaunchKernelGGL((compound_kernel<uint16_t, false>), dim3(nwg), dim3(256), lds, s, a);
+  } else {
+    if (t8) hipLaunchKernelGGL((compound_kernel<uint8_t, true>), dim3(nwg), dim3(256), lds, s, a);
+    else hipLaunchKernelGGL((compound_kernel<uint8_t, false>), dim3(nwg), dim3(256), lds, s, a);
+  }
   LAVISH_CHECK(hipGetLastError());
   return 0;
 }
