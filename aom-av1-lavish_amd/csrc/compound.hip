@@ -22,8 +22,6 @@
 
 #include "lavish_internal.h"
 
-// the tap loops' unroll pragmas only take effect in the T8 instances
-#pragma clang diagnostic ignored "-Wpass-failed"
 
 namespace lavish {
 namespace {
@@ -65,9 +63,21 @@ __global__ __launch_bounds__(256) void compound_kernel(CompArgs a) {
   uint16_t* conv = a.conv + jb.conv_off;
   const int w = a.w, lw = a.lw;
   const int ntx = T8 ? 8 : a.tx, nty = T8 ? 8 : a.ty;
+  constexpr int kUnroll = T8 ? 8 : 1;  // full unroll of the T8 tap loops only
   const int fo_x = ntx / 2 - 1, fo_y = nty / 2 - 1;
-  const int16_t* fx = a.fx[sx];
-  const int16_t* fy = a.fy[sy];
+  const int16_t* fxp = a.fx[sx];
+  const int16_t* fyp = a.fy[sy];
+  // T8: the block's two tap rows live in registers for all its pixels
+  int16_t fx[T8 ? 8 : 1], fy[T8 ? 8 : 1];
+  if (T8) {
+#pragma unroll
+    for (int k = 0; k < (T8 ? 8 : 1); ++k) {
+      fx[k] = fxp[k];
+      fy[k] = fyp[k];
+    }
+  }
+#define FX(k) (T8 ? fx[(k) & (T8 ? 7 : 0)] : fxp[k])
+#define FY(k) (T8 ? fy[(k) & (T8 ? 7 : 0)] : fyp[k])
   int16_t* im = im_all + sub * (a.h + a.ty - 1) * w;
   if (a.any2d) {  // horizontal pass of the 2-D form into LDS (w is a power of two)
     if (path == 3) {
@@ -76,8 +86,8 @@ __global__ __launch_bounds__(256) void compound_kernel(CompArgs a) {
         const int y = e >> lw, x = e & (w - 1);
         const Pix* row = src + (int64_t)(y - fo_y) * a.src_stride + x - fo_x;
         int32_t s = 1 << (a.bd + kFBits - 1);
-#pragma unroll
-        for (int k = 0; k < ntx; ++k) s += fx[k] * (int)row[k];
+#pragma unroll kUnroll
+        for (int k = 0; k < ntx; ++k) s += FX(k) * (int)row[k];
         im[e] = (int16_t)((s + ((1 << a.r0) >> 1)) >> a.r0);
       }
     }
@@ -94,20 +104,20 @@ __global__ __launch_bounds__(256) void compound_kernel(CompArgs a) {
     } else if (path == 1) {
       const Pix* row = src + (int64_t)y * a.src_stride + x - fo_x;
       int32_t s = 0;
-#pragma unroll
-      for (int k = 0; k < ntx; ++k) s += fx[k] * (int)row[k];
+#pragma unroll kUnroll
+      for (int k = 0; k < ntx; ++k) s += FX(k) * (int)row[k];
       res = (1 << (kFBits - a.r1)) * ((s + ((1 << a.r0) >> 1)) >> a.r0) + a.round_offset;
     } else if (path == 2) {
       const Pix* col = src + (int64_t)(y - fo_y) * a.src_stride + x;
       int32_t s = 0;
-#pragma unroll
-      for (int k = 0; k < nty; ++k) s += fy[k] * (int)col[(int64_t)k * a.src_stride];
+#pragma unroll kUnroll
+      for (int k = 0; k < nty; ++k) s += FY(k) * (int)col[(int64_t)k * a.src_stride];
       s *= 1 << (kFBits - a.r0);
       res = ((s + ((1 << a.r1) >> 1)) >> a.r1) + a.round_offset;
     } else {
       int32_t s = 1 << a.offset_bits;
-#pragma unroll
-      for (int k = 0; k < nty; ++k) s += fy[k] * (int)im[((y + k) << lw) + x];
+#pragma unroll kUnroll
+      for (int k = 0; k < nty; ++k) s += FY(k) * (int)im[((y + k) << lw) + x];
       res = (uint16_t)((s + ((1 << a.r1) >> 1)) >> a.r1);
     }
     uint16_t* c = conv + (int64_t)y * a.conv_stride + x;
@@ -121,6 +131,8 @@ __global__ __launch_bounds__(256) void compound_kernel(CompArgs a) {
     const int v = (tt + ((1 << a.round_bits) >> 1)) >> a.round_bits;
     dst[(int64_t)y * a.dst_stride + x] = (Pix)min(max(v, 0), pmax);
   }
+#undef FX
+#undef FY
 }
 
 }  // namespace
