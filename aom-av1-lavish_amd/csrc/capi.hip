@@ -184,7 +184,14 @@ void shim_reject(const char* what, int rc) {
 void* StreamScratch::acquire(size_t bytes, hipStream_t s) {
   int dev = 0;
   LAVISH_CHECK(hipGetDevice(&dev));
-  if (device != dev) {  // one device per process; a switch starts afresh
+  if (device != dev) {  // a device switch frees the old device's buffer and starts afresh
+    if (device >= 0) {
+      LAVISH_CHECK(hipSetDevice(device));
+      if (pending) LAVISH_CHECK(hipEventSynchronize(done));
+      if (ptr) LAVISH_CHECK(hipFree(ptr));
+      LAVISH_CHECK(hipEventDestroy(done));
+      LAVISH_CHECK(hipSetDevice(dev));
+    }
     ptr = nullptr;
     cap = 0;
     pending = false;

@@ -22,6 +22,7 @@
 // about once (the overlap hits L2: consecutive jobs share an XCD).  12-tap
 // kernels (MULTITAP_SHARP2, temporal filtering only) take a direct,
 // per-pixel path.
+#include "interp_kernels.h"
 #include "lavish_internal.h"
 
 namespace lavish {
@@ -35,78 +36,11 @@ struct IJob {
 };
 static_assert(sizeof(IJob) == sizeof(LavishInterPredJob) && sizeof(IJob) == 32, "job layout");
 
-// [kind][phase][tap]: 0 REGULAR 1 SMOOTH 2 SHARP 3 BILINEAR, 4 / 5 the
-// 4-tap REGULAR / SMOOTH kernels (8-tap layout) -- filter.h:111-243
-__constant__ int16_t kK8[6][16][8] = {
-  { { 0, 0, 0, 128, 0, 0, 0, 0 }, { 0, 2, -6, 126, 8, -2, 0, 0 },
-    { 0, 2, -10, 122, 18, -4, 0, 0 }, { 0, 2, -12, 116, 28, -8, 2, 0 },
-    { 0, 2, -14, 110, 38, -10, 2, 0 }, { 0, 2, -14, 102, 48, -12, 2, 0 },
-    { 0, 2, -16, 94, 58, -12, 2, 0 }, { 0, 2, -14, 84, 66, -12, 2, 0 },
-    { 0, 2, -14, 76, 76, -14, 2, 0 }, { 0, 2, -12, 66, 84, -14, 2, 0 },
-    { 0, 2, -12, 58, 94, -16, 2, 0 }, { 0, 2, -12, 48, 102, -14, 2, 0 },
-    { 0, 2, -10, 38, 110, -14, 2, 0 }, { 0, 2, -8, 28, 116, -12, 2, 0 },
-    { 0, 0, -4, 18, 122, -10, 2, 0 }, { 0, 0, -2, 8, 126, -6, 2, 0 } },
-  { { 0, 0, 0, 128, 0, 0, 0, 0 }, { 0, 2, 28, 62, 34, 2, 0, 0 },
-    { 0, 0, 26, 62, 36, 4, 0, 0 }, { 0, 0, 22, 62, 40, 4, 0, 0 },
-    { 0, 0, 20, 60, 42, 6, 0, 0 }, { 0, 0, 18, 58, 44, 8, 0, 0 },
-    { 0, 0, 16, 56, 46, 10, 0, 0 }, { 0, -2, 16, 54, 48, 12, 0, 0 },
-    { 0, -2, 14, 52, 52, 14, -2, 0 }, { 0, 0, 12, 48, 54, 16, -2, 0 },
-    { 0, 0, 10, 46, 56, 16, 0, 0 }, { 0, 0, 8, 44, 58, 18, 0, 0 },
-    { 0, 0, 6, 42, 60, 20, 0, 0 }, { 0, 0, 4, 40, 62, 22, 0, 0 },
-    { 0, 0, 4, 36, 62, 26, 0, 0 }, { 0, 0, 2, 34, 62, 28, 2, 0 } },
-  { { 0, 0, 0, 128, 0, 0, 0, 0 }, { -2, 2, -6, 126, 8, -2, 2, 0 },
-    { -2, 6, -12, 124, 16, -6, 4, -2 }, { -2, 8, -18, 120, 26, -10, 6, -2 },
-    { -4, 10, -22, 116, 38, -14, 6, -2 }, { -4, 10, -22, 108, 48, -18, 8, -2 },
-    { -4, 10, -24, 100, 60, -20, 8, -2 }, { -4, 10, -24, 90, 70, -22, 10, -2 },
-    { -4, 12, -24, 80, 80, -24, 12, -4 }, { -2, 10, -22, 70, 90, -24, 10, -4 },
-    { -2, 8, -20, 60, 100, -24, 10, -4 }, { -2, 8, -18, 48, 108, -22, 10, -4 },
-    { -2, 6, -14, 38, 116, -22, 10, -4 }, { -2, 6, -10, 26, 120, -18, 8, -2 },
-    { -2, 4, -6, 16, 124, -12, 6, -2 }, { 0, 2, -2, 8, 126, -6, 2, -2 } },
-  { { 0, 0, 0, 128, 0, 0, 0, 0 }, { 0, 0, 0, 120, 8, 0, 0, 0 },
-    { 0, 0, 0, 112, 16, 0, 0, 0 }, { 0, 0, 0, 104, 24, 0, 0, 0 },
-    { 0, 0, 0, 96, 32, 0, 0, 0 }, { 0, 0, 0, 88, 40, 0, 0, 0 },
-    { 0, 0, 0, 80, 48, 0, 0, 0 }, { 0, 0, 0, 72, 56, 0, 0, 0 },
-    { 0, 0, 0, 64, 64, 0, 0, 0 }, { 0, 0, 0, 56, 72, 0, 0, 0 },
-    { 0, 0, 0, 48, 80, 0, 0, 0 }, { 0, 0, 0, 40, 88, 0, 0, 0 },
-    { 0, 0, 0, 32, 96, 0, 0, 0 }, { 0, 0, 0, 24, 104, 0, 0, 0 },
-    { 0, 0, 0, 16, 112, 0, 0, 0 }, { 0, 0, 0, 8, 120, 0, 0, 0 } },
-  { { 0, 0, 0, 128, 0, 0, 0, 0 }, { 0, 0, -4, 126, 8, -2, 0, 0 },
-    { 0, 0, -8, 122, 18, -4, 0, 0 }, { 0, 0, -10, 116, 28, -6, 0, 0 },
-    { 0, 0, -12, 110, 38, -8, 0, 0 }, { 0, 0, -12, 102, 48, -10, 0, 0 },
-    { 0, 0, -14, 94, 58, -10, 0, 0 }, { 0, 0, -12, 84, 66, -10, 0, 0 },
-    { 0, 0, -12, 76, 76, -12, 0, 0 }, { 0, 0, -10, 66, 84, -12, 0, 0 },
-    { 0, 0, -10, 58, 94, -14, 0, 0 }, { 0, 0, -10, 48, 102, -12, 0, 0 },
-    { 0, 0, -8, 38, 110, -12, 0, 0 }, { 0, 0, -6, 28, 116, -10, 0, 0 },
-    { 0, 0, -4, 18, 122, -8, 0, 0 }, { 0, 0, -2, 8, 126, -4, 0, 0 } },
-  { { 0, 0, 0, 128, 0, 0, 0, 0 }, { 0, 0, 30, 62, 34, 2, 0, 0 },
-    { 0, 0, 26, 62, 36, 4, 0, 0 }, { 0, 0, 22, 62, 40, 4, 0, 0 },
-    { 0, 0, 20, 60, 42, 6, 0, 0 }, { 0, 0, 18, 58, 44, 8, 0, 0 },
-    { 0, 0, 16, 56, 46, 10, 0, 0 }, { 0, 0, 14, 54, 48, 12, 0, 0 },
-    { 0, 0, 12, 52, 52, 12, 0, 0 }, { 0, 0, 12, 48, 54, 14, 0, 0 },
-    { 0, 0, 10, 46, 56, 16, 0, 0 }, { 0, 0, 8, 44, 58, 18, 0, 0 },
-    { 0, 0, 6, 42, 60, 20, 0, 0 }, { 0, 0, 4, 40, 62, 22, 0, 0 },
-    { 0, 0, 4, 36, 62, 26, 0, 0 }, { 0, 0, 2, 34, 62, 30, 0, 0 } },
-};
+// filter.h:111-243 (interp_kernels.h)
+__constant__ int16_t kK8[6][16][8] = LAVISH_K8_INIT;
 
 // MULTITAP_SHARP2
-__constant__ int16_t kK12[16][12] = {
-  { 0, 0, 0, 0, 0, 128, 0, 0, 0, 0, 0, 0 },
-  { 0, 1, -2, 3, -7, 127, 8, -4, 2, -1, 1, 0 },
-  { -1, 2, -3, 6, -13, 124, 18, -8, 4, -2, 2, -1 },
-  { -1, 3, -4, 8, -18, 120, 28, -12, 7, -4, 2, -1 },
-  { -1, 3, -6, 10, -21, 115, 38, -15, 8, -5, 3, -1 },
-  { -2, 4, -6, 12, -24, 108, 49, -18, 10, -6, 3, -2 },
-  { -2, 4, -7, 13, -25, 100, 60, -21, 11, -7, 4, -2 },
-  { -2, 4, -7, 13, -26, 91, 71, -24, 13, -7, 4, -2 },
-  { -2, 4, -7, 13, -25, 81, 81, -25, 13, -7, 4, -2 },
-  { -2, 4, -7, 13, -24, 71, 91, -26, 13, -7, 4, -2 },
-  { -2, 4, -7, 11, -21, 60, 100, -25, 13, -7, 4, -2 },
-  { -2, 3, -6, 10, -18, 49, 108, -24, 12, -6, 4, -2 },
-  { -1, 3, -5, 8, -15, 38, 115, -21, 10, -6, 3, -1 },
-  { -1, 2, -4, 7, -12, 28, 120, -18, 8, -4, 3, -1 },
-  { -1, 2, -2, 4, -8, 18, 124, -13, 6, -3, 2, -1 },
-  { 0, 1, -1, 2, -4, 8, 127, -7, 3, -2, 1, 0 },
-};
+__constant__ int16_t kK12[16][12] = LAVISH_K12_INIT;
 
 struct IpArgs {
   const void* ref;
@@ -598,3 +532,25 @@ extern "C" int lavish_build_inter_pred_after_subpel(const void* ref, int ref_str
                           mvs, dst, dst_stride, bit_depth, highbd, nullptr, 0, 0,
                           (hipStream_t)stream);
 }
+
+// Host copy of the same kernels: av1_get_interp_filter_params_with_block_size
+// (av1/common/filter.h:253-259) as data -- the kernel rows a caller puts in
+// LavishInterpFilterParams::filter_ptr for (interp_filter, block dimension).
+static const int16_t kK8Host[6][16][8] = LAVISH_K8_INIT;
+static const int16_t kK12Host[16][12] = LAVISH_K12_INIT;
+
+extern "C" int lavish_interp_kernels(int interp_filter, int size, int16_t* out) {
+  if (interp_filter < 0 || interp_filter > 4 || size <= 0 || out == nullptr) return -1;
+  if (interp_filter == 4) {  // MULTITAP_SHARP2: 12 taps at every size
+    for (int p = 0; p < 16; ++p)
+      for (int k = 0; k < 12; ++k) out[p * 12 + k] = kK12Host[p][k];
+    return 12;
+  }
+  // av1_interp_4tap for sizes <= 4: REGULAR / SMOOTH / SHARP(-> REGULAR 4) / BILINEAR
+  static const int k4[4] = {4, 5, 4, 3};
+  const int kind = size <= 4 ? k4[interp_filter] : interp_filter;
+  for (int p = 0; p < 16; ++p)
+    for (int k = 0; k < 8; ++k) out[p * 8 + k] = kK8Host[kind][p][k];
+  return 8;
+}
+

@@ -96,6 +96,15 @@ struct StreamScratch {
   void release(hipStream_t s);
 };
 
+// Under-aligned word vectors for byte-addressed loads (pixel rows at any byte
+// offset).  aligned(1) makes no alignment promise to the compiler, so it
+// cannot split, merge or scalarise on an assumed 8 / 16-byte boundary; the
+// queues run in unaligned-access mode, so each still lowers to one
+// global_load_dwordx2 / x4 (or ds_read_b64 / b128) at the byte address.
+typedef uint32_t u32x2u __attribute__((ext_vector_type(2), aligned(1)));
+typedef uint32_t u32x4u __attribute__((ext_vector_type(4), aligned(1)));
+typedef uint32_t u32u __attribute__((aligned(1)));
+
 // Wave-local memory ordering: lanes of one wave exchange data through LDS
 // with no workgroup barrier (each wave owns its tile); these fences only stop
 // the compiler from moving LDS accesses across the exchange point (LDS ops of

@@ -49,23 +49,23 @@ __device__ __forceinline__ void load_row(const uint8_t* p, uint32_t (&out)[DW]) 
   // global address space: global_load (not flat: no LDS-aperture check and
   // no lgkmcnt dependency)
   if constexpr (DW % 4 == 0) {
-    typedef const __attribute__((address_space(1))) u32x4* gptr4;
+    typedef const __attribute__((address_space(1))) u32x4u* gptr4;
     const gptr4 q = (gptr4)p;
 #pragma unroll
     for (int i = 0; i < DW / 4; ++i) {
-      const u32x4 v = q[i];
+      const u32x4u v = q[i];
       out[4 * i] = v.x;
       out[4 * i + 1] = v.y;
       out[4 * i + 2] = v.z;
       out[4 * i + 3] = v.w;
     }
   } else if constexpr (DW == 2) {
-    typedef const __attribute__((address_space(1))) u32x2* gptr2;
-    const u32x2 v = *(gptr2)p;
+    typedef const __attribute__((address_space(1))) u32x2u* gptr2;
+    const u32x2u v = *(gptr2)p;
     out[0] = v.x;
     out[1] = v.y;
   } else {
-    typedef const __attribute__((address_space(1))) uint32_t* gptr;
+    typedef const __attribute__((address_space(1))) u32u* gptr;
 #pragma unroll
     for (int i = 0; i < DW; ++i) out[i] = ((gptr)p)[i];
   }
@@ -413,18 +413,18 @@ struct Search {
         if constexpr (G::DW % 4 == 0) {
 #pragma unroll
           for (int i = 0; i < G::DW / 4; ++i) {
-            const u32x4 v = ((const __attribute__((address_space(3))) u32x4*)p)[i];
+            const u32x4u v = ((const __attribute__((address_space(3))) u32x4u*)p)[i];
             w[4 * i] = v.x;
             w[4 * i + 1] = v.y;
             w[4 * i + 2] = v.z;
             w[4 * i + 3] = v.w;
           }
         } else if constexpr (G::DW == 2) {
-          const u32x2 v = *(const __attribute__((address_space(3))) u32x2*)p;
+          const u32x2u v = *(const __attribute__((address_space(3))) u32x2u*)p;
           w[0] = v.x;
           w[1] = v.y;
         } else {
-          w[0] = *(const __attribute__((address_space(3))) uint32_t*)p;
+          w[0] = *(const __attribute__((address_space(3))) u32u*)p;
         }
 #pragma unroll
         for (int i = 0; i < G::DW; ++i) acc = sad4(s[k][i], w[i], acc);
@@ -449,7 +449,7 @@ struct Search {
             const int wr = row - wr0 + y;
             const int xb = col - wc0 + 4 * x4 + (int)(((uint32_t)wbase + __umul24(wr, c.rs & 3)) & 3);
             const lds_u8 p = (lds_u8)win + (wr * WN::DW * 4 + xb);
-            var_acc(sv[v], *(const __attribute__((address_space(3))) uint32_t*)p, sum, sse);
+            var_acc(sv[v], *(const __attribute__((address_space(3))) u32u*)p, sum, sse);
           }
         }
         return var_finish<W, H>(c, sum, sse, row, col);

@@ -80,16 +80,14 @@ struct U8Shape {
 };
 
 __device__ __forceinline__ void load_words(const uint8_t* p, int c, uint32_t (&w)[4]) {
-  typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
-  typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
   if (c == 4) {
-    const u32x4 v = *(const __attribute__((address_space(1))) u32x4*)p;
+    const u32x4u v = *(const __attribute__((address_space(1))) u32x4u*)p;
     w[0] = v.x; w[1] = v.y; w[2] = v.z; w[3] = v.w;
   } else if (c == 2) {
-    const u32x2 v = *(const __attribute__((address_space(1))) u32x2*)p;
+    const u32x2u v = *(const __attribute__((address_space(1))) u32x2u*)p;
     w[0] = v.x; w[1] = v.y; w[2] = 0; w[3] = 0;
   } else {
-    w[0] = *(const __attribute__((address_space(1))) uint32_t*)p;
+    w[0] = *(const __attribute__((address_space(1))) u32u*)p;
     w[1] = 0; w[2] = 0; w[3] = 0;
   }
 }

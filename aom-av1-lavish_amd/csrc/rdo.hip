@@ -988,14 +988,17 @@ int rdo_plane_px64(RdoArgs& a, int tx_size, int width, int height, hipStream_t s
                      a.nblocks, a.bw, W, H, max_eob(tx_size), a.stride, jobs);
   LAVISH_CHECK(hipGetLastError());
   rc = inv_txfm_add_batch(a.dqcoeff, tx_size, jobs, a.nblocks, plane, a.stride, a.bd, 1, s);
-  if (rc) return rc;
-  hipLaunchKernelGGL(px64_finish_kernel, dim3(a.nblocks), dim3(256), 0, s, a.src, a.pred,
-                     plane, a.stride, a.bw, W, H, tx_size == 4 ? 1 : 0, a.bd, a.rdmult,
-                     a.out);
-  LAVISH_CHECK(hipGetLastError());
+  if (rc == 0) {
+    hipLaunchKernelGGL(px64_finish_kernel, dim3(a.nblocks), dim3(256), 0, s, a.src, a.pred,
+                       plane, a.stride, a.bw, W, H, tx_size == 4 ? 1 : 0, a.bd, a.rdmult,
+                       a.out);
+    LAVISH_CHECK(hipGetLastError());
+  }
+  // both scratches are released on every path: the copy and the job kernel
+  // are already queued on `s`, so a later acquire must wait for them
   t_px_plane[tx_size].release(s);
   t_px_jobs[tx_size].release(s);
-  return 0;
+  return rc;
 }
 
 int rdo_reconstruct(uint32_t size_mask, const LavishRdoBlock* const* rec,

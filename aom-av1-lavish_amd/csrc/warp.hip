@@ -59,14 +59,14 @@ template <typename Pix>
 __device__ __forceinline__ void load8(const Pix* row, int x, int width, uint32_t (&p)[4]) {
   if (x >= 0 && x + 7 < width) {
     if constexpr (sizeof(Pix) == 1) {
-      const u32x2 w = *(const __attribute__((address_space(1))) u32x2*)(row + x);
+      const u32x2u w = *(const __attribute__((address_space(1))) u32x2u*)(row + x);
       // v_perm_b32: bytes (b0, 0, b1, 0) ... (0x0c selects a zero byte)
       p[0] = __builtin_amdgcn_perm(0u, w.x, 0x0c010c00u);
       p[1] = __builtin_amdgcn_perm(0u, w.x, 0x0c030c02u);
       p[2] = __builtin_amdgcn_perm(0u, w.y, 0x0c010c00u);
       p[3] = __builtin_amdgcn_perm(0u, w.y, 0x0c030c02u);
     } else {
-      const u32x4 w = *(const __attribute__((address_space(1))) u32x4*)(row + x);
+      const u32x4u w = *(const __attribute__((address_space(1))) u32x4u*)(row + x);
       p[0] = w.x;
       p[1] = w.y;
       p[2] = w.z;

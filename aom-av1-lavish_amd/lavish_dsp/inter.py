@@ -67,6 +67,18 @@ for _n in ("av1_convolve_2d_sr_hip", "av1_convolve_x_sr_hip", "av1_convolve_y_sr
            "av1_highbd_convolve_y_sr_hip", "aom_convolve_copy_hip",
            "aom_highbd_convolve_copy_hip"):
     getattr(_lib, _n).restype = None
+_lib.lavish_interp_kernels.argtypes = [_i32, _i32, _vp]
+_lib.lavish_interp_kernels.restype = _i32
+
+
+def interp_kernels(interp_filter, size):
+    """The library's kernel table for av1_get_interp_filter_params_with_block_size
+    (av1/common/filter.h:253-259): int16 [16, taps] (lavish_interp_kernels)."""
+    out = np.zeros(16 * 12, np.int16)
+    taps = _lib.lavish_interp_kernels(interp_filter, size, out.ctypes.data)
+    if taps < 0:
+        raise ValueError("lavish_interp_kernels(%d, %d) rejected" % (interp_filter, size))
+    return out[:16 * taps].reshape(16, taps)
 
 
 def conv_rounds(bd):

@@ -47,6 +47,18 @@ sys.path.insert(0, os.path.join(ROOT, "aom-av1-lavish_amd"))
 
 METRIC = "superblocks/s (fwd_txfm+quant+SAD RDO inner loop), 1080p cpu-used=6, 1/2/4/8 GPU"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
+# int32 VALU peak: 256 CUs x 2 wave64 instructions / cycle (a wave issues a
+# VALU op over 2 cycles, 4 SIMDs) x 64 lanes x 2.4 GHz (MI355X_MICROARCH.md)
+VALU_PEAK_TOPS = 256 * 2 * 64 * 2.4e9 / 1e12
+C4_VALU_JSON = os.path.join(ROOT, "profiles", "c4_valu.json")
+
+
+def metric_name(args):
+    """BASELINE.json's metric for the default (headline) workload; the other
+    workloads name themselves so their lines are never read as the headline."""
+    if args.workload == "rdo":
+        return METRIC
+    return "superblocks/s, workload %s (component bench; not the headline metric)" % args.workload
 
 
 def parse():
@@ -220,6 +232,28 @@ def cpu_baseline_c4(args):
                       % (passes, W, sb, args.workload, threads, dt)}
 
 
+def c4_roofline(ms, W=3840, H=2160):
+    """C4 is VALU-bound (decision mode writes little: hbm_frac ~6 %), so its
+    roofline is int32 VALU lane-operations: the per-step SQ_INSTS_VALU of
+    every kernel of the step (wave instructions x 64 lanes), counted by a
+    rocprofv3 --pmc pass of `bench.py --workload c4` (tools/valu_summary.py ->
+    profiles/c4_valu.json), over the live event-timed step."""
+    if (W, H) != (3840, 2160) or not os.path.exists(C4_VALU_JSON):
+        return None
+    try:
+        v = json.load(open(C4_VALU_JSON))
+    except (ValueError, OSError):
+        return None
+    ops = float(v["valu_instr_per_step"]) * 64
+    achieved = ops / (ms * 1e-3) / 1e12
+    return {"bound": "valu", "kernel": "all kernels of the C4 step (rdo_kernel x5 sizes + "
+            "sb_decide + reconstruction)", "achieved": round(achieved, 2),
+            "peak": round(VALU_PEAK_TOPS, 1), "unit": "Tops (int32 lane-ops)",
+            "frac": round(achieved / VALU_PEAK_TOPS, 4), "traffic": v.get("hbm_bytes_per_step"),
+            "avg_launch_ms": round(ms, 4), "algorithmic_ops_per_launch": round(ops),
+            "counts": "profiles/c4_valu.json (%s)" % v.get("source", "")}
+
+
 def c4_leg(L, steps, warmup, rdmult, qindex, W=3840, H=2160):
     """The C4 step (4K 10-bit RDO of every candidate size / type + per-SB TX
     size + reconstruction, bench.py --workload c4) timed with HIP events on
@@ -246,7 +280,7 @@ def c4_leg(L, steps, warmup, rdmult, qindex, W=3840, H=2160):
     ms = sum(a.elapsed_time(b) for a, b in ev) / steps
     nbytes = c4_algorithmic_bytes(L, W, H)
     sb = sb64_count(W, H)
-    return {"workload": "c4: %dx%d 10-bit frame; fused TX-type RDO (subtract, fwd txfm, highbd "
+    return c4_roofline(ms, W, H), {"workload": "c4: %dx%d 10-bit frame; fused TX-type RDO (subtract, fwd txfm, highbd "
                         "quantize_fp, satd, TX-domain block error, rate_estimator, RDCOST) of "
                         "64x64 DCT, 32x32 DCT+IDTX, 16x16/8x8/4x4 all types; per-SB TX size; "
                         "reconstruction; rdmult %d, qindex %d" % (W, H, rdmult, qindex),
@@ -323,7 +357,7 @@ def main_c4(args):
     c4_bytes = c4_algorithmic_bytes(L, W, H)
     y0, y1 = shard.bands(H, world)[rank]
     line = {
-        "metric": METRIC,
+        "metric": metric_name(args), "workload": args.workload,
         "value": round(value, 2),
         "unit": "SB64/s",
         "n_gpus": world,
@@ -357,6 +391,11 @@ def main_c4(args):
                      "algorithmic_bytes_per_launch": c4_bytes},
     }
     line["roofline"]["frac"] = round(line["roofline"]["achieved"] / HBM_PEAK_GBS, 4)
+    if args.workload == "c4" and world == 1:
+        rv = c4_roofline(step_ms, W, H)  # the bound that applies: int32 VALU
+        if rv is not None:
+            line["hbm_roofline"] = line["roofline"]
+            line["roofline"] = rv
     if rank == 0 and world == 1 and not args.no_cpu:
         line["cpu_baseline"] = cpu_baseline_c4(args)
     if rank == 0:
@@ -478,7 +517,7 @@ def main_inter(args):
             traffic = None
     sb = sb64_count(W, H)
     line = {
-        "metric": METRIC,
+        "metric": metric_name(args), "workload": args.workload,
         "value": round(world * sb * args.steps / elapsed, 2),
         "unit": "SB64/s",
         "n_gpus": world,
@@ -632,7 +671,7 @@ def main_pixel(args):
     nbytes = pixel_bytes(len(jobs_np))
     sb = sb64_count(W, H)
     line = {
-        "metric": METRIC,
+        "metric": metric_name(args), "workload": args.workload,
         "value": round(world * sb * args.steps / elapsed, 2),
         "unit": "SB64/s",
         "n_gpus": world,
@@ -800,7 +839,7 @@ def main_warp(args):
     nbytes = warp_bytes(len(jobs_np))
     sb = sb64_count(W, H)
     line = {
-        "metric": METRIC,
+        "metric": metric_name(args), "workload": args.workload,
         "value": round(world * sb * args.steps / elapsed, 2),
         "unit": "SB64/s",
         "n_gpus": world,
@@ -865,10 +904,11 @@ def compound_setup(W, H, nrefs, seed):
 
 
 def compound_tables():
-    """EIGHTTAP_REGULAR kernels for 16-wide blocks (av1/common/filter.h)."""
-    sys.path.insert(0, os.path.join(ROOT, "tests"))
-    import _oracle as O
-    return np.stack([O.interp_kernel(0, 16, p) for p in range(16)])
+    """EIGHTTAP_REGULAR kernels for 16-wide blocks (av1/common/filter.h), from
+    the library's own table (lavish_interp_kernels, pinned to the reference
+    text by tests/test_capi_cpu.py)."""
+    import lavish_dsp.inter as I
+    return I.interp_kernels(I.EIGHTTAP_REGULAR, 16)
 
 
 COMPOUND_CP = [dict(do_average=0, round_0=3, round_1=7, is_compound=1, use_dist_wtd_comp_avg=0,
@@ -968,7 +1008,7 @@ def main_compound(args):
     nbytes = nj * (2 * 256 + 2 * 512 + 512 + 256 + 2 * 32)
     sb = sb64_count(W, H)
     line = {
-        "metric": METRIC,
+        "metric": metric_name(args), "workload": args.workload,
         "value": round(world * sb * args.steps / elapsed, 2),
         "unit": "SB64/s",
         "n_gpus": world,
@@ -1139,7 +1179,7 @@ def main_tpl(args):
     sb = sb64_count(W, H)
     recs = T.records_numpy(tf.out)
     line = {
-        "metric": METRIC,
+        "metric": metric_name(args), "workload": args.workload,
         "value": round(world * sb * args.steps / elapsed, 2),
         "unit": "SB64/s",
         "n_gpus": world,
@@ -1299,7 +1339,7 @@ def main_rate(args):
     sb = sb64_count(W, H)
     nbytes = c4_algorithmic_bytes(L, W, H) - 8 * W * H  # no reconstruction in this step
     line = {
-        "metric": METRIC,
+        "metric": metric_name(args), "workload": args.workload,
         "value": round(sb * args.steps / elapsed, 2),
         "unit": "SB64/s",
         "n_gpus": 1,
@@ -1521,7 +1561,7 @@ def main():
                     "cost-list surface minimum, iters_per_step %d) chained on the device"
                     % ("1/8" if args.qindex < 128 else "1/4", SUB_ITERS))
     line = {
-        "metric": METRIC,
+        "metric": metric_name(args), "workload": args.workload,
         "value": round(value, 2),
         "unit": "SB64/s",
         "n_gpus": world,
@@ -1556,8 +1596,14 @@ def main():
     if args.workload == "rdo" and not args.no_c4:
         # the 4K 10-bit RDO configuration (BASELINE configs[3]), timed after
         # the headline region so the driver's run records it too
-        line["c4"] = c4_leg(L, max(5, args.steps // 2), max(2, args.warmup), args.rdmult,
-                            args.qindex)
+        roof4, line["c4"] = c4_leg(L, max(5, args.steps // 2), max(2, args.warmup),
+                                   args.rdmult, args.qindex)
+        line["c4"]["roofline"] = roof4
+        if rank == 0 and world == 1 and not args.no_cpu:
+            a4 = argparse.Namespace(**vars(args))
+            a4.workload = "c4"
+            a4.cpu_seconds = max(3.0, args.cpu_seconds / 2)
+            line["c4"]["cpu_baseline"] = cpu_baseline_c4(a4)
     if rank == 0 and world == 1 and not args.no_cpu:
         line["cpu_baseline"] = cpu_baseline(args)
     if rank == 0:

@@ -641,6 +641,13 @@ int lavish_build_inter_pred_batch(const void *ref, int ref_stride, int ref_width
                                   const LavishInterPredJob *jobs, int njobs,
                                   void *dst, int dst_stride, int bit_depth,
                                   int highbd, void *stream);
+/* The interpolation kernels the library itself uses, as data:
+ * av1_get_interp_filter_params_with_block_size(interp_filter, size)
+ * (av1/common/filter.h:253-259) -> out[16][taps] (one row per 1/16 phase),
+ * returns taps (8, or 12 for MULTITAP_SHARP2), -1 on bad arguments.  For
+ * callers that build LavishInterpFilterParams (the RTCD convolve shims, the
+ * compound batch) without the reference's tables at hand.  Host only. */
+int lavish_interp_kernels(int interp_filter, int size, int16_t *out);
 /* The same with job j's mv taken from a sub-pel search result (chained on
  * the device after lavish_subpel_search_batch / _after_diamond). */
 int lavish_build_inter_pred_after_subpel(const void *ref, int ref_stride,

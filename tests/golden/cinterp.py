@@ -27,6 +27,7 @@ tests run under):
 
 Unsupported constructs raise CError at parse or call time (never silently).
 """
+import struct as _s
 import os
 import re
 
@@ -172,10 +173,22 @@ def promote(t):
     return t
 
 
+def to_f32(v):
+    """Round a Python number to the nearest IEEE single (round-to-nearest-even;
+    ints beyond 2^53 rounded directly, not through a double)."""
+    if isinstance(v, int) and abs(v) >= (1 << 53):
+        import numpy as _np
+        return float(_np.float32(_np.int64(v)))  # one correctly rounded cvt
+    return _s.unpack("<f", _s.pack("<f", float(v)))[0]
+
+
 def common_type(a, b):
+    # usual arithmetic conversions (C11 6.3.1.8): with a floating operand the
+    # result is the wider FLOATING type present; an integer operand converts
+    # to it (float + int64 is a float operation)
     if isinstance(a, Flt) or isinstance(b, Flt):
-        return DOUBLE if (getattr(a, "bits", 0) == 64 or getattr(b, "bits", 0) == 64
-                          or not isinstance(a, Flt) or not isinstance(b, Flt)) else FLOAT
+        return DOUBLE if (getattr(a, "bits", 0) == 64 and isinstance(a, Flt)) or \
+            (getattr(b, "bits", 0) == 64 and isinstance(b, Flt)) else FLOAT
     a, b = promote(a), promote(b)
     if a.bits == b.bits and a.signed == b.signed:
         return a
@@ -1264,7 +1277,9 @@ def num_const(text):
     low = s.lower()
     if ("." in s or ("e" in low and not low.startswith("0x"))) or (low.endswith("f") and not low.startswith("0x")):
         v = float(s.rstrip("fFlL"))
-        return v, (FLOAT if low.endswith("f") else DOUBLE)
+        if low.endswith("f"):
+            return to_f32(v), FLOAT
+        return v, DOUBLE
     suf = ""
     while s and s[-1] in "uUlL":
         suf = s[-1].lower() + suf
@@ -1643,8 +1658,7 @@ class TU:
             return dst.wrap
         if isinstance(dst, Flt):
             if dst.bits == 32:
-                import struct as _s
-                return lambda v: _s.unpack("f", _s.pack("f", float(v)))[0]
+                return to_f32
             return float
         if isinstance(dst, Ptr):
             if isinstance(src, Int):
@@ -1861,7 +1875,9 @@ class TU:
 
     def arith(self, op, rt, at, bt):
         """(a, b) -> result for integer binary op in type rt"""
-        w = rt.wrap if isinstance(rt, Int) else (lambda v: v)
+        # FLOAT results are rounded to single after every operation (exact for
+        # + - * / of single operands computed in double: 53 >= 2 * 24 + 2)
+        w = rt.wrap if isinstance(rt, Int) else (to_f32 if rt.bits == 32 else (lambda v: v))
         if op == "+":
             return lambda a, b: w(a + b)
         if op == "-":
@@ -1870,7 +1886,7 @@ class TU:
             return lambda a, b: w(a * b)
         if op == "/":
             if isinstance(rt, Flt):
-                return lambda a, b: a / b
+                return lambda a, b: w(a / b)
             return lambda a, b: w(abs(a) // abs(b) * (1 if (a >= 0) == (b >= 0) else -1))
         if op == "%":
             return lambda a, b: w(a - (abs(a) // abs(b) * (1 if (a >= 0) == (b >= 0) else -1)) * b)
@@ -2103,9 +2119,15 @@ class TU:
             (af, _), = A
             return (lambda fr: 64 - (af(fr) & (2 ** 64 - 1)).bit_length()), INT
         if name in ("sqrt",):
-            (af, _), = A
+            (af, at), = A
             import math
-            return (lambda fr: math.sqrt(af(fr))), DOUBLE
+            ca = self.converter(at, DOUBLE)
+            return (lambda fr: math.sqrt(ca(af(fr)))), DOUBLE
+        if name in ("sqrtf",):  # correctly rounded: sqrt in double, then to single
+            (af, at), = A
+            import math
+            ca = self.converter(at, FLOAT)
+            return (lambda fr: to_f32(math.sqrt(ca(af(fr))))), FLOAT
         return None
 
     # ---- statements: fn(frame) -> None | BRK | CONT | RET ----

@@ -1112,7 +1112,7 @@ TR_SIZES = [0, 1, 2, 3, 4, 5, 6, 9, 13, 14, 17]  # 4x4 8x8 16x16 32x32 64x64 4x8
 TR_TYPES = {16: [0, 3, 9, 10, 11, 14], 32: [0, 9], 64: [0]}
 
 
-def gen_trellis(txfm_fix):
+def gen_trellis(txfm_fix, sharpness=None):
     """av1_optimize_b (av1/encoder/encodemb.c:87-103) -> av1_optimize_txb
     (av1/encoder/txb_rdopt.c:326-449) on av1_quant's FP output (the
     use_optimize_b path of search_tx_type), from forward-transform outputs of
@@ -1120,7 +1120,10 @@ def gen_trellis(txfm_fix):
     200, sharpness 0 / 1, luma inter / luma intra / chroma, tx types of the
     three classes, random TXB_CTX and random LV_MAP cost / tx-type cost
     tables.  Outputs: the rate, the new eob, qcoeff / dqcoeff and the
-    txb_entropy_ctx."""
+    txb_entropy_ctx.  sharpness=2 (fix_trellis_s2.npz): every block at
+    quant_sharpness 2, where the trellis rdmult is scaled down by 2^4 and only
+    levels >= 2 may drop (txb_rdopt.c:359-363,397-401): larger rdmult and
+    levels, so the walk acts on a good share of the blocks."""
     tu = C.TU(REF, ["av1/encoder/encoder.h", "av1/encoder/txb_rdopt.c",
                     "av1/encoder/encodetxb.c", "av1/common/txb_common.c", "av1/common/scan.c",
                     "av1/encoder/encodemb.c", "av1/encoder/av1_quantize.c", "aom_dsp/quantize.c",
@@ -1128,7 +1131,7 @@ def gen_trellis(txfm_fix):
     check_errors(tu, ["av1_optimize_b", "av1_optimize_txb", "av1_quant", "av1_setup_quant",
                       "av1_build_quantizer"])
     E = tu.enums
-    rnd = ACMRandom(0xbaba + 9)
+    rnd = ACMRandom(0xbaba + 9 if sharpness is None else 0xbaba + 16)
     cc_tabs = np.array([rnd.generate(4000) for _ in range(10 * CC_COEFF_COST)], np.int32)
     eob_tabs = np.array([rnd.generate(4000) for _ in range(14 * CC_EOB_COST)], np.int32)
     cpi = tu.struct_obj("AV1_COMP")
@@ -1172,11 +1175,16 @@ def gen_trellis(txfm_fix):
                 for qindex in (40, 120, 200):
                     for plane, inter in ((0, 1), (0, 0), (1, 1)):
                         b = rnd.generate(len(src))
-                        scale = (1, 4, 16, 64)[rnd.generate(4)]
+                        scale = (1, 4, 16, 64)[rnd.generate(4)] if sharpness is None else \
+                            (1, 2)[rnd.generate(2)]
                         c = np.clip(src[b].astype(np.int64)[:n] // scale << (bd - 8),
                                     -(1 << (bd + 7)), (1 << (bd + 7)) - 1)
-                        sharp = rnd.generate(2)
-                        rdmult = 200 + rnd.generate((3000, 60000)[rnd.generate(2)])
+                        if sharpness is None:
+                            sharp = rnd.generate(2)
+                            rdmult = 200 + rnd.generate((3000, 60000)[rnd.generate(2)])
+                        else:
+                            sharp = sharpness
+                            rdmult = 20000 + rnd.generate(400000)
                         p0 = _get(X, "plane")[plane]
                         for fld, srct, nm in (("quant_fp_QTX", Q, "y_quant_fp"),
                                               ("round_fp_QTX", Q, "y_round_fp"),
@@ -1225,7 +1233,8 @@ def gen_trellis(txfm_fix):
                                    "sharpness", "rdmult", "txb_skip_ctx", "dc_sign_ctx",
                                    "tx_type_cost", "eob_in", "eob", "rate", "entropy_ctx",
                                    "index"])}
-    np.savez_compressed(os.path.join(HERE, "fix_trellis.npz"), **out)
+    np.savez_compressed(os.path.join(HERE, "fix_trellis.npz" if sharpness is None
+                                     else "fix_trellis_s%d.npz" % sharpness), **out)
 
 
 # ----------------------------------------------------------------------------
@@ -1442,9 +1451,253 @@ def gen_compound():
     np.savez_compressed(os.path.join(HERE, "fix_compound.npz"), **out)
 
 
+# ----------------------------------------------------------------------------
+# single-reference convolutions (av1/common/convolve.c:76-188, 687-787)
+# ----------------------------------------------------------------------------
+CONV_SIZES = [(2, 2), (2, 4), (4, 2), (4, 4), (8, 4), (4, 8), (8, 8), (16, 16), (32, 8),
+              (8, 32), (64, 16), (16, 64), (32, 32), (64, 64), (128, 128)]
+
+
+def gen_convolve():
+    """av1_convolve_{x,y,2d}_sr_c and av1_highbd_convolve_{x,y,2d}_sr_c -- the
+    non-copy paths of convolve_2d_facade_single (convolve.c:614-634 / highbd
+    :1106-1128) -- for bd 8 / 10 / 12, every block size class 2x2 .. 128x128,
+    filters REGULAR / SMOOTH / SHARP / BILINEAR / MULTITAP_SHARP2 through
+    av1_get_interp_filter_params_with_block_size (the 4-tap kernels for
+    dimensions <= 4), non-zero sub-pel phases, and the single-prediction
+    rounding of get_conv_params_no_round (convolve.h:63-96).  Ragged flat
+    arrays: the source window of case k is src[src_off[k]:...] with its
+    origin at (6, 6) of a (h + 13) x (w + 13) plane (room for 12 taps), the
+    output dst[dst_off[k]:...] is h x w."""
+    tu = C.TU(REF, ["aom/aom_integer.h", "aom_ports/mem.h", "aom_dsp/aom_dsp_common.h",
+                    "aom_dsp/aom_filter.h", "av1/common/enums.h", "av1/common/filter.h",
+                    "av1/common/convolve.h", "av1/common/convolve.c"],
+              C.reference_defines(REF))
+    names = ["av1_convolve_2d_sr_c", "av1_convolve_x_sr_c", "av1_convolve_y_sr_c",
+             "av1_highbd_convolve_2d_sr_c", "av1_highbd_convolve_x_sr_c",
+             "av1_highbd_convolve_y_sr_c", "av1_get_interp_filter_params_with_block_size"]
+    check_errors(tu, names)
+    rnd = ACMRandom(0xbaba + 13)
+    rows, srcs, dsts = [], [], []
+    so = do = 0
+    fpw = tu.func("av1_get_interp_filter_params_with_block_size")
+    for bd in (8, 10, 12):
+        hb = bd > 8
+        et = "uint16_t" if hb else "uint8_t"
+        pre = "av1_highbd_" if hb else "av1_"
+        r0 = 5 if bd == 12 else 3  # get_conv_params_no_round(.., is_compound 0, bd)
+        r1 = 14 - r0
+        for si, (w, h) in enumerate(CONV_SIZES):
+            t0 = time.time()
+            for path in (1, 2, 3):  # x, y, 2-D
+                f = (si + path + bd) % 5
+                fx = f if path != 2 else 0
+                fy = f if path != 1 else 0
+                if path == 3 and si % 2:
+                    fy = (f + 2) % 5  # dual filter
+                sx = 1 + rnd.generate(15) if path != 2 else 0
+                sy = 1 + rnd.generate(15) if path != 1 else 0
+                SS = w + 13
+                src = np.array(_pix(rnd, (h + 13) * SS, bd)).reshape(h + 13, SS)
+                sp = tu.buffer(et, src.reshape(-1).tolist())
+                blk = C.Pointer(sp.buf, 6 * SS + 6, sp.ty)
+                dp = tu.buffer(et, [0x5A] * (w * h))
+                cp = tu.struct_obj("ConvolveParams")
+                _set(cp.buf[0], do_average=0, dst=C.Pointer(None, 0, tu.ctype("CONV_BUF_TYPE")),
+                     dst_stride=0, round_0=r0, round_1=r1, plane=0, is_compound=0,
+                     use_dist_wtd_comp_avg=0, fwd_offset=0, bck_offset=0)
+                fpx = fpw(fx, w)
+                fpy = fpw(fy, h)
+                if path == 1:
+                    a = [blk, SS, dp, w, w, h, fpx, sx, cp]
+                    fn = "convolve_x_sr_c"
+                elif path == 2:
+                    a = [blk, SS, dp, w, w, h, fpy, sy]
+                    fn = "convolve_y_sr_c"
+                else:
+                    a = [blk, SS, dp, w, w, h, fpx, fpy, sx, sy, cp]
+                    fn = "convolve_2d_sr_c"
+                if hb:
+                    a.append(bd)
+                tu.func(pre + fn)(*a)
+                rows.append([bd, w, h, path, fx, fy, sx, sy, r0, r1, so, do])
+                srcs.append(src.reshape(-1).astype(np.uint16))
+                dsts.append(np.array(dp.buf, np.uint16))
+                so += src.size
+                do += w * h
+            print("  convolve bd %d %dx%d %.1fs" % (bd, w, h, time.time() - t0))
+    out = {"rows": np.array(rows, np.int64), "src": np.concatenate(srcs),
+           "dst": np.concatenate(dsts), "origin": np.array([6, 6, 13], np.int64),
+           "row_fields": np.array(["bd", "w", "h", "path", "filter_x", "filter_y", "subpel_x",
+                                   "subpel_y", "round_0", "round_1", "src_off", "dst_off"])}
+    np.savez_compressed(os.path.join(HERE, "fix_convolve.npz"), **out)
+
+
+def gen_compound12():
+    """The 12-tap (MULTITAP_SHARP2) forms of av1_dist_wtd_convolve_{x,y,2d}_c and
+    their highbd versions (convolve.c:291-489,790-988), which the 8-tap
+    fix_compound cases do not reach: bd 8 / 10 / 12, sizes 8x8 .. 128x128 (the
+    largest im_block), first pass / average / distance-weighted average.
+    Ragged flat arrays like fix_convolve; origin (6, 6) of an (h + 13) x
+    (w + 13) source, the conv buffer and dst are h x w with stride w."""
+    tu = C.TU(REF, ["aom/aom_integer.h", "aom_ports/mem.h", "aom_dsp/aom_dsp_common.h",
+                    "aom_dsp/aom_filter.h", "av1/common/enums.h", "av1/common/filter.h",
+                    "av1/common/convolve.h", "av1/common/convolve.c"],
+              C.reference_defines(REF))
+    names = ["av1_dist_wtd_convolve_x_c", "av1_dist_wtd_convolve_y_c",
+             "av1_dist_wtd_convolve_2d_c", "av1_highbd_dist_wtd_convolve_x_c",
+             "av1_highbd_dist_wtd_convolve_y_c", "av1_highbd_dist_wtd_convolve_2d_c",
+             "av1_get_interp_filter_params_with_block_size"]
+    check_errors(tu, names)
+    rnd = ACMRandom(0xbaba + 14)
+    fpw = tu.func("av1_get_interp_filter_params_with_block_size")
+    rows, srcs, dsts_in, dsts, convs_in, convs = [], [], [], [], [], []
+    so = do = 0
+    for bd in (8, 10, 12):
+        hb = bd > 8
+        et = "uint16_t" if hb else "uint8_t"
+        pre = "av1_highbd_" if hb else "av1_"
+        for (w, h) in ((8, 8), (16, 8), (8, 32), (32, 32), (128, 128)):
+            t0 = time.time()
+            for path in (1, 2, 3):
+                modes = (0,) if w == 128 else (0, 1, 2)
+                if w == 128 and path != 3:
+                    continue
+                for mode in modes:
+                    sx = 1 + rnd.generate(15) if path != 2 else 0
+                    sy = 1 + rnd.generate(15) if path != 1 else 0
+                    SS = w + 13
+                    src = np.array(_pix(rnd, (h + 13) * SS, bd)).reshape(h + 13, SS)
+                    sp = tu.buffer(et, src.reshape(-1).tolist())
+                    blk = C.Pointer(sp.buf, 6 * SS + 6, sp.ty)
+                    d_in = _pix(rnd, h * w, bd)
+                    c_in = [rnd.rand16() & ((1 << (bd + 4)) - 1) for _ in range(h * w)]
+                    dp = tu.buffer(et, d_in)
+                    cb = tu.buffer("CONV_BUF_TYPE", c_in)
+                    cp = tu.struct_obj("ConvolveParams")
+                    intbuf = bd + 7 - 3 + 2
+                    r0 = 3 + (intbuf - 16 if intbuf > 16 else 0)
+                    jj, ii = rnd.generate(4), rnd.generate(2)
+                    fwd, bck = (QUANT_DIST[jj][ii], QUANT_DIST[jj][1 - ii]) if mode == 2 else (0, 0)
+                    _set(cp.buf[0], do_average=int(mode > 0), dst=cb, dst_stride=w, round_0=r0,
+                         round_1=7, plane=0, is_compound=1, use_dist_wtd_comp_avg=int(mode == 2),
+                         fwd_offset=fwd, bck_offset=bck)
+                    fpx, fpy = fpw(4, w), fpw(4, h)
+                    a = [blk, SS, dp, w, w, h]
+                    if path == 1:
+                        a += [fpx, sx, cp]
+                    elif path == 2:
+                        a += [fpy, sy, cp]
+                    else:
+                        a += [fpx, fpy, sx, sy, cp]
+                    if hb:
+                        a.append(bd)
+                    fn = ["", "dist_wtd_convolve_x_c", "dist_wtd_convolve_y_c",
+                          "dist_wtd_convolve_2d_c"][path]
+                    tu.func(pre + fn)(*a)
+                    rows.append([bd, w, h, path, mode, sx, sy, r0, 7, fwd, bck, so, do])
+                    srcs.append(src.reshape(-1).astype(np.uint16))
+                    dsts_in.append(np.array(d_in, np.uint16))
+                    dsts.append(np.array(dp.buf, np.uint16))
+                    convs_in.append(np.array(c_in, np.uint16))
+                    convs.append(np.array(cb.buf, np.uint16))
+                    so += src.size
+                    do += w * h
+            print("  compound12 bd %d %dx%d %.1fs" % (bd, w, h, time.time() - t0))
+    out = {"rows": np.array(rows, np.int64), "src": np.concatenate(srcs),
+           "dst_in": np.concatenate(dsts_in), "dst": np.concatenate(dsts),
+           "conv_in": np.concatenate(convs_in), "conv": np.concatenate(convs),
+           "origin": np.array([6, 6, 13], np.int64),
+           "row_fields": np.array(["bd", "w", "h", "path", "mode", "subpel_x", "subpel_y",
+                                   "round_0", "round_1", "fwd_offset", "bck_offset", "src_off",
+                                   "dst_off"])}
+    np.savez_compressed(os.path.join(HERE, "fix_compound12.npz"), **out)
+
+
+# ----------------------------------------------------------------------------
+# TX-pruning features (av1/encoder/rdopt.c:514-609, tx_search.c:1411-1473)
+# ----------------------------------------------------------------------------
+FEAT_SIZES = [0, 1, 2, 3, 5, 6, 7, 8, 9, 10, 13, 14, 15, 16]  # every tx size <= 32x32
+HORVER_ONLY = [(64, 64), (128, 128), (64, 128), (128, 64), (16, 64), (64, 16), (2, 2), (4, 128)]
+
+
+def gen_txfeat():
+    """get_energy_distribution_finer (static in tx_search.c:1411-1473) and
+    av1_get_horver_correlation_full_c (rdopt.c:514-609) -- prune_tx_2D's two
+    feature vectors (tx_search.c:1516-1529) -- on residual blocks of every tx
+    size <= 32x32: the reference test's (Rand16 % 4096) - 2048 blocks
+    (test/horver_correlation_test.cc:55-66), an all-zero block (the total ==
+    0 branch), a constant block, small-range and 8-bit-range residuals; and
+    av1_get_horver_correlation_full_c alone on larger / odd shapes.  Floats
+    stored as their int32 bit patterns."""
+    tu = C.TU(REF, ["av1/encoder/encoder.h", "av1/encoder/tx_search.c", "av1/encoder/rdopt.c"],
+              C.reference_defines(REF))
+    check_errors(tu, ["get_energy_distribution_finer", "av1_get_horver_correlation_full_c"])
+    rnd = ACMRandom(0xbaba + 15)
+    efin = tu.func("get_energy_distribution_finer")
+    hv = tu.func("av1_get_horver_correlation_full_c")
+    f32 = lambda v: np.array([v], np.float32).view(np.int32)[0]
+
+    def block(kind, w, h):
+        if kind == 0:
+            return [(rnd.rand16() % 4096) - 2048 for _ in range(w * h)]
+        if kind == 1:
+            return [0] * (w * h)
+        if kind == 2:
+            return [37] * (w * h)
+        if kind == 3:
+            return [(rnd.rand16() % 17) - 8 for _ in range(w * h)]
+        return [(rnd.rand16() % 511) - 255 for _ in range(w * h)]
+
+    rows, blocks, feats = [], [], []
+    off = 0
+    for s in FEAT_SIZES:
+        w, h = TX_W[s], TX_H[s]
+        t0 = time.time()
+        for kind in (0, 0, 1, 2, 3, 4, 0):
+            stride = w + 3  # the caller's stride is the block width; any stride is legal
+            vals = block(kind, w, h)
+            buf = np.zeros((h, stride), np.int16)
+            buf[:, :w] = np.array(vals, np.int16).reshape(h, w)
+            dp = tu.buffer("int16_t", buf.reshape(-1).tolist())
+            hd, vd = tu.buffer("float", 16), tu.buffer("float", 16)
+            efin(dp, stride, w, h, hd, vd)
+            hc, vc = tu.buffer("float", 1), tu.buffer("float", 1)
+            hv(dp, stride, w, h, hc, vc)
+            fv = [f32(v) for v in hd.buf] + [f32(v) for v in vd.buf] + [f32(hc.buf[0]),
+                                                                      f32(vc.buf[0])]
+            rows.append([s, w, h, kind, off])
+            blocks.append(buf[:, :w].reshape(-1))
+            feats.append(fv)
+            off += w * h
+        print("  txfeat %dx%d %.1fs" % (w, h, time.time() - t0))
+    hrows, hblocks, hout = [], [], []
+    hoff = 0
+    for (w, h) in HORVER_ONLY:
+        for kind in (0, 4):
+            vals = block(kind, w, h)
+            dp = tu.buffer("int16_t", vals)
+            hc, vc = tu.buffer("float", 1), tu.buffer("float", 1)
+            hv(dp, w, w, h, hc, vc)
+            hrows.append([w, h, kind, hoff])
+            hblocks.append(np.array(vals, np.int16))
+            hout.append([f32(hc.buf[0]), f32(vc.buf[0])])
+            hoff += w * h
+        print("  horver %dx%d" % (w, h))
+    out = {"rows": np.array(rows, np.int64), "blocks": np.concatenate(blocks).astype(np.int16),
+           "features": np.array(feats, np.int32),
+           "horver_rows": np.array(hrows, np.int64),
+           "horver_blocks": np.concatenate(hblocks).astype(np.int16),
+           "horver": np.array(hout, np.int32),
+           "row_fields": np.array(["tx_size", "w", "h", "kind", "off"]),
+           "feature_layout": np.array(["hordist[16]", "verdist[16]", "hcorr", "vcorr"])}
+    np.savez_compressed(os.path.join(HERE, "fix_txfeat.npz"), **out)
+
+
 def main(argv):
     sections = argv or ["txfm", "qparams", "quant", "inv", "pixel", "wht", "nmv", "mcomp",
-                        "subpel", "tpl", "qfacade", "costcoeffs", "trellis", "warp", "compound"]
+                        "subpel", "tpl", "qfacade", "costcoeffs", "trellis", "warp", "compound",
+                        "convolve", "compound12", "txfeat", "trellis2"]
     t0 = time.time()
     ttx = None
     if "txfm" in sections or "inv" in sections or "wht" in sections:
@@ -1485,6 +1738,14 @@ def main(argv):
         gen_warp()
     if "compound" in sections:
         gen_compound()
+    if "convolve" in sections:
+        gen_convolve()
+    if "compound12" in sections:
+        gen_compound12()
+    if "txfeat" in sections:
+        gen_txfeat()
+    if "trellis2" in sections:
+        gen_trellis(dict(np.load(os.path.join(HERE, "fix_txfm.npz"))), sharpness=2)
     print("done in %.0fs" % (time.time() - t0))
 
 

@@ -148,3 +148,19 @@ def test_shear_params_host_matches_reference():
         assert (ok,) + tuple(int(v) for v in out) == tuple(int(v) for v in (row[0], *row[7:11]))
         n_ok += ok
     assert n_ok > len(F["shear"]) // 2
+
+
+@pytest.mark.parametrize("f", range(5))
+@pytest.mark.parametrize("size", [2, 4, 8, 16, 128])
+def test_interp_kernels_match_reference_tables(f, size):
+    """lavish_interp_kernels = av1_get_interp_filter_params_with_block_size
+    (filter.h:253-259) over the reference's own kernel tables (filter.h)."""
+    import lavish_dsp.inter as I
+    names8 = ["av1_sub_pel_filters_8", "av1_sub_pel_filters_8smooth",
+              "av1_sub_pel_filters_8sharp", "av1_bilinear_filters"]
+    names4 = ["av1_sub_pel_filters_4", "av1_sub_pel_filters_4smooth", "av1_sub_pel_filters_4",
+              "av1_bilinear_filters"]
+    F = TABLES["interp_filters"]
+    exp = F["av1_sub_pel_filters_12sharp"] if f == 4 else \
+        (F[names4[f]] if size <= 4 else F[names8[f]])
+    np.testing.assert_array_equal(I.interp_kernels(f, size), np.array(exp, np.int16))

@@ -428,3 +428,108 @@ def test_dist_wtd_convolve_matches_reference():
                             src_off=org * SS + org)
         np.testing.assert_array_equal(conv, F["conv"][k], err_msg=str(k))
         np.testing.assert_array_equal(dst.astype(np.uint16), F["dst"][k], err_msg=str(k))
+
+
+def test_convolve_sr_matches_reference():
+    """orc convolve_block against av1_convolve_{x,y,2d}_sr_c and the highbd
+    forms executed from the reference (fix_convolve.npz): bd 8/10/12, 2x2 ..
+    128x128, the five filters incl. 12-tap MULTITAP_SHARP2."""
+    F = _load("fix_convolve.npz")
+    J = {n: i for i, n in enumerate(F["row_fields"])}
+    oy, ox, pad = (int(v) for v in F["origin"])
+    paths = set()
+    for r in F["rows"]:
+        g = lambda k: int(r[J[k]])
+        w, h, bd = g("w"), g("h"), g("bd")
+        SS = w + pad
+        src = F["src"][g("src_off"):g("src_off") + (h + pad) * SS].reshape(h + pad, SS)
+        src = np.ascontiguousarray(src.astype(np.uint8 if bd == 8 else np.uint16))
+        fx = O.interp_kernel(g("filter_x"), w, g("subpel_x"))
+        fy = O.interp_kernel(g("filter_y"), h, g("subpel_y"))
+        got = O.convolve_block(src, oy * SS + ox, SS, w, h, g("path"), fx, fy, g("round_0"),
+                               g("round_1"), bd)
+        exp = F["dst"][g("dst_off"):g("dst_off") + w * h].reshape(h, w)
+        np.testing.assert_array_equal(got.astype(np.int64), exp, err_msg=str(r))
+        paths.add((g("path"), g("filter_x") == 4 or g("filter_y") == 4))
+    assert len(paths) == 6  # x / y / 2-D, with and without the 12-tap kernel
+
+
+def test_dist_wtd_convolve_12tap_matches_reference():
+    """orc_dist_wtd_convolve against the 12-tap (MULTITAP_SHARP2) compound
+    convolutions executed from the reference (fix_compound12.npz)."""
+    F = _load("fix_compound12.npz")
+    J = {n: i for i, n in enumerate(F["row_fields"])}
+    oy, ox, pad = (int(v) for v in F["origin"])
+    for r in F["rows"]:
+        g = lambda n: int(r[J[n]])
+        bd, w, h = g("bd"), g("w"), g("h")
+        hb = bd > 8
+        SS = w + pad
+        src = F["src"][g("src_off"):g("src_off") + (h + pad) * SS]
+        src = np.ascontiguousarray(src.astype(np.uint16 if hb else np.uint8))
+        d0 = g("dst_off")
+        dst = F["dst_in"][d0:d0 + w * h].astype(np.uint16 if hb else np.uint8).copy()
+        conv = F["conv_in"][d0:d0 + w * h].copy()
+        fx = O.interp_kernel(4, w, g("subpel_x"))
+        fy = O.interp_kernel(4, h, g("subpel_y"))
+        cp = dict(do_average=int(g("mode") > 0), round_0=g("round_0"), round_1=g("round_1"),
+                  is_compound=1, use_dist_wtd_comp_avg=int(g("mode") == 2),
+                  fwd_offset=g("fwd_offset"), bck_offset=g("bck_offset"))
+        O.dist_wtd_convolve(g("path"), src, SS, dst, w, w, h, fx, fy, cp, conv, w, bd, int(hb),
+                            src_off=oy * SS + ox)
+        np.testing.assert_array_equal(conv, F["conv"][d0:d0 + w * h], err_msg=str(r))
+        np.testing.assert_array_equal(dst.astype(np.uint16), F["dst"][d0:d0 + w * h],
+                                      err_msg=str(r))
+
+
+def _features(F, k):
+    """Expected prune_tx_2D feature vectors of fix_txfeat row k."""
+    s, w, h = (int(v) for v in F["rows"][k][:3])
+    f = F["features"][k].view(np.float32)
+    nh = w if w <= 8 else w // 2
+    nv = h if h <= 8 else h // 2
+    return (np.concatenate([f[:nh - 1], f[32:33]]), np.concatenate([f[16:16 + nv - 1], f[33:34]]))
+
+
+def test_tx_prune_features_match_reference():
+    """orc_tx_prune_features / orc_horver_correlation_full against
+    get_energy_distribution_finer + av1_get_horver_correlation_full_c executed
+    from the reference (fix_txfeat.npz): float bit patterns, 0 ULP."""
+    F = _load("fix_txfeat.npz")
+    for k, (s, w, h, kind, off) in enumerate(F["rows"]):
+        blk = F["blocks"][off:off + w * h].reshape(h, w)
+        hf, vf = O.tx_prune_features(blk, w, h)
+        eh, ev = _features(F, k)
+        np.testing.assert_array_equal(hf[0][:len(eh)].view(np.int32), eh.view(np.int32))
+        np.testing.assert_array_equal(vf[0][:len(ev)].view(np.int32), ev.view(np.int32))
+    for k, (w, h, kind, off) in enumerate(F["horver_rows"]):
+        blk = F["horver_blocks"][off:off + w * h].reshape(h, w)
+        got = np.array(O.horver_full(blk, w, w, h), np.float32).view(np.int32)
+        np.testing.assert_array_equal(got, F["horver"][k])
+
+
+def test_optimize_b_sharpness2_matches_reference():
+    """orc_optimize_b against av1_optimize_b executed from the reference at
+    quant_sharpness 2 (fix_trellis_s2.npz); the walk changes a good share of
+    the blocks there."""
+    F = _load("fix_trellis_s2.npz")
+    J = {n: i for i, n in enumerate(F["row_fields"])}
+    blob = O.coeff_costs_blob(F["coeff_costs"], F["eob_costs"])
+    changed = 0
+    for r in F["rows"]:
+        g = lambda k: int(r[J[k]])
+        assert g("sharpness") == 2
+        n = O.max_eob(g("tx_size"))
+        i = g("index")
+        dqv = O.quant_arrays(O.build_quant(g("bd"), g("qindex")))["dequant"]
+        e, rate, ec, qc, dq = O.optimize_b(
+            blob, F["coeff"][i][:n], F["qcoeff_in"][i][:n], F["dqcoeff_in"][i][:n],
+            g("eob_in"), g("plane"), g("tx_size"), g("tx_type"), g("bd"), g("is_inter"),
+            g("rdmult"), g("sharpness"), dqv, g("txb_skip_ctx"), g("dc_sign_ctx"),
+            g("tx_type_cost"))
+        msg = str({k: g(k) for k in J})
+        assert (e, rate, ec) == (g("eob"), g("rate"), g("entropy_ctx")), msg
+        np.testing.assert_array_equal(qc, F["qcoeff"][i][:n], err_msg=msg)
+        np.testing.assert_array_equal(dq, F["dqcoeff"][i][:n], err_msg=msg)
+        changed += int((qc != F["qcoeff_in"][i][:n]).any())
+    assert changed > len(F["rows"]) // 4, changed
