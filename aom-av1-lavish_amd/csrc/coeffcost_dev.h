@@ -56,35 +56,16 @@ __device__ __forceinline__ int br_ctx_mag(int cls, int mag, int pos, int col, in
   return pos == 0 ? mag : mag + (near ? 7 : 14);
 }
 
-// get_nz_mag (txb_common.h:150-173) + get_nz_map_ctx_from_stats over the map
-__device__ __forceinline__ int lower_ctx(int cls, int wlt, int wgt, const uint8_t* lv, int stride,
-                                         int pos, int col, int row) {
-  const uint8_t* l = lv + col * stride + row;
-  int mag = min3(l[stride]) + min3(l[1]);
-  if (cls == 0) {
-    mag += min3(l[stride + 1]) + min3(l[2 * stride]) + min3(l[2]);
-  } else if (cls == 2) {
-    mag += min3(l[2]) + min3(l[3]) + min3(l[4]);
-  } else {
-    mag += min3(l[2 * stride]) + min3(l[3 * stride]) + min3(l[4 * stride]);
-  }
-  return nz_ctx(cls, wlt, wgt, mag, pos, col, row);
-}
-
-// get_br_ctx (txb_common.h:103-135) over the map
-__device__ __forceinline__ int br_ctx(int cls, const uint8_t* lv, int stride, int pos, int col,
-                                      int row) {
-  const uint8_t* l = lv + col * stride + row;
-  const int third = cls == 0 ? l[stride + 1] : (cls == 1 ? l[2 * stride] : l[2]);
-  return br_ctx_mag(cls, l[1] + l[stride] + third, pos, col, row);
-}
-
-// The neighbour offsets of get_nz_mag / get_br_ctx for one tx class, fixed
-// per block: lower_ctx_off / br_ctx_off read through them with no per-
-// coefficient class branch.  (The class-branching forms above, inlined into
-// the trellis walk, were miscompiled by the ROCm 7.2 compiler for the
-// vertical class: the l[2] address register of the br_ctx load was left
-// undefined on that path.)
+// get_nz_mag (txb_common.h:150-173) / get_br_ctx (:103-135) over the map.
+// The neighbour offsets of one tx class are fixed per block, and
+// lower_ctx_off / br_ctx_off read through them with no per-coefficient class
+// branch.  The class-branching form (third = cls == 0 ? l[stride + 1] :
+// cls == 1 ? l[2 * stride] : l[2]) is miscompiled by ROCm 7.2 for gfx950
+// once inlined into the trellis walk: on the vertical-class path the
+// ds_read_u8 address VGPR is never written (`implicit-def`), see
+// profiles/r03_trellis_miscompile_isa.txt and the A/B reproducer
+// tools/dbg/build_trellis_cb.sh.  Both kernels (trellis, coefficient cost)
+// use this one form.
 struct NbrOff {
   int nz0, nz1, nz2;  // get_nz_mag's three class-dependent neighbours
   int br;             // get_br_ctx's third neighbour
@@ -132,9 +113,10 @@ __device__ __forceinline__ int br_cost(const int32_t* tab, int ctx, int level) {
 
 // warehouse_efficients_txb's term of the coefficient v at raster pos (col,
 // row) with scan index i < eob, n = coefficients of the adjusted size
-__device__ __forceinline__ int coeff_term(const int32_t* tab, int cls, int wlt, int wgt,
-                                          const uint8_t* lv, int stride, int n, int pos, int col,
-                                          int row, int i, int eob, int v, int dc_sign_ctx) {
+__device__ __forceinline__ int coeff_term(const int32_t* tab, const NbrOff& nb, int cls, int wlt,
+                                          int wgt, const uint8_t* lv, int stride, int n, int pos,
+                                          int col, int row, int i, int eob, int v,
+                                          int dc_sign_ctx) {
   const int level = abs(v);
   int cost;
   if (i == eob - 1) {
@@ -142,8 +124,9 @@ __device__ __forceinline__ int coeff_term(const int32_t* tab, int cls, int wlt, 
     cost = tab[kBaseEob + ctx * 3 + min3(level) - 1];
     if (level > 2) cost += br_cost(tab, br_ctx_eob(cls, pos, col, row), level);
   } else {
-    cost = tab[kBase + lower_ctx(cls, wlt, wgt, lv, stride, pos, col, row) * 8 + min3(level)];
-    if (level > 2) cost += br_cost(tab, br_ctx(cls, lv, stride, pos, col, row), level);
+    cost = tab[kBase + lower_ctx_off(nb, cls, wlt, wgt, lv, stride, pos, col, row) * 8 +
+               min3(level)];
+    if (level > 2) cost += br_cost(tab, br_ctx_off(nb, cls, lv, stride, pos, col, row), level);
   }
   if (level) cost += i ? 512 : tab[kDcSign + dc_sign_ctx * 2 + (v < 0)];
   return cost;

@@ -106,6 +106,7 @@ __global__ __launch_bounds__(256) void cost_coeffs_kernel(CcArgs a) {
       wave_sync();
     }
     const int dcctx = a.ctx ? a.ctx[bb].dc_sign_ctx : 0;
+    const NbrOff nb = nbr_off(a.cls, stride);
     int cost = 0;
 #pragma unroll
     for (int k = 0; k < KC; ++k) {
@@ -124,8 +125,8 @@ __global__ __launch_bounds__(256) void cost_coeffs_kernel(CcArgs a) {
           cost += i == eob - 1 ? (level - 1) << 11 : kCostLut[min(level, 14)];
           continue;
         }
-        cost += coeff_term(tab, a.cls, a.wlt, a.wgt, lv, stride, N, pos0 + e, col, row0 + e, i,
-                           eob, v, dcctx);
+        cost += coeff_term(tab, nb, a.cls, a.wlt, a.wgt, lv, stride, N, pos0 + e, col, row0 + e,
+                           i, eob, v, dcctx);
       }
     }
 #pragma unroll

@@ -14,8 +14,9 @@ sed -e 's/lower_ctx_off(nb, cls,/lower_ctx(cls,/' -e 's/br_ctx_off(nb, cls,/br_c
     $P/csrc/trellis.hip > $P/csrc/_trellis_cb.hip
 grep -c "lower_ctx(cls\|br_ctx(cls" $P/csrc/_trellis_cb.hip
 F="-O3 -std=c++17 -fPIC --offload-arch=gfx950 -Wall -Wno-unused-function -munsafe-fp-atomics"
-/opt/rocm/bin/hipcc $F -c $P/csrc/_trellis_cb.hip -o $T/trellis_cb.o
-/opt/rocm/bin/hipcc $F --cuda-device-only -S $P/csrc/_trellis_cb.hip -o $T/trellis_cb.s
+CB="-include $R/tools/dbg/classbranch_helpers.h"
+/opt/rocm/bin/hipcc $F $CB -c $P/csrc/_trellis_cb.hip -o $T/trellis_cb.o
+/opt/rocm/bin/hipcc $F $CB --cuda-device-only -S $P/csrc/_trellis_cb.hip -o $T/trellis_cb.s
 /opt/rocm/bin/hipcc $F --cuda-device-only -S $P/csrc/trellis.hip -o $T/trellis_off.s
 rm -f $P/csrc/_trellis_cb.hip
 objs=$(ls $P/build/*.o | grep -v '/trellis.o$')
