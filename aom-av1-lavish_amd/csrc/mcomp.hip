@@ -146,7 +146,18 @@ struct Ctx {
   const int32_t* mvjcost;
   const int32_t* mvcost0;  // centred at MV_MAX
   const int32_t* mvcost1;
+  // tiled copy of the reference buffer (LavishRefTiles): the block origin's
+  // row / column in the whole buffer, strip-column height, field size
+  const uint8_t* tiles;
+  int oy, ox, fh, fsz;
 };
+
+// byte offset of buffer pixel (y, x) in the tiled copy: field y & 1, strip
+// x >> 4 (bytes [16k, 16k + 32) of each field row), field row y >> 1
+__device__ __forceinline__ uint32_t tile_off(const Ctx& c, int y, int x) {
+  return (uint32_t)((y & 1) * c.fsz) +
+         ((uint32_t)(__mul24(x >> 4, c.fh) + (y >> 1)) << 5) + (uint32_t)(x & 15);
+}
 
 __device__ __forceinline__ int sad_lambda(int t) { return t == 1 ? 32 : t == 2 ? 15 : t == 3 ? 8 : 0; }
 __device__ __forceinline__ int sse_lambda(int t) { return t == 1 ? 2 : t == 2 ? 0 : t == 3 ? 1 : 0; }
@@ -267,9 +278,11 @@ __device__ __forceinline__ int site_dc(int i) { return ((0x2885 >> (2 * i)) & 3)
 
 // UA: candidate rows as byte-addressed loads (DIAMOND: its global-memory
 // steps are the large-radius ones) or aligned loads + v_alignbyte (the
-// pattern searches, see load_row_aligned)
-template <int W, int H, bool SKIP, bool UA = true>
+// pattern searches, see load_row_aligned).  TL: candidate rows from the
+// tiled copy (c.tiles), byte-addressed inside one 32-byte strip row.
+template <int W, int H, bool SKIP, bool UA = true, bool TL = false>
 struct Search {
+  static_assert(!TL || W <= 16, "tiled candidate rows: w <= 16");
   using G = Geo<W, H, SKIP>;
   using WN = Win<W, H>;
   // source rows live in VGPRs up to 32 words per lane (32x32 and smaller);
@@ -319,14 +332,32 @@ struct Search {
     }
   }
 
-  // group-partial SAD of the block at ref + off, reduced over the 8 lanes.
-  // Lanes whose candidate is not valid read the block at `safe` (in range)
-  // instead: no divergent branch around the loads; callers mask the result.
-  __device__ __forceinline__ uint32_t group_sad(const Ctx& c, int64_t off, bool valid,
-                                                int64_t safe) const {
-    off = valid ? off : safe;
+  // group-partial SAD of the candidate at mv (r, cc), reduced over the 8
+  // lanes.  Lanes whose candidate is not valid read the block at (sr, sc)
+  // (in range) instead: no divergent branch around the loads; callers mask
+  // the result.
+  __device__ __forceinline__ uint32_t group_sad(const Ctx& c, int r, int cc, bool valid, int sr,
+                                                int sc) const {
+    r = valid ? r : sr;
+    cc = valid ? cc : sc;
+    const int64_t off = (int64_t)__mul24(r, c.rs) + cc;
     uint32_t acc = 0;
-    if constexpr (kCache) {
+    if constexpr (TL) {
+      // lane l's rows: field rows (oy + r + row * YS) of strip (ox + cc) >> 4;
+      // with the downsampled SAD a group's 8 rows are consecutive rows of one
+      // field: 256 contiguous bytes (2-3 cache lines) per candidate
+      const int x = c.ox + cc;
+#pragma unroll
+      for (int k = 0; k < G::RPL; ++k) {
+        const int row = l + 8 * k;
+        if (row < G::RH) {
+          uint32_t t[G::DW];
+          load_row<G::DW>(c.tiles + tile_off(c, c.oy + r + row * G::YS, x), t);
+#pragma unroll
+          for (int i = 0; i < G::DW; ++i) acc = sad4(s[k][i], t[i], acc);
+        }
+      }
+    } else if constexpr (kCache) {
 #pragma unroll
       for (int k = 0; k < G::RPL; ++k) {
         const int row = l + 8 * k;
@@ -359,8 +390,8 @@ struct Search {
     acc = group_sum8(acc);
     return SKIP ? 2 * acc : acc;
   }
-  __device__ __forceinline__ uint32_t group_sad(const Ctx& c, int64_t off) const {
-    return group_sad(c, off, true, off);
+  __device__ __forceinline__ uint32_t group_sad(const Ctx& c, int r, int cc) const {
+    return group_sad(c, r, cc, true, r, cc);
   }
 
   // copy the window around (row, col): rows outside [row_min, row_max + H)
@@ -469,7 +500,7 @@ struct Search {
     scol = min(max(scol, c.col_min), c.col_max);
     int row = srow, col = scol, off_center = 0, center = 0;
     if (!have_c0 || c0row != srow || c0col != scol) {
-      c0sad = rdlane(group_sad(c, (int64_t)srow * c.rs + scol), 0);
+      c0sad = rdlane(group_sad(c, srow, scol), 0);
       have_c0 = true;
       c0row = srow;
       c0col = scol;
@@ -494,8 +525,7 @@ struct Search {
       // keep every index inside the cost tables, valid or not
       const uint32_t mvs = mvsad_cost(c, r, cc);
       const uint32_t mine = inwin ? group_sad_win(c, r, cc, valid)
-                                  : group_sad(c, __mul24(r, c.rs) + cc, valid,
-                                              __mul24(row, c.rs) + col);
+                                  : group_sad(c, r, cc, valid, row, col);
       // key = cost * 8 + site (costs < 2^26 for blocks <= 128x128)
       const uint32_t key = valid ? ((mine + mvs) << 3) | (uint32_t)g : ~0u;
       const uint32_t kmin = groups_min(key);
@@ -537,8 +567,7 @@ __device__ void int_sad_list(const S_t& S, const Ctx& c, int lane, int br, int b
     // (check_bounds of the reference only skips this test when it holds)
     const bool valid =
         g < 5 && cc >= c.col_min && cc <= c.col_max && r >= c.row_min && r <= c.row_max;
-    const uint32_t sad =
-        S.group_sad(c, (int64_t)r * c.rs + cc, valid, (int64_t)br * c.rs + bc);
+    const uint32_t sad = S.group_sad(c, r, cc, valid, br, bc);
     const uint32_t v = valid ? sad : 0x7FFFFFFFu;
 #pragma unroll
     for (int i = 0; i < 5; ++i) cl[i] = (int)rdlane(v, 8 * i);
@@ -551,11 +580,11 @@ __device__ void int_sad_list(const S_t& S, const Ctx& c, int lane, int br, int b
 }
 
 // full_pixel_diamond (mcomp.c:1479-1526)
-template <int W, int H, bool SKIP>
+template <int W, int H, bool SKIP, bool TL>
 __device__ int full_pixel_diamond(const Ctx& c, int lane, int srow, int scol, int step_param,
                                   int& brow, int& bcol, int& steps, int& searches, lds_u32 win,
                                   bool want_cl, int (&cl)[5]) {
-  Search<W, H, SKIP> S;
+  Search<W, H, SKIP, true, TL> S;
   S.load_src(c, lane, win);
   int n, num00 = 0;
   S.diamond(c, lane, srow, scol, step_param, brow, bcol, n, steps);
@@ -609,11 +638,11 @@ __device__ __forceinline__ void bigdia_site(int s, int i, int& dr, int& dc) {
 // Lane group g evaluates candidate g; the keyed minimum is the reference's
 // sequential update order (update_mvs_and_sad, mcomp.c:858-877), whose raw
 // SAD is kept as raw_bestsad.
-template <int W, int H, bool SKIP>
+template <int W, int H, bool SKIP, bool TL>
 __device__ int pattern(const Ctx& c, int lane, int srow, int scol, int search_step, bool do_init,
                        bool want_cl, int (&cl)[5], int& brow, int& bcol, int& steps,
                        int& nsad) {
-  Search<W, H, SKIP, false> S;
+  Search<W, H, SKIP, false, TL> S;
   S.load_src(c, lane);
   const int g = lane >> 3;
   search_step = min(search_step, kMaxSteps - 1);
@@ -622,7 +651,7 @@ __device__ int pattern(const Ctx& c, int lane, int srow, int scol, int search_st
   int bc = min(max(scol, c.col_min), c.col_max);
   if (want_cl) cl[0] = cl[1] = cl[2] = cl[3] = cl[4] = INT_MAX;
   bool has_sad = false;
-  uint32_t raw = rdlane(S.group_sad(c, (int64_t)br * c.rs + bc), 0);
+  uint32_t raw = rdlane(S.group_sad(c, br, bc), 0);
   uint32_t best = raw + mvsad_cost(c, br, bc);
   ++nsad;
   // one round: candidate idx (groups g < cnt) of scale s around (br, bc);
@@ -636,8 +665,7 @@ __device__ int pattern(const Ctx& c, int lane, int srow, int scol, int search_st
     // (check_bounds only skips this test when it holds)
     const bool valid =
         g < cnt && cc >= c.col_min && cc <= c.col_max && r >= c.row_min && r <= c.row_max;
-    const uint32_t mine =
-        S.group_sad(c, (int64_t)r * c.rs + cc, valid, (int64_t)br * c.rs + bc);
+    const uint32_t mine = S.group_sad(c, r, cc, valid, br, bc);
     const uint32_t key = valid ? ((mine + mvsad_cost(c, r, cc)) << 3) | (uint32_t)g : ~0u;
     uint32_t kmin = groups_min(key);
     ++steps;
@@ -734,9 +762,10 @@ __device__ int pattern(const Ctx& c, int lane, int srow, int scol, int search_st
 enum { kDiamond = 0, kBigdia = 5, kFastDiamond = 8, kFastBigdia = 9, kVfastDiamond = 10 };
 
 // PAT: the BIGDIA-site pattern searches (method 5 / 8 / 9 / 10), else DIAMOND
-template <int W, int H, bool PAT>
+template <int W, int H, bool PAT, bool TL>
 __global__ __launch_bounds__(256, (W <= 16 && H <= 16) ? 8 : 7) void diamond_kernel(const uint8_t* __restrict__ src, int ss,
                                                       const uint8_t* __restrict__ ref, int rs,
+                                                      LavishRefTiles tiles,
                                                       const Job* __restrict__ jobs, int njobs,
                                                       int step_param, LavishMvCostParams cost,
                                                       int skip, int method,
@@ -774,22 +803,31 @@ __global__ __launch_bounds__(256, (W <= 16 && H <= 16) ? 8 : 7) void diamond_ker
   c.mvjcost = cost.mvjcost;
   c.mvcost0 = cost.mvcost[0];
   c.mvcost1 = cost.mvcost[1];
+  if constexpr (TL) {
+    c.tiles = tiles.data;
+    c.fh = tiles.field_rows;
+    c.fsz = (int)tiles.field_bytes;
+    // the job's block origin as (row, column) of the whole buffer (uniform)
+    const int oy = (int)(jb.ref_off / rs);
+    c.oy = __builtin_amdgcn_readfirstlane(oy);
+    c.ox = __builtin_amdgcn_readfirstlane((int)(jb.ref_off - (int64_t)oy * rs));
+  }
   const bool want_cl = cost_lists != nullptr;
   int cl[5] = {INT_MAX, INT_MAX, INT_MAX, INT_MAX, INT_MAX};
   int br, bc, steps = 0, searches = 0, sme;
   auto search = [&](auto skip_tag) {
     constexpr bool SK = decltype(skip_tag)::value;
     if constexpr (!PAT) {
-      return full_pixel_diamond<W, H, SK>(c, lane, jb.start_row, jb.start_col, step_param, br,
-                                          bc, steps, searches, win, want_cl, cl);
+      return full_pixel_diamond<W, H, SK, TL>(c, lane, jb.start_row, jb.start_col, step_param,
+                                              br, bc, steps, searches, win, want_cl, cl);
     } else {
       // searches: the SAD blocks read (start, candidates, cost list) (do_init 1) / fast_dia / vfast_dia / fast_bigdia (mcomp.c:1266-1316)
       const int step = method == kBigdia        ? step_param
                        : method == kFastDiamond ? max(kMaxSteps - 2, step_param)
                        : method == kVfastDiamond ? max(kMaxSteps - 1, step_param)
                                                  : max(kMaxSteps - 3, step_param);
-      return pattern<W, H, SK>(c, lane, jb.start_row, jb.start_col, step, method == kBigdia,
-                               want_cl, cl, br, bc, steps, searches);
+      return pattern<W, H, SK, TL>(c, lane, jb.start_row, jb.start_col, step,
+                                   method == kBigdia, want_cl, cl, br, bc, steps, searches);
     }
   };
   // use_downsampled_sad applies to blocks at least 16 high (mcomp.c:132-133)
@@ -818,20 +856,68 @@ __global__ __launch_bounds__(256, (W <= 16 && H <= 16) ? 8 : 7) void diamond_ker
   }
 }
 
-template <int W, int H>
-void launch(const uint8_t* src, int ss, const uint8_t* ref, int rs, const LavishDiamondJob* jobs,
-            int njobs, int step_param, const LavishMvCostParams& cost, int skip, int method,
-            LavishDiamondResult* out, int32_t* cost_lists, hipStream_t s) {
+template <int W, int H, bool TL>
+void launch_tl(const uint8_t* src, int ss, const uint8_t* ref, int rs, const LavishRefTiles& t,
+               const LavishDiamondJob* jobs, int njobs, int step_param,
+               const LavishMvCostParams& cost, int skip, int method, LavishDiamondResult* out,
+               int32_t* cost_lists, hipStream_t s) {
   int nwg = (njobs + 3) / 4;
   nwg = (nwg + 7) & ~7;
   if (method == kDiamond)
-    hipLaunchKernelGGL((diamond_kernel<W, H, false>), dim3(nwg), dim3(256), 0, s, src, ss, ref,
-                       rs, (const Job*)jobs, njobs, step_param, cost, skip, method, out,
+    hipLaunchKernelGGL((diamond_kernel<W, H, false, TL>), dim3(nwg), dim3(256), 0, s, src, ss,
+                       ref, rs, t, (const Job*)jobs, njobs, step_param, cost, skip, method, out,
                        cost_lists);
   else
-    hipLaunchKernelGGL((diamond_kernel<W, H, true>), dim3(nwg), dim3(256), 0, s, src, ss, ref,
-                       rs, (const Job*)jobs, njobs, step_param, cost, skip, method, out,
+    hipLaunchKernelGGL((diamond_kernel<W, H, true, TL>), dim3(nwg), dim3(256), 0, s, src, ss,
+                       ref, rs, t, (const Job*)jobs, njobs, step_param, cost, skip, method, out,
                        cost_lists);
+}
+
+template <int W, int H>
+void launch(const uint8_t* src, int ss, const uint8_t* ref, int rs, const LavishRefTiles* t,
+            const LavishDiamondJob* jobs, int njobs, int step_param,
+            const LavishMvCostParams& cost, int skip, int method, LavishDiamondResult* out,
+            int32_t* cost_lists, hipStream_t s) {
+  if constexpr (W <= 16) {
+    if (t != nullptr) {
+      launch_tl<W, H, true>(src, ss, ref, rs, *t, jobs, njobs, step_param, cost, skip, method,
+                            out, cost_lists, s);
+      return;
+    }
+  }
+  const LavishRefTiles none{};
+  launch_tl<W, H, false>(src, ss, ref, rs, none, jobs, njobs, step_param, cost, skip, method,
+                         out, cost_lists, s);
+}
+
+// LavishRefTiles copy: one thread per 16-byte half of a 32-byte strip row
+// (strip k, field row fy, field f = bytes [16k + 16 half, +16) of buffer row
+// 2 fy + f); bytes past the row end or past the last row are zero
+__global__ __launch_bounds__(256) void ref_tiles_kernel(const uint8_t* __restrict__ ref,
+                                                        int stride, int rows, int nstrips,
+                                                        int fh, uint8_t* __restrict__ out,
+                                                        int64_t nchunks) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= nchunks) return;
+  const int half = (int)(i & 1);
+  const int64_t rowi = i >> 1;                   // (f * nstrips + k) * fh + fy
+  const int fy = (int)(rowi % fh);
+  const int64_t fk = rowi / fh;
+  const int k = (int)(fk % nstrips), f = (int)(fk / nstrips);
+  const int y = 2 * fy + f, x = 16 * k + 16 * half;
+  u32x4 v = {0u, 0u, 0u, 0u};
+  if (y < rows) {
+    const uint8_t* p = ref + (int64_t)y * stride + x;
+    if (x + 16 <= stride) {
+      const u32x4u w = *(const __attribute__((address_space(1))) u32x4u*)p;
+      v = u32x4{w.x, w.y, w.z, w.w};
+    } else {
+      uint32_t b[4] = {0u, 0u, 0u, 0u};
+      for (int j = 0; j < 16 && x + j < stride; ++j) b[j >> 2] |= (uint32_t)p[j] << (8 * (j & 3));
+      v = u32x4{b[0], b[1], b[2], b[3]};
+    }
+  }
+  *(u32x4*)(out + 16 * i) = v;
 }
 
 }  // namespace
@@ -839,8 +925,10 @@ void launch(const uint8_t* src, int ss, const uint8_t* ref, int rs, const Lavish
 int fullpel_batch(const uint8_t* src, int src_stride, const uint8_t* ref, int ref_stride, int w,
                   int h, const LavishDiamondJob* jobs, int njobs, int method, int step_param,
                   const LavishMvCostParams* cost, int use_downsampled_sad,
-                  LavishDiamondResult* out, int32_t* cost_lists, hipStream_t s) {
+                  LavishDiamondResult* out, int32_t* cost_lists, hipStream_t s,
+                  const LavishRefTiles* tiles = nullptr) {
   if (njobs <= 0) return 0;
+  if (tiles != nullptr && (tiles->data == nullptr || tiles->stride != ref_stride)) return -5;
   if (step_param < 0 || step_param >= kMaxSteps) return -1;
   if (cost == nullptr || cost->mv_cost_type < 0 || cost->mv_cost_type > 4) return -2;
   if (cost->mv_cost_type == 0 &&
@@ -851,7 +939,7 @@ int fullpel_batch(const uint8_t* src, int src_stride, const uint8_t* ref, int re
     return -4;
 #define LAVISH_DIA_CASE(W, H)                                                                 \
   if (w == W && h == H) {                                                                     \
-    launch<W, H>(src, src_stride, ref, ref_stride, jobs, njobs, step_param, *cost,            \
+    launch<W, H>(src, src_stride, ref, ref_stride, tiles, jobs, njobs, step_param, *cost,     \
                  use_downsampled_sad, method, out, cost_lists, s);                            \
     LAVISH_CHECK(hipGetLastError());                                                          \
     return 0;                                                                                 \
@@ -882,6 +970,40 @@ extern "C" int lavish_full_pixel_search_batch(const uint8_t* src, int src_stride
   return fullpel_batch(src, src_stride, ref, ref_stride, w, h, jobs, njobs, search_method,
                        step_param, cost, use_downsampled_sad, out, cost_lists,
                        (hipStream_t)stream);
+}
+
+static int64_t tiles_nstrips(int stride) { return (stride + 15) / 16; }
+
+extern "C" int64_t lavish_ref_tiles_bytes(int stride, int rows) {
+  if (stride <= 0 || rows <= 0) return -1;
+  return 2 * tiles_nstrips(stride) * ((rows + 1) / 2) * 32;
+}
+
+extern "C" int lavish_ref_tiles_build(const uint8_t* ref, int stride, int rows, uint8_t* data,
+                                      LavishRefTiles* tiles, void* stream) {
+  const int64_t bytes = lavish_ref_tiles_bytes(stride, rows);
+  if (ref == nullptr || data == nullptr || tiles == nullptr || bytes <= 0) return -1;
+  if (bytes >= ((int64_t)1 << 31)) return -1;  // 32-bit offsets in the search kernels
+  const int nstrips = (int)tiles_nstrips(stride), fh = (rows + 1) / 2;
+  tiles->data = data;
+  tiles->field_bytes = (int64_t)nstrips * fh * 32;
+  tiles->field_rows = fh;
+  tiles->stride = stride;
+  const int64_t nchunks = bytes / 16;
+  hipLaunchKernelGGL(ref_tiles_kernel, dim3((unsigned)((nchunks + 255) / 256)), dim3(256), 0,
+                     (hipStream_t)stream, ref, stride, rows, nstrips, fh, data, nchunks);
+  LAVISH_CHECK(hipGetLastError());
+  return 0;
+}
+
+extern "C" int lavish_full_pixel_search_batch_tiled(
+    const uint8_t* src, int src_stride, const uint8_t* ref, int ref_stride,
+    const LavishRefTiles* tiles, int w, int h, const LavishDiamondJob* jobs, int njobs,
+    int search_method, int step_param, const LavishMvCostParams* cost, int use_downsampled_sad,
+    LavishDiamondResult* out, int32_t* cost_lists, void* stream) {
+  return fullpel_batch(src, src_stride, ref, ref_stride, w, h, jobs, njobs, search_method,
+                       step_param, cost, use_downsampled_sad, out, cost_lists,
+                       (hipStream_t)stream, tiles);
 }
 
 extern "C" int lavish_diamond_search_batch(const uint8_t* src, int src_stride, const uint8_t* ref,

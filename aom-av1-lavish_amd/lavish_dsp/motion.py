@@ -49,6 +49,49 @@ _lib.lavish_full_pixel_search_batch.argtypes = [_vp, _i32, _vp, _i32, _i32, _i32
 _lib.lavish_full_pixel_search_batch.restype = _i32
 
 
+class RefTilesDesc(ctypes.Structure):
+    """LavishRefTiles (include/lavish_dsp.h)."""
+    _fields_ = [("data", ctypes.c_void_p), ("field_bytes", ctypes.c_int64),
+                ("field_rows", ctypes.c_int32), ("stride", ctypes.c_int32)]
+
+
+_lib.lavish_ref_tiles_bytes.argtypes = [_i32, _i32]
+_lib.lavish_ref_tiles_bytes.restype = ctypes.c_int64
+_lib.lavish_ref_tiles_build.argtypes = [_vp, _i32, _i32, _vp, ctypes.POINTER(RefTilesDesc), _vp]
+_lib.lavish_ref_tiles_build.restype = _i32
+_lib.lavish_full_pixel_search_batch_tiled.argtypes = [
+    _vp, _i32, _vp, _i32, ctypes.POINTER(RefTilesDesc), _i32, _i32, _vp, _i32, _i32, _i32,
+    ctypes.POINTER(MvCostParams), _i32, _vp, _vp, _vp]
+_lib.lavish_full_pixel_search_batch_tiled.restype = _i32
+
+
+class RefTiles:
+    """The searches' candidate-row copy of a device u8 reference buffer
+    (lavish_ref_tiles_build): every row of `ref` viewed as rows x stride.
+    build() refreshes it (asynchronously, on `stream`) after the buffer
+    changes."""
+
+    def __init__(self, ref, stride=None):
+        import torch
+        assert ref.dtype == torch.uint8 and ref.is_contiguous()
+        self.ref = ref
+        self.stride = int(stride if stride is not None else ref.shape[-1])
+        self.rows = ref.numel() // self.stride
+        n = _lib.lavish_ref_tiles_bytes(self.stride, self.rows)
+        if n <= 0:
+            raise ValueError("lavish_ref_tiles_bytes rejected (%d, %d)" % (self.stride, self.rows))
+        self.data = torch.empty(n, dtype=torch.uint8, device=ref.device)
+        self.desc = RefTilesDesc()
+
+    def build(self, stream=None):
+        rc = _lib.lavish_ref_tiles_build(_vp(self.ref.data_ptr()), self.stride, self.rows,
+                                         _vp(self.data.data_ptr()), ctypes.byref(self.desc),
+                                         _stream_ptr(stream))
+        if rc != 0:
+            raise ValueError("lavish_ref_tiles_build rejected its arguments (rc=%d)" % rc)
+        return self
+
+
 class MvCosts:
     """Device copy of an nmv cost context (x->mv_costs): mvjcost int32[4] and
     mvcost int32[2][2 * MV_MAX + 1] as av1_build_nmv_cost_table lays them
@@ -201,7 +244,7 @@ def diamond_search_batch(src, ref, w, h, jobs, step_param=0, mv_cost_type=MV_COS
 
 def full_pixel_search_batch(src, ref, w, h, jobs, cost, method="diamond", step_param=0,
                             use_downsampled_sad=False, cost_list=False, out=None,
-                            cost_lists=None, stream=None):
+                            cost_lists=None, stream=None, tiles=None):
     """lavish_full_pixel_search_batch (av1_full_pixel_search): planes and jobs
     as diamond_search_batch, cost a MvCostParams (MvCosts.cost_params or
     l1_cost_params).  Returns (RESULT_DTYPE byte tensor, int32 [n, 5] cost
@@ -214,11 +257,19 @@ def full_pixel_search_batch(src, ref, w, h, jobs, cost, method="diamond", step_p
         out = torch.empty(nj * RESULT_DTYPE.itemsize, dtype=torch.uint8, device=src.device)
     if cost_list and cost_lists is None:
         cost_lists = torch.empty((nj, 5), dtype=torch.int32, device=src.device)
-    rc = _lib.lavish_full_pixel_search_batch(
-        _vp(src.data_ptr()), src.stride(0), _vp(ref.data_ptr()), src.stride(0), w, h,
-        _vp(jobs.data_ptr()), nj, SEARCH_METHODS[method], step_param, ctypes.byref(cost),
-        int(use_downsampled_sad), _vp(out.data_ptr()),
-        _vp(cost_lists.data_ptr()) if cost_list else None, _stream_ptr(stream))
+    if tiles is not None:  # RefTiles of `ref`: candidate rows from the tiled copy
+        assert tiles.ref.data_ptr() == ref.data_ptr() and tiles.stride == src.stride(0)
+        rc = _lib.lavish_full_pixel_search_batch_tiled(
+            _vp(src.data_ptr()), src.stride(0), _vp(ref.data_ptr()), src.stride(0),
+            ctypes.byref(tiles.desc), w, h, _vp(jobs.data_ptr()), nj, SEARCH_METHODS[method],
+            step_param, ctypes.byref(cost), int(use_downsampled_sad), _vp(out.data_ptr()),
+            _vp(cost_lists.data_ptr()) if cost_list else None, _stream_ptr(stream))
+    else:
+        rc = _lib.lavish_full_pixel_search_batch(
+            _vp(src.data_ptr()), src.stride(0), _vp(ref.data_ptr()), src.stride(0), w, h,
+            _vp(jobs.data_ptr()), nj, SEARCH_METHODS[method], step_param, ctypes.byref(cost),
+            int(use_downsampled_sad), _vp(out.data_ptr()),
+            _vp(cost_lists.data_ptr()) if cost_list else None, _stream_ptr(stream))
     if rc != 0:
         raise ValueError("lavish_full_pixel_search_batch rejected its arguments (rc=%d)" % rc)
     return out, (cost_lists if cost_list else None)

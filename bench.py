@@ -1434,9 +1434,15 @@ def main():
         sub_out = torch.empty(len(jobs_np) * M.SUBPEL_RESULT_DTYPE.itemsize, dtype=torch.uint8,
                               device="cuda")
 
+    # the searches' candidate-row copy of the references (LavishRefTiles),
+    # rebuilt inside every step: the frame's references are new per frame
+    c3_tiles = M.RefTiles(trefs, st)
+
     def c3(on):
+        c3_tiles.build(stream=on)
         M.full_pixel_search_batch(tsrc, trefs, C3_BLOCK, C3_BLOCK, tjobs, c3_cost, "diamond", 0,
-                                  C3_SKIP, C3_CL, out=c3_out, cost_lists=c3_cl, stream=on)
+                                  C3_SKIP, C3_CL, out=c3_out, cost_lists=c3_cl, stream=on,
+                                  tiles=c3_tiles)
         if do_sub:  # chained on the device: starts + cost lists = the full-pel results
             M.find_best_sub_pixel_tree_batch(tsrc, trefs, C3_BLOCK, C3_BLOCK, sub_jobs, c3_cost,
                                              "pruned_more", SUB_FORCED_STOP, allow_hp, SUB_ITERS,
@@ -1520,8 +1526,9 @@ def main():
         c2_ms = sum(evs[k][3].elapsed_time(evs[k][4]) for k in range(KS)) / KS
     c2_bytes = sum(algorithmic_bytes(L, s, W, H) for s in sizes)
     c3_res = M.results_numpy(c3_out) if do_c3 else None
+    # + the tiled copy of the references: read once, written at 2x
     c3_bytes = c3_algorithmic_bytes(c3_res, len(jobs_np), C3_BLOCK, C3_BLOCK, C3_SKIP, C3_CL) \
-        if do_c3 else 0
+        + trefs.numel() + c3_tiles.data.numel() if do_c3 else 0
 
     traffic = None
     if os.path.exists(args.pmc_json):
@@ -1539,7 +1546,8 @@ def main():
                 "algorithmic_bytes_per_launch": c2_bytes}
     else:
         roof = {"bound": "hbm",
-                "kernel": "diamond_kernel<16,16,false> (lavish_full_pixel_search_batch)",
+                "kernel": "ref_tiles_kernel + diamond_kernel<16,16,false,true> "
+                          "(lavish_ref_tiles_build + lavish_full_pixel_search_batch_tiled)",
                 "achieved": round(c3_bytes / (c3_ms * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBS,
                 "unit": "GB/s", "traffic": None, "avg_launch_ms": round(c3_ms, 4),
                 "algorithmic_bytes_per_launch": c3_bytes}
@@ -1554,7 +1562,8 @@ def main():
     if do_c3:
         legs.append("C3 DIAMOND full-pel search of every %dx%d block x %d refs (downsampled SAD, "
                     "MV_COST_ENTROPY default nmv context, sadperbit %d, errorperbit %d, "
-                    "cost list, step_param 0)" % (C3_BLOCK, C3_BLOCK, args.refs,
+                    "cost list, step_param 0; candidate rows from the references' tiled copy, "
+                    "rebuilt per step)" % (C3_BLOCK, C3_BLOCK, args.refs,
                                                   c3_cost.sad_per_bit, c3_cost.error_per_bit))
     if do_sub:
         legs.append("sub-pel refinement SUBPEL_TREE_PRUNED_MORE to %s pel (bilinear svf, "

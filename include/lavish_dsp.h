@@ -547,6 +547,43 @@ int lavish_full_pixel_search_batch(const uint8_t *src, int src_stride,
                                    LavishDiamondResult *out, int32_t *cost_lists,
                                    void *stream);
 
+/* Candidate-row layout of the reference buffer for the full-pel searches
+ * (the build's own addition, no reference counterpart; results are
+ * identical with or without it).  The searches read, per candidate, rows
+ * y, y + 2, ... (downsampled SAD) of a w <= 16 byte segment at any column:
+ * in the linear plane every such row is a separate cache line.  The tiled
+ * copy splits the buffer's rows by parity (two fields) and each field into
+ * 32-byte-wide column strips starting every 16 bytes (strip k holds bytes
+ * [16k, 16k + 32) of every field row, consecutive field rows 32 bytes
+ * apart), so a 16-byte segment lies in one strip and a downsampled 16-row
+ * candidate in 2-3 cache lines instead of 8.  2x the buffer's bytes.
+ *   rows: rows of the whole buffer (all reference planes stacked, stride
+ *   `ref_stride`); the tiled copy must be rebuilt when the buffer changes. */
+typedef struct LavishRefTiles {
+  const uint8_t *data; /* device; lavish_ref_tiles_bytes(stride, rows) bytes */
+  int64_t field_bytes; /* bytes of one field (the odd field follows the even) */
+  int32_t field_rows;  /* (rows + 1) / 2 */
+  int32_t stride;      /* the linear buffer's stride (= ref_stride) */
+} LavishRefTiles;
+int64_t lavish_ref_tiles_bytes(int stride, int rows);
+/* Fills tiles->data (caller-allocated, device) from the linear buffer and
+ * sets the other fields; asynchronous on `stream`.  -1 on bad arguments or
+ * a copy of 2 GiB or more. */
+int lavish_ref_tiles_build(const uint8_t *ref, int stride, int rows, uint8_t *data,
+                           LavishRefTiles *tiles, void *stream);
+/* lavish_full_pixel_search_batch reading candidate rows from the tiled copy
+ * of the same `ref` buffer (w <= 16; other sizes, or tiles == NULL, run the
+ * linear form).  Same results. */
+int lavish_full_pixel_search_batch_tiled(const uint8_t *src, int src_stride,
+                                         const uint8_t *ref, int ref_stride,
+                                         const LavishRefTiles *tiles, int w, int h,
+                                         const LavishDiamondJob *jobs, int njobs,
+                                         int search_method, int step_param,
+                                         const LavishMvCostParams *cost,
+                                         int use_downsampled_sad,
+                                         LavishDiamondResult *out,
+                                         int32_t *cost_lists, void *stream);
+
 /* ---- sub-pixel refinement ------------------------
  * av1_find_best_sub_pixel_tree_pruned_more (av1/encoder/mcomp.c:2907-2981;
  * subpel_search_method SUBPEL_TREE_PRUNED_MORE, speed >= 4) without a cost

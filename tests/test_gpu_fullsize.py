@@ -65,8 +65,14 @@ def test_c3_1080p_7refs_all_jobs(L):
     sub = M.find_best_sub_pixel_tree_batch(tsrc, trefs, b.C3_BLOCK, b.C3_BLOCK, M.to_device(sj),
                                            cp, "pruned_more", b.SUB_FORCED_STOP, allow_hp,
                                            b.SUB_ITERS, fullpel=fp, cost_lists=cl)
+    # the bench's form: candidate rows from the tiled copy (LavishRefTiles)
+    tiles = M.RefTiles(trefs, st).build()
+    fpt, clt = M.full_pixel_search_batch(tsrc, trefs, b.C3_BLOCK, b.C3_BLOCK, M.to_device(jobs),
+                                         cp, "diamond", 0, b.C3_SKIP, b.C3_CL, tiles=tiles)
     torch.cuda.synchronize()
     got, got_cl = M.results_numpy(fp), cl.cpu().numpy()
+    np.testing.assert_array_equal(M.results_numpy(fpt), got)
+    np.testing.assert_array_equal(clt.cpu().numpy(), got_cl)
     exp, exp_cl = O.full_pixel_search_batch(src.reshape(-1), refs.reshape(-1), st, b.C3_BLOCK,
                                             b.C3_BLOCK, jobs, "diamond", 0, b.C3_COST, spb, epb,
                                             mvj, mvc, skip=b.C3_SKIP, cost_list=b.C3_CL,

@@ -21,19 +21,24 @@ def F():
     return dict(np.load(os.path.join(GOLD, "fix_mcomp.npz")))
 
 
-def test_full_pixel_search_vs_reference(F):
+@pytest.mark.parametrize("tiled", [False, True])
+def test_full_pixel_search_vs_reference(F, tiled):
+    """tiled: candidate rows from the LavishRefTiles copy of the references
+    (w <= 16; larger blocks take the linear form through the same call)."""
     import torch
     assert torch.cuda.is_available()
     from lavish_dsp import motion as M
     src = torch.from_numpy(F["src"]).cuda()
     refs = torch.from_numpy(np.ascontiguousarray(F["refs"])).cuda()
+    tiles = M.RefTiles(refs, src.stride(0)).build() if tiled else None
     costs = M.MvCosts(F["mvjcost_lp"], F["mvcost_lp"])
     n = 0
     for case, bw, bh, epb, spb, rec, rows, J in mcomp_groups(F):
         m, use_cl, ctype, skip, sp = (int(v) for v in case)
         cp = costs.cost_params(spb, epb, ctype)
         out, cl = M.full_pixel_search_batch(src, refs, bw, bh, M.to_device(rec), cp,
-                                            MS_METHODS[m], sp, bool(skip), bool(use_cl))
+                                            MS_METHODS[m], sp, bool(skip), bool(use_cl),
+                                            tiles=tiles)
         torch.cuda.synchronize()
         res = M.results_numpy(out)
         msg = "case %s %dx%d" % ([int(v) for v in case], bw, bh)
@@ -135,3 +140,26 @@ def test_fullpel_then_subpel_chain(F):
         np.testing.assert_array_equal(a, b)
         checked += len(rows)
     assert checked > 50
+
+
+@pytest.mark.parametrize("stride,rows", [(64, 48), (2240, 9), (100, 7)])
+def test_ref_tiles_layout(stride, rows):
+    """lavish_ref_tiles_build: field f, strip k, field row fy holds bytes
+    [16k, 16k + 32) of buffer row 2 fy + f; zero past the row end / last row."""
+    import torch
+    from lavish_dsp import motion as M
+    rng = np.random.default_rng(stride + rows)
+    buf = rng.integers(0, 256, (rows, stride)).astype(np.uint8)
+    t = M.RefTiles(torch.from_numpy(buf).cuda(), stride).build()
+    torch.cuda.synchronize()
+    got = t.data.cpu().numpy()
+    ns, fh = (stride + 15) // 16, (rows + 1) // 2
+    assert t.desc.field_rows == fh and t.desc.field_bytes == ns * fh * 32
+    assert got.size == 2 * ns * fh * 32
+    pad = np.zeros((2 * fh, ns * 16 + 32), np.uint8)
+    pad[:rows, :stride] = buf
+    exp = np.zeros((2, ns, fh, 32), np.uint8)
+    for f in range(2):
+        for k in range(ns):
+            exp[f, k] = pad[f::2, 16 * k:16 * k + 32]
+    np.testing.assert_array_equal(got.reshape(2, ns, fh, 32), exp)
