@@ -159,6 +159,8 @@ __device__ __forceinline__ uint32_t tile_off(const Ctx& c, int y, int x) {
          ((uint32_t)(__mul24(x >> 4, c.fh) + (y >> 1)) << 5) + (uint32_t)(x & 15);
 }
 
+__device__ const int32_t kZeroRate[1] = {0};
+
 __device__ __forceinline__ int sad_lambda(int t) { return t == 1 ? 32 : t == 2 ? 15 : t == 3 ? 8 : 0; }
 __device__ __forceinline__ int sse_lambda(int t) { return t == 1 ? 2 : t == 2 ? 0 : t == 3 ? 1 : 0; }
 
@@ -168,12 +170,32 @@ __device__ __forceinline__ int mv_rate(const Ctx& c, int dr, int dc) {
   return c.mvjcost[joint] + c.mvcost0[dr] + c.mvcost1[dc];
 }
 
-// mvsad_err_cost (mcomp.c:329-350); the L1 lambdas are 0 for MV_COST_NONE
-__device__ __forceinline__ uint32_t mvsad_cost(const Ctx& c, int row, int col) {
+// mvsad_err_cost (mcomp.c:329-350); the L1 lambdas are 0 for MV_COST_NONE.
+// In two parts so a search step can put the table loads in flight before
+// its candidate's SAD load and consume them after (one L2 round trip per
+// step, not two): mvsad_rate() issues the three loads -- branch-free: for
+// the L1 / none cost types the kernel points the tables at kZeroRate and
+// the indices are 0 -- and mvsad_finish() forms the cost.
+struct MvRate {
+  int32_t j, r, c;
+};
+__device__ __forceinline__ MvRate mvsad_rate(const Ctx& c, int row, int col) {
   const int dr = (row - c.full_ref_row) * 8, dc = (col - c.full_ref_col) * 8;
-  if (c.cost_type == 0)  // ROUND_POWER_OF_TWO(., AV1_PROB_COST_SHIFT); rates < 2^24
-    return (__umul24((uint32_t)mv_rate(c, dr, dc), (uint32_t)c.sad_per_bit) + 256u) >> 9;
-  return (uint32_t)((c.sad_lambda * (abs(dr) + abs(dc))) >> 3);
+  const bool ent = c.cost_type == 0;
+  const int joint = ent ? ((dc != 0) | ((dr != 0) << 1)) : 0;  // av1_get_mv_joint
+  typedef const __attribute__((address_space(1))) int32_t* gi32;
+  return MvRate{((gi32)c.mvjcost)[joint], ((gi32)c.mvcost0)[ent ? dr : 0],
+                ((gi32)c.mvcost1)[ent ? dc : 0]};
+}
+__device__ __forceinline__ uint32_t mvsad_finish(const Ctx& c, const MvRate& m, int row, int col) {
+  const int dr = (row - c.full_ref_row) * 8, dc = (col - c.full_ref_col) * 8;
+  // ROUND_POWER_OF_TWO(., AV1_PROB_COST_SHIFT); rates < 2^24
+  const uint32_t e = (__umul24((uint32_t)(m.j + m.r + m.c), (uint32_t)c.sad_per_bit) + 256u) >> 9;
+  const uint32_t l1 = (uint32_t)((c.sad_lambda * (abs(dr) + abs(dc))) >> 3);
+  return c.cost_type == 0 ? e : l1;
+}
+__device__ __forceinline__ uint32_t mvsad_cost(const Ctx& c, int row, int col) {
+  return mvsad_finish(c, mvsad_rate(c, row, col), row, col);
 }
 // mv_err_cost (mcomp.c:290-314)
 __device__ __forceinline__ int mv_cost(const Ctx& c, int row, int col) {
@@ -508,26 +530,25 @@ struct Search {
     uint32_t best = mvsad_cost(c, row, col) + c0sad;
     const int tot = kMaxSteps - search_step;
     inwin = false;
-    for (int step = tot - 1; step >= 0; --step) {
-      const int rad = 1 << step;
-      if constexpr (WN::kOn && kCache) {
-        if (!inwin && rad <= WN::MAXRAD && win != nullptr) {
-          // a later run reaching radius 8 at the same point finds its window
-          if (!wfilled || wr0 != row - WN::R || wc0 != col - WN::R) fill(c, lane, row, col);
-          wfilled = true;
-          inwin = true;
-        }
-      }
+    // one step: the 8 sites at radius rad around (row, col), straight-line
+    // (the candidate's SAD load and the mv-cost table loads issue together)
+    auto step_at = [&](int rad, auto win_tag) {
+      constexpr bool INW = decltype(win_tag)::value;
       // (all_in of the reference only skips this test when it holds)
       const int r = row + sdr * rad, cc = col + sdc * rad;
       const bool valid = cc >= c.col_min && cc <= c.col_max && r >= c.row_min && r <= c.row_max;
-      // the mv cost first (its table reads overlap the SAD); |r|, |cc| < 2048
-      // keep every index inside the cost tables, valid or not
-      const uint32_t mvs = mvsad_cost(c, r, cc);
-      const uint32_t mine = inwin ? group_sad_win(c, r, cc, valid)
-                                  : group_sad(c, r, cc, valid, row, col);
-      // key = cost * 8 + site (costs < 2^26 for blocks <= 128x128)
-      const uint32_t key = valid ? ((mine + mvs) << 3) | (uint32_t)g : ~0u;
+      // the mv-cost table loads first, consumed after the SAD: both L2
+      // round trips overlap (|r|, |cc| < 2048 keep every index inside the
+      // cost tables, valid or not)
+      const MvRate mr = mvsad_rate(c, r, cc);
+      uint32_t mine;
+      if constexpr (INW) mine = group_sad_win(c, r, cc, valid);
+      else mine = group_sad(c, r, cc, valid, row, col);
+      const uint32_t mvs = mvsad_finish(c, mr, r, cc);
+      // key = cost * 8 + site (costs < 2^26 for blocks <= 128x128); ~0 for
+      // an invalid site -- an OR, not a select, so the cost (and its loads)
+      // is computed unconditionally, in the SAD's basic block
+      const uint32_t key = (((mine + mvs) << 3) | (uint32_t)g) | (valid ? 0u : ~0u);
       const uint32_t kmin = groups_min(key);
       ++steps;
       if (kmin < (best << 3)) {
@@ -538,6 +559,21 @@ struct Search {
         off_center = 1;
       }
       if (!off_center) ++center;
+    };
+    int step = tot - 1;
+    constexpr bool kWin = WN::kOn && kCache;
+    // large radii: candidates from global memory (L2)
+    for (; step >= 0 && (!kWin || win == nullptr || (1 << step) > WN::MAXRAD); --step)
+      step_at(1 << step, std::false_type{});
+    if constexpr (kWin) {
+      if (step >= 0) {
+        // radius <= 8: the walk stays inside the LDS window around (row, col)
+        // (a later run reaching radius 8 at the same point finds its window)
+        if (!wfilled || wr0 != row - WN::R || wc0 != col - WN::R) fill(c, lane, row, col);
+        wfilled = true;
+        inwin = true;
+        for (; step >= 0; --step) step_at(1 << step, std::true_type{});
+      }
     }
     brow = row;
     bcol = col;
@@ -665,8 +701,10 @@ __device__ int pattern(const Ctx& c, int lane, int srow, int scol, int search_st
     // (check_bounds only skips this test when it holds)
     const bool valid =
         g < cnt && cc >= c.col_min && cc <= c.col_max && r >= c.row_min && r <= c.row_max;
+    const MvRate mr = mvsad_rate(c, r, cc);  // in flight with the SAD's loads
     const uint32_t mine = S.group_sad(c, r, cc, valid, br, bc);
-    const uint32_t key = valid ? ((mine + mvsad_cost(c, r, cc)) << 3) | (uint32_t)g : ~0u;
+    const uint32_t key =
+        (((mine + mvsad_finish(c, mr, r, cc)) << 3) | (uint32_t)g) | (valid ? 0u : ~0u);
     uint32_t kmin = groups_min(key);
     ++steps;
     nsad += __popcll(__ballot(valid)) >> 3;  // candidate blocks read this round
@@ -758,12 +796,18 @@ __device__ int pattern(const Ctx& c, int lane, int srow, int scol, int search_st
   return var_cost<W, H>(c, lane, br, bc);  // get_mvpred_var_cost
 }
 
+// waves (jobs) per workgroup of the search kernels
+#ifndef LAVISH_DK_WAVES
+#define LAVISH_DK_WAVES 4
+#endif
+constexpr int kDkWaves = LAVISH_DK_WAVES;
+
 // search_method values of SEARCH_METHODS (av1/encoder/mcomp_structs.h:56-86)
 enum { kDiamond = 0, kBigdia = 5, kFastDiamond = 8, kFastBigdia = 9, kVfastDiamond = 10 };
 
 // PAT: the BIGDIA-site pattern searches (method 5 / 8 / 9 / 10), else DIAMOND
 template <int W, int H, bool PAT, bool TL>
-__global__ __launch_bounds__(256, (W <= 16 && H <= 16) ? 8 : 7) void diamond_kernel(const uint8_t* __restrict__ src, int ss,
+__global__ __launch_bounds__(64 * kDkWaves, (W <= 16 && H <= 16) ? 8 : 7) void diamond_kernel(const uint8_t* __restrict__ src, int ss,
                                                       const uint8_t* __restrict__ ref, int rs,
                                                       LavishRefTiles tiles,
                                                       const Job* __restrict__ jobs, int njobs,
@@ -776,10 +820,10 @@ __global__ __launch_bounds__(256, (W <= 16 && H <= 16) ? 8 : 7) void diamond_ker
   const int wg = (blockIdx.x & 7) * (nwg >> 3) + (blockIdx.x >> 3);
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int j = wg * 4 + wave;
+  const int j = wg * kDkWaves + wave;
   if (j >= njobs) return;
   constexpr int WS = PAT ? 1 : Win<W, H>::SIZE;  // the window serves DIAMOND only
-  __shared__ uint32_t win_s[4 * WS];
+  __shared__ uint32_t win_s[kDkWaves * WS];
   const lds_u32 win = (!PAT && Win<W, H>::kOn) ? (lds_u32)(win_s + wave * WS) : nullptr;
   const Job jb = jobs[j];
   Ctx c;
@@ -800,9 +844,10 @@ __global__ __launch_bounds__(256, (W <= 16 && H <= 16) ? 8 : 7) void diamond_ker
   c.sse_lambda = sse_lambda(cost.mv_cost_type);
   c.sad_per_bit = cost.sad_per_bit;
   c.error_per_bit = cost.error_per_bit;
-  c.mvjcost = cost.mvjcost;
-  c.mvcost0 = cost.mvcost[0];
-  c.mvcost1 = cost.mvcost[1];
+  const bool ent = cost.mv_cost_type == 0;  // (mvsad_cost: zero tables otherwise)
+  c.mvjcost = ent ? cost.mvjcost : kZeroRate;
+  c.mvcost0 = ent ? cost.mvcost[0] : kZeroRate;
+  c.mvcost1 = ent ? cost.mvcost[1] : kZeroRate;
   if constexpr (TL) {
     c.tiles = tiles.data;
     c.fh = tiles.field_rows;
@@ -856,19 +901,286 @@ __global__ __launch_bounds__(256, (W <= 16 && H <= 16) ? 8 : 7) void diamond_ker
   }
 }
 
+// ---------------------------------------------------------------------------
+// DIAMOND, 16x16 blocks, tiled references: eight jobs per wave.
+//
+// The one-job-per-wave kernel spends ~70 VALU + ~60 SALU instructions per
+// 8-site step on one job: its time goes to instruction issue and to the
+// per-step dependency chain, not to memory (halving its address-path work
+// with the tiled layout changed nothing, profiles/r03_*).  Here lane
+// (j = lane >> 3, l = lane & 7) works for job j of eight: a step evaluates
+// the job's 8 sites one after the other, lane l reading row 2l (downsampled
+// SAD; rows l and l + 8 otherwise) of each candidate from the tiled copy, so
+// one load instruction covers one site of all eight jobs (8 x 256 contiguous
+// bytes) and one step's bookkeeping serves eight jobs.  Each job carries its
+// own walk in the lanes of its group (row, col, radius, search index, num00
+// state): jobs at different radii / searches step together, branch-free.
+// full_pixel_diamond's var costs do not steer the search sequence (n and
+// num00 come from the walks alone), so each search's result is recorded and
+// the var costs are evaluated once the job's walks are done, in the
+// reference's order with its strict "sme < bestsme".  Then the cost list,
+// the downsampled-SAD quality check (mcomp.c:1840-1867) and, for the jobs it
+// fails, a second pass with full-row SADs.  Bit-exact with diamond_kernel.
+constexpr int kLjJobs = 8;  // jobs per wave
+
+__device__ __forceinline__ uint32_t group_min8(uint32_t v) {  // min over the 8-lane group
+  v = min(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, false));
+  v = min(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xF, 0xF, false));
+  v = min(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x141, 0xF, 0xF, false));
+  return v;
+}
+
+// source rows of lane l: sk = row 2l (downsampled SAD), fr[k] = row l + 8k
+struct LjSrc {
+  uint32_t sk[4], fr[2][4];
+};
+
+// group SAD of the job's candidate at (r, cc) (in range), from the tiles
+template <bool SKIP>
+__device__ __forceinline__ uint32_t lj_sad(const Ctx& c, const LjSrc& s, int l, int r, int cc) {
+  const int x = c.ox + cc;
+  uint32_t acc = 0;
+  if constexpr (SKIP) {
+    uint32_t t[4];
+    load_row<4>(c.tiles + tile_off(c, c.oy + r + 2 * l, x), t);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) acc = sad4(s.sk[i], t[i], acc);
+  } else {
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      uint32_t t[4];
+      load_row<4>(c.tiles + tile_off(c, c.oy + r + l + 8 * k, x), t);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) acc = sad4(s.fr[k][i], t[i], acc);
+    }
+  }
+  acc = group_sum8(acc);
+  return SKIP ? 2 * acc : acc;
+}
+
+// aom_variance16x16 + mv_err_cost at (r, cc), the linear reference; lane l
+// takes rows l and l + 8
+__device__ __forceinline__ int lj_var(const Ctx& c, const LjSrc& s, int l, int r, int cc) {
+  int sum = 0;
+  uint32_t sse = 0;
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    uint32_t t[4];
+    load_row<4>(c.ref + (int64_t)(r + l + 8 * k) * c.rs + cc, t);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) var_acc(s.fr[k][i], t[i], sum, sse);
+  }
+  const uint32_t ts = group_sum8((uint32_t)sum), tq = group_sum8(sse);
+  const uint32_t var = tq - (uint32_t)(((int64_t)(int)ts * (int)ts) / 256);
+  return (int)var + mv_cost(c, r, cc);
+}
+
+// one pass of full_pixel_diamond (+ its cost list) for the wave's jobs whose
+// `run` is set; accumulates steps / searches, leaves the pass's best mv, var
+// cost and cost list
+template <bool SKIP>
+__device__ void lj_pass(const Ctx& c, const LjSrc& s, int l, bool run, int step_param,
+                        bool want_cl, uint32_t* res, int& steps, int& searches, int& br,
+                        int& bc, int& sme, int (&cl)[5]) {
+  // (br / bc carry the start mv on entry; diamond_search_sad clamps it)
+  const int srow = min(max(br, c.row_min), c.row_max);
+  const int scol = min(max(bc, c.col_min), c.col_max);
+  const int sdr = site_dr(l), sdc = site_dc(l);
+  // the start: its SAD once per pass (every run restarts there)
+  const uint32_t c0 = lj_sad<SKIP>(c, s, l, srow, scol) + mvsad_cost(c, srow, scol);
+  const int further = kMaxSteps - 1 - step_param;
+  bool active = run;
+  bool first = true;
+  int n = 0, row = srow, col = scol, stp = kMaxSteps - step_param - 1, center = 0, nres = 0;
+  bool offc = false;
+  uint32_t best = c0;
+  while (__builtin_amdgcn_ballot_w64(active) != 0) {
+    const int rad = 1 << stp;
+    // lane l: site l's cost (its loads in flight with the SAD loads below)
+    const int rl = row + sdr * rad, cl_ = col + sdc * rad;
+    const bool vl = cl_ >= c.col_min && cl_ <= c.col_max && rl >= c.row_min && rl <= c.row_max;
+    const MvRate mr = mvsad_rate(c, rl, cl_);
+    uint32_t mine = 0;
+#pragma unroll
+    for (int t = 0; t < 8; ++t) {
+      const int r = row + site_dr(t) * rad, cc = col + site_dc(t) * rad;
+      const bool v = cc >= c.col_min && cc <= c.col_max && r >= c.row_min && r <= c.row_max;
+      const uint32_t sd = lj_sad<SKIP>(c, s, l, v ? r : row, v ? cc : col);
+      mine = l == t ? sd : mine;
+    }
+    const uint32_t key =
+        (((mine + mvsad_finish(c, mr, rl, cl_)) << 3) | (uint32_t)l) | (vl ? 0u : ~0u);
+    const uint32_t kmin = group_min8(key);
+    if (active) {
+      ++steps;
+      if (kmin < (best << 3)) {
+        best = kmin >> 3;
+        const int i = (int)(kmin & 7);
+        row += site_dr(i) * rad;
+        col += site_dc(i) * rad;
+        offc = true;
+      }
+      if (!offc) ++center;
+      if (--stp < 0) {  // this diamond_search_sad run is over
+        if (l == 0) res[nres] = ((uint32_t)(uint16_t)row << 16) | (uint16_t)col;
+        ++nres;
+        ++searches;
+        if (first) n = center;       // the first run's num00
+        else if (center) n += center;
+        first = false;
+        if (n < further) {           // the next run, one step shorter
+          ++n;
+          row = srow;
+          col = scol;
+          best = c0;
+          stp = kMaxSteps - (step_param + n) - 1;
+          center = 0;
+          offc = false;
+        } else {
+          active = false;
+          stp = 0;  // a finished job keeps stepping in place at radius 1 (masked)
+        }
+      }
+    }
+  }
+  wave_sync();
+  if (!run) return;
+  // var costs of the runs' results in order, strict "<" (full_pixel_diamond)
+  for (int i = 0; i < nres; ++i) {
+    const uint32_t p = res[i];
+    const int r = (int16_t)(p >> 16), cc = (int16_t)(p & 0xFFFF);
+    const int v = lj_var(c, s, l, r, cc);
+    if (i == 0 || v < sme) {
+      sme = v;
+      br = r;
+      bc = cc;
+    }
+  }
+  if (want_cl) {  // calc_int_sad_list around (br, bc): centre, left, bottom, right, top
+#pragma unroll
+    for (int t = 0; t < 5; ++t) {
+      const int r = br + (t == 2 ? 1 : t == 4 ? -1 : 0), cc = bc + (t == 1 ? -1 : t == 3 ? 1 : 0);
+      const bool v = t == 0 ||
+                     (cc >= c.col_min && cc <= c.col_max && r >= c.row_min && r <= c.row_max);
+      const uint32_t sd = lj_sad<SKIP>(c, s, l, v ? r : br, v ? cc : bc);
+      cl[t] = v ? (int)(sd + mvsad_cost(c, r, cc)) : INT_MAX;
+    }
+  }
+}
+
+__global__ __launch_bounds__(256, 4) void diamond_lj_kernel(
+    const uint8_t* __restrict__ src, int ss, const uint8_t* __restrict__ ref, int rs,
+    LavishRefTiles tiles, const Job* __restrict__ jobs, int njobs, int step_param,
+    LavishMvCostParams cost, int skip, LavishDiamondResult* __restrict__ out,
+    int32_t* __restrict__ cost_lists) {
+  // XCD-aware: consecutive job groups (neighbouring blocks) share an XCD's L2
+  const int nwg = gridDim.x;  // multiple of 8
+  const int wg = (blockIdx.x & 7) * (nwg >> 3) + (blockIdx.x >> 3);
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int jg = lane >> 3, l = lane & 7;
+  const int j0 = (wg * 4 + wave) * kLjJobs;
+  if (j0 >= njobs) return;
+  const int j = min(j0 + jg, njobs - 1);  // a surplus group repeats the last job, never stores
+  const bool mine_job = j0 + jg < njobs;
+  __shared__ uint32_t res_s[4][kLjJobs][kMaxSteps];
+  uint32_t* res = res_s[wave][jg];
+  const Job jb = jobs[j];
+  Ctx c;
+  c.src = src + jb.src_off;
+  c.ref = ref + jb.ref_off;
+  c.ss = ss;
+  c.rs = rs;
+  c.col_min = jb.col_min;
+  c.col_max = jb.col_max;
+  c.row_min = jb.row_min;
+  c.row_max = jb.row_max;
+  c.ref_mv_row = jb.ref_mv_row;
+  c.ref_mv_col = jb.ref_mv_col;
+  c.full_ref_row = rawpel(jb.ref_mv_row);
+  c.full_ref_col = rawpel(jb.ref_mv_col);
+  c.cost_type = cost.mv_cost_type;
+  c.sad_lambda = sad_lambda(cost.mv_cost_type);
+  c.sse_lambda = sse_lambda(cost.mv_cost_type);
+  c.sad_per_bit = cost.sad_per_bit;
+  c.error_per_bit = cost.error_per_bit;
+  const bool ent = cost.mv_cost_type == 0;
+  c.mvjcost = ent ? cost.mvjcost : kZeroRate;
+  c.mvcost0 = ent ? cost.mvcost[0] : kZeroRate;
+  c.mvcost1 = ent ? cost.mvcost[1] : kZeroRate;
+  c.tiles = tiles.data;
+  c.fh = tiles.field_rows;
+  c.fsz = (int)tiles.field_bytes;
+  c.oy = (int)(jb.ref_off / rs);
+  c.ox = (int)(jb.ref_off - (int64_t)c.oy * rs);
+  LjSrc s;
+  load_row<4>(c.src + (int64_t)(2 * l) * ss, s.sk);
+  load_row<4>(c.src + (int64_t)l * ss, s.fr[0]);
+  load_row<4>(c.src + (int64_t)(l + 8) * ss, s.fr[1]);
+  const bool want_cl = cost_lists != nullptr;
+  int cl[5] = {INT_MAX, INT_MAX, INT_MAX, INT_MAX, INT_MAX};
+  int steps = 0, searches = 0, sme = 0;
+  int br = jb.start_row, bc = jb.start_col;
+  bool full = true;
+  if (skip) {
+    lj_pass<true>(c, s, l, true, step_param, want_cl, res, steps, searches, br, bc, sme, cl);
+    // quality check of the row-skipping search (mcomp.c:1840-1867): sad and
+    // sad_skip at the result, rows l and l + 8 of lane l (same parity as l)
+    uint32_t all = 0;
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      uint32_t t[4];
+      load_row<4>(c.ref + (int64_t)(br + l + 8 * k) * rs + bc, t);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) all = sad4(s.fr[k][i], t[i], all);
+    }
+    const int sad = (int)group_sum8(all);
+    const int ssad = (int)(2 * group_sum8((l & 1) ? 0u : all));
+    full = sad > 16 && abs(ssad - sad) * 10 >= max(sad, 1) * 9;
+    if (full) {
+      br = jb.start_row;
+      bc = jb.start_col;
+    }
+  }
+  if (__builtin_amdgcn_ballot_w64(full) != 0)
+    lj_pass<false>(c, s, l, full, step_param, want_cl, res, steps, searches, br, bc, sme, cl);
+  if (!mine_job) return;
+  if (l == 0) {
+    LavishDiamondResult r;
+    r.best_row = (int16_t)br;
+    r.best_col = (int16_t)bc;
+    r.bestsme = sme;
+    r.steps = steps;
+    r.searches = searches;
+    out[j] = r;
+  }
+  if (want_cl && l < 5) {
+    const int v = l == 0 ? cl[0] : l == 1 ? cl[1] : l == 2 ? cl[2] : l == 3 ? cl[3] : cl[4];
+    cost_lists[5 * (int64_t)j + l] = v;
+  }
+}
+
+static bool lj_enabled() {  // LAVISH_DIAMOND_LJ=0: the one-job-per-wave kernel (A/B)
+  static const bool on = [] {
+    const char* e = getenv("LAVISH_DIAMOND_LJ");
+    return e == nullptr || atoi(e) != 0;
+  }();
+  return on;
+}
+
 template <int W, int H, bool TL>
 void launch_tl(const uint8_t* src, int ss, const uint8_t* ref, int rs, const LavishRefTiles& t,
                const LavishDiamondJob* jobs, int njobs, int step_param,
                const LavishMvCostParams& cost, int skip, int method, LavishDiamondResult* out,
                int32_t* cost_lists, hipStream_t s) {
-  int nwg = (njobs + 3) / 4;
+  int nwg = (njobs + kDkWaves - 1) / kDkWaves;
   nwg = (nwg + 7) & ~7;
   if (method == kDiamond)
-    hipLaunchKernelGGL((diamond_kernel<W, H, false, TL>), dim3(nwg), dim3(256), 0, s, src, ss,
+    hipLaunchKernelGGL((diamond_kernel<W, H, false, TL>), dim3(nwg), dim3(64 * kDkWaves), 0, s, src, ss,
                        ref, rs, t, (const Job*)jobs, njobs, step_param, cost, skip, method, out,
                        cost_lists);
   else
-    hipLaunchKernelGGL((diamond_kernel<W, H, true, TL>), dim3(nwg), dim3(256), 0, s, src, ss,
+    hipLaunchKernelGGL((diamond_kernel<W, H, true, TL>), dim3(nwg), dim3(64 * kDkWaves), 0, s, src, ss,
                        ref, rs, t, (const Job*)jobs, njobs, step_param, cost, skip, method, out,
                        cost_lists);
 }
@@ -880,6 +1192,15 @@ void launch(const uint8_t* src, int ss, const uint8_t* ref, int rs, const Lavish
             int32_t* cost_lists, hipStream_t s) {
   if constexpr (W <= 16) {
     if (t != nullptr) {
+      if constexpr (W == 16 && H == 16) {
+        if (method == kDiamond && lj_enabled()) {  // eight jobs per wave
+          const int waves = (njobs + kLjJobs - 1) / kLjJobs;
+          const int nwg = (((waves + 3) / 4) + 7) & ~7;
+          hipLaunchKernelGGL(diamond_lj_kernel, dim3(nwg), dim3(256), 0, s, src, ss, ref, rs, *t,
+                             (const Job*)jobs, njobs, step_param, cost, skip, out, cost_lists);
+          return;
+        }
+      }
       launch_tl<W, H, true>(src, ss, ref, rs, *t, jobs, njobs, step_param, cost, skip, method,
                             out, cost_lists, s);
       return;

@@ -188,19 +188,31 @@ __device__ __forceinline__ void txq_types(const TxqArgs& a,
   }
 }
 
+// LDS of one workgroup of size W x H: t1 (column results, padded rows), t2
+// (coefficients, 16-byte aligned), the three inverse scans
+template <int W, int H>
+struct TxqLds {
+  using T = Tile<W, H>;
+  static constexpr int kT2Off = (4 * T::T1 * 4 + 15) & ~15;          // bytes
+  static constexpr int kIscOff = kT2Off + 4 * T::T2 * 4;
+  static constexpr int kBytes = kIscOff + 3 * T::N * 2;
+};
+
 // One 256-thread workgroup = 4 independent wave tiles (no workgroup
 // barriers after the shared iscan load).  Grid: (tile quad, type group); the
 // type groups of one tile quad get workgroup ids congruent mod 8, i.e. the
-// same XCD, so repeated residual reads hit that XCD's L2.
+// same XCD, so repeated residual reads hit that XCD's L2.  `id` is the
+// workgroup's index within this size's grid (a multiple of 8 from the
+// launch's start, so id & 7 is still the XCD).
 template <int W, int H>
-__global__ __launch_bounds__(256, 2) void txq_plane_kernel(TxqArgs a) {
+__device__ __forceinline__ void txq_plane_body(const TxqArgs& a, int id, char* lds) {
   using T = Tile<W, H>;
+  using LL = TxqLds<W, H>;
   constexpr int H_ = H;
-  __shared__ int32_t t1s[4 * T::T1];
-  __shared__ __attribute__((aligned(16))) int32_t t2s[4 * T::T2];
-  __shared__ int16_t isc[3 * T::N];  // inverse scans: default, mcol, mrow
+  int32_t* t1s = reinterpret_cast<int32_t*>(lds);
+  int32_t* t2s = reinterpret_cast<int32_t*>(lds + LL::kT2Off);
+  int16_t* isc = reinterpret_cast<int16_t*>(lds + LL::kIscOff);  // default, mcol, mrow
 
-  const int id = blockIdx.x;
   const int inner = id & 7, rest = id >> 3;
   const int tg = rest % a.tgroups, quad = (rest / a.tgroups) * 8 + inner;
   const int ntiles = (a.nblocks + T::P - 1) / T::P;
@@ -272,6 +284,101 @@ __global__ __launch_bounds__(256, 2) void txq_plane_kernel(TxqArgs a) {
 #undef LAVISH_TXQ_RUN
 }
 
+template <int W, int H>
+__global__ __launch_bounds__(256, 2) void txq_plane_kernel(TxqArgs a) {
+  __shared__ __attribute__((aligned(16))) char lds[TxqLds<W, H>::kBytes];
+  txq_plane_body<W, H>(a, blockIdx.x, lds);
+}
+
+// ---------------------------------------------------------------------------
+// One launch for many TX sizes (lavish_txq_frame): the sizes' grids back to
+// back in one grid, heaviest first; workgroup g runs size k with
+// wg0[k] <= g < wg0[k + 1].  No cross-stream fork / join and no per-kernel
+// tail between sizes.  Class 0: the sizes up to 16 points (<= 115 VGPRs,
+// <= 37 KB LDS: 4 waves / SIMD); class 1: the 32-point sizes.
+// The per-size arguments are separate kernel parameters at a fixed slot per
+// size (txq_slot): one aggregate parameter holding all of them is copied to
+// scratch memory once any field is indexed dynamically (measured: 10x
+// slower); a TxqArgs parameter of its own is read in place, as in
+// txq_plane_kernel.
+constexpr int kMultiMax = 9;
+struct TxqDispatch {
+  int code[kMultiMax];       // dispatch entry k: tx_size
+  int wg0[kMultiMax + 1];    // dispatch entry k: first workgroup (multiples of 8)
+  int n;
+};
+struct TxqMulti {
+  TxqArgs a[kMultiMax];      // by slot (txq_slot(tx_size))
+  TxqDispatch d;
+};
+__host__ __device__ constexpr int txq_slot(int s) {
+  return s == 0 ? 0 : s == 1 ? 1 : s == 2 ? 2 : s == 5 ? 3 : s == 6 ? 4 : s == 7 ? 5
+       : s == 8 ? 6 : s == 13 ? 7 : s == 14 ? 8
+       : s == 3 ? 0 : s == 9 ? 1 : s == 10 ? 2 : s == 15 ? 3 : s == 16 ? 4 : -1;
+}
+static_assert(sizeof(TxqMulti) <= 4096, "kernel argument size");
+
+constexpr int lds_bytes(int s) {
+  return s == 0 ? TxqLds<4, 4>::kBytes : s == 1 ? TxqLds<8, 8>::kBytes
+       : s == 2 ? TxqLds<16, 16>::kBytes : s == 3 ? TxqLds<32, 32>::kBytes
+       : s == 5 ? TxqLds<4, 8>::kBytes : s == 6 ? TxqLds<8, 4>::kBytes
+       : s == 7 ? TxqLds<8, 16>::kBytes : s == 8 ? TxqLds<16, 8>::kBytes
+       : s == 9 ? TxqLds<16, 32>::kBytes : s == 10 ? TxqLds<32, 16>::kBytes
+       : s == 13 ? TxqLds<4, 16>::kBytes : s == 14 ? TxqLds<16, 4>::kBytes
+       : s == 15 ? TxqLds<8, 32>::kBytes : s == 16 ? TxqLds<32, 8>::kBytes : 0;
+}
+__host__ __device__ constexpr bool txq_class(int s) {  // 1: a 32-point size
+  return s == 3 || s == 9 || s == 10 || s == 15 || s == 16;
+}
+constexpr int class_lds(int cls) {
+  int m = 16;
+  for (int s = 0; s < 17; ++s)
+    if ((s < 4 || s > 4) && s != 11 && s != 12 && lds_bytes(s) > 0 && (txq_class(s) ? 1 : 0) == cls)
+      m = lds_bytes(s) > m ? lds_bytes(s) : m;
+  return m;
+}
+
+template <int CLS>
+__global__ __launch_bounds__(256, 2) void txq_multi_kernel(TxqDispatch d, TxqArgs a0, TxqArgs a1,
+                                                           TxqArgs a2, TxqArgs a3, TxqArgs a4,
+                                                           TxqArgs a5, TxqArgs a6, TxqArgs a7,
+                                                           TxqArgs a8) {
+  __shared__ __attribute__((aligned(16))) char lds[class_lds(CLS)];
+  const int g = blockIdx.x;
+  int code = d.code[0], id = g;
+#pragma unroll
+  for (int k = 1; k < kMultiMax; ++k) {  // constant indices only
+    if (k < d.n && g >= d.wg0[k]) {
+      code = d.code[k];
+      id = g - d.wg0[k];
+    }
+  }
+  if constexpr (CLS == 0) {
+    switch (code) {
+      case 0: txq_plane_body<4, 4>(a0, id, lds); break;
+      case 1: txq_plane_body<8, 8>(a1, id, lds); break;
+      case 2: txq_plane_body<16, 16>(a2, id, lds); break;
+      case 5: txq_plane_body<4, 8>(a3, id, lds); break;
+      case 6: txq_plane_body<8, 4>(a4, id, lds); break;
+      case 7: txq_plane_body<8, 16>(a5, id, lds); break;
+      case 8: txq_plane_body<16, 8>(a6, id, lds); break;
+      case 13: txq_plane_body<4, 16>(a7, id, lds); break;
+      case 14: txq_plane_body<16, 4>(a8, id, lds); break;
+      default: break;
+    }
+  } else {
+    switch (code) {
+      case 3: txq_plane_body<32, 32>(a0, id, lds); break;
+      case 9: txq_plane_body<16, 32>(a1, id, lds); break;
+      case 10: txq_plane_body<32, 16>(a2, id, lds); break;
+      case 15: txq_plane_body<8, 32>(a3, id, lds); break;
+      case 16: txq_plane_body<32, 8>(a4, id, lds); break;
+      default: break;
+    }
+  }
+
+}
+
 // generic quantizer: one workgroup per block, any scan order.
 template <int LS>
 __global__ __launch_bounds__(256) void quant_kernel(const int32_t* coeff, int n,
@@ -333,15 +440,42 @@ static void build_chunks(TxqArgs& a, int nbg) {
   a.tgroups = cnt;
 }
 
+// the grid of one size (0: nothing to do); fills the type chunks of `a`
 template <int W, int H>
-static void launch_plane(TxqArgs a, hipStream_t s) {
+static int plan_plane(TxqArgs& a) {
   constexpr int P = Tile<W, H>::P * 4;  // blocks per workgroup (4 wave tiles)
   const int nbg = (a.nblocks + P - 1) / P;
-  if (nbg == 0) return;
+  if (nbg == 0) return 0;
   build_chunks(a, nbg);
-  const int grid = ((nbg + 7) / 8) * 8 * a.tgroups;
+  return ((nbg + 7) / 8) * 8 * a.tgroups;
+}
+
+template <int W, int H>
+static void launch_plane(TxqArgs a, hipStream_t s) {
+  const int grid = plan_plane<W, H>(a);
+  if (grid == 0) return;
   hipLaunchKernelGGL((txq_plane_kernel<W, H>), dim3(grid), dim3(256), 0, s, a);
   LAVISH_CHECK(hipGetLastError());
+}
+
+static int plan_size(int tx_size, TxqArgs& a) {
+  switch (tx_size) {
+    case 0: return plan_plane<4, 4>(a);
+    case 1: return plan_plane<8, 8>(a);
+    case 2: return plan_plane<16, 16>(a);
+    case 3: return plan_plane<32, 32>(a);
+    case 5: return plan_plane<4, 8>(a);
+    case 6: return plan_plane<8, 4>(a);
+    case 7: return plan_plane<8, 16>(a);
+    case 8: return plan_plane<16, 8>(a);
+    case 9: return plan_plane<16, 32>(a);
+    case 10: return plan_plane<32, 16>(a);
+    case 13: return plan_plane<4, 16>(a);
+    case 14: return plan_plane<16, 4>(a);
+    case 15: return plan_plane<8, 32>(a);
+    case 16: return plan_plane<32, 8>(a);
+    default: return -1;
+  }
 }
 
 static QP to_qp(const LavishQuantParams* p) {
@@ -358,6 +492,10 @@ static QP to_qp(const LavishQuantParams* p) {
   return q;
 }
 
+int txq_args(const int16_t* residual, int stride, int width, int height, int tx_size,
+             uint32_t type_mask, int bd, int quant_kind, const LavishQuantParams* qp,
+             int32_t* qcoeff, int32_t* dqcoeff, uint16_t* eob, int32_t* coeff, TxqArgs& a);
+
 int txq_plane(const int16_t* residual, int stride, int width, int height, int tx_size,
               uint32_t type_mask, int bd, int quant_kind, const LavishQuantParams* qp,
               int32_t* qcoeff, int32_t* dqcoeff, uint16_t* eob, int32_t* coeff,
@@ -371,6 +509,35 @@ int txq_plane(const int16_t* residual, int stride, int width, int height, int tx
     return txq_plane_64(residual, stride, width, height, tx_size, type_mask, bd, quant_kind, qp,
                         qcoeff, dqcoeff, eob, coeff, s);
   TxqArgs a{};
+  const int rc = txq_args(residual, stride, width, height, tx_size, type_mask, bd, quant_kind,
+                          qp, qcoeff, dqcoeff, eob, coeff, a);
+  if (rc) return rc;
+  switch (tx_size) {
+    case 0: launch_plane<4, 4>(a, s); break;
+    case 1: launch_plane<8, 8>(a, s); break;
+    case 2: launch_plane<16, 16>(a, s); break;
+    case 3: launch_plane<32, 32>(a, s); break;
+    case 5: launch_plane<4, 8>(a, s); break;
+    case 6: launch_plane<8, 4>(a, s); break;
+    case 7: launch_plane<8, 16>(a, s); break;
+    case 8: launch_plane<16, 8>(a, s); break;
+    case 9: launch_plane<16, 32>(a, s); break;
+    case 10: launch_plane<32, 16>(a, s); break;
+    case 13: launch_plane<4, 16>(a, s); break;
+    case 14: launch_plane<16, 4>(a, s); break;
+    case 15: launch_plane<8, 32>(a, s); break;
+    case 16: launch_plane<32, 8>(a, s); break;
+    default: return -2;
+  }
+  return 0;
+}
+
+// TxqArgs of one (size <= 32 points, plane) job; 0 or the API's error code
+int txq_args(const int16_t* residual, int stride, int width, int height, int tx_size,
+             uint32_t type_mask, int bd, int quant_kind, const LavishQuantParams* qp,
+             int32_t* qcoeff, int32_t* dqcoeff, uint16_t* eob, int32_t* coeff, TxqArgs& a) {
+  const int W = tx_w(tx_size), H = tx_h(tx_size);
+  a = TxqArgs{};
   a.res = residual;
   a.stride = stride;
   a.bw = width / W;
@@ -389,23 +556,6 @@ int txq_plane(const int16_t* residual, int stride, int width, int height, int tx
   a.dqcoeff = dqcoeff;
   a.eob = eob;
   a.coeff = coeff;
-  switch (tx_size) {
-    case 0: launch_plane<4, 4>(a, s); break;
-    case 1: launch_plane<8, 8>(a, s); break;
-    case 2: launch_plane<16, 16>(a, s); break;
-    case 3: launch_plane<32, 32>(a, s); break;
-    case 5: launch_plane<4, 8>(a, s); break;
-    case 6: launch_plane<8, 4>(a, s); break;
-    case 7: launch_plane<8, 16>(a, s); break;
-    case 8: launch_plane<16, 8>(a, s); break;
-    case 9: launch_plane<16, 32>(a, s); break;
-    case 10: launch_plane<32, 16>(a, s); break;
-    case 13: launch_plane<4, 16>(a, s); break;
-    case 14: launch_plane<16, 4>(a, s); break;
-    case 15: launch_plane<8, 32>(a, s); break;
-    case 16: launch_plane<32, 8>(a, s); break;
-    default: return -2;
-  }
   return 0;
 }
 
@@ -504,14 +654,57 @@ int txq_frame(const int16_t* residual, int stride, int width, int height, uint32
       order[j - 1] = t;
     }
   int rc = 0;
-  hipStream_t* fs = fan_out(caller);
-  for (int i = 0; i < n && rc == 0; ++i) {
-    const int s = order[i];
-    rc = txq_plane(residual, stride, width, height, s, type_masks[s], bd, quant_kind, qp,
-                   qcoeff[s], dqcoeff[s], eob[s], nullptr, fs[i % kFrameStreams]);
+  static const int mode = [] {
+    const char* e = getenv("LAVISH_TXQ_FRAME_MODE");  // A/B experiments only
+    return e ? atoi(e) : 1;
+  }();
+  if (mode == 0) {  // per-size kernels over the caller + 2 internal streams
+    hipStream_t* fs = fan_out(caller);
+    for (int i = 0; i < n && rc == 0; ++i) {
+      const int s = order[i];
+      rc = txq_plane(residual, stride, width, height, s, type_masks[s], bd, quant_kind, qp,
+                     qcoeff[s], dqcoeff[s], eob[s], nullptr, fs[i % kFrameStreams]);
+    }
+    fan_in(caller);
+    return rc;
   }
-  fan_in(caller);
-  return rc;
+  // one launch per class, on the caller's stream: the 32-point class (few,
+  // register-heavy workgroups) first, then the <= 16-point class
+  for (int cls = 1; cls >= 0; --cls) {
+    TxqMulti m{};
+    int g = 0;
+    for (int i = 0; i < n; ++i) {
+      const int s = order[i];
+      if ((txq_class(s) ? 1 : 0) != cls) continue;
+      if (tx_w(s) > 32 || tx_h(s) > 32) {  // 64-point sizes: their own path
+        rc = txq_plane(residual, stride, width, height, s, type_masks[s], bd, quant_kind, qp,
+                       qcoeff[s], dqcoeff[s], eob[s], nullptr, caller);
+        if (rc) return rc;
+        continue;
+      }
+      if (m.d.n == kMultiMax) return -2;
+      TxqArgs& a = m.a[txq_slot(s)];
+      rc = txq_args(residual, stride, width, height, s, type_masks[s], bd, quant_kind, qp,
+                    qcoeff[s], dqcoeff[s], eob[s], nullptr, a);
+      if (rc) return rc;
+      const int grid = plan_size(s, a);
+      if (grid <= 0) continue;
+      m.d.code[m.d.n] = s;
+      m.d.wg0[m.d.n] = g;
+      g += grid;
+      ++m.d.n;
+    }
+    if (m.d.n == 0) continue;
+    m.d.wg0[m.d.n] = g;
+    if (cls == 0)
+      hipLaunchKernelGGL(txq_multi_kernel<0>, dim3(g), dim3(256), 0, caller, m.d, m.a[0], m.a[1],
+                         m.a[2], m.a[3], m.a[4], m.a[5], m.a[6], m.a[7], m.a[8]);
+    else
+      hipLaunchKernelGGL(txq_multi_kernel<1>, dim3(g), dim3(256), 0, caller, m.d, m.a[0], m.a[1],
+                         m.a[2], m.a[3], m.a[4], m.a[5], m.a[6], m.a[7], m.a[8]);
+    LAVISH_CHECK(hipGetLastError());
+  }
+  return 0;
 }
 
 }  // namespace lavish

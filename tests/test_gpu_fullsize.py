@@ -1,6 +1,10 @@
 """GPU parity at the BASELINE.json configurations' full sizes (SURVEY.md
 8(d)), every job / block / superblock against the oracle:
 
+* C2: lavish_txq_frame -- the call bench.py times -- on the bench's 1920x1080
+  residual: every block of all 14 TX sizes <= 32x32 x every valid TX type,
+  qcoeff / dqcoeff / eob bit-exact;
+
 * C3: DIAMOND full-pel search of every 16x16 block of a 1920x1080 frame
   against 7 references (56 280 jobs) with the 1080p speed features bench.py
   times (downsampled SAD, entropy mv cost, cost lists) and the sub-pel
@@ -38,6 +42,30 @@ def _bench():
     b = importlib.util.module_from_spec(spec)
     spec.loader.exec_module(b)
     return b
+
+
+def test_c2_txq_frame_1080p_all_blocks(L):
+    """The bench's C2 leg exactly as timed (lavish_txq_frame, one launch per
+    size class) against the oracle's txq_plane of every size."""
+    import torch
+    import lavish_dsp.synth as synth
+    res = synth.residual_plane(1920, 1080, 8, seed=1234)
+    dres = torch.from_numpy(res).cuda()
+    sizes = [s for s in range(19) if L.TX_W[s] <= 32 and L.TX_H[s] <= 32]
+    qp = L.build_quant_params(8, 128, L.QUANT_FP)
+    frame = L.FrameOutputs(dres, sizes)
+    outs = L.txq_frame(dres, frame, qp)
+    torch.cuda.synchronize()
+    oq = O.build_quant(8, 128)
+    for s in sizes:
+        qc, dq, eob = O.txq_plane(res, s, L.valid_type_mask(s), oq, threads=THREADS)
+        np.testing.assert_array_equal(outs[s]["qcoeff"].cpu().numpy(), qc.transpose(1, 0, 2),
+                                      err_msg="size %d qcoeff" % s)
+        np.testing.assert_array_equal(outs[s]["dqcoeff"].cpu().numpy(), dq.transpose(1, 0, 2),
+                                      err_msg="size %d dqcoeff" % s)
+        np.testing.assert_array_equal(outs[s]["eob"].cpu().numpy().view(np.uint16), eob.T,
+                                      err_msg="size %d eob" % s)
+        del qc, dq, eob
 
 
 def test_c3_1080p_7refs_all_jobs(L):
