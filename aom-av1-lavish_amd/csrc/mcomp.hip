@@ -226,15 +226,17 @@ __device__ __forceinline__ void var_acc(uint32_t a, uint32_t b, int& sum, uint32
 }
 
 template <int W, int H>
-__device__ __forceinline__ int var_finish(const Ctx& c, int sum, uint32_t sse, int row, int col) {
+__device__ __forceinline__ int var_finish(const Ctx& c, int sum, uint32_t sse, int row, int col,
+                                          uint32_t* vout = nullptr) {
   const uint32_t ts = groups_sum(group_sum8((uint32_t)sum)), tq = groups_sum(group_sum8(sse));
   const uint32_t var = tq - (uint32_t)(((int64_t)(int)ts * (int)ts) / (W * H));
+  if (vout) *vout = var;
   return (int)var + mv_cost(c, row, col);
 }
 
 // the whole wave walks the W*H pixels one word per lane, from global memory
 template <int W, int H>
-__device__ int var_cost(const Ctx& c, int lane, int row, int col) {
+__device__ int var_cost(const Ctx& c, int lane, int row, int col, uint32_t* vout = nullptr) {
   constexpr int DW = W / 4;
   int sum = 0;
   uint32_t sse = 0;
@@ -246,7 +248,7 @@ __device__ int var_cost(const Ctx& c, int lane, int row, int col) {
     load_row<1>(rb + (int64_t)y * c.rs + 4 * x, b);
     var_acc(a[0], b[0], sum, sse);
   }
-  return var_finish<W, H>(c, sum, sse, row, col);
+  return var_finish<W, H>(c, sum, sse, row, col, vout);
 }
 
 // sdf and sdsf (aom_sad / aom_sad_skip) at a full-pel mv in one pass: the
@@ -489,7 +491,8 @@ struct Search {
 
   // var cost at (row, col): from the window when the last search filled one
   // (its result lies within 15 pixels of the fill centre)
-  __device__ __forceinline__ int var_cost_at(const Ctx& c, int lane, int row, int col) const {
+  __device__ __forceinline__ int var_cost_at(const Ctx& c, int lane, int row, int col,
+                                             uint32_t* vout = nullptr) const {
     if constexpr (kVarWin) {
       if (inwin) {
         int sum = 0;
@@ -505,10 +508,10 @@ struct Search {
             var_acc(sv[v], *(const __attribute__((address_space(3))) u32u*)p, sum, sse);
           }
         }
-        return var_finish<W, H>(c, sum, sse, row, col);
+        return var_finish<W, H>(c, sum, sse, row, col, vout);
       }
     }
-    return var_cost<W, H>(c, lane, row, col);
+    return var_cost<W, H>(c, lane, row, col, vout);
   }
 
   // diamond_search_sad (no second_pred): returns bestsad
@@ -674,12 +677,23 @@ __device__ __forceinline__ void bigdia_site(int s, int i, int& dr, int& dc) {
 // Lane group g evaluates candidate g; the keyed minimum is the reference's
 // sequential update order (update_mvs_and_sad, mcomp.c:858-877), whose raw
 // SAD is kept as raw_bestsad.
-template <int W, int H, bool SKIP, bool TL>
+// WINP (a wave-serial caller, the TPL wavefront): the search first copies the
+// (H + 30) x (W + 30) reference window around its clamped start into LDS
+// (win: Win<W, H>::SIZE dwords, then 4 + 2 x 31 ints of mv-cost rates: the
+// joint costs and the mvcost rows / columns of the window's 31 full-pel
+// rows / columns), and every round whose candidates all lie inside it reads
+// SADs and mv costs from LDS: one memory latency per search instead of one
+// per round.  Rounds that reach outside read global memory as before.  vout:
+// the plain variance at the result (the sub-pel step's FULL_PEL error).
+template <int W, int H, bool SKIP, bool TL, bool WINP = false>
 __device__ int pattern(const Ctx& c, int lane, int srow, int scol, int search_step, bool do_init,
                        bool want_cl, int (&cl)[5], int& brow, int& bcol, int& steps,
-                       int& nsad) {
+                       int& nsad, lds_u32 win = nullptr, uint32_t* vout = nullptr) {
+  static_assert(!WINP || (Win<W, H>::kOn && !TL), "window: w, h <= 32, linear layout");
+  using WN = Win<W, H>;
+  constexpr int NR = 2 * WN::R + 1;  // full-pel rows / columns a window spans
   Search<W, H, SKIP, false, TL> S;
-  S.load_src(c, lane);
+  S.load_src(c, lane, WINP ? win : nullptr);
   const int g = lane >> 3;
   search_step = min(search_step, kMaxSteps - 1);
   int best_init_s = kMaxSteps - 1 - search_step;  // search_steps[] = {10, 9, ..., 0}
@@ -687,8 +701,40 @@ __device__ int pattern(const Ctx& c, int lane, int srow, int scol, int search_st
   int bc = min(max(scol, c.col_min), c.col_max);
   if (want_cl) cl[0] = cl[1] = cl[2] = cl[3] = cl[4] = INT_MAX;
   bool has_sad = false;
-  uint32_t raw = rdlane(S.group_sad(c, br, bc), 0);
-  uint32_t best = raw + mvsad_cost(c, br, bc);
+  typedef __attribute__((address_space(3))) int32_t* lds_i32;
+  lds_i32 rates = nullptr;
+  if constexpr (WINP) {
+    rates = (lds_i32)(win + WN::SIZE);
+    const bool ent = c.cost_type == 0;
+    typedef const __attribute__((address_space(1))) int32_t* gi32;
+    const int wr0 = br - WN::R, wc0 = bc - WN::R;
+    // |row - full_ref| <= 1023 + 15 inside the window: inside the tables
+    if (lane < 4) rates[lane] = ent ? ((gi32)c.mvjcost)[lane] : 0;
+    if (lane < NR) {
+      rates[4 + lane] = ent ? ((gi32)c.mvcost0)[(wr0 + lane - c.full_ref_row) * 8] : 0;
+      rates[4 + NR + lane] = ent ? ((gi32)c.mvcost1)[(wc0 + lane - c.full_ref_col) * 8] : 0;
+    }
+    S.fill(c, lane, br, bc);  // (its wave_sync covers the rate stores)
+  }
+  // every candidate within d pixels of (r0, c0) inside the window
+  auto in_win = [&](int r0, int c0, int d) {
+    return WINP && r0 - d >= S.wr0 && r0 + d <= S.wr0 + 2 * WN::R && c0 - d >= S.wc0 &&
+           c0 + d <= S.wc0 + 2 * WN::R;
+  };
+  auto rate_win = [&](int r, int cc) {
+    const int dr = (r - c.full_ref_row) * 8, dc = (cc - c.full_ref_col) * 8;
+    const int joint = c.cost_type == 0 ? ((dc != 0) | ((dr != 0) << 1)) : 0;
+    const int ir = min(max(r - S.wr0, 0), NR - 1), ic = min(max(cc - S.wc0, 0), NR - 1);
+    return MvRate{rates[joint], rates[4 + ir], rates[4 + NR + ic]};
+  };
+  uint32_t raw, best;
+  if (in_win(br, bc, 0)) {
+    raw = rdlane(S.group_sad_win(c, br, bc, true), 0);
+    best = raw + mvsad_finish(c, rate_win(br, bc), br, bc);
+  } else {
+    raw = rdlane(S.group_sad(c, br, bc), 0);
+    best = raw + mvsad_cost(c, br, bc);
+  }
   ++nsad;
   // one round: candidate idx (groups g < cnt) of scale s around (br, bc);
   // returns the winning group or -1.  clmode 1: raw SADs of the valid
@@ -701,8 +747,15 @@ __device__ int pattern(const Ctx& c, int lane, int srow, int scol, int search_st
     // (check_bounds only skips this test when it holds)
     const bool valid =
         g < cnt && cc >= c.col_min && cc <= c.col_max && r >= c.row_min && r <= c.row_max;
-    const MvRate mr = mvsad_rate(c, r, cc);  // in flight with the SAD's loads
-    const uint32_t mine = S.group_sad(c, r, cc, valid, br, bc);
+    MvRate mr;
+    uint32_t mine;
+    if (in_win(br, bc, 1 << s)) {  // scale s moves at most 2^s (4 points of 1 at s = 0)
+      mr = rate_win(r, cc);
+      mine = S.group_sad_win(c, r, cc, valid);
+    } else {
+      mr = mvsad_rate(c, r, cc);  // in flight with the SAD's loads
+      mine = S.group_sad(c, r, cc, valid, br, bc);
+    }
     const uint32_t key =
         (((mine + mvsad_finish(c, mr, r, cc)) << 3) | (uint32_t)g) | (valid ? 0u : ~0u);
     uint32_t kmin = groups_min(key);
@@ -793,7 +846,11 @@ __device__ int pattern(const Ctx& c, int lane, int srow, int scol, int search_st
     if (!has_sad) nsad += 1 + (cl[1] != INT_MAX) + (cl[2] != INT_MAX) + (cl[3] != INT_MAX) +
                           (cl[4] != INT_MAX);
   }
-  return var_cost<W, H>(c, lane, br, bc);  // get_mvpred_var_cost
+  if constexpr (WINP) {
+    S.inwin = in_win(br, bc, 0);
+    return S.var_cost_at(c, lane, br, bc, vout);  // get_mvpred_var_cost
+  }
+  return var_cost<W, H>(c, lane, br, bc, vout);  // get_mvpred_var_cost
 }
 
 // waves (jobs) per workgroup of the search kernels
@@ -805,27 +862,9 @@ constexpr int kDkWaves = LAVISH_DK_WAVES;
 // search_method values of SEARCH_METHODS (av1/encoder/mcomp_structs.h:56-86)
 enum { kDiamond = 0, kBigdia = 5, kFastDiamond = 8, kFastBigdia = 9, kVfastDiamond = 10 };
 
-// PAT: the BIGDIA-site pattern searches (method 5 / 8 / 9 / 10), else DIAMOND
-template <int W, int H, bool PAT, bool TL>
-__global__ __launch_bounds__(64 * kDkWaves, (W <= 16 && H <= 16) ? 8 : 7) void diamond_kernel(const uint8_t* __restrict__ src, int ss,
-                                                      const uint8_t* __restrict__ ref, int rs,
-                                                      LavishRefTiles tiles,
-                                                      const Job* __restrict__ jobs, int njobs,
-                                                      int step_param, LavishMvCostParams cost,
-                                                      int skip, int method,
-                                                      LavishDiamondResult* __restrict__ out,
-                                                      int32_t* __restrict__ cost_lists) {
-  // XCD-aware: consecutive job quads (neighbouring blocks) share an XCD's L2
-  const int nwg = gridDim.x;  // multiple of 8
-  const int wg = (blockIdx.x & 7) * (nwg >> 3) + (blockIdx.x >> 3);
-  const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int j = wg * kDkWaves + wave;
-  if (j >= njobs) return;
-  constexpr int WS = PAT ? 1 : Win<W, H>::SIZE;  // the window serves DIAMOND only
-  __shared__ uint32_t win_s[kDkWaves * WS];
-  const lds_u32 win = (!PAT && Win<W, H>::kOn) ? (lds_u32)(win_s + wave * WS) : nullptr;
-  const Job jb = jobs[j];
+// search context of one job: its buffers, FullMvLimits, ref_mv and mv costs
+__device__ __forceinline__ Ctx job_ctx(const uint8_t* src, int ss, const uint8_t* ref, int rs,
+                                       const Job& jb, const LavishMvCostParams& cost) {
   Ctx c;
   c.src = src + jb.src_off;
   c.ref = ref + jb.ref_off;
@@ -848,31 +887,33 @@ __global__ __launch_bounds__(64 * kDkWaves, (W <= 16 && H <= 16) ? 8 : 7) void d
   c.mvjcost = ent ? cost.mvjcost : kZeroRate;
   c.mvcost0 = ent ? cost.mvcost[0] : kZeroRate;
   c.mvcost1 = ent ? cost.mvcost[1] : kZeroRate;
-  if constexpr (TL) {
-    c.tiles = tiles.data;
-    c.fh = tiles.field_rows;
-    c.fsz = (int)tiles.field_bytes;
-    // the job's block origin as (row, column) of the whole buffer (uniform)
-    const int oy = (int)(jb.ref_off / rs);
-    c.oy = __builtin_amdgcn_readfirstlane(oy);
-    c.ox = __builtin_amdgcn_readfirstlane((int)(jb.ref_off - (int64_t)oy * rs));
-  }
-  const bool want_cl = cost_lists != nullptr;
-  int cl[5] = {INT_MAX, INT_MAX, INT_MAX, INT_MAX, INT_MAX};
-  int br, bc, steps = 0, searches = 0, sme;
+  return c;
+}
+
+// av1_full_pixel_search (mcomp.c:1755-1873, no mesh) of one job by one wave:
+// DIAMOND (PAT false) or the BIGDIA-site pattern searches (method 5 / 8 /
+// 9 / 10), the downsampled-SAD quality check and its full-SAD redo.
+// searches: DIAMOND runs / the SAD blocks read by a pattern search.
+template <int W, int H, bool PAT, bool TL, bool WINP = false>
+__device__ __forceinline__ int job_search(const Ctx& c, int lane, int start_row, int start_col,
+                                          int step_param, int skip, int method, lds_u32 win,
+                                          bool want_cl, int (&cl)[5], int& br, int& bc,
+                                          int& steps, int& searches, uint32_t* vout = nullptr) {
+  int sme;
   auto search = [&](auto skip_tag) {
     constexpr bool SK = decltype(skip_tag)::value;
     if constexpr (!PAT) {
-      return full_pixel_diamond<W, H, SK, TL>(c, lane, jb.start_row, jb.start_col, step_param,
-                                              br, bc, steps, searches, win, want_cl, cl);
+      return full_pixel_diamond<W, H, SK, TL>(c, lane, start_row, start_col, step_param, br, bc,
+                                              steps, searches, win, want_cl, cl);
     } else {
-      // searches: the SAD blocks read (start, candidates, cost list) (do_init 1) / fast_dia / vfast_dia / fast_bigdia (mcomp.c:1266-1316)
+      // bigdia (do_init 1) / fast_dia / vfast_dia / fast_bigdia (mcomp.c:1266-1316)
       const int step = method == kBigdia        ? step_param
                        : method == kFastDiamond ? max(kMaxSteps - 2, step_param)
                        : method == kVfastDiamond ? max(kMaxSteps - 1, step_param)
                                                  : max(kMaxSteps - 3, step_param);
-      return pattern<W, H, SK, TL>(c, lane, jb.start_row, jb.start_col, step,
-                                   method == kBigdia, want_cl, cl, br, bc, steps, searches);
+      return pattern<W, H, SK, TL, WINP>(c, lane, start_row, start_col, step,
+                                         method == kBigdia, want_cl, cl, br, bc, steps, searches,
+                                         win, vout);
     }
   };
   // use_downsampled_sad applies to blocks at least 16 high (mcomp.c:132-133)
@@ -886,6 +927,45 @@ __global__ __launch_bounds__(64 * kDkWaves, (W <= 16 && H <= 16) ? 8 : 7) void d
   } else {
     sme = search(std::false_type{});
   }
+  return sme;
+}
+
+// PAT: the BIGDIA-site pattern searches (method 5 / 8 / 9 / 10), else DIAMOND
+template <int W, int H, bool PAT, bool TL>
+__global__ __launch_bounds__(64 * kDkWaves, (W <= 16 && H <= 16) ? 8 : 7) void diamond_kernel(const uint8_t* __restrict__ src, int ss,
+                                                      const uint8_t* __restrict__ ref, int rs,
+                                                      LavishRefTiles tiles,
+                                                      const Job* __restrict__ jobs, int njobs,
+                                                      int step_param, LavishMvCostParams cost,
+                                                      int skip, int method,
+                                                      LavishDiamondResult* __restrict__ out,
+                                                      int32_t* __restrict__ cost_lists) {
+  // XCD-aware: consecutive job quads (neighbouring blocks) share an XCD's L2
+  const int nwg = gridDim.x;  // multiple of 8
+  const int wg = (blockIdx.x & 7) * (nwg >> 3) + (blockIdx.x >> 3);
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int j = wg * kDkWaves + wave;
+  if (j >= njobs) return;
+  constexpr int WS = PAT ? 1 : Win<W, H>::SIZE;  // the window serves DIAMOND only
+  __shared__ uint32_t win_s[kDkWaves * WS];
+  const lds_u32 win = (!PAT && Win<W, H>::kOn) ? (lds_u32)(win_s + wave * WS) : nullptr;
+  const Job jb = jobs[j];
+  Ctx c = job_ctx(src, ss, ref, rs, jb, cost);
+  if constexpr (TL) {
+    c.tiles = tiles.data;
+    c.fh = tiles.field_rows;
+    c.fsz = (int)tiles.field_bytes;
+    // the job's block origin as (row, column) of the whole buffer (uniform)
+    const int oy = (int)(jb.ref_off / rs);
+    c.oy = __builtin_amdgcn_readfirstlane(oy);
+    c.ox = __builtin_amdgcn_readfirstlane((int)(jb.ref_off - (int64_t)oy * rs));
+  }
+  const bool want_cl = cost_lists != nullptr;
+  int cl[5] = {INT_MAX, INT_MAX, INT_MAX, INT_MAX, INT_MAX};
+  int br, bc, steps = 0, searches = 0;
+  const int sme = job_search<W, H, PAT, TL>(c, lane, jb.start_row, jb.start_col, step_param, skip,
+                                            method, win, want_cl, cl, br, bc, steps, searches);
   if (lane == 0) {
     LavishDiamondResult r;
     r.best_row = (int16_t)br;
@@ -898,6 +978,240 @@ __global__ __launch_bounds__(64 * kDkWaves, (W <= 16 && H <= 16) ? 8 : 7) void d
   if (want_cl && lane < 5) {
     const int v = lane == 0 ? cl[0] : lane == 1 ? cl[1] : lane == 2 ? cl[2] : lane == 3 ? cl[3] : cl[4];
     cost_lists[5 * (int64_t)j + lane] = v;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// TPL motion search with the reference's start-mv candidates (mode_estimation,
+// av1/encoder/tpl_model.c:640-743): for every (reference, block) in raster
+// order the centre mvs are the zero mv plus the above, left and above-right
+// blocks' finished tpl mvs of the same reference that are not is_alike_mv
+// (:319-333) to the ones already taken, the optional third-pass mv replacing
+// centre 0 (:687-703); with prune_starting_mv their full SADs at the clamped
+// full-pel centres rank them (qsort by compare_sad, :310-317, stable for
+// these <= 4 entries), the list is cut to 4 - prune_starting_mv and by the
+// SAD-gap rule (:720-727); motion_estimation (:249-303) runs per centre with
+// ref_mv = the centre (mv cost, av1_set_mv_search_range) and the smallest
+// sub-pel error wins (strict <).  With tpl_sf.subpel_force_stop FULL_PEL
+// (speed >= 5) the sub-pel step returns setup_center_error: the variance at
+// the full-pel best (MV_COST_NONE adds nothing) and the tpl mv is that best
+// x 8.
+//
+// The dependency on finished neighbours makes this a wavefront: one wave per
+// (reference, block row) walks its row left to right.  A block's tpl mv is
+// published by one device-scope atomic store into the mv array, which the
+// call first fills with INVALID_MV; a wave waits for the above-right block by
+// polling that slot (the mv itself is the ready flag: no separate progress
+// counter and no second round trip), keeps the above mv from the previous
+// step and the left mv in registers.  Rows are dealt out by an atomic ticket
+// in (row, reference) order, so a waiting wave's producer already runs (no
+// dependence on dispatch order); every wait is bounded, and a wave that gives
+// up counts the failure in sync[1] and stops waiting, so the grid always
+// drains.  Device-scope atomics bypass the per-XCD L2s, which are not
+// coherent with each other.  The FAST_BIGDIA-family searches run with the
+// LDS window of pattern() (one memory latency per search).
+struct TplMvArgs {
+  const uint8_t* src;
+  const uint8_t* ref;
+  int ss, rs;
+  const Job* jobs;  // [nrefs][rows * cols]: offsets and x->mv_limits
+  int cols, rows, nrefs;
+  int step_param, skip, method, prune, alike_thr;
+  LavishMvCostParams cost;
+  const int32_t* third;  // [nrefs][rows * cols] int_mv or null
+  int32_t* mvs;          // out: tpl mv (int_mv) per job; INVALID_MV until published
+  LavishDiamondResult* out;
+  int32_t* cost_lists;
+  int32_t* centers;      // out: the winning centre (int_mv) per job, or null
+  int32_t* sync;         // [0] ticket, [1] failed waits
+};
+
+constexpr int kTplMaxSpins = 1 << 22;  // ~0.3 s of s_sleep 2 per wait
+constexpr int32_t kInvalidMv = (int32_t)0x80008000;  // INVALID_MV (mv.h)
+
+__device__ __forceinline__ int mv_row(int32_t m) { return (int16_t)(m & 0xFFFF); }
+__device__ __forceinline__ int mv_col(int32_t m) { return (int16_t)((uint32_t)m >> 16); }
+__device__ __forceinline__ int32_t mv_pack(int row, int col) {
+  return (int32_t)(((uint32_t)(uint16_t)col << 16) | (uint16_t)row);
+}
+
+// a[i] of a 4-entry register array for a dynamic i (select chains, no
+// private-memory indexing)
+__device__ __forceinline__ int get4(const int (&v)[4], int i) {
+  return i == 0 ? v[0] : i == 1 ? v[1] : i == 2 ? v[2] : v[3];
+}
+__device__ __forceinline__ void set4(int (&v)[4], int i, int x) {
+#pragma unroll
+  for (int k = 0; k < 4; ++k) v[k] = i == k ? x : v[k];
+}
+
+template <bool PAT>
+__global__ __launch_bounds__(64) void tpl_mv_kernel(TplMvArgs a) {
+  constexpr int W = 16, H = 16;
+  using WN = Win<W, H>;
+  const int lane = threadIdx.x;
+  // reference window (+ the pattern searches' mv-cost rates)
+  __shared__ uint32_t win_s[WN::SIZE + (PAT ? 4 + 2 * (2 * WN::R + 1) : 0)];
+  const lds_u32 win = (lds_u32)win_s;
+  int t = 0;
+  if (lane == 0)
+    t = __hip_atomic_fetch_add(a.sync, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  t = __builtin_amdgcn_readfirstlane(t);
+  const int ref = t % a.nrefs, row = t / a.nrefs;
+  if (row >= a.rows) return;
+  const int64_t nb = (int64_t)a.rows * a.cols;
+  int32_t* const mvs = a.mvs + ref * nb;
+  bool waiting = true;
+  // poll a published mv of the row above (uniform)
+  auto await_mv = [&](int64_t k) -> int32_t {
+    int32_t m = __hip_atomic_load(mvs + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    int spins = 0;
+    while (m == kInvalidMv && waiting) {
+      __builtin_amdgcn_s_sleep(2);
+      m = __hip_atomic_load(mvs + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (++spins >= kTplMaxSpins) {
+        if (lane == 0)
+          __hip_atomic_fetch_add(a.sync + 1, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        waiting = false;
+      }
+    }
+    return __builtin_amdgcn_readfirstlane(m);
+  };
+  const bool want_cl = a.cost_lists != nullptr;
+  int32_t above = 0, left = 0;
+  for (int col = 0; col < a.cols; ++col) {
+    const int64_t bi = (int64_t)row * a.cols + col;
+    int32_t above_right = 0;
+    if (row > 0) {
+      if (col == 0) above = await_mv(bi - a.cols);
+      if (col + 1 < a.cols) above_right = await_mv(bi - a.cols + 1);
+    }
+    const int64_t j = ref * nb + bi;
+    const Job jb = a.jobs[j];
+    // centre candidates (row, col in 1/8 pel) and their SADs
+    int cr[4] = {0, 0, 0, 0}, cc[4] = {0, 0, 0, 0}, cs[4] = {0, 0, 0, 0};
+    int n = 1;
+    // is_alike_mv against centres [from, n)
+    auto alike = [&](int r, int c, int from) {
+      bool al = false;
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        al |= i >= from && i < n && abs(cc[i] - c) < a.alike_thr && abs(cr[i] - r) < a.alike_thr;
+      return al;
+    };
+    auto add = [&](int32_t m) {
+      const int r = mv_row(m), c = mv_col(m);
+      if (!alike(r, c, 0)) {
+        set4(cr, n, r);
+        set4(cc, n, c);
+        ++n;
+      }
+    };
+    if (row > 0) add(above);
+    if (col > 0) add(left);
+    if (row > 0 && col + 1 < a.cols) add(above_right);
+    if (a.third) {
+      const int32_t m = a.third[j];
+      if (m != kInvalidMv && !alike(mv_row(m), mv_col(m), 1)) {
+        cr[0] = mv_row(m);
+        cc[0] = mv_col(m);
+      }
+    }
+    Ctx c = job_ctx(a.src, a.ss, a.ref, a.rs, jb, a.cost);
+    // with one centre the ranking and both cuts change nothing: skip the SAD
+    if (a.prune && n > 1) {
+      // get_fullmv_from_mv + clamp_fullmv to x->mv_limits, then sdf: the n
+      // SADs' loads in flight together
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        if (i < n) {
+          const int fr = min(max(rawpel(cr[i]), (int)jb.row_min), (int)jb.row_max);
+          const int fc = min(max(rawpel(cc[i]), (int)jb.col_min), (int)jb.col_max);
+          int sad, ssad;
+          sad_and_skip<W, H>(c, lane, fr, fc, sad, ssad);
+          cs[i] = sad;
+        }
+      }
+      // insertion sort: stable, like glibc's qsort on <= 4 entries; as
+      // compare-exchanges of neighbours (i from 1, each sinking left)
+#pragma unroll
+      for (int i = 1; i < 4; ++i) {
+#pragma unroll
+        for (int k = i; k > 0; --k) {
+          if (i < n && cs[k - 1] > cs[k]) {
+            const int r = cr[k], q = cc[k], x = cs[k];
+            cr[k] = cr[k - 1];
+            cc[k] = cc[k - 1];
+            cs[k] = cs[k - 1];
+            cr[k - 1] = r;
+            cc[k - 1] = q;
+            cs[k - 1] = x;
+          }
+        }
+      }
+      n = min(4 - a.prune, n);
+      if (n > 1 && (get4(cs, n - 1) - get4(cs, n - 2)) * 5 > get4(cs, n - 2)) --n;
+    }
+    uint32_t bestsme = 0xFFFFFFFFu;
+    int best_r = 0, best_c = 0, win_i = 0;
+    int bcl[5] = {INT_MAX, INT_MAX, INT_MAX, INT_MAX, INT_MAX};
+    LavishDiamondResult best{};
+    for (int i = 0; i < n; ++i) {
+      const int mr = get4(cr, i), mc = get4(cc, i);
+      // av1_make_default_fullpel_ms_params with ref_mv = the centre
+      Ctx ci = c;
+      ci.ref_mv_row = mr;
+      ci.ref_mv_col = mc;
+      ci.full_ref_row = rawpel(mr);
+      ci.full_ref_col = rawpel(mc);
+      // av1_set_mv_search_range (mcomp.c:206-234): MAX_FULL_PEL_VAL 1023,
+      // MV_LOW / MV_UPP = -/+ (1 << 14)
+      ci.col_min = max((int)jb.col_min, max(((mc + 7) >> 3) - 1023, -2047));
+      ci.row_min = max((int)jb.row_min, max(((mr + 7) >> 3) - 1023, -2047));
+      ci.col_max = max(ci.col_min, min((int)jb.col_max, min((mc >> 3) + 1023, 2047)));
+      ci.row_max = max(ci.row_min, min((int)jb.row_max, min((mr >> 3) + 1023, 2047)));
+      int cl[5] = {INT_MAX, INT_MAX, INT_MAX, INT_MAX, INT_MAX};
+      int br, bc, steps = 0, searches = 0;
+      uint32_t var = 0;
+      const int sme = job_search<W, H, PAT, false, PAT>(ci, lane, rawpel(mr), rawpel(mc),
+                                                        a.step_param, a.skip, a.method, win,
+                                                        want_cl, cl, br, bc, steps, searches,
+                                                        &var);
+      // find_fractional_mv_step at FULL_PEL: setup_center_error, the plain
+      // variance at the full-pel best (MV_COST_NONE); the pattern searches
+      // return it with their var cost
+      if constexpr (!PAT) {
+        Ctx cv = ci;
+        cv.cost_type = 4;
+        cv.sse_lambda = 0;
+        var = (uint32_t)var_cost<W, H>(cv, lane, br, bc);
+      }
+      if (var < bestsme) {
+        bestsme = var;
+        best_r = br;
+        best_c = bc;
+        win_i = i;
+        best.best_row = (int16_t)br;
+        best.best_col = (int16_t)bc;
+        best.bestsme = sme;
+        best.steps = steps;
+        best.searches = searches;
+#pragma unroll
+        for (int k = 0; k < 5; ++k) bcl[k] = cl[k];
+      }
+    }
+    const int32_t mine = mv_pack(8 * best_r, 8 * best_c);
+    if (lane == 0) {
+      __hip_atomic_store(mvs + bi, mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      a.out[j] = best;
+      if (a.centers) a.centers[j] = mv_pack(get4(cr, win_i), get4(cc, win_i));
+    }
+    if (want_cl && lane < 5) {
+      const int v = lane == 0 ? bcl[0] : lane == 1 ? bcl[1] : lane == 2 ? bcl[2] : lane == 3 ? bcl[3] : bcl[4];
+      a.cost_lists[5 * j + lane] = v;
+    }
+    left = mine;
+    above = above_right;
   }
 }
 
@@ -1273,6 +1587,67 @@ int fullpel_batch(const uint8_t* src, int src_stride, const uint8_t* ref, int re
 }  // namespace lavish
 
 using namespace lavish;
+
+extern "C" int64_t lavish_tpl_motion_sync_ints(int nrefs, int rows) {
+  if (nrefs <= 0 || rows <= 0) return -1;
+  return 2;
+}
+
+extern "C" int lavish_tpl_motion_search(const uint8_t* src, int src_stride, const uint8_t* ref,
+                                        int ref_stride, const LavishDiamondJob* jobs, int cols,
+                                        int rows, int nrefs, const LavishTplMvParams* p,
+                                        const LavishMvCostParams* cost,
+                                        const int32_t* third_pass_mvs, int32_t* mvs,
+                                        LavishDiamondResult* out, int32_t* cost_lists,
+                                        int32_t* centers, int32_t* sync, void* stream) {
+  if (cols <= 0 || rows <= 0 || nrefs <= 0) return cols == 0 || rows == 0 || nrefs == 0 ? 0 : -1;
+  if (p == nullptr || jobs == nullptr || mvs == nullptr || out == nullptr || sync == nullptr)
+    return -1;
+  if ((int64_t)cols * rows * nrefs >= ((int64_t)1 << 31)) return -1;
+  if (p->subpel_force_stop != 3) return -6;  // FULL_PEL only (speed >= 5)
+  if (p->prune_starting_mv < 0 || p->prune_starting_mv > 3) return -1;
+  if (p->skip_alike_starting_mv < 0 || p->skip_alike_starting_mv > 2) return -1;
+  if (p->step_param < 0) return -1;
+  if (cost == nullptr || cost->mv_cost_type < 0 || cost->mv_cost_type > 4) return -2;
+  if (cost->mv_cost_type == 0 &&
+      (cost->mvjcost == nullptr || cost->mvcost[0] == nullptr || cost->mvcost[1] == nullptr))
+    return -2;
+  const int m = p->search_method;
+  if (m != kDiamond && m != kBigdia && m != kFastDiamond && m != kFastBigdia &&
+      m != kVfastDiamond)
+    return -4;
+  hipStream_t s = (hipStream_t)stream;
+  LAVISH_CHECK(hipMemsetAsync(sync, 0, sizeof(int32_t) * 2, s));
+  LAVISH_CHECK(hipMemsetD32Async((hipDeviceptr_t)mvs, kInvalidMv, (size_t)cols * rows * nrefs, s));
+  TplMvArgs a;
+  a.src = src;
+  a.ref = ref;
+  a.ss = src_stride;
+  a.rs = ref_stride;
+  a.jobs = (const Job*)jobs;
+  a.cols = cols;
+  a.rows = rows;
+  a.nrefs = nrefs;
+  a.step_param = min(p->step_param, kMaxSteps - 2);  // motion_estimation (tpl_model.c:270-271)
+  a.skip = p->use_downsampled_sad;
+  a.method = m;
+  a.prune = p->prune_starting_mv;
+  a.alike_thr = p->skip_alike_starting_mv == 0 ? 1 : p->skip_alike_starting_mv == 1 ? 64 : 128;
+  a.cost = *cost;
+  a.third = third_pass_mvs;
+  a.mvs = mvs;
+  a.out = out;
+  a.cost_lists = cost_lists;
+  a.centers = centers;
+  a.sync = sync;
+  const dim3 grid((unsigned)(nrefs * rows));
+  if (m == kDiamond)
+    hipLaunchKernelGGL(tpl_mv_kernel<false>, grid, dim3(64), 0, s, a);
+  else
+    hipLaunchKernelGGL(tpl_mv_kernel<true>, grid, dim3(64), 0, s, a);
+  LAVISH_CHECK(hipGetLastError());
+  return 0;
+}
 
 static LavishMvCostParams l1_cost(int mv_cost_type) {
   LavishMvCostParams c = {};

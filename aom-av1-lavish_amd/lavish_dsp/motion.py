@@ -191,11 +191,13 @@ def mv_limits(mi_rows, mi_cols, mi_row, mi_col, mi_height, mi_width, border, ref
 
 
 def frame_jobs(width, height, stride, border, plane_bytes, bw, bh, nrefs, ref_mv=(0, 0),
-               start_mv=(0, 0)):
+               start_mv=(0, 0), mv_border=None):
     """Jobs for every full bw x bh block of a width x height frame against
     each of nrefs padded reference planes (plane k at k * plane_bytes), in
     reference-major, raster block order.  Padded planes: origin at
-    (border, border), `stride` bytes per row."""
+    (border, border), `stride` bytes per row.  mv_border: the border the mv
+    limits allow (av1_set_mv_limits; default the padding, TPL uses
+    tpl_data->border_in_pixels = 32, tpl_model.c:155-156)."""
     mi_rows = ((height + 7) & ~7) // MI_SIZE   # aligned to 8 px like mi_params
     mi_cols = ((width + 7) & ~7) // MI_SIZE
     nbx, nby = width // bw, height // bh
@@ -204,8 +206,9 @@ def frame_jobs(width, height, stride, border, plane_bytes, bw, bh, nrefs, ref_mv
     ys = np.repeat(np.arange(nby) * bh, nbx)
     xs = np.tile(np.arange(nbx) * bw, nby)
     one["src_off"] = (ys + border) * stride + xs + border
+    mb = border if mv_border is None else mv_border
     lim = np.array([mv_limits(mi_rows, mi_cols, y // MI_SIZE, x // MI_SIZE, bh // MI_SIZE,
-                              bw // MI_SIZE, border, ref_mv) for y, x in zip(ys, xs)])
+                              bw // MI_SIZE, mb, ref_mv) for y, x in zip(ys, xs)])
     one["col_min"], one["col_max"], one["row_min"], one["row_max"] = lim.T
     one["start_row"], one["start_col"] = start_mv
     one["ref_mv_row"], one["ref_mv_col"] = ref_mv

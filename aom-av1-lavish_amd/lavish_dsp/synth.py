@@ -45,3 +45,26 @@ def motion_planes(width, height, nrefs, border=160, seed=1234):
     refs = np.stack([pad_plane(shifted(frame(width, height, 8, seed + 101 * k), 3 * k, -2 * k),
                                border) for k in range(1, nrefs + 1)])
     return np.ascontiguousarray(src), np.ascontiguousarray(refs)
+
+
+def tpl_motion_planes(width, height, nrefs, border, seed):
+    """TPL motion-search input: the current frame and nrefs references whose
+    content moves by a different large displacement (up to +-28 pixels) in
+    each quadrant, with fresh +-3 noise -- beyond a zero-start FAST_BIGDIA's
+    reach, so the neighbour-seeded start mvs (tpl_model.c:640-735) decide
+    the result.  Returns (src[Hp, Wp], refs[nrefs, Hp, Wp]), padded."""
+    rng = np.random.default_rng(seed)
+    src = frame(width, height, 8, seed)
+    refs = []
+    for _ in range(nrefs):
+        ref = np.empty_like(src)
+        for qy in range(2):
+            for qx in range(2):
+                dx, dy = (int(v) for v in rng.integers(-28, 29, size=2))
+                sh = shifted(src, dx, dy).astype(np.int16)
+                sh = np.clip(sh + rng.integers(-3, 4, size=sh.shape), 0, 255).astype(np.uint8)
+                ys = slice(qy * height // 2, (qy + 1) * height // 2)
+                xs = slice(qx * width // 2, (qx + 1) * width // 2)
+                ref[ys, xs] = sh[ys, xs]
+        refs.append(pad_plane(ref, border))
+    return np.ascontiguousarray(pad_plane(src, border)), np.ascontiguousarray(np.stack(refs))

@@ -12,10 +12,11 @@ the device for every 16x16 block x reference of a frame:
   tpl_get_satd_cost per reference, the cheapest one, txfm_quant_rdcost
                                       -> lavish_tpl_block_batch
 
-Intra candidates and the reference's per-block start-mv selection
-(prune_starting_mv / compare_sad over neighbouring tpl stats, which depends
-on already-finished blocks) stay with the caller: the start / center mv of
-each (block, reference) comes in the motion jobs."""
+The full-pel step runs with the reference's per-block start-mv selection
+(tpl_motion_search: neighbouring tpl mvs, is_alike_mv, prune_starting_mv;
+a device wavefront, since each block needs its finished neighbours) or,
+with neighbour_starts=False, from the jobs' start mvs.  Intra candidates
+stay with the caller."""
 import ctypes
 
 import numpy as np
@@ -34,6 +35,9 @@ _lib.lavish_tpl_block_batch.argtypes = [_vp, _i32, _vp, _i64, _i32, _i32, _i32, 
 _lib.lavish_tpl_block_batch.restype = _i32
 
 TPL_BSIZE = 16  # set_tpl_stats_block_size (tpl_model.c:137-145)
+# tpl_data->border_in_pixels = ALIGN_POWER_OF_TWO(16 + 2 * AOM_INTERP_EXTEND, 5)
+# (tpl_model.c:155-156): the mv limits of the TPL motion search
+TPL_BORDER = 32
 
 
 def tpl_block_batch(src, preds, bsize, bit_depth, qp, width=None, height=None, out=None,
@@ -78,6 +82,82 @@ def records_numpy(out):
     return out.cpu().numpy().view(TPL_BLOCK_DTYPE)
 
 
+class TplMvParams(ctypes.Structure):
+    """LavishTplMvParams: the tpl_sf / mv_sf fields motion_estimation reads."""
+    _fields_ = [("search_method", _i32), ("step_param", _i32), ("use_downsampled_sad", _i32),
+                ("prune_starting_mv", _i32), ("skip_alike_starting_mv", _i32),
+                ("subpel_force_stop", _i32)]
+
+
+_lib.lavish_tpl_motion_sync_ints.argtypes = [_i32, _i32]
+_lib.lavish_tpl_motion_sync_ints.restype = _i64
+_lib.lavish_tpl_motion_search.argtypes = [_vp, _i32, _vp, _i32, _vp, _i32, _i32, _i32,
+                                          ctypes.POINTER(TplMvParams),
+                                          ctypes.POINTER(M.MvCostParams), _vp, _vp, _vp, _vp,
+                                          _vp, _vp, _vp]
+_lib.lavish_tpl_motion_search.restype = _i32
+INVALID_MV = -0x7FFF8000  # 0x80008000 as int32
+
+
+def pack_mv(row, col):
+    """int_mv.as_int of (row, col) (1/8 pel, row in the low half)."""
+    r = np.asarray(row, np.int64) & 0xFFFF
+    c = np.asarray(col, np.int64) & 0xFFFF
+    return ((c << 16) | r).astype(np.uint32).view(np.int32)
+
+
+def unpack_mv(m):
+    m = np.asarray(m).astype(np.int32).view(np.uint32)
+    return ((m & 0xFFFF).astype(np.uint16).view(np.int16).astype(np.int32),
+            (m >> 16).astype(np.uint16).view(np.int16).astype(np.int32))
+
+
+def tpl_motion_search(src, ref, jobs, cols, rows, nrefs, cost, search_method="fast_bigdia",
+                      step_param=6, use_downsampled_sad=False, prune_starting_mv=3,
+                      skip_alike_starting_mv=2, third_pass_mvs=None, cost_list=True,
+                      out=None, stream=None):
+    """lavish_tpl_motion_search: mode_estimation's per-reference motion search
+    with neighbour start mvs, as a device wavefront.  src / ref / jobs as
+    motion.full_pixel_search_batch (jobs [nrefs][rows * cols] raster, limits
+    = x->mv_limits); third_pass_mvs: None or an int32 device tensor of int_mv.
+    out: None or a dict of preallocated tensors (mvs, fp, cl, centers, sync).
+    Returns that dict: mvs int32 [nrefs * rows * cols] (int_mv), fp (RESULT
+    records), cl (int32 [n, 5] or None), centers (int_mv), sync."""
+    import torch
+    assert src.dtype == torch.uint8 and ref.dtype == torch.uint8
+    assert src.is_contiguous() and ref.is_contiguous(), "planes must be C-contiguous"
+    n = nrefs * rows * cols
+    assert jobs.numel() == n * M.JOB_DTYPE.itemsize
+    dev = src.device
+    if out is None:
+        out = {"mvs": torch.empty(n, dtype=torch.int32, device=dev),
+               "fp": torch.empty(n * M.RESULT_DTYPE.itemsize, dtype=torch.uint8, device=dev),
+               "cl": torch.empty((n, 5), dtype=torch.int32, device=dev) if cost_list else None,
+               "centers": torch.empty(n, dtype=torch.int32, device=dev),
+               "sync": torch.empty(int(_lib.lavish_tpl_motion_sync_ints(nrefs, rows)),
+                                   dtype=torch.int32, device=dev)}
+    p = TplMvParams(M.SEARCH_METHODS[search_method], step_param, int(use_downsampled_sad),
+                    prune_starting_mv, skip_alike_starting_mv, M.FULL_PEL)
+    if third_pass_mvs is not None:
+        assert third_pass_mvs.dtype == torch.int32 and third_pass_mvs.numel() == n
+    cl = out["cl"]
+    rc = _lib.lavish_tpl_motion_search(
+        _vp(src.data_ptr()), src.stride(0), _vp(ref.data_ptr()), src.stride(0),
+        _vp(jobs.data_ptr()), cols, rows, nrefs, ctypes.byref(p), ctypes.byref(cost),
+        _vp(third_pass_mvs.data_ptr()) if third_pass_mvs is not None else None,
+        _vp(out["mvs"].data_ptr()), _vp(out["fp"].data_ptr()),
+        _vp(cl.data_ptr()) if cl is not None else None, _vp(out["centers"].data_ptr()),
+        _vp(out["sync"].data_ptr()), _stream_ptr(stream))
+    if rc != 0:
+        raise ValueError("lavish_tpl_motion_search rejected its arguments (rc=%d)" % rc)
+    return out
+
+
+def tpl_motion_failures(out):
+    """Waits that timed out in the last tpl_motion_search (0 = valid)."""
+    return int(out["sync"][-1].item())
+
+
 class TplFrame:
     """Device state of one TPL frame leg (8-bit): padded source / reference
     planes (border >= AOM_BORDER_IN_PIXELS for the predictor), the motion jobs
@@ -86,7 +166,9 @@ class TplFrame:
 
     def __init__(self, src_np, refs_np, width, height, border, qindex, rdmult,
                  search_method="fast_bigdia", step_param=6, forced_stop=M.FULL_PEL,
-                 subpel_method="pruned_more", start_mvs=None, device="cuda"):
+                 subpel_method="pruned_more", start_mvs=None, device="cuda",
+                 neighbour_starts=True, prune_starting_mv=3, skip_alike_starting_mv=2,
+                 use_downsampled_sad=False, mv_border=TPL_BORDER):
         import torch
         from . import build_quant_params, QUANT_FP
         assert border >= I.AOM_BORDER_IN_PIXELS
@@ -98,12 +180,22 @@ class TplFrame:
         self.refs = torch.from_numpy(refs_np).to(device)
         org = border * self.stride + border
         self.org = org
-        jobs = M.frame_jobs(width, height, self.stride, border, src_np.size, bs, bs, self.nrefs)
+        jobs = M.frame_jobs(width, height, self.stride, border, src_np.size, bs, bs, self.nrefs,
+                            mv_border=mv_border)
+        # the reference's start mvs (mode_estimation, tpl_model.c:640-735):
+        # neighbour-seeded centres, a device wavefront; needs FULL_PEL
+        self.neighbour_starts = neighbour_starts and start_mvs is None
+        assert not self.neighbour_starts or forced_stop == M.FULL_PEL, \
+            "neighbour start mvs need tpl_sf.subpel_force_stop FULL_PEL"
+        self.prune, self.alike = prune_starting_mv, skip_alike_starting_mv
+        self.skip_sad = use_downsampled_sad
+        self.cols, self.rows = width // bs, height // bs
         if start_mvs is not None:
             jobs["start_row"], jobs["start_col"] = start_mvs[:, 0], start_mvs[:, 1]
         self.jobs_np = jobs
         self.jobs = M.to_device(jobs)
-        sj = M.subpel_jobs(width, height, border, bs, bs, jobs, np.zeros(len(jobs), M.RESULT_DTYPE))
+        sj = M.subpel_jobs(width, height, mv_border, bs, bs, jobs,
+                           np.zeros(len(jobs), M.RESULT_DTYPE))
         self.sub_jobs = M.to_device(sj)
         # inter prediction jobs: job j = (ref k, block) -> pred plane k, same position
         nb = (width // bs) * (height // bs)
@@ -134,12 +226,24 @@ class TplFrame:
         self.recon = torch.empty((height, width), dtype=torch.uint8, device=device)
         self.costs = torch.empty((nb, self.nrefs), dtype=torch.int32, device=device)
         self.src_view = self.src[border:border + height, border:border + width]
+        self.mv_out = None
+        if self.neighbour_starts:
+            self.mv_out = {"mvs": torch.empty(n, dtype=torch.int32, device=device), "fp": self.fp,
+                           "cl": self.cl,
+                           "centers": torch.empty(n, dtype=torch.int32, device=device),
+                           "sync": torch.empty(int(_lib.lavish_tpl_motion_sync_ints(
+                               self.nrefs, self.rows)), dtype=torch.int32, device=device)}
 
     def step(self, stream=None, ref_costs=True):
         bs = TPL_BSIZE
-        M.full_pixel_search_batch(self.src, self.refs, bs, bs, self.jobs, self.cost,
-                                  self.search_method, self.step_param, False, True, out=self.fp,
-                                  cost_lists=self.cl, stream=stream)
+        if self.neighbour_starts:
+            tpl_motion_search(self.src, self.refs, self.jobs, self.cols, self.rows, self.nrefs,
+                              self.cost, self.search_method, self.step_param, self.skip_sad,
+                              self.prune, self.alike, out=self.mv_out, stream=stream)
+        else:
+            M.full_pixel_search_batch(self.src, self.refs, bs, bs, self.jobs, self.cost,
+                                      self.search_method, self.step_param, self.skip_sad, True,
+                                      out=self.fp, cost_lists=self.cl, stream=stream)
         M.find_best_sub_pixel_tree_batch(self.src, self.refs, bs, bs, self.sub_jobs,
                                          self.cost_none, self.subpel_method, self.forced_stop,
                                          self.allow_hp, 1, fullpel=self.fp, cost_lists=self.cl,

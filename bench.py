@@ -1053,8 +1053,9 @@ def tpl_block_bytes(W, H, nrefs, bs=16):
 
 
 def cpu_baseline_tpl(args):
-    """The oracle chain (full-pel, sub-pel, prediction, block leg) on a 1920x256
-    strip with the bench's parameters, repeated for ~cpu_seconds."""
+    """The oracle chain (start-mv full-pel, sub-pel, prediction, block leg) on
+    a 1920x256 strip with the bench's parameters, repeated for ~cpu_seconds
+    (the start-mv walk uses one thread per reference, the rest all cores)."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import _oracle as O
     import lavish_dsp.inter as I
@@ -1062,9 +1063,9 @@ def cpu_baseline_tpl(args):
     import lavish_dsp.synth as synth
     threads = host_cores()
     W, Hs, R, border = args.width, 256, args.refs, TPL_BORDER
-    src, refs = synth.motion_planes(W, Hs, R, border)
+    src, refs = synth.tpl_motion_planes(W, Hs, R, border, seed=1234)
     st = src.shape[1]
-    jobs = M.frame_jobs(W, Hs, st, border, src.size, 16, 16, R)
+    jobs = M.frame_jobs(W, Hs, st, border, src.size, 16, 16, R, mv_border=32)
     allow_hp = args.qindex < 128
     mvj, mvc = M.default_mv_cost_tables(allow_hp)
     spb, epb = M.sad_per_bit(args.qindex), M.error_per_bit(args.rdmult)
@@ -1078,10 +1079,11 @@ def cpu_baseline_tpl(args):
     passes = 0
     t0 = time.perf_counter()
     while True:
-        fp, cl = O.full_pixel_search_batch(src.reshape(-1), refs.reshape(-1), st, 16, 16, jobs,
-                                           "fast_bigdia", 6, 0, spb, epb, mvj, mvc,
-                                           cost_list=True, threads=threads)
-        sj = M.subpel_jobs(W, Hs, border, 16, 16, jobs, fp)
+        # the start-mv walk is sequential per reference: one thread each
+        _, fp, cl, _ = O.tpl_motion_search(src.reshape(-1), refs.reshape(-1), st, jobs, W // 16,
+                                           Hs // 16, R, "fast_bigdia", 6, False, 3, 2, spb, epb,
+                                           mvj, mvc, 0)
+        sj = M.subpel_jobs(W, Hs, 32, 16, 16, jobs, fp)
         sub = O.subpel_search_batch(src.reshape(-1), refs.reshape(-1), st, 16, 16, sj, 2,
                                     M.FULL_PEL, allow_hp, 1, M.MV_COST_NONE, 0, None, None, cl,
                                     threads=threads)
@@ -1119,7 +1121,7 @@ def main_tpl(args):
     if world > 1:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
     W, H, R = args.width, args.height, args.refs
-    src, refs = synth.motion_planes(W, H, R, TPL_BORDER, seed=1234 + rank)
+    src, refs = synth.tpl_motion_planes(W, H, R, TPL_BORDER, seed=1234 + rank)
     tf = T.TplFrame(src, refs, W, H, TPL_BORDER, args.qindex, args.rdmult)
     stream = torch.cuda.current_stream()
     bs = T.TPL_BSIZE
@@ -1127,9 +1129,10 @@ def main_tpl(args):
     def step(ev=None):
         mark = (lambda i: ev[i].record(stream)) if ev is not None else (lambda i: None)
         mark(0)
-        M.full_pixel_search_batch(tf.src, tf.refs, bs, bs, tf.jobs, tf.cost, tf.search_method,
-                                  tf.step_param, False, True, out=tf.fp, cost_lists=tf.cl,
-                                  stream=stream)
+        # mode_estimation's start mvs + FAST_BIGDIA: the device wavefront
+        T.tpl_motion_search(tf.src, tf.refs, tf.jobs, tf.cols, tf.rows, tf.nrefs, tf.cost,
+                            tf.search_method, tf.step_param, tf.skip_sad, tf.prune, tf.alike,
+                            out=tf.mv_out, stream=stream)
         mark(1)
         M.find_best_sub_pixel_tree_batch(tf.src, tf.refs, bs, bs, tf.sub_jobs, tf.cost_none,
                                          tf.subpel_method, tf.forced_stop, tf.allow_hp, 1,
@@ -1168,7 +1171,9 @@ def main_tpl(args):
         raise RuntimeError("HIP error during bench: %s" % (status,))
     K = args.steps
     legs = [sum(ev[k][i].elapsed_time(ev[k][i + 1]) for k in range(K)) / K for i in range(4)]
-    names = ["fullpel_fast_bigdia", "subpel", "inter_pred", "tpl_block"]
+    names = ["fullpel_start_mv_wavefront", "subpel", "inter_pred", "tpl_block"]
+    if T.tpl_motion_failures(tf.mv_out):
+        raise RuntimeError("tpl motion wavefront: a wait timed out")
     blk_bytes = tpl_block_bytes(W, H, R)
     fp_res = M.results_numpy(tf.fp)
     # full-pel leg bytes: per job the source block, the var cost's 2 blocks,
@@ -1193,16 +1198,20 @@ def main_tpl(args):
         "data": "synthetic (seeded 1080p content, lavish_dsp/synth.py)",
         "config": {
             "workload": "tpl: %dx%d 8-bit frame per step; TPL inter leg of every 16x16 block x %d "
-                        "refs: FAST_BIGDIA full-pel (step_param 6, MV_COST_ENTROPY default nmv "
-                        "context, cost list) -> sub-pel forced stop FULL_PEL (MV_COST_NONE) -> "
+                        "refs: mode_estimation's start mvs (neighbour tpl mvs, is_alike_mv "
+                        "skip_alike 2, prune_starting_mv 3: full-SAD ranking, one search) as a "
+                        "device wavefront + FAST_BIGDIA full-pel (step_param 6, "
+                        "MV_COST_ENTROPY default nmv context, ref_mv = the centre, cost list, mv "
+                        "border 32) -> sub-pel forced stop FULL_PEL (MV_COST_NONE) -> "
                         "EIGHTTAP_REGULAR prediction -> tpl_get_satd_cost per ref, best ref, "
                         "get_quantize_error (quantize_fp qindex %d) + rate_estimator + recon; "
                         "%d SB64/frame" % (W, H, R, args.qindex, sb),
             "parallelism": "frame-per-rank x%d" % world,
         },
         "roofline": ({"bound": "hbm",
-                      "kernel": "diamond_kernel<16,16,true> (FAST_BIGDIA, "
-                                "lavish_full_pixel_search_batch)",
+                      "kernel": "tpl_mv_kernel<true> (FAST_BIGDIA with the start-mv "
+                                "candidates, lavish_tpl_motion_search wavefront; latency-bound: "
+                                "%d dependent block steps)" % (tf.cols + 2 * (tf.rows - 1)),
                       "achieved": round(fp_bytes / (legs[0] * 1e-3) / 1e9, 1),
                       "peak": HBM_PEAK_GBS, "unit": "GB/s", "traffic": None,
                       "avg_launch_ms": round(legs[0], 4),
@@ -1217,6 +1226,11 @@ def main_tpl(args):
         "tpl": {"blocks": int(len(recs)), "mean_eob": round(float(recs["eob"].mean()), 2),
                 "refs_chosen": int(len(set(recs["best_ref"].tolist()))),
                 "fullpel_sad_blocks_per_job": round(float(fp_res["searches"].mean()), 2),
+                "wavefront": {"block_steps": tf.cols + 2 * (tf.rows - 1),
+                              "us_per_block_step": round(legs[0] * 1e3 /
+                                                         (tf.cols + 2 * (tf.rows - 1)), 3),
+                              "jobs_started_off_zero": int(np.count_nonzero(
+                                  tf.mv_out["centers"].cpu().numpy()))},
                 "block_leg": {"ms": round(legs[3], 4), "algorithmic_bytes": blk_bytes,
                               "achieved_GBps": round(blk_bytes / (legs[3] * 1e-3) / 1e9, 1)}},
     }

@@ -727,6 +727,57 @@ int lavish_tpl_block_batch(const void *src, int src_stride, const void *preds,
                            void *recon, int recon_stride, int32_t *ref_costs,
                            void *stream);
 
+/* ---- TPL motion search with start-mv candidates --
+ * Replaces the per-reference loop of mode_estimation
+ * (av1/encoder/tpl_model.c:632-743) for a frame of 16x16 TPL blocks
+ * (set_tpl_stats_block_size, :136-144): centre mvs = zero, then the above,
+ * left and above-right blocks' tpl mvs of the same reference unless
+ * is_alike_mv (:319-333, threshold by skip_alike_starting_mv), the optional
+ * third-pass mv in slot 0 (:687-703); with prune_starting_mv the full-SAD
+ * ranking at the clamped full-pel centres and the cut (:705-728); then
+ * motion_estimation (:249-303) per centre -- av1_full_pixel_search with
+ * ref_mv = the centre, tpl_sf.search_method, step_param =
+ * AOMMIN(reduce_first_step_size, 9), the caller's mv costs and
+ * use_downsampled_sad, a cost list when cost_lists != NULL -- keeping the
+ * lowest sub-pel error (strict <).  subpel_force_stop must be FULL_PEL
+ * (speed >= 5, speed_features.c:1212-1216; else -6): the tpl mv is the
+ * full-pel best x 8.  Blocks depend on their finished neighbours: the call
+ * runs as a device wavefront (one wave per reference x block row).
+ *   jobs: [nrefs][rows * cols] LavishDiamondJob in raster order (offsets;
+ *     limits = x->mv_limits of av1_set_mv_limits with tpl border_in_pixels;
+ *     start / ref_mv fields ignored); the src / ref planes as for
+ *     lavish_full_pixel_search_batch.
+ *   third_pass_mvs: NULL or int_mv [nrefs][rows * cols] (INVALID_MV =
+ *     0x80008000 for none).
+ *   out (device): mvs int_mv [nrefs][rows * cols] = tpl_stats->mv[rf_idx]
+ *     (row in the low 16 bits); out: the winning full-pel search's
+ *     LavishDiamondResult; cost_lists (or NULL) its cost list; centers (or
+ *     NULL) its centre mv (int_mv).
+ *   sync: device int32 scratch of lavish_tpl_motion_sync_ints(nrefs, rows)
+ *     entries (zeroed by the call); after the stream drains, sync[1] != 0
+ *     means a wait timed out (results invalid).  mvs is filled with
+ *     INVALID_MV first and each entry published once, when final.
+ * Returns 0, -1 bad geometry / parameters, -2 bad costs, -4 bad method,
+ * -6 subpel_force_stop != FULL_PEL. */
+typedef struct LavishTplMvParams {
+  int search_method;          /* tpl_sf.search_method (SEARCH_METHODS value) */
+  int step_param;             /* tpl_sf.reduce_first_step_size */
+  int use_downsampled_sad;    /* mv_sf.use_downsampled_sad */
+  int prune_starting_mv;      /* tpl_sf.prune_starting_mv, 0..3 */
+  int skip_alike_starting_mv; /* tpl_sf.skip_alike_starting_mv, 0..2 */
+  int subpel_force_stop;      /* tpl_sf.subpel_force_stop: FULL_PEL (3) */
+} LavishTplMvParams;
+
+int64_t lavish_tpl_motion_sync_ints(int nrefs, int rows);
+int lavish_tpl_motion_search(const uint8_t *src, int src_stride,
+                             const uint8_t *ref, int ref_stride,
+                             const LavishDiamondJob *jobs, int cols, int rows,
+                             int nrefs, const LavishTplMvParams *p,
+                             const LavishMvCostParams *cost,
+                             const int32_t *third_pass_mvs, int32_t *mvs,
+                             LavishDiamondResult *out, int32_t *cost_lists,
+                             int32_t *centers, int32_t *sync, void *stream);
+
 /* ---- TX-type pruning features ---------------------
  * Every full bw x bh block of an int16 residual plane (raster order):
  * av1_get_horver_correlation_full (av1/encoder/rdopt.c:514-609) -> hcorr /

@@ -351,6 +351,15 @@ void orc_tpl_block_batch(const void *src, int src_stride, const void *preds, lon
                          int pred_stride, int nrefs, int width, int height, int bsize, int bd,
                          const OrcQuant *q, OrcTplBlock *out, void *recon, int recon_stride,
                          int32_t *ref_costs, int threads);
+/* mode_estimation's per-reference motion search with start-mv candidates
+ * (oracle_tpl.c; 16x16 blocks, subpel_force_stop FULL_PEL); layouts as
+ * lavish_tpl_motion_search (include/lavish_dsp.h); one thread per reference */
+void orc_tpl_motion_search(const uint8_t *src, int src_stride, const uint8_t *ref,
+                           int ref_stride, const OrcDiamondJob *jobs, int cols, int rows,
+                           int nrefs, int method, int step_param, int skip_sad,
+                           int prune_starting_mv, int skip_alike_starting_mv,
+                           const OrcMvCost *cost, const int32_t *third, int32_t *mvs,
+                           OrcDiamondResult *out, int32_t *cost_lists, int32_t *centers);
 
 /* ---- av1_quant selection (oracle_qfacade.c): mode 0 FP, 1 B, 2 DC, 3 skip
  * quant, 4 search_tx_type's satd gate; returns use_optimize_b | kind << 1 -- */

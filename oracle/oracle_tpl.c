@@ -11,6 +11,7 @@
  * oracle's pinned pieces (orc_fwd_txfm2d, orc_quantize_fp, orc_block_error,
  * orc_inv_txfm2d_add).
  */
+#include <limits.h>
 #include <pthread.h>
 #include <stdlib.h>
 #include <string.h>
@@ -124,4 +125,163 @@ void orc_tpl_block_batch(const void *src, int src_stride, const void *preds, lon
   }
   if (threads > 1)
     for (int t = 0; t < threads; ++t) pthread_join(tid[t], NULL);
+}
+
+/* ---- TPL motion search with start-mv candidates ------------------------
+ * mode_estimation's per-reference loop (av1/encoder/tpl_model.c:632-743)
+ * over a frame of TPL blocks in raster order, one thread per reference (the
+ * references are independent; within one the blocks are sequential, as in
+ * the reference's row-synchronised walk):
+ *   center_mvs = {zero}; above (:656-664), left (:666-674), above-right
+ *   (:676-685) tpl mvs of the same reference unless is_alike_mv (:319-333);
+ *   the third-pass mv into slot 0 (:687-703); prune_starting_mv (:705-728):
+ *   sdf at the clamped full-pel centres, qsort by compare_sad (:310-317;
+ *   insertion sort here: stable, as glibc's qsort is for <= 4 entries),
+ *   the cut to 4 - prune_starting_mv, the SAD-gap cut; motion_estimation
+ *   (:249-303) per centre: av1_full_pixel_search from get_fullmv_from_mv
+ *   (centre) with ref_mv = centre (av1_make_default_fullpel_ms_params ->
+ *   av1_set_mv_search_range, mcomp.c:95-164,206-234) and, at
+ *   subpel_force_stop FULL_PEL, the sub-pel step's setup_center_error: the
+ *   variance at the full-pel best (MV_COST_NONE); strict < keeps the first
+ *   best (:736-739). */
+typedef struct {
+  const uint8_t *src, *ref;
+  int ss, rs, cols, rows, method, step_param, skip, prune, thr, nrefs;
+  const OrcMvCost *cost;
+  const OrcDiamondJob *jobs;
+  const int32_t *third;
+  int32_t *mvs, *cls, *centers;
+  OrcDiamondResult *out;
+  int ref_idx;
+} TplMvArg;
+
+static int rawpel_mv(int x) { return (x + 3 + (x >= 0)) >> 3; } /* GET_MV_RAWPEL, mv.h:28 */
+static int mvr(int32_t m) { return (int16_t)(m & 0xFFFF); }
+static int mvc(int32_t m) { return (int16_t)((uint32_t)m >> 16); }
+static int32_t mvpack(int r, int c) { return (int32_t)(((uint32_t)(uint16_t)c << 16) | (uint16_t)r); }
+
+typedef struct {
+  int row, col, sad;
+} CenterMv; /* center_mv_t */
+
+static int is_alike(int r, int c, const CenterMv *cm, int n, int thr) {
+  for (int i = 0; i < n; ++i)
+    if (abs(cm[i].col - c) < thr && abs(cm[i].row - r) < thr) return 1;
+  return 0;
+}
+
+/* AOMMIN(reduce_first_step_size, MAX_MVSEARCH_STEPS - 2) (:270-271) */
+#define MAX_TPL_STEP 9
+
+static void *tpl_mv_worker(void *v) {
+  const TplMvArg *a = (const TplMvArg *)v;
+  const int k = a->ref_idx;
+  const long nb = (long)a->rows * a->cols;
+  int32_t *mvs = a->mvs + k * nb;
+  for (int r = 0; r < a->rows; ++r)
+    for (int c = 0; c < a->cols; ++c) {
+      const long bi = (long)r * a->cols + c, j = k * nb + bi;
+      const OrcDiamondJob *jb = &a->jobs[j];
+      CenterMv cm[4] = { { 0, 0, INT_MAX }, { 0, 0, INT_MAX }, { 0, 0, INT_MAX },
+                         { 0, 0, INT_MAX } };
+      int n = 1;
+      int32_t cand[3];
+      int nc = 0;
+      if (r > 0) cand[nc++] = mvs[bi - a->cols];
+      if (c > 0) cand[nc++] = mvs[bi - 1];
+      if (r > 0 && c + 1 < a->cols) cand[nc++] = mvs[bi - a->cols + 1];
+      for (int i = 0; i < nc; ++i)
+        if (!is_alike(mvr(cand[i]), mvc(cand[i]), cm, n, a->thr)) {
+          cm[n].row = mvr(cand[i]);
+          cm[n].col = mvc(cand[i]);
+          ++n;
+        }
+      if (a->third && a->third[j] != (int32_t)0x80008000 &&
+          !is_alike(mvr(a->third[j]), mvc(a->third[j]), cm + 1, n - 1, a->thr)) {
+        cm[0].row = mvr(a->third[j]);
+        cm[0].col = mvc(a->third[j]);
+      }
+      const uint8_t *sb = a->src + jb->src_off, *rb = a->ref + jb->ref_off;
+      if (a->prune) {
+        for (int i = 0; i < n; ++i) {
+          int fr = rawpel_mv(cm[i].row), fc = rawpel_mv(cm[i].col);
+          fr = fr < jb->row_min ? jb->row_min : fr > jb->row_max ? jb->row_max : fr;
+          fc = fc < jb->col_min ? jb->col_min : fc > jb->col_max ? jb->col_max : fc;
+          cm[i].sad = (int)orc_sad(sb, a->ss, rb + (long)fr * a->rs + fc, a->rs, 16, 16);
+        }
+        for (int i = 1; i < n; ++i) {
+          const CenterMv x = cm[i];
+          int q = i;
+          while (q > 0 && cm[q - 1].sad > x.sad) {
+            cm[q] = cm[q - 1];
+            --q;
+          }
+          cm[q] = x;
+        }
+        if (n > 4 - a->prune) n = 4 - a->prune;
+        if (n > 1 && (cm[n - 1].sad - cm[n - 2].sad) * 5 > cm[n - 2].sad) --n;
+      }
+      unsigned bestsme = 0xFFFFFFFFu;
+      int best_r = 0, best_c = 0;
+      for (int i = 0; i < n; ++i) {
+        OrcMsParams p = { sb, a->ss, rb, a->rs, 16, 16, jb->col_min, jb->col_max, jb->row_min,
+                          jb->row_max, cm[i].row, cm[i].col, a->cost->mv_cost_type, a->skip,
+                          a->cost };
+        /* av1_set_mv_search_range (MAX_FULL_PEL_VAL 1023, MV_LOW/UPP -/+2^14) */
+        int t;
+        t = ((cm[i].col + 7) >> 3) - 1023; t = t > -2047 ? t : -2047;
+        if (p.col_min < t) p.col_min = t;
+        t = ((cm[i].row + 7) >> 3) - 1023; t = t > -2047 ? t : -2047;
+        if (p.row_min < t) p.row_min = t;
+        t = (cm[i].col >> 3) + 1023; t = t < 2047 ? t : 2047;
+        if (p.col_max > t) p.col_max = t;
+        t = (cm[i].row >> 3) + 1023; t = t < 2047 ? t : 2047;
+        if (p.row_max > t) p.row_max = t;
+        if (p.col_max < p.col_min) p.col_max = p.col_min;
+        if (p.row_max < p.row_min) p.row_max = p.row_min;
+        int cl[5], br, bc, steps = 0;
+        const int sme = orc_full_pixel_search(&p, a->method, rawpel_mv(cm[i].row),
+                                              rawpel_mv(cm[i].col), a->step_param,
+                                              a->cls ? cl : NULL, &br, &bc, &steps);
+        unsigned sse;
+        const unsigned thissme =
+            orc_variance(sb, a->ss, rb + (long)br * a->rs + bc, a->rs, 16, 16, &sse);
+        if (thissme < bestsme) {
+          bestsme = thissme;
+          best_r = br;
+          best_c = bc;
+          a->out[j].best_row = (int16_t)br;
+          a->out[j].best_col = (int16_t)bc;
+          a->out[j].bestsme = sme;
+          a->out[j].steps = steps;
+          a->out[j].reserved = 0;
+          if (a->cls) memcpy(a->cls + 5 * j, cl, sizeof(cl));
+          if (a->centers) a->centers[j] = mvpack(cm[i].row, cm[i].col);
+        }
+      }
+      mvs[bi] = mvpack(8 * best_r, 8 * best_c);
+    }
+  return NULL;
+}
+
+void orc_tpl_motion_search(const uint8_t *src, int src_stride, const uint8_t *ref,
+                           int ref_stride, const OrcDiamondJob *jobs, int cols, int rows,
+                           int nrefs, int method, int step_param, int skip_sad,
+                           int prune_starting_mv, int skip_alike_starting_mv,
+                           const OrcMvCost *cost, const int32_t *third, int32_t *mvs,
+                           OrcDiamondResult *out, int32_t *cost_lists, int32_t *centers) {
+  static const int thr[3] = { 1, 8 << 3, 16 << 3 }; /* mv_diff_thr (:322) */
+  if (nrefs > 64) nrefs = 64;
+  pthread_t tid[64];
+  TplMvArg args[64];
+  const int sp = step_param < MAX_TPL_STEP ? step_param : MAX_TPL_STEP;
+  for (int k = 0; k < nrefs; ++k) {
+    args[k] = (TplMvArg){ src, ref, src_stride, ref_stride, cols, rows, method, sp, skip_sad,
+                          prune_starting_mv, thr[skip_alike_starting_mv], nrefs, cost, jobs,
+                          third, mvs, cost_lists, centers, out, k };
+    if (nrefs > 1) pthread_create(&tid[k], NULL, tpl_mv_worker, &args[k]);
+    else tpl_mv_worker(&args[k]);
+  }
+  if (nrefs > 1)
+    for (int k = 0; k < nrefs; ++k) pthread_join(tid[k], NULL);
 }

@@ -461,6 +461,47 @@ def full_pixel_search_batch(src, ref, stride, w, h, jobs, method="diamond", step
     return out, cls
 
 
+def tpl_motion_search(src, ref, stride, jobs, cols, rows, nrefs, method="fast_bigdia",
+                      step_param=6, skip=False, prune_starting_mv=3, skip_alike_starting_mv=2,
+                      sad_per_bit=0, error_per_bit=0, mvjcost=None, mvcost=None, mv_cost_type=0,
+                      third=None, cost_list=True):
+    """orc_tpl_motion_search: mode_estimation's per-reference motion search with
+    the neighbour start mvs (16x16, FULL_PEL).  Returns (mvs int32 int_mv,
+    results, cost lists or None, centers int32 int_mv)."""
+    L = lib()
+    fn = L.orc_tpl_motion_search
+    fn.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p,
+                   ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                   ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.POINTER(OrcMvCost),
+                   ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                   ctypes.c_void_p]
+    jobs = np.ascontiguousarray(jobs)
+    assert len(jobs) == nrefs * rows * cols
+    keep = []
+    c = OrcMvCost(mv_cost_type, sad_per_bit, error_per_bit)
+    if mvjcost is not None:
+        mj = np.ascontiguousarray(mvjcost, np.int32)
+        mc = np.ascontiguousarray(mvcost, np.int32)
+        keep += [mj, mc]
+        mid = (mc.shape[1] - 1) // 2
+        c.mvjcost = mj.ctypes.data
+        c.mvcost[0] = mc.ctypes.data + 4 * mid
+        c.mvcost[1] = mc.ctypes.data + 4 * (mc.shape[1] + mid)
+    n = len(jobs)
+    out = np.zeros(n, np.dtype([("best_row", "<i2"), ("best_col", "<i2"), ("bestsme", "<i4"),
+                                ("steps", "<i4"), ("searches", "<i4")], align=True))
+    cls = np.full((n, 5), 0x7FFFFFFF, np.int32) if cost_list else None
+    mvs = np.zeros(n, np.int32)
+    centers = np.zeros(n, np.int32)
+    if third is not None:
+        third = np.ascontiguousarray(third, np.int32)
+    fn(P(src), stride, P(ref), stride, P(jobs), cols, rows, nrefs, FP_METHODS[method], step_param,
+       int(skip), prune_starting_mv, skip_alike_starting_mv, ctypes.byref(c),
+       P(third) if third is not None else None, P(mvs), P(out), P(cls) if cost_list else None,
+       P(centers))
+    return mvs, out, cls, centers
+
+
 def subpel_search_batch(src, ref, stride, w, h, jobs, method=2, forced_stop=0, allow_hp=False,
                         iters=1, mv_cost_type=3, error_per_bit=0, mvjcost=None, mvcost=None,
                         cost_lists=None, threads=1):

@@ -1349,6 +1349,11 @@ class TU:
                 toks = self.pp.process(fh.read(), f)
             self.parse_top(toks, f)
 
+    def add_source(self, text, fname):
+        """Parse extra C text in this TU (e.g. a wrapper around a fragment of a
+        reference function body, read from the reference at run time)."""
+        self.parse_top(self.pp.process(text, fname), fname)
+
     # ---- top level ----
     def parse_top(self, toks, fname):
         i = 0
@@ -2105,6 +2110,23 @@ class TU:
             (af, at), = A
             rt = INT if name == "abs" else LONG
             return (lambda fr: rt.wrap(abs(af(fr)))), rt
+        if name in ("qsort",):
+            # glibc qsort on the <= 4-element arrays the reference sorts is an
+            # insertion sort (stable); the same here, through the comparator
+            (bf, _), (nf, _), _, (cf, _) = A
+
+            def f(fr):
+                p, n, cmp = bf(fr), nf(fr), cf(fr)
+                cells = p.buf
+                for i in range(1, n):
+                    k = i
+                    while k > 0 and cmp(Pointer(cells, p.off + k - 1, p.ty),
+                                        Pointer(cells, p.off + k, p.ty)) > 0:
+                        cells[p.off + k - 1], cells[p.off + k] = \
+                            cells[p.off + k], cells[p.off + k - 1]
+                        k -= 1
+                return None
+            return f, VOID
         if name in ("assert",):
             return (lambda fr: None), VOID
         if name in ("fprintf", "printf", "fflush"):

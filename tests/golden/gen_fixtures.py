@@ -1694,10 +1694,173 @@ def gen_txfeat():
     np.savez_compressed(os.path.join(HERE, "fix_txfeat.npz"), **out)
 
 
+TPLMV_CASES = [  # (tpl_sf.search_method, reduce_first_step_size, use_downsampled_sad,
+                 #  prune_starting_mv, skip_alike_starting_mv)
+    ("FAST_BIGDIA", 6, 0, 3, 2),   # speed >= 5 (speed_features.c:1212-1216)
+    ("FAST_BIGDIA", 6, 1, 2, 2),
+    ("DIAMOND", 6, 0, 1, 1),
+    ("BIGDIA", 0, 0, 0, 0),
+]
+
+
+def tplmv_fragment(tu):
+    """mode_estimation's per-reference start-mv selection and search
+    (av1/encoder/tpl_model.c, from `int_mv best_rfidx_mv = { 0 };` up to the
+    store into tpl_stats->mv[rf_idx]), read from the reference and wrapped in
+    a function whose parameters are the locals that code uses; returns the
+    tpl mv and the (pruned) centre list."""
+    with open(os.path.join(REF, "av1/encoder/tpl_model.c")) as fh:
+        lines = fh.read().split("\n")
+    a = next(i for i, l in enumerate(lines) if "int_mv best_rfidx_mv = { 0 };" in l)
+    b = next(i for i, l in enumerate(lines)
+             if i > a and "tpl_stats->mv[rf_idx].as_int = best_rfidx_mv.as_int;" in l)
+    body = "\n".join(lines[a:b])
+    text = ("void lavish_tplmv_fragment(AV1_COMP *cpi, MACROBLOCK *x, TplDepFrame *tpl_frame, "
+            "TplParams *tpl_data, const GF_GROUP *gf_group, int frame_offset, "
+            "uint8_t block_mis_log2, int mi_row, int mi_col, int mi_height, int mi_width, "
+            "int rf_idx, BLOCK_SIZE bsize, uint8_t *src_mb_buffer, int src_stride, "
+            "uint8_t *ref_mb, int ref_stride, int_mv *result, int *n_centers, "
+            "int *centers_out) {\n  MACROBLOCKD *xd = &x->e_mbd;\n  AV1_COMMON *cm = &cpi->common;\n" + body +
+            "\n  result->as_int = best_rfidx_mv.as_int;\n  *n_centers = refmv_count;\n"
+            "  for (int q = 0; q < 4; ++q) {\n"
+            "    centers_out[3 * q] = center_mvs[q].mv.as_mv.row;\n"
+            "    centers_out[3 * q + 1] = center_mvs[q].mv.as_mv.col;\n"
+            "    centers_out[3 * q + 2] = center_mvs[q].sad;\n  }\n}\n")
+    tu.add_source(text, "<tpl_model.c:%d-%d>" % (a + 1, b))
+
+
+def gen_tplmv():
+    """The TPL start-mv candidates and per-centre motion search
+    (mode_estimation, av1/encoder/tpl_model.c:640-743 executed from the
+    reference text via tplmv_fragment, with motion_estimation :249-303,
+    av1_full_pixel_search and av1_find_best_sub_pixel_tree_pruned_more at
+    subpel_force_stop FULL_PEL) over every 16x16 block of a small frame pair,
+    in raster order with the tpl mvs stored back as tpl_model_store does,
+    for four tpl_sf settings.  The third-pass candidate (needs a
+    third_pass_ctx) is not exercised here."""
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(HERE)), "aom-av1-lavish_amd"))
+    import lavish_dsp.synth as synth
+    tu = C.TU(REF, ["aom_dsp/sad.c", "aom_dsp/variance.c", "av1/encoder/mcomp.c",
+                    "av1/encoder/tpl_model.c"], C.reference_defines(REF))
+    tplmv_fragment(tu)
+    check_errors(tu, ["lavish_tplmv_fragment", "motion_estimation", "av1_full_pixel_search",
+                      "av1_find_best_sub_pixel_tree_pruned_more", "av1_init_dsmotion_compensation",
+                      "av1_init_motion_compensation_bigdia", "av1_set_mv_limits", "compare_sad",
+                      "is_alike_mv", "av1_tpl_ptr_pos"])
+    E = tu.enums
+    W, H, BORDER, MVB, NREF = 96, 64, 96, 32, 2
+    out = nmv_cost_tables()
+    src_np, refs_np = synth.tpl_motion_planes(W, H, NREF, BORDER, seed=2718)
+    stride = src_np.shape[1]
+    out["src"], out["refs"] = src_np, refs_np
+    out["geom"] = np.array([W, H, BORDER, MVB, NREF], np.int32)
+    src_buf = tu.buffer("uint8_t", src_np.reshape(-1).tolist())
+    ref_bufs = [tu.buffer("uint8_t", r.reshape(-1).tolist()) for r in refs_np]
+    org = BORDER * stride + BORDER
+    cols, rows = W // 16, H // 16
+    mi_params = tu.struct_obj("CommonModeInfoParams")
+    mi_cols = ((W + 7) & ~7) // 4
+    _set(mi_params.buf[0], mi_rows=((H + 7) & ~7) // 4, mi_cols=mi_cols)
+    fn = tu.func
+    bsize = E["BLOCK_16X16"]
+    allow_hp = 1
+    qindex, rdmult = 100, 1800
+    sad_per_bit = 4  # (an input of the search; av1_set_sad_per_bit gives 4 near qindex 100)
+    error_per_bit = max(rdmult >> 6, 1)  # av1_set_error_per_bit (rd.h:305-307)
+    recs = []
+    for ci, (mname, rfs, skip, prune, alike) in enumerate(TPLMV_CASES):
+        cpi = tu.struct_obj("AV1_COMP")
+        CP = cpi.buf[0]
+        ppi = tu.struct_obj("AV1_PRIMARY")
+        _set(CP, ppi=ppi)
+        vt = _get(ppi.buf[0], "fn_ptr")[bsize]
+        _set(vt, sdf=fn("aom_sad16x16"), sdsf=fn("aom_sad_skip_16x16"), vf=fn("aom_variance16x16"),
+             sdx4df=fn("aom_sad16x16x4d"), sdx3df=fn("aom_sad16x16x3d"),
+             sdsx4df=fn("aom_sad_skip_16x16x4d"), svf=fn("aom_sub_pixel_variance16x16"))
+        sf = _get(CP, "sf")
+        _set(_get(sf, "tpl_sf"), prune_starting_mv=prune, skip_alike_starting_mv=alike,
+             reduce_first_step_size=rfs, search_method=E[mname], subpel_force_stop=E["FULL_PEL"])
+        _set(_get(sf, "mv_sf"), search_method=E["DIAMOND"], use_bsize_dependent_search_method=0,
+             use_downsampled_sad=skip, subpel_search_method=E["SUBPEL_TREE_PRUNED_MORE"],
+             use_fullpel_costlist=1, subpel_force_stop=E["EIGHTH_PEL"], subpel_iters_per_step=1,
+             use_accurate_subpel_search=E["USE_2_TAPS"], exhaustive_searches_thresh=0,
+             prune_mesh_search=0, obmc_full_pixel_search_level=0)
+        msp = _get(CP, "mv_search_params")
+        cfgs = _get(msp, "search_site_cfg")  # [SS_CFG_TOTAL][NUM_DISTINCT_SEARCH_METHODS], flat
+        nd = E["NUM_DISTINCT_SEARCH_METHODS"]
+        sct = tu.ctype("search_site_config")
+        for cfg_i in range(E["SS_CFG_TOTAL"]):
+            fn("av1_init_dsmotion_compensation")(C.Pointer(cfgs, cfg_i * nd + E["DIAMOND"], sct),
+                                                 stride, 0)
+            fn("av1_init_motion_compensation_bigdia")(
+                C.Pointer(cfgs, cfg_i * nd + E["BIGDIA"], sct), stride, 0)
+        _set(msp, find_fractional_mv_step=fn("av1_find_best_sub_pixel_tree_pruned_more"))
+        _set(_get(_get(CP, "common"), "features"), allow_high_precision_mv=allow_hp)
+        # x: mv costs (the default context's hp tables), error / sad per bit
+        x = tu.struct_obj("MACROBLOCK")
+        X = x.buf[0]
+        mvcosts = tu.struct_obj("MvCosts")
+        MC = mvcosts.buf[0]
+        _get(MC, "nmv_joint_cost")[:] = [int(v) for v in out["mvjcost_hp"]]
+        mc = [tu.buffer("int", out["mvcost_hp"][k].tolist()) for k in range(2)]
+        nmv = _get(MC, "nmv_cost")
+        nmv[0], nmv[1] = (C.Pointer(c.buf, MV_MAX, c.ty) for c in mc)
+        _set(MC, mv_cost_stack=C.Pointer(nmv, 0, C.Ptr(tu.ctype("int"))))
+        _set(X, mv_costs=mvcosts, errorperbit=error_per_bit, sadperbit=sad_per_bit, qindex=qindex)
+        xd = _get(X, "e_mbd")
+        mbmi = tu.struct_obj("MB_MODE_INFO")
+        scf = tu.struct_obj("struct scale_factors")
+        _set(scf.buf[0], x_scale_fp=1 << 14, y_scale_fp=1 << 14)
+        _set(xd, mi=C.Pointer([mbmi], 0, C.Ptr(tu.ctype("MB_MODE_INFO"))))
+        _get(xd, "block_ref_scale_factors")[0] = scf
+        _set(_get(xd, "tile"), mi_col_start=0, mi_col_end=mi_cols, mi_row_start=0,
+             mi_row_end=((H + 7) & ~7) // 4)
+        # this frame's tpl stats (tpl_model_store's slot per 16x16 block)
+        stats = tu.buffer("TplDepStats", rows * cols)
+        tpl_frame = tu.struct_obj("TplDepFrame")
+        _set(tpl_frame.buf[0], tpl_stats_ptr=stats, stride=cols)
+        tpl_data = tu.struct_obj("TplParams")
+        for k in range(NREF):
+            for r in range(rows):
+                for c in range(cols):
+                    mi_row, mi_col = 4 * r, 4 * c
+                    _set(xd, up_available=int(r > 0), left_available=int(c > 0))
+                    lim = tu.struct_obj("FullMvLimits")
+                    fn("av1_set_mv_limits")(mi_params, lim, mi_row, mi_col, 4, 4, MVB)
+                    _set(X, mv_limits=C.copy_obj(lim.buf[0]))
+                    off = org + 16 * r * stride + 16 * c
+                    res = tu.struct_obj("int_mv")
+                    ncen = tu.buffer("int", 1)
+                    cens = tu.buffer("int", 12)
+                    fn("lavish_tplmv_fragment")(
+                        cpi, x, tpl_frame, tpl_data, None, 0, 2, mi_row, mi_col, 4, 4, k, bsize,
+                        C.Pointer(src_buf.buf, off, C.UCHAR), stride,
+                        C.Pointer(ref_bufs[k].buf, off, C.UCHAR), stride, res, ncen, cens)
+                    mv = _get(C.union_member(res.buf[0], 1), "as_mv")
+                    mvr, mvc = _get(mv, "row"), _get(mv, "col")
+                    # tpl_model_store: tpl_stats->mv[rf_idx] of this block
+                    st = stats.buf[r * cols + c]
+                    smv = _get(st, "mv")[k]
+                    C.union_member(smv, 1)
+                    _set(_get(smv, "as_mv"), row=mvr, col=mvc)
+                    L = lim.buf[0]
+                    recs.append([ci, k, r, c, mvr, mvc, ncen.buf[0]] + list(cens.buf) +
+                                [_get(L, f) for f in ("col_min", "col_max", "row_min", "row_max")])
+            print("  tplmv case %d ref %d: %d blocks" % (ci, k, len(recs)))
+    out["recs"] = np.array(recs, np.int64)
+    out["rec_fields"] = np.array(["case", "ref", "row", "col", "mv_row", "mv_col", "n_centers"] +
+                                 ["c%d_%s" % (q, f) for q in range(4) for f in ("row", "col", "sad")] +
+                                 ["col_min", "col_max", "row_min", "row_max"])
+    out["cases"] = np.array([[E[m], rfs, sk, pr, al] for m, rfs, sk, pr, al in TPLMV_CASES],
+                            np.int32)
+    out["params"] = np.array([qindex, rdmult, sad_per_bit, error_per_bit, allow_hp], np.int32)
+    np.savez_compressed(os.path.join(HERE, "fix_tplmv.npz"), **out)
+
+
 def main(argv):
     sections = argv or ["txfm", "qparams", "quant", "inv", "pixel", "wht", "nmv", "mcomp",
                         "subpel", "tpl", "qfacade", "costcoeffs", "trellis", "warp", "compound",
-                        "convolve", "compound12", "txfeat", "trellis2"]
+                        "convolve", "compound12", "txfeat", "trellis2", "tplmv"]
     t0 = time.time()
     ttx = None
     if "txfm" in sections or "inv" in sections or "wht" in sections:
@@ -1746,6 +1909,8 @@ def main(argv):
         gen_txfeat()
     if "trellis2" in sections:
         gen_trellis(dict(np.load(os.path.join(HERE, "fix_txfm.npz"))), sharpness=2)
+    if "tplmv" in sections:
+        gen_tplmv()
     print("done in %.0fs" % (time.time() - t0))
 
 

@@ -87,16 +87,22 @@ def test_tpl_block_batch_rejects(T):
         T.tpl_block_batch(src, src, 4, 8, qp)
 
 
-def test_tpl_frame_chain_vs_oracle(T):
-    """TplFrame.step (four kernels chained on one stream) against the same
-    chain of oracles on a 320x192 frame with 3 references."""
+@pytest.mark.parametrize("neighbours", [True, False])
+def test_tpl_frame_chain_vs_oracle(T, neighbours):
+    """TplFrame.step (the kernels chained on one stream) against the same
+    chain of oracles on a 320x192 frame with 3 references: the full-pel step
+    with the reference's neighbour-seeded start mvs (the default,
+    orc_tpl_motion_search) or from the zero mv."""
     import torch
     import lavish_dsp.inter as I
     import lavish_dsp.motion as M
     import lavish_dsp.synth as synth
     W, H, R, border, qindex, rdmult = 320, 192, 3, 288, 110, 1500
-    src, refs = synth.motion_planes(W, H, R, border, seed=77)
-    tf = T.TplFrame(src, refs, W, H, border, qindex, rdmult)
+    if neighbours:
+        src, refs = synth.tpl_motion_planes(W, H, R, border, seed=77)
+    else:
+        src, refs = synth.motion_planes(W, H, R, border, seed=77)
+    tf = T.TplFrame(src, refs, W, H, border, qindex, rdmult, neighbour_starts=neighbours)
     out = tf.step()
     torch.cuda.synchronize()
     got = T.records_numpy(out)
@@ -104,11 +110,20 @@ def test_tpl_frame_chain_vs_oracle(T):
     gcost = tf.costs.cpu().numpy()
     st = src.shape[1]
     mvj, mvc = M.default_mv_cost_tables(tf.allow_hp)
-    fp, cl = O.full_pixel_search_batch(src.reshape(-1), refs.reshape(-1), st, 16, 16, tf.jobs_np,
-                                       "fast_bigdia", 6, 0, M.sad_per_bit(qindex),
-                                       M.error_per_bit(rdmult), mvj, mvc, cost_list=True,
-                                       threads=8)
-    sj = M.subpel_jobs(W, H, border, 16, 16, tf.jobs_np, fp)
+    spb, epb = M.sad_per_bit(qindex), M.error_per_bit(rdmult)
+    if neighbours:
+        assert T.tpl_motion_failures(tf.mv_out) == 0
+        _, fp, cl, _ = O.tpl_motion_search(src.reshape(-1), refs.reshape(-1), st, tf.jobs_np,
+                                           W // 16, H // 16, R, "fast_bigdia", 6, False, 3, 2,
+                                           spb, epb, mvj, mvc, 0)
+    else:
+        fp, cl = O.full_pixel_search_batch(src.reshape(-1), refs.reshape(-1), st, 16, 16,
+                                           tf.jobs_np, "fast_bigdia", 6, 0, spb, epb, mvj, mvc,
+                                           cost_list=True, threads=8)
+    gfp = M.results_numpy(tf.fp)
+    np.testing.assert_array_equal(gfp["best_row"], fp["best_row"])
+    np.testing.assert_array_equal(gfp["best_col"], fp["best_col"])
+    sj = M.subpel_jobs(W, H, T.TPL_BORDER, 16, 16, tf.jobs_np, fp)
     sub = O.subpel_search_batch(src.reshape(-1), refs.reshape(-1), st, 16, 16, sj, 2, M.FULL_PEL,
                                 tf.allow_hp, 1, M.MV_COST_NONE, 0, None, None, cl, threads=8)
     np.testing.assert_array_equal(M.subpel_results_numpy(tf.sub)["best_row"], sub["best_row"])

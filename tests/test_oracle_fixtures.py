@@ -533,3 +533,52 @@ def test_optimize_b_sharpness2_matches_reference():
         np.testing.assert_array_equal(dq, F["dqcoeff"][i][:n], err_msg=msg)
         changed += int((qc != F["qcoeff_in"][i][:n]).any())
     assert changed > len(F["rows"]) // 4, changed
+
+
+SEARCH_METHOD_NAMES = {0: "diamond", 5: "bigdia", 8: "fast_diamond", 9: "fast_bigdia",
+                       10: "vfast_diamond"}
+
+
+def tplmv_case_inputs(F, ci):
+    """Jobs and search settings of fix_tplmv case ci (the fixture's frame)."""
+    import lavish_dsp.motion as M
+    W, H, border, mvb, nref = (int(v) for v in F["geom"])
+    src = F["src"]
+    jobs = M.frame_jobs(W, H, src.shape[1], border, src.size, 16, 16, nref, mv_border=mvb)
+    meth, rfs, skip, prune, alike = (int(v) for v in F["cases"][ci])
+    return jobs, (SEARCH_METHOD_NAMES[meth], rfs, bool(skip), prune, alike), (W // 16, H // 16,
+                                                                            nref)
+
+
+def test_tpl_motion_search_matches_reference():
+    """orc_tpl_motion_search against mode_estimation's start-mv selection and
+    per-centre motion_estimation executed from the reference text
+    (fix_tplmv.npz: every block of a 96x64 frame x 2 references, four tpl_sf
+    settings): the tpl mv of every block, the mv limits, and the winning centre
+    is one of the reference's (pruned) centres."""
+    import lavish_dsp.tpl as T
+    F = _load("fix_tplmv.npz")
+    fld = {n: i for i, n in enumerate(F["rec_fields"])}
+    recs = F["recs"]
+    qindex, rdmult, spb, epb, allow_hp = (int(v) for v in F["params"])
+    for ci in range(len(F["cases"])):
+        jobs, (meth, sp, skip, prune, alike), (cols, rows, nref) = tplmv_case_inputs(F, ci)
+        rc = recs[recs[:, fld["case"]] == ci]
+        assert len(rc) == len(jobs)
+        for f in ("col_min", "col_max", "row_min", "row_max"):
+            np.testing.assert_array_equal(jobs[f], rc[:, fld[f]], err_msg=f)
+        mvs, fp, cl, cen = O.tpl_motion_search(
+            F["src"].reshape(-1), F["refs"].reshape(-1), F["src"].shape[1], jobs, cols, rows,
+            nref, meth, sp, skip, prune, alike, spb, epb, F["mvjcost_hp"], F["mvcost_hp"], 0)
+        r, c = T.unpack_mv(mvs)
+        msg = "case %d" % ci
+        np.testing.assert_array_equal(r, rc[:, fld["mv_row"]], err_msg=msg)
+        np.testing.assert_array_equal(c, rc[:, fld["mv_col"]], err_msg=msg)
+        cr, cc = T.unpack_mv(cen)
+        for i in range(len(rc)):
+            n = int(rc[i, fld["n_centers"]])
+            opts = {(int(rc[i, fld["c%d_row" % q]]), int(rc[i, fld["c%d_col" % q]]))
+                    for q in range(n)}
+            assert (int(cr[i]), int(cc[i])) in opts, (msg, i)
+        # the neighbours matter in this content: some searches start off zero
+        assert np.count_nonzero(cen) > 0, msg
