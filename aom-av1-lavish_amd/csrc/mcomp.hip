@@ -1382,14 +1382,15 @@ __device__ void lj_pass(const Ctx& c, const LjSrc& s, int l, bool run, int step_
   }
 }
 
-__global__ __launch_bounds__(256, 4) void diamond_lj_kernel(
+// one group of 4 x 8 jobs: virtual workgroup vwg of nvwg (a multiple of 8)
+__device__ __forceinline__ void lj_group(
     const uint8_t* __restrict__ src, int ss, const uint8_t* __restrict__ ref, int rs,
-    LavishRefTiles tiles, const Job* __restrict__ jobs, int njobs, int step_param,
-    LavishMvCostParams cost, int skip, LavishDiamondResult* __restrict__ out,
-    int32_t* __restrict__ cost_lists) {
+    const LavishRefTiles& tiles, const Job* __restrict__ jobs, int njobs, int step_param,
+    const LavishMvCostParams& cost, int skip, LavishDiamondResult* __restrict__ out,
+    int32_t* __restrict__ cost_lists, int vwg, int nvwg) {
+  __shared__ uint32_t res_s[4][kLjJobs][kMaxSteps];  // (LDS-addressed, not through a pointer)
   // XCD-aware: consecutive job groups (neighbouring blocks) share an XCD's L2
-  const int nwg = gridDim.x;  // multiple of 8
-  const int wg = (blockIdx.x & 7) * (nwg >> 3) + (blockIdx.x >> 3);
+  const int wg = (vwg & 7) * (nvwg >> 3) + (vwg >> 3);
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   const int jg = lane >> 3, l = lane & 7;
@@ -1397,7 +1398,6 @@ __global__ __launch_bounds__(256, 4) void diamond_lj_kernel(
   if (j0 >= njobs) return;
   const int j = min(j0 + jg, njobs - 1);  // a surplus group repeats the last job, never stores
   const bool mine_job = j0 + jg < njobs;
-  __shared__ uint32_t res_s[4][kLjJobs][kMaxSteps];
   uint32_t* res = res_s[wave][jg];
   const Job jb = jobs[j];
   Ctx c;
@@ -1474,6 +1474,27 @@ __global__ __launch_bounds__(256, 4) void diamond_lj_kernel(
   }
 }
 
+// nvwg virtual workgroups over gridDim.x (<= nvwg, both multiples of 8, so a
+// virtual workgroup runs on the XCD of its first): with a smaller grid the
+// search holds fewer CU slots while a concurrent leg runs beside it
+__global__ __launch_bounds__(256, 4) void diamond_lj_kernel(
+    const uint8_t* __restrict__ src, int ss, const uint8_t* __restrict__ ref, int rs,
+    LavishRefTiles tiles, const Job* __restrict__ jobs, int njobs, int step_param,
+    LavishMvCostParams cost, int skip, LavishDiamondResult* __restrict__ out,
+    int32_t* __restrict__ cost_lists, int nvwg) {
+  for (int v = blockIdx.x; v < nvwg; v += gridDim.x)
+    lj_group(src, ss, ref, rs, tiles, jobs, njobs, step_param, cost, skip, out, cost_lists, v,
+             nvwg);
+}
+
+static int lj_grid_cap() {  // LAVISH_C3_WGS=n: at most n workgroups (rounded to 8)
+  static const int cap = [] {
+    const char* e = getenv("LAVISH_C3_WGS");
+    return e == nullptr ? 0 : (atoi(e) + 7) & ~7;
+  }();
+  return cap;
+}
+
 static bool lj_enabled() {  // LAVISH_DIAMOND_LJ=0: the one-job-per-wave kernel (A/B)
   static const bool on = [] {
     const char* e = getenv("LAVISH_DIAMOND_LJ");
@@ -1510,8 +1531,11 @@ void launch(const uint8_t* src, int ss, const uint8_t* ref, int rs, const Lavish
         if (method == kDiamond && lj_enabled()) {  // eight jobs per wave
           const int waves = (njobs + kLjJobs - 1) / kLjJobs;
           const int nwg = (((waves + 3) / 4) + 7) & ~7;
-          hipLaunchKernelGGL(diamond_lj_kernel, dim3(nwg), dim3(256), 0, s, src, ss, ref, rs, *t,
-                             (const Job*)jobs, njobs, step_param, cost, skip, out, cost_lists);
+          const int cap = lj_grid_cap();
+          const int grid = cap > 0 && cap < nwg ? cap : nwg;
+          hipLaunchKernelGGL(diamond_lj_kernel, dim3(grid), dim3(256), 0, s, src, ss, ref, rs,
+                             *t, (const Job*)jobs, njobs, step_param, cost, skip, out, cost_lists,
+                             nwg);
           return;
         }
       }
@@ -1525,34 +1549,49 @@ void launch(const uint8_t* src, int ss, const uint8_t* ref, int rs, const Lavish
                          out, cost_lists, s);
 }
 
-// LavishRefTiles copy: one thread per 16-byte half of a 32-byte strip row
-// (strip k, field row fy, field f = bytes [16k + 16 half, +16) of buffer row
-// 2 fy + f); bytes past the row end or past the last row are zero
+// LavishRefTiles copy through LDS, both sides coalesced: a workgroup takes
+// field f, strips [k0, k0 + 8) and field rows [fy0, fy0 + 32): it reads the
+// 32 source rows' 144-byte segments (the 8 strips + the 16 bytes the last
+// strip row overlaps into) as 16-byte chunks, then writes the 8 strips' 1 KB
+// runs (32 field rows x 32 bytes each).  Bytes past the row end or past the
+// last row are zero.
+constexpr int kTilesK = 8, kTilesF = 32, kTilesC = kTilesK + 1;  // chunks per row segment
 __global__ __launch_bounds__(256) void ref_tiles_kernel(const uint8_t* __restrict__ ref,
                                                         int stride, int rows, int nstrips,
                                                         int fh, uint8_t* __restrict__ out,
-                                                        int64_t nchunks) {
-  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (i >= nchunks) return;
-  const int half = (int)(i & 1);
-  const int64_t rowi = i >> 1;                   // (f * nstrips + k) * fh + fy
-  const int fy = (int)(rowi % fh);
-  const int64_t fk = rowi / fh;
-  const int k = (int)(fk % nstrips), f = (int)(fk / nstrips);
-  const int y = 2 * fy + f, x = 16 * k + 16 * half;
-  u32x4 v = {0u, 0u, 0u, 0u};
-  if (y < rows) {
-    const uint8_t* p = ref + (int64_t)y * stride + x;
-    if (x + 16 <= stride) {
-      const u32x4u w = *(const __attribute__((address_space(1))) u32x4u*)p;
-      v = u32x4{w.x, w.y, w.z, w.w};
-    } else {
-      uint32_t b[4] = {0u, 0u, 0u, 0u};
-      for (int j = 0; j < 16 && x + j < stride; ++j) b[j >> 2] |= (uint32_t)p[j] << (8 * (j & 3));
-      v = u32x4{b[0], b[1], b[2], b[3]};
+                                                        int ktiles, int ftiles) {
+  __shared__ u32x4 seg[kTilesF][kTilesC];
+  const int t = threadIdx.x;
+  int b = blockIdx.x;
+  const int kt = b % ktiles;
+  b /= ktiles;
+  const int ft = b % ftiles;
+  const int f = b / ftiles;
+  const int k0 = kt * kTilesK, fy0 = ft * kTilesF;
+  for (int idx = t; idx < kTilesF * kTilesC; idx += 256) {
+    const int i = idx / kTilesC, m = idx - i * kTilesC;
+    const int y = 2 * (fy0 + i) + f, x = 16 * (k0 + m);
+    u32x4 v = {0u, 0u, 0u, 0u};
+    if (y < rows && x < stride) {
+      const uint8_t* p = ref + (int64_t)y * stride + x;
+      if (x + 16 <= stride) {
+        const u32x4u w = *(const __attribute__((address_space(1))) u32x4u*)p;
+        v = u32x4{w.x, w.y, w.z, w.w};
+      } else {
+        uint32_t q[4] = {0u, 0u, 0u, 0u};
+        for (int j = 0; j < 16 && x + j < stride; ++j) q[j >> 2] |= (uint32_t)p[j] << (8 * (j & 3));
+        v = u32x4{q[0], q[1], q[2], q[3]};
+      }
     }
+    seg[i][m] = v;
   }
-  *(u32x4*)(out + 16 * i) = v;
+  __syncthreads();
+  for (int q = t; q < kTilesK * kTilesF * 2; q += 256) {
+    const int kk = q >> 6, i = (q >> 1) & (kTilesF - 1), h = q & 1;
+    const int k = k0 + kk, fy = fy0 + i;
+    if (k < nstrips && fy < fh)
+      *(u32x4*)(out + ((((int64_t)f * nstrips + k) * fh + fy) << 5) + 16 * h) = seg[i][kk + h];
+  }
 }
 
 }  // namespace
@@ -1685,9 +1724,9 @@ extern "C" int lavish_ref_tiles_build(const uint8_t* ref, int stride, int rows, 
   tiles->field_bytes = (int64_t)nstrips * fh * 32;
   tiles->field_rows = fh;
   tiles->stride = stride;
-  const int64_t nchunks = bytes / 16;
-  hipLaunchKernelGGL(ref_tiles_kernel, dim3((unsigned)((nchunks + 255) / 256)), dim3(256), 0,
-                     (hipStream_t)stream, ref, stride, rows, nstrips, fh, data, nchunks);
+  const int ktiles = (nstrips + kTilesK - 1) / kTilesK, ftiles = (fh + kTilesF - 1) / kTilesF;
+  hipLaunchKernelGGL(ref_tiles_kernel, dim3((unsigned)(2 * ktiles * ftiles)), dim3(256), 0,
+                     (hipStream_t)stream, ref, stride, rows, nstrips, fh, data, ktiles, ftiles);
   LAVISH_CHECK(hipGetLastError());
   return 0;
 }
