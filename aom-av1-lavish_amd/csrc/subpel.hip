@@ -26,10 +26,27 @@
 // each), applies the two bilinear passes with the reference's rounding and
 // accumulates (sum, sse); wave sums end in SGPRs and the sequential
 // check_better_fast updates run on the scalar unit in the reference's order.
+//
+// SUBPEL_TREE with subpel_search_type USE_4_TAPS / USE_8_TAPS takes the
+// upsampled prediction's error instead (check_better -> upsampled_pref_error,
+// mcomp.c:2402-2491,2528-2551 -> aom_upsampled_pred_c, reconinter_enc.c:
+// 424-496, unscaled): per candidate the 8-tap-layout kernel row of
+// av1_get_filter (filter.h:276-285) at phase 2 * q3, aom_convolve8_horiz_c /
+// _vert_c (aom_dsp/aom_convolve.c:36-73: round by FILTER_BITS, clip to 8
+// bits; the 2-D case filters rows -3 .. +4 horizontally first), then vf.
+// Each lane computes its 4-pixel segments' prediction from the 8 x 12 source
+// bytes around them.  USE_2_TAPS is the bilinear kernel through the same
+// passes, which is the svf's arithmetic exactly (same weights, same rounding,
+// no clipping possible): it takes the svf path.
+#include "interp_kernels.h"
 #include "lavish_internal.h"
 
 namespace lavish {
 namespace {
+
+// [kind][phase][tap] (interp_kernels.h): 0 the 8-tap regular, 4 the 4-tap
+// regular kernels (av1_get_filter's USE_8_TAPS / USE_4_TAPS)
+__constant__ int16_t kUpK[6][16][8] = LAVISH_K8_INIT;
 
 struct SJob {
   int64_t src_off, ref_off;
@@ -82,6 +99,7 @@ struct SpCtx {
   int ref_mv_row, ref_mv_col;
   int col_min, col_max, row_min, row_max;
   int lambda;  // mv_err_cost_ L1 lambda (0: MV_COST_NONE)
+  int up_kind;  // -1: the bilinear svf error; else kUpK kind of the upsampled error
   bool entropy;
   int error_per_bit;
   const int32_t* mvjcost;
@@ -122,11 +140,112 @@ __device__ __forceinline__ void seg4(const SpCtx& c, const uint8_t* base, int y,
   }
 }
 
+// 12 consecutive bytes at p as three dwords (dword-aligned loads + alignbyte)
+__device__ __forceinline__ void load12(const uint8_t* p, uint32_t (&d)[3]) {
+  typedef const __attribute__((address_space(1))) uint32_t* gptr;
+  const uintptr_t a = (uintptr_t)p;
+  const gptr q = (gptr)(a & ~(uintptr_t)3);
+  const uint32_t sh = (uint32_t)(a & 3);
+  const uint32_t w0 = q[0], w1 = q[1], w2 = q[2], w3 = q[3];
+  d[0] = __builtin_amdgcn_alignbyte(w1, w0, sh);
+  d[1] = __builtin_amdgcn_alignbyte(w2, w1, sh);
+  d[2] = __builtin_amdgcn_alignbyte(w3, w2, sh);
+}
+__device__ __forceinline__ int byte_at(const uint32_t (&d)[3], int i) {
+  return (d[i >> 2] >> (8 * (i & 3))) & 0xFF;
+}
+__device__ __forceinline__ int clip8(int v) { return min(max(v, 0), 255); }
+
+// aom_convolve8_horiz of 4 pixels: src bytes p[-3 .. 7]
+__device__ __forceinline__ void hconv4(const uint8_t* p, const int (&k)[8], int (&o)[4]) {
+  uint32_t d[3];
+  load12(p - 3, d);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    int sum = 0;
+#pragma unroll
+    for (int t = 0; t < 8; ++t) sum += byte_at(d, i + t) * k[t];
+    o[i] = clip8((sum + 64) >> 7);  // ROUND_POWER_OF_TWO(sum, FILTER_BITS), clip_pixel
+  }
+}
+
+// (sum, sse) of src - upsampled(ref at mv) over this lane's segments
+template <int W, int H>
+__device__ __noinline__ void seg_err_up(const SpCtx& c, const uint32_t (&sv)[Sp<W, H>::NS],
+                                        int lane, int row, int col, int& sum, uint32_t& sse) {
+  using S = Sp<W, H>;
+  const int sx = col & 7, sy = row & 7;
+  int kx[8], ky[8];
+#pragma unroll
+  for (int t = 0; t < 8; ++t) {
+    kx[t] = kUpK[c.up_kind][2 * sx][t];
+    ky[t] = kUpK[c.up_kind][2 * sy][t];
+  }
+  const uint8_t* base = c.ref + (int64_t)(row >> 3) * c.rs + (col >> 3);
+  auto segment = [&](int sg, uint32_t sw) {
+    const int y = sg / S::SPR, x = 4 * (sg % S::SPR);
+    const uint8_t* p = base + (int64_t)y * c.rs + x;
+    int v[4];
+    if (sx == 0 && sy == 0) {
+      uint32_t d[3];
+      load12(p, d);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) v[i] = byte_at(d, i);
+    } else if (sy == 0) {
+      hconv4(p, kx, v);
+    } else if (sx == 0) {
+      int acc[4] = {0, 0, 0, 0};
+#pragma unroll
+      for (int t = 0; t < 8; ++t) {
+        uint32_t d[3];
+        load12(p + (int64_t)(t - 3) * c.rs, d);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) acc[i] += byte_at(d, i) * ky[t];
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) v[i] = clip8((acc[i] + 64) >> 7);
+    } else {
+      int acc[4] = {0, 0, 0, 0};
+#pragma unroll
+      for (int t = 0; t < 8; ++t) {
+        int h[4];
+        hconv4(p + (int64_t)(t - 3) * c.rs, kx, h);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) acc[i] += h[i] * ky[t];
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) v[i] = clip8((acc[i] + 64) >> 7);
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int d = v[i] - (int)((sw >> (8 * i)) & 0xFF);
+      sum += d;
+      sse += (uint32_t)(d * d);
+    }
+  };
+  if constexpr (S::kCache) {
+#pragma unroll
+    for (int n = 0; n < S::NS; ++n)
+      if (lane + 64 * n < S::SEG) segment(lane + 64 * n, sv[n]);
+  } else {
+#pragma unroll 1
+    for (int sg = lane; sg < S::SEG; sg += 64) {
+      uint32_t d[3];
+      load12(c.src + (int64_t)(sg / S::SPR) * c.ss + 4 * (sg % S::SPR), d);
+      segment(sg, d[0]);
+    }
+  }
+}
+
 // (sum, sse) of src - bilinear(ref at mv) over this lane's segments
 template <int W, int H>
 __device__ __forceinline__ void seg_err(const SpCtx& c, const uint32_t (&sv)[Sp<W, H>::NS],
                                         int lane, int row, int col, int& sum, uint32_t& sse) {
   using S = Sp<W, H>;
+  if (c.up_kind >= 0) {
+    seg_err_up<W, H>(c, sv, lane, row, col, sum, sse);
+    return;
+  }
   const int xo = col & 7, yo = row & 7;
   const int f0 = kBil2t[xo][0], f1 = kBil2t[xo][1];
   const int g0 = kBil2t[yo][0], g1 = kBil2t[yo][1];
@@ -280,7 +399,8 @@ __global__ __launch_bounds__(256) void subpel_kernel(const uint8_t* __restrict__
                                                      const uint8_t* __restrict__ ref, int rs,
                                                      const SJob* __restrict__ jobs, int njobs,
                                                      const LavishDiamondResult* __restrict__ fp,
-                                                     int method, int forced_stop, int allow_hp,
+                                                     int method, int up_kind,
+                                                     int forced_stop, int allow_hp,
                                                      int iters, LavishMvCostParams cost,
                                                      const int32_t* __restrict__ cost_lists,
                                                      LavishSubpelResult* out) {
@@ -305,6 +425,7 @@ __global__ __launch_bounds__(256) void subpel_kernel(const uint8_t* __restrict__
   c.row_max = jb.row_max;
   // mv_err_cost_ lambdas: SSE_LAMBDA_LOWRES 2, MIDRES 0, HDRES 1; NONE 0
   c.lambda = cost.mv_cost_type == 1 ? 2 : cost.mv_cost_type == 3 ? 1 : 0;
+  c.up_kind = method == 0 ? up_kind : -1;  // only SUBPEL_TREE takes the upsampled error
   c.entropy = cost.mv_cost_type == 0;
   c.error_per_bit = cost.error_per_bit;
   c.mvjcost = cost.mvjcost;
@@ -399,22 +520,25 @@ __global__ __launch_bounds__(256) void subpel_kernel(const uint8_t* __restrict__
 
 template <int W, int H>
 void launch(const uint8_t* src, int ss, const uint8_t* ref, int rs, const LavishSubpelJob* jobs,
-            int njobs, const LavishDiamondResult* fp, int method, int forced_stop, int allow_hp,
-            int iters, const LavishMvCostParams& cost, const int32_t* cost_lists,
+            int njobs, const LavishDiamondResult* fp, int method, int up_kind, int forced_stop,
+            int allow_hp, int iters, const LavishMvCostParams& cost, const int32_t* cost_lists,
             LavishSubpelResult* out, hipStream_t s) {
   int nwg = (njobs + 3) / 4;
   nwg = (nwg + 7) & ~7;
   hipLaunchKernelGGL((subpel_kernel<W, H>), dim3(nwg), dim3(256), 0, s, src, ss, ref, rs,
-                     (const SJob*)jobs, njobs, fp, method, forced_stop, allow_hp, iters, cost,
-                     cost_lists, out);
+                     (const SJob*)jobs, njobs, fp, method, up_kind, forced_stop, allow_hp, iters,
+                     cost, cost_lists, out);
 }
 
 int subpel_batch(const uint8_t* src, int src_stride, const uint8_t* ref, int ref_stride, int w,
                  int h, const LavishSubpelJob* jobs, int njobs, const LavishDiamondResult* fp,
                  int method, int forced_stop, int allow_hp, int iters_per_step,
                  const LavishMvCostParams* cost, const int32_t* cost_lists,
-                 LavishSubpelResult* out, hipStream_t s) {
+                 LavishSubpelResult* out, hipStream_t s, int search_type = 0) {
   if (njobs <= 0) return 0;
+  if (search_type < 0 || search_type > 3) return -7;
+  // USE_2_TAPS_ORIG / USE_2_TAPS: the svf; USE_4_TAPS / USE_8_TAPS: kUpK kind
+  const int up_kind = search_type == 2 ? 4 : search_type == 3 ? 0 : -1;
   if (forced_stop < 0 || forced_stop > 3) return -1;
   if (cost == nullptr || cost->mv_cost_type < 0 || cost->mv_cost_type > 4) return -2;
   if (cost->mv_cost_type == 0 &&
@@ -424,8 +548,8 @@ int subpel_batch(const uint8_t* src, int src_stride, const uint8_t* ref, int ref
   if (method < 0 || method > 2) return -6;  // SUBPEL_TREE (bilinear) / _PRUNED / _PRUNED_MORE
 #define LAVISH_SP_CASE(W, H)                                                                   \
   if (w == W && h == H) {                                                                      \
-    launch<W, H>(src, src_stride, ref, ref_stride, jobs, njobs, fp, method, forced_stop,       \
-                 allow_hp, iters_per_step, *cost, cost_lists, out, s);                         \
+    launch<W, H>(src, src_stride, ref, ref_stride, jobs, njobs, fp, method, up_kind,          \
+                 forced_stop, allow_hp, iters_per_step, *cost, cost_lists, out, s);            \
     LAVISH_CHECK(hipGetLastError());                                                           \
     return 0;                                                                                  \
   }
@@ -481,4 +605,15 @@ extern "C" int lavish_find_best_sub_pixel_tree_batch(
   return subpel_batch(src, src_stride, ref, ref_stride, w, h, jobs, njobs, fullpel,
                       subpel_search_method, forced_stop, allow_hp, iters_per_step, cost,
                       cost_lists, out, (hipStream_t)stream);
+}
+
+extern "C" int lavish_find_best_sub_pixel_tree_batch_ex(
+    const uint8_t* src, int src_stride, const uint8_t* ref, int ref_stride, int w, int h,
+    const LavishSubpelJob* jobs, const LavishDiamondResult* fullpel, int njobs,
+    int subpel_search_method, int subpel_search_type, int forced_stop, int allow_hp,
+    int iters_per_step, const LavishMvCostParams* cost, const int32_t* cost_lists,
+    LavishSubpelResult* out, void* stream) {
+  return subpel_batch(src, src_stride, ref, ref_stride, w, h, jobs, njobs, fullpel,
+                      subpel_search_method, forced_stop, allow_hp, iters_per_step, cost,
+                      cost_lists, out, (hipStream_t)stream, subpel_search_type);
 }

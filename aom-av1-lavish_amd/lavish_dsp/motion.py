@@ -372,13 +372,22 @@ _lib.lavish_find_best_sub_pixel_tree_batch.argtypes = [
     _vp, _i32, _vp, _i32, _i32, _i32, _vp, _vp, _i32, _i32, _i32, _i32, _i32,
     ctypes.POINTER(MvCostParams), _vp, _vp, _vp]
 _lib.lavish_find_best_sub_pixel_tree_batch.restype = _i32
+_lib.lavish_find_best_sub_pixel_tree_batch_ex.argtypes = [
+    _vp, _i32, _vp, _i32, _i32, _i32, _vp, _vp, _i32, _i32, _i32, _i32, _i32, _i32,
+    ctypes.POINTER(MvCostParams), _vp, _vp, _vp]
+_lib.lavish_find_best_sub_pixel_tree_batch_ex.restype = _i32
+# SUBPEL_SEARCH_TYPE (av1/common/filter.h:45-50)
+USE_2_TAPS_ORIG, USE_2_TAPS, USE_4_TAPS, USE_8_TAPS = range(4)
 
 
 def find_best_sub_pixel_tree_batch(src, ref, w, h, jobs, cost, method="pruned_more",
                                    forced_stop=EIGHTH_PEL, allow_hp=False, iters_per_step=1,
-                                   fullpel=None, cost_lists=None, out=None, stream=None):
-    """lavish_find_best_sub_pixel_tree_batch: av1_find_best_sub_pixel_tree
-    ("tree", bilinear error), _pruned or _pruned_more with any mv cost (MvCostParams) and the full-pel cost lists
+                                   fullpel=None, cost_lists=None, out=None, stream=None,
+                                   search_type=USE_2_TAPS_ORIG):
+    """lavish_find_best_sub_pixel_tree_batch_ex: av1_find_best_sub_pixel_tree
+    ("tree"; the bilinear error with search_type USE_2_TAPS_ORIG / USE_2_TAPS,
+    the upsampled prediction's with USE_4_TAPS / USE_8_TAPS), _pruned or
+    _pruned_more with any mv cost (MvCostParams) and the full-pel cost lists
     (device int32 [n, 5] or None); fullpel: device RESULT_DTYPE bytes to start
     from (or None: the jobs' start fields)."""
     import torch
@@ -392,10 +401,11 @@ def find_best_sub_pixel_tree_batch(src, ref, w, h, jobs, cost, method="pruned_mo
     if out is None:
         out = torch.empty(nj * SUBPEL_RESULT_DTYPE.itemsize, dtype=torch.uint8,
                           device=src.device)
-    rc = _lib.lavish_find_best_sub_pixel_tree_batch(
+    rc = _lib.lavish_find_best_sub_pixel_tree_batch_ex(
         _vp(src.data_ptr()), src.stride(0), _vp(ref.data_ptr()), src.stride(0), w, h,
         _vp(jobs.data_ptr()), None if fullpel is None else _vp(fullpel.data_ptr()), nj,
-        SUBPEL_METHODS[method], forced_stop, int(allow_hp), iters_per_step, ctypes.byref(cost),
+        SUBPEL_METHODS[method], search_type, forced_stop, int(allow_hp), iters_per_step,
+        ctypes.byref(cost),
         None if cost_lists is None else _vp(cost_lists.data_ptr()), _vp(out.data_ptr()),
         _stream_ptr(stream))
     if rc != 0:

@@ -649,6 +649,23 @@ int lavish_find_best_sub_pixel_tree_batch(
     int njobs, int subpel_search_method, int forced_stop, int allow_hp,
     int iters_per_step, const LavishMvCostParams *cost, const int32_t *cost_lists,
     LavishSubpelResult *out, void *stream);
+/* The same with var_params.subpel_search_type (SUBPEL_SEARCH_TYPE,
+ * av1/common/filter.h:45-50: 0 USE_2_TAPS_ORIG, 1 USE_2_TAPS, 2 USE_4_TAPS,
+ * 3 USE_8_TAPS; else -7).  SUBPEL_TREE with a type other than
+ * USE_2_TAPS_ORIG ranks by upsampled_pref_error (av1/encoder/mcomp.c:
+ * 2402-2491, check_better / first_level_check / second_level_check_v2's
+ * check_better branch) -- aom_upsampled_pred_c's prediction
+ * (av1/encoder/reconinter_enc.c:424-496, unscaled reference) -- which for
+ * USE_2_TAPS equals the bilinear svf.  The pruned methods take the svf for
+ * every type (check_better_fast on an unscaled reference), as in the
+ * reference.  The speed-0..3 default is SUBPEL_TREE with USE_8_TAPS
+ * (speed_features.c:1929-1931). */
+int lavish_find_best_sub_pixel_tree_batch_ex(
+    const uint8_t *src, int src_stride, const uint8_t *ref, int ref_stride, int w,
+    int h, const LavishSubpelJob *jobs, const LavishDiamondResult *fullpel,
+    int njobs, int subpel_search_method, int subpel_search_type, int forced_stop,
+    int allow_hp, int iters_per_step, const LavishMvCostParams *cost,
+    const int32_t *cost_lists, LavishSubpelResult *out, void *stream);
 
 /* ---- Inter prediction -----------------------------
  * av1_enc_build_one_inter_predictor (av1/encoder/reconinter_enc.c:47-51) for

@@ -262,6 +262,15 @@ void orc_subpel_search_batch(const uint8_t *src, int src_stride, const uint8_t *
                              int subpel_method, int forced_stop, int allow_hp,
                              int iters_per_step, const OrcMvCost *cost,
                              const int32_t *cost_lists, OrcSubpelResult *out, int threads);
+/* the same with SUBPEL_SEARCH_TYPE (0 USE_2_TAPS_ORIG, 1 USE_2_TAPS, 2
+ * USE_4_TAPS, 3 USE_8_TAPS): SUBPEL_TREE's error is then the upsampled
+ * prediction's (upsampled_pref_error) */
+void orc_subpel_search_batch_ex(const uint8_t *src, int src_stride, const uint8_t *ref,
+                                int ref_stride, int w, int h, const OrcSubpelJob *jobs,
+                                long njobs, int subpel_method, int subpel_search_type,
+                                int forced_stop, int allow_hp, int iters_per_step,
+                                const OrcMvCost *cost, const int32_t *cost_lists,
+                                OrcSubpelResult *out, int threads);
 
 /* ---- TX-type pruning features (oracle_txfeat.c) ---- */
 void orc_horver_correlation_full(const int16_t *diff, int stride, int width,

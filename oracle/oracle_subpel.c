@@ -17,6 +17,12 @@
  *   get_best_diag_step                        mcomp.c:2555-2562
  *   mv_err_cost_ (entropy / L1 / none)        mcomp.c:290-323
  *   av1_is_subpelmv_in_range                  mcomp.h:375-379
+ *   SUBPEL_TREE with subpel_search_type != USE_2_TAPS_ORIG: first_level_check
+ *     / check_better / upsampled_pref_error (mcomp.c:2402-2491,2528-2551,
+ *     2689-2723), second_level_check_v2's check_better branch (:2752-2762),
+ *     aom_upsampled_pred_c (reconinter_enc.c:424-496, unscaled) through
+ *     aom_convolve8_horiz_c / _vert_c (aom_dsp/aom_convolve.c:36-113) with
+ *     av1_get_filter (filter.h:276-285)
  * 8-bit planes.  MVs in 1/8 pel; the reference block at mv is at
  * ref + (row >> 3) * stride + (col >> 3) with offsets (col & 7, row & 7).
  */
@@ -31,6 +37,7 @@ typedef struct {
   int ss, rs, w, h, cost_type;
   const OrcSubpelJob *jb;
   const OrcMvCost *cost; /* MV_COST_ENTROPY tables and error_per_bit */
+  int search_type;       /* SUBPEL_SEARCH_TYPE of SUBPEL_TREE: 0 USE_2_TAPS_ORIG .. 3 USE_8_TAPS */
 } SpCtx;
 
 static int sp_lambda(int t) { return t == 1 ? 2 : t == 2 ? 0 : t == 3 ? 1 : 0; }
@@ -59,17 +66,72 @@ static unsigned sp_svf(const SpCtx *c, int row, int col, unsigned *sse) {
                                 c->w, c->h, sse);
 }
 
+static uint8_t clip8(int v) { return (uint8_t)(v < 0 ? 0 : v > 255 ? 255 : v); }
+
+/* upsampled_pref_error (mcomp.c:2402-2491) for an unscaled reference, no
+ * second_pred: aom_upsampled_pred_c's prediction at mv, then vf.  The kernel
+ * row is av1_get_filter(subpel_search) at phase 2 * q3: USE_2_TAPS the
+ * bilinear, USE_4_TAPS the 4-tap regular, USE_8_TAPS the 8-tap regular
+ * kernels, all in the 8-tap layout; each aom_convolve8 pass rounds by
+ * FILTER_BITS and clips to 8 bits, the 2-D case filtering rows -3 .. h + 4
+ * horizontally into a temporary first. */
+static unsigned sp_upsampled(const SpCtx *c, int row, int col, unsigned *sse) {
+  const int w = c->w, h = c->h, sx = col & 7, sy = row & 7;
+  const uint8_t *r = c->ref + c->jb->ref_off + (ptrdiff_t)(row >> 3) * c->rs + (col >> 3);
+  const int filt = c->search_type == 1 ? 3 : 0;    /* BILINEAR : EIGHTTAP_REGULAR */
+  const int size = c->search_type == 2 ? 4 : 8;    /* a size of 4 selects the 4-tap kernels */
+  int16_t kx[8], ky[8];
+  orc_interp_kernel(filt, size, 2 * sx, kx);
+  orc_interp_kernel(filt, size, 2 * sy, ky);
+  static __thread uint8_t pred[128 * 128], tmp[(128 + 7) * 128];
+  if (!sx && !sy) {
+    for (int y = 0; y < h; ++y)
+      for (int x = 0; x < w; ++x) pred[y * w + x] = r[(ptrdiff_t)y * c->rs + x];
+  } else if (!sy) {
+    for (int y = 0; y < h; ++y)
+      for (int x = 0; x < w; ++x) {
+        int sum = 0;
+        for (int k = 0; k < 8; ++k) sum += r[(ptrdiff_t)y * c->rs + x - 3 + k] * kx[k];
+        pred[y * w + x] = clip8((sum + 64) >> 7);
+      }
+  } else if (!sx) {
+    for (int y = 0; y < h; ++y)
+      for (int x = 0; x < w; ++x) {
+        int sum = 0;
+        for (int k = 0; k < 8; ++k) sum += r[(ptrdiff_t)(y - 3 + k) * c->rs + x] * ky[k];
+        pred[y * w + x] = clip8((sum + 64) >> 7);
+      }
+  } else {
+    for (int y = 0; y < h + 7; ++y)
+      for (int x = 0; x < w; ++x) {
+        int sum = 0;
+        for (int k = 0; k < 8; ++k) sum += r[(ptrdiff_t)(y - 3) * c->rs + x - 3 + k] * kx[k];
+        tmp[y * w + x] = clip8((sum + 64) >> 7);
+      }
+    for (int y = 0; y < h; ++y)
+      for (int x = 0; x < w; ++x) {
+        int sum = 0;
+        for (int k = 0; k < 8; ++k) sum += tmp[(y + k) * w + x] * ky[k];
+        pred[y * w + x] = clip8((sum + 64) >> 7);
+      }
+  }
+  return orc_variance(pred, w, c->src + c->jb->src_off, c->ss, w, h, sse);
+}
+
 typedef struct {
   int row, col;
   unsigned besterr, sse1;
   int distortion;
 } SpBest;
 
-/* check_better_fast: returns the candidate's cost, INT_MAX when out of range */
+/* check_better_fast (the svf estimate) or, for SUBPEL_TREE with a
+ * subpel_search_type other than USE_2_TAPS_ORIG, check_better (the upsampled
+ * prediction): returns the candidate's cost, INT_MAX when out of range */
 static unsigned sp_check(const SpCtx *c, int row, int col, SpBest *b) {
   if (!sp_in_range(c, row, col)) return INT_MAX;
   unsigned sse;
-  const int thismse = (int)sp_svf(c, row, col, &sse);
+  const int thismse =
+      (int)(c->search_type ? sp_upsampled(c, row, col, &sse) : sp_svf(c, row, col, &sse));
   unsigned cost = (unsigned)sp_mv_cost(c, row, col);
   cost += (unsigned)thismse;
   if (cost < b->besterr) {
@@ -211,18 +273,22 @@ static void *sp_worker(void *v) {
   return NULL;
 }
 
-void orc_subpel_search_batch(const uint8_t *src, int src_stride, const uint8_t *ref,
-                             int ref_stride, int w, int h, const OrcSubpelJob *jobs, long njobs,
-                             int subpel_method, int forced_stop, int allow_hp,
-                             int iters_per_step, const OrcMvCost *cost,
-                             const int32_t *cost_lists, OrcSubpelResult *out, int threads) {
+void orc_subpel_search_batch_ex(const uint8_t *src, int src_stride, const uint8_t *ref,
+                                int ref_stride, int w, int h, const OrcSubpelJob *jobs,
+                                long njobs, int subpel_method, int subpel_search_type,
+                                int forced_stop, int allow_hp, int iters_per_step,
+                                const OrcMvCost *cost, const int32_t *cost_lists,
+                                OrcSubpelResult *out, int threads) {
   if (threads < 1) threads = 1;
   if (threads > 64) threads = 64;
+  /* only SUBPEL_TREE takes the upsampled error (the pruned searches use
+   * check_better_fast, which for an unscaled reference is the svf) */
+  const int st = subpel_method == 0 ? subpel_search_type : 0;
   pthread_t tid[64];
   SpArg args[64];
   for (int t = 0; t < threads; ++t) {
     args[t].base =
-        (SpCtx){ src, ref, src_stride, ref_stride, w, h, cost->mv_cost_type, NULL, cost };
+        (SpCtx){ src, ref, src_stride, ref_stride, w, h, cost->mv_cost_type, NULL, cost, st };
     args[t].jobs = jobs;
     args[t].out = out;
     args[t].cls = cost_lists;
@@ -237,6 +303,16 @@ void orc_subpel_search_batch(const uint8_t *src, int src_stride, const uint8_t *
   }
   if (threads > 1)
     for (int t = 0; t < threads; ++t) pthread_join(tid[t], NULL);
+}
+
+void orc_subpel_search_batch(const uint8_t *src, int src_stride, const uint8_t *ref,
+                             int ref_stride, int w, int h, const OrcSubpelJob *jobs, long njobs,
+                             int subpel_method, int forced_stop, int allow_hp,
+                             int iters_per_step, const OrcMvCost *cost,
+                             const int32_t *cost_lists, OrcSubpelResult *out, int threads) {
+  orc_subpel_search_batch_ex(src, src_stride, ref, ref_stride, w, h, jobs, njobs, subpel_method,
+                             0, forced_stop, allow_hp, iters_per_step, cost, cost_lists, out,
+                             threads);
 }
 
 void orc_subpel_batch(const uint8_t *src, int src_stride, const uint8_t *ref, int ref_stride,

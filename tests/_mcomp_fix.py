@@ -58,5 +58,6 @@ def subpel_groups(F, mc):
         for f in ("start_row", "start_col", "ref_mv_row", "ref_mv_col", "col_min", "col_max",
                   "row_min", "row_max"):
             rec[f] = rows[:, J[f]]
-        cls = np.ascontiguousarray(rows[:, J["cl0"]:J["cl4"] + 1].astype(np.int32))
+        cls = (np.ascontiguousarray(rows[:, J["cl0"]:J["cl4"] + 1].astype(np.int32))
+               if "cl0" in J else None)  # (fix_subpel_up: SUBPEL_TREE takes no cost list)
         yield F["cases"][ci], bw, bh, epb, rec, cls, rows, J

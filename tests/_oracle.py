@@ -504,16 +504,17 @@ def tpl_motion_search(src, ref, stride, jobs, cols, rows, nrefs, method="fast_bi
 
 def subpel_search_batch(src, ref, stride, w, h, jobs, method=2, forced_stop=0, allow_hp=False,
                         iters=1, mv_cost_type=3, error_per_bit=0, mvjcost=None, mvcost=None,
-                        cost_lists=None, threads=1):
-    """orc_subpel_search_batch: SUBPEL_TREE (method 0, bilinear error),
-    SUBPEL_TREE_PRUNED (1) / _PRUNED_MORE (2) with any mv cost and optional
-    full-pel cost lists."""
+                        cost_lists=None, threads=1, search_type=0):
+    """orc_subpel_search_batch_ex: SUBPEL_TREE (method 0; bilinear error with
+    search_type 0 USE_2_TAPS_ORIG, else the upsampled prediction of
+    USE_2_TAPS / USE_4_TAPS / USE_8_TAPS), SUBPEL_TREE_PRUNED (1) /
+    _PRUNED_MORE (2) with any mv cost and optional full-pel cost lists."""
     L = lib()
-    fn = L.orc_subpel_search_batch
+    fn = L.orc_subpel_search_batch_ex
     fn.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
                    ctypes.c_int, ctypes.c_void_p, ctypes.c_long, ctypes.c_int, ctypes.c_int,
-                   ctypes.c_int, ctypes.c_int, ctypes.POINTER(OrcMvCost), ctypes.c_void_p,
-                   ctypes.c_void_p, ctypes.c_int]
+                   ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.POINTER(OrcMvCost),
+                   ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
     jobs = np.ascontiguousarray(jobs)
     c = OrcMvCost(mv_cost_type, 0, error_per_bit)
     keep = []
@@ -527,8 +528,9 @@ def subpel_search_batch(src, ref, stride, w, h, jobs, method=2, forced_stop=0, a
         c.mvcost[1] = mc.ctypes.data + 4 * (mc.shape[1] + mid)
     out = np.zeros(len(jobs), SUBPEL_RESULT)
     cl = None if cost_lists is None else np.ascontiguousarray(cost_lists, np.int32)
-    fn(P(src), stride, P(ref), stride, w, h, P(jobs), len(jobs), method, forced_stop,
-       int(allow_hp), iters, ctypes.byref(c), None if cl is None else P(cl), P(out), threads)
+    fn(P(src), stride, P(ref), stride, w, h, P(jobs), len(jobs), method, search_type,
+       forced_stop, int(allow_hp), iters, ctypes.byref(c), None if cl is None else P(cl), P(out),
+       threads)
     return out
 
 

@@ -1694,6 +1694,123 @@ def gen_txfeat():
     np.savez_compressed(os.path.join(HERE, "fix_txfeat.npz"), **out)
 
 
+SPU_CASES = [  # SUBPEL_TREE with the upsampled error: (subpel_search_type, allow_hp,
+               # forced_stop, iters_per_step, cost type)
+    ("USE_8_TAPS", 1, "EIGHTH_PEL", 2, "MV_COST_ENTROPY"),   # the default (speed_features.c:1931)
+    ("USE_8_TAPS", 0, "QUARTER_PEL", 1, "MV_COST_L1_HDRES"),
+    ("USE_4_TAPS", 1, "EIGHTH_PEL", 2, "MV_COST_ENTROPY"),
+    ("USE_4_TAPS", 1, "HALF_PEL", 1, "MV_COST_NONE"),
+    ("USE_2_TAPS", 1, "EIGHTH_PEL", 2, "MV_COST_ENTROPY"),
+]
+SPU_SIZES = {(16, 16): 3, (8, 8): 3, (32, 32): 2, (64, 64): 1, (16, 8): 2, (8, 32): 1, (4, 4): 2,
+             (128, 128): 1}
+
+
+def gen_subpel_up():
+    """av1_find_best_sub_pixel_tree (av1/encoder/mcomp.c:3128-3196) with
+    subpel_search_type USE_2_TAPS / USE_4_TAPS / USE_8_TAPS: first_level_check
+    and second_level_check_v2 through check_better / upsampled_pref_error
+    (:2402-2551,2689-2778) -> aom_upsampled_pred_c (reconinter_enc.c:424-496)
+    -> aom_convolve8_horiz_c / _vert_c, unscaled reference, from full-pel
+    results of fix_mcomp.npz."""
+    F = dict(np.load(os.path.join(HERE, "fix_mcomp.npz")))
+    tu = C.TU(REF, ["aom_dsp/variance.c", "av1/encoder/mcomp.c", "aom_dsp/aom_convolve.c",
+                    "av1/encoder/reconinter_enc.c"], C.reference_defines(REF))
+    check_errors(tu, ["av1_find_best_sub_pixel_tree", "aom_upsampled_pred_c",
+                      "aom_convolve8_horiz_c", "aom_convolve8_vert_c",
+                      "av1_set_subpel_mv_search_range"])
+    E = tu.enums
+    W, H, BORDER, NREF = (int(v) for v in F["geom"])
+    src_np, refs_np = F["src"], F["refs"]
+    stride = src_np.shape[1]
+    org = BORDER * stride + BORDER
+    src_buf = tu.buffer("uint8_t", src_np.reshape(-1).tolist())
+    ref_bufs = [tu.buffer("uint8_t", r.reshape(-1).tolist()) for r in refs_np]
+    tabs = {}
+    for nm in ("lp", "hp"):
+        mj = tu.buffer("int", F["mvjcost_" + nm].tolist())
+        mc = [tu.buffer("int", F["mvcost_" + nm][k].tolist()) for k in range(2)]
+        tabs[nm] = (mj, [C.Pointer(c.buf, MV_MAX, c.ty) for c in mc])
+    mi_params = tu.struct_obj("CommonModeInfoParams")
+    _set(mi_params.buf[0], mi_rows=((H + 7) & ~7) // 4, mi_cols=((W + 7) & ~7) // 4)
+    # xd: mi[0] not intrabc, unscaled reference, an 8-bit current buffer
+    xd = tu.struct_obj("MACROBLOCKD")
+    mbmi = tu.struct_obj("MB_MODE_INFO")
+    sf = tu.struct_obj("struct scale_factors")
+    _set(sf.buf[0], x_scale_fp=1 << 14, y_scale_fp=1 << 14)
+    ybuf = tu.struct_obj("YV12_BUFFER_CONFIG")
+    _set(ybuf.buf[0], flags=0)
+    _set(xd.buf[0], mi=C.Pointer([mbmi], 0, C.Ptr(tu.ctype("MB_MODE_INFO"))), cur_buf=ybuf, bd=8)
+    _get(xd.buf[0], "block_ref_scale_factors")[0] = sf
+    cm = tu.struct_obj("AV1_COMMON")
+    J = {n: i for i, n in enumerate(F["job_fields"])}
+    rnd = ACMRandom(0xbaba + 9)
+    picked = {}
+    for r in F["jobs"]:
+        key = (int(r[J["bw"]]), int(r[J["bh"]]))
+        if key in SPU_SIZES and len(picked.setdefault(key, [])) < 2 * SPU_SIZES[key] + 3 and \
+                int(F["cases"][r[J["case"]]][1]):
+            picked[key].append(r)
+    jobs = []
+    for (bw, bh), rows in picked.items():
+        fn = tu.func
+        vtab = tu.struct_obj("aom_variance_fn_ptr_t")
+        sz = "%dx%d" % (bw, bh)
+        _set(vtab.buf[0], vf=fn("aom_variance%s" % sz), svf=fn("aom_sub_pixel_variance%s" % sz))
+        for ci, (stype, hp, fstop, iters, ctype) in enumerate(SPU_CASES):
+            for r in rows[ci % 2::2][:SPU_SIZES[(bw, bh)]]:
+                by, bx, k = int(r[J["by"]]), int(r[J["bx"]]), int(r[J["ref"]])
+                ref_mv = (int(r[J["ref_mv_row"]]), int(r[J["ref_mv_col"]]))
+                lim = tu.struct_obj("FullMvLimits")
+                tu.func("av1_set_mv_limits")(mi_params, lim, by // 4, bx // 4, bh // 4, bw // 4,
+                                             BORDER)
+                rmv = tu.struct_obj("MV")
+                _set(rmv.buf[0], row=ref_mv[0], col=ref_mv[1])
+                ms = tu.struct_obj("SUBPEL_MOTION_SEARCH_PARAMS")
+                P = ms.buf[0]
+                tu.func("av1_set_subpel_mv_search_range")(
+                    C.Pointer([_get(P, "mv_limits")], 0, tu.ctype("SubpelMvLimits")), lim, rmv)
+                sl = _get(P, "mv_limits")
+                slims = [_get(sl, f) for f in ("col_min", "col_max", "row_min", "row_max")]
+                _set(P, allow_hp=hp, cost_list=None, forced_stop=E[fstop], iters_per_step=iters)
+                mcp = _get(P, "mv_cost_params")
+                mj, mc = tabs["hp" if hp else "lp"]
+                epb = 31 + 11 * rnd.generate(7)
+                _set(mcp, ref_mv=rmv, mv_cost_type=E[ctype], mvjcost=mj, error_per_bit=epb,
+                     sad_per_bit=0)
+                _get(mcp, "mvcost")[0], _get(mcp, "mvcost")[1] = mc[0], mc[1]
+                vp = _get(P, "var_params")
+                sbuf = tu.struct_obj("struct buf_2d")
+                _set(sbuf.buf[0], buf=C.Pointer(src_buf.buf, org + by * stride + bx, C.UCHAR),
+                     stride=stride, width=bw, height=bh)
+                rbuf = tu.struct_obj("struct buf_2d")
+                _set(rbuf.buf[0], buf=C.Pointer(ref_bufs[k].buf, org + by * stride + bx, C.UCHAR),
+                     stride=stride, width=W, height=H)
+                _set(vp, vfp=vtab, subpel_search_type=E[stype], w=bw, h=bh)
+                _set(_get(vp, "ms_buffers"), ref=rbuf, src=sbuf, second_pred=None, mask=None,
+                     mask_stride=0, inv_mask=0, wsrc=None, obmc_mask=None)
+                smv = C.new_obj(tu.ctype("MV"))
+                start = (int(r[J["best_row"]]) * 8, int(r[J["best_col"]]) * 8)
+                _set(smv, row=start[0], col=start[1])
+                best = tu.struct_obj("MV")
+                dist, sse = tu.buffer("int", 1), tu.buffer("unsigned int", 1)
+                err = tu.func("av1_find_best_sub_pixel_tree")(xd, cm, ms, smv, best, dist, sse,
+                                                               None)
+                bm = best.buf[0]
+                jobs.append([bw, bh, ci, by, bx, k, ref_mv[0], ref_mv[1], start[0], start[1]] +
+                            slims + [epb, _get(bm, "row"), _get(bm, "col"), err, dist.buf[0],
+                                     sse.buf[0]])
+        print("  subpel_up %-7s %d jobs" % (sz, len(jobs)))
+    out = {"jobs": np.array(jobs, np.int64)}
+    out["job_fields"] = np.array(["bw", "bh", "case", "by", "bx", "ref", "ref_mv_row",
+                                  "ref_mv_col", "start_row", "start_col", "col_min", "col_max",
+                                  "row_min", "row_max", "error_per_bit", "best_row", "best_col",
+                                  "besterr", "distortion", "sse"])
+    out["cases"] = np.array([[E[st], hp, E[fs], it, E[ct]] for st, hp, fs, it, ct in SPU_CASES],
+                            np.int32)
+    np.savez_compressed(os.path.join(HERE, "fix_subpel_up.npz"), **out)
+
+
 TPLMV_CASES = [  # (tpl_sf.search_method, reduce_first_step_size, use_downsampled_sad,
                  #  prune_starting_mv, skip_alike_starting_mv)
     ("FAST_BIGDIA", 6, 0, 3, 2),   # speed >= 5 (speed_features.c:1212-1216)
@@ -1860,7 +1977,7 @@ def gen_tplmv():
 def main(argv):
     sections = argv or ["txfm", "qparams", "quant", "inv", "pixel", "wht", "nmv", "mcomp",
                         "subpel", "tpl", "qfacade", "costcoeffs", "trellis", "warp", "compound",
-                        "convolve", "compound12", "txfeat", "trellis2", "tplmv"]
+                        "convolve", "compound12", "txfeat", "trellis2", "tplmv", "subpel_up"]
     t0 = time.time()
     ttx = None
     if "txfm" in sections or "inv" in sections or "wht" in sections:
@@ -1911,6 +2028,8 @@ def main(argv):
         gen_trellis(dict(np.load(os.path.join(HERE, "fix_txfm.npz"))), sharpness=2)
     if "tplmv" in sections:
         gen_tplmv()
+    if "subpel_up" in sections:
+        gen_subpel_up()
     print("done in %.0fs" % (time.time() - t0))
 
 

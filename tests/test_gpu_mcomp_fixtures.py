@@ -163,3 +163,60 @@ def test_ref_tiles_layout(stride, rows):
         for k in range(ns):
             exp[f, k] = pad[f::2, 16 * k:16 * k + 32]
     np.testing.assert_array_equal(got.reshape(2, ns, fh, 32), exp)
+
+
+def test_subpel_tree_upsampled_vs_reference(F):
+    """lavish_find_best_sub_pixel_tree_batch_ex (SUBPEL_TREE, subpel_search_type
+    USE_2_TAPS / USE_4_TAPS / USE_8_TAPS) against av1_find_best_sub_pixel_tree
+    executed from the reference with the upsampled prediction error
+    (tests/golden/fix_subpel_up.npz): best mv, besterr, distortion, sse."""
+    import torch
+    from lavish_dsp import motion as M
+    from _mcomp_fix import subpel_groups
+    S = dict(np.load(os.path.join(GOLD, "fix_subpel_up.npz")))
+    src = torch.from_numpy(F["src"]).cuda()
+    refs = torch.from_numpy(np.ascontiguousarray(F["refs"])).cuda()
+    costs = {t: M.MvCosts(F["mvjcost_" + t], F["mvcost_" + t]) for t in ("lp", "hp")}
+    n = 0
+    for case, bw, bh, epb, rec, _, rows, J in subpel_groups(S, F):
+        stype, hp, fstop, iters, ctype = (int(v) for v in case)
+        cp = costs["hp" if hp else "lp"].cost_params(0, epb, ctype)
+        out = M.find_best_sub_pixel_tree_batch(src, refs, bw, bh, M.to_device(rec), cp, "tree",
+                                               fstop, bool(hp), iters, search_type=stype)
+        torch.cuda.synchronize()
+        res = M.subpel_results_numpy(out)
+        msg = "case %s %dx%d" % ([int(v) for v in case], bw, bh)
+        for f in ("best_row", "best_col", "besterr", "distortion", "sse"):
+            np.testing.assert_array_equal(res[f].astype(np.int64), rows[:, J[f]],
+                                          err_msg=msg + " " + f)
+        n += len(rows)
+    assert n == len(S["jobs"])
+
+
+@pytest.mark.parametrize("stype", [2, 3])
+@pytest.mark.parametrize("bw,bh", [(16, 16), (8, 8), (32, 16), (64, 64), (4, 8)])
+def test_subpel_tree_upsampled_vs_oracle(stype, bw, bh):
+    """Every block of a 320x192 frame x 2 references (SUBPEL_TREE, USE_4_TAPS /
+    USE_8_TAPS, entropy costs, from the DIAMOND full-pel results) against the
+    oracle's upsampled error, bit-exact."""
+    import torch
+    import _oracle as O
+    from lavish_dsp import motion as M, synth
+    W, H, R, border = 320, 192, 2, 160
+    src, refs = synth.motion_planes(W, H, R, border, seed=91 + bw + stype)
+    st = src.shape[1]
+    jobs = M.frame_jobs(W, H, st, border, src.size, bw, bh, R, ref_mv=(12, -20))
+    mvj, mvc = M.default_mv_cost_tables(True)
+    fp, _ = O.full_pixel_search_batch(src.reshape(-1), refs.reshape(-1), st, bw, bh, jobs,
+                                      "diamond", 2, 0, 4, 40, mvj, mvc, threads=8)
+    sj = M.subpel_jobs(W, H, border, bw, bh, jobs, fp, ref_mv=(12, -20))
+    exp = O.subpel_search_batch(src.reshape(-1), refs.reshape(-1), st, bw, bh, sj, 0, 0, True,
+                                2, 0, 40, mvj, mvc, None, threads=8, search_type=stype)
+    costs = M.MvCosts(mvj, mvc)
+    out = M.find_best_sub_pixel_tree_batch(
+        torch.from_numpy(src).cuda(), torch.from_numpy(refs).cuda(), bw, bh, M.to_device(sj),
+        costs.cost_params(0, 40, M.MV_COST_ENTROPY), "tree", 0, True, 2, search_type=stype)
+    torch.cuda.synchronize()
+    got = M.subpel_results_numpy(out)
+    for f in ("best_row", "best_col", "besterr", "distortion", "sse"):
+        np.testing.assert_array_equal(got[f], exp[f], err_msg=f)

@@ -582,3 +582,29 @@ def test_tpl_motion_search_matches_reference():
             assert (int(cr[i]), int(cc[i])) in opts, (msg, i)
         # the neighbours matter in this content: some searches start off zero
         assert np.count_nonzero(cen) > 0, msg
+
+
+def test_subpel_tree_upsampled_vs_reference():
+    """orc_subpel_search_batch_ex (SUBPEL_TREE) against av1_find_best_sub_pixel_tree
+    executed from the reference with subpel_search_type USE_2_TAPS /
+    USE_4_TAPS / USE_8_TAPS -- check_better through upsampled_pref_error and
+    aom_upsampled_pred_c (tests/golden/fix_subpel_up.npz)."""
+    from _mcomp_fix import subpel_groups
+    F, mc = _load("fix_subpel_up.npz"), _load("fix_mcomp.npz")
+    stride = mc["src"].shape[1]
+    n = 0
+    moved = 0
+    for case, bw, bh, epb, rec, _, rows, J in subpel_groups(F, mc):
+        stype, hp, fstop, iters, ctype = (int(v) for v in case)
+        tab = "hp" if hp else "lp"
+        res = O.subpel_search_batch(mc["src"], mc["refs"], stride, bw, bh, rec, 0, fstop,
+                                    bool(hp), iters, ctype, epb, mc["mvjcost_" + tab],
+                                    mc["mvcost_" + tab], None, search_type=stype)
+        msg = "case %s %dx%d" % (list(case), bw, bh)
+        for f in ("best_row", "best_col", "besterr", "distortion", "sse"):
+            np.testing.assert_array_equal(res[f].astype(np.int64), rows[:, J[f]],
+                                          err_msg=msg + " " + f)
+        moved += int(np.count_nonzero((res["best_row"] & 7) | (res["best_col"] & 7)))
+        n += len(rows)
+    assert n == len(F["jobs"])
+    assert moved > n // 2  # most searches end on a sub-pel position
