@@ -549,7 +549,9 @@ class RdoFrame:
         self.dq = _P19(*[self.outs[s]["dqcoeff"].data_ptr() if s in self.outs else 0
                          for s in range(19)])
         H, W = src.shape
-        self.recon = torch.empty_like(src)
+        # the reconstruction keeps the planes' row stride (a view of a wider
+        # buffer when src is a column segment of a frame)
+        self.recon = torch.empty((H, src.stride(0)), dtype=src.dtype, device=src.device)[:, :W]
         self.sb_tx_size = torch.empty(((W + 63) // 64) * ((H + 63) // 64), dtype=torch.uint8,
                                       device=src.device)
 

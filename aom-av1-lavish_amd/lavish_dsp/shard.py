@@ -1,81 +1,235 @@
-"""C5: superblock-row sharding of the C4 RDO step over GPUs.
+"""C5: the C4 RDO step sharded over GPUs by superblock rows.
 
-SB rows are independent for C4 as defined (residual / prediction given):
-every TX block and every 64x64 superblock decision lies inside one SB row.
-Rank r takes a contiguous band of SB rows, runs the fused RDO + per-SB
-TX-size decision + reconstruction on it, and the reconstructed bands are
-all-gathered so that every rank holds the whole reconstructed frame (what the
-next SB row's intra prediction / the next frame's inter prediction reads).
-The exchange is one all-gather per frame over RCCL (xGMI) -- 2 bytes per
-pixel of the frame, ~16.6 MB at 4K -- the only collective on the path.
+For C4 as defined (residual / prediction given) every TX block and every
+64x64 superblock decision lies inside one SB, so any set of SBs is an
+independent unit; what the ranks must exchange is the reconstruction: the
+next SB row's intra prediction reads the reconstructed row above, the next
+frame's inter prediction the whole frame (north_star: "an RCCL/xGMI
+all-gather of the reconstructed row for next-row intra prediction").  Two
+forms, both one process per GPU over torch.distributed (RCCL on the GPUs,
+gloo on the CPU for the tests):
 
-The band bookkeeping and the exchange are plain torch.distributed code, so
-they run (and are tested) under gloo on the CPU as well; the per-band work
-is a callback.
+band (the throughput form, `sharded_frame`):
+  The frame's R SB rows are dealt as floor(R / G) contiguous full rows per
+  rank plus the R mod G leftover rows cut into G equal column segments
+  (one each), so every rank holds exactly R / G SB rows of work: at 4K
+  (34 rows) and 8 GPUs 4 rows + a quarter row each, no 34/40 = 85% cap of
+  whole-row bands.  Each rank computes its band, then its tail segment, and
+  all-gathers each part as soon as it is computed -- the band's gather
+  (equal-sized on every rank) runs on a communication stream while the tail
+  segment computes (`async_op`), then the tail segments are gathered.
+  (`partition` gives the rectangles.)
+
+row wavefront (the full-encoder-faithful form, `wavefront_frame`,
+SURVEY 8(e)(ii) and ethread.c:113-160):
+  SB row r runs on rank r mod G, in column chunks; before chunk c of row r
+  the rank needs the bottom edge (the last `edge_rows` pixel rows, what the
+  next row's intra predictors read) of row r - 1 up to chunk c + 1 (the
+  above-right dependency), which rank (r - 1) mod G sends point-to-point as
+  soon as it finishes each chunk; the received edges are written into the
+  receiver's reconstruction above its row.  After every wave of G rows the
+  wave's reconstructed rows are all-gathered (one SB row per rank: the
+  per-row all-gather of north_star), on the communication stream, while the
+  next wave computes.
+
+process_rect(y0, y1, x0, x1) -> the reconstructed [y1 - y0, x1 - x0] region
+is the per-rank work (the GPU C4 step in `c4_rect_processor`, the oracle's in
+the tests); the bookkeeping and the exchanges are plain torch.distributed.
 """
+
+SB = 64
 
 
 def sb_rows(height):
-    return (height + 63) // 64
+    return (height + SB - 1) // SB
+
+
+def sb_cols(width):
+    return (width + SB - 1) // SB
 
 
 def bands(height, world):
-    """Pixel-row bands [(y0, y1)] of a frame, one per rank: contiguous,
-    balanced SB-row counts (the first rows % world ranks take one extra)."""
+    """Pixel-row bands [(y0, y1)] of whole SB rows, one per rank, contiguous,
+    balanced to +-1 SB row (the round-2 partition; kept for reference)."""
     n = sb_rows(height)
     out = []
     for r in range(world):
         r0 = n * r // world
         r1 = n * (r + 1) // world
-        out.append((min(r0 * 64, height), min(r1 * 64, height)))
+        out.append((min(r0 * SB, height), min(r1 * SB, height)))
     return out
 
 
-def gather_bands(local, height, rank, world, group=None):
-    """All-gather the per-rank bands (local: [y1 - y0, W] tensor of this rank's
-    band) into the whole [height, W] frame on every rank.  Bands are padded
-    to the largest band so a single all_gather_into_tensor moves them."""
+def partition(height, width, world):
+    """Per rank: (band, tail) pixel rectangles (y0, y1, x0, x1) or None.
+    band: floor(R / G) whole SB rows, contiguous, rank-major; tail: rank g's
+    column segment of the L = R mod G leftover rows -- leftover row i is cut
+    into n_i = G (i + 1) // L - G i // L segments (whole SBs, widths within
+    one SB), so the G segments go one per rank.  When L divides G every rank
+    gets exactly R / G rows of work (4K: 34 rows = 8 x (4 + 1/4))."""
+    R, C = sb_rows(height), sb_cols(width)
+    full = R // world
+    L = R - full * world
+    out = []
+    for g in range(world):
+        band = (g * full * SB, min((g + 1) * full * SB, height), 0, width) if full else None
+        tail = None
+        if L:
+            row = next(i for i in range(L) if g < world * (i + 1) // L)
+            first = world * row // L
+            segs = world * (row + 1) // L - first
+            k = g - first
+            c0, c1 = C * k // segs, C * (k + 1) // segs
+            y0 = (full * world + row) * SB
+            tail = (y0, min(y0 + SB, height), c0 * SB, min(c1 * SB, width))
+        out.append((band, tail))
+    return out
+
+
+def _gather_rects(local, rects, full, group, async_op):
+    """All-gather equally shaped per-rank regions (local: this rank's
+    [h, w] tensor; rects: every rank's (y0, y1, x0, x1), None for none)
+    into `full`; regions are zero-padded to the largest one.  Returns a
+    finisher (call it to wait and unpack)."""
     import torch
     import torch.distributed as dist
-    bs = bands(height, world)
-    y0, y1 = bs[rank]
-    assert local.shape[0] == y1 - y0
-    W = local.shape[1]
-    hmax = max(b1 - b0 for b0, b1 in bs)
-    send = torch.zeros((hmax, W), dtype=local.dtype, device=local.device)
-    send[:y1 - y0] = local
-    recv = torch.empty((world * hmax, W), dtype=local.dtype, device=local.device)
+    world = len(rects)
+    hmax = max((r[1] - r[0]) for r in rects if r is not None)
+    wmax = max((r[3] - r[2]) for r in rects if r is not None)
+    send = torch.zeros((hmax, wmax), dtype=full.dtype, device=full.device)
+    if local is not None:
+        send[:local.shape[0], :local.shape[1]] = local
+    recv = torch.empty((world * hmax, wmax), dtype=full.dtype, device=full.device)
+    work = None
     if world > 1:
-        # moved as bytes: neither RCCL nor gloo reduces/gathers int16
-        dist.all_gather_into_tensor(recv.view(torch.uint8), send.view(torch.uint8), group=group)
+        # moved as bytes: neither RCCL nor gloo gathers int16 as a dtype
+        work = dist.all_gather_into_tensor(recv.view(torch.uint8), send.view(torch.uint8),
+                                           group=group, async_op=async_op)
     else:
         recv.copy_(send)
-    full = torch.empty((height, W), dtype=local.dtype, device=local.device)
-    for r, (b0, b1) in enumerate(bs):
-        full[b0:b1] = recv[r * hmax:r * hmax + (b1 - b0)]
+
+    def finish():
+        if work is not None and async_op:
+            work.wait()
+        for g, r in enumerate(rects):
+            if r is None:
+                continue
+            y0, y1, x0, x1 = r
+            full[y0:y1, x0:x1] = recv[g * hmax:g * hmax + (y1 - y0), :x1 - x0]
+    return finish
+
+
+def sharded_frame(height, width, rank, world, process_rect, group=None, like=None):
+    """The band form: run process_rect on this rank's band, start its
+    all-gather asynchronously, run the tail segment, gather the tails, and
+    return the whole reconstructed frame (identical on every rank)."""
+    import torch
+    parts = partition(height, width, world)
+    band, tail = parts[rank]
+    if world == 1:  # one rank: the band is the frame, nothing to exchange
+        return process_rect(*band)
+    full = None
+    fin = []
+    for phase, rect in enumerate((band, tail)):
+        rects = [p[phase] for p in parts]
+        if all(r is None for r in rects):
+            continue
+        local = process_rect(*rect) if rect is not None else None
+        if full is None:
+            ref = local if local is not None else like
+            full = torch.empty((height, width), dtype=ref.dtype, device=ref.device)
+        fin.append(_gather_rects(local, rects, full, group, async_op=True))
+    for f in fin:
+        f()
     return full
 
 
-def sharded_frame(height, rank, world, process_band, group=None):
-    """Run process_band(y0, y1) -> reconstructed band on this rank's band and
-    return the whole reconstructed frame (identical on every rank)."""
-    y0, y1 = bands(height, world)[rank]
-    return gather_bands(process_band(y0, y1), height, rank, world, group)
+def wavefront_frame(height, width, rank, world, process_rect, chunks=4, edge_rows=4,
+                    p2p_group=None, gather_group=None, dtype=None, device=None, log=None):
+    """The row-wavefront form: SB row r on rank r % G, processed in `chunks`
+    column chunks; chunk c of row r waits for the bottom `edge_rows` pixel
+    rows of row r - 1 up to chunk c + 1 (point-to-point from rank
+    (r - 1) % G, which sends each chunk's edge when it is done); after each
+    wave of G rows the wave's rows are all-gathered.  Returns the whole
+    reconstructed frame (identical on every rank).  The edges and the
+    gathers must use different process groups (communicators): a rank's
+    receive for the next wave must not queue behind its pending gather of
+    this one, which waits for the sender.  log: optional list that receives
+    ('recv', row, chunk) / ('send', row, chunk) events."""
+    import torch
+    import torch.distributed as dist
+    R, C = sb_rows(height), sb_cols(width)
+    chunks = max(1, min(chunks, C))
+    cx = [min(C * k // chunks * SB, width) for k in range(chunks + 1)]
+    full = torch.zeros((height, width), dtype=dtype, device=device)
+    nxt, prv = (rank + 1) % world, (rank - 1) % world
+    pending = []   # outstanding sends
+    gathers = []
+    for w0 in range(0, R, world):
+        wave = list(range(w0, min(w0 + world, R)))
+        mine = w0 + rank if w0 + rank < R else None
+        if mine is not None:
+            y0, y1 = mine * SB, min((mine + 1) * SB, height)
+            got = 0   # chunks of the row above received
+            for c in range(chunks):
+                # above-right: the row above's chunks 0 .. c + 1 (ethread.c
+                # sync_range; the reference's own row-above dependency)
+                need = min(c + 2, chunks) if mine > 0 else 0
+                while got < need:
+                    edge = torch.empty((edge_rows, cx[got + 1] - cx[got]), dtype=dtype,
+                                       device=device)
+                    if world > 1:
+                        dist.recv(edge.view(torch.uint8), src=prv, group=p2p_group)
+                    else:
+                        edge.copy_(full[y0 - edge_rows:y0, cx[got]:cx[got + 1]])
+                    full[y0 - edge_rows:y0, cx[got]:cx[got + 1]] = edge
+                    if log is not None:
+                        log.append(("recv", mine - 1, got))
+                    got += 1
+                rec = process_rect(y0, y1, cx[c], cx[c + 1])
+                full[y0:y1, cx[c]:cx[c + 1]] = rec
+                if mine + 1 < R and world > 1:
+                    e = rec[rec.shape[0] - edge_rows:].contiguous()
+                    pending.append((dist.isend(e.view(torch.uint8), dst=nxt, group=p2p_group),
+                                    e))
+                    if log is not None:
+                        log.append(("send", mine, c))
+        # the wave's rows: one SB row per rank (the per-row all-gather)
+        rects = [(r * SB, min((r + 1) * SB, height), 0, width) for r in wave] + \
+            [None] * (world - len(wave))
+        local = full[mine * SB:min((mine + 1) * SB, height)].clone() if mine is not None else None
+        gathers.append(_gather_rects(local, rects, full, gather_group, async_op=True))
+    for f in gathers:
+        f()
+    for work, _ in pending:
+        work.wait()
+    return full
 
 
-def c4_band_processor(src, pred, qp, rdmult, bit_depth, frames):
-    """process_band for the GPU path: lavish_rdo_frame + reconstruct on the
-    rows [y0, y1) of device planes (views share the full planes' stride).
-    `frames` caches the RdoFrame output buffers per band (bands may run
-    concurrently on different streams, so no two share buffers)."""
+def c4_rect_processor(src, pred, qp, rdmult, bit_depth, frames):
+    """process_rect for the GPU path: lavish_rdo_frame + reconstruct on the
+    rectangle [y0, y1) x [x0, x1) of device planes (views keep the planes'
+    stride).  `frames` caches the RdoFrame output buffers per rectangle."""
     import lavish_dsp as L
 
-    def run(y0, y1):
-        s, p = src[y0:y1], pred[y0:y1]
-        key = (y0, y1, s.shape[1])
+    def run(y0, y1, x0, x1):
+        s, p = src[y0:y1, x0:x1], pred[y0:y1, x0:x1]
+        key = (y0, y1, x0, x1)
         if key not in frames:
-            frames[key] = L.RdoFrame(s)
+            # a rectangle lower / narrower than a candidate size holds none of
+            # its blocks: leave the size out (the per-SB decision skips sizes
+            # that do not tile the SB, so the result is the whole frame's)
+            masks = {t: m for t, m in L.C4_TYPE_MASKS.items()
+                     if L.TX_W[t] <= x1 - x0 and L.TX_H[t] <= y1 - y0}
+            frames[key] = L.RdoFrame(s, masks)
         fr = frames[key]
         L.rdo_frame(s, p, fr, qp, rdmult, bit_depth)
         return fr.recon
     return run
+
+
+def c4_band_processor(src, pred, qp, rdmult, bit_depth, frames):
+    """process_band(y0, y1) over whole-width bands (kept for callers of the
+    round-2 interface)."""
+    run = c4_rect_processor(src, pred, qp, rdmult, bit_depth, frames)
+    return lambda y0, y1: run(y0, y1, 0, src.shape[1])

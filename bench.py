@@ -77,6 +77,9 @@ def parse():
     ap.add_argument("--border", type=int, default=160)
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--c5-form", choices=("band", "wavefront"), default="band",
+                    help="C5 sharding: balanced band + tail segments with overlapped "
+                         "all-gathers, or the row-wavefront with p2p edges (lavish_dsp/shard.py)")
     ap.add_argument("--no-c4", action="store_true",
                     help="skip the c4 sub-object (4K 10-bit RDO step) of the default line")
     ap.add_argument("--serial", action="store_true",
@@ -315,10 +318,17 @@ def main_c4(args):
     stream = torch.cuda.current_stream()
     frames = {}
     if args.workload == "c5":
-        proc = shard.c4_band_processor(src, pred, qp, args.rdmult, 10, frames)
+        proc = shard.c4_rect_processor(src, pred, qp, args.rdmult, 10, frames)
+        if args.c5_form == "wavefront":
+            # edges and row gathers on separate communicators (shard.py)
+            p2p = dist.new_group(list(range(world))) if world > 1 else None
 
-        def step():
-            return shard.sharded_frame(H, rank, world, proc)
+            def step():
+                return shard.wavefront_frame(H, W, rank, world, proc, chunks=4, p2p_group=p2p,
+                                             dtype=torch.int16, device="cuda")
+        else:
+            def step():
+                return shard.sharded_frame(H, W, rank, world, proc)
     else:
         fr = L.RdoFrame(src)
 
@@ -355,7 +365,7 @@ def main_c4(args):
     sb = sb64_count(W, H)
     value = sb * args.steps / elapsed  # one frame per step for the whole job
     c4_bytes = c4_algorithmic_bytes(L, W, H)
-    y0, y1 = shard.bands(H, world)[rank]
+    band, tail = shard.partition(H, W, world)[rank]
     line = {
         "metric": metric_name(args), "workload": args.workload,
         "value": round(value, 2),
@@ -377,9 +387,13 @@ def main_c4(args):
                         % (args.workload, W, H,
                            "pixel-domain distortion (inverse txfm + recon + sse per type)"
                            if args.workload == "c4px" else "TX-domain block error",
-                           "; SB rows sharded over ranks + RCCL all-gather of the "
-                           "reconstruction" if args.workload == "c5" else "", sb),
-            "parallelism": ("sb-row bands x%d (rank %d rows %d-%d)" % (world, rank, y0, y1))
+                           ("; SB rows sharded over ranks (%s form) + RCCL all-gather of "
+                            "the reconstruction" % args.c5_form) if args.workload == "c5" else "",
+                           sb),
+            "parallelism": ("sb-row %s x%d (rank %d: band %s, tail %s)"
+                            % ("band+tail segments" if args.c5_form == "band"
+                               else "round-robin rows, p2p edge wavefront", world, rank, band,
+                               tail))
             if args.workload == "c5" else "frame-per-rank x%d" % world,
         },
         "roofline": {"bound": "hbm", "kernel": "rdo_kernel<W,H,%d> x5 sizes + reconstruction "

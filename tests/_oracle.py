@@ -575,6 +575,8 @@ def rdo_plane(src, pred, tx_size, type_mask, bd, q, rdmult, threads=1, px=False)
     out = np.zeros(nb, RDO_DTYPE)
     qc = np.zeros((nb, n), np.int32)
     dq = np.zeros((nb, n), np.int32)
+    if nb == 0:  # the plane is narrower / lower than one block of this size
+        return out, qc, dq
     fn(P(src), P(pred), W, W, H, tx_size, type_mask, bd, ctypes.byref(q), rdmult, P(out), P(qc),
        P(dq), threads)
     return out, qc, dq

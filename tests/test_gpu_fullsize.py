@@ -175,9 +175,42 @@ def test_c5_bands_world1_three_streams(L):
     full = torch.cat(parts, 0)
     np.testing.assert_array_equal(full.cpu().numpy(), whole.recon.cpu().numpy())
     # and through sharded_frame (world 1: one band, the whole frame)
-    one = shard.sharded_frame(H, 0, 1, proc)
+    rect = shard.c4_rect_processor(ts, tp, qp, rdmult, 10, frames)
+    one = shard.sharded_frame(H, W, 0, 1, rect)
     torch.cuda.synchronize()
     np.testing.assert_array_equal(one.cpu().numpy(), whole.recon.cpu().numpy())
+
+
+def test_c5_partition_rects_on_gpu(L):
+    """Every rank's band and tail rectangle of shard.partition for worlds
+    2..8 (tails are column segments: views with the frame's stride), each
+    computed by the HIP C4 step on its own, assemble to the whole-frame
+    reconstruction; so does the row-wavefront form at world 1 (3 column
+    chunks per SB row)."""
+    import torch
+    import lavish_dsp.shard as shard
+    W, H, rdmult = 1280, 784, 1700   # 13 SB rows: tails for every world > 1
+    src, pred = _c4_planes(W, H)
+    ts = torch.from_numpy(src.view(np.int16)).cuda()
+    tp = torch.from_numpy(pred.view(np.int16)).cuda()
+    qp = L.build_quant_params(10, 128, L.QUANT_FP)
+    whole = L.RdoFrame(ts)
+    L.rdo_frame(ts, tp, whole, qp, rdmult, 10)
+    ref = whole.recon.cpu().numpy()
+    frames = {}
+    rect = shard.c4_rect_processor(ts, tp, qp, rdmult, 10, frames)
+    for world in range(2, 9):
+        full = torch.empty_like(ts)
+        for band, tail in shard.partition(H, W, world):
+            for r in (band, tail):
+                if r is not None:
+                    y0, y1, x0, x1 = r
+                    full[y0:y1, x0:x1] = rect(*r)
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(full.cpu().numpy(), ref, err_msg="world %d" % world)
+    wf = shard.wavefront_frame(H, W, 0, 1, rect, chunks=3, dtype=torch.int16, device="cuda")
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(wf.cpu().numpy(), ref)
 
 
 def test_pixel_1080p_7refs_all_jobs(L):
