@@ -33,8 +33,8 @@ SURVEY 8(e)(ii) and ethread.c:113-160):
   next wave computes.
 
 process_rect(y0, y1, x0, x1) -> the reconstructed [y1 - y0, x1 - x0] region
-is the per-rank work (the GPU C4 step in `c4_rect_processor`, the oracle's in
-the tests); the bookkeeping and the exchanges are plain torch.distributed.
+is the per-rank work (the GPU C4 step in `c4_rect_processor`; the CPU tests pass
+their own); the bookkeeping and the exchanges are plain torch.distributed.
 """
 
 SB = 64
