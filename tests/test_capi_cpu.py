@@ -164,3 +164,55 @@ def test_interp_kernels_match_reference_tables(f, size):
     exp = F["av1_sub_pel_filters_12sharp"] if f == 4 else \
         (F[names4[f]] if size <= 4 else F[names8[f]])
     np.testing.assert_array_equal(I.interp_kernels(f, size), np.array(exp, np.int16))
+
+
+def test_swar_nz_mag_identity():
+    """The rate mode of rdo_kernel (csrc/rdo.hip, MODE 3) forms get_nz_mag's
+    clipped neighbour sums for 8 positions per 32-bit word: each 4-bit level
+    clipped to 3 as (x & 3) | 3 * (bit 2 | bit 3), then the class's five
+    neighbour words (nibble shifts across words) added without carries.
+    Check that arithmetic against the per-position sum for random level maps
+    of every class and row width."""
+    import numpy as np
+    rng = np.random.default_rng(7)
+    M = 0xFFFFFFFF
+
+    def words(levels):  # 4-bit levels (clipped to 15) -> packed words, 8 per word
+        n = (len(levels) + 7) // 8
+        w = [0] * n
+        for c, v in enumerate(levels):
+            w[c >> 3] |= min(int(v), 15) << (4 * (c & 7))
+        return w
+
+    def min3w(w):
+        out = []
+        for x in w:
+            f = ((x >> 2) | (x >> 3)) & 0x11111111
+            out.append((x & 0x33333333) | f | ((f << 1) & M))
+        return out
+
+    def sh(m, w, k):
+        return ((m[w] >> (4 * k)) | (((m[w + 1] << (32 - 4 * k)) & M) if w + 1 < len(m) else 0)) & M
+
+    for KW in (4, 8, 16, 32):
+        for _ in range(200):
+            rows = [rng.integers(0, 20, KW) * (rng.random(KW) < 0.5) for _ in range(5)]
+            m = [min3w(words(r)) for r in rows]
+            NW = len(m[0])
+            nib = lambda d, c: min(int(rows[d][c]), 15) if c < KW else 0
+            for cls in range(3):
+                for w in range(NW):
+                    base = sh(m[0], w, 1) + m[1][w]
+                    s = (base + sh(m[1], w, 1) + sh(m[0], w, 2) + m[2][w] if cls == 0 else
+                         base + sh(m[0], w, 2) + sh(m[0], w, 3) + sh(m[0], w, 4) if cls == 1 else
+                         base + m[2][w] + m[3][w] + m[4][w]) & M
+                    for k in range(8):
+                        c = 8 * w + k
+                        if c >= KW:
+                            continue
+                        mn = lambda v: min(v, 3)
+                        exp = mn(nib(0, c + 1)) + mn(nib(1, c))
+                        exp += (mn(nib(1, c + 1)) + mn(nib(0, c + 2)) + mn(nib(2, c)) if cls == 0
+                                else mn(nib(0, c + 2)) + mn(nib(0, c + 3)) + mn(nib(0, c + 4))
+                                if cls == 1 else mn(nib(2, c)) + mn(nib(3, c)) + mn(nib(4, c)))
+                        assert (s >> (4 * k)) & 15 == exp, (KW, cls, c)

@@ -35,8 +35,9 @@ def main(fdir, wdir, out):
         fb = 2.0 * f.get(k, 0.0)
         wb = w.get(k, 0.0)
         kernels[k] = {"fetch_bytes_x2": round(fb), "write_bytes": round(wb), "hbm_bytes": round(fb + wb)}
-    txq = [v for k, v in kernels.items() if "txq_plane_kernel" in k]
-    dia = [v for k, v in kernels.items() if "diamond_kernel" in k]
+    txq = [v for k, v in kernels.items() if "txq_plane_kernel" in k or "txq_multi_kernel" in k]
+    dia = [v for k, v in kernels.items()
+           if "diamond_kernel" in k or "diamond_lj_kernel" in k or "ref_tiles_kernel" in k]
     res = {
         "method": "rocprofv3 --kernel-trace --pmc FETCH_SIZE / WRITE_SIZE in separate passes of "
                   "bench.py; per-dispatch average excluding the first dispatch; FETCH_SIZE x2 "
