@@ -842,7 +842,26 @@ __device__ int pattern(const Ctx& c, int lane, int srow, int scol, int search_st
   brow = br;
   bcol = bc;
   if (want_cl) {
-    int_sad_list(S, c, lane, br, bc, has_sad, cl);
+    if (in_win(br, bc, 1)) {
+      // calc_int_sad_list (int_sad_list) with the window's SADs and rates
+      if (!has_sad) {
+        const int dr = g == 2 ? 1 : g == 4 ? -1 : 0, dc = g == 1 ? -1 : g == 3 ? 1 : 0;
+        const int r = br + dr, cc = bc + dc;
+        const bool valid =
+            g < 5 && cc >= c.col_min && cc <= c.col_max && r >= c.row_min && r <= c.row_max;
+        const uint32_t sad = S.group_sad_win(c, r, cc, valid);
+        const uint32_t v = valid ? sad : 0x7FFFFFFFu;
+#pragma unroll
+        for (int i = 0; i < 5; ++i) cl[i] = (int)rdlane(v, 8 * i);
+      }
+      cl[0] += (int)mvsad_finish(c, rate_win(br, bc), br, bc);
+      if (cl[1] != INT_MAX) cl[1] += (int)mvsad_finish(c, rate_win(br, bc - 1), br, bc - 1);
+      if (cl[2] != INT_MAX) cl[2] += (int)mvsad_finish(c, rate_win(br + 1, bc), br + 1, bc);
+      if (cl[3] != INT_MAX) cl[3] += (int)mvsad_finish(c, rate_win(br, bc + 1), br, bc + 1);
+      if (cl[4] != INT_MAX) cl[4] += (int)mvsad_finish(c, rate_win(br - 1, bc), br - 1, bc);
+    } else {
+      int_sad_list(S, c, lane, br, bc, has_sad, cl);
+    }
     if (!has_sad) nsad += 1 + (cl[1] != INT_MAX) + (cl[2] != INT_MAX) + (cl[3] != INT_MAX) +
                           (cl[4] != INT_MAX);
   }
@@ -1079,6 +1098,7 @@ __global__ __launch_bounds__(64) void tpl_mv_kernel(TplMvArgs a) {
   };
   const bool want_cl = a.cost_lists != nullptr;
   int32_t above = 0, left = 0;
+  Job jn = a.jobs[ref * nb + (int64_t)row * a.cols];  // the next block's job, loaded a step ahead
   for (int col = 0; col < a.cols; ++col) {
     const int64_t bi = (int64_t)row * a.cols + col;
     int32_t above_right = 0;
@@ -1087,7 +1107,8 @@ __global__ __launch_bounds__(64) void tpl_mv_kernel(TplMvArgs a) {
       if (col + 1 < a.cols) above_right = await_mv(bi - a.cols + 1);
     }
     const int64_t j = ref * nb + bi;
-    const Job jb = a.jobs[j];
+    const Job jb = jn;
+    if (col + 1 < a.cols) jn = a.jobs[j + 1];
     // centre candidates (row, col in 1/8 pel) and their SADs
     int cr[4] = {0, 0, 0, 0}, cc[4] = {0, 0, 0, 0}, cs[4] = {0, 0, 0, 0};
     int n = 1;

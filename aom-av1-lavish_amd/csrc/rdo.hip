@@ -283,6 +283,30 @@ __device__ __forceinline__ void rdo_types(const RdoArgs& a, const int32_t (&res)
           auto nib = [&](int d, int c) -> int {
             return c < KW ? (int)((pk[d][c >> 3] >> (4 * (c & 7))) & 15u) : 0;
           };
+          // get_nz_mag for 8 positions per word at once (SWAR on the
+          // nibbles): every neighbour clipped to 3 -- x & 3, or 3 where bit
+          // 2 or 3 is set -- then the class's five neighbours, each a
+          // nibble shift of a row word, summed without carries (<= 15)
+          uint32_t m3[5][NW];
+#pragma unroll
+          for (int d = 0; d < 5; ++d)
+#pragma unroll
+            for (int w = 0; w < NW; ++w) {
+              const uint32_t x = pk[d][w];
+              const uint32_t f = ((x >> 2) | (x >> 3)) & 0x11111111u;
+              m3[d][w] = (x & 0x33333333u) | f | (f << 1);
+            }
+          auto sh = [&](int d, int w, int k) -> uint32_t {  // nibble c + k of row d, word w
+            return (m3[d][w] >> (4 * k)) | (w + 1 < NW ? m3[d][w + 1] << (32 - 4 * k) : 0u);
+          };
+          uint32_t nzs[NW];
+#pragma unroll
+          for (int w = 0; w < NW; ++w) {
+            const uint32_t base = sh(0, w, 1) + m3[1][w];
+            nzs[w] = cls == 0 ? base + sh(1, w, 1) + sh(0, w, 2) + m3[2][w]
+                   : cls == 1 ? base + sh(0, w, 2) + sh(0, w, 3) + sh(0, w, 4)
+                              : base + m3[2][w] + m3[3][w] + m3[4][w];
+          }
           const bool has_ctx = a.txb_ctx != nullptr && live && bb < nvalid;
           const LavishTxbCtx tc = has_ctx ? a.txb_ctx[blk0 + bb] : LavishTxbCtx{0, 0};
 #pragma unroll
@@ -290,20 +314,14 @@ __device__ __forceinline__ void rdo_types(const RdoArgs& a, const int32_t (&res)
             const int rc = c * KH + r;
             const int i = iscan[rc];
             if (i < last) {
-              const int right = nib(0, c + 1), below = nib(1, c);
-              int nzmag = cc::min3(right) + cc::min3(below), third;
-              if (cls == 0) {
-                third = nib(1, c + 1);
-                nzmag += cc::min3(third) + cc::min3(nib(0, c + 2)) + cc::min3(nib(2, c));
-              } else if (cls == 1) {
-                third = nib(0, c + 2);
-                nzmag += cc::min3(third) + cc::min3(nib(0, c + 3)) + cc::min3(nib(0, c + 4));
-              } else {
-                third = nib(2, c);
-                nzmag += cc::min3(third) + cc::min3(nib(3, c)) + cc::min3(nib(4, c));
-              }
+              const int nzmag = (int)((nzs[c >> 3] >> (4 * (c & 7))) & 15u);
+              // get_br_ctx's raw sum, needed only above level 2
+              int brmag = 0;
+              if (abs(q[c]) > 2)
+                brmag = nib(0, c + 1) + nib(1, c) +
+                        (cls == 0 ? nib(1, c + 1) : cls == 1 ? nib(0, c + 2) : nib(2, c));
               rate += cc::coeff_term_mag(s_cc, cls, a.nz_wlt, a.nz_wgt, NC, rc, c, r, i, last,
-                                         q[c], tc.dc_sign_ctx, nzmag, right + below + third);
+                                         q[c], tc.dc_sign_ctx, nzmag, brmag);
             }
           }
 #pragma unroll
@@ -516,8 +534,20 @@ __device__ __forceinline__ void rdo_types(const RdoArgs& a, const int32_t (&res)
 // with pixel-domain distortion (sizes <= 32x32; BDI = bit-depth index), 3:
 // mode 1 ranked by the coefficient rate (av1_cost_coeffs_txb) instead of
 // rate_estimator.
+// Occupancy: a rdo_kernel wave holds a column (or row) of its block per lane
+// through each 1-D transform, so the large sizes sit just above a VGPR
+// step of the unified 512-register file (32x32 TX-domain: 266 registers =
+// 1 wave per SIMD, latency bound at 14% of the VALU peak).  The TX-domain
+// decision kernels of the sizes of 512+ coefficients ask for 2 waves per
+// SIMD (<= 256 registers), the 16x16 one for 4 (<= 128).
+template <int W, int H, int MODE>
+constexpr int rdo_waves() {
+  return (MODE == 1 && W * H >= 512) ? 2 : (MODE == 1 && W == 16 && H == 16) ? 4 : 1;
+}
+
 template <int W, int H, int MODE, int BDI>
-__global__ __launch_bounds__(64) void rdo_kernel(RdoArgs a) {
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(rdo_waves<W, H, MODE>())))
+void rdo_kernel(RdoArgs a) {
   using T = RTile<W, H>;
   __shared__ int32_t t1[T::T1];
   __shared__ __attribute__((aligned(16))) int32_t t2[MODE == 0 ? T::T2 : 4];
