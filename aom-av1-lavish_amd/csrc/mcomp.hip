@@ -1334,13 +1334,19 @@ __device__ void lj_pass(const Ctx& c, const LjSrc& s, int l, bool run, int step_
     // lane l: site l's cost (its loads in flight with the SAD loads below)
     const int rl = row + sdr * rad, cl_ = col + sdc * rad;
     const bool vl = cl_ >= c.col_min && cl_ <= c.col_max && rl >= c.row_min && rl <= c.row_max;
-    const MvRate mr = mvsad_rate(c, rl, cl_);
+    // loads only for in-range sites of jobs still walking: out-of-range
+    // sites (most of the large radii) and finished jobs issue no vector
+    // memory requests (the address path is the kernel's bound); a job's 8
+    // lanes share both conditions, so each group's DPP sum stays whole
+    MvRate mr = {0, 0, 0};
+    if (vl && active) mr = mvsad_rate(c, rl, cl_);
     uint32_t mine = 0;
 #pragma unroll
     for (int t = 0; t < 8; ++t) {
       const int r = row + site_dr(t) * rad, cc = col + site_dc(t) * rad;
       const bool v = cc >= c.col_min && cc <= c.col_max && r >= c.row_min && r <= c.row_max;
-      const uint32_t sd = lj_sad<SKIP>(c, s, l, v ? r : row, v ? cc : col);
+      uint32_t sd = 0;
+      if (v && active) sd = lj_sad<SKIP>(c, s, l, r, cc);
       mine = l == t ? sd : mine;
     }
     const uint32_t key =
