@@ -1568,7 +1568,7 @@ def main():
     # dominant kernel: the longer leg
     if do_c2 and (c2_ms >= c3_ms):
         roof = {"bound": "hbm",
-                "kernel": "lavish_txq_frame (14 txq_plane_kernel<W,H> over 3 streams)",
+                "kernel": "lavish_txq_frame (txq_multi_kernel<0> + <1>: one launch per VGPR class, 14 sizes)",
                 "achieved": round(c2_bytes / (c2_ms * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBS,
                 "unit": "GB/s", "traffic": traffic, "avg_launch_ms": round(c2_ms, 4),
                 "algorithmic_bytes_per_launch": c2_bytes}
