@@ -43,10 +43,13 @@ template <int W, int H>
 struct InvTile {
   static constexpr int MN = W < H ? W : H;
   static constexpr int P = 64 / MN;            // blocks per wave
-  static constexpr int RPT = H / MN;           // row transforms per lane
   static constexpr int CPT = W / MN;           // column transforms per lane
   static constexpr int KW = W > 32 ? 32 : W;   // stored coefficient columns
   static constexpr int KH = H > 32 ? 32 : H;   // stored coefficient rows
+  // row transforms per lane: only the KH stored rows (rows >= 32 of a
+  // 64-high block hold zero coefficients, so their row outputs are zero and
+  // the column transforms take them as compile-time zeros)
+  static constexpr int RPT = (P * KH + 63) / 64;
   static constexpr int NC = KW * KH;           // stored words per block
   static constexpr int T1S = W + 1;
 };
@@ -60,7 +63,7 @@ __global__ __launch_bounds__(64) void inv_tile_kernel(const int32_t* __restrict_
   using B = Bd<BDI>;
   constexpr int P = T::P, T1S = T::T1S;
   __shared__ int32_t cf[P * T::NC];
-  __shared__ int32_t t1[P * H * T1S];
+  __shared__ int32_t t1[P * T::KH * T1S];   // rows >= KH are zero, not stored
   __shared__ InvJob jb[P];
 
   const int lane = threadIdx.x;
@@ -85,9 +88,10 @@ __global__ __launch_bounds__(64) void inv_tile_kernel(const int32_t* __restrict_
 #pragma unroll
   for (int k = 0; k < T::RPT; ++k) {
     const int idx = k * 64 + lane;
-    const int b = idx / H, r = idx - b * H;
-    const int mine = jb[b].tx_type;
-    bool pending = true;
+    const int b = idx / T::KH, r = idx - b * T::KH;
+    const bool live = (P * T::KH) % 64 == 0 || idx < P * T::KH;
+    const int mine = live ? jb[b].tx_type : 0;
+    bool pending = live;
     while (__ballot(pending)) {
       if (pending) {
         const int t = __builtin_amdgcn_readfirstlane(mine);
@@ -98,13 +102,13 @@ __global__ __launch_bounds__(64) void inv_tile_kernel(const int32_t* __restrict_
           int32_t in[W], out[W];
 #pragma unroll
           for (int c = 0; c < W; ++c) {
-            int32_t v = (c < T::KW && r < T::KH) ? cf[b * T::NC + c * T::KH + r] : 0;
+            int32_t v = c < T::KW ? cf[b * T::NC + c * T::KH + r] : 0;
             if constexpr (C::rect2) v = rshift64((int64_t)v * 2896, 12);
             in[c] = clamp_bits<B::clamp_in_row>(v);
           }
           inv_1d<W, 12, B::rng_row>(kr, in, out);
 #pragma unroll
-          for (int c = 0; c < W; ++c) t1[(b * H + r) * T1S + c] = rshift_r(out[c], -C::is0);
+          for (int c = 0; c < W; ++c) t1[(b * T::KH + r) * T1S + c] = rshift_r(out[c], -C::is0);
         }
       }
     }
@@ -131,7 +135,7 @@ __global__ __launch_bounds__(64) void inv_tile_kernel(const int32_t* __restrict_
           int32_t in[H], out[H];
 #pragma unroll
           for (int r = 0; r < H; ++r)
-            in[r] = clamp_bits<B::clamp_in_col>(t1[(b * H + r) * T1S + cc]);
+            in[r] = r < T::KH ? clamp_bits<B::clamp_in_col>(t1[(b * T::KH + r) * T1S + cc]) : 0;
           inv_1d<H, 12, B::rng_col>(kc, in, out);
           if (jb[b].eob != 0) {
             PIX* d = dst + jb[b].dst_off + c;
