@@ -54,10 +54,11 @@ struct InvTile {
   static constexpr int T1S = W + 1;
 };
 
+// one tile: the P jobs from j0
 template <int W, int H, int BDI, typename PIX>
-__global__ __launch_bounds__(64) void inv_tile_kernel(const int32_t* __restrict__ dq,
-                                                      const InvJob* __restrict__ jobs, int njobs,
-                                                      PIX* __restrict__ dst, int stride) {
+__device__ __forceinline__ void inv_tile(const int32_t* __restrict__ dq,
+                                         const InvJob* __restrict__ jobs, int njobs, int j0,
+                                         PIX* __restrict__ dst, int stride) {
   using T = InvTile<W, H>;
   using C = TxCfg<W, H>;
   using B = Bd<BDI>;
@@ -67,13 +68,16 @@ __global__ __launch_bounds__(64) void inv_tile_kernel(const int32_t* __restrict_
   __shared__ InvJob jb[P];
 
   const int lane = threadIdx.x;
-  const int j0 = blockIdx.x * P;
+  __syncthreads();  // the previous tile's readers of jb / cf / t1 are done
   if (lane < P) {
     InvJob z{};
     z.eob = 0;
     jb[lane] = (j0 + lane < njobs) ? jobs[j0 + lane] : z;
   }
   __syncthreads();
+  // eob 0 adds nothing (av1_inverse_transform_block returns, idct.c:308): a
+  // tile without a coded block leaves before any load or transform
+  if (!__builtin_amdgcn_ballot_w64(lane < P && jb[lane < P ? lane : 0].eob != 0)) return;
   // stage the tile's dequantized coefficients (coalesced within a block)
   for (int i = lane; i < P * T::NC; i += 64) {
     const int b = i / T::NC, w = i - b * T::NC;
@@ -152,26 +156,58 @@ __global__ __launch_bounds__(64) void inv_tile_kernel(const int32_t* __restrict_
   }
 }
 
+// njobs jobs as one list, or -- when slot_cnt is given -- a job list built on
+// the device in slots of slot_cap jobs (C4: one slot per SB, its chosen
+// coded blocks first, slot_cnt[slot] of them): the grid strides over the
+// tiles, a tile never straddles two slots, and tiles past a slot's count
+// are skipped
 template <int W, int H, int BDI, typename PIX>
-void launch(const int32_t* dq, const LavishInvJob* jobs, int njobs, PIX* dst, int stride,
-            hipStream_t s) {
+__global__ __launch_bounds__(64) void inv_tile_kernel(const int32_t* __restrict__ dq,
+                                                      const InvJob* __restrict__ jobs, int njobs,
+                                                      const uint16_t* __restrict__ slot_cnt,
+                                                      int slot_cap, PIX* __restrict__ dst,
+                                                      int stride) {
   constexpr int P = InvTile<W, H>::P;
-  hipLaunchKernelGGL((inv_tile_kernel<W, H, BDI, PIX>), dim3((njobs + P - 1) / P), dim3(64), 0,
-                     s, dq, (const InvJob*)jobs, njobs, dst, stride);
+  const int tps = slot_cnt ? (slot_cap + P - 1) / P : 1;  // tiles per slot
+  const int ntiles = slot_cnt ? (njobs / slot_cap) * tps : (njobs + P - 1) / P;
+  for (int t = blockIdx.x; t < ntiles; t += gridDim.x) {
+    if (slot_cnt) {
+      const int sl = t / tps, k = t - sl * tps;
+      const int c = slot_cnt[sl];
+      if (k * P >= c) continue;
+      inv_tile<W, H, BDI, PIX>(dq, jobs, sl * slot_cap + c, sl * slot_cap + k * P, dst, stride);
+    } else {
+      inv_tile<W, H, BDI, PIX>(dq, jobs, njobs, t * P, dst, stride);
+    }
+  }
+}
+
+// slotted lists: at most this many workgroups, looping over the tiles
+constexpr int kInvMaxGrid = 4096;
+
+template <int W, int H, int BDI, typename PIX>
+void launch(const int32_t* dq, const LavishInvJob* jobs, int njobs, const uint16_t* slot_cnt,
+            int slot_cap, PIX* dst, int stride, hipStream_t s) {
+  constexpr int P = InvTile<W, H>::P;
+  int grid = slot_cnt ? (njobs / slot_cap) * ((slot_cap + P - 1) / P) : (njobs + P - 1) / P;
+  if (slot_cnt != nullptr && grid > kInvMaxGrid) grid = kInvMaxGrid;
+  if (grid == 0) return;
+  hipLaunchKernelGGL((inv_tile_kernel<W, H, BDI, PIX>), dim3(grid), dim3(64), 0, s, dq,
+                     (const InvJob*)jobs, njobs, slot_cnt, slot_cap, dst, stride);
 }
 
 template <int W, int H>
-int dispatch_bd(const int32_t* dq, const LavishInvJob* jobs, int njobs, void* dst, int stride,
-                int bd, int highbd, hipStream_t s) {
+int dispatch_bd(const int32_t* dq, const LavishInvJob* jobs, int njobs, const uint16_t* slot_cnt,
+                int slot_cap, void* dst, int stride, int bd, int highbd, hipStream_t s) {
   if (!highbd) {
     if (bd != 8) return -4;
-    launch<W, H, 0, uint8_t>(dq, jobs, njobs, (uint8_t*)dst, stride, s);
+    launch<W, H, 0, uint8_t>(dq, jobs, njobs, slot_cnt, slot_cap, (uint8_t*)dst, stride, s);
   } else if (bd == 8) {
-    launch<W, H, 0, uint16_t>(dq, jobs, njobs, (uint16_t*)dst, stride, s);
+    launch<W, H, 0, uint16_t>(dq, jobs, njobs, slot_cnt, slot_cap, (uint16_t*)dst, stride, s);
   } else if (bd == 10) {
-    launch<W, H, 1, uint16_t>(dq, jobs, njobs, (uint16_t*)dst, stride, s);
+    launch<W, H, 1, uint16_t>(dq, jobs, njobs, slot_cnt, slot_cap, (uint16_t*)dst, stride, s);
   } else if (bd == 12) {
-    launch<W, H, 2, uint16_t>(dq, jobs, njobs, (uint16_t*)dst, stride, s);
+    launch<W, H, 2, uint16_t>(dq, jobs, njobs, slot_cnt, slot_cap, (uint16_t*)dst, stride, s);
   } else {
     return -4;
   }
@@ -181,29 +217,31 @@ int dispatch_bd(const int32_t* dq, const LavishInvJob* jobs, int njobs, void* ds
 }  // namespace
 
 int inv_txfm_add_batch(const int32_t* dq, int tx_size, const LavishInvJob* jobs, int njobs,
-                       void* dst, int stride, int bd, int highbd, hipStream_t s) {
+                       void* dst, int stride, int bd, int highbd, hipStream_t s,
+                       const uint16_t* slot_cnt, int slot_cap) {
+  if (slot_cnt != nullptr && (slot_cap <= 0 || njobs % slot_cap)) return -3;
   if (njobs <= 0) return 0;
   int rc;
   switch (tx_size) {
-    case 0: rc = dispatch_bd<4, 4>(dq, jobs, njobs, dst, stride, bd, highbd, s); break;
-    case 1: rc = dispatch_bd<8, 8>(dq, jobs, njobs, dst, stride, bd, highbd, s); break;
-    case 2: rc = dispatch_bd<16, 16>(dq, jobs, njobs, dst, stride, bd, highbd, s); break;
-    case 3: rc = dispatch_bd<32, 32>(dq, jobs, njobs, dst, stride, bd, highbd, s); break;
-    case 4: rc = dispatch_bd<64, 64>(dq, jobs, njobs, dst, stride, bd, highbd, s); break;
-    case 5: rc = dispatch_bd<4, 8>(dq, jobs, njobs, dst, stride, bd, highbd, s); break;
-    case 6: rc = dispatch_bd<8, 4>(dq, jobs, njobs, dst, stride, bd, highbd, s); break;
-    case 7: rc = dispatch_bd<8, 16>(dq, jobs, njobs, dst, stride, bd, highbd, s); break;
-    case 8: rc = dispatch_bd<16, 8>(dq, jobs, njobs, dst, stride, bd, highbd, s); break;
-    case 9: rc = dispatch_bd<16, 32>(dq, jobs, njobs, dst, stride, bd, highbd, s); break;
-    case 10: rc = dispatch_bd<32, 16>(dq, jobs, njobs, dst, stride, bd, highbd, s); break;
-    case 11: rc = dispatch_bd<32, 64>(dq, jobs, njobs, dst, stride, bd, highbd, s); break;
-    case 12: rc = dispatch_bd<64, 32>(dq, jobs, njobs, dst, stride, bd, highbd, s); break;
-    case 13: rc = dispatch_bd<4, 16>(dq, jobs, njobs, dst, stride, bd, highbd, s); break;
-    case 14: rc = dispatch_bd<16, 4>(dq, jobs, njobs, dst, stride, bd, highbd, s); break;
-    case 15: rc = dispatch_bd<8, 32>(dq, jobs, njobs, dst, stride, bd, highbd, s); break;
-    case 16: rc = dispatch_bd<32, 8>(dq, jobs, njobs, dst, stride, bd, highbd, s); break;
-    case 17: rc = dispatch_bd<16, 64>(dq, jobs, njobs, dst, stride, bd, highbd, s); break;
-    case 18: rc = dispatch_bd<64, 16>(dq, jobs, njobs, dst, stride, bd, highbd, s); break;
+    case 0: rc = dispatch_bd<4, 4>(dq, jobs, njobs, slot_cnt, slot_cap, dst, stride, bd, highbd, s); break;
+    case 1: rc = dispatch_bd<8, 8>(dq, jobs, njobs, slot_cnt, slot_cap, dst, stride, bd, highbd, s); break;
+    case 2: rc = dispatch_bd<16, 16>(dq, jobs, njobs, slot_cnt, slot_cap, dst, stride, bd, highbd, s); break;
+    case 3: rc = dispatch_bd<32, 32>(dq, jobs, njobs, slot_cnt, slot_cap, dst, stride, bd, highbd, s); break;
+    case 4: rc = dispatch_bd<64, 64>(dq, jobs, njobs, slot_cnt, slot_cap, dst, stride, bd, highbd, s); break;
+    case 5: rc = dispatch_bd<4, 8>(dq, jobs, njobs, slot_cnt, slot_cap, dst, stride, bd, highbd, s); break;
+    case 6: rc = dispatch_bd<8, 4>(dq, jobs, njobs, slot_cnt, slot_cap, dst, stride, bd, highbd, s); break;
+    case 7: rc = dispatch_bd<8, 16>(dq, jobs, njobs, slot_cnt, slot_cap, dst, stride, bd, highbd, s); break;
+    case 8: rc = dispatch_bd<16, 8>(dq, jobs, njobs, slot_cnt, slot_cap, dst, stride, bd, highbd, s); break;
+    case 9: rc = dispatch_bd<16, 32>(dq, jobs, njobs, slot_cnt, slot_cap, dst, stride, bd, highbd, s); break;
+    case 10: rc = dispatch_bd<32, 16>(dq, jobs, njobs, slot_cnt, slot_cap, dst, stride, bd, highbd, s); break;
+    case 11: rc = dispatch_bd<32, 64>(dq, jobs, njobs, slot_cnt, slot_cap, dst, stride, bd, highbd, s); break;
+    case 12: rc = dispatch_bd<64, 32>(dq, jobs, njobs, slot_cnt, slot_cap, dst, stride, bd, highbd, s); break;
+    case 13: rc = dispatch_bd<4, 16>(dq, jobs, njobs, slot_cnt, slot_cap, dst, stride, bd, highbd, s); break;
+    case 14: rc = dispatch_bd<16, 4>(dq, jobs, njobs, slot_cnt, slot_cap, dst, stride, bd, highbd, s); break;
+    case 15: rc = dispatch_bd<8, 32>(dq, jobs, njobs, slot_cnt, slot_cap, dst, stride, bd, highbd, s); break;
+    case 16: rc = dispatch_bd<32, 8>(dq, jobs, njobs, slot_cnt, slot_cap, dst, stride, bd, highbd, s); break;
+    case 17: rc = dispatch_bd<16, 64>(dq, jobs, njobs, slot_cnt, slot_cap, dst, stride, bd, highbd, s); break;
+    case 18: rc = dispatch_bd<64, 16>(dq, jobs, njobs, slot_cnt, slot_cap, dst, stride, bd, highbd, s); break;
     default: return -1;
   }
   if (rc == 0) LAVISH_CHECK(hipGetLastError());

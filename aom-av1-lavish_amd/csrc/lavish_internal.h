@@ -42,9 +42,12 @@ int txq_plane_64(const int16_t* residual, int stride, int width, int height, int
                  int32_t* qcoeff, int32_t* dqcoeff, uint16_t* eob, int32_t* coeff,
                  hipStream_t s);
 
-// inverse transform batch (inv.hip)
+// inverse transform batch (inv.hip); slot_cnt (device, nullable): the job
+// list is njobs / slot_cap slots of slot_cap jobs, of which the first
+// slot_cnt[slot] are live (job lists built on the device)
 int inv_txfm_add_batch(const int32_t* dq, int tx_size, const LavishInvJob* jobs, int njobs,
-                       void* dst, int stride, int bd, int highbd, hipStream_t s);
+                       void* dst, int stride, int bd, int highbd, hipStream_t s,
+                       const uint16_t* slot_cnt = nullptr, int slot_cap = 0);
 // the coefficient-rate decision (lavish_rdo_plane_rate): device CoeffCosts,
 // per-block TXB_CTX (nullable) and get_tx_type_cost per tx type (host, nullable)
 struct RateCfg {

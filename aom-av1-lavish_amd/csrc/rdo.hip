@@ -861,16 +861,24 @@ struct SbArgs {
   int nsizes;
   int sizes[19];                       // candidate order: largest area first
   const LavishRdoBlock* rec[19];
+  LavishInvJob* jobs[19];              // per size: one slot of `cap` jobs per SB
+  uint16_t* cnt[19];                   // per size and SB: its live jobs
   int sbw, sbh;                        // superblocks per row / column
-  int width, height;
+  int width, height, stride;
   uint8_t* sb_tx_size;
 };
 
 // per SB64: the candidate TX size whose blocks' summed RD cost is lowest
 // (sizes that do not tile the SB with full blocks are skipped; ties keep
-// the earlier, larger size)
+// the earlier, larger size), then the inverse-transform jobs of that size's
+// blocks with eob > 0 -- a block with eob 0 adds nothing
+// (av1_inverse_transform_block, idct.c:308) and the other sizes' blocks are
+// not reconstructed at all.
 // One wave64 per SB: lanes stride the SB's blocks of a size, a 64-bit xor
 // reduction sums their costs; the size scan stays sequential (strict <).
+// Jobs go to the SB's own slot of each size's list (no atomics, nothing to
+// zero first): the chosen size's coded blocks, compacted by ballot, and a
+// count of 0 in every other size's slot.
 __global__ __launch_bounds__(256) void sb_decide_kernel(SbArgs a) {
   const int sb = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
@@ -898,24 +906,38 @@ __global__ __launch_bounds__(256) void sb_decide_kernel(SbArgs a) {
       best_s = s;
     }
   }
-  if (lane == 0) a.sb_tx_size[sb] = (uint8_t)best_s;
-}
-
-// inverse-transform jobs of one size: the block's best type / eob where its
-// SB chose this size, eob 0 (untouched) elsewhere
-__global__ void inv_jobs_kernel(int s, const LavishRdoBlock* rec, int nblocks, int bw, int stride,
-                                int sbw, const uint8_t* sb_tx_size, LavishInvJob* jobs) {
-  const int blk = blockIdx.x * blockDim.x + threadIdx.x;
-  if (blk >= nblocks) return;
+  if (lane == 0) {
+    a.sb_tx_size[sb] = (uint8_t)best_s;
+    for (int i = 0; i < a.nsizes; ++i)
+      if (a.sizes[i] != best_s) a.cnt[a.sizes[i]][sb] = 0;
+  }
+  if (best_s == 255) return;  // no candidate tiles this SB: recon = pred
+  const int s = best_s;
   const int W = tx_w_dev(s), H = tx_h_dev(s);
-  const int by = blk / bw, bx = blk - by * bw;
-  const int y = by * H, x = bx * W;
-  LavishInvJob j;
-  j.dst_off = (int64_t)y * stride + x;
-  j.coeff_off = (int64_t)blk * max_eob_dev(s);
-  j.tx_type = rec[blk].best_type;
-  j.eob = sb_tx_size[(y / 64) * sbw + x / 64] == s ? rec[blk].eob : 0;
-  jobs[blk] = j;
+  const int bw = a.width / W, nx = x1 / W, nblk = nx * (y1 / H), n = max_eob_dev(s);
+  LavishInvJob* const slot = a.jobs[s] + (size_t)sb * ((64 / W) * (64 / H));
+  int base = 0;
+  for (int k0 = 0; k0 < nblk; k0 += 64) {
+    const int k = k0 + lane;
+    const int y = k / nx, x = k - y * nx;
+    const int blk = (sy * 64 / H + y) * bw + sx * 64 / W + x;
+    const bool live = k < nblk;
+    const LavishRdoBlock r = a.rec[s][live ? blk : 0];
+    const bool coded = live && r.eob != 0;
+    const uint64_t m = __builtin_amdgcn_ballot_w64(coded);
+    if (coded) {
+      const int at = base + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                                      __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
+      LavishInvJob j;
+      j.dst_off = (int64_t)(sy * 64 + y * H) * a.stride + sx * 64 + x * W;
+      j.coeff_off = (int64_t)blk * n;
+      j.tx_type = r.best_type;
+      j.eob = r.eob;
+      slot[at] = j;
+    }
+    base += __popcll(m);
+  }
+  if (lane == 0) a.cnt[s][sb] = (uint16_t)base;
 }
 
 // inverse-transform job list of lavish_rdo_reconstruct: reused call after
@@ -1050,28 +1072,39 @@ int rdo_reconstruct(uint32_t size_mask, const LavishRdoBlock* const* rec,
   a.sbh = (height + 63) / 64;
   a.width = width;
   a.height = height;
+  a.stride = stride;
   a.sb_tx_size = sb_tx_size;
+  // scratch: per candidate size one slot of (64 / w) x (64 / h) jobs per SB
+  // and the SBs' job counts
   const int nsb = a.sbw * a.sbh;
+  size_t joff[19] = {}, coff[19] = {}, bytes = 0;
+  for (int i = 0; i < a.nsizes; ++i) {
+    const int t = a.sizes[i];
+    joff[t] = bytes;
+    bytes += (size_t)nsb * (64 / tx_w(t)) * (64 / tx_h(t)) * sizeof(LavishInvJob);
+  }
+  for (int i = 0; i < a.nsizes; ++i) {
+    const int t = a.sizes[i];
+    coff[t] = bytes;
+    bytes += ((size_t)nsb * sizeof(uint16_t) + 15) & ~(size_t)15;
+  }
+  char* scratch = (char*)t_rs.acquire(bytes, s);
+  for (int i = 0; i < a.nsizes; ++i) {
+    const int t = a.sizes[i];
+    a.jobs[t] = (LavishInvJob*)(scratch + joff[t]);
+    a.cnt[t] = (uint16_t*)(scratch + coff[t]);
+  }
   hipLaunchKernelGGL(sb_decide_kernel, dim3((nsb + 3) / 4), dim3(256), 0, s, a);
   LAVISH_CHECK(hipGetLastError());
-  // recon = pred, then add the chosen blocks' residuals size by size
+  // recon = pred, then add the chosen coded blocks' residuals size by size
   LAVISH_CHECK(hipMemcpy2DAsync(recon, (size_t)stride * 2, pred, (size_t)stride * 2,
                                 (size_t)width * 2, height, hipMemcpyDeviceToDevice, s));
-  size_t maxb = 0;
   for (int i = 0; i < a.nsizes; ++i) {
     const int t = a.sizes[i];
-    maxb = max(maxb, (size_t)(width / tx_w(t)) * (height / tx_h(t)));
-  }
-  LavishInvJob* jobs = (LavishInvJob*)t_rs.acquire(maxb * sizeof(LavishInvJob), s);
-  for (int i = 0; i < a.nsizes; ++i) {
-    const int t = a.sizes[i];
-    const int bw = width / tx_w(t);
-    const int nb = bw * (height / tx_h(t));
-    if (nb == 0) continue;
-    hipLaunchKernelGGL(inv_jobs_kernel, dim3((nb + 255) / 256), dim3(256), 0, s, t, rec[t], nb,
-                       bw, stride, a.sbw, sb_tx_size, jobs);
-    LAVISH_CHECK(hipGetLastError());
-    const int rc = inv_txfm_add_batch(dqcoeff[t], t, jobs, nb, recon, stride, bd, 1, s);
+    if ((width / tx_w(t)) * (height / tx_h(t)) == 0) continue;
+    const int cap = (64 / tx_w(t)) * (64 / tx_h(t));
+    const int rc = inv_txfm_add_batch(dqcoeff[t], t, a.jobs[t], nsb * cap, recon, stride, bd, 1,
+                                      s, a.cnt[t], cap);
     if (rc) {
       t_rs.release(s);
       return rc;

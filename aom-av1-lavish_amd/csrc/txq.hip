@@ -614,7 +614,16 @@ static FrameStreams& frame_streams() {
   return t_fs;
 }
 
-int fan_width() { return kFrameStreams; }
+// LAVISH_FAN_STREAMS=1: every size on the caller's stream (isolated
+// per-kernel timings under a profiler); default kFrameStreams
+int fan_width() {
+  static const int w = [] {
+    const char* e = getenv("LAVISH_FAN_STREAMS");
+    const int v = e ? atoi(e) : kFrameStreams;
+    return v < 1 ? 1 : (v > kFrameStreams ? kFrameStreams : v);
+  }();
+  return w;
+}
 
 // fork: the internal streams wait for everything queued on `caller`; slot 0
 // is the caller itself

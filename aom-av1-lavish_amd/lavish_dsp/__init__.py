@@ -535,7 +535,7 @@ class RdoFrame:
     """Per-size outputs of rdo_frame + the reconstruction buffers, allocated
     once for a plane shape and reused every call."""
 
-    def __init__(self, src, type_masks=None):
+    def __init__(self, src, type_masks=None, recon=None):
         import torch
         self.type_masks = dict(type_masks or C4_TYPE_MASKS)
         self.sizes = sorted(self.type_masks)
@@ -551,7 +551,13 @@ class RdoFrame:
         H, W = src.shape
         # the reconstruction keeps the planes' row stride (a view of a wider
         # buffer when src is a column segment of a frame)
-        self.recon = torch.empty((H, src.stride(0)), dtype=src.dtype, device=src.device)[:, :W]
+        if recon is not None:  # the caller's plane (e.g. a view of a whole frame)
+            assert recon.shape == src.shape and recon.stride(0) == src.stride(0) \
+                and recon.stride(1) == 1 and recon.dtype == src.dtype
+            self.recon = recon
+        else:
+            self.recon = torch.empty((H, src.stride(0)), dtype=src.dtype,
+                                     device=src.device)[:, :W]
         self.sb_tx_size = torch.empty(((W + 63) // 64) * ((H + 63) // 64), dtype=torch.uint8,
                                       device=src.device)
 

@@ -66,7 +66,8 @@ def partition(height, width, world):
     column segment of the L = R mod G leftover rows -- leftover row i is cut
     into n_i = G (i + 1) // L - G i // L segments (whole SBs, widths within
     one SB), so the G segments go one per rank.  When L divides G every rank
-    gets exactly R / G rows of work (4K: 34 rows = 8 x (4 + 1/4))."""
+    gets exactly R / G rows of work (4K: 34 rows = 8 x (4 + 1/4)).  A leftover
+    row is never cut finer than its C SB columns (ranks beyond get no tail)."""
     R, C = sb_rows(height), sb_cols(width)
     full = R // world
     L = R - full * world
@@ -77,11 +78,14 @@ def partition(height, width, world):
         if L:
             row = next(i for i in range(L) if g < world * (i + 1) // L)
             first = world * row // L
-            segs = world * (row + 1) // L - first
+            # at most one segment per SB column: on a frame narrower than
+            # the segment count the surplus ranks get no tail
+            segs = min(world * (row + 1) // L - first, C)
             k = g - first
-            c0, c1 = C * k // segs, C * (k + 1) // segs
-            y0 = (full * world + row) * SB
-            tail = (y0, min(y0 + SB, height), c0 * SB, min(c1 * SB, width))
+            if k < segs:
+                c0, c1 = C * k // segs, C * (k + 1) // segs
+                y0 = (full * world + row) * SB
+                tail = (y0, min(y0 + SB, height), c0 * SB, min(c1 * SB, width))
         out.append((band, tail))
     return out
 
@@ -145,23 +149,29 @@ def sharded_frame(height, width, rank, world, process_rect, group=None, like=Non
 
 
 def wavefront_frame(height, width, rank, world, process_rect, chunks=4, edge_rows=4,
-                    p2p_group=None, gather_group=None, dtype=None, device=None, log=None):
+                    p2p_group=None, gather_group=None, dtype=None, device=None, log=None,
+                    out=None):
     """The row-wavefront form: SB row r on rank r % G, processed in `chunks`
     column chunks; chunk c of row r waits for the bottom `edge_rows` pixel
     rows of row r - 1 up to chunk c + 1 (point-to-point from rank
-    (r - 1) % G, which sends each chunk's edge when it is done); after each
-    wave of G rows the wave's rows are all-gathered.  Returns the whole
-    reconstructed frame (identical on every rank).  The edges and the
+    (r - 1) % G, which sends each chunk's edge when it is done) and hands
+    them to the chunk: process_rect(y0, y1, x0, x1, above=E) with E the
+    [edge_rows, x0 : x1 + the next chunk] pixels above the chunk (None on row
+    0) -- what the next row's intra prediction reads (above and above-right);
+    after each wave of G rows the wave's rows are all-gathered.  Returns the
+    whole reconstructed frame (identical on every rank).  The edges and the
     gathers must use different process groups (communicators): a rank's
     receive for the next wave must not queue behind its pending gather of
-    this one, which waits for the sender.  log: optional list that receives
-    ('recv', row, chunk) / ('send', row, chunk) events."""
+    this one, which waits for the sender.  out: the frame buffer to fill
+    (process_rect may return views of it, then nothing is copied).  log:
+    optional list that receives ('recv', row, chunk) / ('send', row, chunk)
+    events."""
     import torch
     import torch.distributed as dist
     R, C = sb_rows(height), sb_cols(width)
     chunks = max(1, min(chunks, C))
     cx = [min(C * k // chunks * SB, width) for k in range(chunks + 1)]
-    full = torch.zeros((height, width), dtype=dtype, device=device)
+    full = out if out is not None else torch.zeros((height, width), dtype=dtype, device=device)
     nxt, prv = (rank + 1) % world, (rank - 1) % world
     pending = []   # outstanding sends
     gathers = []
@@ -170,30 +180,36 @@ def wavefront_frame(height, width, rank, world, process_rect, chunks=4, edge_row
         mine = w0 + rank if w0 + rank < R else None
         if mine is not None:
             y0, y1 = mine * SB, min((mine + 1) * SB, height)
-            got = 0   # chunks of the row above received
+            edges = []   # the row above's bottom edge, chunk by chunk as received
             for c in range(chunks):
                 # above-right: the row above's chunks 0 .. c + 1 (ethread.c
                 # sync_range; the reference's own row-above dependency)
                 need = min(c + 2, chunks) if mine > 0 else 0
-                while got < need:
-                    edge = torch.empty((edge_rows, cx[got + 1] - cx[got]), dtype=dtype,
-                                       device=device)
+                while len(edges) < need:
+                    got = len(edges)
                     if world > 1:
+                        edge = torch.empty((edge_rows, cx[got + 1] - cx[got]), dtype=full.dtype,
+                                           device=full.device)
                         dist.recv(edge.view(torch.uint8), src=prv, group=p2p_group)
-                    else:
-                        edge.copy_(full[y0 - edge_rows:y0, cx[got]:cx[got + 1]])
-                    full[y0 - edge_rows:y0, cx[got]:cx[got + 1]] = edge
+                    else:  # the row above is this rank's own, already in the frame
+                        edge = full[y0 - edge_rows:y0, cx[got]:cx[got + 1]]
+                    edges.append(edge)
                     if log is not None:
                         log.append(("recv", mine - 1, got))
-                    got += 1
-                rec = process_rect(y0, y1, cx[c], cx[c + 1])
-                full[y0:y1, cx[c]:cx[c + 1]] = rec
+                above = (torch.cat(edges[c:need], 1) if need - c > 1 else edges[c]) \
+                    if mine > 0 else None
+                rec = process_rect(y0, y1, cx[c], cx[c + 1], above=above)
+                dst = full[y0:y1, cx[c]:cx[c + 1]]
+                if rec.data_ptr() != dst.data_ptr():
+                    dst.copy_(rec)
                 if mine + 1 < R and world > 1:
                     e = rec[rec.shape[0] - edge_rows:].contiguous()
                     pending.append((dist.isend(e.view(torch.uint8), dst=nxt, group=p2p_group),
                                     e))
                     if log is not None:
                         log.append(("send", mine, c))
+        if world == 1:
+            continue  # every row is already in the frame
         # the wave's rows: one SB row per rank (the per-row all-gather)
         rects = [(r * SB, min((r + 1) * SB, height), 0, width) for r in wave] + \
             [None] * (world - len(wave))
@@ -206,13 +222,17 @@ def wavefront_frame(height, width, rank, world, process_rect, chunks=4, edge_row
     return full
 
 
-def c4_rect_processor(src, pred, qp, rdmult, bit_depth, frames):
+def c4_rect_processor(src, pred, qp, rdmult, bit_depth, frames, out=None):
     """process_rect for the GPU path: lavish_rdo_frame + reconstruct on the
     rectangle [y0, y1) x [x0, x1) of device planes (views keep the planes'
-    stride).  `frames` caches the RdoFrame output buffers per rectangle."""
+    stride).  `frames` caches the RdoFrame output buffers per rectangle.  out
+    (optional, a frame-sized plane with src's stride): each rectangle's
+    reconstruction is written straight into its view of it.  `above` (the
+    wavefront's received edge) is accepted and not read: C4 as defined takes
+    its prediction as input, so no intra predictor consumes it here."""
     import lavish_dsp as L
 
-    def run(y0, y1, x0, x1):
+    def run(y0, y1, x0, x1, above=None):
         s, p = src[y0:y1, x0:x1], pred[y0:y1, x0:x1]
         key = (y0, y1, x0, x1)
         if key not in frames:
@@ -221,7 +241,8 @@ def c4_rect_processor(src, pred, qp, rdmult, bit_depth, frames):
             # that do not tile the SB, so the result is the whole frame's)
             masks = {t: m for t, m in L.C4_TYPE_MASKS.items()
                      if L.TX_W[t] <= x1 - x0 and L.TX_H[t] <= y1 - y0}
-            frames[key] = L.RdoFrame(s, masks)
+            frames[key] = L.RdoFrame(s, masks,
+                                     recon=out[y0:y1, x0:x1] if out is not None else None)
         fr = frames[key]
         L.rdo_frame(s, p, fr, qp, rdmult, bit_depth)
         return fr.recon

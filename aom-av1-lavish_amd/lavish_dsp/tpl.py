@@ -234,7 +234,12 @@ class TplFrame:
                            "sync": torch.empty(int(_lib.lavish_tpl_motion_sync_ints(
                                self.nrefs, self.rows)), dtype=torch.int32, device=device)}
 
-    def step(self, stream=None, ref_costs=True):
+    def step(self, stream=None, ref_costs=True, check=True):
+        """One TPL frame leg.  check (default): wait for the frame and raise
+        if a wavefront wait timed out -- such a frame's start mvs are not the
+        reference's (the kernel skips the unpublished neighbour and counts
+        it); check=False leaves the frame asynchronous, and the caller must
+        call check() before using the results."""
         bs = TPL_BSIZE
         if self.neighbour_starts:
             tpl_motion_search(self.src, self.refs, self.jobs, self.cols, self.rows, self.nrefs,
@@ -254,4 +259,12 @@ class TplFrame:
         tpl_block_batch(self.src_view, self.preds, bs, 8, self.qp, out=self.out,
                         recon=self.recon, ref_costs=self.costs if ref_costs else None,
                         stream=stream)
+        if check:
+            self.check()
         return self.out
+
+    def check(self):
+        """Raise if the last wavefront's waits timed out (synchronises)."""
+        if self.neighbour_starts and tpl_motion_failures(self.mv_out):
+            raise RuntimeError("tpl motion wavefront: %d wait(s) timed out; the frame's start "
+                               "mvs are invalid" % tpl_motion_failures(self.mv_out))

@@ -77,6 +77,8 @@ def parse():
     ap.add_argument("--border", type=int, default=160)
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--c5-chunks", type=int, default=4,
+                    help="c5 wavefront: column chunks per SB row")
     ap.add_argument("--c5-form", choices=("band", "wavefront"), default="band",
                     help="C5 sharding: balanced band + tail segments with overlapped "
                          "all-gathers, or the row-wavefront with p2p edges (lavish_dsp/shard.py)")
@@ -193,17 +195,21 @@ def cpu_baseline(args):
                       % (passes, W, Hs, sb, args.workload, threads, dt)}
 
 
-def c4_algorithmic_bytes(L, W, H):
+def c4_algorithmic_bytes(L, W, H, coded=None):
     """C4 bytes per frame (decision mode): per candidate size
     src + pred read once (2 x 2 B / pixel), the winner's qcoeff + dqcoeff
-    (8 B / coefficient) and a 40 B decision record per block; then the
-    reconstruction reads pred and writes recon (4 B / pixel) and reads the
-    chosen dqcoeff (<= 4 B / pixel)."""
+    (8 B / coefficient) and a 40 B decision record per block, the decision's
+    read of each record's 8 B cost; then the reconstruction reads pred and
+    writes recon (4 B / pixel) and reads the dqcoeff of the chosen coded
+    blocks (`coded`: per size, per type counts, c4_coded_blocks; without it
+    every chosen block, <= 4 B / pixel)."""
     tot = 0
     for s in L.C4_TYPE_MASKS:
         nb = (W // L.TX_W[s]) * (H // L.TX_H[s])
-        tot += 4 * W * H + nb * (8 * L.max_eob(s) + 40)
-    return tot + 8 * W * H
+        tot += 4 * W * H + nb * (8 * L.max_eob(s) + 40 + 8)
+        if coded is not None:
+            tot += 4 * L.max_eob(s) * int(np.sum(coded.get(s, 0)))
+    return tot + (4 if coded is not None else 8) * W * H
 
 
 def cpu_baseline_c4(args):
@@ -235,26 +241,92 @@ def cpu_baseline_c4(args):
                       % (passes, W, sb, args.workload, threads, dt)}
 
 
-def c4_roofline(ms, W=3840, H=2160):
-    """C4 is VALU-bound (decision mode writes little: hbm_frac ~6 %), so its
-    roofline is int32 VALU lane-operations: the per-step SQ_INSTS_VALU of
-    every kernel of the step (wave instructions x 64 lanes), counted by a
-    rocprofv3 --pmc pass of `bench.py --workload c4` (tools/valu_summary.py ->
-    profiles/c4_valu.json), over the live event-timed step."""
-    if (W, H) != (3840, 2160) or not os.path.exists(C4_VALU_JSON):
+C4_OPS_JSON = os.path.join(ROOT, "profiles", "c4_ops.json")
+
+
+def c4_coded_blocks(L, fr):
+    """Per (size, type): the blocks the per-SB decision chose with eob > 0 --
+    the ones the reconstruction inverse-transforms (idct.c:308: eob 0 adds
+    nothing).  Read back after the timed region."""
+    sb = fr.sb_tx_size.cpu().numpy()
+    H, W = fr.recon.shape
+    sbw = (W + 63) // 64
+    out = {}
+    for s in fr.sizes:
+        w, h = L.TX_W[s], L.TX_H[s]
+        rec = fr.outs[s]["records"].cpu().numpy().view(L.RDO_DTYPE)
+        bw, bh = W // w, H // h
+        if bw * bh == 0:
+            continue
+        by, bx = np.divmod(np.arange(bw * bh), bw)
+        chosen = sb[(by * h // 64) * sbw + bx * w // 64] == s
+        coded = chosen & (rec["eob"] != 0)
+        out[s] = np.bincount(rec["best_type"][coded], minlength=16)
+    return out
+
+
+def c4_algorithmic_ops(W, H, masks, coded):
+    """Algorithmic int32 ops of the C4 step ("C4
+    algorithmic ops"), from profiles/c4_ops.json (tools/c4_ops.py: the
+    reference's 1-D bodies executed with a counting integer).  Per candidate
+    size s (w x h, n stored coefficients) and block:
+      subtract w h + sum over the mask's vertical kinds of fwd_col[v]
+      + sum over the mask's types t of (fwd_row[h(t)] + 41 n + 17) + 3
+    (41 per coefficient: quantize_fp 21, satd 2, block error 9,
+    rate_estimator 9; 17 per (block, type): distortion shift, RDCOST, select;
+    3: the per-SB sum), then per chosen coded block of type t:
+      inv_row[h(t)] + inv_col[v(t)]."""
+    c = json.load(open(C4_OPS_JSON))
+    vtx, htx = c["vtx"], c["htx"]
+    pc = sum(c["per_coefficient"].values())
+    pbt = c["per_block_type"]["dist_shift_rdcost_select"]
+    total = 0
+    for s, mask in masks.items():
+        z = c["sizes"][str(s)]
+        nb = (W // z["W"]) * (H // z["H"])
+        types = [t for t in range(16) if (mask >> t) & 1]
+        per = z["W"] * z["H"] + c["per_block_decide"]
+        per += sum(z["fwd_col"][str(v)] for v in sorted({vtx[t] for t in types}))
+        per += sum(z["fwd_row"][str(htx[t])] + pc * z["n"] + pbt for t in types)
+        total += nb * per
+        for t, k in enumerate(coded.get(s, [])):
+            if k:
+                total += int(k) * (z["inv_row"][str(htx[t])] + z["inv_col"][str(vtx[t])])
+    return total
+
+
+def c4_roofline(ms, W, H, masks, coded, nbytes):
+    """C4 is VALU-bound (decision mode writes little), so its roofline is
+    int32 VALU lane-operations: `frac` = the algorithmic op count
+    (c4_algorithmic_ops) over the live event-timed step against the VALU
+    peak; `issue_frac` = the issued SQ_INSTS_VALU x 64 lanes of a rocprofv3
+    --pmc pass (profiles/c4_valu.json, tools/valu_summary.py) over the same
+    time; `traffic_over_algorithmic` = that pass's HBM bytes (FETCH_SIZE x2 +
+    WRITE_SIZE) over the algorithmic bytes."""
+    if not os.path.exists(C4_OPS_JSON):
         return None
-    try:
-        v = json.load(open(C4_VALU_JSON))
-    except (ValueError, OSError):
-        return None
-    ops = float(v["valu_instr_per_step"]) * 64
+    ops = c4_algorithmic_ops(W, H, masks, coded)
     achieved = ops / (ms * 1e-3) / 1e12
-    return {"bound": "valu", "kernel": "all kernels of the C4 step (rdo_kernel x5 sizes + "
+    roof = {"bound": "valu", "kernel": "all kernels of the C4 step (rdo_kernel x5 sizes + "
             "sb_decide + reconstruction)", "achieved": round(achieved, 2),
             "peak": round(VALU_PEAK_TOPS, 1), "unit": "Tops (int32 lane-ops)",
-            "frac": round(achieved / VALU_PEAK_TOPS, 4), "traffic": v.get("hbm_bytes_per_step"),
-            "avg_launch_ms": round(ms, 4), "algorithmic_ops_per_launch": round(ops),
-            "counts": "profiles/c4_valu.json (%s)" % v.get("source", "")}
+            "frac": round(achieved / VALU_PEAK_TOPS, 4), "traffic": None,
+            "avg_launch_ms": round(ms, 4), "algorithmic_ops_per_launch": ops,
+            "ops": "algorithmic (DESIGN.md section 5; profiles/c4_ops.json)"}
+    if (W, H) == (3840, 2160) and os.path.exists(C4_VALU_JSON):
+        try:
+            v = json.load(open(C4_VALU_JSON))
+        except (ValueError, OSError):
+            v = None
+        if v is not None:
+            issued = float(v["valu_instr_per_step"]) * 64
+            roof["issue_frac"] = round(issued / (ms * 1e-3) / 1e12 / VALU_PEAK_TOPS, 4)
+            roof["issued_ops_per_launch"] = round(issued)
+            roof["traffic"] = v.get("hbm_bytes_per_step")
+            if roof["traffic"]:
+                roof["traffic_over_algorithmic"] = round(roof["traffic"] / nbytes, 3)
+            roof["counts"] = "profiles/c4_valu.json (%s)" % v.get("source", "")
+    return roof
 
 
 def c4_leg(L, steps, warmup, rdmult, qindex, W=3840, H=2160):
@@ -281,9 +353,11 @@ def c4_leg(L, steps, warmup, rdmult, qindex, W=3840, H=2160):
         ev[k][1].record(stream)
     torch.cuda.synchronize()
     ms = sum(a.elapsed_time(b) for a, b in ev) / steps
-    nbytes = c4_algorithmic_bytes(L, W, H)
+    coded = c4_coded_blocks(L, fr)
+    nbytes = c4_algorithmic_bytes(L, W, H, coded)
     sb = sb64_count(W, H)
-    return c4_roofline(ms, W, H), {"workload": "c4: %dx%d 10-bit frame; fused TX-type RDO (subtract, fwd txfm, highbd "
+    roof = c4_roofline(ms, W, H, fr.type_masks, coded, nbytes)
+    return roof, {"workload": "c4: %dx%d 10-bit frame; fused TX-type RDO (subtract, fwd txfm, highbd "
                         "quantize_fp, satd, TX-domain block error, rate_estimator, RDCOST) of "
                         "64x64 DCT, 32x32 DCT+IDTX, 16x16/8x8/4x4 all types; per-SB TX size; "
                         "reconstruction; rdmult %d, qindex %d" % (W, H, rdmult, qindex),
@@ -318,14 +392,16 @@ def main_c4(args):
     stream = torch.cuda.current_stream()
     frames = {}
     if args.workload == "c5":
-        proc = shard.c4_rect_processor(src, pred, qp, args.rdmult, 10, frames)
+        # every rectangle reconstructs straight into its view of one frame plane
+        frame_out = torch.empty_like(src)
+        proc = shard.c4_rect_processor(src, pred, qp, args.rdmult, 10, frames, out=frame_out)
         if args.c5_form == "wavefront":
             # edges and row gathers on separate communicators (shard.py)
             p2p = dist.new_group(list(range(world))) if world > 1 else None
 
             def step():
-                return shard.wavefront_frame(H, W, rank, world, proc, chunks=4, p2p_group=p2p,
-                                             dtype=torch.int16, device="cuda")
+                return shard.wavefront_frame(H, W, rank, world, proc, chunks=args.c5_chunks,
+                                             p2p_group=p2p, out=frame_out)
         else:
             def step():
                 return shard.sharded_frame(H, W, rank, world, proc)
@@ -364,7 +440,8 @@ def main_c4(args):
     step_ms = sum(a.elapsed_time(b) for a, b in ev) / args.steps
     sb = sb64_count(W, H)
     value = sb * args.steps / elapsed  # one frame per step for the whole job
-    c4_bytes = c4_algorithmic_bytes(L, W, H)
+    coded = c4_coded_blocks(L, fr) if args.workload != "c5" else None
+    c4_bytes = c4_algorithmic_bytes(L, W, H, coded)
     band, tail = shard.partition(H, W, world)[rank]
     line = {
         "metric": metric_name(args), "workload": args.workload,
@@ -406,7 +483,8 @@ def main_c4(args):
     }
     line["roofline"]["frac"] = round(line["roofline"]["achieved"] / HBM_PEAK_GBS, 4)
     if args.workload == "c4" and world == 1:
-        rv = c4_roofline(step_ms, W, H)  # the bound that applies: int32 VALU
+        # the bound that applies: int32 VALU
+        rv = c4_roofline(step_ms, W, H, fr.type_masks, coded, c4_bytes)
         if rv is not None:
             line["hbm_roofline"] = line["roofline"]
             line["roofline"] = rv

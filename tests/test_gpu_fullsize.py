@@ -186,10 +186,11 @@ def test_c5_partition_rects_on_gpu(L):
     2..8 (tails are column segments: views with the frame's stride), each
     computed by the HIP C4 step on its own, assemble to the whole-frame
     reconstruction; so does the row-wavefront form at world 1 (3 column
-    chunks per SB row)."""
+    chunks per SB row), once with copies and once writing every chunk
+    straight into the frame.  C5's configuration: 3840x2160 10-bit."""
     import torch
     import lavish_dsp.shard as shard
-    W, H, rdmult = 1280, 784, 1700   # 13 SB rows: tails for every world > 1
+    W, H, rdmult = 3840, 2160, 1700   # 34 SB rows: tails for every world but 2
     src, pred = _c4_planes(W, H)
     ts = torch.from_numpy(src.view(np.int16)).cuda()
     tp = torch.from_numpy(pred.view(np.int16)).cuda()
@@ -211,6 +212,12 @@ def test_c5_partition_rects_on_gpu(L):
     wf = shard.wavefront_frame(H, W, 0, 1, rect, chunks=3, dtype=torch.int16, device="cuda")
     torch.cuda.synchronize()
     np.testing.assert_array_equal(wf.cpu().numpy(), ref)
+    out = torch.full_like(ts, -1)
+    direct = shard.c4_rect_processor(ts, tp, qp, rdmult, 10, {}, out=out)
+    wf = shard.wavefront_frame(H, W, 0, 1, direct, chunks=4, out=out)
+    torch.cuda.synchronize()
+    assert wf.data_ptr() == out.data_ptr()
+    np.testing.assert_array_equal(out.cpu().numpy(), ref)
 
 
 def test_pixel_1080p_7refs_all_jobs(L):

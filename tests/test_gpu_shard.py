@@ -1,7 +1,10 @@
-"""C5 with the HIP C4 step in the ranks: two processes on one GPU (gloo
-between them, reconstructions moved through host memory), the band form and
-the row-wavefront form of lavish_dsp/shard.py, each rank's frame equal to the
-single-process whole-frame step."""
+"""C5 at its configuration size (3840x2160 10-bit) with the HIP C4 step in
+the ranks: two processes on one GPU (gloo between them, reconstructions
+moved through host memory), the band form and the row-wavefront form of
+lavish_dsp/shard.py, each rank's frame equal to the single-process
+whole-frame step; in the wavefront form every chunk's received edge (the 4
+pixel rows above it and its above-right chunk) equals those rows of the
+whole-frame reconstruction."""
 import os
 import socket
 import sys
@@ -11,7 +14,8 @@ import pytest
 
 pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-W, H, RDMULT = 1280, 784, 1700   # 13 SB rows: world 2 has a split tail row
+W, H, RDMULT = 3840, 2160, 1700   # 34 SB rows (the last 48 px high)
+CHUNKS = 4
 
 
 def _free_port():
@@ -46,15 +50,19 @@ def _worker(rank, world, port, q, form):
         qp = L.build_quant_params(10, 128, L.QUANT_FP)
         gpu = shard.c4_rect_processor(ts, tp, qp, RDMULT, 10, {})
 
-        def rect(y0, y1, x0, x1):   # the HIP step; gloo moves host tensors
-            return gpu(y0, y1, x0, x1).cpu()
+        aboves = []
+
+        def rect(y0, y1, x0, x1, above=None):   # the HIP step; gloo moves host tensors
+            if above is not None:
+                aboves.append((y0, x0, above.numpy().view(np.uint16).copy()))
+            return gpu(y0, y1, x0, x1, above=above).cpu()
         if form == "band":
             full = shard.sharded_frame(H, W, rank, world, rect)
         else:
             p2p = dist.new_group(list(range(world)))
-            full = shard.wavefront_frame(H, W, rank, world, rect, chunks=4, p2p_group=p2p,
+            full = shard.wavefront_frame(H, W, rank, world, rect, chunks=CHUNKS, p2p_group=p2p,
                                          dtype=torch.int16)
-        q.put((rank, full.numpy().view(np.uint16).copy()))
+        q.put((rank, (full.numpy().view(np.uint16).copy(), aboves)))
         dist.destroy_process_group()
     except Exception as e:  # pragma: no cover - reported to the parent
         import traceback
@@ -82,6 +90,18 @@ def test_c5_two_ranks_hip_step(form):
     got = dict(q.get(timeout=150) for _ in range(2))
     for p in procs:
         p.join(timeout=60)
+    C = (W + 63) // 64
+    cx = [min(C * k // CHUNKS * 64, W) for k in range(CHUNKS + 1)]
     for r in range(2):
         assert not isinstance(got[r], str), got[r]
-        np.testing.assert_array_equal(got[r], ref)
+        full, aboves = got[r]
+        np.testing.assert_array_equal(full, ref)
+        if form == "wave":
+            rows = [row for row in range(r, (H + 63) // 64, 2) if row > 0]
+            assert len(aboves) == CHUNKS * len(rows)
+            for y0, x0, above in aboves:
+                c = cx.index(x0)
+                np.testing.assert_array_equal(above, ref[y0 - 4:y0, x0:cx[min(c + 2, CHUNKS)]],
+                                              err_msg="edge above (%d, %d)" % (y0, x0))
+        else:
+            assert aboves == []

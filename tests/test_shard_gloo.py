@@ -80,9 +80,12 @@ def _worker(rank, world, port, q, form):
         H, W = GEOM
         src, pred = T.planes(10, 5, Wp=W, Hp=H)
         done = []
+        aboves = []
 
-        def rect(y0, y1, x0, x1):
+        def rect(y0, y1, x0, x1, above=None):
             done.append((y0, y1, x0, x1))
+            if above is not None:  # the received edge, as the chunk got it
+                aboves.append((y0, x0, above.numpy().view(np.uint16).copy()))
             _, _, rec = T.oracle_frame(np.ascontiguousarray(src[y0:y1, x0:x1]),
                                        np.ascontiguousarray(pred[y0:y1, x0:x1]), 10, MASKS, 1500,
                                        threads=1)
@@ -94,7 +97,7 @@ def _worker(rank, world, port, q, form):
             p2p = dist.new_group(list(range(world)))
             full = shard.wavefront_frame(H, W, rank, world, rect, chunks=3, p2p_group=p2p,
                                          dtype=torch.int16, log=log)
-        q.put((rank, full.numpy().view(np.uint16).copy(), done, log))
+        q.put((rank, full.numpy().view(np.uint16).copy(), done, (log, aboves)))
         dist.destroy_process_group()
     except Exception as e:  # pragma: no cover - reported to the parent
         import traceback
@@ -140,6 +143,25 @@ def test_band_form_matches_single_process(world):
         assert done == [x for x in parts[r] if x is not None]  # band, then tail
 
 
+def test_partition_narrow_frames():
+    """A leftover row is cut into at most its SB columns: on frames narrower
+    than the rank count no tail is empty, surplus ranks get none, and every
+    pixel is still covered once."""
+    shard = _shard()
+    for W in (64, 128, 320):
+        for R in range(1, 12):
+            H = 64 * R - 8
+            for world in range(1, 9):
+                cov = np.zeros((H, W), np.int32)
+                for band, tail in shard.partition(H, W, world):
+                    for rc in (band, tail):
+                        if rc is not None:
+                            y0, y1, x0, x1 = rc
+                            assert y1 > y0 and x1 > x0, (W, H, world, rc)
+                            cov[y0:y1, x0:x1] += 1
+                assert (cov == 1).all(), (W, H, world)
+
+
 @pytest.mark.parametrize("world", [2, 3])
 def test_wavefront_form_matches_single_process(world):
     """Row r on rank r % G, 3 column chunks per row: every rank ends with the
@@ -150,10 +172,21 @@ def test_wavefront_form_matches_single_process(world):
     ref = _reference()
     H, W = GEOM
     R = (H + 63) // 64
+    C = (W + 63) // 64
+    cx = [min(C * k // 3 * 64, W) for k in range(4)]
     for r in range(world):
-        full, done, log = got[r]
+        full, done, logs = got[r]
         assert not isinstance(full, str), full
         np.testing.assert_array_equal(full, ref)
+        log, aboves = logs
+        # every chunk below row 0 got the row above's bottom 4 pixel rows over
+        # its own columns and the next chunk's (above-right), exactly as the
+        # single-process reconstruction has them
+        assert len(aboves) == sum(3 for y0, _, x0, _ in done if y0 > 0 and x0 == 0)
+        for y0, x0, above in aboves:
+            c = cx.index(x0)
+            x1 = cx[min(c + 2, 3)]
+            np.testing.assert_array_equal(above, ref[y0 - 4:y0, x0:x1], err_msg=str((y0, x0)))
         rows = [y0 // 64 for y0, _, _, _ in done]
         assert rows == sorted(rows) and all(row % world == r for row in rows)
         if world > 1:
