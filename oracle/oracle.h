@@ -451,6 +451,9 @@ void orc_warp_batch(const void *ref, int width, int height, int stride, void *pr
                     int p_stride, uint16_t *dst, int dst_stride, const void *jobs, long njobs,
                     int ss_x, int ss_y, int bd, int hbd, const OrcConvParams *cp, int threads);
 
+/* search_tx_type's RDCOST + first-strictly-lowest type choice (oracle_rdo.c) */
+int orc_rd_select(int rdmult, const int *rates, const int64_t *dists, int n, int64_t *rds);
+
 #ifdef __cplusplus
 }
 #endif

@@ -37,6 +37,30 @@
 
 static int get_msb(unsigned n) { return 31 - __builtin_clz(n); }
 
+/* RDCOST (av1/encoder/rd.h:31-33): ROUND_POWER_OF_TWO(rate * rdmult,
+ * AV1_PROB_COST_SHIFT) + dist * (1 << RDDIV_BITS) */
+static int64_t rdcost(int rdmult, int rate, int64_t dist) {
+  return ((((int64_t)rate) * rdmult + 256) >> 9) + dist * 128;
+}
+
+/* search_tx_type's best-type update (tx_search.c:2243-2256): the first
+ * candidate of strictly lowest RDCOST wins; rds[i] = each candidate's cost.
+ * The per-block loop below uses the same two lines; pinned by
+ * tests/golden/fix_rdselect.npz. */
+int orc_rd_select(int rdmult, const int *rates, const int64_t *dists, int n, int64_t *rds) {
+  int64_t best_rd = INT64_MAX;
+  int best = -1;
+  for (int i = 0; i < n; ++i) {
+    const int64_t rd = rdcost(rdmult, rates[i], dists[i]);
+    rds[i] = rd;
+    if (rd < best_rd) {
+      best_rd = rd;
+      best = i;
+    }
+  }
+  return best;
+}
+
 /* rate_estimator (tpl_model.c:214-226): DCT_DCT scan of tx_size */
 static int rate_estimator(const int32_t *qcoeff, int eob, int tx_size) {
   const int16_t *scan = orc_scan(tx_size, 0);
@@ -155,7 +179,7 @@ static void *rdo_rows(void *arg) {
                                         j->txb_ctx ? j->txb_ctx[2 * blk + 1] : 0,
                                         j->tx_type_costs ? j->tx_type_costs[t] : 0, 0)
                   : rate_estimator(qc, eob, j->tx_size);
-        const int64_t rd = ((((int64_t)rate) * j->rdmult + 256) >> 9) + dist * 128;
+        const int64_t rd = rdcost(j->rdmult, rate, dist);
         if (rd < best.rdcost) {
           best.best_type = t;
           best.eob = eob;

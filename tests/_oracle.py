@@ -1020,3 +1020,16 @@ def dist_wtd_batch(src, src_stride, dst, dst_stride, conv, conv_stride, w, h, jo
     fn(P(src), src_stride, P(dst), dst_stride, P(conv), conv_stride, w, h, P(jobs), len(jobs),
        P(fx), fx.shape[1], P(fy), fy.shape[1], ctypes.byref(c), bd, int(src.dtype == np.uint16),
        threads)
+
+
+def rd_select(rdmult, rates, dists):
+    """orc_rd_select: RDCOST of each (rate, dist) and the index of the first
+    strictly lowest (search_tx_type's update)."""
+    L = lib()
+    rates = np.ascontiguousarray(rates, np.int32)
+    dists = np.ascontiguousarray(dists, np.int64)
+    rds = np.zeros(len(rates), np.int64)
+    L.orc_rd_select.restype = ctypes.c_int
+    best = L.orc_rd_select(ctypes.c_int(int(rdmult)), P(rates), P(dists),
+                           ctypes.c_int(len(rates)), P(rds))
+    return best, rds

@@ -2145,6 +2145,18 @@ class TU:
             import math
             ca = self.converter(at, DOUBLE)
             return (lambda fr: math.sqrt(ca(af(fr)))), DOUBLE
+        if name in ("round",):  # C99 round: half-way cases away from zero, exact
+            (af, at), = A
+            import math
+            ca = self.converter(at, DOUBLE)
+
+            def c_round(x):
+                if x != x or math.isinf(x):
+                    return x
+                a = abs(x)
+                fl = math.floor(a)
+                return math.copysign(fl + 1.0 if a - fl >= 0.5 else fl, x)
+            return (lambda fr: c_round(ca(af(fr)))), DOUBLE
         if name in ("sqrtf",):  # correctly rounded: sqrt in double, then to single
             (af, at), = A
             import math

@@ -1846,19 +1846,33 @@ def tplmv_fragment(tu):
     tu.add_source(text, "<tpl_model.c:%d-%d>" % (a + 1, b))
 
 
-def gen_tplmv():
+def gen_tplmv(third=False):
     """The TPL start-mv candidates and per-centre motion search
     (mode_estimation, av1/encoder/tpl_model.c:640-743 executed from the
     reference text via tplmv_fragment, with motion_estimation :249-303,
     av1_full_pixel_search and av1_find_best_sub_pixel_tree_pruned_more at
     subpel_force_stop FULL_PEL) over every 16x16 block of a small frame pair,
     in raster order with the tpl mvs stored back as tpl_model_store does,
-    for four tpl_sf settings.  The third-pass candidate (needs a
-    third_pass_ctx) is not exercised here."""
+    for four tpl_sf settings -> fix_tplmv.npz.
+
+    third=True -> fix_tplmv3.npz: the same with cpi->third_pass_ctx set, so
+    the third-pass candidate (tpl_model.c:687-703) takes part: the reference's
+    av1/encoder/thirdpass.c (CONFIG_THREE_PASS 1, its third-pass build) maps
+    each block to a second-pass mode info of a 64x48 frame (ratio 1.5 x
+    1.333..., av1_get_third_pass_ratio / _mi) and scales its mv for the
+    reference frame (av1_get_third_pass_adjusted_mv); the mode infos are
+    seeded random (ref_frame pairs over INTRA_FRAME .. ALTREF_FRAME, mvs in
+    +-200 1/8 pel).  The fixture records each block's adjusted third-pass mv
+    (the kernel's per-job input) beside the tpl mv."""
     sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(HERE)), "aom-av1-lavish_amd"))
     import lavish_dsp.synth as synth
-    tu = C.TU(REF, ["aom_dsp/sad.c", "aom_dsp/variance.c", "av1/encoder/mcomp.c",
-                    "av1/encoder/tpl_model.c"], C.reference_defines(REF))
+    defines = C.reference_defines(REF)
+    files = ["aom_dsp/sad.c", "aom_dsp/variance.c", "av1/encoder/mcomp.c",
+             "av1/encoder/tpl_model.c"]
+    if third:
+        defines.update({"CONFIG_THREE_PASS": 1, "CONFIG_AV1_DECODER": 1})
+        files.append("av1/encoder/thirdpass.c")
+    tu = C.TU(REF, files, defines)
     tplmv_fragment(tu)
     check_errors(tu, ["lavish_tplmv_fragment", "motion_estimation", "av1_full_pixel_search",
                       "av1_find_best_sub_pixel_tree_pruned_more", "av1_init_dsmotion_compensation",
@@ -1885,11 +1899,38 @@ def gen_tplmv():
     sad_per_bit = 4  # (an input of the search; av1_set_sad_per_bit gives 4 near qindex 100)
     error_per_bit = max(rdmult >> 6, 1)  # av1_set_error_per_bit (rd.h:305-307)
     recs = []
+    gf_group = tpc = None
+    if third:
+        # the second pass's frame: 64x48 (mi 16 x 12), one seeded mode info per mi
+        W2, H2 = 64, 48
+        mr2, mc2 = H2 // 4, W2 // 4
+        rng = np.random.default_rng(0x3a55)
+        mis = tu.buffer("THIRD_PASS_MI_INFO", mr2 * mc2)
+        for i in range(mr2 * mc2):
+            mi = mis.buf[i]
+            rf = _get(mi, "ref_frame")
+            rf[0], rf[1] = (int(v) for v in rng.integers(0, 8, size=2))
+            mvs2 = _get(mi, "mv")
+            for q in range(2):
+                C.union_member(mvs2[q], 1)
+                _set(_get(mvs2[q], "as_mv"), row=int(rng.integers(-200, 201)),
+                     col=int(rng.integers(-200, 201)))
+        tpc = tu.struct_obj("THIRD_PASS_DEC_CTX")
+        fi = _get(tpc.buf[0], "frame_info")[0]
+        _set(fi, width=W2, height=H2, mi_rows=mr2, mi_cols=mc2, mi_stride=mc2,
+             mi_info=C.Pointer(mis.buf, 0, tu.ctype("THIRD_PASS_MI_INFO")))
+        _set(tpc.buf[0], frame_info_count=1)
+        gf_group = tu.struct_obj("GF_GROUP")
+        _set(gf_group.buf[0], size=1)
+    thirds = []
     for ci, (mname, rfs, skip, prune, alike) in enumerate(TPLMV_CASES):
         cpi = tu.struct_obj("AV1_COMP")
         CP = cpi.buf[0]
         ppi = tu.struct_obj("AV1_PRIMARY")
         _set(CP, ppi=ppi)
+        if third:
+            _set(CP, third_pass_ctx=tpc)
+            _set(_get(CP, "common"), width=W, height=H)
         vt = _get(ppi.buf[0], "fn_ptr")[bsize]
         _set(vt, sdf=fn("aom_sad16x16"), sdsf=fn("aom_sad_skip_16x16"), vf=fn("aom_variance16x16"),
              sdx4df=fn("aom_sad16x16x4d"), sdx3df=fn("aom_sad16x16x3d"),
@@ -1937,6 +1978,7 @@ def gen_tplmv():
         tpl_frame = tu.struct_obj("TplDepFrame")
         _set(tpl_frame.buf[0], tpl_stats_ptr=stats, stride=cols)
         tpl_data = tu.struct_obj("TplParams")
+        _set(tpl_data.buf[0], frame_idx=0)
         for k in range(NREF):
             for r in range(rows):
                 for c in range(cols):
@@ -1949,8 +1991,16 @@ def gen_tplmv():
                     res = tu.struct_obj("int_mv")
                     ncen = tu.buffer("int", 1)
                     cens = tu.buffer("int", 12)
+                    if third:  # the block's adjusted third-pass mv, as the fragment derives it
+                        rh, rw = tu.buffer("double", 1), tu.buffer("double", 1)
+                        fn("av1_get_third_pass_ratio")(tpc, 0, H, W, rh, rw)
+                        tmi = fn("av1_get_third_pass_mi")(tpc, 0, mi_row, mi_col, rh.buf[0],
+                                                          rw.buf[0])
+                        tmv = fn("av1_get_third_pass_adjusted_mv")(tmi, rh.buf[0], rw.buf[0],
+                                                                   k + E["LAST_FRAME"])
+                        thirds.append(_get(C.union_member(tmv, 0), "as_int"))
                     fn("lavish_tplmv_fragment")(
-                        cpi, x, tpl_frame, tpl_data, None, 0, 2, mi_row, mi_col, 4, 4, k, bsize,
+                        cpi, x, tpl_frame, tpl_data, gf_group, 0, 2, mi_row, mi_col, 4, 4, k, bsize,
                         C.Pointer(src_buf.buf, off, C.UCHAR), stride,
                         C.Pointer(ref_bufs[k].buf, off, C.UCHAR), stride, res, ncen, cens)
                     mv = _get(C.union_member(res.buf[0], 1), "as_mv")
@@ -1971,13 +2021,116 @@ def gen_tplmv():
     out["cases"] = np.array([[E[m], rfs, sk, pr, al] for m, rfs, sk, pr, al in TPLMV_CASES],
                             np.int32)
     out["params"] = np.array([qindex, rdmult, sad_per_bit, error_per_bit, allow_hp], np.int32)
-    np.savez_compressed(os.path.join(HERE, "fix_tplmv.npz"), **out)
+    if third:
+        # per case, per job (reference-major, raster): the adjusted mv as int_mv
+        out["third"] = np.array(thirds, np.int64).astype(np.uint32).view(np.int32).reshape(
+            len(TPLMV_CASES), -1)
+    np.savez_compressed(os.path.join(HERE, "fix_tplmv3.npz" if third else "fix_tplmv.npz"), **out)
+
+
+def rdselect_fragment(tu):
+    """search_tx_type's cost and best-type update (av1/encoder/tx_search.c,
+    from `const int64_t rd =` -- RDCOST of rd.h:31-33 -- through the end of
+    its `if (rd < best_rd) { ... }` block), read from the reference and run
+    in a loop over candidate (rate, dist) pairs; the locals the block uses
+    (x->plane[0], best_rd_stats, the dqcoeff buffers) are the wrapper's."""
+    with open(os.path.join(REF, "av1/encoder/tx_search.c")) as fh:
+        lines = fh.read().split("\n")
+    a = next(i for i, l in enumerate(lines) if l.strip() == "const int64_t rd =" and
+             "RDCOST(x->rdmult, this_rd_stats.rate, this_rd_stats.dist);" in lines[i + 1])
+    b = next(i for i, l in enumerate(lines) if i > a and "p->dqcoeff = tmp_dqcoeff;" in l) + 1
+    assert lines[b].strip() == "}"
+    body = "\n".join(lines[a:b + 1])
+    text = ("#include \"av1/encoder/block.h\"\n#include \"av1/encoder/rd.h\"\n"
+            "void lavish_rd_select(MACROBLOCK *x, int n, const int *rates, const int64_t *dists,"
+            " int64_t *rds, int *best_out, int64_t *best_rd_out, tran_low_t *buf_a,"
+            " tran_low_t *buf_b) {\n"
+            "  const int plane = 0, block = 0;\n"
+            "  struct macroblock_plane *const p = &x->plane[plane];\n"
+            "  RD_STATS best_rd_stats_s;\n  RD_STATS *best_rd_stats = &best_rd_stats_s;\n"
+            "  int64_t best_rd = INT64_MAX;\n  TX_TYPE best_tx_type = DCT_DCT;\n"
+            "  uint8_t best_txb_ctx = 0;\n  uint16_t best_eob = 0;\n"
+            "  tran_low_t *best_dqcoeff = buf_a;\n  p->dqcoeff = buf_b;\n"
+            "  int found = -1;\n"
+            "  for (int tx_type = 0; tx_type < n; ++tx_type) {\n"
+            "    RD_STATS this_rd_stats;\n"
+            "    this_rd_stats.rate = rates[tx_type];\n"
+            "    this_rd_stats.dist = dists[tx_type];\n"
+            "    this_rd_stats.sse = 0;\n"
+            "    x->plane[plane].eobs[block] = (uint16_t)tx_type;\n" + body +
+            "\n    rds[tx_type] = rd;\n"
+            "    if (best_tx_type == tx_type && best_rd == rd) found = tx_type;\n  }\n"
+            "  *best_out = found;\n  *best_rd_out = best_rd;\n"
+            "  (void)best_txb_ctx; (void)best_eob; (void)best_dqcoeff; (void)best_rd_stats;\n}\n")
+    tu.add_source(text, "<tx_search.c:%d-%d>" % (a + 1, b + 1))
+
+
+def gen_rdselect():
+    """RDCOST and search_tx_type's keep-first-strictly-lowest type update
+    executed from the reference text (rdselect_fragment) over seeded candidate
+    lists: 16 candidates per list (the 16 TX types), rates / dists from
+    small to the largest the C4 step produces (rate < 2^24 in 1/512 bits,
+    dist < 2^44), rdmult 1 .. 2^20, and lists with planted equal costs
+    (different rate / dist pairs with the same RDCOST) so the tie rule is
+    exercised -> fix_rdselect.npz."""
+    tu = C.TU(REF, [], C.reference_defines(REF))
+    rdselect_fragment(tu)
+    check_errors(tu, ["lavish_rd_select"])
+    rng = np.random.default_rng(0x4d5e)
+    fn = tu.func("lavish_rd_select")
+    x = tu.struct_obj("MACROBLOCK")
+    eobs = tu.buffer("uint16_t", 16)
+    tctx = tu.buffer("uint8_t", 16)
+    _set(_get(x.buf[0], "plane")[0], eobs=C.Pointer(eobs.buf, 0, tu.ctype("uint16_t")),
+         txb_entropy_ctx=C.Pointer(tctx.buf, 0, tu.ctype("uint8_t")))
+    bufa, bufb = tu.buffer("tran_low_t", 4), tu.buffer("tran_low_t", 4)
+    lists = []
+    for li in range(240):
+        rdmult = int([1, 7, 1700, 2000, 40000, 1 << 20][li % 6])
+        n = 16
+        rmax = [1 << 10, 1 << 16, 1 << 24][li % 3]
+        dmax = [1 << 12, 1 << 30, 1 << 44][(li // 3) % 3]
+        rates = rng.integers(0, rmax, size=n)
+        dists = rng.integers(0, dmax, size=n)
+        if li % 4 == 0:  # plant ties: candidate j gets candidate i's cost via another pair
+            for _ in range(4):
+                i, j = (int(v) for v in rng.integers(0, n, size=2))
+                rates[j] = rates[i] + 512 * int(rng.integers(0, 3))
+                # same ROUND_POWER_OF_TWO(rate * rdmult, 9) + dist * 128 as i
+                ri = (int(rates[i]) * rdmult + 256) >> 9
+                rj = (int(rates[j]) * rdmult + 256) >> 9
+                dj = (ri - rj) // 128 + int(dists[i])
+                if dj >= 0 and (ri - rj) % 128 == 0:
+                    dists[j] = dj
+                else:
+                    rates[j], dists[j] = rates[i], dists[i]
+        if li % 5 == 1:  # every candidate equal: the first one wins
+            rates[:] = rates[0]
+            dists[:] = dists[0]
+        _set(x.buf[0], rdmult=rdmult)
+        rb = tu.buffer("int", [int(v) for v in rates])
+        db = tu.buffer("int64_t", [int(v) for v in dists])
+        rds = tu.buffer("int64_t", n)
+        best, best_rd = tu.buffer("int", 1), tu.buffer("int64_t", 1)
+        fn(x, n, rb, db, rds, best, best_rd, bufa, bufb)
+        lists.append((rdmult, rates.copy(), dists.copy(), list(rds.buf), best.buf[0],
+                      best_rd.buf[0]))
+    np.savez_compressed(os.path.join(HERE, "fix_rdselect.npz"),
+                        rdmult=np.array([l[0] for l in lists], np.int32),
+                        rates=np.array([l[1] for l in lists], np.int32),
+                        dists=np.array([l[2] for l in lists], np.int64),
+                        rds=np.array([l[3] for l in lists], np.int64),
+                        best=np.array([l[4] for l in lists], np.int32),
+                        best_rd=np.array([l[5] for l in lists], np.int64))
+    print("  rdselect: %d lists, %d with ties" % (
+        len(lists), sum(len(set(l[3])) < 16 for l in lists)))
 
 
 def main(argv):
     sections = argv or ["txfm", "qparams", "quant", "inv", "pixel", "wht", "nmv", "mcomp",
                         "subpel", "tpl", "qfacade", "costcoeffs", "trellis", "warp", "compound",
-                        "convolve", "compound12", "txfeat", "trellis2", "tplmv", "subpel_up"]
+                        "convolve", "compound12", "txfeat", "trellis2", "tplmv", "subpel_up", "tplmv3",
+                        "rdselect"]
     t0 = time.time()
     ttx = None
     if "txfm" in sections or "inv" in sections or "wht" in sections:
@@ -2028,6 +2181,10 @@ def main(argv):
         gen_trellis(dict(np.load(os.path.join(HERE, "fix_txfm.npz"))), sharpness=2)
     if "tplmv" in sections:
         gen_tplmv()
+    if "tplmv3" in sections:
+        gen_tplmv(third=True)
+    if "rdselect" in sections:
+        gen_rdselect()
     if "subpel_up" in sections:
         gen_subpel_up()
     print("done in %.0fs" % (time.time() - t0))

@@ -131,3 +131,30 @@ def test_tpl_motion_search_vs_reference(T):
         rc = F["recs"][F["recs"][:, fld["case"]] == ci]
         np.testing.assert_array_equal(r, rc[:, fld["mv_row"]], err_msg="case %d" % ci)
         np.testing.assert_array_equal(c, rc[:, fld["mv_col"]], err_msg="case %d" % ci)
+
+
+def test_tpl_motion_search_third_pass_vs_reference(T):
+    """With the third-pass candidate: lavish_tpl_motion_search fed each
+    block's adjusted third-pass mv against mode_estimation executed from the
+    reference with a third_pass_ctx (tests/golden/fix_tplmv3.npz)."""
+    import torch
+    import lavish_dsp.motion as M
+    from test_oracle_fixtures import _load, tplmv_case_inputs
+    F = _load("fix_tplmv3.npz")
+    fld = {n: i for i, n in enumerate(F["rec_fields"])}
+    qindex, rdmult, spb, epb, allow_hp = (int(v) for v in F["params"])
+    costs = M.MvCosts(F["mvjcost_hp"], F["mvcost_hp"], device="cuda")
+    cost = costs.cost_params(spb, epb, M.MV_COST_ENTROPY)
+    src = torch.from_numpy(F["src"]).cuda()
+    refs = torch.from_numpy(F["refs"]).cuda()
+    for ci in range(len(F["cases"])):
+        jobs, (meth, sp, skip, prune, alike), (cols, rows, nref) = tplmv_case_inputs(F, ci)
+        third = torch.from_numpy(np.ascontiguousarray(F["third"][ci], dtype=np.int32)).cuda()
+        out = T.tpl_motion_search(src, refs, M.to_device(jobs), cols, rows, nref, cost, meth, sp,
+                                  skip, prune, alike, third)
+        torch.cuda.synchronize()
+        assert T.tpl_motion_failures(out) == 0
+        r, c = T.unpack_mv(out["mvs"].cpu().numpy())
+        rc = F["recs"][F["recs"][:, fld["case"]] == ci]
+        np.testing.assert_array_equal(r, rc[:, fld["mv_row"]], err_msg="case %d" % ci)
+        np.testing.assert_array_equal(c, rc[:, fld["mv_col"]], err_msg="case %d" % ci)

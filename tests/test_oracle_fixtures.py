@@ -584,6 +584,57 @@ def test_tpl_motion_search_matches_reference():
         assert np.count_nonzero(cen) > 0, msg
 
 
+def test_rd_select_matches_reference():
+    """The C4 composition's cost and type choice (oracle_rdo.c rdcost +
+    orc_rd_select, the two lines rdo_rows runs per candidate type) against
+    RDCOST and search_tx_type's best-type update executed from the reference
+    text (fix_rdselect.npz: 240 lists of 16 candidates, rdmult 1 .. 2^20,
+    rates < 2^24, dists < 2^44, planted equal costs): every cost and the
+    winning index (the first of strictly lowest cost) agree."""
+    F = _load("fix_rdselect.npz")
+    ties = 0
+    for i in range(len(F["rdmult"])):
+        best, rds = O.rd_select(F["rdmult"][i], F["rates"][i], F["dists"][i])
+        np.testing.assert_array_equal(rds, F["rds"][i], err_msg="list %d" % i)
+        assert best == F["best"][i] and rds[best] == F["best_rd"][i], i
+        ties += int(np.count_nonzero(rds == rds[best]) > 1)
+    assert ties > 0  # the tie rule was exercised
+
+
+def test_tpl_motion_search_third_pass_matches_reference():
+    """The same with the third-pass candidate (tpl_model.c:687-703): the
+    reference ran with cpi->third_pass_ctx set and its CONFIG_THREE_PASS
+    thirdpass.c mapping each block to a second-pass mode info
+    (fix_tplmv3.npz); the oracle takes each block's adjusted mv as recorded
+    there (INVALID_MV where the mode info has no such reference)."""
+    import lavish_dsp.tpl as T
+    F = _load("fix_tplmv3.npz")
+    fld = {n: i for i, n in enumerate(F["rec_fields"])}
+    recs = F["recs"]
+    qindex, rdmult, spb, epb, allow_hp = (int(v) for v in F["params"])
+    valid = 0
+    for ci in range(len(F["cases"])):
+        jobs, (meth, sp, skip, prune, alike), (cols, rows, nref) = tplmv_case_inputs(F, ci)
+        rc = recs[recs[:, fld["case"]] == ci]
+        third = np.ascontiguousarray(F["third"][ci], dtype=np.int32)
+        valid += int(np.count_nonzero(third.view(np.uint32) != 0x80008000))
+        mvs, fp, cl, cen = O.tpl_motion_search(
+            F["src"].reshape(-1), F["refs"].reshape(-1), F["src"].shape[1], jobs, cols, rows,
+            nref, meth, sp, skip, prune, alike, spb, epb, F["mvjcost_hp"], F["mvcost_hp"], 0,
+            third)
+        r, c = T.unpack_mv(mvs)
+        msg = "case %d" % ci
+        np.testing.assert_array_equal(r, rc[:, fld["mv_row"]], err_msg=msg)
+        np.testing.assert_array_equal(c, rc[:, fld["mv_col"]], err_msg=msg)
+        cr, cc = T.unpack_mv(cen)
+        for i in range(len(rc)):
+            n = int(rc[i, fld["n_centers"]])
+            opts = {(int(rc[i, fld["c%d_row" % q]]), int(rc[i, fld["c%d_col" % q]]))
+                    for q in range(n)}
+            assert (int(cr[i]), int(cc[i])) in opts, (msg, i)
+    assert valid > 0  # some blocks have a third-pass mv for their reference
+
+
 def test_subpel_tree_upsampled_vs_reference():
     """orc_subpel_search_batch_ex (SUBPEL_TREE) against av1_find_best_sub_pixel_tree
     executed from the reference with subpel_search_type USE_2_TAPS /
