@@ -54,6 +54,31 @@ struct InvTile {
   static constexpr int T1S = W + 1;
 };
 
+// inv_1d with the consumer of the output inlined into each kind's branch:
+// one output array per branch, so no pointer to a merged private array
+// survives (a shared `out` written by three branches and read after them
+// was left in scratch by the optimiser)
+template <int N, int BIT, int RNG, typename F>
+__device__ __forceinline__ void inv_1d_then(int kind, const int32_t* in, F&& use) {
+  if (kind == 0) {
+    int32_t o[N];
+    idct<N, BIT, RNG>(in, o);
+    use(o);
+  } else if (kind == 1) {
+    if constexpr (N <= 16) {
+      int32_t o[N];
+      iadst<N, BIT, RNG>(in, o);
+      use(o);
+    }
+  } else {
+    if constexpr (N <= 32) {
+      int32_t o[N];
+      iidentity<N>(in, o);
+      use(o);
+    }
+  }
+}
+
 // one tile: the P jobs from j0
 template <int W, int H, int BDI, typename PIX>
 __device__ __forceinline__ void inv_tile(const int32_t* __restrict__ dq,
@@ -70,9 +95,18 @@ __device__ __forceinline__ void inv_tile(const int32_t* __restrict__ dq,
   const int lane = threadIdx.x;
   __syncthreads();  // the previous tile's readers of jb / cf / t1 are done
   if (lane < P) {
-    InvJob z{};
-    z.eob = 0;
-    jb[lane] = (j0 + lane < njobs) ? jobs[j0 + lane] : z;
+    // (two stores, not a select between the job and a local zero job: the
+    // select made the local a scratch object read through a flat pointer)
+    if (j0 + lane < njobs) {
+      jb[lane] = jobs[j0 + lane];
+    } else {
+      InvJob z;
+      z.dst_off = 0;
+      z.coeff_off = 0;
+      z.tx_type = 0;
+      z.eob = 0;
+      jb[lane] = z;
+    }
   }
   __syncthreads();
   // eob 0 adds nothing (av1_inverse_transform_block returns, idct.c:308): a
@@ -103,16 +137,17 @@ __device__ __forceinline__ void inv_tile(const int32_t* __restrict__ dq,
           pending = false;
           const int ht = (kHtxP >> (2 * t)) & 3;
           const int kr = ht == 3 ? 2 : (ht == 0 ? 0 : 1);
-          int32_t in[W], out[W];
+          int32_t in[W];
 #pragma unroll
           for (int c = 0; c < W; ++c) {
             int32_t v = c < T::KW ? cf[b * T::NC + c * T::KH + r] : 0;
             if constexpr (C::rect2) v = rshift64((int64_t)v * 2896, 12);
             in[c] = clamp_bits<B::clamp_in_row>(v);
           }
-          inv_1d<W, 12, B::rng_row>(kr, in, out);
+          inv_1d_then<W, 12, B::rng_row>(kr, in, [&](const int32_t(&out)[W]) {
 #pragma unroll
-          for (int c = 0; c < W; ++c) t1[(b * T::KH + r) * T1S + c] = rshift_r(out[c], -C::is0);
+            for (int c = 0; c < W; ++c) t1[(b * T::KH + r) * T1S + c] = rshift_r(out[c], -C::is0);
+          });
         }
       }
     }
@@ -136,20 +171,22 @@ __device__ __forceinline__ void inv_tile(const int32_t* __restrict__ dq,
           const int kc = vt == 3 ? 2 : (vt == 0 ? 0 : 1);
           const bool ud = vt == 2, lr = ht == 2;
           const int cc = lr ? W - 1 - c : c;
-          int32_t in[H], out[H];
+          int32_t in[H];
 #pragma unroll
           for (int r = 0; r < H; ++r)
             in[r] = r < T::KH ? clamp_bits<B::clamp_in_col>(t1[(b * T::KH + r) * T1S + cc]) : 0;
-          inv_1d<H, 12, B::rng_col>(kc, in, out);
-          if (jb[b].eob != 0) {
-            PIX* d = dst + jb[b].dst_off + c;
+          const bool coded = jb[b].eob != 0;
+          PIX* d = dst + jb[b].dst_off + c;
+          inv_1d_then<H, 12, B::rng_col>(kc, in, [&](const int32_t(&out)[H]) {
+            if (coded) {
 #pragma unroll
-            for (int r = 0; r < H; ++r) {
-              const int32_t res = rshift_r(ud ? out[H - 1 - r] : out[r], -C::is1);
-              const int v = (int)d[(int64_t)r * stride] + res;
-              d[(int64_t)r * stride] = (PIX)(v < 0 ? 0 : (v > maxv ? maxv : v));
+              for (int r = 0; r < H; ++r) {
+                const int32_t res = rshift_r(ud ? out[H - 1 - r] : out[r], -C::is1);
+                const int v = (int)d[(int64_t)r * stride] + res;
+                d[(int64_t)r * stride] = (PIX)(v < 0 ? 0 : (v > maxv ? maxv : v));
+              }
             }
-          }
+          });
         }
       }
     }

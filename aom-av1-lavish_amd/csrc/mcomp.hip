@@ -1084,6 +1084,9 @@ __global__ __launch_bounds__(64) void tpl_mv_kernel(TplMvArgs a) {
   // poll a published mv of the row above (uniform)
   auto await_mv = [&](int64_t k) -> int32_t {
     int32_t m = __hip_atomic_load(mvs + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#if defined(LAVISH_EXP_TPL) && LAVISH_EXP_TPL == 1
+    return __builtin_amdgcn_readfirstlane(m);  // timing-only: no wait (wrong results)
+#endif
     int spins = 0;
     while (m == kInvalidMv && waiting) {
       __builtin_amdgcn_s_sleep(2);
@@ -1121,6 +1124,9 @@ __global__ __launch_bounds__(64) void tpl_mv_kernel(TplMvArgs a) {
       return al;
     };
     auto add = [&](int32_t m) {
+      // a slot still holding INVALID_MV is a neighbour whose wait timed out
+      // (counted in sync[1], the caller raises): never a centre
+      if (m == kInvalidMv) return;
       const int r = mv_row(m), c = mv_col(m);
       if (!alike(r, c, 0)) {
         set4(cr, n, r);
@@ -1257,6 +1263,8 @@ __global__ __launch_bounds__(64) void tpl_mv_kernel(TplMvArgs a) {
 // the downsampled-SAD quality check (mcomp.c:1840-1867) and, for the jobs it
 // fails, a second pass with full-row SADs.  Bit-exact with diamond_kernel.
 constexpr int kLjJobs = 8;  // jobs per wave
+constexpr int kMvDecHalf = 2047;          // MV_MAX / 8: full-pel reach of the cost tables
+constexpr int kMvDecN = 2 * kMvDecHalf + 1;
 
 __device__ __forceinline__ uint32_t group_min8(uint32_t v) {  // min over the 8-lane group
   v = min(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, false));
@@ -1310,19 +1318,80 @@ __device__ __forceinline__ int lj_var(const Ctx& c, const LjSrc& s, int l, int r
   return (int)var + mv_cost(c, r, cc);
 }
 
+// N candidates' group SADs with every load in flight before the first SAD:
+// (r[i], cc[i]) in range where v[i]; an invalid candidate's rows are read at
+// an offset past the tiled buffer's end, which the buffer descriptor's range
+// check drops (no memory request, the value 0; its SAD is masked by the
+// caller).  Loads through a branch per candidate were serialised by the
+// compiler, one memory round trip per candidate (profiles/r04_c3_isa_*).
+template <bool SKIP, int N>
+__device__ __forceinline__ void lj_sads(const Ctx& c, const LjSrc& s, int l,
+                                        __amdgpu_buffer_rsrc_t trs, int oob, const int (&r)[N],
+                                        const int (&cc)[N], const bool (&v)[N],
+                                        uint32_t (&out)[N]) {
+  constexpr int RW = SKIP ? 1 : 2;  // rows per lane
+  u32x4 t[N][RW];
+#pragma unroll
+  for (int i = 0; i < N; ++i)
+#pragma unroll
+    for (int k = 0; k < RW; ++k) {
+      const int y = c.oy + r[i] + (SKIP ? 2 * l : l + 8 * k);
+      t[i][k] = __builtin_amdgcn_raw_buffer_load_b128(
+          trs, v[i] ? (int)tile_off(c, y, c.ox + cc[i]) : oob, 0, 0);
+    }
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    uint32_t acc = 0;
+#pragma unroll
+    for (int k = 0; k < RW; ++k) {
+      const uint32_t* q = SKIP ? s.sk : s.fr[k];
+      acc = sad4(q[0], t[i][k].x, acc);
+      acc = sad4(q[1], t[i][k].y, acc);
+      acc = sad4(q[2], t[i][k].z, acc);
+      acc = sad4(q[3], t[i][k].w, acc);
+    }
+    acc = group_sum8(acc);
+    out[i] = SKIP ? 2 * acc : acc;
+  }
+}
+
+// mvsad_err_cost's table reads for the entropy cost through the decimated
+// copy of the caller's row / column tables (dec[0..4094] = mvcost0[8 k],
+// dec[4095..] = mvcost1[8 k], k = -2047 .. 2047, built per call by
+// mvcost_dec_kernel): a full-pel search only ever indexes multiples of 8,
+// so the copy is contiguous in what a step reads (a job's 8 sites differ by
+// +-rad full pels) and the site costs of a step share cache lines.
+__device__ __forceinline__ MvRate mvsad_rate_dec(const Ctx& c, const int32_t* dec, int row,
+                                                 int col) {
+  if (dec == nullptr) return mvsad_rate(c, row, col);
+  const int kr = row - c.full_ref_row, kc = col - c.full_ref_col;
+  const int joint = (kc != 0) | ((kr != 0) << 1);  // av1_get_mv_joint
+  typedef const __attribute__((address_space(1))) int32_t* gi32;
+  return MvRate{((gi32)c.mvjcost)[joint], ((gi32)dec)[kr + kMvDecHalf],
+                ((gi32)dec)[kc + kMvDecHalf + kMvDecN]};
+}
+
 // one pass of full_pixel_diamond (+ its cost list) for the wave's jobs whose
 // `run` is set; accumulates steps / searches, leaves the pass's best mv, var
 // cost and cost list
 template <bool SKIP>
-__device__ void lj_pass(const Ctx& c, const LjSrc& s, int l, bool run, int step_param,
-                        bool want_cl, uint32_t* res, int& steps, int& searches, int& br,
-                        int& bc, int& sme, int (&cl)[5]) {
+__device__ void lj_pass(const Ctx& c, const LjSrc& s, int l, __amdgpu_buffer_rsrc_t trs, int oob,
+                        const int32_t* dec, bool run, int step_param, bool want_cl,
+                        uint32_t* res, int& steps,
+                        int& searches, int& br, int& bc, int& sme, int (&cl)[5]) {
   // (br / bc carry the start mv on entry; diamond_search_sad clamps it)
   const int srow = min(max(br, c.row_min), c.row_max);
   const int scol = min(max(bc, c.col_min), c.col_max);
   const int sdr = site_dr(l), sdc = site_dc(l);
   // the start: its SAD once per pass (every run restarts there)
-  const uint32_t c0 = lj_sad<SKIP>(c, s, l, srow, scol) + mvsad_cost(c, srow, scol);
+  uint32_t c0;
+  {
+    const int r1[1] = {srow}, c1[1] = {scol};
+    const bool v1[1] = {true};
+    uint32_t o1[1];
+    lj_sads<SKIP, 1>(c, s, l, trs, oob, r1, c1, v1, o1);
+    c0 = o1[0] + mvsad_finish(c, mvsad_rate_dec(c, dec, srow, scol), srow, scol);
+  }
   const int further = kMaxSteps - 1 - step_param;
   bool active = run;
   bool first = true;
@@ -1335,19 +1404,31 @@ __device__ void lj_pass(const Ctx& c, const LjSrc& s, int l, bool run, int step_
     const int rl = row + sdr * rad, cl_ = col + sdc * rad;
     const bool vl = cl_ >= c.col_min && cl_ <= c.col_max && rl >= c.row_min && rl <= c.row_max;
     // loads only for in-range sites of jobs still walking: out-of-range
-    // sites (most of the large radii) and finished jobs issue no vector
-    // memory requests (the address path is the kernel's bound); a job's 8
-    // lanes share both conditions, so each group's DPP sum stays whole
+    // sites (most of the large radii) and finished jobs issue no memory
+    // requests (the range-checked offset); a job's 8 lanes share both
+    // conditions, so each group's DPP sum stays whole
     MvRate mr = {0, 0, 0};
-    if (vl && active) mr = mvsad_rate(c, rl, cl_);
+    if (vl && active) mr = mvsad_rate_dec(c, dec, rl, cl_);
     uint32_t mine = 0;
+    // the 8 sites: all loads issued, then the SADs (SKIP: 8 x 1 row per
+    // lane; full rows: two halves of 4 sites x 2 rows)
+    constexpr int NS = SKIP ? 8 : 4;
 #pragma unroll
-    for (int t = 0; t < 8; ++t) {
-      const int r = row + site_dr(t) * rad, cc = col + site_dc(t) * rad;
-      const bool v = cc >= c.col_min && cc <= c.col_max && r >= c.row_min && r <= c.row_max;
-      uint32_t sd = 0;
-      if (v && active) sd = lj_sad<SKIP>(c, s, l, r, cc);
-      mine = l == t ? sd : mine;
+    for (int h = 0; h < 8 / NS; ++h) {
+      int rr[NS], cc[NS];
+      bool vv[NS];
+      uint32_t sd[NS];
+#pragma unroll
+      for (int i = 0; i < NS; ++i) {
+        const int t = h * NS + i;
+        rr[i] = row + site_dr(t) * rad;
+        cc[i] = col + site_dc(t) * rad;
+        vv[i] = active && cc[i] >= c.col_min && cc[i] <= c.col_max && rr[i] >= c.row_min &&
+                rr[i] <= c.row_max;
+      }
+      lj_sads<SKIP, NS>(c, s, l, trs, oob, rr, cc, vv, sd);
+#pragma unroll
+      for (int i = 0; i < NS; ++i) mine = l == h * NS + i ? sd[i] : mine;
     }
     const uint32_t key =
         (((mine + mvsad_finish(c, mr, rl, cl_)) << 3) | (uint32_t)l) | (vl ? 0u : ~0u);
@@ -1398,14 +1479,22 @@ __device__ void lj_pass(const Ctx& c, const LjSrc& s, int l, bool run, int step_
     }
   }
   if (want_cl) {  // calc_int_sad_list around (br, bc): centre, left, bottom, right, top
+    int rr[5], cc[5];
+    bool vv[5];
+    uint32_t sd[5];
+    MvRate m[5];
 #pragma unroll
     for (int t = 0; t < 5; ++t) {
-      const int r = br + (t == 2 ? 1 : t == 4 ? -1 : 0), cc = bc + (t == 1 ? -1 : t == 3 ? 1 : 0);
-      const bool v = t == 0 ||
-                     (cc >= c.col_min && cc <= c.col_max && r >= c.row_min && r <= c.row_max);
-      const uint32_t sd = lj_sad<SKIP>(c, s, l, v ? r : br, v ? cc : bc);
-      cl[t] = v ? (int)(sd + mvsad_cost(c, r, cc)) : INT_MAX;
+      rr[t] = br + (t == 2 ? 1 : t == 4 ? -1 : 0);
+      cc[t] = bc + (t == 1 ? -1 : t == 3 ? 1 : 0);
+      vv[t] = t == 0 ||
+              (cc[t] >= c.col_min && cc[t] <= c.col_max && rr[t] >= c.row_min && rr[t] <= c.row_max);
+      m[t] = mvsad_rate_dec(c, dec, vv[t] ? rr[t] : br, vv[t] ? cc[t] : bc);  // (in-range indices)
     }
+    lj_sads<SKIP, 5>(c, s, l, trs, oob, rr, cc, vv, sd);
+#pragma unroll
+    for (int t = 0; t < 5; ++t)
+      cl[t] = vv[t] ? (int)(sd[t] + mvsad_finish(c, m[t], rr[t], cc[t])) : INT_MAX;
   }
 }
 
@@ -1413,8 +1502,8 @@ __device__ void lj_pass(const Ctx& c, const LjSrc& s, int l, bool run, int step_
 __device__ __forceinline__ void lj_group(
     const uint8_t* __restrict__ src, int ss, const uint8_t* __restrict__ ref, int rs,
     const LavishRefTiles& tiles, const Job* __restrict__ jobs, int njobs, int step_param,
-    const LavishMvCostParams& cost, int skip, LavishDiamondResult* __restrict__ out,
-    int32_t* __restrict__ cost_lists, int vwg, int nvwg) {
+    const LavishMvCostParams& cost, const int32_t* dec, int skip,
+    LavishDiamondResult* __restrict__ out, int32_t* __restrict__ cost_lists, int vwg, int nvwg) {
   __shared__ uint32_t res_s[4][kLjJobs][kMaxSteps];  // (LDS-addressed, not through a pointer)
   // XCD-aware: consecutive job groups (neighbouring blocks) share an XCD's L2
   const int wg = (vwg & 7) * (nvwg >> 3) + (vwg >> 3);
@@ -1454,6 +1543,11 @@ __device__ __forceinline__ void lj_group(
   c.fsz = (int)tiles.field_bytes;
   c.oy = (int)(jb.ref_off / rs);
   c.ox = (int)(jb.ref_off - (int64_t)c.oy * rs);
+  // the tiled copy through a range-checked buffer descriptor (uniform:
+  // kernel arguments only); `oob` = an offset past its end
+  const int oob = (int)(2 * tiles.field_bytes);
+  const __amdgpu_buffer_rsrc_t trs =
+      __builtin_amdgcn_make_buffer_rsrc((void*)tiles.data, 0, oob, 0x00020000);
   LjSrc s;
   load_row<4>(c.src + (int64_t)(2 * l) * ss, s.sk);
   load_row<4>(c.src + (int64_t)l * ss, s.fr[0]);
@@ -1464,7 +1558,8 @@ __device__ __forceinline__ void lj_group(
   int br = jb.start_row, bc = jb.start_col;
   bool full = true;
   if (skip) {
-    lj_pass<true>(c, s, l, true, step_param, want_cl, res, steps, searches, br, bc, sme, cl);
+    lj_pass<true>(c, s, l, trs, oob, dec, true, step_param, want_cl, res, steps, searches, br, bc,
+                  sme, cl);
     // quality check of the row-skipping search (mcomp.c:1840-1867): sad and
     // sad_skip at the result, rows l and l + 8 of lane l (same parity as l)
     uint32_t all = 0;
@@ -1484,7 +1579,8 @@ __device__ __forceinline__ void lj_group(
     }
   }
   if (__builtin_amdgcn_ballot_w64(full) != 0)
-    lj_pass<false>(c, s, l, full, step_param, want_cl, res, steps, searches, br, bc, sme, cl);
+    lj_pass<false>(c, s, l, trs, oob, dec, full, step_param, want_cl, res, steps, searches, br, bc,
+                   sme, cl);
   if (!mine_job) return;
   if (l == 0) {
     LavishDiamondResult r;
@@ -1507,12 +1603,31 @@ __device__ __forceinline__ void lj_group(
 __global__ __launch_bounds__(256, 4) void diamond_lj_kernel(
     const uint8_t* __restrict__ src, int ss, const uint8_t* __restrict__ ref, int rs,
     LavishRefTiles tiles, const Job* __restrict__ jobs, int njobs, int step_param,
-    LavishMvCostParams cost, int skip, LavishDiamondResult* __restrict__ out,
+    LavishMvCostParams cost, const int32_t* dec, int skip, LavishDiamondResult* __restrict__ out,
     int32_t* __restrict__ cost_lists, int nvwg) {
   for (int v = blockIdx.x; v < nvwg; v += gridDim.x)
-    lj_group(src, ss, ref, rs, tiles, jobs, njobs, step_param, cost, skip, out, cost_lists, v,
-             nvwg);
+    lj_group(src, ss, ref, rs, tiles, jobs, njobs, step_param, cost, dec, skip, out, cost_lists,
+             v, nvwg);
 }
+
+// the decimated entropy cost tables of mvsad_rate_dec
+__global__ __launch_bounds__(256) void mvcost_dec_kernel(const int32_t* __restrict__ mvcost0,
+                                                         const int32_t* __restrict__ mvcost1,
+                                                         int32_t* __restrict__ dec) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= 2 * kMvDecN) return;
+  const int k = (i % kMvDecN) - kMvDecHalf;
+  dec[i] = (i < kMvDecN ? mvcost0 : mvcost1)[8 * k];
+}
+
+static bool lj_dec_enabled() {  // LAVISH_C3_MVDEC=0: the caller's tables directly (A/B)
+  static const bool on = [] {
+    const char* e = getenv("LAVISH_C3_MVDEC");
+    return e == nullptr || atoi(e) != 0;
+  }();
+  return on;
+}
+thread_local StreamScratch t_mvdec;
 
 static int lj_grid_cap() {  // LAVISH_C3_WGS=n: at most n workgroups (rounded to 8)
   static const int cap = [] {
@@ -1560,9 +1675,16 @@ void launch(const uint8_t* src, int ss, const uint8_t* ref, int rs, const Lavish
           const int nwg = (((waves + 3) / 4) + 7) & ~7;
           const int cap = lj_grid_cap();
           const int grid = cap > 0 && cap < nwg ? cap : nwg;
+          int32_t* dec = nullptr;
+          if (cost.mv_cost_type == 0 && lj_dec_enabled()) {
+            dec = (int32_t*)t_mvdec.acquire(2 * kMvDecN * sizeof(int32_t), s);
+            hipLaunchKernelGGL(mvcost_dec_kernel, dim3((2 * kMvDecN + 255) / 256), dim3(256), 0,
+                               s, cost.mvcost[0], cost.mvcost[1], dec);
+          }
           hipLaunchKernelGGL(diamond_lj_kernel, dim3(grid), dim3(256), 0, s, src, ss, ref, rs,
-                             *t, (const Job*)jobs, njobs, step_param, cost, skip, out, cost_lists,
-                             nwg);
+                             *t, (const Job*)jobs, njobs, step_param, cost, (const int32_t*)dec,
+                             skip, out, cost_lists, nwg);
+          if (dec) t_mvdec.release(s);
           return;
         }
       }

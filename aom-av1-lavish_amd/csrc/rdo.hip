@@ -540,9 +540,21 @@ __device__ __forceinline__ void rdo_types(const RdoArgs& a, const int32_t (&res)
 // 1 wave per SIMD, latency bound at 14% of the VALU peak).  The TX-domain
 // decision kernels of the sizes of 512+ coefficients ask for 2 waves per
 // SIMD (<= 256 registers), the 16x16 one for 4 (<= 128).
+#ifndef LAVISH_RDO_WV16
+#define LAVISH_RDO_WV16 4
+#endif
+#ifndef LAVISH_RDO_WV32
+#define LAVISH_RDO_WV32 2
+#endif
+#ifndef LAVISH_RDO_WV64
+#define LAVISH_RDO_WV64 2
+#endif
 template <int W, int H, int MODE>
 constexpr int rdo_waves() {
-  return (MODE == 1 && W * H >= 512) ? 2 : (MODE == 1 && W == 16 && H == 16) ? 4 : 1;
+  if (MODE != 1) return 1;
+  if (W == 16 && H == 16) return LAVISH_RDO_WV16;
+  if (W * H >= 2048) return LAVISH_RDO_WV64;
+  return W * H >= 512 ? LAVISH_RDO_WV32 : 1;
 }
 
 template <int W, int H, int MODE, int BDI>
@@ -1053,9 +1065,43 @@ int rdo_plane_px64(RdoArgs& a, int tx_size, int width, int height, hipStream_t s
   return rc;
 }
 
+// reconstruction scratch: per candidate size one slot of (64 / w) x (64 / h)
+// jobs per SB, then the SBs' job counts; offsets into it
+size_t recon_scratch_layout(const SbArgs& a, int nsb, size_t (&joff)[19], size_t (&coff)[19]) {
+  size_t bytes = 0;
+  for (int i = 0; i < a.nsizes; ++i) {
+    const int t = a.sizes[i];
+    joff[t] = bytes;
+    bytes += (size_t)nsb * (64 / tx_w(t)) * (64 / tx_h(t)) * sizeof(LavishInvJob);
+  }
+  for (int i = 0; i < a.nsizes; ++i) {
+    const int t = a.sizes[i];
+    coff[t] = bytes;
+    bytes += ((size_t)nsb * sizeof(uint16_t) + 15) & ~(size_t)15;
+  }
+  return bytes;
+}
+
+// scratch_out: nullptr -> the per-thread stream-ordered scratch; else the
+// caller's buffer of recon_scratch_bytes() (a captured graph owns one)
+int rdo_reconstruct_impl(uint32_t size_mask, const LavishRdoBlock* const* rec,
+                         const int32_t* const* dqcoeff, int width, int height,
+                         const uint16_t* pred, uint16_t* recon, int stride, int bd,
+                         uint8_t* sb_tx_size, hipStream_t s, char* own_scratch,
+                         size_t* scratch_bytes);
+
 int rdo_reconstruct(uint32_t size_mask, const LavishRdoBlock* const* rec,
                     const int32_t* const* dqcoeff, int width, int height, const uint16_t* pred,
                     uint16_t* recon, int stride, int bd, uint8_t* sb_tx_size, hipStream_t s) {
+  return rdo_reconstruct_impl(size_mask, rec, dqcoeff, width, height, pred, recon, stride, bd,
+                              sb_tx_size, s, nullptr, nullptr);
+}
+
+int rdo_reconstruct_impl(uint32_t size_mask, const LavishRdoBlock* const* rec,
+                         const int32_t* const* dqcoeff, int width, int height,
+                         const uint16_t* pred, uint16_t* recon, int stride, int bd,
+                         uint8_t* sb_tx_size, hipStream_t s, char* own_scratch,
+                         size_t* scratch_bytes) {
   SbArgs a{};
   for (int t = 0; t < 19; ++t)
     if ((size_mask >> t) & 1) a.sizes[a.nsizes++] = t;
@@ -1074,21 +1120,15 @@ int rdo_reconstruct(uint32_t size_mask, const LavishRdoBlock* const* rec,
   a.height = height;
   a.stride = stride;
   a.sb_tx_size = sb_tx_size;
-  // scratch: per candidate size one slot of (64 / w) x (64 / h) jobs per SB
-  // and the SBs' job counts
   const int nsb = a.sbw * a.sbh;
-  size_t joff[19] = {}, coff[19] = {}, bytes = 0;
-  for (int i = 0; i < a.nsizes; ++i) {
-    const int t = a.sizes[i];
-    joff[t] = bytes;
-    bytes += (size_t)nsb * (64 / tx_w(t)) * (64 / tx_h(t)) * sizeof(LavishInvJob);
+  size_t joff[19] = {}, coff[19] = {};
+  const size_t bytes = recon_scratch_layout(a, nsb, joff, coff);
+  if (scratch_bytes != nullptr) {  // size query
+    *scratch_bytes = bytes;
+    if (own_scratch == nullptr) return 0;
   }
-  for (int i = 0; i < a.nsizes; ++i) {
-    const int t = a.sizes[i];
-    coff[t] = bytes;
-    bytes += ((size_t)nsb * sizeof(uint16_t) + 15) & ~(size_t)15;
-  }
-  char* scratch = (char*)t_rs.acquire(bytes, s);
+  const bool shared = own_scratch == nullptr;
+  char* scratch = shared ? (char*)t_rs.acquire(bytes, s) : own_scratch;
   for (int i = 0; i < a.nsizes; ++i) {
     const int t = a.sizes[i];
     a.jobs[t] = (LavishInvJob*)(scratch + joff[t]);
@@ -1106,11 +1146,11 @@ int rdo_reconstruct(uint32_t size_mask, const LavishRdoBlock* const* rec,
     const int rc = inv_txfm_add_batch(dqcoeff[t], t, a.jobs[t], nsb * cap, recon, stride, bd, 1,
                                       s, a.cnt[t], cap);
     if (rc) {
-      t_rs.release(s);
+      if (shared) t_rs.release(s);
       return rc;
     }
   }
-  t_rs.release(s);
+  if (shared) t_rs.release(s);
   return 0;
 }
 
@@ -1182,4 +1222,90 @@ extern "C" int lavish_rdo_plane_rate(const uint16_t* src, const uint16_t* pred, 
   return lavish::rdo_plane(src, pred, stride, width, height, tx_size, type_mask, bit_depth, qp,
                            rdmult, out, qcoeff, dqcoeff, (hipStream_t)stream, 0, block_mask,
                            block_map, &rc);
+}
+
+// ---------------------------------------------------------------------------
+// A captured C4 step: lavish_rdo_frame + lavish_rdo_reconstruct for fixed
+// buffers recorded once into a HIP graph, replayed with one launch.  For
+// callers that run the step on many small rectangles (the C5 row wavefront's
+// chunks), where ~15 kernel launches and the fan-out events per call cost
+// more host time than the rectangle's GPU work.  The graph owns the
+// reconstruction's job scratch, so replays on any stream are independent of
+// the per-thread scratch; two replays of one graph must not overlap.
+// ---------------------------------------------------------------------------
+struct LavishRdoGraph {
+  hipGraph_t graph = nullptr;
+  hipGraphExec_t exec = nullptr;
+  void* scratch = nullptr;
+};
+
+extern "C" int lavish_rdo_graph_create(const uint16_t* src, const uint16_t* pred, int stride,
+                                       int width, int height, uint32_t size_mask,
+                                       const uint32_t* type_masks, int bit_depth,
+                                       const LavishQuantParams* qp, int rdmult,
+                                       LavishRdoBlock* const* records, int32_t* const* qcoeff,
+                                       int32_t* const* dqcoeff, uint16_t* recon,
+                                       uint8_t* sb_tx_size, LavishRdoGraph** out) {
+  if (out == nullptr) return -3;
+  *out = nullptr;
+  size_t bytes = 0;
+  int rc = lavish::rdo_reconstruct_impl(size_mask, (const LavishRdoBlock* const*)records,
+                                        (const int32_t* const*)dqcoeff, width, height, pred,
+                                        recon, stride, bit_depth, sb_tx_size, nullptr, nullptr,
+                                        &bytes);
+  if (rc) return rc;
+  LavishRdoGraph* g = new LavishRdoGraph();
+  LAVISH_CHECK(hipMalloc(&g->scratch, bytes > 0 ? bytes : 16));
+  hipStream_t cs;
+  LAVISH_CHECK(hipStreamCreateWithFlags(&cs, hipStreamNonBlocking));
+  // one uncaptured run first: the library's lazily created state (internal
+  // streams, device scan tables: synchronous uploads) must exist before the
+  // capture, which may only record stream work
+  rc = lavish::rdo_frame(src, pred, stride, width, height, size_mask, type_masks, bit_depth, qp,
+                         rdmult, records, qcoeff, dqcoeff, cs);
+  if (rc == 0)
+    rc = lavish::rdo_reconstruct_impl(size_mask, (const LavishRdoBlock* const*)records,
+                                      (const int32_t* const*)dqcoeff, width, height, pred, recon,
+                                      stride, bit_depth, sb_tx_size, cs, (char*)g->scratch,
+                                      &bytes);
+  LAVISH_CHECK(hipStreamSynchronize(cs));
+  if (rc != 0) {
+    LAVISH_CHECK(hipStreamDestroy(cs));
+    lavish_rdo_graph_destroy(g);
+    return rc;
+  }
+  LAVISH_CHECK(hipStreamBeginCapture(cs, hipStreamCaptureModeThreadLocal));
+  rc = lavish::rdo_frame(src, pred, stride, width, height, size_mask, type_masks, bit_depth, qp,
+                         rdmult, records, qcoeff, dqcoeff, cs);
+  if (rc == 0)
+    rc = lavish::rdo_reconstruct_impl(size_mask, (const LavishRdoBlock* const*)records,
+                                      (const int32_t* const*)dqcoeff, width, height, pred, recon,
+                                      stride, bit_depth, sb_tx_size, cs, (char*)g->scratch,
+                                      &bytes);
+  hipGraph_t graph = nullptr;
+  LAVISH_CHECK(hipStreamEndCapture(cs, &graph));
+  LAVISH_CHECK(hipStreamDestroy(cs));
+  g->graph = graph;
+  if (rc == 0 && graph != nullptr)
+    LAVISH_CHECK(hipGraphInstantiate(&g->exec, graph, nullptr, nullptr, 0));
+  if (rc != 0 || g->exec == nullptr) {
+    lavish_rdo_graph_destroy(g);
+    return rc ? rc : -8;
+  }
+  *out = g;
+  return 0;
+}
+
+extern "C" int lavish_rdo_graph_launch(LavishRdoGraph* g, void* stream) {
+  if (g == nullptr || g->exec == nullptr) return -3;
+  LAVISH_CHECK(hipGraphLaunch(g->exec, (hipStream_t)stream));
+  return 0;
+}
+
+extern "C" void lavish_rdo_graph_destroy(LavishRdoGraph* g) {
+  if (g == nullptr) return;
+  if (g->exec) LAVISH_CHECK(hipGraphExecDestroy(g->exec));
+  if (g->graph) LAVISH_CHECK(hipGraphDestroy(g->graph));
+  if (g->scratch) LAVISH_CHECK(hipFree(g->scratch));
+  delete g;
 }

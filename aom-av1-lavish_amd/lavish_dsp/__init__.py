@@ -562,6 +562,48 @@ class RdoFrame:
                                       device=src.device)
 
 
+if hasattr(_lib, "lavish_rdo_graph_create"):  # (older A/B builds lack it)
+    _lib.lavish_rdo_graph_create.argtypes = [_vp, _vp, _i32, _i32, _i32, ctypes.c_uint32, _vp,
+                                             _i32, ctypes.POINTER(QuantParams), _i32, _vp, _vp,
+                                             _vp, _vp, _vp, ctypes.POINTER(ctypes.c_void_p)]
+    _lib.lavish_rdo_graph_create.restype = _i32
+    _lib.lavish_rdo_graph_launch.argtypes = [_vp, _vp]
+    _lib.lavish_rdo_graph_launch.restype = _i32
+    _lib.lavish_rdo_graph_destroy.argtypes = [_vp]
+    _lib.lavish_rdo_graph_destroy.restype = None
+
+
+class RdoGraph:
+    """lavish_rdo_graph_create: the C4 step (rdo_frame + reconstruct) of one
+    RdoFrame on fixed src / pred planes, captured once into a HIP graph;
+    launch() replays it with one host call."""
+
+    def __init__(self, src, pred, frame, qp, rdmult, bit_depth=10):
+        assert src.stride(1) == 1 and src.shape == pred.shape
+        H, W = src.shape
+        self._keep = (src, pred, frame, qp)
+        g = ctypes.c_void_p()
+        rc = _lib.lavish_rdo_graph_create(
+            ctypes.c_void_p(src.data_ptr()), ctypes.c_void_p(pred.data_ptr()), src.stride(0), W,
+            H, frame.size_mask, frame.tm, bit_depth, ctypes.byref(qp), rdmult, frame.rec, frame.q,
+            frame.dq, ctypes.c_void_p(frame.recon.data_ptr()),
+            ctypes.c_void_p(frame.sb_tx_size.data_ptr()), ctypes.byref(g))
+        if rc != 0:
+            raise ValueError("lavish_rdo_graph_create failed (rc=%d)" % rc)
+        self._g = g
+
+    def launch(self, stream=None):
+        rc = _lib.lavish_rdo_graph_launch(self._g, _stream_ptr(stream))
+        if rc != 0:
+            raise ValueError("lavish_rdo_graph_launch failed (rc=%d)" % rc)
+
+    def __del__(self):
+        g = getattr(self, "_g", None)
+        if g:
+            _lib.lavish_rdo_graph_destroy(g)
+            self._g = None
+
+
 def rdo_frame(src, pred, frame, qp, rdmult, bit_depth=10, reconstruct=True, stream=None,
               px=False):
     """C4 on one frame: lavish_rdo_frame (px=True: lavish_rdo_frame_px,

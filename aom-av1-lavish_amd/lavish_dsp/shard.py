@@ -222,14 +222,16 @@ def wavefront_frame(height, width, rank, world, process_rect, chunks=4, edge_row
     return full
 
 
-def c4_rect_processor(src, pred, qp, rdmult, bit_depth, frames, out=None):
+def c4_rect_processor(src, pred, qp, rdmult, bit_depth, frames, out=None, graphs=False):
     """process_rect for the GPU path: lavish_rdo_frame + reconstruct on the
     rectangle [y0, y1) x [x0, x1) of device planes (views keep the planes'
     stride).  `frames` caches the RdoFrame output buffers per rectangle.  out
     (optional, a frame-sized plane with src's stride): each rectangle's
     reconstruction is written straight into its view of it.  `above` (the
     wavefront's received edge) is accepted and not read: C4 as defined takes
-    its prediction as input, so no intra predictor consumes it here."""
+    its prediction as input, so no intra predictor consumes it here.  graphs:
+    each rectangle's step is captured once into a HIP graph
+    (lavish_rdo_graph_create) and replayed with one launch per call."""
     import lavish_dsp as L
 
     def run(y0, y1, x0, x1, above=None):
@@ -243,8 +245,13 @@ def c4_rect_processor(src, pred, qp, rdmult, bit_depth, frames, out=None):
                      if L.TX_W[t] <= x1 - x0 and L.TX_H[t] <= y1 - y0}
             frames[key] = L.RdoFrame(s, masks,
                                      recon=out[y0:y1, x0:x1] if out is not None else None)
+            if graphs:
+                frames[key].graph = L.RdoGraph(s, p, frames[key], qp, rdmult, bit_depth)
         fr = frames[key]
-        L.rdo_frame(s, p, fr, qp, rdmult, bit_depth)
+        if graphs:
+            fr.graph.launch()
+        else:
+            L.rdo_frame(s, p, fr, qp, rdmult, bit_depth)
         return fr.recon
     return run
 

@@ -77,6 +77,9 @@ def parse():
     ap.add_argument("--border", type=int, default=160)
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--c5-no-graphs", action="store_true",
+                    help="c5: launch each rectangle's step directly instead of replaying its "
+                         "captured HIP graph")
     ap.add_argument("--c5-chunks", type=int, default=4,
                     help="c5 wavefront: column chunks per SB row")
     ap.add_argument("--c5-form", choices=("band", "wavefront"), default="band",
@@ -394,7 +397,8 @@ def main_c4(args):
     if args.workload == "c5":
         # every rectangle reconstructs straight into its view of one frame plane
         frame_out = torch.empty_like(src)
-        proc = shard.c4_rect_processor(src, pred, qp, args.rdmult, 10, frames, out=frame_out)
+        proc = shard.c4_rect_processor(src, pred, qp, args.rdmult, 10, frames, out=frame_out,
+                                       graphs=not args.c5_no_graphs)
         if args.c5_form == "wavefront":
             # edges and row gathers on separate communicators (shard.py)
             p2p = dist.new_group(list(range(world))) if world > 1 else None

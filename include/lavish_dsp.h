@@ -462,6 +462,24 @@ int lavish_rdo_reconstruct(uint32_t size_mask,
                            int stride, int bit_depth, uint8_t *sb_tx_size,
                            void *stream);
 
+/* The C4 step captured once for fixed buffers: lavish_rdo_frame (all sizes
+ * of size_mask) + lavish_rdo_reconstruct recorded into a HIP graph that
+ * lavish_rdo_graph_launch replays with one launch on any stream (device
+ * pointers and parameters are the capture's; replays of one graph must not
+ * overlap).  No reference counterpart: a launch-count aid for callers that
+ * run the step on many small rectangles.  -8: capture / instantiation
+ * failed. */
+typedef struct LavishRdoGraph LavishRdoGraph;
+int lavish_rdo_graph_create(const uint16_t *src, const uint16_t *pred, int stride,
+                            int width, int height, uint32_t size_mask,
+                            const uint32_t *type_masks, int bit_depth,
+                            const LavishQuantParams *qp, int rdmult,
+                            LavishRdoBlock *const *records, int32_t *const *qcoeff,
+                            int32_t *const *dqcoeff, uint16_t *recon, uint8_t *sb_tx_size,
+                            LavishRdoGraph **graph);
+int lavish_rdo_graph_launch(LavishRdoGraph *graph, void *stream);
+void lavish_rdo_graph_destroy(LavishRdoGraph *graph);
+
 /* ---- C3: DIAMOND full-pixel motion search ------------------------------
  * av1_full_pixel_search with search_method DIAMOND (av1/encoder/mcomp.c:
  * 1755-1895 -> full_pixel_diamond :1479-1526 -> diamond_search_sad

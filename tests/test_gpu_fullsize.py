@@ -212,12 +212,42 @@ def test_c5_partition_rects_on_gpu(L):
     wf = shard.wavefront_frame(H, W, 0, 1, rect, chunks=3, dtype=torch.int16, device="cuda")
     torch.cuda.synchronize()
     np.testing.assert_array_equal(wf.cpu().numpy(), ref)
-    out = torch.full_like(ts, -1)
-    direct = shard.c4_rect_processor(ts, tp, qp, rdmult, 10, {}, out=out)
-    wf = shard.wavefront_frame(H, W, 0, 1, direct, chunks=4, out=out)
-    torch.cuda.synchronize()
-    assert wf.data_ptr() == out.data_ptr()
-    np.testing.assert_array_equal(out.cpu().numpy(), ref)
+    for graphs in (False, True):  # direct launches / each chunk a replayed HIP graph
+        out = torch.full_like(ts, -1)
+        direct = shard.c4_rect_processor(ts, tp, qp, rdmult, 10, {}, out=out, graphs=graphs)
+        for _ in range(2):  # the second pass replays every cached chunk
+            out.fill_(-1)
+            wf = shard.wavefront_frame(H, W, 0, 1, direct, chunks=4, out=out)
+            torch.cuda.synchronize()
+            assert wf.data_ptr() == out.data_ptr()
+            np.testing.assert_array_equal(out.cpu().numpy(), ref, err_msg="graphs %s" % graphs)
+
+
+def test_rdo_graph_replays_new_inputs(L):
+    """lavish_rdo_graph_create captures the C4 step for fixed buffers; a replay
+    after the planes' contents change gives the direct step's result on the
+    new contents (records, coefficients, reconstruction, per-SB sizes)."""
+    import torch
+    W, H, rdmult = 640, 448, 1700
+    src, pred = _c4_planes(W, H)
+    ts = torch.from_numpy(src.view(np.int16)).cuda()
+    tp = torch.from_numpy(pred.view(np.int16)).cuda()
+    qp = L.build_quant_params(10, 128, L.QUANT_FP)
+    gfr = L.RdoFrame(ts)
+    g = L.RdoGraph(ts, tp, gfr, qp, rdmult, 10)
+    for it in range(3):
+        if it:
+            tp.copy_(torch.roll(tp, shifts=(it, 2 * it), dims=(0, 1)))
+        g.launch()
+        dfr = L.RdoFrame(ts)
+        L.rdo_frame(ts, tp, dfr, qp, rdmult, 10)
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(gfr.recon.cpu().numpy(), dfr.recon.cpu().numpy())
+        np.testing.assert_array_equal(gfr.sb_tx_size.cpu().numpy(), dfr.sb_tx_size.cpu().numpy())
+        for s in gfr.sizes:
+            for k in ("records", "qcoeff"):
+                np.testing.assert_array_equal(gfr.outs[s][k].cpu().numpy(),
+                                              dfr.outs[s][k].cpu().numpy(), err_msg=str((it, s)))
 
 
 def test_pixel_1080p_7refs_all_jobs(L):
