@@ -1498,19 +1498,20 @@ __device__ void lj_pass(const Ctx& c, const LjSrc& s, int l, __amdgpu_buffer_rsr
   }
 }
 
-// one group of 4 x 8 jobs: virtual workgroup vwg of nvwg (a multiple of 8)
+// one group of WPG x 8 jobs: virtual workgroup vwg of nvwg (a multiple of 8)
+template <int WPG>
 __device__ __forceinline__ void lj_group(
     const uint8_t* __restrict__ src, int ss, const uint8_t* __restrict__ ref, int rs,
     const LavishRefTiles& tiles, const Job* __restrict__ jobs, int njobs, int step_param,
     const LavishMvCostParams& cost, const int32_t* dec, int skip,
     LavishDiamondResult* __restrict__ out, int32_t* __restrict__ cost_lists, int vwg, int nvwg) {
-  __shared__ uint32_t res_s[4][kLjJobs][kMaxSteps];  // (LDS-addressed, not through a pointer)
+  __shared__ uint32_t res_s[WPG][kLjJobs][kMaxSteps];  // (LDS-addressed, not through a pointer)
   // XCD-aware: consecutive job groups (neighbouring blocks) share an XCD's L2
   const int wg = (vwg & 7) * (nvwg >> 3) + (vwg >> 3);
   const int lane = threadIdx.x & 63;
-  const int wave = threadIdx.x >> 6;
+  const int wave = WPG == 1 ? 0 : threadIdx.x >> 6;
   const int jg = lane >> 3, l = lane & 7;
-  const int j0 = (wg * 4 + wave) * kLjJobs;
+  const int j0 = (wg * WPG + wave) * kLjJobs;
   if (j0 >= njobs) return;
   const int j = min(j0 + jg, njobs - 1);  // a surplus group repeats the last job, never stores
   const bool mine_job = j0 + jg < njobs;
@@ -1600,14 +1601,29 @@ __device__ __forceinline__ void lj_group(
 // nvwg virtual workgroups over gridDim.x (<= nvwg, both multiples of 8, so a
 // virtual workgroup runs on the XCD of its first): with a smaller grid the
 // search holds fewer CU slots while a concurrent leg runs beside it
-__global__ __launch_bounds__(256, 4) void diamond_lj_kernel(
+// WPG waves per workgroup: 1 lets the dispatcher refill a SIMD slot as soon
+// as one wave's eight jobs are done (a 4-wave workgroup holds its slots until
+// its slowest wave ends, and a new one needs four free slots on one CU)
+#ifndef LAVISH_LJ_WAVES
+#define LAVISH_LJ_WAVES 4  // minimum waves per SIMD requested (VGPR budget 512 / this)
+#endif
+template <int WPG>
+__global__ __launch_bounds__(64 * WPG, LAVISH_LJ_WAVES) void diamond_lj_kernel(
     const uint8_t* __restrict__ src, int ss, const uint8_t* __restrict__ ref, int rs,
     LavishRefTiles tiles, const Job* __restrict__ jobs, int njobs, int step_param,
     LavishMvCostParams cost, const int32_t* dec, int skip, LavishDiamondResult* __restrict__ out,
     int32_t* __restrict__ cost_lists, int nvwg) {
   for (int v = blockIdx.x; v < nvwg; v += gridDim.x)
-    lj_group(src, ss, ref, rs, tiles, jobs, njobs, step_param, cost, dec, skip, out, cost_lists,
-             v, nvwg);
+    lj_group<WPG>(src, ss, ref, rs, tiles, jobs, njobs, step_param, cost, dec, skip, out,
+                  cost_lists, v, nvwg);
+}
+
+static int lj_wpg() {  // LAVISH_C3_WPG=4: four waves per workgroup (the round-3 shape, A/B)
+  static const int w = [] {
+    const char* e = getenv("LAVISH_C3_WPG");
+    return e != nullptr && atoi(e) == 4 ? 4 : 1;
+  }();
+  return w;
 }
 
 // the decimated entropy cost tables of mvsad_rate_dec
@@ -1672,7 +1688,8 @@ void launch(const uint8_t* src, int ss, const uint8_t* ref, int rs, const Lavish
       if constexpr (W == 16 && H == 16) {
         if (method == kDiamond && lj_enabled()) {  // eight jobs per wave
           const int waves = (njobs + kLjJobs - 1) / kLjJobs;
-          const int nwg = (((waves + 3) / 4) + 7) & ~7;
+          const int wpg = lj_wpg();
+          const int nwg = (((waves + wpg - 1) / wpg) + 7) & ~7;
           const int cap = lj_grid_cap();
           const int grid = cap > 0 && cap < nwg ? cap : nwg;
           int32_t* dec = nullptr;
@@ -1681,9 +1698,14 @@ void launch(const uint8_t* src, int ss, const uint8_t* ref, int rs, const Lavish
             hipLaunchKernelGGL(mvcost_dec_kernel, dim3((2 * kMvDecN + 255) / 256), dim3(256), 0,
                                s, cost.mvcost[0], cost.mvcost[1], dec);
           }
-          hipLaunchKernelGGL(diamond_lj_kernel, dim3(grid), dim3(256), 0, s, src, ss, ref, rs,
-                             *t, (const Job*)jobs, njobs, step_param, cost, (const int32_t*)dec,
-                             skip, out, cost_lists, nwg);
+          if (wpg == 1)
+            hipLaunchKernelGGL(diamond_lj_kernel<1>, dim3(grid), dim3(64), 0, s, src, ss, ref,
+                               rs, *t, (const Job*)jobs, njobs, step_param, cost,
+                               (const int32_t*)dec, skip, out, cost_lists, nwg);
+          else
+            hipLaunchKernelGGL(diamond_lj_kernel<4>, dim3(grid), dim3(256), 0, s, src, ss, ref,
+                               rs, *t, (const Job*)jobs, njobs, step_param, cost,
+                               (const int32_t*)dec, skip, out, cost_lists, nwg);
           if (dec) t_mvdec.release(s);
           return;
         }

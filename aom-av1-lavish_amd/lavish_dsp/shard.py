@@ -150,7 +150,7 @@ def sharded_frame(height, width, rank, world, process_rect, group=None, like=Non
 
 def wavefront_frame(height, width, rank, world, process_rect, chunks=4, edge_rows=4,
                     p2p_group=None, gather_group=None, dtype=None, device=None, log=None,
-                    out=None):
+                    out=None, streams=None):
     """The row-wavefront form: SB row r on rank r % G, processed in `chunks`
     column chunks; chunk c of row r waits for the bottom `edge_rows` pixel
     rows of row r - 1 up to chunk c + 1 (point-to-point from rank
@@ -165,13 +165,19 @@ def wavefront_frame(height, width, rank, world, process_rect, chunks=4, edge_row
     this one, which waits for the sender.  out: the frame buffer to fill
     (process_rect may return views of it, then nothing is copied).  log:
     optional list that receives ('recv', row, chunk) / ('send', row, chunk)
-    events."""
+    events.  streams (world 1, device work): the rows are dealt round-robin
+    over these streams and each chunk waits, through events, only for the
+    row above's chunk it depends on -- the wavefront's diagonal parallelism
+    on one GPU (the reference's row threads, ethread.c:113-160)."""
     import torch
     import torch.distributed as dist
     R, C = sb_rows(height), sb_cols(width)
     chunks = max(1, min(chunks, C))
     cx = [min(C * k // chunks * SB, width) for k in range(chunks + 1)]
     full = out if out is not None else torch.zeros((height, width), dtype=dtype, device=device)
+    if world == 1 and streams:
+        return _wavefront_streams(height, width, process_rect, chunks, cx, edge_rows, full,
+                                  streams, log)
     nxt, prv = (rank + 1) % world, (rank - 1) % world
     pending = []   # outstanding sends
     gathers = []
@@ -219,6 +225,45 @@ def wavefront_frame(height, width, rank, world, process_rect, chunks=4, edge_row
         f()
     for work, _ in pending:
         work.wait()
+    return full
+
+
+def _wavefront_streams(height, width, process_rect, chunks, cx, edge_rows, full, streams, log):
+    """wavefront_frame at world 1 over several streams: row r on
+    streams[r % len(streams)]; chunk c of row r waits for the event of row
+    r - 1's chunk min(c + 1, chunks - 1) (chunks of a row complete in order
+    on its stream), reads its edge rows from the frame, and records its own
+    event; the caller's stream then waits for every row."""
+    import torch
+    R = sb_rows(height)
+    caller = torch.cuda.current_stream()
+    start = torch.cuda.Event()
+    start.record(caller)
+    prev = None   # the row above's per-chunk events
+    for r in range(R):
+        st = streams[r % len(streams)]
+        st.wait_event(start)
+        y0, y1 = r * SB, min((r + 1) * SB, height)
+        evs = []
+        with torch.cuda.stream(st):
+            for c in range(chunks):
+                above = None
+                if r > 0:
+                    need = min(c + 2, chunks)
+                    st.wait_event(prev[need - 1])
+                    above = full[y0 - edge_rows:y0, cx[c]:cx[need]]
+                    if log is not None:
+                        log.append(("recv", r - 1, need - 1))
+                rec = process_rect(y0, y1, cx[c], cx[c + 1], above=above)
+                dst = full[y0:y1, cx[c]:cx[c + 1]]
+                if rec.data_ptr() != dst.data_ptr():
+                    dst.copy_(rec)
+                e = torch.cuda.Event()
+                e.record(st)
+                evs.append(e)
+        prev = evs
+    for st in streams:
+        caller.wait_stream(st)
     return full
 
 

@@ -216,3 +216,37 @@ def test_swar_nz_mag_identity():
                                 else mn(nib(0, c + 2)) + mn(nib(0, c + 3)) + mn(nib(0, c + 4))
                                 if cls == 1 else mn(nib(2, c)) + mn(nib(3, c)) + mn(nib(4, c)))
                         assert (s >> (4 * k)) & 15 == exp, (KW, cls, c)
+
+
+def test_benched_kernels_scratch_and_spills():
+    """Code-object metadata of the kernels on the benched paths (the
+    library's gfx950 images, tools/kernel_resources.py): the C3 search, the
+    C2 multi-size kernels and every inverse tile kernel use no scratch; the
+    C4 decision kernels whose occupancy requests make the compiler spill
+    spill exactly what profiles/r04_v2_rdo_occupancy_ab.json measured as
+    faster than the spill-free requests -- a toolchain change that moves
+    these counts fails here and calls for re-measuring."""
+    import shutil
+    import sys
+    if not os.path.exists("/opt/rocm/lib/llvm/bin/clang-offload-bundler") or \
+            shutil.which("c++filt") is None:
+        pytest.skip("ROCm code-object tools not present")
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import kernel_resources as KR
+    lib = os.path.join(ROOT, "aom-av1-lavish_amd", "liblavish_hip.so")
+    res = KR.kernel_resources(lib)
+    dm = dict(zip(sorted(res), KR.demangled(sorted(res))))
+    by = {dm[n]: v for n, v in res.items()}
+    checked = 0
+    for name, v in by.items():
+        if any(k in name for k in ("diamond_lj_kernel", "txq_multi_kernel", "inv_tile_kernel",
+                                   "ref_tiles_kernel", "mvcost_dec_kernel", "sb_decide_kernel")):
+            assert v.get("private_segment_fixed_size", 0) == 0, name
+            checked += 1
+    assert checked >= 80
+    ab = json.load(open(os.path.join(ROOT, "profiles", "r04_v2_rdo_occupancy_ab.json")))
+    want = ab["A_default_16x16_4w_32x32_2w_64x64_2w"]["kernels"]
+    for name, v in want.items():
+        got = by[name]
+        for k in ("vgpr_count", "vgpr_spill_count", "private_segment_fixed_size"):
+            assert got.get(k) == v.get(k), (name, k, got.get(k), v.get(k))

@@ -212,12 +212,15 @@ def test_c5_partition_rects_on_gpu(L):
     wf = shard.wavefront_frame(H, W, 0, 1, rect, chunks=3, dtype=torch.int16, device="cuda")
     torch.cuda.synchronize()
     np.testing.assert_array_equal(wf.cpu().numpy(), ref)
-    for graphs in (False, True):  # direct launches / each chunk a replayed HIP graph
+    # direct launches / each chunk a replayed HIP graph / graphs over 4
+    # streams with the chunk dependencies as events
+    for graphs, nst in ((False, 0), (True, 0), (True, 4)):
         out = torch.full_like(ts, -1)
         direct = shard.c4_rect_processor(ts, tp, qp, rdmult, 10, {}, out=out, graphs=graphs)
+        streams = [torch.cuda.Stream() for _ in range(nst)] or None
         for _ in range(2):  # the second pass replays every cached chunk
             out.fill_(-1)
-            wf = shard.wavefront_frame(H, W, 0, 1, direct, chunks=4, out=out)
+            wf = shard.wavefront_frame(H, W, 0, 1, direct, chunks=4, out=out, streams=streams)
             torch.cuda.synchronize()
             assert wf.data_ptr() == out.data_ptr()
             np.testing.assert_array_equal(out.cpu().numpy(), ref, err_msg="graphs %s" % graphs)
