@@ -112,10 +112,26 @@ __device__ __forceinline__ void inv_tile(const int32_t* __restrict__ dq,
   // eob 0 adds nothing (av1_inverse_transform_block returns, idct.c:308): a
   // tile without a coded block leaves before any load or transform
   if (!__builtin_amdgcn_ballot_w64(lane < P && jb[lane < P ? lane : 0].eob != 0)) return;
-  // stage the tile's dequantized coefficients (coalesced within a block)
-  for (int i = lane; i < P * T::NC; i += 64) {
-    const int b = i / T::NC, w = i - b * T::NC;
-    cf[i] = jb[b].eob ? dq[jb[b].coeff_off + w] : 0;
+  // stage the tile's dequantized coefficients (coalesced within a block):
+  // every load in flight before the first LDS store (a load-store loop
+  // waited one memory latency per iteration).  An uncoded block reads
+  // coefficient 0 of the list (a valid address) and stores zeros.
+  {
+    constexpr int NI = (P * T::NC + 63) / 64;
+    int32_t v[NI];
+#pragma unroll
+    for (int k = 0; k < NI; ++k) {
+      const int i = min(64 * k + lane, P * T::NC - 1);
+      const int b = i / T::NC, w = i - b * T::NC;
+      const bool on = jb[b].eob != 0;
+      v[k] = dq[on ? jb[b].coeff_off + w : 0];
+      v[k] = on ? v[k] : 0;
+    }
+#pragma unroll
+    for (int k = 0; k < NI; ++k) {
+      const int i = 64 * k + lane;
+      if ((P * T::NC) % 64 == 0 || i < P * T::NC) cf[i] = v[k];
+    }
   }
   __syncthreads();
 
@@ -177,12 +193,21 @@ __device__ __forceinline__ void inv_tile(const int32_t* __restrict__ dq,
             in[r] = r < T::KH ? clamp_bits<B::clamp_in_col>(t1[(b * T::KH + r) * T1S + cc]) : 0;
           const bool coded = jb[b].eob != 0;
           PIX* d = dst + jb[b].dst_off + c;
+          // the column's pixels read before the transform, so the H loads
+          // are in flight together (interleaved with the stores they would
+          // wait one latency per row: the rows may alias for all the
+          // compiler knows)
+          int px[H];
+          if (coded) {
+#pragma unroll
+            for (int r = 0; r < H; ++r) px[r] = (int)d[(int64_t)r * stride];
+          }
           inv_1d_then<H, 12, B::rng_col>(kc, in, [&](const int32_t(&out)[H]) {
             if (coded) {
 #pragma unroll
               for (int r = 0; r < H; ++r) {
                 const int32_t res = rshift_r(ud ? out[H - 1 - r] : out[r], -C::is1);
-                const int v = (int)d[(int64_t)r * stride] + res;
+                const int v = px[r] + res;
                 d[(int64_t)r * stride] = (PIX)(v < 0 ? 0 : (v > maxv ? maxv : v));
               }
             }
@@ -197,7 +222,8 @@ __device__ __forceinline__ void inv_tile(const int32_t* __restrict__ dq,
 // the device in slots of slot_cap jobs (C4: one slot per SB, its chosen
 // coded blocks first, slot_cnt[slot] of them): the grid strides over the
 // tiles, a tile never straddles two slots, and tiles past a slot's count
-// are skipped
+// are skipped (one workgroup per slot serialised the tiles of SBs that
+// chose small sizes: 21 -> 155 us for 60 SBs of 4x4, profiles/r04_v5_*)
 template <int W, int H, int BDI, typename PIX>
 __global__ __launch_bounds__(64) void inv_tile_kernel(const int32_t* __restrict__ dq,
                                                       const InvJob* __restrict__ jobs, int njobs,
@@ -219,8 +245,10 @@ __global__ __launch_bounds__(64) void inv_tile_kernel(const int32_t* __restrict_
   }
 }
 
-// slotted lists: at most this many workgroups, looping over the tiles
-constexpr int kInvMaxGrid = 4096;
+// slotted lists: at most this many workgroups, looping over the tiles.  A
+// size no SB chose still costs ~6 us: 4 096 workgroups reading 8 counts
+// each measured the same as 16 384 reading one (profiles/r04_v7_*)
+constexpr int kInvMaxGrid = 16384;
 
 template <int W, int H, int BDI, typename PIX>
 void launch(const int32_t* dq, const LavishInvJob* jobs, int njobs, const uint16_t* slot_cnt,

@@ -421,31 +421,40 @@ struct Search {
   // copy the window around (row, col): rows outside [row_min, row_max + H)
   // (never touched by a valid candidate) repeat the nearest row inside; all
   // loads are issued before the first store
-  __device__ __forceinline__ void fill(const Ctx& c, int lane, int row, int col) {
+  static constexpr int kFillN = WN::ROWS * WN::Q, kFillNI = (kFillN + 63) / 64;
+  typedef uint32_t fill_v __attribute__((ext_vector_type(4)));
+  // fill() in two halves, so a caller can keep several windows' loads in
+  // flight: the loads (and the window origin), then the LDS stores
+  __device__ __forceinline__ void fill_load(const Ctx& c, int lane, int row, int col,
+                                            fill_v (&v)[kFillNI]) {
     typedef const __attribute__((address_space(1))) uint32_t* gptr;
     wr0 = row - WN::R;
     wc0 = col - WN::R;
     wbase = (uintptr_t)(c.ref + (int64_t)wr0 * c.rs + wc0);
     const int rlo = max(0, c.row_min - wr0), rhi = min(WN::ROWS, c.row_max + H - wr0);
-    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-    typedef __attribute__((address_space(3))) u32x4* lptr4;
-    constexpr int N = WN::ROWS * WN::Q, NI = (N + 63) / 64;
-    u32x4 v[NI];
 #pragma unroll
-    for (int it = 0; it < NI; ++it) {
-      const int i = min(64 * it + lane, N - 1);
+    for (int it = 0; it < kFillNI; ++it) {
+      const int i = min(64 * it + lane, kFillN - 1);
       const int wr = i / WN::Q, d = i - wr * WN::Q;
       const int sr = min(max(wr, rlo), rhi - 1);
       // dword-aligned 16-byte load (any dword alignment is a single access)
       const uintptr_t ra = ((wbase + (int64_t)sr * c.rs) & ~(uintptr_t)3) + 16 * d;
       const gptr q = (gptr)ra;
-      v[it] = u32x4{q[0], q[1], q[2], q[3]};
+      v[it] = fill_v{q[0], q[1], q[2], q[3]};
     }
+  }
+  __device__ __forceinline__ void fill_store(int lane, const fill_v (&v)[kFillNI]) const {
+    typedef __attribute__((address_space(3))) fill_v* lptr4;
 #pragma unroll
-    for (int it = 0; it < NI; ++it) {
+    for (int it = 0; it < kFillNI; ++it) {
       const int i = 64 * it + lane;
-      if (i < N) ((lptr4)win)[i] = v[it];
+      if (i < kFillN) ((lptr4)win)[i] = v[it];
     }
+  }
+  __device__ __forceinline__ void fill(const Ctx& c, int lane, int row, int col) {
+    fill_v v[kFillNI];
+    fill_load(c, lane, row, col, v);
+    fill_store(lane, v);
     wave_sync();
   }
 
@@ -655,16 +664,24 @@ __device__ __forceinline__ int rawpel(int x) { return (x + 3 + (x >= 0)) >> 3; }
 // ---------------------------------------------------------------- BIGDIA --
 // av1_init_motion_compensation_bigdia (mcomp.c:498-550): scale 0 has the 4
 // nearest points, scale s >= 1 8 points of radius r = 2^(s-1) / 2r.
+// Offsets as 3-bit fields of (d + 2) in units of the scale's r, read by a
+// shift per lane (the select chains over i compiled to exec-mask branches):
+// scale 0 (0,-1) (1,0) (0,1) (-1,0); scale s >= 1, r = 2^(s-1):
+// (-r,-r) (0,-2r) (r,-r) (2r,0) (r,r) (0,2r) (-r,r) (-2r,0)
+constexpr uint32_t bigdia_pack(const int (&d)[8]) {
+  uint32_t p = 0;
+  for (int i = 0; i < 8; ++i) p |= (uint32_t)(d[i] + 2) << (3 * i);
+  return p;
+}
+constexpr int kBdR0[8] = {0, 1, 0, -1, 0, 0, 0, 0}, kBdC0[8] = {-1, 0, 1, 0, 0, 0, 0, 0};
+constexpr int kBdR1[8] = {-1, 0, 1, 2, 1, 0, -1, -2}, kBdC1[8] = {-1, -2, -1, 0, 1, 2, 1, 0};
+constexpr uint32_t kBdPR0 = bigdia_pack(kBdR0), kBdPC0 = bigdia_pack(kBdC0);
+constexpr uint32_t kBdPR1 = bigdia_pack(kBdR1), kBdPC1 = bigdia_pack(kBdC1);
 __device__ __forceinline__ void bigdia_site(int s, int i, int& dr, int& dc) {
-  if (s == 0) {
-    dr = (i == 1) ? 1 : (i == 3) ? -1 : 0;
-    dc = (i == 0) ? -1 : (i == 2) ? 1 : 0;
-    return;
-  }
-  const int r = 1 << (s - 1);
-  // (-r,-r) (0,-2r) (r,-r) (2r,0) (r,r) (0,2r) (-r,r) (-2r,0)
-  dr = (i == 0 || i == 6) ? -r : (i == 2 || i == 4) ? r : (i == 3) ? 2 * r : (i == 7) ? -2 * r : 0;
-  dc = (i == 0 || i == 2) ? -r : (i == 4 || i == 6) ? r : (i == 1) ? -2 * r : (i == 5) ? 2 * r : 0;
+  const uint32_t pr = s == 0 ? kBdPR0 : kBdPR1, pc = s == 0 ? kBdPC0 : kBdPC1;
+  const int sh = s == 0 ? 0 : s - 1;
+  dr = ((int)((pr >> (3 * i)) & 7) - 2) * (1 << sh);
+  dc = ((int)((pc >> (3 * i)) & 7) - 2) * (1 << sh);
 }
 
 // pattern_search (mcomp.c:1017-1245) over the BIGDIA sites: with
@@ -685,10 +702,64 @@ __device__ __forceinline__ void bigdia_site(int s, int i, int& dr, int& dc) {
 // SADs and mv costs from LDS: one memory latency per search instead of one
 // per round.  Rounds that reach outside read global memory as before.  vout:
 // the plain variance at the result (the sub-pel step's FULL_PEL error).
+typedef __attribute__((address_space(3))) int32_t* lds_i32;
+
+// the window's mv-cost rates (after the window in LDS): the joint costs and
+// the mvcost rows / columns of its 31 full-pel rows / columns around the
+// clamped start (br, bc); lane l's three values
+template <int W, int H>
+__device__ __forceinline__ void win_rates_load(const Ctx& c, int lane, int br, int bc,
+                                               int (&r)[3]) {
+  using WN = Win<W, H>;
+  constexpr int NR = 2 * WN::R + 1;
+  const bool ent = c.cost_type == 0;
+  typedef const __attribute__((address_space(1))) int32_t* gi32;
+  const int wr0 = br - WN::R, wc0 = bc - WN::R;
+  const int l = min(lane, NR - 1);
+  // |row - full_ref| <= 1023 + 15 inside the window: inside the tables
+  r[0] = ent ? ((gi32)c.mvjcost)[lane & 3] : 0;
+  r[1] = ent ? ((gi32)c.mvcost0)[(wr0 + l - c.full_ref_row) * 8] : 0;
+  r[2] = ent ? ((gi32)c.mvcost1)[(wc0 + l - c.full_ref_col) * 8] : 0;
+}
+template <int W, int H>
+__device__ __forceinline__ void win_rates_store(lds_u32 win, int lane, const int (&r)[3]) {
+  using WN = Win<W, H>;
+  constexpr int NR = 2 * WN::R + 1;
+  const lds_i32 rates = (lds_i32)(win + WN::SIZE);
+  if (lane < 4) rates[lane] = r[0];
+  if (lane < NR) {
+    rates[4 + lane] = r[1];
+    rates[4 + NR + lane] = r[2];
+  }
+}
+
+// pattern()'s LDS window around the clamped start (br, bc): the reference
+// window, then the mv-cost rates of its 31 full-pel rows / columns; S (any
+// Search over this window) gets the window's origin
+template <int W, int H, class S_t>
+__device__ __forceinline__ void win_prefill(S_t& S, const Ctx& c, int lane, lds_u32 win, int br,
+                                            int bc, bool filled) {
+  using WN = Win<W, H>;
+  S.win = win;
+  if (filled) {  // the same window, already in LDS (S.fill without the copy)
+    S.wr0 = br - WN::R;
+    S.wc0 = bc - WN::R;
+    S.wbase = (uintptr_t)(c.ref + (int64_t)S.wr0 * c.rs + S.wc0);
+    return;
+  }
+  int r[3];
+  win_rates_load<W, H>(c, lane, br, bc, r);
+  win_rates_store<W, H>(win, lane, r);
+  S.fill(c, lane, br, bc);  // (its wave_sync covers the rate stores)
+}
+
+// prefilled (WINP): the caller already copied this search's window
+// (win_prefill at the same clamped start and limits)
 template <int W, int H, bool SKIP, bool TL, bool WINP = false>
 __device__ int pattern(const Ctx& c, int lane, int srow, int scol, int search_step, bool do_init,
                        bool want_cl, int (&cl)[5], int& brow, int& bcol, int& steps,
-                       int& nsad, lds_u32 win = nullptr, uint32_t* vout = nullptr) {
+                       int& nsad, lds_u32 win = nullptr, uint32_t* vout = nullptr,
+                       bool prefilled = false) {
   static_assert(!WINP || (Win<W, H>::kOn && !TL), "window: w, h <= 32, linear layout");
   using WN = Win<W, H>;
   constexpr int NR = 2 * WN::R + 1;  // full-pel rows / columns a window spans
@@ -701,20 +772,10 @@ __device__ int pattern(const Ctx& c, int lane, int srow, int scol, int search_st
   int bc = min(max(scol, c.col_min), c.col_max);
   if (want_cl) cl[0] = cl[1] = cl[2] = cl[3] = cl[4] = INT_MAX;
   bool has_sad = false;
-  typedef __attribute__((address_space(3))) int32_t* lds_i32;
   lds_i32 rates = nullptr;
   if constexpr (WINP) {
     rates = (lds_i32)(win + WN::SIZE);
-    const bool ent = c.cost_type == 0;
-    typedef const __attribute__((address_space(1))) int32_t* gi32;
-    const int wr0 = br - WN::R, wc0 = bc - WN::R;
-    // |row - full_ref| <= 1023 + 15 inside the window: inside the tables
-    if (lane < 4) rates[lane] = ent ? ((gi32)c.mvjcost)[lane] : 0;
-    if (lane < NR) {
-      rates[4 + lane] = ent ? ((gi32)c.mvcost0)[(wr0 + lane - c.full_ref_row) * 8] : 0;
-      rates[4 + NR + lane] = ent ? ((gi32)c.mvcost1)[(wc0 + lane - c.full_ref_col) * 8] : 0;
-    }
-    S.fill(c, lane, br, bc);  // (its wave_sync covers the rate stores)
+    win_prefill<W, H>(S, c, lane, win, br, bc, prefilled);
   }
   // every candidate within d pixels of (r0, c0) inside the window
   auto in_win = [&](int r0, int c0, int d) {
@@ -917,7 +978,8 @@ template <int W, int H, bool PAT, bool TL, bool WINP = false>
 __device__ __forceinline__ int job_search(const Ctx& c, int lane, int start_row, int start_col,
                                           int step_param, int skip, int method, lds_u32 win,
                                           bool want_cl, int (&cl)[5], int& br, int& bc,
-                                          int& steps, int& searches, uint32_t* vout = nullptr) {
+                                          int& steps, int& searches, uint32_t* vout = nullptr,
+                                          bool prefilled = false) {
   int sme;
   auto search = [&](auto skip_tag) {
     constexpr bool SK = decltype(skip_tag)::value;
@@ -932,7 +994,7 @@ __device__ __forceinline__ int job_search(const Ctx& c, int lane, int start_row,
                                                  : max(kMaxSteps - 3, step_param);
       return pattern<W, H, SK, TL, WINP>(c, lane, start_row, start_col, step,
                                          method == kBigdia, want_cl, cl, br, bc, steps, searches,
-                                         win, vout);
+                                         win, vout, prefilled);
     }
   };
   // use_downsampled_sad applies to blocks at least 16 high (mcomp.c:132-133)
@@ -1046,6 +1108,12 @@ struct TplMvArgs {
 };
 
 constexpr int kTplMaxSpins = 1 << 22;  // ~0.3 s of s_sleep 2 per wait
+#ifndef LAVISH_TPL_PREFILL
+#define LAVISH_TPL_PREFILL 1  // 0: ranking SADs from global memory, then each search's own fill (A/B)
+#endif
+#ifndef LAVISH_TPL_SPEC
+#define LAVISH_TPL_SPEC 1  // 0: no work before the above-right wait (A/B)
+#endif
 constexpr int32_t kInvalidMv = (int32_t)0x80008000;  // INVALID_MV (mv.h)
 
 __device__ __forceinline__ int mv_row(int32_t m) { return (int16_t)(m & 0xFFFF); }
@@ -1064,18 +1132,45 @@ __device__ __forceinline__ void set4(int (&v)[4], int i, int x) {
   for (int k = 0; k < 4; ++k) v[k] = i == k ? x : v[k];
 }
 
+// LAVISH_TPL_PROF=1 (a diagnostic build, never the product): the wave's
+// clock per step phase, summed over the grid into g_tpl_prof: [0] awaits,
+// [1] centres + windows + ranking + searches after the await (speculative
+// walk: the new-centre redo), [2] the same before the await (speculative
+// walk), [3] new centres after the await, [4] publish, [5] the whole walk,
+// [6] awaits that slept, [7] blocks, [9..12] steps with 1..4 centres before
+// the ranking (non-speculative walk)
+#ifndef LAVISH_TPL_PROF
+#define LAVISH_TPL_PROF 0
+#endif
+#if LAVISH_TPL_PROF
+__device__ unsigned long long g_tpl_prof[16];
+#define TPL_PROF(...) __VA_ARGS__
+__device__ __forceinline__ void tpl_lap(unsigned long long& acc, uint64_t& t) {
+  const uint64_t now = clock64();
+  acc += now - t;
+  t = now;
+}
+#else
+#define TPL_PROF(...)
+#endif
+
 template <bool PAT>
 __global__ __launch_bounds__(64) void tpl_mv_kernel(TplMvArgs a) {
   constexpr int W = 16, H = 16;
   using WN = Win<W, H>;
+  constexpr int WSZ = WN::SIZE + (PAT ? 4 + 2 * (2 * WN::R + 1) : 0);
+  // PAT: one window per centre, all copied at once; DIAMOND: one
+  constexpr bool kPrefill = PAT && LAVISH_TPL_PREFILL;
+  constexpr bool kSpec = kPrefill && LAVISH_TPL_SPEC;
+  using SW = Search<W, H, false, false, false>;
   const int lane = threadIdx.x;
-  // reference window (+ the pattern searches' mv-cost rates)
-  __shared__ uint32_t win_s[WN::SIZE + (PAT ? 4 + 2 * (2 * WN::R + 1) : 0)];
-  const lds_u32 win = (lds_u32)win_s;
+  // reference windows (+ the pattern searches' mv-cost rates)
+  __shared__ uint32_t win_s[kPrefill ? 4 : 1][WSZ];
   int t = 0;
   if (lane == 0)
     t = __hip_atomic_fetch_add(a.sync, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   t = __builtin_amdgcn_readfirstlane(t);
+  TPL_PROF(unsigned long long prof[16] = {});
   const int ref = t % a.nrefs, row = t / a.nrefs;
   if (row >= a.rows) return;
   const int64_t nb = (int64_t)a.rows * a.cols;
@@ -1084,13 +1179,11 @@ __global__ __launch_bounds__(64) void tpl_mv_kernel(TplMvArgs a) {
   // poll a published mv of the row above (uniform)
   auto await_mv = [&](int64_t k) -> int32_t {
     int32_t m = __hip_atomic_load(mvs + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#if defined(LAVISH_EXP_TPL) && LAVISH_EXP_TPL == 1
-    return __builtin_amdgcn_readfirstlane(m);  // timing-only: no wait (wrong results)
-#endif
     int spins = 0;
     while (m == kInvalidMv && waiting) {
       __builtin_amdgcn_s_sleep(2);
       m = __hip_atomic_load(mvs + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      TPL_PROF(prof[6] += spins == 0);
       if (++spins >= kTplMaxSpins) {
         if (lane == 0)
           __hip_atomic_fetch_add(a.sync + 1, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1102,13 +1195,238 @@ __global__ __launch_bounds__(64) void tpl_mv_kernel(TplMvArgs a) {
   const bool want_cl = a.cost_lists != nullptr;
   int32_t above = 0, left = 0;
   Job jn = a.jobs[ref * nb + (int64_t)row * a.cols];  // the next block's job, loaded a step ahead
+  TPL_PROF(const uint64_t tk0 = clock64());
+  if constexpr (kSpec) {
+    // The row walk with speculation: everything a block needs but the
+    // above-right neighbour (the job, the source, the centres from the zero
+    // / above / left mvs, their windows and ranking SADs, and the searches of
+    // the ranking's top centres) is done before waiting for that neighbour.
+    // When it arrives it either adds no centre (is_alike_mv to one taken) --
+    // the speculative result is the block's -- or a new last centre, which
+    // gets its window and SAD; the ranking reruns over all centres and only
+    // searches not yet run are added.  The searches' results are kept per
+    // centre, so the outcome is the sequential one's (tpl_model.c:640-743).
+    // With a third-pass mv (it replaces centre 0 unless alike to any
+    // neighbour centre, the above-right one included) there is no
+    // speculation.
+    SW P;
+    for (int col = 0; col < a.cols; ++col) {
+      const int64_t bi = (int64_t)row * a.cols + col;
+      TPL_PROF(uint64_t tp = clock64());
+      if (row > 0 && col == 0) above = await_mv(bi - a.cols);
+      const int64_t j = ref * nb + bi;
+      const Job jb = jn;
+      if (col + 1 < a.cols) jn = a.jobs[j + 1];
+      const bool has_ar = row > 0 && col + 1 < a.cols;
+      const bool spec = a.third == nullptr;
+      int cr[4] = {0, 0, 0, 0}, cc[4] = {0, 0, 0, 0}, cs[4] = {0, 0, 0, 0};
+      int n = 1;
+      auto alike = [&](int r, int c, int from) {
+        bool al = false;
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          al |= i >= from && i < n && abs(cc[i] - c) < a.alike_thr && abs(cr[i] - r) < a.alike_thr;
+        return al;
+      };
+      auto add = [&](int32_t m) {
+        if (m == kInvalidMv) return;  // a timed-out wait never yields a centre
+        const int r = mv_row(m), c = mv_col(m);
+        if (!alike(r, c, 0)) {
+          set4(cr, n, r);
+          set4(cc, n, c);
+          ++n;
+        }
+      };
+      const Ctx c = job_ctx(a.src, a.ss, a.ref, a.rs, jb, a.cost);
+      auto centre_ctx = [&](int i) {
+        const int mr = get4(cr, i), mc = get4(cc, i);
+        Ctx ci = c;
+        ci.ref_mv_row = mr;
+        ci.ref_mv_col = mc;
+        ci.full_ref_row = rawpel(mr);
+        ci.full_ref_col = rawpel(mc);
+        // av1_set_mv_search_range (mcomp.c:206-234)
+        ci.col_min = max((int)jb.col_min, max(((mc + 7) >> 3) - 1023, -2047));
+        ci.row_min = max((int)jb.row_min, max(((mr + 7) >> 3) - 1023, -2047));
+        ci.col_max = max(ci.col_min, min((int)jb.col_max, min((mc >> 3) + 1023, 2047)));
+        ci.row_max = max(ci.row_min, min((int)jb.row_max, min((mr >> 3) + 1023, 2047)));
+        return ci;
+      };
+      P.load_src(c, lane, (lds_u32)win_s[0]);  // (the source rows of the ranking SADs)
+      // per centre (original index): its search's results once run
+      int have = 0, rvar[4] = {0, 0, 0, 0}, rbr[4] = {0, 0, 0, 0}, rbc[4] = {0, 0, 0, 0};
+      int rsme[4] = {0, 0, 0, 0}, rst[4] = {0, 0, 0, 0}, rse[4] = {0, 0, 0, 0};
+      int rcl[5][4];
+#pragma unroll
+      for (int q = 0; q < 5; ++q) rcl[q][0] = rcl[q][1] = rcl[q][2] = rcl[q][3] = INT_MAX;
+      int ix[4] = {0, 1, 2, 3}, np = 1, nf = 0;
+      int32_t above_right = 0;
+      for (int phase = spec ? 0 : 1; phase < 2; ++phase) {
+        if (phase == 0) {
+          if (row > 0) add(above);
+          if (col > 0) add(left);
+        } else {
+          if (has_ar) above_right = await_mv(bi - a.cols + 1);
+          TPL_PROF(tpl_lap(prof[0], tp));
+          if (spec) {
+            const int n0 = n;
+            if (has_ar) add(above_right);
+            if (n == n0) break;  // nothing new: the speculative result stands
+            TPL_PROF(prof[3] += 1);
+          } else {
+            if (row > 0) add(above);
+            if (col > 0) add(left);
+            if (has_ar) add(above_right);
+            const int32_t m = a.third[j];
+            if (m != kInvalidMv && !alike(mv_row(m), mv_col(m), 1)) {
+              cr[0] = mv_row(m);
+              cc[0] = mv_col(m);
+            }
+          }
+        }
+        // windows (pattern's own fill at the start clamped to the centre's
+        // limits, all loads in flight together) and ranking SADs of the
+        // centres [nf, n)
+        {
+          typename SW::fill_v v[4][SW::kFillNI];
+          int rt[4][3];
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            if (k >= nf && k < n) {
+              const Ctx ci = centre_ctx(k);
+              const int sr = min(max(rawpel(get4(cr, k)), ci.row_min), ci.row_max);
+              const int sc = min(max(rawpel(get4(cc, k)), ci.col_min), ci.col_max);
+              P.fill_load(ci, lane, sr, sc, v[k]);
+              win_rates_load<W, H>(ci, lane, sr, sc, rt[k]);
+            }
+          }
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            if (k >= nf && k < n) {
+              P.win = (lds_u32)win_s[k];
+              P.fill_store(lane, v[k]);
+              win_rates_store<W, H>(P.win, lane, rt[k]);
+            }
+          }
+          wave_sync();
+          if (a.prune) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+              if (k >= nf && k < n) {
+                const Ctx ci = centre_ctx(k);
+                const int sr = min(max(rawpel(get4(cr, k)), ci.row_min), ci.row_max);
+                const int sc = min(max(rawpel(get4(cc, k)), ci.col_min), ci.col_max);
+                const int fr = min(max(rawpel(get4(cr, k)), (int)jb.row_min), (int)jb.row_max);
+                const int fc = min(max(rawpel(get4(cc, k)), (int)jb.col_min), (int)jb.col_max);
+                int sad;
+                if (fr == sr && fc == sc) {
+                  win_prefill<W, H>(P, ci, lane, (lds_u32)win_s[k], sr, sc, true);  // (origin only)
+                  sad = (int)rdlane(P.group_sad_win(ci, fr, fc, true), 0);
+                } else {  // off the window centre: from global memory
+                  int ssad;
+                  sad_and_skip<W, H>(c, lane, fr, fc, sad, ssad);
+                }
+                set4(cs, k, sad);
+              }
+            }
+          }
+          nf = n;
+        }
+        // the ranking: stable insertion sort of the centres by SAD (glibc's
+        // qsort on <= 4 entries), cut to 4 - prune_starting_mv and by the
+        // SAD-gap rule
+        ix[0] = 0;
+        ix[1] = 1;
+        ix[2] = 2;
+        ix[3] = 3;
+        np = n;
+        if (a.prune && n > 1) {
+          int sc4[4] = {cs[0], cs[1], cs[2], cs[3]};
+#pragma unroll
+          for (int i = 1; i < 4; ++i) {
+#pragma unroll
+            for (int k = i; k > 0; --k) {
+              if (i < n && sc4[k - 1] > sc4[k]) {
+                const int x = sc4[k], o = ix[k];
+                sc4[k] = sc4[k - 1];
+                ix[k] = ix[k - 1];
+                sc4[k - 1] = x;
+                ix[k - 1] = o;
+              }
+            }
+          }
+          np = min(4 - a.prune, n);
+          if (np > 1 && (get4(sc4, np - 1) - get4(sc4, np - 2)) * 5 > get4(sc4, np - 2)) --np;
+        }
+        // the searches of the kept centres not yet run
+#pragma unroll 1
+        for (int i = 0; i < np; ++i) {
+          const int k = get4(ix, i);
+          if ((have >> k) & 1) continue;
+          const int mr = get4(cr, k), mc = get4(cc, k);
+          const Ctx ci = centre_ctx(k);
+          int cl[5] = {INT_MAX, INT_MAX, INT_MAX, INT_MAX, INT_MAX};
+          int br, bc, steps = 0, searches = 0;
+          uint32_t var = 0;
+          const int sme = job_search<W, H, PAT, false, PAT>(ci, lane, rawpel(mr), rawpel(mc),
+                                                            a.step_param, a.skip, a.method,
+                                                            (lds_u32)win_s[k], want_cl, cl, br, bc,
+                                                            steps, searches, &var, true);
+          have |= 1 << k;
+          set4(rvar, k, (int)var);
+          set4(rbr, k, br);
+          set4(rbc, k, bc);
+          set4(rsme, k, sme);
+          set4(rst, k, steps);
+          set4(rse, k, searches);
+#pragma unroll
+          for (int q = 0; q < 5; ++q) set4(rcl[q], k, cl[q]);
+        }
+        TPL_PROF(tpl_lap(prof[phase == 0 ? 2 : 1], tp));
+      }
+      // the kept centres in ranking order: the smallest error wins (strict <)
+      int win_k = get4(ix, 0);
+      uint32_t bestsme = (uint32_t)get4(rvar, win_k);
+      for (int i = 1; i < np; ++i) {
+        const int k = get4(ix, i);
+        if ((uint32_t)get4(rvar, k) < bestsme) {
+          bestsme = (uint32_t)get4(rvar, k);
+          win_k = k;
+        }
+      }
+      const int best_r = get4(rbr, win_k), best_c = get4(rbc, win_k);
+      const int32_t mine = mv_pack(8 * best_r, 8 * best_c);
+      if (lane == 0) {
+        __hip_atomic_store(mvs + bi, mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        LavishDiamondResult best;
+        best.best_row = (int16_t)best_r;
+        best.best_col = (int16_t)best_c;
+        best.bestsme = get4(rsme, win_k);
+        best.steps = get4(rst, win_k);
+        best.searches = get4(rse, win_k);
+        a.out[j] = best;
+        if (a.centers) a.centers[j] = mv_pack(get4(cr, win_k), get4(cc, win_k));
+      }
+      if (want_cl && lane < 5) {
+        int v = INT_MAX;
+#pragma unroll
+        for (int q = 0; q < 5; ++q) v = lane == q ? get4(rcl[q], win_k) : v;
+        a.cost_lists[5 * j + lane] = v;
+      }
+      left = mine;
+      above = above_right;
+      TPL_PROF(tpl_lap(prof[4], tp));
+    }
+  } else {
   for (int col = 0; col < a.cols; ++col) {
     const int64_t bi = (int64_t)row * a.cols + col;
     int32_t above_right = 0;
+    TPL_PROF(uint64_t tp = clock64());
     if (row > 0) {
       if (col == 0) above = await_mv(bi - a.cols);
       if (col + 1 < a.cols) above_right = await_mv(bi - a.cols + 1);
     }
+    TPL_PROF(tpl_lap(prof[0], tp));
     const int64_t j = ref * nb + bi;
     const Job jb = jn;
     if (col + 1 < a.cols) jn = a.jobs[j + 1];
@@ -1145,8 +1463,80 @@ __global__ __launch_bounds__(64) void tpl_mv_kernel(TplMvArgs a) {
       }
     }
     Ctx c = job_ctx(a.src, a.ss, a.ref, a.rs, jb, a.cost);
-    // with one centre the ranking and both cuts change nothing: skip the SAD
-    if (a.prune && n > 1) {
+    TPL_PROF(prof[8 + n] += 1);  // centres before the ranking
+    // av1_make_default_fullpel_ms_params with ref_mv = centre i
+    auto centre_ctx = [&](int i) {
+      const int mr = get4(cr, i), mc = get4(cc, i);
+      Ctx ci = c;
+      ci.ref_mv_row = mr;
+      ci.ref_mv_col = mc;
+      ci.full_ref_row = rawpel(mr);
+      ci.full_ref_col = rawpel(mc);
+      // av1_set_mv_search_range (mcomp.c:206-234): MAX_FULL_PEL_VAL 1023,
+      // MV_LOW / MV_UPP = -/+ (1 << 14)
+      ci.col_min = max((int)jb.col_min, max(((mc + 7) >> 3) - 1023, -2047));
+      ci.row_min = max((int)jb.row_min, max(((mr + 7) >> 3) - 1023, -2047));
+      ci.col_max = max(ci.col_min, min((int)jb.col_max, min((mc >> 3) + 1023, 2047)));
+      ci.row_max = max(ci.row_min, min((int)jb.row_max, min((mr >> 3) + 1023, 2047)));
+      return ci;
+    };
+    // the search's start: the centre clamped to its own limits
+    auto centre_start = [&](const Ctx& ci, int i, int& sr, int& sc) {
+      sr = min(max(rawpel(get4(cr, i)), ci.row_min), ci.row_max);
+      sc = min(max(rawpel(get4(cc, i)), ci.col_min), ci.col_max);
+    };
+    const bool rank = a.prune && n > 1;  // one centre: the ranking and both cuts change nothing
+    int ix[4] = {0, 1, 2, 3};            // original centre of each sorted position
+    if constexpr (kPrefill) {
+      // every centre's search window (pattern's own fill: the start clamped
+      // to the centre's limits) with all loads in flight together; the
+      // ranking SADs then come from the windows wherever the ranking's clamp
+      // (x->mv_limits) lands on the window centre: the ranking and the
+      // windows share one memory latency
+      SW P;
+      P.load_src(c, lane, (lds_u32)win_s[0]);
+      typename SW::fill_v v[4][SW::kFillNI];
+      int rt[4][3];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int k = min(i, n - 1);  // (surplus slots repeat the last centre, never stored)
+        const Ctx ci = centre_ctx(k);
+        int sr, sc;
+        centre_start(ci, k, sr, sc);
+        P.fill_load(ci, lane, sr, sc, v[i]);
+        win_rates_load<W, H>(ci, lane, sr, sc, rt[i]);
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        if (i < n) {
+          P.win = (lds_u32)win_s[i];
+          P.fill_store(lane, v[i]);
+          win_rates_store<W, H>(P.win, lane, rt[i]);
+        }
+      }
+      wave_sync();
+      if (rank) {
+        uint32_t part[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int k = min(i, n - 1);
+          const Ctx ci = centre_ctx(k);
+          int sr, sc;
+          centre_start(ci, k, sr, sc);
+          const int fr = min(max(rawpel(get4(cr, k)), (int)jb.row_min), (int)jb.row_max);
+          const int fc = min(max(rawpel(get4(cc, k)), (int)jb.col_min), (int)jb.col_max);
+          P.win = (lds_u32)win_s[k];
+          win_prefill<W, H>(P, ci, lane, P.win, sr, sc, true);  // (origin only)
+          part[i] = P.group_sad_win(ci, fr, fc, fr == sr && fc == sc);
+          cs[i] = (int)rdlane(part[i], 0);
+          if (fr != sr || fc != sc) {  // off the window centre: from global memory
+            int sad, ssad;
+            sad_and_skip<W, H>(c, lane, fr, fc, sad, ssad);
+            cs[i] = sad;
+          }
+        }
+      }
+    } else if (rank) {
       // get_fullmv_from_mv + clamp_fullmv to x->mv_limits, then sdf: the n
       // SADs' loads in flight together
 #pragma unroll
@@ -1159,6 +1549,8 @@ __global__ __launch_bounds__(64) void tpl_mv_kernel(TplMvArgs a) {
           cs[i] = sad;
         }
       }
+    }
+    if (rank) {
       // insertion sort: stable, like glibc's qsort on <= 4 entries; as
       // compare-exchanges of neighbours (i from 1, each sinking left)
 #pragma unroll
@@ -1166,44 +1558,37 @@ __global__ __launch_bounds__(64) void tpl_mv_kernel(TplMvArgs a) {
 #pragma unroll
         for (int k = i; k > 0; --k) {
           if (i < n && cs[k - 1] > cs[k]) {
-            const int r = cr[k], q = cc[k], x = cs[k];
+            const int r = cr[k], q = cc[k], x = cs[k], o = ix[k];
             cr[k] = cr[k - 1];
             cc[k] = cc[k - 1];
             cs[k] = cs[k - 1];
+            ix[k] = ix[k - 1];
             cr[k - 1] = r;
             cc[k - 1] = q;
             cs[k - 1] = x;
+            ix[k - 1] = o;
           }
         }
       }
       n = min(4 - a.prune, n);
       if (n > 1 && (get4(cs, n - 1) - get4(cs, n - 2)) * 5 > get4(cs, n - 2)) --n;
     }
+    TPL_PROF(tpl_lap(prof[1], tp));
     uint32_t bestsme = 0xFFFFFFFFu;
     int best_r = 0, best_c = 0, win_i = 0;
     int bcl[5] = {INT_MAX, INT_MAX, INT_MAX, INT_MAX, INT_MAX};
     LavishDiamondResult best{};
     for (int i = 0; i < n; ++i) {
       const int mr = get4(cr, i), mc = get4(cc, i);
-      // av1_make_default_fullpel_ms_params with ref_mv = the centre
-      Ctx ci = c;
-      ci.ref_mv_row = mr;
-      ci.ref_mv_col = mc;
-      ci.full_ref_row = rawpel(mr);
-      ci.full_ref_col = rawpel(mc);
-      // av1_set_mv_search_range (mcomp.c:206-234): MAX_FULL_PEL_VAL 1023,
-      // MV_LOW / MV_UPP = -/+ (1 << 14)
-      ci.col_min = max((int)jb.col_min, max(((mc + 7) >> 3) - 1023, -2047));
-      ci.row_min = max((int)jb.row_min, max(((mr + 7) >> 3) - 1023, -2047));
-      ci.col_max = max(ci.col_min, min((int)jb.col_max, min((mc >> 3) + 1023, 2047)));
-      ci.row_max = max(ci.row_min, min((int)jb.row_max, min((mr >> 3) + 1023, 2047)));
+      const Ctx ci = centre_ctx(i);
       int cl[5] = {INT_MAX, INT_MAX, INT_MAX, INT_MAX, INT_MAX};
       int br, bc, steps = 0, searches = 0;
       uint32_t var = 0;
+      const lds_u32 win = (lds_u32)win_s[kPrefill ? get4(ix, i) : 0];
       const int sme = job_search<W, H, PAT, false, PAT>(ci, lane, rawpel(mr), rawpel(mc),
                                                         a.step_param, a.skip, a.method, win,
                                                         want_cl, cl, br, bc, steps, searches,
-                                                        &var);
+                                                        &var, kPrefill);
       // find_fractional_mv_step at FULL_PEL: setup_center_error, the plain
       // variance at the full-pel best (MV_COST_NONE); the pattern searches
       // return it with their var cost
@@ -1227,6 +1612,7 @@ __global__ __launch_bounds__(64) void tpl_mv_kernel(TplMvArgs a) {
         for (int k = 0; k < 5; ++k) bcl[k] = cl[k];
       }
     }
+    TPL_PROF(tpl_lap(prof[2], tp));
     const int32_t mine = mv_pack(8 * best_r, 8 * best_c);
     if (lane == 0) {
       __hip_atomic_store(mvs + bi, mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1239,7 +1625,16 @@ __global__ __launch_bounds__(64) void tpl_mv_kernel(TplMvArgs a) {
     }
     left = mine;
     above = above_right;
+    TPL_PROF(tpl_lap(prof[4], tp));
   }
+  }
+#if LAVISH_TPL_PROF
+  prof[5] = clock64() - tk0;
+  prof[7] = a.cols;
+  if (lane == 0)
+    for (int k = 0; k < 16; ++k)
+      __hip_atomic_fetch_add(&g_tpl_prof[k], prof[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#endif
 }
 
 // ---------------------------------------------------------------------------
@@ -1413,6 +1808,7 @@ __device__ void lj_pass(const Ctx& c, const LjSrc& s, int l, __amdgpu_buffer_rsr
     // the 8 sites: all loads issued, then the SADs (SKIP: 8 x 1 row per
     // lane; full rows: two halves of 4 sites x 2 rows)
     constexpr int NS = SKIP ? 8 : 4;
+    if (active)  // finished jobs' lanes off for the whole step (one branch; measured neutral, r04_v6)
 #pragma unroll
     for (int h = 0; h < 8 / NS; ++h) {
       int rr[NS], cc[NS];
@@ -1601,9 +1997,10 @@ __device__ __forceinline__ void lj_group(
 // nvwg virtual workgroups over gridDim.x (<= nvwg, both multiples of 8, so a
 // virtual workgroup runs on the XCD of its first): with a smaller grid the
 // search holds fewer CU slots while a concurrent leg runs beside it
-// WPG waves per workgroup: 1 lets the dispatcher refill a SIMD slot as soon
-// as one wave's eight jobs are done (a 4-wave workgroup holds its slots until
-// its slowest wave ends, and a new one needs four free slots on one CU)
+// WPG waves per workgroup.  1 would let the dispatcher refill a SIMD slot as
+// soon as one wave's eight jobs are done; measured, four-wave workgroups are
+// faster (0.294 vs 0.303 ms, profiles/r04_v5_c3_wpg_ab.txt): the four waves
+// of a workgroup are consecutive job groups on one CU, sharing its L1
 #ifndef LAVISH_LJ_WAVES
 #define LAVISH_LJ_WAVES 4  // minimum waves per SIMD requested (VGPR budget 512 / this)
 #endif
@@ -1618,10 +2015,10 @@ __global__ __launch_bounds__(64 * WPG, LAVISH_LJ_WAVES) void diamond_lj_kernel(
                   cost_lists, v, nvwg);
 }
 
-static int lj_wpg() {  // LAVISH_C3_WPG=4: four waves per workgroup (the round-3 shape, A/B)
+static int lj_wpg() {  // LAVISH_C3_WPG=1: one wave per workgroup (A/B)
   static const int w = [] {
     const char* e = getenv("LAVISH_C3_WPG");
-    return e != nullptr && atoi(e) == 4 ? 4 : 1;
+    return e != nullptr && atoi(e) == 1 ? 1 : 4;
   }();
   return w;
 }
@@ -1797,6 +2194,17 @@ int fullpel_batch(const uint8_t* src, int src_stride, const uint8_t* ref, int re
 }  // namespace lavish
 
 using namespace lavish;
+
+#if LAVISH_TPL_PROF
+extern "C" int lavish_dbg_tpl_prof(unsigned long long* out16, int reset) {
+  if (hipMemcpyFromSymbol(out16, HIP_SYMBOL(lavish::g_tpl_prof), 16 * 8) != hipSuccess) return -1;
+  if (reset) {
+    const unsigned long long z[16] = {};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(lavish::g_tpl_prof), z, sizeof(z)) != hipSuccess) return -1;
+  }
+  return 0;
+}
+#endif
 
 extern "C" int64_t lavish_tpl_motion_sync_ints(int nrefs, int rows) {
   if (nrefs <= 0 || rows <= 0) return -1;

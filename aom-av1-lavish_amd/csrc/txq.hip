@@ -678,8 +678,13 @@ int txq_frame(const int16_t* residual, int stride, int width, int height, uint32
     return rc;
   }
   // one launch per class, on the caller's stream: the 32-point class (few,
-  // register-heavy workgroups) first, then the <= 16-point class
+  // register-heavy workgroups) first, then the <= 16-point class.  mode 2
+  // (LAVISH_TXQ_FRAME_MODE=2, A/B): the 32-point class on an internal
+  // stream beside the other (fork / join through fan_out / fan_in) --
+  // measured slower (C2 0.565 -> 0.577 ms, profiles/r04_v5_c2_streams_ab.txt)
+  hipStream_t* fs = mode == 2 ? fan_out(caller) : nullptr;
   for (int cls = 1; cls >= 0; --cls) {
+    const hipStream_t cs = (mode == 2 && cls == 1) ? fs[1] : caller;
     TxqMulti m{};
     int g = 0;
     for (int i = 0; i < n; ++i) {
@@ -687,15 +692,18 @@ int txq_frame(const int16_t* residual, int stride, int width, int height, uint32
       if ((txq_class(s) ? 1 : 0) != cls) continue;
       if (tx_w(s) > 32 || tx_h(s) > 32) {  // 64-point sizes: their own path
         rc = txq_plane(residual, stride, width, height, s, type_masks[s], bd, quant_kind, qp,
-                       qcoeff[s], dqcoeff[s], eob[s], nullptr, caller);
-        if (rc) return rc;
+                       qcoeff[s], dqcoeff[s], eob[s], nullptr, cs);
+        if (rc) break;
         continue;
       }
-      if (m.d.n == kMultiMax) return -2;
+      if (m.d.n == kMultiMax) {
+        rc = -2;
+        break;
+      }
       TxqArgs& a = m.a[txq_slot(s)];
       rc = txq_args(residual, stride, width, height, s, type_masks[s], bd, quant_kind, qp,
                     qcoeff[s], dqcoeff[s], eob[s], nullptr, a);
-      if (rc) return rc;
+      if (rc) break;
       const int grid = plan_size(s, a);
       if (grid <= 0) continue;
       m.d.code[m.d.n] = s;
@@ -703,17 +711,19 @@ int txq_frame(const int16_t* residual, int stride, int width, int height, uint32
       g += grid;
       ++m.d.n;
     }
+    if (rc) break;
     if (m.d.n == 0) continue;
     m.d.wg0[m.d.n] = g;
     if (cls == 0)
-      hipLaunchKernelGGL(txq_multi_kernel<0>, dim3(g), dim3(256), 0, caller, m.d, m.a[0], m.a[1],
+      hipLaunchKernelGGL(txq_multi_kernel<0>, dim3(g), dim3(256), 0, cs, m.d, m.a[0], m.a[1],
                          m.a[2], m.a[3], m.a[4], m.a[5], m.a[6], m.a[7], m.a[8]);
     else
-      hipLaunchKernelGGL(txq_multi_kernel<1>, dim3(g), dim3(256), 0, caller, m.d, m.a[0], m.a[1],
+      hipLaunchKernelGGL(txq_multi_kernel<1>, dim3(g), dim3(256), 0, cs, m.d, m.a[0], m.a[1],
                          m.a[2], m.a[3], m.a[4], m.a[5], m.a[6], m.a[7], m.a[8]);
     LAVISH_CHECK(hipGetLastError());
   }
-  return 0;
+  if (mode == 2) fan_in(caller);
+  return rc;
 }
 
 }  // namespace lavish

@@ -492,6 +492,11 @@ def main_c4(args):
                      "algorithmic_bytes_per_launch": c4_bytes},
     }
     line["roofline"]["frac"] = round(line["roofline"]["achieved"] / HBM_PEAK_GBS, 4)
+    if coded is not None:  # chosen blocks with eob > 0 per TX size (what the inverse runs on)
+        line["coded_blocks"] = {"%dx%d" % (L.TX_W[s], L.TX_H[s]): int(v.sum())
+                                for s, v in coded.items()}
+        line["sb_tx_size"] = {"%dx%d" % (L.TX_W[s], L.TX_H[s]): int(n) for s, n in zip(
+            *np.unique(fr.sb_tx_size.cpu().numpy(), return_counts=True)) if s < 19}
     if args.workload == "c4" and world == 1:
         # the bound that applies: int32 VALU
         rv = c4_roofline(step_ms, W, H, fr.type_masks, coded, c4_bytes)
