@@ -273,6 +273,29 @@ __device__ void sad_and_skip(const Ctx& c, int lane, int row, int col, int& sad,
   ssad = (int)(2 * te);
 }
 
+// sdf (full-row SAD) of a 16x16 block at up to 4 full-pel positions (r[k],
+// cc[k]) for k in [from, to): one source word and four reference words per
+// lane, every load in flight before the first SAD (a call per position
+// waited one memory latency each)
+__device__ __forceinline__ void sad16_multi(const Ctx& c, int lane, const int (&r)[4],
+                                            const int (&cc)[4], int from, int to, int (&out)[4]) {
+  const int y = lane >> 2, x = 4 * (lane & 3);
+  uint32_t sa[1], rb[4][1];
+  load_row<1>(c.src + (int64_t)y * c.ss + x, sa);
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int kk = min(max(k, from), to - 1);  // (surplus slots repeat a valid position)
+    const int rr = k == kk ? r[k] : (kk == 0 ? r[0] : kk == 1 ? r[1] : kk == 2 ? r[2] : r[3]);
+    const int cq = k == kk ? cc[k] : (kk == 0 ? cc[0] : kk == 1 ? cc[1] : kk == 2 ? cc[2] : cc[3]);
+    load_row<1>(c.ref + (int64_t)(rr + y) * c.rs + cq + x, rb[k]);
+  }
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const uint32_t t = groups_sum(group_sum8(sad4(sa[0], rb[k][0], 0)));
+    if (k >= from && k < to) out[k] = (int)t;
+  }
+}
+
 typedef __attribute__((address_space(3))) uint32_t* lds_u32;
 typedef __attribute__((address_space(3))) uint8_t* lds_u8;
 
@@ -843,9 +866,9 @@ __device__ int pattern(const Ctx& c, int lane, int srow, int scol, int search_st
     bc += dc;
   };
   // next_chkpts_indices: k - 1, k, k + 1 (cyclic over n)
-  auto around = [](int j, int k, int n) {
-    return j == 0 ? (k == 0 ? n - 1 : k - 1) : j == 1 ? k : (k == n - 1 ? 0 : k + 1);
-  };
+  // (n is 4 or 8: a mask, no per-lane select chain -- those compiled to
+  // exec-mask branches)
+  auto around = [](int j, int k, int n) { return (k + j - 1 + n) & (n - 1); };
   int k = -1;
   if (do_init) {
     const int smax = best_init_s;
@@ -1109,10 +1132,15 @@ struct TplMvArgs {
 
 constexpr int kTplMaxSpins = 1 << 22;  // ~0.3 s of s_sleep 2 per wait
 #ifndef LAVISH_TPL_PREFILL
-#define LAVISH_TPL_PREFILL 1  // 0: ranking SADs from global memory, then each search's own fill (A/B)
+#define LAVISH_TPL_PREFILL 0  // 1: every centre's window copied at once, ranking SADs from them (A/B)
 #endif
+// LAVISH_TPL_SPEC=1: the speculative row walk (below).  Measured slower
+// than the plain walk once the search got cheaper (2.04-2.12 vs 1.90 ms per
+// 1080p x 7 refs, profiles/r04_v8_tpl_runs.jsonl): its extra per-block work
+// (every kept centre's search before the wait, the bookkeeping of results
+// per centre) costs more than the dependency latency it hides.
 #ifndef LAVISH_TPL_SPEC
-#define LAVISH_TPL_SPEC 1  // 0: no work before the above-right wait (A/B)
+#define LAVISH_TPL_SPEC 0
 #endif
 constexpr int32_t kInvalidMv = (int32_t)0x80008000;  // INVALID_MV (mv.h)
 
@@ -1154,27 +1182,96 @@ __device__ __forceinline__ void tpl_lap(unsigned long long& acc, uint64_t& t) {
 #define TPL_PROF(...)
 #endif
 
+// A block's results, handed from the searching wave to the publishing wave
+struct TplBox {
+  int seq;  // block index + 1 once the payload below is written
+  int mv, br, bc, sme, steps, searches, center, cl[5];
+};
+
 template <bool PAT>
-__global__ __launch_bounds__(64) void tpl_mv_kernel(TplMvArgs a) {
+__global__ __launch_bounds__(128) void tpl_mv_kernel(TplMvArgs a) {
   constexpr int W = 16, H = 16;
   using WN = Win<W, H>;
   constexpr int WSZ = WN::SIZE + (PAT ? 4 + 2 * (2 * WN::R + 1) : 0);
   // PAT: one window per centre, all copied at once; DIAMOND: one
   constexpr bool kPrefill = PAT && LAVISH_TPL_PREFILL;
-  constexpr bool kSpec = kPrefill && LAVISH_TPL_SPEC;
+  constexpr bool kSpec = PAT && LAVISH_TPL_SPEC;
   using SW = Search<W, H, false, false, false>;
-  const int lane = threadIdx.x;
+  const int lane = threadIdx.x & 63;
   // reference windows (+ the pattern searches' mv-cost rates)
   __shared__ uint32_t win_s[kPrefill ? 4 : 1][WSZ];
-  int t = 0;
-  if (lane == 0)
-    t = __hip_atomic_fetch_add(a.sync, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  t = __builtin_amdgcn_readfirstlane(t);
+  __shared__ int res_s[kSpec ? 4 : 1][11];  // the speculative walk's search results
+  __shared__ TplBox box_s[2];               // results by block parity
+  __shared__ int ack_s, ticket_s;           // blocks published; the row ticket
+  if (threadIdx.x == 0) {
+    ticket_s = __hip_atomic_fetch_add(a.sync, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    ack_s = 0;
+    box_s[0].seq = box_s[1].seq = 0;
+  }
+  __syncthreads();
+  const int t = __builtin_amdgcn_readfirstlane(ticket_s);
   TPL_PROF(unsigned long long prof[16] = {});
   const int ref = t % a.nrefs, row = t / a.nrefs;
   if (row >= a.rows) return;
   const int64_t nb = (int64_t)a.rows * a.cols;
   int32_t* const mvs = a.mvs + ref * nb;
+  // Wave 1 publishes: the searching wave (0) hands each block's results over
+  // in LDS and goes on.  On gfx9 a wave's stores and loads share one
+  // completion counter, so a wave that stored its block's mv (a device-scope
+  // store, ~2 us to complete) waited for that store at its next load; with
+  // the stores on another wave the walk's loads wait for themselves only.
+  if (threadIdx.x >= 64) {
+    for (int col = 0; col < a.cols; ++col) {
+      TplBox& b = box_s[col & 1];
+      int spins = 0;
+      while (__hip_atomic_load(&b.seq, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != col + 1) {
+        __builtin_amdgcn_s_sleep(1);
+        if (++spins >= kTplMaxSpins) {  // (bounded: the grid always drains)
+          if (lane == 0)
+            __hip_atomic_fetch_add(a.sync + 1, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          break;
+        }
+      }
+      const int64_t bi = (int64_t)row * a.cols + col, j = ref * nb + bi;
+      if (lane == 0) {
+        __hip_atomic_store(mvs + bi, b.mv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        LavishDiamondResult best;
+        best.best_row = (int16_t)b.br;
+        best.best_col = (int16_t)b.bc;
+        best.bestsme = b.sme;
+        best.steps = b.steps;
+        best.searches = b.searches;
+        a.out[j] = best;
+        if (a.centers) a.centers[j] = b.center;
+      }
+      if (a.cost_lists != nullptr && lane < 5) a.cost_lists[5 * j + lane] = b.cl[lane];
+      __hip_atomic_store(&ack_s, col + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+    return;
+  }
+  // block col's results to the publishing wave (box reused every 2 blocks)
+  auto publish = [&](int col, int32_t mv, int br, int bc, int sme, int steps, int searches,
+                     int32_t center, const int* cl5) {
+    TplBox& b = box_s[col & 1];
+    int spins = 0;
+    while (col >= 2 &&
+           __hip_atomic_load(&ack_s, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < col - 1) {
+      __builtin_amdgcn_s_sleep(1);
+      if (++spins >= kTplMaxSpins) break;
+    }
+    if (lane == 0) {
+      b.mv = mv;
+      b.br = br;
+      b.bc = bc;
+      b.sme = sme;
+      b.steps = steps;
+      b.searches = searches;
+      b.center = center;
+#pragma unroll
+      for (int q = 0; q < 5; ++q) b.cl[q] = cl5[q];
+      __hip_atomic_store(&b.seq, col + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+  };
   bool waiting = true;
   // poll a published mv of the row above (uniform)
   auto await_mv = [&](int64_t k) -> int32_t {
@@ -1194,7 +1291,23 @@ __global__ __launch_bounds__(64) void tpl_mv_kernel(TplMvArgs a) {
   };
   const bool want_cl = a.cost_lists != nullptr;
   int32_t above = 0, left = 0;
-  Job jn = a.jobs[ref * nb + (int64_t)row * a.cols];  // the next block's job, loaded a step ahead
+  // the next block's job, loaded a step ahead as one dword per lane (lanes
+  // 0..7) and kept in a vector register until the step that uses it: loaded
+  // straight into scalars, the compiler waited for it at the load (one
+  // exposed memory latency per block)
+  auto job_load = [&](int64_t k) -> uint32_t {
+    return ((const uint32_t*)(a.jobs + k))[min(lane, 7)];
+  };
+  auto job_get = [&](uint32_t w) {
+    uint32_t d[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) d[q] = (uint32_t)__builtin_amdgcn_readlane((int)w, q);
+    Job jb;
+    __builtin_memcpy(&jb, d, sizeof(Job));
+    return jb;
+  };
+  static_assert(sizeof(Job) == 32, "job: 8 dwords");
+  uint32_t jw = job_load(ref * nb + (int64_t)row * a.cols);
   TPL_PROF(const uint64_t tk0 = clock64());
   if constexpr (kSpec) {
     // The row walk with speculation: everything a block needs but the
@@ -1215,8 +1328,8 @@ __global__ __launch_bounds__(64) void tpl_mv_kernel(TplMvArgs a) {
       TPL_PROF(uint64_t tp = clock64());
       if (row > 0 && col == 0) above = await_mv(bi - a.cols);
       const int64_t j = ref * nb + bi;
-      const Job jb = jn;
-      if (col + 1 < a.cols) jn = a.jobs[j + 1];
+      const Job jb = job_get(jw);
+      if (col + 1 < a.cols) jw = job_load(j + 1);
       const bool has_ar = row > 0 && col + 1 < a.cols;
       const bool spec = a.third == nullptr;
       int cr[4] = {0, 0, 0, 0}, cc[4] = {0, 0, 0, 0}, cs[4] = {0, 0, 0, 0};
@@ -1252,13 +1365,11 @@ __global__ __launch_bounds__(64) void tpl_mv_kernel(TplMvArgs a) {
         ci.row_max = max(ci.row_min, min((int)jb.row_max, min((mr >> 3) + 1023, 2047)));
         return ci;
       };
-      P.load_src(c, lane, (lds_u32)win_s[0]);  // (the source rows of the ranking SADs)
-      // per centre (original index): its search's results once run
-      int have = 0, rvar[4] = {0, 0, 0, 0}, rbr[4] = {0, 0, 0, 0}, rbc[4] = {0, 0, 0, 0};
-      int rsme[4] = {0, 0, 0, 0}, rst[4] = {0, 0, 0, 0}, rse[4] = {0, 0, 0, 0};
-      int rcl[5][4];
-#pragma unroll
-      for (int q = 0; q < 5; ++q) rcl[q][0] = rcl[q][1] = rcl[q][2] = rcl[q][3] = INT_MAX;
+      if constexpr (kPrefill) P.load_src(c, lane, (lds_u32)win_s[0]);  // (the window SADs' source rows)
+      // per centre (original index): its search's results once run, in LDS
+      // (res_s[k]: var, row, col, sme, steps, searches, cost list) -- in
+      // registers they were 44 live scalars across every search
+      int have = 0;
       int ix[4] = {0, 1, 2, 3}, np = 1, nf = 0;
       int32_t above_right = 0;
       for (int phase = spec ? 0 : 1; phase < 2; ++phase) {
@@ -1284,10 +1395,24 @@ __global__ __launch_bounds__(64) void tpl_mv_kernel(TplMvArgs a) {
             }
           }
         }
+        TPL_PROF(tpl_lap(prof[8], tp));
         // windows (pattern's own fill at the start clamped to the centre's
         // limits, all loads in flight together) and ranking SADs of the
         // centres [nf, n)
-        {
+        if constexpr (!kPrefill) {  // ranking SADs from global memory, all in flight
+          if (a.prune) {
+            // get_fullmv_from_mv + clamp_fullmv to x->mv_limits, then sdf
+            int fr[4], fc[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+              fr[k] = min(max(rawpel(cr[k]), (int)jb.row_min), (int)jb.row_max);
+              fc[k] = min(max(rawpel(cc[k]), (int)jb.col_min), (int)jb.col_max);
+            }
+            sad16_multi(c, lane, fr, fc, nf, n, cs);
+          }
+          nf = n;
+          TPL_PROF(tpl_lap(prof[10], tp));
+        } else {
           typename SW::fill_v v[4][SW::kFillNI];
           int rt[4][3];
 #pragma unroll
@@ -1309,6 +1434,7 @@ __global__ __launch_bounds__(64) void tpl_mv_kernel(TplMvArgs a) {
             }
           }
           wave_sync();
+          TPL_PROF(tpl_lap(prof[9], tp));
           if (a.prune) {
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
@@ -1331,6 +1457,7 @@ __global__ __launch_bounds__(64) void tpl_mv_kernel(TplMvArgs a) {
             }
           }
           nf = n;
+          TPL_PROF(tpl_lap(prof[10], tp));
         }
         // the ranking: stable insertion sort of the centres by SAD (glibc's
         // qsort on <= 4 entries), cut to 4 - prune_starting_mv and by the
@@ -1358,61 +1485,54 @@ __global__ __launch_bounds__(64) void tpl_mv_kernel(TplMvArgs a) {
           np = min(4 - a.prune, n);
           if (np > 1 && (get4(sc4, np - 1) - get4(sc4, np - 2)) * 5 > get4(sc4, np - 2)) --np;
         }
+        TPL_PROF(tpl_lap(prof[11], tp));
         // the searches of the kept centres not yet run
 #pragma unroll 1
         for (int i = 0; i < np; ++i) {
           const int k = get4(ix, i);
           if ((have >> k) & 1) continue;
+          TPL_PROF(prof[13] += 1);
           const int mr = get4(cr, k), mc = get4(cc, k);
           const Ctx ci = centre_ctx(k);
           int cl[5] = {INT_MAX, INT_MAX, INT_MAX, INT_MAX, INT_MAX};
           int br, bc, steps = 0, searches = 0;
           uint32_t var = 0;
-          const int sme = job_search<W, H, PAT, false, PAT>(ci, lane, rawpel(mr), rawpel(mc),
-                                                            a.step_param, a.skip, a.method,
-                                                            (lds_u32)win_s[k], want_cl, cl, br, bc,
-                                                            steps, searches, &var, true);
+          const int sme = job_search<W, H, PAT, false, PAT>(
+              ci, lane, rawpel(mr), rawpel(mc), a.step_param, a.skip, a.method,
+              (lds_u32)win_s[kPrefill ? k : 0], want_cl, cl, br, bc, steps, searches, &var,
+              kPrefill);
           have |= 1 << k;
-          set4(rvar, k, (int)var);
-          set4(rbr, k, br);
-          set4(rbc, k, bc);
-          set4(rsme, k, sme);
-          set4(rst, k, steps);
-          set4(rse, k, searches);
+          if (lane == 0) {
+            int* o = res_s[k];
+            o[0] = (int)var;
+            o[1] = br;
+            o[2] = bc;
+            o[3] = sme;
+            o[4] = steps;
+            o[5] = searches;
 #pragma unroll
-          for (int q = 0; q < 5; ++q) set4(rcl[q], k, cl[q]);
+            for (int q = 0; q < 5; ++q) o[6 + q] = cl[q];
+          }
         }
-        TPL_PROF(tpl_lap(prof[phase == 0 ? 2 : 1], tp));
+        TPL_PROF(tpl_lap(prof[12], tp));
       }
       // the kept centres in ranking order: the smallest error wins (strict <)
+      wave_sync();
       int win_k = get4(ix, 0);
-      uint32_t bestsme = (uint32_t)get4(rvar, win_k);
+      uint32_t bestsme = (uint32_t)res_s[win_k][0];
       for (int i = 1; i < np; ++i) {
         const int k = get4(ix, i);
-        if ((uint32_t)get4(rvar, k) < bestsme) {
-          bestsme = (uint32_t)get4(rvar, k);
+        if ((uint32_t)res_s[k][0] < bestsme) {
+          bestsme = (uint32_t)res_s[k][0];
           win_k = k;
         }
       }
-      const int best_r = get4(rbr, win_k), best_c = get4(rbc, win_k);
+      const int* w = res_s[win_k];
+      const int best_r = w[1], best_c = w[2];
       const int32_t mine = mv_pack(8 * best_r, 8 * best_c);
-      if (lane == 0) {
-        __hip_atomic_store(mvs + bi, mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        LavishDiamondResult best;
-        best.best_row = (int16_t)best_r;
-        best.best_col = (int16_t)best_c;
-        best.bestsme = get4(rsme, win_k);
-        best.steps = get4(rst, win_k);
-        best.searches = get4(rse, win_k);
-        a.out[j] = best;
-        if (a.centers) a.centers[j] = mv_pack(get4(cr, win_k), get4(cc, win_k));
-      }
-      if (want_cl && lane < 5) {
-        int v = INT_MAX;
-#pragma unroll
-        for (int q = 0; q < 5; ++q) v = lane == q ? get4(rcl[q], win_k) : v;
-        a.cost_lists[5 * j + lane] = v;
-      }
+      publish(col, mine, best_r, best_c, w[3], w[4], w[5],
+              mv_pack(get4(cr, win_k), get4(cc, win_k)), w + 6);
+      (void)j;
       left = mine;
       above = above_right;
       TPL_PROF(tpl_lap(prof[4], tp));
@@ -1428,8 +1548,8 @@ __global__ __launch_bounds__(64) void tpl_mv_kernel(TplMvArgs a) {
     }
     TPL_PROF(tpl_lap(prof[0], tp));
     const int64_t j = ref * nb + bi;
-    const Job jb = jn;
-    if (col + 1 < a.cols) jn = a.jobs[j + 1];
+    const Job jb = job_get(jw);
+    if (col + 1 < a.cols) jw = job_load(j + 1);
     // centre candidates (row, col in 1/8 pel) and their SADs
     int cr[4] = {0, 0, 0, 0}, cc[4] = {0, 0, 0, 0}, cs[4] = {0, 0, 0, 0};
     int n = 1;
@@ -1539,16 +1659,13 @@ __global__ __launch_bounds__(64) void tpl_mv_kernel(TplMvArgs a) {
     } else if (rank) {
       // get_fullmv_from_mv + clamp_fullmv to x->mv_limits, then sdf: the n
       // SADs' loads in flight together
+      int fr[4], fc[4];
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        if (i < n) {
-          const int fr = min(max(rawpel(cr[i]), (int)jb.row_min), (int)jb.row_max);
-          const int fc = min(max(rawpel(cc[i]), (int)jb.col_min), (int)jb.col_max);
-          int sad, ssad;
-          sad_and_skip<W, H>(c, lane, fr, fc, sad, ssad);
-          cs[i] = sad;
-        }
+        fr[i] = min(max(rawpel(cr[i]), (int)jb.row_min), (int)jb.row_max);
+        fc[i] = min(max(rawpel(cc[i]), (int)jb.col_min), (int)jb.col_max);
       }
+      sad16_multi(c, lane, fr, fc, 0, n, cs);
     }
     if (rank) {
       // insertion sort: stable, like glibc's qsort on <= 4 entries; as
@@ -1614,15 +1731,8 @@ __global__ __launch_bounds__(64) void tpl_mv_kernel(TplMvArgs a) {
     }
     TPL_PROF(tpl_lap(prof[2], tp));
     const int32_t mine = mv_pack(8 * best_r, 8 * best_c);
-    if (lane == 0) {
-      __hip_atomic_store(mvs + bi, mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      a.out[j] = best;
-      if (a.centers) a.centers[j] = mv_pack(get4(cr, win_i), get4(cc, win_i));
-    }
-    if (want_cl && lane < 5) {
-      const int v = lane == 0 ? bcl[0] : lane == 1 ? bcl[1] : lane == 2 ? bcl[2] : lane == 3 ? bcl[3] : bcl[4];
-      a.cost_lists[5 * j + lane] = v;
-    }
+    publish(col, mine, best_r, best_c, best.bestsme, best.steps, best.searches,
+            mv_pack(get4(cr, win_i), get4(cc, win_i)), bcl);
     left = mine;
     above = above_right;
     TPL_PROF(tpl_lap(prof[4], tp));
@@ -2260,9 +2370,9 @@ extern "C" int lavish_tpl_motion_search(const uint8_t* src, int src_stride, cons
   a.sync = sync;
   const dim3 grid((unsigned)(nrefs * rows));
   if (m == kDiamond)
-    hipLaunchKernelGGL(tpl_mv_kernel<false>, grid, dim3(64), 0, s, a);
+    hipLaunchKernelGGL(tpl_mv_kernel<false>, grid, dim3(128), 0, s, a);
   else
-    hipLaunchKernelGGL(tpl_mv_kernel<true>, grid, dim3(64), 0, s, a);
+    hipLaunchKernelGGL(tpl_mv_kernel<true>, grid, dim3(128), 0, s, a);
   LAVISH_CHECK(hipGetLastError());
   return 0;
 }

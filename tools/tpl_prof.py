@@ -53,7 +53,9 @@ def main(reps=5):
            "new_centre_after_wait_frac": round(v[3] / steps, 4),
            "walk_cycles_per_wave": round(v[5] / max(1, reps * tf.rows * tf.nrefs), 1),
            "polls_ready_first_time": v[6],
-           "centres_before_ranking": {str(k): v[8 + k] for k in range(1, 5)}}
+           "speculative_walk_cycles_per_step": {n: round(v[8 + i] / steps, 1) for i, n in enumerate(
+               ["centres", "window_fill", "ranking_sads", "sort_cut", "searches"])},
+           "searches_per_step": round(v[13] / steps, 3)}
     print(json.dumps(out))
 
 
