@@ -1860,6 +1860,26 @@ __device__ __forceinline__ void lj_sads(const Ctx& c, const LjSrc& s, int l,
   }
 }
 
+// lj_sads (downsampled rows) for offsets into the tiled copy computed by the
+// caller: lane l's row 2l of each candidate
+template <int N>
+__device__ __forceinline__ void lj_sads_off(const LjSrc& s, __amdgpu_buffer_rsrc_t trs, int oob,
+                                            const uint32_t (&off)[N], const bool (&v)[N],
+                                            uint32_t (&out)[N]) {
+  u32x4 t[N];
+#pragma unroll
+  for (int i = 0; i < N; ++i)
+    t[i] = __builtin_amdgcn_raw_buffer_load_b128(trs, v[i] ? (int)off[i] : oob, 0, 0);
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    uint32_t acc = sad4(s.sk[0], t[i].x, 0);
+    acc = sad4(s.sk[1], t[i].y, acc);
+    acc = sad4(s.sk[2], t[i].z, acc);
+    acc = sad4(s.sk[3], t[i].w, acc);
+    out[i] = 2 * group_sum8(acc);
+  }
+}
+
 // mvsad_err_cost's table reads for the entropy cost through the decimated
 // copy of the caller's row / column tables (dec[0..4094] = mvcost0[8 k],
 // dec[4095..] = mvcost1[8 k], k = -2047 .. 2047, built per call by
@@ -1918,6 +1938,45 @@ __device__ void lj_pass(const Ctx& c, const LjSrc& s, int l, __amdgpu_buffer_rsr
     // the 8 sites: all loads issued, then the SADs (SKIP: 8 x 1 row per
     // lane; full rows: two halves of 4 sites x 2 rows)
     constexpr int NS = SKIP ? 8 : 4;
+    if constexpr (SKIP) {
+      // the sites' tile offsets and range checks from per-step parts: the
+      // walk's position is in range, so a site is valid iff its row and
+      // column moves stay inside; with an even radius the site rows keep
+      // the field of row y and move its row half linearly (rad / 2 strip
+      // rows), so an offset is one add of a row part (3 per step) and a
+      // column part (3 per step) instead of a tile_off per site
+      const bool up = row - rad >= c.row_min, dn = row + rad <= c.row_max;
+      const bool lf = col - rad >= c.col_min, rt = col + rad <= c.col_max;
+      const int y0 = c.oy + row + 2 * l, x0 = c.ox + col;
+      uint32_t off[8];
+      bool vv[8];
+      if (stp > 0) {
+        const int yb = (y0 & 1) * c.fsz + ((y0 >> 1) << 5), d16 = rad << 4;
+        const int f32 = c.fh << 5;
+        auto xo = [&](int x) { return __mul24(x >> 4, f32) + (x & 15); };
+        const int xm = xo(x0 - rad), xc = xo(x0), xp = xo(x0 + rad);
+#pragma unroll
+        for (int t = 0; t < 8; ++t) {
+          const int dr = site_dr(t), dc = site_dc(t);
+          off[t] = (uint32_t)((dr < 0 ? yb - d16 : dr > 0 ? yb + d16 : yb) +
+                              (dc < 0 ? xm : dc > 0 ? xp : xc));
+        }
+      } else {
+#pragma unroll
+        for (int t = 0; t < 8; ++t) off[t] = tile_off(c, y0 + site_dr(t), x0 + site_dc(t));
+      }
+#pragma unroll
+      for (int t = 0; t < 8; ++t) {
+        const int dr = site_dr(t), dc = site_dc(t);
+        vv[t] = active && (dr < 0 ? up : dr > 0 ? dn : true) && (dc < 0 ? lf : dc > 0 ? rt : true);
+      }
+      if (active) {
+        uint32_t sd[8];
+        lj_sads_off<8>(s, trs, oob, off, vv, sd);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) mine = l == i ? sd[i] : mine;
+      }
+    } else
     if (active)  // finished jobs' lanes off for the whole step (one branch; measured neutral, r04_v6)
 #pragma unroll
     for (int h = 0; h < 8 / NS; ++h) {

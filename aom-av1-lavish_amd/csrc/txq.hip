@@ -714,11 +714,17 @@ int txq_frame(const int16_t* residual, int stride, int width, int height, uint32
     if (rc) break;
     if (m.d.n == 0) continue;
     m.d.wg0[m.d.n] = g;
+    // LAVISH_C2_LDS_PAD=n (A/B only): n more bytes of LDS per workgroup, so
+    // fewer C2 workgroups fit a CU and a concurrent leg's waves find room
+    static const int pad = [] {
+      const char* e = getenv("LAVISH_C2_LDS_PAD");
+      return e ? atoi(e) : 0;
+    }();
     if (cls == 0)
-      hipLaunchKernelGGL(txq_multi_kernel<0>, dim3(g), dim3(256), 0, cs, m.d, m.a[0], m.a[1],
+      hipLaunchKernelGGL(txq_multi_kernel<0>, dim3(g), dim3(256), pad, cs, m.d, m.a[0], m.a[1],
                          m.a[2], m.a[3], m.a[4], m.a[5], m.a[6], m.a[7], m.a[8]);
     else
-      hipLaunchKernelGGL(txq_multi_kernel<1>, dim3(g), dim3(256), 0, cs, m.d, m.a[0], m.a[1],
+      hipLaunchKernelGGL(txq_multi_kernel<1>, dim3(g), dim3(256), pad, cs, m.d, m.a[0], m.a[1],
                          m.a[2], m.a[3], m.a[4], m.a[5], m.a[6], m.a[7], m.a[8]);
     LAVISH_CHECK(hipGetLastError());
   }
