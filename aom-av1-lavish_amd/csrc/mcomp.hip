@@ -24,6 +24,8 @@
 // reference pixels come from L2 / MALL (a 1080p padded reference is ~2.5 MB).
 #include <type_traits>
 
+#include <atomic>
+
 #include "lavish_internal.h"
 
 namespace lavish {
@@ -292,6 +294,37 @@ __device__ __forceinline__ void sad16_multi(const Ctx& c, int lane, const int (&
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
     const uint32_t t = groups_sum(group_sum8(sad4(sa[0], rb[k][0], 0)));
+    if (k >= from && k < to) out[k] = (int)t;
+  }
+}
+
+// sad16_multi in two halves: the loads (a caller can issue them before a
+// wait and use them after it), then the SADs
+struct Sad16Loads {
+  uint32_t sa, rb[4];
+};
+__device__ __forceinline__ Sad16Loads sad16_load(const Ctx& c, int lane, const int (&r)[4],
+                                                 const int (&cc)[4], int from, int to) {
+  const int y = lane >> 2, x = 4 * (lane & 3);
+  Sad16Loads L;
+  uint32_t t[1];
+  load_row<1>(c.src + (int64_t)y * c.ss + x, t);
+  L.sa = t[0];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int kk = min(max(k, from), to - 1);
+    const int rr = k == kk ? r[k] : (kk == 0 ? r[0] : kk == 1 ? r[1] : kk == 2 ? r[2] : r[3]);
+    const int cq = k == kk ? cc[k] : (kk == 0 ? cc[0] : kk == 1 ? cc[1] : kk == 2 ? cc[2] : cc[3]);
+    load_row<1>(c.ref + (int64_t)(rr + y) * c.rs + cq + x, t);
+    L.rb[k] = t[0];
+  }
+  return L;
+}
+__device__ __forceinline__ void sad16_finish(const Sad16Loads& L, int from, int to,
+                                             int (&out)[4]) {
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const uint32_t t = groups_sum(group_sum8(sad4(L.sa, L.rb[k], 0)));
     if (k >= from && k < to) out[k] = (int)t;
   }
 }
@@ -1542,11 +1575,7 @@ __global__ __launch_bounds__(128) void tpl_mv_kernel(TplMvArgs a) {
     const int64_t bi = (int64_t)row * a.cols + col;
     int32_t above_right = 0;
     TPL_PROF(uint64_t tp = clock64());
-    if (row > 0) {
-      if (col == 0) above = await_mv(bi - a.cols);
-      if (col + 1 < a.cols) above_right = await_mv(bi - a.cols + 1);
-    }
-    TPL_PROF(tpl_lap(prof[0], tp));
+    if (row > 0 && col == 0) above = await_mv(bi - a.cols);
     const int64_t j = ref * nb + bi;
     const Job jb = job_get(jw);
     if (col + 1 < a.cols) jw = job_load(j + 1);
@@ -1574,15 +1603,49 @@ __global__ __launch_bounds__(128) void tpl_mv_kernel(TplMvArgs a) {
     };
     if (row > 0) add(above);
     if (col > 0) add(left);
-    if (row > 0 && col + 1 < a.cols) add(above_right);
+    Ctx c = job_ctx(a.src, a.ss, a.ref, a.rs, jb, a.cost);
+    // get_fullmv_from_mv + clamp_fullmv to x->mv_limits: the ranking's point
+    int fr[4], fc[4];
+    auto rank_points = [&]() {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        fr[i] = min(max(rawpel(cr[i]), (int)jb.row_min), (int)jb.row_max);
+        fc[i] = min(max(rawpel(cc[i]), (int)jb.col_min), (int)jb.col_max);
+      }
+    };
+    // the ranking loads of the centres known before the above-right block
+    // (zero / above / left) go out before its wait; their SADs are taken
+    // after it (without prune_starting_mv nothing is ranked)
+    const int n0 = n;
+    Sad16Loads pre{};
+    if (!kPrefill && a.prune) {
+      rank_points();
+      pre = sad16_load(c, lane, fr, fc, 0, n0);
+    }
+    if (row > 0 && col + 1 < a.cols) {
+      above_right = await_mv(bi - a.cols + 1);
+      add(above_right);
+    }
+    TPL_PROF(tpl_lap(prof[0], tp));
+    bool c0_new = false;
     if (a.third) {
       const int32_t m = a.third[j];
       if (m != kInvalidMv && !alike(mv_row(m), mv_col(m), 1)) {
         cr[0] = mv_row(m);
         cc[0] = mv_col(m);
+        c0_new = true;
       }
     }
-    Ctx c = job_ctx(a.src, a.ss, a.ref, a.rs, jb, a.cost);
+    if (!kPrefill && a.prune && n > 1) {
+      if (n > n0 || c0_new) {  // the above-right centre / a third-pass centre 0: after the wait
+        rank_points();
+        const Sad16Loads post = sad16_load(c, lane, fr, fc, c0_new ? 0 : n0, n);
+        if (!c0_new) sad16_finish(pre, 0, n0, cs);
+        sad16_finish(post, c0_new ? 0 : n0, n, cs);
+      } else {
+        sad16_finish(pre, 0, n, cs);
+      }
+    }
     TPL_PROF(prof[8 + n] += 1);  // centres before the ranking
     // av1_make_default_fullpel_ms_params with ref_mv = centre i
     auto centre_ctx = [&](int i) {
@@ -1656,16 +1719,6 @@ __global__ __launch_bounds__(128) void tpl_mv_kernel(TplMvArgs a) {
           }
         }
       }
-    } else if (rank) {
-      // get_fullmv_from_mv + clamp_fullmv to x->mv_limits, then sdf: the n
-      // SADs' loads in flight together
-      int fr[4], fc[4];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        fr[i] = min(max(rawpel(cr[i]), (int)jb.row_min), (int)jb.row_max);
-        fc[i] = min(max(rawpel(cc[i]), (int)jb.col_min), (int)jb.col_max);
-      }
-      sad16_multi(c, lane, fr, fc, 0, n, cs);
     }
     if (rank) {
       // insertion sort: stable, like glibc's qsort on <= 4 entries; as
@@ -2211,11 +2264,16 @@ static bool lj_dec_enabled() {  // LAVISH_C3_MVDEC=0: the caller's tables direct
 }
 thread_local StreamScratch t_mvdec;
 
-static int lj_grid_cap() {  // LAVISH_C3_WGS=n: at most n workgroups (rounded to 8)
-  static const int cap = [] {
+// at most this many workgroups for the 16x16 DIAMOND search (rounded to 8;
+// 0: one per 32 jobs): lavish_set_search_workgroup_cap, else LAVISH_C3_WGS
+static std::atomic<int> g_lj_cap{-1};
+static int lj_grid_cap() {
+  int cap = g_lj_cap.load(std::memory_order_relaxed);
+  if (cap < 0) {
     const char* e = getenv("LAVISH_C3_WGS");
-    return e == nullptr ? 0 : (atoi(e) + 7) & ~7;
-  }();
+    cap = e == nullptr ? 0 : (atoi(e) + 7) & ~7;
+    g_lj_cap.store(cap, std::memory_order_relaxed);
+  }
   return cap;
 }
 
@@ -2374,6 +2432,12 @@ extern "C" int lavish_dbg_tpl_prof(unsigned long long* out16, int reset) {
   return 0;
 }
 #endif
+
+extern "C" int lavish_set_search_workgroup_cap(int workgroups) {
+  if (workgroups < 0) return -1;
+  lavish::g_lj_cap.store((workgroups + 7) & ~7, std::memory_order_relaxed);
+  return 0;
+}
 
 extern "C" int64_t lavish_tpl_motion_sync_ints(int nrefs, int rows) {
   if (nrefs <= 0 || rows <= 0) return -1;

@@ -906,11 +906,16 @@ __global__ __launch_bounds__(256) void sb_decide_kernel(SbArgs a) {
     const int bw = a.width / W, nx = x1 / W, nblk = nx * (y1 / H);
     // costs are >= 0; a block without a candidate costs INT64_MAX, so the
     // sums saturate there instead of wrapping
-    int64_t sum = 0;
-    for (int k = lane; k < nblk; k += 64) {
+    // (nblk <= 256: the loads of up to 4 blocks per lane in flight together;
+    // a sum of non-negative costs saturating at INT64_MAX is order-free)
+    int64_t v[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int k = lane + 64 * q;
       const int y = k / nx, x = k - y * nx;
-      sum = sat_add(sum, a.rec[s][(sy * 64 / H + y) * bw + sx * 64 / W + x].rdcost);
+      v[q] = k < nblk ? a.rec[s][(sy * 64 / H + y) * bw + sx * 64 / W + x].rdcost : 0;
     }
+    int64_t sum = sat_add(sat_add(v[0], v[1]), sat_add(v[2], v[3]));
 #pragma unroll
     for (int m = 1; m < 64; m <<= 1) sum = sat_add(sum, __shfl_xor(sum, m));
     if (sum < best) {

@@ -63,6 +63,9 @@ _lib.lavish_full_pixel_search_batch_tiled.argtypes = [
     _vp, _i32, _vp, _i32, ctypes.POINTER(RefTilesDesc), _i32, _i32, _vp, _i32, _i32, _i32,
     ctypes.POINTER(MvCostParams), _i32, _vp, _vp, _vp]
 _lib.lavish_full_pixel_search_batch_tiled.restype = _i32
+if hasattr(_lib, "lavish_set_search_workgroup_cap"):  # (older experiment builds lack it)
+    _lib.lavish_set_search_workgroup_cap.argtypes = [_i32]
+    _lib.lavish_set_search_workgroup_cap.restype = _i32
 
 
 class RefTiles:
@@ -113,6 +116,15 @@ class MvCosts:
         c.mvcost[1] = self.mvcost.data_ptr() + row + 4 * MV_MAX
         c._owner = self  # the device tables live as long as the parameters
         return c
+
+
+def set_search_workgroup_cap(workgroups):
+    """lavish_set_search_workgroup_cap: at most `workgroups` workgroups for
+    the 16x16 DIAMOND search (0: no cap) -- a scheduling knob for running the
+    search beside other streams' work; results do not depend on it."""
+    rc = _lib.lavish_set_search_workgroup_cap(int(workgroups))
+    if rc:
+        raise ValueError("lavish_set_search_workgroup_cap(%r): %d" % (workgroups, rc))
 
 
 def default_mv_cost_tables(allow_hp=False):

@@ -87,6 +87,8 @@ def parse():
                          "all-gathers, or the row-wavefront with p2p edges (lavish_dsp/shard.py)")
     ap.add_argument("--no-c4", action="store_true",
                     help="skip the c4 sub-object (4K 10-bit RDO step) of the default line")
+    ap.add_argument("--c3-wg-cap", type=int, default=C3_WG_CAP,
+                    help="workgroups of the C3 search when it runs beside C2 (0: no cap)")
     ap.add_argument("--serial", action="store_true",
                     help="run the C3 and C2 legs back to back on one stream (default: C3 on a "
                          "second stream beside C2)")
@@ -140,6 +142,7 @@ C3_BLOCK = 16
 C3_COST = 0     # MV_COST_ENTROPY (the RDO path's x->mv_cost_type)
 C3_SKIP = True  # use_downsampled_sad (>= 720p, speed_features.c:205-209)
 C3_CL = True    # cost list: subpel_search_method != SUBPEL_TREE (cond_cost_list)
+C3_WG_CAP = 512  # C3's workgroups beside C2 (profiles/r04_v11_*: the step's best)
 # sub-pixel refinement after the full-pel search (c3sub): SUBPEL_TREE_PRUNED_MORE
 # (speed >= 4), subpel_force_stop EIGHTH_PEL, iters_per_step 1 (speed >= 2),
 # allow_high_precision_mv = qindex < HIGH_PRECISION_MV_QTHRESH (128)
@@ -1593,6 +1596,9 @@ def main():
         if do_c3:
             if ev is not None:
                 ev[1].record(side)
+            # beside C2 the search runs in fewer workgroups (it holds fewer CU
+            # slots and C2 stretches less: DESIGN.md section 5); alone, uncapped
+            M.set_search_workgroup_cap(args.c3_wg_cap if ovl else 0)
             c3(side)
             if ev is not None:
                 ev[2].record(side)
@@ -1712,7 +1718,9 @@ def main():
                         % (args.workload, W, H, " + ".join(legs), sb),
             "tx_sizes": [L.TX_SIZES[s] for s in sizes] if do_c2 else [],
             "parallelism": "frame-per-rank x%d" % world,
-            "legs": "C3 on a second stream beside C2" if overlap else "C3 then C2, one stream",
+            "legs": ("C3 on a second stream beside C2 (C3 in at most %d workgroups)"
+                     % args.c3_wg_cap if args.c3_wg_cap else
+                     "C3 on a second stream beside C2") if overlap else "C3 then C2, one stream",
         },
         "roofline": roof,
         "legs_ms": {"c2_txq_frame": round(c2_ms, 4), "c3_diamond": round(c3_ms, 4),

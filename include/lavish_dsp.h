@@ -602,6 +602,15 @@ int lavish_full_pixel_search_batch_tiled(const uint8_t *src, int src_stride,
                                          LavishDiamondResult *out,
                                          int32_t *cost_lists, void *stream);
 
+/* Process-wide cap on the workgroups of the 16x16 DIAMOND search of
+ * lavish_full_pixel_search_batch[_tiled] (rounded up to 8; 0 = no cap, one
+ * workgroup per 32 jobs).  A scheduling knob for running the search beside
+ * another stream's work (the search holds fewer CU slots and runs longer);
+ * results do not depend on it.  Default from LAVISH_C3_WGS, else 0; -1 for a
+ * negative value.  No reference counterpart (the reference's search runs on
+ * the encoder's threads). */
+int lavish_set_search_workgroup_cap(int workgroups);
+
 /* ---- sub-pixel refinement ------------------------
  * av1_find_best_sub_pixel_tree_pruned_more (av1/encoder/mcomp.c:2907-2981;
  * subpel_search_method SUBPEL_TREE_PRUNED_MORE, speed >= 4) without a cost
