@@ -196,7 +196,10 @@ def wavefront_frame(height, width, rank, world, process_rect, chunks=4, edge_row
                     if world > 1:
                         edge = torch.empty((edge_rows, cx[got + 1] - cx[got]), dtype=full.dtype,
                                            device=full.device)
-                        dist.recv(edge.view(torch.uint8), src=prv, group=p2p_group)
+                        # on RCCL the wait orders the caller's stream after the
+                        # receive and returns: the host goes on queueing chunks
+                        # (gloo, the CPU tests, waits on the host)
+                        dist.irecv(edge.view(torch.uint8), src=prv, group=p2p_group).wait()
                     else:  # the row above is this rank's own, already in the frame
                         edge = full[y0 - edge_rows:y0, cx[got]:cx[got + 1]]
                     edges.append(edge)
