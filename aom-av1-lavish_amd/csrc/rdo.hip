@@ -830,10 +830,19 @@ int rdo_frame(const uint16_t* src, const uint16_t* pred, int stride, int width, 
   int order[19], n = 0;
   for (int s = 0; s < 19; ++s)
     if ((size_mask >> s) & 1) order[n++] = s;
-  // most work first, dealt round-robin over the internal streams
+  // most work first, dealt round-robin over the internal streams.
+  // LAVISH_RDO_ORDER=1 (A/B): least work first, so the few-wave,
+  // latency-bound large sizes start beside the small sizes' kernels instead
+  // of trailing them -- measured slower (0.821-0.840 vs 0.811-0.829 ms per 4K
+  // step, profiles/r04_v13_ab_notes.txt)
+  static const int least_first = [] {
+    const char* e = getenv("LAVISH_RDO_ORDER");
+    return e != nullptr && atoi(e) == 1;
+  }();
   auto work = [&](int s) {
-    return (long)__builtin_popcount(type_masks[s]) * (width / tx_w(s)) * (height / tx_h(s)) *
-           max_eob(s);
+    const long w = (long)__builtin_popcount(type_masks[s]) * (width / tx_w(s)) *
+                   (height / tx_h(s)) * max_eob(s);
+    return least_first ? -w : w;
   };
   for (int i = 1; i < n; ++i)
     for (int j = i; j > 0 && work(order[j]) > work(order[j - 1]); --j) {
