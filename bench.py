@@ -89,6 +89,8 @@ def parse():
                     help="skip the c4 sub-object (4K 10-bit RDO step) of the default line")
     ap.add_argument("--c3-wg-cap", type=int, default=C3_WG_CAP,
                     help="workgroups of the C3 search when it runs beside C2 (0: no cap)")
+    ap.add_argument("--c2-priority", type=int, default=0,
+                    help="1: the C2 leg on a high-priority stream beside C3")
     ap.add_argument("--serial", action="store_true",
                     help="run the C3 and C2 legs back to back on one stream (default: C3 on a "
                          "second stream beside C2)")
@@ -1534,6 +1536,10 @@ def main():
     do_c2 = args.workload in ("rdo", "c2")
     do_c3 = args.workload in ("rdo", "c3", "c3sub")
     do_sub = args.workload == "c3sub"
+    if args.c2_priority and do_c2 and do_c3 and not args.serial:
+        # C2 (the step's long leg) on a high-priority stream, C3 beside it on
+        # a normal one: freed CU slots go to C2's workgroups first
+        torch.cuda.set_stream(torch.cuda.Stream(priority=-1))
     stream = torch.cuda.current_stream()
 
     # C2 input: residual plane (each rank its own frame)
