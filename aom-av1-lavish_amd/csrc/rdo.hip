@@ -1150,22 +1150,24 @@ int rdo_reconstruct_impl(uint32_t size_mask, const LavishRdoBlock* const* rec,
   }
   hipLaunchKernelGGL(sb_decide_kernel, dim3((nsb + 3) / 4), dim3(256), 0, s, a);
   LAVISH_CHECK(hipGetLastError());
-  // recon = pred, then add the chosen coded blocks' residuals size by size
+  // recon = pred, then add the chosen coded blocks' residuals: the sizes'
+  // inverse launches side by side over the fan-out streams (every SB chose
+  // one size, so they write disjoint pixels; a size no SB chose still costs a
+  // launch of ~6 us, which then overlaps the others instead of following them)
   LAVISH_CHECK(hipMemcpy2DAsync(recon, (size_t)stride * 2, pred, (size_t)stride * 2,
                                 (size_t)width * 2, height, hipMemcpyDeviceToDevice, s));
-  for (int i = 0; i < a.nsizes; ++i) {
+  hipStream_t* fs = fan_out(s);
+  int rc = 0, k = 0;
+  for (int i = 0; i < a.nsizes && rc == 0; ++i) {
     const int t = a.sizes[i];
     if ((width / tx_w(t)) * (height / tx_h(t)) == 0) continue;
     const int cap = (64 / tx_w(t)) * (64 / tx_h(t));
-    const int rc = inv_txfm_add_batch(dqcoeff[t], t, a.jobs[t], nsb * cap, recon, stride, bd, 1,
-                                      s, a.cnt[t], cap);
-    if (rc) {
-      if (shared) t_rs.release(s);
-      return rc;
-    }
+    rc = inv_txfm_add_batch(dqcoeff[t], t, a.jobs[t], nsb * cap, recon, stride, bd, 1,
+                            fs[k++ % fan_width()], a.cnt[t], cap);
   }
+  fan_in(s);
   if (shared) t_rs.release(s);
-  return 0;
+  return rc;
 }
 
 }  // namespace lavish
