@@ -1135,7 +1135,8 @@ __global__ __launch_bounds__(64 * kDkWaves, (W <= 16 && H <= 16) ? 8 : 7) void d
 // x 8.
 //
 // The dependency on finished neighbours makes this a wavefront: one wave per
-// (reference, block row) walks its row left to right.  A block's tpl mv is
+// (reference, block row) walks its row left to right, a second wave of its
+// workgroup does the walk's global stores (below).  A block's tpl mv is
 // published by one device-scope atomic store into the mv array, which the
 // call first fills with INVALID_MV; a wave waits for the above-right block by
 // polling that slot (the mv itself is the ready flag: no separate progress
