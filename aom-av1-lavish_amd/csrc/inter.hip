@@ -414,10 +414,9 @@ template <typename T, int CW>
 void launch_cw(const IpArgs& a, hipStream_t s) {
   constexpr bool kFastOk = sizeof(T) == 1 && CW == 4;
   const bool fast = kFastOk && !a.custom;
-  // rows per thread: 16 amortises the 7 extra horizontal rows better, 8 keeps
-  // more waves resident (LAVISH_INTER_RMAX=8 selects it, for measurement)
-  static const int rmax = getenv("LAVISH_INTER_RMAX") ? atoi(getenv("LAVISH_INTER_RMAX")) : 16;
-  const int R = a.h < 8 ? a.h : (fast && a.h >= 16 && rmax >= 16 ? 16 : 8);
+  // rows per thread: 16 amortises the 7 extra horizontal rows better than 8
+  // (which would keep more waves resident)
+  const int R = a.h < 8 ? a.h : (fast && a.h >= 16 ? 16 : 8);
   const int64_t threads = (int64_t)a.njobs * (a.w / CW) * (a.h / R);
   if (threads >= (1LL << 31) - 256 * 8) {
     set_error("lavish_build_inter_pred_batch: job list too large for one launch",

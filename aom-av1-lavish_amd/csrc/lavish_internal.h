@@ -69,6 +69,7 @@ int inter_pred_batch(const void* ref, int ref_stride, int ref_width, int ref_hei
 
 // fork / join over the library's per-thread internal streams
 int fan_width();
+int set_fan_width(int w);
 hipStream_t* fan_out(hipStream_t caller);
 void fan_in(hipStream_t caller);
 

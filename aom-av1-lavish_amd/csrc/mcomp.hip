@@ -1255,18 +1255,32 @@ __global__ __launch_bounds__(128) void tpl_mv_kernel(TplMvArgs a) {
   // store, ~2 us to complete) waited for that store at its next load; with
   // the stores on another wave the walk's loads wait for themselves only.
   if (threadIdx.x >= 64) {
+    // The publisher's wait covers the searching wave's own waits on the row
+    // above (each bounded by kTplMaxSpins x s_sleep 2), so it gets twice that
+    // budget.  On a timeout the box holds no valid payload (col - 2's, or
+    // nothing for col 0 / 1): the block and the rest of the row publish
+    // INVALID_MV, which neighbours skip like an unavailable mv, the failure is
+    // counted in sync[1] (TplFrame.check raises) and every block is
+    // acknowledged so the searching wave never waits on this wave again.
+    bool dead = false;
     for (int col = 0; col < a.cols; ++col) {
       TplBox& b = box_s[col & 1];
       int spins = 0;
-      while (__hip_atomic_load(&b.seq, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != col + 1) {
-        __builtin_amdgcn_s_sleep(1);
-        if (++spins >= kTplMaxSpins) {  // (bounded: the grid always drains)
+      while (!dead &&
+             __hip_atomic_load(&b.seq, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != col + 1) {
+        __builtin_amdgcn_s_sleep(2);
+        if (++spins >= 2 * kTplMaxSpins) {  // (bounded: the grid always drains)
           if (lane == 0)
             __hip_atomic_fetch_add(a.sync + 1, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          break;
+          dead = true;
+          __hip_atomic_store(&ack_s, a.cols, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
         }
       }
       const int64_t bi = (int64_t)row * a.cols + col, j = ref * nb + bi;
+      if (dead) {
+        if (lane == 0) __hip_atomic_store(mvs + bi, kInvalidMv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        continue;
+      }
       if (lane == 0) {
         __hip_atomic_store(mvs + bi, b.mv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         LavishDiamondResult best;
@@ -2238,14 +2252,6 @@ __global__ __launch_bounds__(64 * WPG, LAVISH_LJ_WAVES) void diamond_lj_kernel(
                   cost_lists, v, nvwg);
 }
 
-static int lj_wpg() {  // LAVISH_C3_WPG=1: one wave per workgroup (A/B)
-  static const int w = [] {
-    const char* e = getenv("LAVISH_C3_WPG");
-    return e != nullptr && atoi(e) == 1 ? 1 : 4;
-  }();
-  return w;
-}
-
 // the decimated entropy cost tables of mvsad_rate_dec
 __global__ __launch_bounds__(256) void mvcost_dec_kernel(const int32_t* __restrict__ mvcost0,
                                                          const int32_t* __restrict__ mvcost1,
@@ -2256,35 +2262,12 @@ __global__ __launch_bounds__(256) void mvcost_dec_kernel(const int32_t* __restri
   dec[i] = (i < kMvDecN ? mvcost0 : mvcost1)[8 * k];
 }
 
-static bool lj_dec_enabled() {  // LAVISH_C3_MVDEC=0: the caller's tables directly (A/B)
-  static const bool on = [] {
-    const char* e = getenv("LAVISH_C3_MVDEC");
-    return e == nullptr || atoi(e) != 0;
-  }();
-  return on;
-}
 thread_local StreamScratch t_mvdec;
 
 // at most this many workgroups for the 16x16 DIAMOND search (rounded to 8;
-// 0: one per 32 jobs): lavish_set_search_workgroup_cap, else LAVISH_C3_WGS
-static std::atomic<int> g_lj_cap{-1};
-static int lj_grid_cap() {
-  int cap = g_lj_cap.load(std::memory_order_relaxed);
-  if (cap < 0) {
-    const char* e = getenv("LAVISH_C3_WGS");
-    cap = e == nullptr ? 0 : (atoi(e) + 7) & ~7;
-    g_lj_cap.store(cap, std::memory_order_relaxed);
-  }
-  return cap;
-}
-
-static bool lj_enabled() {  // LAVISH_DIAMOND_LJ=0: the one-job-per-wave kernel (A/B)
-  static const bool on = [] {
-    const char* e = getenv("LAVISH_DIAMOND_LJ");
-    return e == nullptr || atoi(e) != 0;
-  }();
-  return on;
-}
+// 0: one per 32 jobs): lavish_set_search_workgroup_cap
+static std::atomic<int> g_lj_cap{0};
+static int lj_grid_cap() { return g_lj_cap.load(std::memory_order_relaxed); }
 
 template <int W, int H, bool TL>
 void launch_tl(const uint8_t* src, int ss, const uint8_t* ref, int rs, const LavishRefTiles& t,
@@ -2311,24 +2294,19 @@ void launch(const uint8_t* src, int ss, const uint8_t* ref, int rs, const Lavish
   if constexpr (W <= 16) {
     if (t != nullptr) {
       if constexpr (W == 16 && H == 16) {
-        if (method == kDiamond && lj_enabled()) {  // eight jobs per wave
+        if (method == kDiamond) {  // eight jobs per wave
           const int waves = (njobs + kLjJobs - 1) / kLjJobs;
-          const int wpg = lj_wpg();
+          constexpr int wpg = 4;
           const int nwg = (((waves + wpg - 1) / wpg) + 7) & ~7;
           const int cap = lj_grid_cap();
           const int grid = cap > 0 && cap < nwg ? cap : nwg;
           int32_t* dec = nullptr;
-          if (cost.mv_cost_type == 0 && lj_dec_enabled()) {
+          if (cost.mv_cost_type == 0) {
             dec = (int32_t*)t_mvdec.acquire(2 * kMvDecN * sizeof(int32_t), s);
             hipLaunchKernelGGL(mvcost_dec_kernel, dim3((2 * kMvDecN + 255) / 256), dim3(256), 0,
                                s, cost.mvcost[0], cost.mvcost[1], dec);
           }
-          if (wpg == 1)
-            hipLaunchKernelGGL(diamond_lj_kernel<1>, dim3(grid), dim3(64), 0, s, src, ss, ref,
-                               rs, *t, (const Job*)jobs, njobs, step_param, cost,
-                               (const int32_t*)dec, skip, out, cost_lists, nwg);
-          else
-            hipLaunchKernelGGL(diamond_lj_kernel<4>, dim3(grid), dim3(256), 0, s, src, ss, ref,
+          hipLaunchKernelGGL(diamond_lj_kernel<wpg>, dim3(grid), dim3(64 * wpg), 0, s, src, ss, ref,
                                rs, *t, (const Job*)jobs, njobs, step_param, cost,
                                (const int32_t*)dec, skip, out, cost_lists, nwg);
           if (dec) t_mvdec.release(s);

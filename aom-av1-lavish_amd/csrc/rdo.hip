@@ -830,19 +830,13 @@ int rdo_frame(const uint16_t* src, const uint16_t* pred, int stride, int width, 
   int order[19], n = 0;
   for (int s = 0; s < 19; ++s)
     if ((size_mask >> s) & 1) order[n++] = s;
-  // most work first, dealt round-robin over the internal streams.
-  // LAVISH_RDO_ORDER=1 (A/B): least work first, so the few-wave,
-  // latency-bound large sizes start beside the small sizes' kernels instead
-  // of trailing them -- measured slower (0.821-0.840 vs 0.811-0.829 ms per 4K
-  // step, profiles/r04_v13_ab_notes.txt)
-  static const int least_first = [] {
-    const char* e = getenv("LAVISH_RDO_ORDER");
-    return e != nullptr && atoi(e) == 1;
-  }();
+  // most work first, dealt round-robin over the internal streams (measured
+  // against least work first, so the few-wave, latency-bound large sizes
+  // start beside the small sizes' kernels: that was slower, 0.821-0.840 vs
+  // 0.811-0.829 ms per 4K step, profiles/r04_v13_ab_notes.txt)
   auto work = [&](int s) {
-    const long w = (long)__builtin_popcount(type_masks[s]) * (width / tx_w(s)) *
-                   (height / tx_h(s)) * max_eob(s);
-    return least_first ? -w : w;
+    return (long)__builtin_popcount(type_masks[s]) * (width / tx_w(s)) * (height / tx_h(s)) *
+           max_eob(s);
   };
   for (int i = 1; i < n; ++i)
     for (int j = i; j > 0 && work(order[j]) > work(order[j - 1]); --j) {
@@ -1261,7 +1255,8 @@ extern "C" int lavish_rdo_graph_create(const uint16_t* src, const uint16_t* pred
                                        const LavishQuantParams* qp, int rdmult,
                                        LavishRdoBlock* const* records, int32_t* const* qcoeff,
                                        int32_t* const* dqcoeff, uint16_t* recon,
-                                       uint8_t* sb_tx_size, LavishRdoGraph** out) {
+                                       uint8_t* sb_tx_size, void* stream,
+                                       LavishRdoGraph** out) {
   if (out == nullptr) return -3;
   *out = nullptr;
   size_t bytes = 0;
@@ -1274,6 +1269,14 @@ extern "C" int lavish_rdo_graph_create(const uint16_t* src, const uint16_t* pred
   LAVISH_CHECK(hipMalloc(&g->scratch, bytes > 0 ? bytes : 16));
   hipStream_t cs;
   LAVISH_CHECK(hipStreamCreateWithFlags(&cs, hipStreamNonBlocking));
+  // the warm-up below reads src / pred and writes every output buffer: order
+  // it after the caller's pending work on them (e.g. a fill of the
+  // reconstruction plane still queued on the caller's stream)
+  hipEvent_t after;
+  LAVISH_CHECK(hipEventCreateWithFlags(&after, hipEventDisableTiming));
+  LAVISH_CHECK(hipEventRecord(after, (hipStream_t)stream));
+  LAVISH_CHECK(hipStreamWaitEvent(cs, after, 0));
+  LAVISH_CHECK(hipEventDestroy(after));
   // one uncaptured run first: the library's lazily created state (internal
   // streams, device scan tables: synchronous uploads) must exist before the
   // capture, which may only record stream work

@@ -18,6 +18,8 @@
 // no MFMA: AV1 butterflies with per-stage 64-bit rounding are not a matrix
 // product.  HBM traffic is the residual once plus 8 bytes per output
 // coefficient per type, so the kernel is bounded by the output write stream.
+#include <atomic>
+
 #include "lavish_internal.h"
 #include "quant_dev.h"
 
@@ -614,15 +616,16 @@ static FrameStreams& frame_streams() {
   return t_fs;
 }
 
-// LAVISH_FAN_STREAMS=1: every size on the caller's stream (isolated
-// per-kernel timings under a profiler); default kFrameStreams
-int fan_width() {
-  static const int w = [] {
-    const char* e = getenv("LAVISH_FAN_STREAMS");
-    const int v = e ? atoi(e) : kFrameStreams;
-    return v < 1 ? 1 : (v > kFrameStreams ? kFrameStreams : v);
-  }();
-  return w;
+// streams the per-size work of lavish_rdo_frame / lavish_rdo_reconstruct is
+// dealt over: kFrameStreams (the caller + internal streams), or 1 (every
+// size on the caller's stream: isolated per-kernel timings under a
+// profiler), set by lavish_set_fan_width
+static std::atomic<int> g_fan_width{kFrameStreams};
+int fan_width() { return g_fan_width.load(std::memory_order_relaxed); }
+int set_fan_width(int w) {
+  if (w < 1 || w > kFrameStreams) return -1;
+  g_fan_width.store(w, std::memory_order_relaxed);
+  return 0;
 }
 
 // fork: the internal streams wait for everything queued on `caller`; slot 0
@@ -663,28 +666,14 @@ int txq_frame(const int16_t* residual, int stride, int width, int height, uint32
       order[j - 1] = t;
     }
   int rc = 0;
-  static const int mode = [] {
-    const char* e = getenv("LAVISH_TXQ_FRAME_MODE");  // A/B experiments only
-    return e ? atoi(e) : 1;
-  }();
-  if (mode == 0) {  // per-size kernels over the caller + 2 internal streams
-    hipStream_t* fs = fan_out(caller);
-    for (int i = 0; i < n && rc == 0; ++i) {
-      const int s = order[i];
-      rc = txq_plane(residual, stride, width, height, s, type_masks[s], bd, quant_kind, qp,
-                     qcoeff[s], dqcoeff[s], eob[s], nullptr, fs[i % kFrameStreams]);
-    }
-    fan_in(caller);
-    return rc;
-  }
   // one launch per class, on the caller's stream: the 32-point class (few,
-  // register-heavy workgroups) first, then the <= 16-point class.  mode 2
-  // (LAVISH_TXQ_FRAME_MODE=2, A/B): the 32-point class on an internal
-  // stream beside the other (fork / join through fan_out / fan_in) --
-  // measured slower (C2 0.565 -> 0.577 ms, profiles/r04_v5_c2_streams_ab.txt)
-  hipStream_t* fs = mode == 2 ? fan_out(caller) : nullptr;
+  // register-heavy workgroups) first, then the <= 16-point class.  (Measured
+  // and dropped: the round-2 per-size kernels over the caller + 2 internal
+  // streams, ~50 us of fork / join per frame; the 32-point class on an
+  // internal stream beside the other, C2 0.565 -> 0.577 ms,
+  // profiles/r04_v5_c2_streams_ab.txt.)
   for (int cls = 1; cls >= 0; --cls) {
-    const hipStream_t cs = (mode == 2 && cls == 1) ? fs[1] : caller;
+    const hipStream_t cs = caller;
     TxqMulti m{};
     int g = 0;
     for (int i = 0; i < n; ++i) {
@@ -714,25 +703,23 @@ int txq_frame(const int16_t* residual, int stride, int width, int height, uint32
     if (rc) break;
     if (m.d.n == 0) continue;
     m.d.wg0[m.d.n] = g;
-    // LAVISH_C2_LDS_PAD=n (A/B only): n more bytes of LDS per workgroup, so
-    // fewer C2 workgroups fit a CU and a concurrent leg's waves find room
-    static const int pad = [] {
-      const char* e = getenv("LAVISH_C2_LDS_PAD");
-      return e ? atoi(e) : 0;
-    }();
+    // (Measured and dropped: an LDS pad so fewer C2 workgroups fit a CU
+    // beside a concurrent leg -- C2 alone 0.51 -> 0.55 / 1.31 ms at 3 / 2
+    // workgroups per CU, profiles/r04_v11_ab_notes.txt.)
     if (cls == 0)
-      hipLaunchKernelGGL(txq_multi_kernel<0>, dim3(g), dim3(256), pad, cs, m.d, m.a[0], m.a[1],
+      hipLaunchKernelGGL(txq_multi_kernel<0>, dim3(g), dim3(256), 0, cs, m.d, m.a[0], m.a[1],
                          m.a[2], m.a[3], m.a[4], m.a[5], m.a[6], m.a[7], m.a[8]);
     else
-      hipLaunchKernelGGL(txq_multi_kernel<1>, dim3(g), dim3(256), pad, cs, m.d, m.a[0], m.a[1],
+      hipLaunchKernelGGL(txq_multi_kernel<1>, dim3(g), dim3(256), 0, cs, m.d, m.a[0], m.a[1],
                          m.a[2], m.a[3], m.a[4], m.a[5], m.a[6], m.a[7], m.a[8]);
     LAVISH_CHECK(hipGetLastError());
   }
-  if (mode == 2) fan_in(caller);
   return rc;
 }
 
 }  // namespace lavish
+
+extern "C" int lavish_set_fan_width(int streams) { return lavish::set_fan_width(streams); }
 
 extern "C" int lavish_txq_frame(const int16_t* residual, int stride, int width, int height,
                                 uint32_t size_mask, const uint32_t* type_masks, int bit_depth,

@@ -200,6 +200,19 @@ def status():
     return _lib.lavish_hip_status(), _lib.lavish_hip_status_string().decode()
 
 
+_lib.lavish_set_fan_width.argtypes = [ctypes.c_int]
+_lib.lavish_set_fan_width.restype = ctypes.c_int
+
+
+def set_fan_width(streams):
+    """lavish_set_fan_width: the streams rdo_frame / rdo_reconstruct deal
+    their per-size kernels over (3, the default, or 1: all on the caller's
+    stream -- isolated per-kernel timings under a profiler)."""
+    rc = _lib.lavish_set_fan_width(int(streams))
+    if rc != 0:
+        raise ValueError("lavish_set_fan_width(%r): %d" % (streams, rc))
+
+
 def _p(a):
     return a.ctypes.data_as(ctypes.c_void_p)
 
@@ -565,7 +578,7 @@ class RdoFrame:
 if hasattr(_lib, "lavish_rdo_graph_create"):  # (older A/B builds lack it)
     _lib.lavish_rdo_graph_create.argtypes = [_vp, _vp, _i32, _i32, _i32, ctypes.c_uint32, _vp,
                                              _i32, ctypes.POINTER(QuantParams), _i32, _vp, _vp,
-                                             _vp, _vp, _vp, ctypes.POINTER(ctypes.c_void_p)]
+                                             _vp, _vp, _vp, _vp, ctypes.POINTER(ctypes.c_void_p)]
     _lib.lavish_rdo_graph_create.restype = _i32
     _lib.lavish_rdo_graph_launch.argtypes = [_vp, _vp]
     _lib.lavish_rdo_graph_launch.restype = _i32
@@ -578,7 +591,7 @@ class RdoGraph:
     RdoFrame on fixed src / pred planes, captured once into a HIP graph;
     launch() replays it with one host call."""
 
-    def __init__(self, src, pred, frame, qp, rdmult, bit_depth=10):
+    def __init__(self, src, pred, frame, qp, rdmult, bit_depth=10, stream=None):
         assert src.stride(1) == 1 and src.shape == pred.shape
         H, W = src.shape
         self._keep = (src, pred, frame, qp)
@@ -587,7 +600,7 @@ class RdoGraph:
             ctypes.c_void_p(src.data_ptr()), ctypes.c_void_p(pred.data_ptr()), src.stride(0), W,
             H, frame.size_mask, frame.tm, bit_depth, ctypes.byref(qp), rdmult, frame.rec, frame.q,
             frame.dq, ctypes.c_void_p(frame.recon.data_ptr()),
-            ctypes.c_void_p(frame.sb_tx_size.data_ptr()), ctypes.byref(g))
+            ctypes.c_void_p(frame.sb_tx_size.data_ptr()), _stream_ptr(stream), ctypes.byref(g))
         if rc != 0:
             raise ValueError("lavish_rdo_graph_create failed (rc=%d)" % rc)
         self._g = g

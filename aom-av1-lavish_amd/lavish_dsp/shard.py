@@ -168,7 +168,9 @@ def wavefront_frame(height, width, rank, world, process_rect, chunks=4, edge_row
     events.  streams (world 1, device work): the rows are dealt round-robin
     over these streams and each chunk waits, through events, only for the
     row above's chunk it depends on -- the wavefront's diagonal parallelism
-    on one GPU (the reference's row threads, ethread.c:113-160)."""
+    on one GPU (the reference's row threads, ethread.c:113-160); the rows
+    overlap on the device only when process_rect replays graphs (see
+    _wavefront_streams)."""
     import torch
     import torch.distributed as dist
     R, C = sb_rows(height), sb_cols(width)
@@ -236,7 +238,11 @@ def _wavefront_streams(height, width, process_rect, chunks, cx, edge_rows, full,
     streams[r % len(streams)]; chunk c of row r waits for the event of row
     r - 1's chunk min(c + 1, chunks - 1) (chunks of a row complete in order
     on its stream), reads its edge rows from the frame, and records its own
-    event; the caller's stream then waits for every row."""
+    event; the caller's stream then waits for every row.  Device concurrency
+    between rows needs process_rect to replay captured graphs
+    (c4_rect_processor(graphs=True)): the direct calls share the library's
+    per-thread fan-out streams and reconstruction scratch, which serialise
+    the rows again (results are the same either way)."""
     import torch
     R = sb_rows(height)
     caller = torch.cuda.current_stream()

@@ -241,6 +241,7 @@ class TplFrame:
         it); check=False leaves the frame asynchronous, and the caller must
         call check() before using the results."""
         bs = TPL_BSIZE
+        self._stream = stream
         if self.neighbour_starts:
             tpl_motion_search(self.src, self.refs, self.jobs, self.cols, self.rows, self.nrefs,
                               self.cost, self.search_method, self.step_param, self.skip_sad,
@@ -264,7 +265,15 @@ class TplFrame:
         return self.out
 
     def check(self):
-        """Raise if the last wavefront's waits timed out (synchronises)."""
+        """Raise if the last wavefront's waits timed out.  Synchronises the
+        stream step() ran on first: the failure count is written there, and a
+        read ordered on another stream could see it before the kernel ends."""
+        import torch
+        st = getattr(self, "_stream", None)
+        if st is not None:
+            st.synchronize()
+        else:
+            torch.cuda.current_stream().synchronize()
         if self.neighbour_starts and tpl_motion_failures(self.mv_out):
             raise RuntimeError("tpl motion wavefront: %d wait(s) timed out; the frame's start "
                                "mvs are invalid" % tpl_motion_failures(self.mv_out))

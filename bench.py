@@ -63,7 +63,10 @@ def metric_name(args):
 
 def parse():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=1,
+                    help="ranks; without a launcher (no WORLD_SIZE) bench.py starts them itself")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="with --gpus N > 1 and no launcher: print the ranks' plan, start nothing")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--workload", choices=("rdo", "c2", "c3", "c3sub", "c4", "c4px", "c5", "inter",
@@ -85,6 +88,10 @@ def parse():
     ap.add_argument("--c5-form", choices=("band", "wavefront"), default="band",
                     help="C5 sharding: balanced band + tail segments with overlapped "
                          "all-gathers, or the row-wavefront with p2p edges (lavish_dsp/shard.py)")
+    ap.add_argument("--c5-emulate", default="",
+                    help="c5 at world 1: also time every rank's partition() rectangles for "
+                         "these world sizes (comma list, e.g. 2,4,8) one rank at a time on this "
+                         "GPU -- the compute-only per-rank time at G ranks")
     ap.add_argument("--no-c4", action="store_true",
                     help="skip the c4 sub-object (4K 10-bit RDO step) of the default line")
     ap.add_argument("--c3-wg-cap", type=int, default=C3_WG_CAP,
@@ -95,6 +102,9 @@ def parse():
                     help="run the C3 and C2 legs back to back on one stream (default: C3 on a "
                          "second stream beside C2)")
     ap.add_argument("--overlap", action="store_true", help=argparse.SUPPRESS)  # the default
+    ap.add_argument("--fan-width", type=int, default=0,
+                    help="1: C4's per-size kernels all on the caller's stream (isolated "
+                         "per-kernel timings under a profiler; lavish_set_fan_width)")
     ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
     return ap.parse_args()
 
@@ -375,6 +385,144 @@ def c4_leg(L, steps, warmup, rdmult, qindex, W=3840, H=2160):
             "hbm_frac": round(nbytes / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
 
 
+def c5_leg(L, steps, warmup, rdmult, qindex, world, rank, W=3840, H=2160, graphs=True,
+           c4_ms=None):
+    """C5 (BASELINE configs[4]) inside the default line at N > 1: the C4 step
+    of ONE 4K 10-bit frame sharded over the ranks in the band form
+    (lavish_dsp/shard.py: floor(R / G) SB rows per rank + a column segment of
+    the leftover rows, each part's reconstruction all-gathered over RCCL as
+    soon as it is computed), timed barrier to barrier, max over ranks; plus
+    each rank's compute alone (its band + tail rectangles, no exchange) and
+    the all-gathers alone (the same tensors, no compute), so the line shows
+    where the time goes."""
+    import torch
+    import torch.distributed as dist
+    import lavish_dsp.shard as shard
+    import lavish_dsp.synth as synth
+    src_np = synth.frame(W, H, 10, 1234).astype(np.uint16)
+    pred_np = synth.shifted(synth.frame(W, H, 10, 1235), 3, -2).astype(np.uint16)
+    src = torch.from_numpy(src_np.view(np.int16)).cuda()
+    pred = torch.from_numpy(pred_np.view(np.int16)).cuda()
+    qp = L.build_quant_params(10, qindex, L.QUANT_FP)
+    frames = {}
+    frame_out = torch.empty_like(src)
+    proc = shard.c4_rect_processor(src, pred, qp, rdmult, 10, frames, out=frame_out,
+                                   graphs=graphs)
+    parts = shard.partition(H, W, world)
+    mine = [r for r in parts[rank] if r is not None]
+
+    def timed(fn, n):
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(n):
+            fn()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        el = time.perf_counter() - t0
+        mx = torch.tensor([el], dtype=torch.float64, device="cuda")
+        if world > 1:
+            dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+        return el / n * 1e3, float(mx.item()) / n * 1e3
+
+    def frame_step():
+        shard.sharded_frame(H, W, rank, world, proc)
+
+    def compute_only():
+        for r in mine:
+            proc(*r)
+
+    # the exchange alone: each phase's all-gather of equal zero-padded parts
+    gathers = []
+    for phase in range(2):
+        rects = [p[phase] for p in parts]
+        if all(r is None for r in rects):
+            continue
+        hmax = max(r[1] - r[0] for r in rects if r is not None)
+        wmax = max(r[3] - r[2] for r in rects if r is not None)
+        snd = torch.zeros((hmax, wmax), dtype=torch.int16, device="cuda")
+        rcv = torch.empty((world * hmax, wmax), dtype=torch.int16, device="cuda")
+        gathers.append((snd, rcv))
+    gather_bytes = sum(r.numel() * 2 for _, r in gathers)
+
+    def gather_only():
+        for snd, rcv in gathers:
+            if world > 1:
+                dist.all_gather_into_tensor(rcv.view(torch.uint8), snd.view(torch.uint8))
+            else:
+                rcv.copy_(snd.repeat(world, 1))
+
+    for _ in range(warmup):
+        frame_step()
+        compute_only()
+        gather_only()
+    mine_ms, step_ms = timed(frame_step, steps)
+    comp_ms, comp_max = timed(compute_only, steps)
+    gath_ms, gath_max = timed(gather_only, steps)
+    per_rank = [None] * world
+    if world > 1:
+        t = torch.zeros(world, dtype=torch.float64, device="cuda")
+        t[rank] = comp_ms
+        dist.all_reduce(t)
+        per_rank = [round(float(x), 4) for x in t.cpu()]
+    else:
+        per_rank = [round(comp_ms, 4)]
+    sb = sb64_count(W, H)
+    out = {"workload": "c5: one %dx%d 10-bit frame per step, the C4 step sharded over %d ranks "
+                       "(band form: floor(R/G) SB rows + a column segment of the leftover rows "
+                       "per rank; each part's reconstruction all-gathered over RCCL)"
+                       % (W, H, world),
+           "n_ranks": world, "ms_per_frame": round(step_ms, 4),
+           "SB64_per_s": round(sb / (step_ms * 1e-3), 1),
+           "rank_rects": [list(p) for p in parts],
+           "compute_ms_per_rank": per_rank, "compute_ms_max": round(comp_max, 4),
+           "allgather_bytes": gather_bytes, "allgather_ms": round(gath_max, 4),
+           "allgather_GBps": round(gather_bytes / (gath_max * 1e-3) / 1e9, 1) if gath_max else None,
+           "graphs": graphs, "steps": steps}
+    if c4_ms:
+        # whole-frame C4 on one GPU (the c4 leg of the same line) over N x this
+        out["strong_scaling_efficiency_vs_c4_leg"] = round(c4_ms / (world * step_ms), 4)
+    return out
+
+
+def c5_emulate(H, W, proc, worlds, steps, warmup, frame_ms):
+    """On one GPU, rank g's share of the band form for each world size G:
+    its partition() rectangles (band, then tail segment) run back to back
+    with nothing else on the device, timed with HIP events -- the
+    compute-only time of that rank at G GPUs (no exchange, no contention
+    from other ranks: each rank owns its GPU).  Reports every rank's time,
+    the slowest, and the compute-only speed-up frame_ms / slowest."""
+    import torch
+    import lavish_dsp.shard as shard
+    stream = torch.cuda.current_stream()
+    out = {}
+    for G in worlds:
+        parts = shard.partition(H, W, G)
+        per = []
+        for g in range(G):
+            rects = [r for r in parts[g] if r is not None]
+            for _ in range(warmup):
+                for r in rects:
+                    proc(*r)
+            torch.cuda.synchronize()
+            ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                  for _ in range(steps)]
+            for a, b in ev:
+                a.record(stream)
+                for r in rects:
+                    proc(*r)
+                b.record(stream)
+            torch.cuda.synchronize()
+            per.append(sum(a.elapsed_time(b) for a, b in ev) / steps)
+        slow = max(per)
+        out[str(G)] = {"rank_ms": [round(x, 4) for x in per], "max_rank_ms": round(slow, 4),
+                       "projected_speedup_compute_only": round(frame_ms / slow, 3),
+                       "rects": [list(p) for p in parts]}
+    return out
+
+
 def main_c4(args):
     """C4 (1 GPU) / C5 (SB rows sharded over the ranks, reconstructed rows
     all-gathered over RCCL) on a 4K 10-bit frame."""
@@ -502,6 +650,9 @@ def main_c4(args):
                                 for s, v in coded.items()}
         line["sb_tx_size"] = {"%dx%d" % (L.TX_W[s], L.TX_H[s]): int(n) for s, n in zip(
             *np.unique(fr.sb_tx_size.cpu().numpy(), return_counts=True)) if s < 19}
+    if args.workload == "c5" and world == 1 and args.c5_emulate:
+        line["c5_emulation"] = c5_emulate(H, W, proc, [int(g) for g in args.c5_emulate.split(",")],
+                                          args.steps, args.warmup, step_ms)
     if args.workload == "c4" and world == 1:
         # the bound that applies: int32 VALU
         rv = c4_roofline(step_ms, W, H, fr.type_masks, coded, c4_bytes)
@@ -1503,8 +1654,172 @@ def main_rate(args):
     print(json.dumps(line), flush=True)
 
 
+class RdoStep:
+    """The default workload's step (C3 beside C2 on one 1080p frame): the
+    device inputs, outputs and launches main() times, kept in one place so
+    tests/test_gpu_bench_step.py runs exactly the timed configuration.
+
+    workload: "rdo" (C2 + C3), "c2", "c3" or "c3sub" (C3 + the chained
+    pruned_more sub-pel refinement).  serial: the legs back to back on the
+    caller's stream; otherwise C3 runs on a side stream beside C2 in at most
+    `c3_wg_cap` workgroups (0: uncapped; alone, C3 always runs uncapped)."""
+
+    def __init__(self, workload="rdo", width=1920, height=1080, refs=7, border=160, qindex=128,
+                 rdmult=2000, seed=1234, serial=False, c3_wg_cap=C3_WG_CAP):
+        import torch
+        import lavish_dsp as L
+        import lavish_dsp.motion as M
+        import lavish_dsp.synth as synth
+        self.L, self.M = L, M
+        W, H = width, height
+        self.do_c2 = workload in ("rdo", "c2")
+        self.do_c3 = workload in ("rdo", "c3", "c3sub")
+        self.do_sub = workload == "c3sub"
+        self.overlap = self.do_c2 and self.do_c3 and not serial
+        self.c3_wg_cap = c3_wg_cap
+        self.stream = torch.cuda.current_stream()
+        # C2 input: residual plane (each rank its own frame)
+        self.res_np = synth.residual_plane(W, H, 8, seed=seed)
+        self.res = torch.from_numpy(self.res_np).cuda()
+        self.sizes = [s for s in range(19) if L.TX_W[s] <= 32 and L.TX_H[s] <= 32]
+        self.qp = L.build_quant_params(8, qindex, L.QUANT_FP)
+        self.frame = L.FrameOutputs(self.res, self.sizes)
+        # C3 input: padded current frame + references, jobs for every 16x16
+        # block x ref
+        self.src_np, self.refs_np = synth.motion_planes(W, H, refs, border, seed=seed)
+        st = self.src_np.shape[1]
+        self.ref_stride = st
+        self.jobs_np = M.frame_jobs(W, H, st, border, self.src_np.size, C3_BLOCK, C3_BLOCK, refs)
+        self.tsrc = torch.from_numpy(self.src_np).cuda()
+        self.trefs = torch.from_numpy(self.refs_np).cuda()
+        self.tjobs = M.to_device(self.jobs_np)
+        n = len(self.jobs_np)
+        self.c3_out = torch.empty(n * M.RESULT_DTYPE.itemsize, dtype=torch.uint8, device="cuda")
+        self.c3_cl = torch.empty((n, 5), dtype=torch.int32, device="cuda")
+        self.allow_hp = qindex < 128
+        self.mv_tables = M.default_mv_cost_tables(self.allow_hp)
+        self.mv_costs = M.MvCosts(*self.mv_tables)
+        self.sad_per_bit, self.error_per_bit = M.sad_per_bit(qindex), M.error_per_bit(rdmult)
+        self.c3_cost = self.mv_costs.cost_params(self.sad_per_bit, self.error_per_bit, C3_COST)
+        if self.do_sub:
+            self.sub_jobs = M.to_device(M.subpel_jobs(W, H, border, C3_BLOCK, C3_BLOCK,
+                                                      self.jobs_np,
+                                                      np.zeros(n, M.RESULT_DTYPE)))
+            self.sub_out = torch.empty(n * M.SUBPEL_RESULT_DTYPE.itemsize, dtype=torch.uint8,
+                                       device="cuda")
+        # the searches' candidate-row copy of the references (LavishRefTiles),
+        # rebuilt inside every step: the frame's references are new per frame
+        self.c3_tiles = M.RefTiles(self.trefs, st)
+        self.side_stream = torch.cuda.Stream()
+        self.fork = torch.cuda.Event()
+        self.join = torch.cuda.Event()
+        torch.cuda.synchronize()
+
+    def c3(self, on):
+        M = self.M
+        self.c3_tiles.build(stream=on)
+        M.full_pixel_search_batch(self.tsrc, self.trefs, C3_BLOCK, C3_BLOCK, self.tjobs,
+                                  self.c3_cost, "diamond", 0, C3_SKIP, C3_CL, out=self.c3_out,
+                                  cost_lists=self.c3_cl, stream=on, tiles=self.c3_tiles)
+        if self.do_sub:  # chained on the device: starts + cost lists = the full-pel results
+            M.find_best_sub_pixel_tree_batch(self.tsrc, self.trefs, C3_BLOCK, C3_BLOCK,
+                                             self.sub_jobs, self.c3_cost, "pruned_more",
+                                             SUB_FORCED_STOP, self.allow_hp, SUB_ITERS,
+                                             fullpel=self.c3_out, cost_lists=self.c3_cl,
+                                             out=self.sub_out, stream=on)
+
+    def step(self, ev=None, ovl=None):
+        """One frame.  ev = (start, c3 start, c3 end, c2 start, c2 end, end),
+        each leg's pair recorded on the stream that leg runs on; ovl: run C3 on
+        the side stream beside C2 (default: the run's mode)."""
+        ovl = self.overlap if ovl is None else ovl
+        stream = self.stream
+        side = self.side_stream if ovl else stream
+        if ev is not None:
+            ev[0].record(stream)
+        if ovl:  # the legs are independent: C3 (TA / latency bound) beside C2 (HBM writes)
+            self.fork.record(stream)
+            side.wait_event(self.fork)
+        if self.do_c3:
+            if ev is not None:
+                ev[1].record(side)
+            # beside C2 the search runs in fewer workgroups (it holds fewer CU
+            # slots and C2 stretches less: DESIGN.md section 5); alone, uncapped
+            self.M.set_search_workgroup_cap(self.c3_wg_cap if ovl else 0)
+            self.c3(side)
+            if ev is not None:
+                ev[2].record(side)
+        if self.do_c2:
+            if ev is not None:
+                ev[3].record(stream)
+            self.L.txq_frame(self.res, self.frame, self.qp, stream=stream)
+            if ev is not None:
+                ev[4].record(stream)
+        if ovl:
+            self.join.record(side)
+            stream.wait_event(self.join)
+        if ev is not None:
+            ev[5].record(stream)
+
+
+def free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as sk:
+        sk.bind(("127.0.0.1", 0))
+        return sk.getsockname()[1]
+
+
+def child_envs(n, port):
+    """The environment of each of the n ranks `--gpus n` starts itself when no
+    launcher set WORLD_SIZE: one process per GPU, torch.distributed's env://
+    rendezvous on 127.0.0.1."""
+    envs = []
+    for r in range(n):
+        e = dict(os.environ)
+        e.update({"RANK": str(r), "LOCAL_RANK": str(r), "WORLD_SIZE": str(n),
+                  "LOCAL_WORLD_SIZE": str(n), "MASTER_ADDR": "127.0.0.1",
+                  "MASTER_PORT": str(port)})
+        envs.append(e)
+    return envs
+
+
+def spawn_ranks(args, argv):
+    """`bench.py --gpus N` without a launcher: start N fresh child processes
+    (before this process touches the GPU; never an exec), each one rank with
+    RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* set, wait for all of them, print
+    rank 0's JSON line and return non-zero if any rank failed.  --dry-run
+    prints the plan (commands and rank environments) instead of starting."""
+    import subprocess
+    n = args.gpus
+    envs = child_envs(n, free_port())
+    cmd = [sys.executable, os.path.abspath(__file__)] + [a for a in argv if a != "--dry-run"]
+    if args.dry_run:
+        keys = ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "MASTER_ADDR",
+                "MASTER_PORT")
+        print(json.dumps({"spawn": n, "cmd": cmd,
+                          "ranks": [{k: e[k] for k in keys} for e in envs]}), flush=True)
+        return 0
+    procs = [subprocess.Popen(cmd, env=e, stdout=subprocess.PIPE if r == 0 else None)
+             for r, e in enumerate(envs)]
+    out0 = procs[0].communicate()[0].decode(errors="replace")
+    rcs = [procs[0].returncode] + [p.wait() for p in procs[1:]]
+    for ln in out0.splitlines():
+        print(ln, flush=True)
+    bad = [(r, rc) for r, rc in enumerate(rcs) if rc != 0]
+    if bad:
+        print("bench.py --gpus %d: ranks failed (rank, exit status): %s" % (n, bad),
+              file=sys.stderr, flush=True)
+        return 1
+    return 0
+
+
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        return spawn_ranks(args, sys.argv[1:])
+    if args.fan_width:
+        import lavish_dsp
+        lavish_dsp.set_fan_width(args.fan_width)
     if args.workload in ("c4", "c4px", "c5"):
         return main_c4(args)
     if args.workload == "inter":
@@ -1523,7 +1838,6 @@ def main():
     import torch.distributed as dist
     import lavish_dsp as L
     import lavish_dsp.motion as M
-    import lavish_dsp.synth as synth
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -1533,92 +1847,15 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
 
     W, H = args.width, args.height
-    do_c2 = args.workload in ("rdo", "c2")
-    do_c3 = args.workload in ("rdo", "c3", "c3sub")
-    do_sub = args.workload == "c3sub"
-    if args.c2_priority and do_c2 and do_c3 and not args.serial:
+    if args.c2_priority and args.workload == "rdo" and not args.serial:
         # C2 (the step's long leg) on a high-priority stream, C3 beside it on
         # a normal one: freed CU slots go to C2's workgroups first
         torch.cuda.set_stream(torch.cuda.Stream(priority=-1))
-    stream = torch.cuda.current_stream()
-
-    # C2 input: residual plane (each rank its own frame)
-    res = torch.from_numpy(synth.residual_plane(W, H, 8, seed=1234 + rank)).cuda()
-    sizes = [s for s in range(19) if L.TX_W[s] <= 32 and L.TX_H[s] <= 32]
-    qp = L.build_quant_params(8, args.qindex, L.QUANT_FP)
-    frame = L.FrameOutputs(res, sizes)
-    # C3 input: padded current frame + references, jobs for every 16x16 block x ref
-    src_np, refs_np = synth.motion_planes(W, H, args.refs, args.border, seed=1234 + rank)
-    st = src_np.shape[1]
-    jobs_np = M.frame_jobs(W, H, st, args.border, src_np.size, C3_BLOCK, C3_BLOCK, args.refs)
-    tsrc, trefs = torch.from_numpy(src_np).cuda(), torch.from_numpy(refs_np).cuda()
-    tjobs = M.to_device(jobs_np)
-    c3_out = torch.empty(len(jobs_np) * M.RESULT_DTYPE.itemsize, dtype=torch.uint8,
-                         device="cuda")
-    c3_cl = torch.empty((len(jobs_np), 5), dtype=torch.int32, device="cuda")
-    allow_hp = args.qindex < 128
-    mv_costs = M.MvCosts(*M.default_mv_cost_tables(allow_hp))
-    c3_cost = mv_costs.cost_params(M.sad_per_bit(args.qindex), M.error_per_bit(args.rdmult),
-                                   C3_COST)
-    torch.cuda.synchronize()
-
-    if do_sub:
-        sub_jobs = M.to_device(M.subpel_jobs(W, H, args.border, C3_BLOCK, C3_BLOCK, jobs_np,
-                                             np.zeros(len(jobs_np), M.RESULT_DTYPE)))
-        sub_out = torch.empty(len(jobs_np) * M.SUBPEL_RESULT_DTYPE.itemsize, dtype=torch.uint8,
-                              device="cuda")
-
-    # the searches' candidate-row copy of the references (LavishRefTiles),
-    # rebuilt inside every step: the frame's references are new per frame
-    c3_tiles = M.RefTiles(trefs, st)
-
-    def c3(on):
-        c3_tiles.build(stream=on)
-        M.full_pixel_search_batch(tsrc, trefs, C3_BLOCK, C3_BLOCK, tjobs, c3_cost, "diamond", 0,
-                                  C3_SKIP, C3_CL, out=c3_out, cost_lists=c3_cl, stream=on,
-                                  tiles=c3_tiles)
-        if do_sub:  # chained on the device: starts + cost lists = the full-pel results
-            M.find_best_sub_pixel_tree_batch(tsrc, trefs, C3_BLOCK, C3_BLOCK, sub_jobs, c3_cost,
-                                             "pruned_more", SUB_FORCED_STOP, allow_hp, SUB_ITERS,
-                                             fullpel=c3_out, cost_lists=c3_cl, out=sub_out,
-                                             stream=on)
-
-    overlap = do_c2 and do_c3 and not args.serial
-    side_stream = torch.cuda.Stream()
-    fork = torch.cuda.Event()
-    join = torch.cuda.Event()
-
-    def step(ev=None, ovl=None):
-        """One frame.  ev = (start, c3 start, c3 end, c2 start, c2 end, end),
-        each leg's pair recorded on the stream that leg runs on; ovl: run C3 on
-        the side stream beside C2 (default: the run's mode)."""
-        ovl = overlap if ovl is None else ovl
-        side = side_stream if ovl else stream
-        if ev is not None:
-            ev[0].record(stream)
-        if ovl:  # the legs are independent: C3 (TA / latency bound) beside C2 (HBM writes)
-            fork.record(stream)
-            side.wait_event(fork)
-        if do_c3:
-            if ev is not None:
-                ev[1].record(side)
-            # beside C2 the search runs in fewer workgroups (it holds fewer CU
-            # slots and C2 stretches less: DESIGN.md section 5); alone, uncapped
-            M.set_search_workgroup_cap(args.c3_wg_cap if ovl else 0)
-            c3(side)
-            if ev is not None:
-                ev[2].record(side)
-        if do_c2:
-            if ev is not None:
-                ev[3].record(stream)
-            L.txq_frame(res, frame, qp, stream=stream)
-            if ev is not None:
-                ev[4].record(stream)
-        if ovl:
-            join.record(side)
-            stream.wait_event(join)
-        if ev is not None:
-            ev[5].record(stream)
+    R = RdoStep(args.workload, W, H, args.refs, args.border, args.qindex, args.rdmult,
+                seed=1234 + rank, serial=args.serial, c3_wg_cap=args.c3_wg_cap)
+    do_c2, do_c3, do_sub, overlap = R.do_c2, R.do_c3, R.do_sub, R.overlap
+    stream, sizes, jobs_np, c3_cost = R.stream, R.sizes, R.jobs_np, R.c3_cost
+    step = R.step
 
     for _ in range(args.warmup):
         step()
@@ -1647,6 +1884,9 @@ def main():
     step_ms = sum(ev[k][0].elapsed_time(ev[k][5]) for k in range(K)) / K
     c3_ms = sum(ev[k][1].elapsed_time(ev[k][2]) for k in range(K)) / K if do_c3 else 0.0
     c2_ms = sum(ev[k][3].elapsed_time(ev[k][4]) for k in range(K)) / K if do_c2 else 0.0
+    # the C3 results the timed region produced (its last step): the serial
+    # pass below overwrites the output buffer
+    c3_res = M.results_numpy(R.c3_out) if do_c3 else None
     legs_overlapped = None
     if overlap:
         # the legs share the GPU in the timed region, which stretches each; the
@@ -1662,10 +1902,9 @@ def main():
         c3_ms = sum(evs[k][1].elapsed_time(evs[k][2]) for k in range(KS)) / KS
         c2_ms = sum(evs[k][3].elapsed_time(evs[k][4]) for k in range(KS)) / KS
     c2_bytes = sum(algorithmic_bytes(L, s, W, H) for s in sizes)
-    c3_res = M.results_numpy(c3_out) if do_c3 else None
     # + the tiled copy of the references: read once, written at 2x
     c3_bytes = c3_algorithmic_bytes(c3_res, len(jobs_np), C3_BLOCK, C3_BLOCK, C3_SKIP, C3_CL) \
-        + trefs.numel() + c3_tiles.data.numel() if do_c3 else 0
+        + R.trefs.numel() + R.c3_tiles.data.numel() if do_c3 else 0
 
     traffic = None
     if os.path.exists(args.pmc_json):
@@ -1752,6 +1991,12 @@ def main():
             a4.workload = "c4"
             a4.cpu_seconds = max(3.0, args.cpu_seconds / 2)
             line["c4"]["cpu_baseline"] = cpu_baseline_c4(a4)
+    if args.workload == "rdo" and world > 1 and not args.no_c4:
+        # the SB-row shard of north_star over RCCL (BASELINE configs[4]): at
+        # N > 1 the driver's scaling run measures it from this object
+        line["c5"] = c5_leg(L, max(5, args.steps // 2), max(2, args.warmup), args.rdmult,
+                            args.qindex, world, rank,
+                            c4_ms=line.get("c4", {}).get("ms_per_frame"))
     if rank == 0 and world == 1 and not args.no_cpu:
         line["cpu_baseline"] = cpu_baseline(args)
     if rank == 0:
@@ -1761,4 +2006,4 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main() or 0)

@@ -116,6 +116,13 @@ int lavish_txq_plane(const int16_t *residual, int stride, int width,
                      int32_t *dqcoeff, uint16_t *eob, int32_t *coeff,
                      void *stream);
 
+/* Streams the per-size kernels of lavish_rdo_frame / lavish_rdo_reconstruct
+ * are dealt over: 3 (default: the caller's stream + 2 internal streams,
+ * forked and joined by events) or 1 (every size on the caller's stream, for
+ * isolated per-kernel timings under a profiler).  Results are identical.
+ * Returns -1 for other values.  No reference counterpart. */
+int lavish_set_fan_width(int streams);
+
 /* Frame batch: lavish_txq_plane for every TX size whose bit is set in
  * size_mask (bit = TX_SIZE), with type_masks[tx_size] and per-size output
  * pointers qcoeff[tx_size] / dqcoeff[tx_size] / eob[tx_size] (arrays of 19
@@ -467,8 +474,10 @@ int lavish_rdo_reconstruct(uint32_t size_mask,
  * lavish_rdo_graph_launch replays with one launch on any stream (device
  * pointers and parameters are the capture's; replays of one graph must not
  * overlap).  No reference counterpart: a launch-count aid for callers that
- * run the step on many small rectangles.  -8: capture / instantiation
- * failed. */
+ * run the step on many small rectangles.  Creation runs the step once
+ * (uncaptured) after the work already queued on `stream` and waits for it:
+ * it WRITES records, qcoeff, dqcoeff, recon and sb_tx_size.  -8: capture /
+ * instantiation failed. */
 typedef struct LavishRdoGraph LavishRdoGraph;
 int lavish_rdo_graph_create(const uint16_t *src, const uint16_t *pred, int stride,
                             int width, int height, uint32_t size_mask,
@@ -476,7 +485,7 @@ int lavish_rdo_graph_create(const uint16_t *src, const uint16_t *pred, int strid
                             const LavishQuantParams *qp, int rdmult,
                             LavishRdoBlock *const *records, int32_t *const *qcoeff,
                             int32_t *const *dqcoeff, uint16_t *recon, uint8_t *sb_tx_size,
-                            LavishRdoGraph **graph);
+                            void *stream, LavishRdoGraph **graph);
 int lavish_rdo_graph_launch(LavishRdoGraph *graph, void *stream);
 void lavish_rdo_graph_destroy(LavishRdoGraph *graph);
 
@@ -606,7 +615,7 @@ int lavish_full_pixel_search_batch_tiled(const uint8_t *src, int src_stride,
  * lavish_full_pixel_search_batch[_tiled] (rounded up to 8; 0 = no cap, one
  * workgroup per 32 jobs).  A scheduling knob for running the search beside
  * another stream's work (the search holds fewer CU slots and runs longer);
- * results do not depend on it.  Default from LAVISH_C3_WGS, else 0; -1 for a
+ * results do not depend on it.  Default 0; -1 for a
  * negative value.  No reference counterpart (the reference's search runs on
  * the encoder's threads). */
 int lavish_set_search_workgroup_cap(int workgroups);

@@ -1,0 +1,107 @@
+"""The headline step exactly as bench.py times it, against the oracle.
+
+bench.RdoStep is the object main() times: C3 (the DIAMOND full-pel search of
+every 16x16 block x 7 references, downsampled SAD, MV_COST_ENTROPY over the
+default nmv tables, cost lists; av1_full_pixel_search, mcomp.c:1755 ->
+full_pixel_diamond :1479 -> diamond_search_sad :1318-1477) on a side stream in
+at most 512 workgroups (lavish_set_search_workgroup_cap: the search kernel
+strides over virtual workgroups) beside C2 (lavish_txq_frame: every block of
+the 14 TX sizes <= 32x32 x every valid type, tx_search.c:2148-2312 ->
+encodemb.c:295-341) on the caller's stream.  Two consecutive steps run, then
+both legs' outputs are compared with the oracle; the search at workgroup
+caps {8, 64, 512, 0} must give identical results.
+"""
+import os
+
+import numpy as np
+import pytest
+
+import _oracle as O
+
+pytestmark = pytest.mark.gpu
+
+THREADS = max(1, min(32, os.cpu_count() or 1))
+
+
+def _bench():
+    import importlib.util
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    spec = importlib.util.spec_from_file_location("bench", os.path.join(root, "bench.py"))
+    b = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(b)
+    return b
+
+
+@pytest.fixture(scope="module")
+def step():
+    import torch
+    assert torch.cuda.is_available()
+    b = _bench()
+    R = b.RdoStep()  # the bench's defaults: 1080p, 7 refs, qindex 128, cap 512, overlapped
+    assert R.overlap and R.c3_wg_cap == b.C3_WG_CAP == 512
+    return b, R
+
+
+@pytest.fixture(scope="module")
+def c3_expected(step):
+    b, R = step
+    mvj, mvc = R.mv_tables
+    return O.full_pixel_search_batch(R.src_np.reshape(-1), R.refs_np.reshape(-1), R.ref_stride,
+                                     b.C3_BLOCK, b.C3_BLOCK, R.jobs_np, "diamond", 0, b.C3_COST,
+                                     R.sad_per_bit, R.error_per_bit, mvj, mvc, skip=b.C3_SKIP,
+                                     cost_list=b.C3_CL, threads=THREADS)
+
+
+def _check_c3(R, exp, exp_cl, what):
+    got = R.M.results_numpy(R.c3_out)
+    for f in ("best_row", "best_col", "bestsme", "steps"):  # the oracle has no search count
+        np.testing.assert_array_equal(got[f], exp[f], err_msg="%s: %s" % (what, f))
+    np.testing.assert_array_equal(R.c3_cl.cpu().numpy(), exp_cl, err_msg=what + ": cost list")
+    return got
+
+
+def test_timed_step_both_legs(step, c3_expected):
+    """Two steps as timed (C3 capped beside C2, two streams), then C3's
+    results and cost lists and every C2 size's qcoeff / dqcoeff / eob."""
+    import torch
+    b, R = step
+    R.c3_out.fill_(0x55)
+    R.c3_cl.fill_(-7)
+    for out in R.frame.outs.values():
+        for t in out.values():
+            t.fill_(0x33)
+    for _ in range(2):
+        R.step()
+    torch.cuda.synchronize()
+    assert R.L.status()[0] == 0, R.L.status()
+    exp, exp_cl = c3_expected
+    got = _check_c3(R, exp, exp_cl, "overlapped, cap 512")
+    assert (np.abs(got["best_row"]) + np.abs(got["best_col"]) > 0).mean() > 0.5
+    oq = O.build_quant(8, 128)
+    for s in R.sizes:
+        qc, dq, eob = O.txq_plane(R.res_np, s, R.L.valid_type_mask(s), oq, threads=THREADS)
+        out = R.frame.outs[s]
+        np.testing.assert_array_equal(out["qcoeff"].cpu().numpy(), qc.transpose(1, 0, 2),
+                                      err_msg="size %d qcoeff" % s)
+        np.testing.assert_array_equal(out["dqcoeff"].cpu().numpy(), dq.transpose(1, 0, 2),
+                                      err_msg="size %d dqcoeff" % s)
+        np.testing.assert_array_equal(out["eob"].cpu().numpy().view(np.uint16), eob.T,
+                                      err_msg="size %d eob" % s)
+        del qc, dq, eob
+
+
+@pytest.mark.parametrize("cap", [8, 64, 512, 0])
+def test_search_workgroup_cap_sweep(step, c3_expected, cap):
+    """The capped search (grid-stride over virtual workgroups) is the
+    uncapped search: identical results at every cap."""
+    import torch
+    b, R = step
+    R.c3_out.fill_(0x55)
+    R.c3_cl.fill_(-7)
+    R.M.set_search_workgroup_cap(cap)
+    try:
+        R.c3(R.stream)
+        torch.cuda.synchronize()
+    finally:
+        R.M.set_search_workgroup_cap(0)
+    _check_c3(R, *c3_expected, what="cap %d" % cap)

@@ -145,6 +145,19 @@ def test_c4_4k_10bit_frame(L):
     np.testing.assert_array_equal(fr.sb_tx_size.cpu().numpy(), choice)
     np.testing.assert_array_equal(fr.recon.cpu().numpy().view(np.uint16), recon)
     assert len(np.unique(choice)) > 1
+    # every size's kernels on the caller's stream (lavish_set_fan_width(1), the
+    # profiling arrangement): the same frame
+    fr1 = L.RdoFrame(ts)
+    L.set_fan_width(1)
+    try:
+        L.rdo_frame(ts, tp, fr1, L.build_quant_params(10, 128, L.QUANT_FP), rdmult, 10)
+        torch.cuda.synchronize()
+    finally:
+        L.set_fan_width(3)
+    np.testing.assert_array_equal(fr1.sb_tx_size.cpu().numpy(), choice)
+    np.testing.assert_array_equal(fr1.recon.cpu().numpy().view(np.uint16), recon)
+    for s in masks:
+        np.testing.assert_array_equal(L.rdo_records(fr1.outs[s])["rdcost"], per[s][0]["rdcost"])
 
 
 def test_c5_bands_world1_three_streams(L):
@@ -237,7 +250,15 @@ def test_rdo_graph_replays_new_inputs(L):
     tp = torch.from_numpy(pred.view(np.int16)).cuda()
     qp = L.build_quant_params(10, 128, L.QUANT_FP)
     gfr = L.RdoFrame(ts)
+    # creation runs the step once after the caller's queued work on the
+    # outputs: the fill below must not land after the warm-up
+    gfr.recon.fill_(-1)
     g = L.RdoGraph(ts, tp, gfr, qp, rdmult, 10)
+    torch.cuda.synchronize()
+    dfr0 = L.RdoFrame(ts)
+    L.rdo_frame(ts, tp, dfr0, qp, rdmult, 10)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(gfr.recon.cpu().numpy(), dfr0.recon.cpu().numpy())
     for it in range(3):
         if it:
             tp.copy_(torch.roll(tp, shifts=(it, 2 * it), dims=(0, 1)))
