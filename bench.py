@@ -651,7 +651,7 @@ def main_c4(args):
         line["sb_tx_size"] = {"%dx%d" % (L.TX_W[s], L.TX_H[s]): int(n) for s, n in zip(
             *np.unique(fr.sb_tx_size.cpu().numpy(), return_counts=True)) if s < 19}
     if args.workload == "c5" and world == 1 and args.c5_emulate:
-        line["c5_emulation"] = c5_emulate(H, W, proc, [int(g) for g in args.c5_emulate.split(",")],
+        line["c5_emulation"] = c5_emulate(H, W, proc, [int(g) for g in args.c5_emulate.replace(":", ",").split(",")],
                                           args.steps, args.warmup, step_ms)
     if args.workload == "c4" and world == 1:
         # the bound that applies: int32 VALU
