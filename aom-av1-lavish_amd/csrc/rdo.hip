@@ -1,705 +1,12 @@
-// rdo.hip -- C4: fused per-block TX-type RDO for gfx950, and the 64-point
-// forward transform sizes.
-//
-// Per TX block and candidate TX type (the body of
-// search_tx_type, av1/encoder/tx_search.c:2148-2312, with TX-domain
-// distortion):
-//   aom_highbd_subtract_block (aom_dsp/subtract.c:38-54)
-//   -> av1_fwd_txfm2d_WxH (av1/encoder/av1_fwd_txfm2d.c:56-312, 64-point
-//      sizes zeroed + re-packed to the 32x32 quadrant)
-//   -> av1_highbd_quantize_fp (av1/encoder/av1_quantize.c:125-198,565-577)
-//   -> aom_satd on the coefficients (aom_dsp/avg.c:509-516)
-//   -> dist_block_tx_domain: av1_highbd_block_error, RIGHT_SIGNED_SHIFT by
-//      (MAX_TX_SCALE - tx_scale) * 2 (tx_search.c:1077-1116)
-//   -> rate_estimator (av1/encoder/tpl_model.c:214-226, DCT_DCT scan)
-//   -> RDCOST(rdmult, rate, dist) (av1/encoder/rd.h:31-33)
-// and the block keeps the first type with the strictly smallest cost (the
-// `<` test of tx_search.c:2246).  Output per block: the decision record and
-// the winning qcoeff / dqcoeff.
-//
-// Mode 0 of the same kernel is the plain lavish_txq_plane contract (every
-// type's qcoeff / dqcoeff / eob) for the 64-point sizes, which txq.hip does
-// not instantiate.
-//
-// Layout per wave: P = 64 / min(W,H) blocks.  Column pass: one column per
-// lane (registers) -> LDS.  Row pass: only the KH = min(H,32) rows that
-// survive the 64-point zeroing are transformed, one per lane; the lane then
-// holds the row's KW = min(W,32) kept coefficients, quantizes them and
-// contributes to the block reductions (xor shuffles over the KH lanes of the
-// block).  The FAST 24-bit path is certified for |residual| <= 1023 for every
-// size including the 64-point ones (tools/range_analysis.py).
-#include <type_traits>
-
-#include "coeffcost_dev.h"
-#include "lavish_internal.h"
-#include "quant_dev.h"
+// rdo.hip -- C4 host side: the per-size decision launches (kernels in
+// rdo_kern.h, instantiated per mode in rdo_m0..3.hip), the frame-level step
+// (every candidate size, the per-SB TX-size decision, the reconstruction),
+// the 64-point pixel-domain path and the captured step (HIP graph).
+#include "rdo_kern.h"
 
 namespace lavish {
 
-struct RdoArgs {
-  const int16_t* res;    // mode 0: residual plane
-  const uint16_t* src;   // mode 1: source / prediction planes (u16)
-  const uint16_t* pred;
-  int stride;
-  int bw, nblocks;
-  int ntypes;
-  int types[16];
-  int bd;
-  int quant_kind;  // mode 0
-  int highbd;      // mode 0
-  int rdmult;      // mode 1
-  QP qp;
-  const int16_t* iscan_type[16];  // per slot: inverse scan of the type (n)
-  // evaluation order: slots grouped by vertical 1-D kind (one column pass per
-  // group); newcol[i] = 1 where order[i] starts a group
-  int order[16];
-  int newcol[16];
-  // decision modes, optional: per-block allowed_tx_mask and search order
-  // (txk_map, [block][16]) as prune_tx_2D leaves them
-  const uint16_t* block_mask;
-  const uint8_t* block_map;
-  const int16_t* iscan_dct;       // DCT_DCT inverse scan (rate_estimator)
-  // MODE 3: the coefficient rate (av1_cost_coeffs_txb) replaces
-  // rate_estimator: the size's luma LV_MAP_COEFF_COST / LV_MAP_EOB_COST,
-  // per-block TXB_CTX (nullable: {0, 0}), get_tx_type_cost per tx type, and
-  // the av1_nz_map_ctx_offset shape of the unadjusted size
-  const int32_t* cc_cost;
-  const int32_t* cc_eob;
-  const LavishTxbCtx* txb_ctx;
-  int tx_type_cost[16];
-  int nz_wlt, nz_wgt;
-  int32_t* qcoeff;
-  int32_t* dqcoeff;
-  uint16_t* eob;
-  int32_t* coeff;
-  LavishRdoBlock* out;
-};
-
 namespace {
-
-template <int W, int H>
-struct RTile {
-  static constexpr int MN = W < H ? W : H;
-  static constexpr int P = 64 / MN;
-  static constexpr int CPT = W / MN;
-  static constexpr int KW = W > 32 ? 32 : W;
-  static constexpr int KH = H > 32 ? 32 : H;
-  static constexpr int NC = KW * KH;                 // coefficients kept per block
-  static constexpr int RPT = (P * KH + 63) / 64;     // kept rows per lane
-  static constexpr int T1S = W + 1;
-  static constexpr int T1 = P * KH * T1S;
-  static constexpr int T2 = P * NC;
-};
-
-__device__ __forceinline__ int get_msb(uint32_t n) { return 31 - __builtin_clz(n); }
-
-// Per-tile LDS of the pixel-domain mode (MODE 2): the prediction pixels, the
-// inverse transform's transposition buffer, and per-block sums.
-template <int W, int H>
-struct PxLds {
-  static constexpr int P = RTile<W, H>::P;
-  static constexpr int T1S = W + 1;
-  uint16_t pred[P * H * W];
-  int32_t tx[P * H * T1S];
-  int64_t bsse[P];  // block_sse (rounded, x16)
-  uint64_t psse[P]; // this type's sum of (src - recon)^2
-};
-
-template <int W, int H, int MODE, bool FAST, int QK, bool HBD, int BDI>
-__device__ __forceinline__ void rdo_types(const RdoArgs& a, const int32_t (&res)[RTile<W, H>::CPT][H],
-                                          int32_t* t1, int32_t* t2, int32_t* tb, PxLds<W, H>* px,
-                                          int lane, int blk0, int nvalid) {
-  using C = TxCfg<W, H>;
-  using T = RTile<W, H>;
-  using B = Bd<BDI>;
-  constexpr int NC = T::NC, KW = T::KW, KH = T::KH, T1S = T::T1S;
-  constexpr int LS = C::log_scale;
-  constexpr bool DEC = MODE >= 1;  // decision modes (1: TX-domain, 2: pixel-domain distortion)
-  constexpr bool RATE = MODE == 3;  // TX-domain distortion, coefficient rate
-  // per (row-pass slot k) running best of the block that slot belongs to
-  int64_t best_rd[T::RPT], best_dist[T::RPT], best_sse[T::RPT];
-  int best_type[T::RPT], best_eob[T::RPT], best_rate[T::RPT], best_satd[T::RPT];
-#pragma unroll
-  for (int k = 0; k < T::RPT; ++k) {
-    best_rd[k] = INT64_MAX;
-    best_dist[k] = best_sse[k] = 0;
-    best_type[k] = best_eob[k] = best_rate[k] = best_satd[k] = 0;
-  }
-  // per block (LDS, read at each decision): the allowed types that also
-  // appear in the block's search order, and each type's position in that
-  // order; identity without per-block data.  A zero mask means DCT_DCT only
-  // (get_tx_mask's rule, tx_search.c:1885-1888).
-  __shared__ uint8_t s_rank[T::P][16];
-  __shared__ uint16_t s_ok[T::P];
-  if constexpr (DEC) {
-    if (lane < T::P) {
-      uint32_t ok = 0xFFFFu;
-      if (lane < nvalid) {
-        const int blk = blk0 + lane;
-        if (a.block_mask) {
-          const uint32_t m = a.block_mask[blk];
-          ok = m ? m : 1u;
-        }
-        if (a.block_map) {
-          uint32_t present = 0;
-          for (int i = 0; i < 16; ++i) s_rank[lane][i] = 16;
-          for (int i = 0; i < 16; ++i) {
-            const int t = a.block_map[(size_t)blk * 16 + i];
-            if (t < 16 && !((present >> t) & 1)) {
-              present |= 1u << t;
-              s_rank[lane][t] = (uint8_t)i;
-            }
-          }
-          ok &= present;
-        } else {
-          for (int i = 0; i < 16; ++i) s_rank[lane][i] = (uint8_t)i;
-        }
-      }
-      s_ok[lane] = (uint16_t)ok;
-    }
-    wave_sync();
-  }
-  // MODE 3: the cost tables
-  __shared__ int32_t s_cc[RATE ? cc::kTabCells : 1];
-  if constexpr (RATE) {
-    for (int i = lane; i < cc::kCostCells; i += 64) s_cc[i] = a.cc_cost[i];
-    if (lane < cc::kEobCells) s_cc[cc::kCostCells + lane] = a.cc_eob[lane];
-    wave_sync();
-  }
-
-  for (int oi = 0; oi < a.ntypes; ++oi) {
-    const int ti = __builtin_amdgcn_readfirstlane(a.order[oi]);
-    const int t = __builtin_amdgcn_readfirstlane(a.types[ti]);
-    const int vt = (kVtxPacked >> (2 * t)) & 3, ht = (kHtxPacked >> (2 * t)) & 3;
-    const int kc = vt == 3 ? 2 : (vt == 0 ? 0 : 1);
-    const int kr = ht == 3 ? 2 : (ht == 0 ? 0 : 1);
-    const bool ud = vt == 2;
-    const bool lr = ht == 2;  // FLIPADST rows: the column results read right to left
-    const int16_t* iscan = a.iscan_type[ti];
-
-    // ---- columns (av1_fwd_txfm2d.c:88-106), once per vertical kind; only
-    // rows < KH are kept ----
-    if (__builtin_amdgcn_readfirstlane(a.newcol[oi])) {
-#pragma unroll
-      for (int k = 0; k < T::CPT; ++k) {
-        const int j = k * 64 + lane;
-        const int b = j / W, c = j % W;
-        int32_t in[H], out[H];
-#pragma unroll
-        for (int r = 0; r < H; ++r) {
-          const int32_t x = ud ? res[k][H - 1 - r] : res[k][r];
-          if constexpr (FAST) in[r] = x * (1 << C::s0);
-          else in[r] = round_shift_1<-C::s0>(x);
-        }
-        fwd_1d<H, C::cos_bit_col, FAST>(kc, in, out);
-#pragma unroll
-        for (int r = 0; r < KH; ++r) t1[(b * KH + r) * T1S + c] = round_shift_1<-C::s1>(out[r]);
-      }
-      wave_sync();
-    }
-
-    // ---- kept rows + quantization + per-block statistics ----
-    int st_last[T::RPT], st_rate[T::RPT], st_satd[T::RPT];
-    int64_t st_dist[T::RPT], st_sse[T::RPT];
-    int32_t st_q[DEC ? T::RPT : 1][DEC ? KW : 1];
-#pragma unroll
-    for (int k = 0; k < T::RPT; ++k) {
-      const int j = k * 64 + lane;
-      const int b = j / KH, r = j % KH;
-      const bool live = b < T::P;
-      const int bb = live ? b : 0;
-      int32_t in[W], out[W];
-      const int32_t* row = t1 + (bb * KH + r) * T1S;
-      if (lr) {
-#pragma unroll
-        for (int c = 0; c < W; ++c) in[c] = row[W - 1 - c];
-      } else {
-#pragma unroll
-        for (int c = 0; c < W; ++c) in[c] = row[c];
-      }
-      fwd_1d<W, C::cos_bit_row, FAST>(kr, in, out);
-      int32_t q[KW];
-      int last = 0, satd = 0;
-      int64_t err = 0, sse = 0;
-      const size_t obase = ((size_t)ti * a.nblocks + blk0 + bb) * NC;
-#pragma unroll
-      for (int c = 0; c < KW; ++c) {
-        int32_t v = round_shift_1<-C::s2>(out[c]);
-        if constexpr (C::rect2) v = rshift64((int64_t)v * 5793, 12);
-        const int rc = c * KH + r;
-        const bool ac = c != 0 || r != 0;
-        if constexpr (MODE == 0 && QK == LAVISH_QUANT_NONE) {
-          q[c] = 0;
-          if (live && bb < nvalid) a.coeff[obase + rc] = v;
-        } else {
-          if constexpr (MODE == 0) {
-            if (a.coeff != nullptr && live && bb < nvalid) a.coeff[obase + rc] = v;
-          }
-          q[c] = quant_one<LS, QK, HBD>(v, ac, a.qp);
-        }
-        if constexpr (DEC) {
-          const int32_t dq = dequant_one<LS>(q[c], ac, a.qp);
-          const int64_t d = (int64_t)v - dq;
-          err += d * d;
-          sse += (int64_t)v * v;
-          satd += abs(v);
-        }
-        if constexpr (MODE == 0) {
-          if (live) t2[bb * NC + rc] = q[c];
-        }
-        last = q[c] != 0 ? max(last, iscan[rc] + 1) : last;
-      }
-#pragma unroll
-      for (int m = 1; m < KH; m <<= 1) last = max(last, __shfl_xor(last, m));
-      if constexpr (MODE == 0) {
-        if (r == 0 && live && bb < nvalid && a.eob != nullptr)
-          a.eob[(size_t)ti * a.nblocks + blk0 + bb] = (uint16_t)last;
-      } else {
-        int rate = 0;
-        if constexpr (RATE) {
-          // av1_cost_coeffs_txb (txb_rdopt.c:599-624) on this type's
-          // quantized block.  Lane = row r of its block, so the |level| map
-          // neighbours of get_nz_mag / get_br_ctx are this lane's own
-          // columns c+1.. and the same columns of rows r+1.. (lanes below):
-          // levels clipped to 15 as nibbles, 8 per word, shifted down the
-          // wave a word at a time; rows past the block read as the zero pad.
-          constexpr int NW = (KW + 7) / 8;
-          const int cls = cc::tx_class(t);
-          const int nrow = cls == 2 ? 4 : 2;  // rows below that a context reads
-          uint32_t pk[5][NW];
-#pragma unroll
-          for (int w = 0; w < NW; ++w) pk[0][w] = 0u;
-#pragma unroll
-          for (int c = 0; c < KW; ++c)
-            pk[0][c >> 3] |= (uint32_t)min(abs(q[c]), 15) << (4 * (c & 7));
-#pragma unroll
-          for (int d = 1; d <= 4; ++d) {
-#pragma unroll
-            for (int w = 0; w < NW; ++w) {
-              const uint32_t x = d <= nrow ? (uint32_t)__shfl_down((int)pk[0][w], d) : 0u;
-              pk[d][w] = r + d < KH ? x : 0u;
-            }
-          }
-          auto nib = [&](int d, int c) -> int {
-            return c < KW ? (int)((pk[d][c >> 3] >> (4 * (c & 7))) & 15u) : 0;
-          };
-          // get_nz_mag for 8 positions per word at once (SWAR on the
-          // nibbles): every neighbour clipped to 3 -- x & 3, or 3 where bit
-          // 2 or 3 is set -- then the class's five neighbours, each a
-          // nibble shift of a row word, summed without carries (<= 15)
-          uint32_t m3[5][NW];
-#pragma unroll
-          for (int d = 0; d < 5; ++d)
-#pragma unroll
-            for (int w = 0; w < NW; ++w) {
-              const uint32_t x = pk[d][w];
-              const uint32_t f = ((x >> 2) | (x >> 3)) & 0x11111111u;
-              m3[d][w] = (x & 0x33333333u) | f | (f << 1);
-            }
-          auto sh = [&](int d, int w, int k) -> uint32_t {  // nibble c + k of row d, word w
-            return (m3[d][w] >> (4 * k)) | (w + 1 < NW ? m3[d][w + 1] << (32 - 4 * k) : 0u);
-          };
-          uint32_t nzs[NW];
-#pragma unroll
-          for (int w = 0; w < NW; ++w) {
-            const uint32_t base = sh(0, w, 1) + m3[1][w];
-            nzs[w] = cls == 0 ? base + sh(1, w, 1) + sh(0, w, 2) + m3[2][w]
-                   : cls == 1 ? base + sh(0, w, 2) + sh(0, w, 3) + sh(0, w, 4)
-                              : base + m3[2][w] + m3[3][w] + m3[4][w];
-          }
-          const bool has_ctx = a.txb_ctx != nullptr && live && bb < nvalid;
-          const LavishTxbCtx tc = has_ctx ? a.txb_ctx[blk0 + bb] : LavishTxbCtx{0, 0};
-#pragma unroll
-          for (int c = 0; c < KW; ++c) {
-            const int rc = c * KH + r;
-            const int i = iscan[rc];
-            if (i < last) {
-              const int nzmag = (int)((nzs[c >> 3] >> (4 * (c & 7))) & 15u);
-              // get_br_ctx's raw sum, needed only above level 2
-              int brmag = 0;
-              if (abs(q[c]) > 2)
-                brmag = nib(0, c + 1) + nib(1, c) +
-                        (cls == 0 ? nib(1, c + 1) : cls == 1 ? nib(0, c + 2) : nib(2, c));
-              rate += cc::coeff_term_mag(s_cc, cls, a.nz_wlt, a.nz_wgt, NC, rc, c, r, i, last,
-                                         q[c], tc.dc_sign_ctx, nzmag, brmag);
-            }
-          }
-#pragma unroll
-          for (int m = 1; m < KH; m <<= 1) rate += __shfl_xor(rate, m);
-          rate = cc::txb_rate(s_cc, cls, tc.txb_skip_ctx, last, a.tx_type_cost[t], rate);
-        } else {
-          // rate_estimator: positions of the DCT_DCT scan below eob
-#pragma unroll
-          for (int c = 0; c < KW; ++c) {
-            const int rc = c * KH + r;
-            const uint32_t al = (uint32_t)abs(q[c]);
-            if (a.iscan_dct[rc] < last) rate += get_msb(al + 1) + 1 + (al > 0);
-          }
-#pragma unroll
-          for (int m = 1; m < KH; m <<= 1) rate += __shfl_xor(rate, m);
-          rate = (rate + 1) << 9;  // AV1_PROB_COST_SHIFT
-        }
-#pragma unroll
-        for (int m = 1; m < KH; m <<= 1) {
-          satd += __shfl_xor(satd, m);
-          err += __shfl_xor(err, m);
-          sse += __shfl_xor(sse, m);
-        }
-        // av1_highbd_block_error rounding, then the TX-domain shift
-        const int sh = 2 * (a.bd - 8);
-        if (sh > 0) {
-          const int64_t rnd = (int64_t)1 << (sh - 1);
-          err = (err + rnd) >> sh;
-          sse = (sse + rnd) >> sh;
-        }
-        constexpr int dshift = (1 - LS) * 2;  // (MAX_TX_SCALE - tx_scale) * 2
-        if constexpr (dshift >= 0) {
-          st_dist[k] = err >> dshift;
-          st_sse[k] = sse >> dshift;
-        } else {
-          st_dist[k] = err << -dshift;
-          st_sse[k] = sse << -dshift;
-        }
-        st_last[k] = last;
-        st_rate[k] = rate;
-        st_satd[k] = satd;
-#pragma unroll
-        for (int c = 0; c < KW; ++c) st_q[k][c] = q[c];
-      }
-      if constexpr (MODE == 2) {
-        // inverse rows (inv_txfm2d_add_c "Rows") straight from this lane's
-        // quantized row: dequantize, x NewInvSqrt2 for 2:1, clamp, 1-D, shift
-        int32_t vin[W], vout[W];
-#pragma unroll
-        for (int c = 0; c < W; ++c) {
-          int32_t v = dequant_one<LS>(q[c], c != 0 || r != 0, a.qp);
-          if constexpr (C::rect2) v = rshift64((int64_t)v * 2896, 12);
-          vin[c] = clamp_bits<B::clamp_in_row>(v);
-        }
-        inv_1d<W, 12, B::rng_row>(kr, vin, vout);
-        if (live) {
-#pragma unroll
-          for (int c = 0; c < W; ++c) px->tx[(bb * H + r) * T1S + c] = rshift_r(vout[c], -C::is0);
-        }
-      }
-    }
-
-    if constexpr (MODE == 2) {
-      wave_sync();
-      // ---- inverse columns + reconstruction + pixel SSE against src ----
-      constexpr int maxv = (1 << B::bd) - 1;
-#pragma unroll
-      for (int k = 0; k < T::CPT; ++k) {
-        const int j = k * 64 + lane;
-        const int b = j / W, c = j % W;
-        const int cc = lr ? W - 1 - c : c;
-        int32_t in[H], out[H];
-#pragma unroll
-        for (int r = 0; r < H; ++r)
-          in[r] = clamp_bits<B::clamp_in_col>(px->tx[(b * H + r) * T1S + cc]);
-        inv_1d<H, 12, B::rng_col>(kc, in, out);
-        uint64_t ps = 0;
-#pragma unroll
-        for (int r = 0; r < H; ++r) {
-          const int p = px->pred[(b * H + r) * W + c];
-          const int v = p + rshift_r(ud ? out[H - 1 - r] : out[r], -C::is1);
-          const int rec = v < 0 ? 0 : (v > maxv ? maxv : v);
-          const int d = p + res[k][r] - rec;  // src - recon
-          ps += (uint64_t)(d * d);
-        }
-#pragma unroll
-        for (int m = 1; m < W; m <<= 1) ps += __shfl_xor(ps, m);
-        if (c == 0) px->psse[b] = ps;
-      }
-      wave_sync();
-    }
-
-    if constexpr (DEC) {
-      // ---- distortion, RDCOST and the running best per block ----
-#pragma unroll
-      for (int k = 0; k < T::RPT; ++k) {
-        const int j = k * 64 + lane;
-        const int b = j / KH, r = j % KH;
-        const bool live = b < T::P;
-        const int bb = live ? b : 0;
-        int64_t dist = st_dist[k], dsse = st_sse[k];
-        if constexpr (MODE == 2) {
-          // search_tx_type with pixel-domain distortion (tx_search.c:2187-2231);
-          // sizes here are <= 32x32, never TX_64X64
-          const int64_t bsse = px->bsse[bb];
-          if (st_last[k] == 0) {
-            dist = bsse;
-          } else {
-            const int sh = 2 * (a.bd - 8);
-            uint64_t ps = px->psse[bb];
-            if (sh > 0) ps = (ps + ((uint64_t)1 << (sh - 1))) >> sh;
-            // 16 * pixel_dist(): an unsigned 32-bit product
-            const int64_t pxd = (int64_t)(uint32_t)(16u * (uint32_t)ps);
-            const bool high = bsse >= (int64_t)128 * 128 * W * H;
-            dist = (high && pxd < dist) ? dist : pxd;
-          }
-          dsse = bsse;
-        }
-        const int64_t rd = (((int64_t)st_rate[k] * a.rdmult + 256) >> 9) + dist * 128;
-        // the reference keeps the first type of strictly smallest cost in
-        // its search order (txk_map; ascending without one); types are
-        // visited here grouped by vertical kind, so equal costs resolve by
-        // that order's rank
-        if (((s_ok[bb] >> t) & 1) &&
-            (rd < best_rd[k] ||
-             (rd == best_rd[k] && s_rank[bb][t] < s_rank[bb][best_type[k]]))) {
-          best_rd[k] = rd;
-          best_dist[k] = dist;
-          best_sse[k] = dsse;
-          best_type[k] = t;
-          best_eob[k] = st_last[k];
-          best_rate[k] = st_rate[k];
-          best_satd[k] = st_satd[k];
-#pragma unroll
-          for (int c = 0; c < KW; ++c)
-            if (live) tb[bb * NC + c * KH + r] = st_q[k][c];
-        }
-      }
-    }
-    wave_sync();
-
-    if constexpr (MODE == 0) {
-      // coalesced copy-out of this type's qcoeff / dqcoeff
-      if (a.qcoeff != nullptr) {
-        const int total = nvalid * NC;
-        const size_t gbase = ((size_t)ti * a.nblocks + blk0) * NC;
-        for (int i = lane * 4; i < total; i += 64 * 4) {
-          const v4i q4 = *reinterpret_cast<const v4i*>(&t2[i]);
-          __builtin_nontemporal_store(q4, reinterpret_cast<v4i*>(&a.qcoeff[gbase + i]));
-          if (a.dqcoeff != nullptr) {
-            const int rc0 = i % NC;
-            v4i d4;
-            d4.x = dequant_one<LS>(q4.x, rc0 != 0, a.qp);
-            d4.y = dequant_one<LS>(q4.y, 1, a.qp);
-            d4.z = dequant_one<LS>(q4.z, 1, a.qp);
-            d4.w = dequant_one<LS>(q4.w, 1, a.qp);
-            __builtin_nontemporal_store(d4, reinterpret_cast<v4i*>(&a.dqcoeff[gbase + i]));
-          }
-        }
-      }
-      wave_sync();
-    }
-  }
-
-  if constexpr (DEC) {
-    // decision records (one lane per block) and the winner's coefficients.
-    // A block none of whose allowed types is in the evaluated set (possible
-    // only with caller masks) has no candidate: record best_type
-    // TX_TYPE_INVALID (255), eob 0, rdcost INT64_MAX, zero coefficients.
-    __shared__ uint8_t s_dead[T::P];
-#pragma unroll
-    for (int k = 0; k < T::RPT; ++k) {
-      const int j = k * 64 + lane;
-      const int b = j / KH, r = j % KH;
-      if (b < T::P && b < nvalid && r == 0) {
-        const bool dead = best_rd[k] == INT64_MAX;
-        LavishRdoBlock o;
-        o.best_type = dead ? 255 : best_type[k];
-        o.eob = best_eob[k];
-        o.rate = best_rate[k];
-        o.satd = best_satd[k];
-        o.dist = best_dist[k];
-        o.sse = best_sse[k];
-        o.rdcost = best_rd[k];
-        a.out[blk0 + b] = o;
-        s_dead[b] = dead;
-      }
-    }
-    wave_sync();
-    const int total = nvalid * NC;
-    const size_t gbase = (size_t)blk0 * NC;
-    for (int i = lane * 4; i < total; i += 64 * 4) {
-      v4i q4 = *reinterpret_cast<const v4i*>(&tb[i]);
-      if (s_dead[i / NC]) q4 = v4i{0, 0, 0, 0};
-      __builtin_nontemporal_store(q4, reinterpret_cast<v4i*>(&a.qcoeff[gbase + i]));
-      const int rc0 = i % NC;
-      v4i d4;
-      d4.x = dequant_one<LS>(q4.x, rc0 != 0, a.qp);
-      d4.y = dequant_one<LS>(q4.y, 1, a.qp);
-      d4.z = dequant_one<LS>(q4.z, 1, a.qp);
-      d4.w = dequant_one<LS>(q4.w, 1, a.qp);
-      __builtin_nontemporal_store(d4, reinterpret_cast<v4i*>(&a.dqcoeff[gbase + i]));
-    }
-  }
-}
-
-// one wave = one tile of P blocks; 64-thread workgroups (LDS per tile is up
-// to ~20 KB for the 64-point sizes).  MODE 0: per-type coefficients (the
-// txq_plane contract), 1: decision with TX-domain distortion, 2: decision
-// with pixel-domain distortion (sizes <= 32x32; BDI = bit-depth index), 3:
-// mode 1 ranked by the coefficient rate (av1_cost_coeffs_txb) instead of
-// rate_estimator.
-// Occupancy: a rdo_kernel wave holds a column (or row) of its block per lane
-// through each 1-D transform, so the large sizes sit just above a VGPR
-// step of the unified 512-register file (32x32 TX-domain: 266 registers =
-// 1 wave per SIMD, latency bound at 14% of the VALU peak).  The TX-domain
-// decision kernels of the sizes of 512+ coefficients ask for 2 waves per
-// SIMD (<= 256 registers), the 16x16 one for 4 (<= 128).
-#ifndef LAVISH_RDO_WV16
-#define LAVISH_RDO_WV16 4
-#endif
-#ifndef LAVISH_RDO_WV32
-#define LAVISH_RDO_WV32 2
-#endif
-#ifndef LAVISH_RDO_WV64
-#define LAVISH_RDO_WV64 2
-#endif
-template <int W, int H, int MODE>
-constexpr int rdo_waves() {
-  if (MODE != 1) return 1;
-  if (W == 16 && H == 16) return LAVISH_RDO_WV16;
-  if (W * H >= 2048) return LAVISH_RDO_WV64;
-  return W * H >= 512 ? LAVISH_RDO_WV32 : 1;
-}
-
-template <int W, int H, int MODE, int BDI>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(rdo_waves<W, H, MODE>())))
-void rdo_kernel(RdoArgs a) {
-  using T = RTile<W, H>;
-  __shared__ int32_t t1[T::T1];
-  __shared__ __attribute__((aligned(16))) int32_t t2[MODE == 0 ? T::T2 : 4];
-  __shared__ __attribute__((aligned(16))) int32_t tb[MODE >= 1 ? T::T2 : 4];
-  __shared__ typename std::conditional<MODE == 2, PxLds<W, H>, int>::type pxs;
-  PxLds<W, H>* px = MODE == 2 ? reinterpret_cast<PxLds<W, H>*>(&pxs) : nullptr;
-
-  const int lane = threadIdx.x;
-  const int blk0 = blockIdx.x * T::P;
-  if (blk0 >= a.nblocks) return;
-  const int nvalid = min(T::P, a.nblocks - blk0);
-
-  int32_t res[T::CPT][H];
-  int32_t amax = 0;
-#pragma unroll
-  for (int k = 0; k < T::CPT; ++k) {
-    const int j = k * 64 + lane;
-    const int b = j / W, c = j % W;
-    const int blk = blk0 + b;
-    int64_t ss = 0;
-    if (b < nvalid) {
-      const int by = blk / a.bw, bx = blk - by * a.bw;
-      const size_t off = (size_t)by * H * a.stride + (size_t)bx * W + c;
-#pragma unroll
-      for (int r = 0; r < H; ++r) {
-        int32_t v;
-        if constexpr (MODE == 0) {
-          v = a.res[off + (size_t)r * a.stride];
-        } else {
-          const int32_t p = a.pred[off + (size_t)r * a.stride];
-          v = (int32_t)a.src[off + (size_t)r * a.stride] - p;
-          if constexpr (MODE == 2) px->pred[(b * H + r) * W + c] = (uint16_t)p;
-        }
-        res[k][r] = v;
-        amax = max(amax, abs(v));
-        ss += (int64_t)v * v;
-      }
-    } else {
-#pragma unroll
-      for (int r = 0; r < H; ++r) {
-        res[k][r] = 0;
-        if constexpr (MODE == 2) px->pred[(b * H + r) * W + c] = 0;
-      }
-    }
-    if constexpr (MODE == 2) {
-      // block_sse (tx_search.c:2079-2094): sum of squares of the residual,
-      // highbd-rounded by 2 (bd - 8) bits, x 16
-#pragma unroll
-      for (int m = 1; m < W; m <<= 1) ss += __shfl_xor(ss, m);
-      constexpr int sh = 2 * (Bd<BDI>::bd - 8);
-      if constexpr (sh > 0) ss = (ss + ((int64_t)1 << (sh - 1))) >> sh;
-      if (c == 0) px->bsse[b] = ss * 16;
-    }
-  }
-  if constexpr (MODE == 2) wave_sync();
-  const bool fast = __builtin_amdgcn_ballot_w64(amax > kFastResidualMax) == 0;
-  if constexpr (MODE >= 1) {
-    if (fast)
-      rdo_types<W, H, MODE, true, LAVISH_QUANT_FP, true, BDI>(a, res, t1, t2, tb, px, lane, blk0,
-                                                              nvalid);
-    else
-      rdo_types<W, H, MODE, false, LAVISH_QUANT_FP, true, BDI>(a, res, t1, t2, tb, px, lane, blk0,
-                                                               nvalid);
-  } else {
-#define LAVISH_RDO_RUN(F, Q, HB) \
-  rdo_types<W, H, 0, F, Q, HB, 0>(a, res, t1, t2, tb, px, lane, blk0, nvalid)
-    if (a.quant_kind == LAVISH_QUANT_NONE) {
-      if (fast) LAVISH_RDO_RUN(true, LAVISH_QUANT_NONE, false);
-      else LAVISH_RDO_RUN(false, LAVISH_QUANT_NONE, false);
-    } else if (a.quant_kind == LAVISH_QUANT_FP) {
-      if (a.highbd) {
-        if (fast) LAVISH_RDO_RUN(true, LAVISH_QUANT_FP, true);
-        else LAVISH_RDO_RUN(false, LAVISH_QUANT_FP, true);
-      } else {
-        if (fast) LAVISH_RDO_RUN(true, LAVISH_QUANT_FP, false);
-        else LAVISH_RDO_RUN(false, LAVISH_QUANT_FP, false);
-      }
-    } else {
-      if (a.highbd) {
-        if (fast) LAVISH_RDO_RUN(true, LAVISH_QUANT_B, true);
-        else LAVISH_RDO_RUN(false, LAVISH_QUANT_B, true);
-      } else {
-        if (fast) LAVISH_RDO_RUN(true, LAVISH_QUANT_B, false);
-        else LAVISH_RDO_RUN(false, LAVISH_QUANT_B, false);
-      }
-    }
-#undef LAVISH_RDO_RUN
-  }
-}
-
-template <int W, int H, int MODE>
-void launch_rdo(const RdoArgs& a, hipStream_t s) {
-  const int grid = (a.nblocks + RTile<W, H>::P - 1) / RTile<W, H>::P;
-  if (grid == 0) return;
-  if constexpr (MODE == 2) {
-    if (a.bd == 8)
-      hipLaunchKernelGGL((rdo_kernel<W, H, 2, 0>), dim3(grid), dim3(64), 0, s, a);
-    else if (a.bd == 10)
-      hipLaunchKernelGGL((rdo_kernel<W, H, 2, 1>), dim3(grid), dim3(64), 0, s, a);
-    else
-      hipLaunchKernelGGL((rdo_kernel<W, H, 2, 2>), dim3(grid), dim3(64), 0, s, a);
-  } else {
-    hipLaunchKernelGGL((rdo_kernel<W, H, MODE, 0>), dim3(grid), dim3(64), 0, s, a);
-  }
-  LAVISH_CHECK(hipGetLastError());
-}
-
-template <int MODE>
-int launch_size(int tx_size, const RdoArgs& a, hipStream_t s) {
-  if constexpr (MODE <= 1 || MODE == 3) {
-    switch (tx_size) {
-      case 4: launch_rdo<64, 64, MODE>(a, s); return 0;
-      case 11: launch_rdo<32, 64, MODE>(a, s); return 0;
-      case 12: launch_rdo<64, 32, MODE>(a, s); return 0;
-      case 17: launch_rdo<16, 64, MODE>(a, s); return 0;
-      case 18: launch_rdo<64, 16, MODE>(a, s); return 0;
-      default: break;
-    }
-  }
-  if constexpr (MODE >= 1) {
-    switch (tx_size) {
-      case 0: launch_rdo<4, 4, MODE>(a, s); return 0;
-      case 1: launch_rdo<8, 8, MODE>(a, s); return 0;
-      case 2: launch_rdo<16, 16, MODE>(a, s); return 0;
-      case 3: launch_rdo<32, 32, MODE>(a, s); return 0;
-      case 5: launch_rdo<4, 8, MODE>(a, s); return 0;
-      case 6: launch_rdo<8, 4, MODE>(a, s); return 0;
-      case 7: launch_rdo<8, 16, MODE>(a, s); return 0;
-      case 8: launch_rdo<16, 8, MODE>(a, s); return 0;
-      case 9: launch_rdo<16, 32, MODE>(a, s); return 0;
-      case 10: launch_rdo<32, 16, MODE>(a, s); return 0;
-      case 13: launch_rdo<4, 16, MODE>(a, s); return 0;
-      case 14: launch_rdo<16, 4, MODE>(a, s); return 0;
-      case 15: launch_rdo<8, 32, MODE>(a, s); return 0;
-      case 16: launch_rdo<32, 8, MODE>(a, s); return 0;
-      default: break;
-    }
-  }
-  return -2;
-}
 
 int fill_types(RdoArgs& a, int tx_size, uint32_t type_mask) {
   a.ntypes = 0;
@@ -757,7 +64,7 @@ int txq_plane_64(const int16_t* residual, int stride, int width, int height, int
   a.dqcoeff = dqcoeff;
   a.eob = eob;
   a.coeff = coeff;
-  return launch_size<0>(tx_size, a, s);
+  return rdo_launch_m0(tx_size, a, s);
 }
 
 // 64-point sizes with pixel-domain distortion (one candidate type: DCT_DCT):
@@ -807,16 +114,16 @@ int rdo_plane(const uint16_t* src, const uint16_t* pred, int stride, int width, 
     for (int t = 0; t < 16; ++t) a.tx_type_cost[t] = rate->tx_type_costs ? rate->tx_type_costs[t] : 0;
     a.nz_wlt = txw < txh;
     a.nz_wgt = txw > txh;
-    return launch_size<3>(tx_size, a, s);
+    return rdo_launch_m3(tx_size, a, s);
   }
   if (px) {
     if (W > 32 || H > 32) {
       if (block_mask || block_map) return -6;  // single-type path
       return rdo_plane_px64(a, tx_size, width, height, s);
     }
-    return launch_size<2>(tx_size, a, s);
+    return rdo_launch_m2(tx_size, a, s);
   }
-  return launch_size<1>(tx_size, a, s);
+  return rdo_launch_m1(tx_size, a, s);
 }
 
 // ---------------------------------------------------------------------------
@@ -1047,7 +354,7 @@ thread_local StreamScratch t_px_plane[19], t_px_jobs[19];
 
 int rdo_plane_px64(RdoArgs& a, int tx_size, int width, int height, hipStream_t s) {
   if (a.ntypes != 1) return -6;  // 64-point sizes have one candidate type
-  int rc = launch_size<1>(tx_size, a, s);
+  int rc = rdo_launch_m1(tx_size, a, s);
   if (rc || a.nblocks == 0) return rc;
   const int W = tx_w(tx_size), H = tx_h(tx_size);
   uint16_t* plane = (uint16_t*)t_px_plane[tx_size].acquire(
