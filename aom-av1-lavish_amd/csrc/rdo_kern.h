@@ -103,6 +103,25 @@ struct RTile {
 
 __device__ __forceinline__ int get_msb(uint32_t n) { return 31 - __builtin_clz(n); }
 
+// Waves per tile of the split form of the TX-domain decision (mode 1): the
+// types of a block are split by vertical 1-D kind (one column pass each)
+// over up to this many waves of one workgroup, which then pick each block's
+// winner across waves (tx_search.c:2246's first type of strictly lowest
+// cost, in search order).  The sizes' valid types give at most 4 kinds
+// (<= 16 points), 2 (32 points: DCT_DCT, IDTX) or 1 (64 points: DCT_DCT).
+// A launch takes the split form only when its grid would leave the SIMDs
+// short of waves (small rectangles: the C5 shard's rows and tail segments),
+// where a wave's lifetime -- every type of its blocks in sequence -- is the
+// kernel's duration; a full frame has waves enough and keeps one wave per
+// tile (measured: the split form is slower there, C4 0.81 -> 1.08 ms).
+template <int W, int H, int MODE, bool SPLIT>
+constexpr int rdo_nvmax() {
+  if (!SPLIT || MODE != 1) return 1;
+  constexpr int M = W > H ? W : H;
+  return M >= 64 ? 1 : (M == 32 ? 2 : 4);
+}
+constexpr int kRdoSplitTiles = 2048;  // below this many tiles a launch splits
+
 // Per-tile LDS of the pixel-domain mode (MODE 2): the prediction pixels, the
 // inverse transform's transposition buffer, and per-block sums.
 template <int W, int H>
@@ -115,10 +134,10 @@ struct PxLds {
   uint64_t psse[P]; // this type's sum of (src - recon)^2
 };
 
-template <int W, int H, int MODE, bool FAST, int QK, bool HBD, int BDI>
+template <int W, int H, int MODE, bool FAST, int QK, bool HBD, int BDI, int NVM>
 __device__ __forceinline__ void rdo_types(const RdoArgs& a, const int32_t (&res)[RTile<W, H>::CPT][H],
-                                          int32_t* t1, int32_t* t2, int32_t* tb, PxLds<W, H>* px,
-                                          int lane, int blk0, int nvalid) {
+                                          int32_t* t1, int32_t* t2, int32_t* tb0, PxLds<W, H>* px,
+                                          int lane, int blk0, int nvalid, int wave, int nv) {
   using C = TxCfg<W, H>;
   using T = RTile<W, H>;
   using B = Bd<BDI>;
@@ -126,6 +145,7 @@ __device__ __forceinline__ void rdo_types(const RdoArgs& a, const int32_t (&res)
   constexpr int LS = C::log_scale;
   constexpr bool DEC = MODE >= 1;  // decision modes (1: TX-domain, 2: pixel-domain distortion)
   constexpr bool RATE = MODE == 3;  // TX-domain distortion, coefficient rate
+  int32_t* const tb = tb0 + wave * T::T2;  // this wave's winners' coefficients
   // per (row-pass slot k) running best of the block that slot belongs to
   int64_t best_rd[T::RPT], best_dist[T::RPT], best_sse[T::RPT];
   int best_type[T::RPT], best_eob[T::RPT], best_rate[T::RPT], best_satd[T::RPT];
@@ -142,7 +162,7 @@ __device__ __forceinline__ void rdo_types(const RdoArgs& a, const int32_t (&res)
   __shared__ uint8_t s_rank[T::P][16];
   __shared__ uint16_t s_ok[T::P];
   if constexpr (DEC) {
-    if (lane < T::P) {
+    if ((NVM > 1 ? (int)threadIdx.x : lane) < T::P) {  // (wave 0 for the workgroup)
       uint32_t ok = 0xFFFFu;
       if (lane < nvalid) {
         const int blk = blk0 + lane;
@@ -167,17 +187,23 @@ __device__ __forceinline__ void rdo_types(const RdoArgs& a, const int32_t (&res)
       }
       s_ok[lane] = (uint16_t)ok;
     }
-    wave_sync();
+    if constexpr (NVM > 1) __syncthreads();
+    else wave_sync();
   }
   // MODE 3: the cost tables
   __shared__ int32_t s_cc[RATE ? cc::kTabCells : 1];
-  if constexpr (RATE) {
+  if constexpr (RATE) {  // (mode 3: one wave per tile)
     for (int i = lane; i < cc::kCostCells; i += 64) s_cc[i] = a.cc_cost[i];
     if (lane < cc::kEobCells) s_cc[cc::kCostCells + lane] = a.cc_eob[lane];
     wave_sync();
   }
 
+  int grp = -1;  // vertical-kind group of order[oi]; group g runs on wave g % nv
   for (int oi = 0; oi < a.ntypes; ++oi) {
+    if constexpr (NVM > 1) {
+      grp += __builtin_amdgcn_readfirstlane(a.newcol[oi]);
+      if (grp % nv != wave) continue;
+    }
     const int ti = __builtin_amdgcn_readfirstlane(a.order[oi]);
     const int t = __builtin_amdgcn_readfirstlane(a.types[ti]);
     const int vt = (kVtxPacked >> (2 * t)) & 3, ht = (kHtxPacked >> (2 * t)) & 3;
@@ -496,7 +522,7 @@ __device__ __forceinline__ void rdo_types(const RdoArgs& a, const int32_t (&res)
     }
   }
 
-  if constexpr (DEC) {
+  if constexpr (DEC && NVM == 1) {
     // decision records (one lane per block) and the winner's coefficients.
     // A block none of whose allowed types is in the evaluated set (possible
     // only with caller masks) has no candidate: record best_type
@@ -526,6 +552,81 @@ __device__ __forceinline__ void rdo_types(const RdoArgs& a, const int32_t (&res)
     for (int i = lane * 4; i < total; i += 64 * 4) {
       v4i q4 = *reinterpret_cast<const v4i*>(&tb[i]);
       if (s_dead[i / NC]) q4 = v4i{0, 0, 0, 0};
+      __builtin_nontemporal_store(q4, reinterpret_cast<v4i*>(&a.qcoeff[gbase + i]));
+      const int rc0 = i % NC;
+      v4i d4;
+      d4.x = dequant_one<LS>(q4.x, rc0 != 0, a.qp);
+      d4.y = dequant_one<LS>(q4.y, 1, a.qp);
+      d4.z = dequant_one<LS>(q4.z, 1, a.qp);
+      d4.w = dequant_one<LS>(q4.w, 1, a.qp);
+      __builtin_nontemporal_store(d4, reinterpret_cast<v4i*>(&a.dqcoeff[gbase + i]));
+    }
+  }
+  if constexpr (DEC && NVM > 1) {
+    // decision records (one lane per block) and the winner's coefficients.
+    // A block none of whose allowed types is in the evaluated set (possible
+    // only with caller masks) has no candidate: record best_type
+    // TX_TYPE_INVALID (255), eob 0, rdcost INT64_MAX, zero coefficients.
+    // With the types over nv waves, each block's winner is the lowest
+    // (rdcost, search rank) over the waves' bests: the sequential scan's
+    // first type of strictly lowest cost, as every rank is distinct.
+    __shared__ uint8_t s_win[T::P];  // winning wave per block, 255: none
+    __shared__ int64_t s_brd[NVM][T::P];
+    __shared__ uint8_t s_brk[NVM][T::P];
+    {
+#pragma unroll
+      for (int k = 0; k < T::RPT; ++k) {
+        const int j = k * 64 + lane;
+        const int b = j / KH, r = j % KH;
+        if (b < T::P && r == 0) {
+          s_brd[wave][b] = best_rd[k];
+          s_brk[wave][b] = best_rd[k] == INT64_MAX ? 255 : s_rank[b][best_type[k]];
+        }
+      }
+      __syncthreads();
+    }
+#pragma unroll
+    for (int k = 0; k < T::RPT; ++k) {
+      const int j = k * 64 + lane;
+      const int b = j / KH, r = j % KH;
+      if (b < T::P && b < nvalid && r == 0) {
+        int win = 0;
+        int64_t wrd = best_rd[k];
+        {
+          int wrk = 256;
+          wrd = INT64_MAX;
+          for (int q = 0; q < nv; ++q) {
+            const int64_t rd = s_brd[q][b];
+            const int rk = s_brk[q][b];
+            if (rd < wrd || (rd == wrd && rk < wrk)) {
+              wrd = rd;
+              wrk = rk;
+              win = q;
+            }
+          }
+        }
+        const bool dead = wrd == INT64_MAX;
+        if (win == wave) {  // (a dead block: wave 0 writes its record)
+          LavishRdoBlock o;
+          o.best_type = dead ? 255 : best_type[k];
+          o.eob = best_eob[k];
+          o.rate = best_rate[k];
+          o.satd = best_satd[k];
+          o.dist = best_dist[k];
+          o.sse = best_sse[k];
+          o.rdcost = best_rd[k];
+          a.out[blk0 + b] = o;
+          s_win[b] = dead ? 255 : (uint8_t)win;
+        }
+      }
+    }
+    __syncthreads();
+    const int total = nvalid * NC;
+    const size_t gbase = (size_t)blk0 * NC;
+    for (int i = (wave * 64 + lane) * 4; i < total; i += nv * 64 * 4) {
+      const int w = s_win[i / NC];
+      v4i q4 = *reinterpret_cast<const v4i*>(&tb0[(w == 255 ? 0 : w) * T::T2 + i]);
+      if (w == 255) q4 = v4i{0, 0, 0, 0};
       __builtin_nontemporal_store(q4, reinterpret_cast<v4i*>(&a.qcoeff[gbase + i]));
       const int rc0 = i % NC;
       v4i d4;
@@ -567,17 +668,26 @@ constexpr int rdo_waves() {
   return W * H >= 512 ? LAVISH_RDO_WV32 : 1;
 }
 
-template <int W, int H, int MODE, int BDI>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(rdo_waves<W, H, MODE>())))
+template <int W, int H, int MODE, int BDI, bool SPLIT = false>
+__global__ __launch_bounds__(64 * (rdo_nvmax<W, H, MODE, SPLIT>()))
+__attribute__((amdgpu_waves_per_eu(rdo_waves<W, H, MODE>())))
 void rdo_kernel(RdoArgs a) {
   using T = RTile<W, H>;
-  __shared__ int32_t t1[T::T1];
+  constexpr int NVM = rdo_nvmax<W, H, MODE, SPLIT>();
+  __shared__ int32_t t1s[NVM * T::T1];
   __shared__ __attribute__((aligned(16))) int32_t t2[MODE == 0 ? T::T2 : 4];
-  __shared__ __attribute__((aligned(16))) int32_t tb[MODE >= 1 ? T::T2 : 4];
+  __shared__ __attribute__((aligned(16))) int32_t tb[MODE >= 1 ? NVM * T::T2 : 4];
   __shared__ typename std::conditional<MODE == 2, PxLds<W, H>, int>::type pxs;
   PxLds<W, H>* px = MODE == 2 ? reinterpret_cast<PxLds<W, H>*>(&pxs) : nullptr;
 
-  const int lane = threadIdx.x;
+  // NVM > 1: the workgroup's waves share one tile, each a share of the types
+  // (threadIdx.x & 63 for the lane made the compiler spill ~2x more in
+  // these register-bound kernels; the mbcnt lane id does not)
+  const int lane = NVM > 1 ? __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u))
+                           : (int)threadIdx.x;
+  const int wave = NVM > 1 ? __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) : 0;
+  const int nv = NVM > 1 ? (int)(blockDim.x >> 6) : 1;
+  int32_t* const t1 = t1s + wave * T::T1;
   const int blk0 = blockIdx.x * T::P;
   if (blk0 >= a.nblocks) return;
   const int nvalid = min(T::P, a.nblocks - blk0);
@@ -628,14 +738,14 @@ void rdo_kernel(RdoArgs a) {
   const bool fast = __builtin_amdgcn_ballot_w64(amax > kFastResidualMax) == 0;
   if constexpr (MODE >= 1) {
     if (fast)
-      rdo_types<W, H, MODE, true, LAVISH_QUANT_FP, true, BDI>(a, res, t1, t2, tb, px, lane, blk0,
-                                                              nvalid);
+      rdo_types<W, H, MODE, true, LAVISH_QUANT_FP, true, BDI, NVM>(a, res, t1, t2, tb, px, lane,
+                                                                   blk0, nvalid, wave, nv);
     else
-      rdo_types<W, H, MODE, false, LAVISH_QUANT_FP, true, BDI>(a, res, t1, t2, tb, px, lane, blk0,
-                                                               nvalid);
+      rdo_types<W, H, MODE, false, LAVISH_QUANT_FP, true, BDI, NVM>(a, res, t1, t2, tb, px, lane,
+                                                                    blk0, nvalid, wave, nv);
   } else {
 #define LAVISH_RDO_RUN(F, Q, HB) \
-  rdo_types<W, H, 0, F, Q, HB, 0>(a, res, t1, t2, tb, px, lane, blk0, nvalid)
+  rdo_types<W, H, 0, F, Q, HB, 0, 1>(a, res, t1, t2, tb, px, lane, blk0, nvalid, 0, 1)
     if (a.quant_kind == LAVISH_QUANT_NONE) {
       if (fast) LAVISH_RDO_RUN(true, LAVISH_QUANT_NONE, false);
       else LAVISH_RDO_RUN(false, LAVISH_QUANT_NONE, false);
@@ -664,6 +774,19 @@ template <int W, int H, int MODE>
 void launch_rdo(const RdoArgs& a, hipStream_t s) {
   const int grid = (a.nblocks + RTile<W, H>::P - 1) / RTile<W, H>::P;
   if (grid == 0) return;
+  // split form (mode 1, small grids): one wave per vertical-kind group of
+  // the mask, at most NVM
+  int groups = 0;
+  for (int i = 0; i < a.ntypes; ++i) groups += a.newcol[i];
+  constexpr int NVM = rdo_nvmax<W, H, MODE, true>();
+  const int nv = groups < NVM ? groups : NVM;
+  if constexpr (NVM > 1) {
+    if (nv > 1 && grid < kRdoSplitTiles) {
+      hipLaunchKernelGGL((rdo_kernel<W, H, MODE, 0, true>), dim3(grid), dim3(64 * nv), 0, s, a);
+      LAVISH_CHECK(hipGetLastError());
+      return;
+    }
+  }
   if constexpr (MODE == 2) {
     if (a.bd == 8)
       hipLaunchKernelGGL((rdo_kernel<W, H, 2, 0>), dim3(grid), dim3(64), 0, s, a);

@@ -123,10 +123,16 @@ def _gather_rects(local, rects, full, group, async_op):
     return finish
 
 
-def sharded_frame(height, width, rank, world, process_rect, group=None, like=None):
+def sharded_frame(height, width, rank, world, process_rect, group=None, like=None,
+                  streams=None):
     """The band form: run process_rect on this rank's band, start its
     all-gather asynchronously, run the tail segment, gather the tails, and
-    return the whole reconstructed frame (identical on every rank)."""
+    return the whole reconstructed frame (identical on every rank).
+    streams (device work, optional): two streams; the band and its gather go
+    on the first, the tail and its gather on the second, so the two parts
+    (independent SBs) compute side by side -- the tail segment's few waves
+    would otherwise run after the band's kernels; the caller's stream then
+    waits for both."""
     import torch
     parts = partition(height, width, world)
     band, tail = parts[rank]
@@ -134,17 +140,40 @@ def sharded_frame(height, width, rank, world, process_rect, group=None, like=Non
         return process_rect(*band)
     full = None
     fin = []
+    caller = torch.cuda.current_stream() if streams else None
+    if streams:
+        start = torch.cuda.Event()
+        start.record(caller)
     for phase, rect in enumerate((band, tail)):
         rects = [p[phase] for p in parts]
         if all(r is None for r in rects):
             continue
-        local = process_rect(*rect) if rect is not None else None
-        if full is None:
-            ref = local if local is not None else like
-            full = torch.empty((height, width), dtype=ref.dtype, device=ref.device)
-        fin.append(_gather_rects(local, rects, full, group, async_op=True))
-    for f in fin:
-        f()
+        if streams:
+            st = streams[phase]
+            st.wait_event(start)
+            with torch.cuda.stream(st):
+                local = process_rect(*rect) if rect is not None else None
+                if full is None:
+                    ref = local if local is not None else like
+                    with torch.cuda.stream(caller):  # allocated on the caller's stream
+                        full = torch.empty((height, width), dtype=ref.dtype, device=ref.device)
+                    st.wait_stream(caller)
+                fin.append(_gather_rects(local, rects, full, group, async_op=True))
+        else:
+            local = process_rect(*rect) if rect is not None else None
+            if full is None:
+                ref = local if local is not None else like
+                full = torch.empty((height, width), dtype=ref.dtype, device=ref.device)
+            fin.append(_gather_rects(local, rects, full, group, async_op=True))
+    if streams:
+        for phase, f in enumerate(fin):
+            with torch.cuda.stream(streams[phase]):
+                f()
+        for st in streams:
+            caller.wait_stream(st)
+    else:
+        for f in fin:
+            f()
     return full
 
 

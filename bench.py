@@ -427,12 +427,26 @@ def c5_leg(L, steps, warmup, rdmult, qindex, world, rank, W=3840, H=2160, graphs
             dist.all_reduce(mx, op=dist.ReduceOp.MAX)
         return el / n * 1e3, float(mx.item()) / n * 1e3
 
-    def frame_step():
-        shard.sharded_frame(H, W, rank, world, proc)
+    streams = [torch.cuda.Stream(), torch.cuda.Stream()] if graphs else None
 
-    def compute_only():
-        for r in mine:
-            proc(*r)
+    def frame_step():
+        shard.sharded_frame(H, W, rank, world, proc, streams=streams)
+
+    caller = torch.cuda.current_stream()
+
+    def compute_only():  # the rank's band and tail side by side, as in frame_step
+        if streams is None:
+            for r in mine:
+                proc(*r)
+            return
+        ev = torch.cuda.Event()
+        ev.record(caller)
+        for st, r in zip(streams, mine):
+            st.wait_event(ev)
+            with torch.cuda.stream(st):
+                proc(*r)
+        for st in streams:
+            caller.wait_stream(st)
 
     # the exchange alone: each phase's all-gather of equal zero-padded parts
     gathers = []
@@ -489,7 +503,8 @@ def c5_leg(L, steps, warmup, rdmult, qindex, world, rank, W=3840, H=2160, graphs
 
 def c5_emulate(H, W, proc, worlds, steps, warmup, frame_ms):
     """On one GPU, rank g's share of the band form for each world size G:
-    its partition() rectangles (band, then tail segment) run back to back
+    its partition() rectangles (band and tail segment side by side on two
+    streams, as sharded_frame runs them) replayed as captured graphs
     with nothing else on the device, timed with HIP events -- the
     compute-only time of that rank at G GPUs (no exchange, no contention
     from other ranks: each rank owns its GPU).  Reports every rank's time,
@@ -497,22 +512,32 @@ def c5_emulate(H, W, proc, worlds, steps, warmup, frame_ms):
     import torch
     import lavish_dsp.shard as shard
     stream = torch.cuda.current_stream()
+    side = [torch.cuda.Stream(), torch.cuda.Stream()]
     out = {}
+
+    def rank_step(rects):  # band and tail side by side (shard.sharded_frame's streams)
+        ev = torch.cuda.Event()
+        ev.record(stream)
+        for st, r in zip(side, rects):
+            st.wait_event(ev)
+            with torch.cuda.stream(st):
+                proc(*r)
+        for st in side:
+            stream.wait_stream(st)
+
     for G in worlds:
         parts = shard.partition(H, W, G)
         per = []
         for g in range(G):
             rects = [r for r in parts[g] if r is not None]
             for _ in range(warmup):
-                for r in rects:
-                    proc(*r)
+                rank_step(rects)
             torch.cuda.synchronize()
             ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
                   for _ in range(steps)]
             for a, b in ev:
                 a.record(stream)
-                for r in rects:
-                    proc(*r)
+                rank_step(rects)
                 b.record(stream)
             torch.cuda.synchronize()
             per.append(sum(a.elapsed_time(b) for a, b in ev) / steps)
@@ -564,8 +589,10 @@ def main_c4(args):
                 return shard.wavefront_frame(H, W, rank, world, proc, chunks=args.c5_chunks,
                                              p2p_group=p2p, out=frame_out, streams=wstreams)
         else:
+            bstreams = None if args.c5_no_graphs else [torch.cuda.Stream(), torch.cuda.Stream()]
+
             def step():
-                return shard.sharded_frame(H, W, rank, world, proc)
+                return shard.sharded_frame(H, W, rank, world, proc, streams=bstreams)
     else:
         fr = L.RdoFrame(src)
 
