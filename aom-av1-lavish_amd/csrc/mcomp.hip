@@ -27,6 +27,7 @@
 #include <atomic>
 
 #include "lavish_internal.h"
+#include "txq_dev.h"
 
 namespace lavish {
 namespace {
@@ -2252,6 +2253,51 @@ __global__ __launch_bounds__(64 * WPG, LAVISH_LJ_WAVES) void diamond_lj_kernel(
                   cost_lists, v, nvwg);
 }
 
+// ---------------------------------------------------------------------------
+// C2 + C3 in one launch (lavish_txq_frame_search): the <= 16-point class of
+// lavish_txq_frame (txq_multi_body<0>) and the 16x16 DIAMOND search's job
+// groups (lj_group) in one grid.  The dispatch order -- units of 8
+// consecutive workgroups, so a unit keeps the XCD congruence both mappings
+// rely on -- places a search unit every `every` units from the start and the
+// transform workgroups around them: the long-lived search waves (a dependent
+// chain of L2 round trips per job) take a bounded share of the CU slots while
+// the transform's write stream keeps the rest, instead of two streams'
+// workgroups racing for the slots.  VGPRs: the larger of the two bodies
+// (both 115), LDS: the class's 37 KB + the search's result slots.
+struct LjLaunch {
+  const uint8_t* src;
+  int ss;
+  const uint8_t* ref;
+  int rs;
+  LavishRefTiles tiles;
+  const Job* jobs;
+  int njobs, step_param;
+  LavishMvCostParams cost;
+  const int32_t* dec;
+  int skip;
+  LavishDiamondResult* out;
+  int32_t* cost_lists;
+  int nvwg;   // the search's virtual workgroups (a multiple of 8)
+  int units;  // nvwg / 8
+  int every;  // a search unit every `every` units of the dispatch order
+};
+
+__global__ __launch_bounds__(256, 4) void txq_search_kernel(TxqDispatch d, TxqArgs a0, TxqArgs a1,
+                                                            TxqArgs a2, TxqArgs a3, TxqArgs a4,
+                                                            TxqArgs a5, TxqArgs a6, TxqArgs a7,
+                                                            TxqArgs a8, LjLaunch c) {
+  __shared__ __attribute__((aligned(16))) char lds[class_lds(0)];
+  const int u = blockIdx.x >> 3, x = blockIdx.x & 7;
+  const int k = u / c.every;
+  if (u - k * c.every == 0 && k < c.units) {
+    lj_group<4>(c.src, c.ss, c.ref, c.rs, c.tiles, c.jobs, c.njobs, c.step_param, c.cost, c.dec,
+                c.skip, c.out, c.cost_lists, k * 8 + x, c.nvwg);
+    return;
+  }
+  const int before = min((u + c.every - 1) / c.every, c.units);  // search units in 0 .. u - 1
+  txq_multi_body<0>(d, a0, a1, a2, a3, a4, a5, a6, a7, a8, (u - before) * 8 + x, lds);
+}
+
 // the decimated entropy cost tables of mvsad_rate_dec
 __global__ __launch_bounds__(256) void mvcost_dec_kernel(const int32_t* __restrict__ mvcost0,
                                                          const int32_t* __restrict__ mvcost1,
@@ -2530,6 +2576,71 @@ extern "C" int lavish_full_pixel_search_batch_tiled(
   return fullpel_batch(src, src_stride, ref, ref_stride, w, h, jobs, njobs, search_method,
                        step_param, cost, use_downsampled_sad, out, cost_lists,
                        (hipStream_t)stream, tiles);
+}
+
+extern "C" int lavish_txq_frame_search(
+    const int16_t* residual, int stride, int width, int height, uint32_t size_mask,
+    const uint32_t* type_masks, int bit_depth, int quant_kind, const LavishQuantParams* qp,
+    int32_t* const* qcoeff, int32_t* const* dqcoeff, uint16_t* const* eob, const uint8_t* src,
+    int src_stride, const uint8_t* ref, int ref_stride, const LavishRefTiles* tiles,
+    const LavishDiamondJob* jobs, int njobs, int step_param, const LavishMvCostParams* cost,
+    int use_downsampled_sad, LavishDiamondResult* out, int32_t* cost_lists, int every,
+    void* stream) {
+  const hipStream_t s = (hipStream_t)stream;
+  if (every < 1) return -6;
+  if (tiles == nullptr || tiles->data == nullptr || tiles->stride != ref_stride) return -5;
+  if (step_param < 0 || step_param >= kMaxSteps) return -1;
+  if (cost == nullptr || cost->mv_cost_type < 0 || cost->mv_cost_type > 4) return -2;
+  if (cost->mv_cost_type == 0 &&
+      (cost->mvjcost == nullptr || cost->mvcost[0] == nullptr || cost->mvcost[1] == nullptr))
+    return -2;
+  // C2: every requested size outside the <= 16-point class as lavish_txq_frame
+  // runs it (the 64-point sizes, then the 32-point class's launch)
+  uint32_t cls0 = 0;
+  for (int t = 0; t < 19; ++t)
+    if (((size_mask >> t) & 1) && tx_w(t) <= 32 && tx_h(t) <= 32 && !txq_class(t)) cls0 |= 1u << t;
+  int rc = 0;
+  if (size_mask & ~cls0) {
+    rc = txq_frame(residual, stride, width, height, size_mask & ~cls0, type_masks, bit_depth,
+                   quant_kind, qp, qcoeff, dqcoeff, eob, s);
+    if (rc) return rc;
+  }
+  TxqMulti m;
+  int g = 0;
+  rc = txq_frame_plan(residual, stride, width, height, cls0, type_masks, bit_depth, quant_kind, qp,
+                      qcoeff, dqcoeff, eob, 0, m, g);
+  if (rc) return rc;
+  LjLaunch c{};
+  c.src = src;
+  c.ss = src_stride;
+  c.ref = ref;
+  c.rs = ref_stride;
+  c.tiles = *tiles;
+  c.jobs = (const Job*)jobs;
+  c.njobs = njobs > 0 ? njobs : 0;
+  c.step_param = step_param;
+  c.cost = *cost;
+  c.skip = use_downsampled_sad;
+  c.out = out;
+  c.cost_lists = cost_lists;
+  const int waves = (c.njobs + kLjJobs - 1) / kLjJobs;
+  c.nvwg = (((waves + 3) / 4) + 7) & ~7;
+  c.units = c.nvwg / 8;
+  if (c.units > 0 && cost->mv_cost_type == 0) {
+    c.dec = (const int32_t*)t_mvdec.acquire(2 * kMvDecN * sizeof(int32_t), s);
+    hipLaunchKernelGGL(mvcost_dec_kernel, dim3((2 * kMvDecN + 255) / 256), dim3(256), 0, s,
+                       cost->mvcost[0], cost->mvcost[1], (int32_t*)c.dec);
+  }
+  // the search units must all lie inside the grid: units * every may not
+  // pass the grid's units (clamp the spacing)
+  const int u2 = g / 8, ut = u2 + c.units;
+  c.every = c.units > 1 ? min(every, max(1, (ut - 1) / (c.units - 1))) : every;
+  if (ut > 0)
+    hipLaunchKernelGGL(txq_search_kernel, dim3(ut * 8), dim3(256), 0, s, m.d, m.a[0], m.a[1],
+                       m.a[2], m.a[3], m.a[4], m.a[5], m.a[6], m.a[7], m.a[8], c);
+  LAVISH_CHECK(hipGetLastError());
+  if (c.dec) t_mvdec.release(s);
+  return 0;
 }
 
 extern "C" int lavish_diamond_search_batch(const uint8_t* src, int src_stride, const uint8_t* ref,

@@ -290,6 +290,41 @@ def full_pixel_search_batch(src, ref, w, h, jobs, cost, method="diamond", step_p
     return out, (cost_lists if cost_list else None)
 
 
+_lib.lavish_txq_frame_search.argtypes = [
+    _vp, _i32, _i32, _i32, ctypes.c_uint32, _vp, _i32, _i32, _vp, _vp, _vp, _vp,
+    _vp, _i32, _vp, _i32, ctypes.POINTER(RefTilesDesc), _vp, _i32, _i32,
+    ctypes.POINTER(MvCostParams), _i32, _vp, _vp, _i32, _vp]
+_lib.lavish_txq_frame_search.restype = _i32
+
+
+def txq_frame_search(residual, frame_out, qp, src, ref, jobs, cost, tiles, out, cost_lists,
+                     every, step_param=0, use_downsampled_sad=True, bit_depth=8,
+                     quant_kind=None, stream=None):
+    """lavish_txq_frame_search: lavish_txq_frame over `frame_out`'s sizes and
+    the 16x16 DIAMOND full_pixel_search_batch (tiled references, cost lists
+    into `cost_lists` when given) in one launch, a search unit every `every`
+    units of the dispatch order.  The tiles must already be built."""
+    import torch
+    import lavish_dsp as L
+    assert residual.dtype == torch.int16 and residual.stride(1) == 1
+    assert src.dtype == torch.uint8 and ref.dtype == torch.uint8 and src.is_contiguous()
+    assert tiles.ref.data_ptr() == ref.data_ptr() and tiles.stride == src.stride(0)
+    H, W = residual.shape
+    nj = jobs.numel() // JOB_DTYPE.itemsize
+    qk = L.QUANT_FP if quant_kind is None else quant_kind
+    rc = _lib.lavish_txq_frame_search(
+        _vp(residual.data_ptr()), residual.stride(0), W, H, frame_out.size_mask, frame_out.tm,
+        bit_depth, qk, ctypes.byref(qp), frame_out.q, frame_out.dq, frame_out.eob,
+        _vp(src.data_ptr()), src.stride(0), _vp(ref.data_ptr()), src.stride(0),
+        ctypes.byref(tiles.desc), _vp(jobs.data_ptr()), nj, step_param, ctypes.byref(cost),
+        int(use_downsampled_sad), _vp(out.data_ptr()),
+        _vp(cost_lists.data_ptr()) if cost_lists is not None else None, int(every),
+        _stream_ptr(stream))
+    if rc != 0:
+        raise ValueError("lavish_txq_frame_search rejected its arguments (rc=%d)" % rc)
+    return frame_out.outs, out
+
+
 def results_numpy(out):
     return out.cpu().numpy().view(RESULT_DTYPE)
 

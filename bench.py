@@ -96,6 +96,13 @@ def parse():
                     help="skip the c4 sub-object (4K 10-bit RDO step) of the default line")
     ap.add_argument("--c3-wg-cap", type=int, default=C3_WG_CAP,
                     help="workgroups of the C3 search when it runs beside C2 (0: no cap)")
+    ap.add_argument("--c3-mode", choices=("fused", "streams"), default=C3_MODE,
+                    help="how C3 runs beside C2: one launch with the search's job groups "
+                         "interleaved among C2's workgroups (lavish_txq_frame_search), or C3 on a "
+                         "second stream in at most --c3-wg-cap workgroups")
+    ap.add_argument("--c3-every", type=int, default=C3_EVERY,
+                    help="fused: a search unit (8 workgroups) every this many units of the "
+                         "dispatch order")
     ap.add_argument("--c2-priority", type=int, default=0,
                     help="1: the C2 leg on a high-priority stream beside C3")
     ap.add_argument("--serial", action="store_true",
@@ -155,6 +162,8 @@ C3_COST = 0     # MV_COST_ENTROPY (the RDO path's x->mv_cost_type)
 C3_SKIP = True  # use_downsampled_sad (>= 720p, speed_features.c:205-209)
 C3_CL = True    # cost list: subpel_search_method != SUBPEL_TREE (cond_cost_list)
 C3_WG_CAP = 512  # C3's workgroups beside C2 (profiles/r04_v11_*: the step's best)
+C3_MODE = "fused"  # C2 + C3 in one launch (lavish_txq_frame_search)
+C3_EVERY = 10      # fused: a search unit every 10 units of the dispatch order
 # sub-pixel refinement after the full-pel search (c3sub): SUBPEL_TREE_PRUNED_MORE
 # (speed >= 4), subpel_force_stop EIGHTH_PEL, iters_per_step 1 (speed >= 2),
 # allow_high_precision_mv = qindex < HIGH_PRECISION_MV_QTHRESH (128)
@@ -1692,7 +1701,8 @@ class RdoStep:
     `c3_wg_cap` workgroups (0: uncapped; alone, C3 always runs uncapped)."""
 
     def __init__(self, workload="rdo", width=1920, height=1080, refs=7, border=160, qindex=128,
-                 rdmult=2000, seed=1234, serial=False, c3_wg_cap=C3_WG_CAP):
+                 rdmult=2000, seed=1234, serial=False, c3_wg_cap=C3_WG_CAP, c3_mode=C3_MODE,
+                 c3_every=C3_EVERY):
         import torch
         import lavish_dsp as L
         import lavish_dsp.motion as M
@@ -1703,7 +1713,10 @@ class RdoStep:
         self.do_c3 = workload in ("rdo", "c3", "c3sub")
         self.do_sub = workload == "c3sub"
         self.overlap = self.do_c2 and self.do_c3 and not serial
+        # fused: the overlapped step as one launch (C3 without the sub-pel leg)
+        self.fused = self.overlap and c3_mode == "fused" and not self.do_sub
         self.c3_wg_cap = c3_wg_cap
+        self.c3_every = c3_every
         self.stream = torch.cuda.current_stream()
         # C2 input: residual plane (each rank its own frame)
         self.res_np = synth.residual_plane(W, H, 8, seed=seed)
@@ -1764,6 +1777,22 @@ class RdoStep:
         side = self.side_stream if ovl else stream
         if ev is not None:
             ev[0].record(stream)
+        if ovl and self.fused:
+            # the tiled references, then C2 + C3 as one grid (both legs' event
+            # pairs bracket the whole launch)
+            if ev is not None:
+                ev[1].record(stream)
+                ev[3].record(stream)
+            self.c3_tiles.build(stream=stream)
+            self.M.txq_frame_search(self.res, self.frame, self.qp, self.tsrc, self.trefs,
+                                    self.tjobs, self.c3_cost, self.c3_tiles, self.c3_out,
+                                    self.c3_cl, self.c3_every, use_downsampled_sad=C3_SKIP,
+                                    stream=stream)
+            if ev is not None:
+                ev[2].record(stream)
+                ev[4].record(stream)
+                ev[5].record(stream)
+            return
         if ovl:  # the legs are independent: C3 (TA / latency bound) beside C2 (HBM writes)
             self.fork.record(stream)
             side.wait_event(self.fork)
@@ -1879,7 +1908,8 @@ def main():
         # a normal one: freed CU slots go to C2's workgroups first
         torch.cuda.set_stream(torch.cuda.Stream(priority=-1))
     R = RdoStep(args.workload, W, H, args.refs, args.border, args.qindex, args.rdmult,
-                seed=1234 + rank, serial=args.serial, c3_wg_cap=args.c3_wg_cap)
+                seed=1234 + rank, serial=args.serial, c3_wg_cap=args.c3_wg_cap,
+                c3_mode=args.c3_mode, c3_every=args.c3_every)
     do_c2, do_c3, do_sub, overlap = R.do_c2, R.do_c3, R.do_sub, R.overlap
     stream, sizes, jobs_np, c3_cost = R.stream, R.sizes, R.jobs_np, R.c3_cost
     step = R.step
@@ -1919,7 +1949,8 @@ def main():
         # the legs share the GPU in the timed region, which stretches each; the
         # per-kernel roofline is taken from a serial pass after it (isolated
         # legs, same inputs), not from the overlapped leg spans
-        legs_overlapped = {"c2_txq_frame": round(c2_ms, 4), "c3_diamond": round(c3_ms, 4)}
+        legs_overlapped = ({"c2_c3_fused_launch": round(c2_ms, 4)} if R.fused else
+                           {"c2_txq_frame": round(c2_ms, 4), "c3_diamond": round(c3_ms, 4)})
         KS = max(5, K // 2)
         evs = [tuple(torch.cuda.Event(enable_timing=True) for _ in range(6)) for _ in range(KS)]
         step(ovl=False)
@@ -1990,9 +2021,11 @@ def main():
                         % (args.workload, W, H, " + ".join(legs), sb),
             "tx_sizes": [L.TX_SIZES[s] for s in sizes] if do_c2 else [],
             "parallelism": "frame-per-rank x%d" % world,
-            "legs": ("C3 on a second stream beside C2 (C3 in at most %d workgroups)"
-                     % args.c3_wg_cap if args.c3_wg_cap else
-                     "C3 on a second stream beside C2") if overlap else "C3 then C2, one stream",
+            "legs": (("C2 + C3 in one launch, a C3 unit of 8 workgroups every %d units "
+                      "(lavish_txq_frame_search)" % args.c3_every) if R.fused else
+                     ("C3 on a second stream beside C2 (C3 in at most %d workgroups)"
+                      % args.c3_wg_cap if args.c3_wg_cap else
+                      "C3 on a second stream beside C2")) if overlap else "C3 then C2, one stream",
         },
         "roofline": roof,
         "legs_ms": {"c2_txq_frame": round(c2_ms, 4), "c3_diamond": round(c3_ms, 4),

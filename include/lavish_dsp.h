@@ -611,6 +611,26 @@ int lavish_full_pixel_search_batch_tiled(const uint8_t *src, int src_stride,
                                          LavishDiamondResult *out,
                                          int32_t *cost_lists, void *stream);
 
+/* C2 and the C3 search in one launch: lavish_txq_frame(residual, ...) and
+ * lavish_full_pixel_search_batch_tiled(src, ..., 16, 16, jobs, njobs,
+ * DIAMOND, ...) with the same results, run as one grid (the 64-point sizes
+ * and the 32-point class of the transform first, as lavish_txq_frame runs
+ * them; then the <= 16-point class's workgroups and the search's job groups
+ * interleaved in the dispatch order, a search unit of 8 workgroups every
+ * `every` units from the start).  The search must be the 16x16 DIAMOND with
+ * a tiled reference copy.  -6: every < 1.  No reference counterpart: the
+ * reference runs the two on the encoder's threads. */
+int lavish_txq_frame_search(const int16_t *residual, int stride, int width, int height,
+                            uint32_t size_mask, const uint32_t *type_masks, int bit_depth,
+                            int quant_kind, const LavishQuantParams *qp,
+                            int32_t *const *qcoeff, int32_t *const *dqcoeff,
+                            uint16_t *const *eob, const uint8_t *src, int src_stride,
+                            const uint8_t *ref, int ref_stride, const LavishRefTiles *tiles,
+                            const LavishDiamondJob *jobs, int njobs, int step_param,
+                            const LavishMvCostParams *cost, int use_downsampled_sad,
+                            LavishDiamondResult *out, int32_t *cost_lists, int every,
+                            void *stream);
+
 /* Process-wide cap on the workgroups of the 16x16 DIAMOND search of
  * lavish_full_pixel_search_batch[_tiled] (rounded up to 8; 0 = no cap, one
  * workgroup per 32 jobs).  A scheduling knob for running the search beside

@@ -3,13 +3,16 @@
 bench.RdoStep is the object main() times: C3 (the DIAMOND full-pel search of
 every 16x16 block x 7 references, downsampled SAD, MV_COST_ENTROPY over the
 default nmv tables, cost lists; av1_full_pixel_search, mcomp.c:1755 ->
-full_pixel_diamond :1479 -> diamond_search_sad :1318-1477) on a side stream in
-at most 512 workgroups (lavish_set_search_workgroup_cap: the search kernel
-strides over virtual workgroups) beside C2 (lavish_txq_frame: every block of
-the 14 TX sizes <= 32x32 x every valid type, tx_search.c:2148-2312 ->
-encodemb.c:295-341) on the caller's stream.  Two consecutive steps run, then
-both legs' outputs are compared with the oracle; the search at workgroup
-caps {8, 64, 512, 0} must give identical results.
+full_pixel_diamond :1479 -> diamond_search_sad :1318-1477) beside C2
+(lavish_txq_frame: every block of the 14 TX sizes <= 32x32 x every valid
+type, tx_search.c:2148-2312 -> encodemb.c:295-341).  The default step runs
+both as one launch (lavish_txq_frame_search: the search's job groups
+interleaved among the transform's workgroups); the "streams" form runs C3 on
+a side stream in at most 512 workgroups (lavish_set_search_workgroup_cap: the
+search kernel strides over virtual workgroups) beside C2 on the caller's
+stream.  Two consecutive steps run, then both legs' outputs are compared
+with the oracle; the search at workgroup caps {8, 64, 512, 0} and the fused
+launch at interleaving strides {1, 3, 10, 40} must give identical results.
 """
 import os
 
@@ -37,9 +40,17 @@ def step():
     import torch
     assert torch.cuda.is_available()
     b = _bench()
-    R = b.RdoStep()  # the bench's defaults: 1080p, 7 refs, qindex 128, cap 512, overlapped
-    assert R.overlap and R.c3_wg_cap == b.C3_WG_CAP == 512
+    R = b.RdoStep()  # the bench's defaults: 1080p, 7 refs, qindex 128, overlapped
+    assert R.overlap and R.fused == (b.C3_MODE == "fused") and R.c3_wg_cap == 512
     return b, R
+
+
+@pytest.fixture(scope="module")
+def c2_expected(step):
+    b, R = step
+    oq = O.build_quant(8, 128)
+    return {s: O.txq_plane(R.res_np, s, R.L.valid_type_mask(s), oq, threads=THREADS)
+            for s in R.sizes}
 
 
 @pytest.fixture(scope="module")
@@ -60,34 +71,64 @@ def _check_c3(R, exp, exp_cl, what):
     return got
 
 
-def test_timed_step_both_legs(step, c3_expected):
-    """Two steps as timed (C3 capped beside C2, two streams), then C3's
-    results and cost lists and every C2 size's qcoeff / dqcoeff / eob."""
-    import torch
-    b, R = step
+def _poison(R):
     R.c3_out.fill_(0x55)
     R.c3_cl.fill_(-7)
     for out in R.frame.outs.values():
         for t in out.values():
             t.fill_(0x33)
-    for _ in range(2):
-        R.step()
-    torch.cuda.synchronize()
-    assert R.L.status()[0] == 0, R.L.status()
-    exp, exp_cl = c3_expected
-    got = _check_c3(R, exp, exp_cl, "overlapped, cap 512")
-    assert (np.abs(got["best_row"]) + np.abs(got["best_col"]) > 0).mean() > 0.5
-    oq = O.build_quant(8, 128)
+
+
+def _check_c2(R, c2_expected, what):
     for s in R.sizes:
-        qc, dq, eob = O.txq_plane(R.res_np, s, R.L.valid_type_mask(s), oq, threads=THREADS)
+        qc, dq, eob = c2_expected[s]
         out = R.frame.outs[s]
         np.testing.assert_array_equal(out["qcoeff"].cpu().numpy(), qc.transpose(1, 0, 2),
-                                      err_msg="size %d qcoeff" % s)
+                                      err_msg="%s: size %d qcoeff" % (what, s))
         np.testing.assert_array_equal(out["dqcoeff"].cpu().numpy(), dq.transpose(1, 0, 2),
-                                      err_msg="size %d dqcoeff" % s)
+                                      err_msg="%s: size %d dqcoeff" % (what, s))
         np.testing.assert_array_equal(out["eob"].cpu().numpy().view(np.uint16), eob.T,
-                                      err_msg="size %d eob" % s)
-        del qc, dq, eob
+                                      err_msg="%s: size %d eob" % (what, s))
+
+
+@pytest.mark.parametrize("mode", ["fused", "streams"])
+def test_timed_step_both_legs(step, c2_expected, c3_expected, mode):
+    """Two steps as timed (fused: one launch; streams: C3 capped beside C2 on
+    two streams), then C3's results and cost lists and every C2 size's
+    qcoeff / dqcoeff / eob."""
+    import torch
+    b, R = step
+    fused = R.fused
+    R.fused = mode == "fused"
+    try:
+        _poison(R)
+        for _ in range(2):
+            R.step()
+        torch.cuda.synchronize()
+    finally:
+        R.fused = fused
+    assert R.L.status()[0] == 0, R.L.status()
+    got = _check_c3(R, *c3_expected, what=mode)
+    assert (np.abs(got["best_row"]) + np.abs(got["best_col"]) > 0).mean() > 0.5
+    _check_c2(R, c2_expected, mode)
+
+
+@pytest.mark.parametrize("every", [1, 3, 10, 40])
+def test_fused_launch_interleave_sweep(step, c2_expected, c3_expected, every):
+    """lavish_txq_frame_search at several interleaving strides (the search's
+    units dispatched every `every` units, clamped into the grid): identical
+    results."""
+    import torch
+    b, R = step
+    _poison(R)
+    R.c3_tiles.build(stream=R.stream)
+    R.M.txq_frame_search(R.res, R.frame, R.qp, R.tsrc, R.trefs, R.tjobs, R.c3_cost, R.c3_tiles,
+                         R.c3_out, R.c3_cl, every, use_downsampled_sad=b.C3_SKIP,
+                         stream=R.stream)
+    torch.cuda.synchronize()
+    assert R.L.status()[0] == 0, R.L.status()
+    _check_c3(R, *c3_expected, what="every %d" % every)
+    _check_c2(R, c2_expected, "every %d" % every)
 
 
 @pytest.mark.parametrize("cap", [8, 64, 512, 0])
