@@ -357,6 +357,43 @@ struct Win {
 __device__ __forceinline__ int site_dr(int i) { return ((0x8858 >> (2 * i)) & 3) - 1; }
 __device__ __forceinline__ int site_dc(int i) { return ((0x2885 >> (2 * i)) & 3) - 1; }
 
+// av1_init_motion_compensation_nstep (mcomp.c:452-494): radius of step st
+// (1, 2, 3, 5, 8, 12, 18, 27, 41, 62, 93, 140, then 210: the radius grows
+// to max((int)(1.5 r + 0.5), r + 1) after each of the first 12 stages) and
+// the step count (NSTEP 15, NSTEP_8PT 16)
+__device__ __forceinline__ int nstep_radius(int st) {
+  constexpr uint32_t kLo[4] = {0x05030201u, 0x1b120c08u, 0x8c5d3e29u, 0xd2d2d2d2u};
+  const int w = st >> 2, b = (st & 3) * 8;
+  const uint32_t v = w == 0 ? kLo[0] : w == 1 ? kLo[1] : w == 2 ? kLo[2] : kLo[3];
+  return (int)((v >> b) & 0xFF);
+}
+// tan_radius = max((int)(0.41 * r), 1) of the 12-point steps (r > 5; in
+// double, as the reference computes it: 3, 4, 7, 11, 16, 25, 38, 57, 86)
+__device__ __forceinline__ int nstep_tan(int st) {
+  const int w = st >> 2, b = (st & 3) * 8;  // (st 0..3: 8-point steps, unused)
+  const uint32_t v = w == 1 ? 0x0b070403u : w == 2 ? 0x39261910u : w == 3 ? 0x56565656u : 0u;
+  return (int)((v >> b) & 0xFF);
+}
+__device__ __forceinline__ int nstep_steps(int level) { return level > 0 ? 16 : 15; }
+// site i + 1 (i = 0..11) at radius r, tangent t: (-r,0) (r,0) (0,-r) (0,r)
+// (-r,-t) (r,t) (-t,r) (t,-r) (-r,t) (r,-t) (t,r) (-t,-r)
+__device__ __forceinline__ void nstep_site(int i, int r, int t, int& dr, int& dc) {
+  // per site: row and column as (sign, r-or-t) codes, 3 bits each: 0 zero,
+  // 1 +r, 2 -r, 3 +t, 4 -t
+  constexpr uint64_t kR = 0x0ull | (2ull << 0) | (1ull << 3) | (0ull << 6) | (0ull << 9) |
+                          (2ull << 12) | (1ull << 15) | (4ull << 18) | (3ull << 21) |
+                          (2ull << 24) | (1ull << 27) | (3ull << 30) | (4ull << 33);
+  constexpr uint64_t kC = 0x0ull | (0ull << 0) | (0ull << 3) | (2ull << 6) | (1ull << 9) |
+                          (4ull << 12) | (3ull << 15) | (1ull << 18) | (2ull << 21) |
+                          (3ull << 24) | (4ull << 27) | (1ull << 30) | (2ull << 33);
+  const int a = (int)((kR >> (3 * i)) & 7), b = (int)((kC >> (3 * i)) & 7);
+  auto val = [&](int code) {
+    return code == 1 ? r : code == 2 ? -r : code == 3 ? t : code == 4 ? -t : 0;
+  };
+  dr = val(a);
+  dc = val(b);
+}
+
 // UA: candidate rows as byte-addressed loads (DIAMOND: its global-memory
 // steps are the large-radius ones) or aligned loads + v_alignbyte (the
 // pattern searches, see load_row_aligned).  TL: candidate rows from the
@@ -649,6 +686,74 @@ struct Search {
     num00 = center;
     return best;
   }
+
+  // diamond_search_sad over the site configuration of
+  // av1_init_motion_compensation_nstep (mcomp.c:452-494; level 0: NSTEP, 15
+  // steps, 12 points once the radius passes 5; level 1: NSTEP_8PT, 16 steps
+  // of 8 points), candidates from global memory.  12 points take two rounds
+  // (sites 1..8, then 9..12); key = cost * 16 + site index, so the minimum
+  // over both rounds is the reference's sequential strict-< scan.  The steps
+  // of an equal radius below an unmoved step are skipped and counted as
+  // centre steps (UPDATE_SEARCH_STEP, mcomp.c:1334-1341).
+  __device__ __forceinline__ uint32_t nstep_diamond(const Ctx& c, int lane, int level, int srow,
+                                                    int scol, int search_step, int& brow,
+                                                    int& bcol, int& num00, int& steps) {
+    const int g = lane >> 3;
+    srow = min(max(srow, c.row_min), c.row_max);
+    scol = min(max(scol, c.col_min), c.col_max);
+    int row = srow, col = scol, off_center = 0, center = 0;
+    if (!have_c0 || c0row != srow || c0col != scol) {
+      c0sad = rdlane(group_sad(c, srow, scol), 0);
+      have_c0 = true;
+      c0row = srow;
+      c0col = scol;
+    }
+    uint32_t best = mvsad_cost(c, row, col) + c0sad;
+    const int tot = nstep_steps(level) - search_step;
+    inwin = false;
+    // one round: site (first + g) of the step at radius rad / tangent tan
+    auto round = [&](int rad, int tan, int first, int cnt) -> uint32_t {
+      const int i = first + g;  // 0-based site index (site i + 1)
+      int dr, dc;
+      nstep_site(i, rad, tan, dr, dc);
+      const int r = row + dr, cc = col + dc;
+      const bool valid = g < cnt && cc >= c.col_min && cc <= c.col_max && r >= c.row_min &&
+                         r <= c.row_max;
+      const MvRate mr = mvsad_rate(c, r, cc);
+      const uint32_t mine = group_sad(c, r, cc, valid, row, col);
+      const uint32_t mvs = mvsad_finish(c, mr, r, cc);
+      return groups_min((((mine + mvs) << 4) | (uint32_t)i) | (valid ? 0u : ~0u));
+    };
+    for (int step = tot - 1; step >= 0; --step) {
+      const int rad = nstep_radius(step);
+      const int npts = (rad <= 5 || level > 0) ? 8 : 12;
+      const int tan = npts == 8 ? rad : nstep_tan(step);
+      uint32_t kmin = round(rad, tan, 0, 8);
+      if (npts == 12) kmin = min(kmin, round(rad, tan, 8, 4));
+      ++steps;
+      bool moved = false;
+      if (kmin < (best << 4)) {
+        best = kmin >> 4;
+        int dr, dc;
+        nstep_site((int)(kmin & 15), rad, tan, dr, dc);
+        row += dr;
+        col += dc;
+        off_center = 1;
+        moved = true;
+      }
+      if (!off_center) ++center;
+      if (!moved && step > 2) {
+        while (nstep_radius(step - 1) == rad && step > 2) {
+          ++center;
+          --step;
+        }
+      }
+    }
+    brow = row;
+    bcol = col;
+    num00 = center;
+    return best;
+  }
 };
 
 // cl[i] = v for a wave-uniform but dynamic i, without a private-array index
@@ -685,21 +790,27 @@ __device__ void int_sad_list(const S_t& S, const Ctx& c, int lane, int br, int b
 }
 
 // full_pixel_diamond (mcomp.c:1479-1526)
+// level -1: DIAMOND (av1_init_dsmotion_compensation); 0 / 1: NSTEP /
+// NSTEP_8PT (no LDS window: their radii do not shrink by halves)
 template <int W, int H, bool SKIP, bool TL>
 __device__ int full_pixel_diamond(const Ctx& c, int lane, int srow, int scol, int step_param,
                                   int& brow, int& bcol, int& steps, int& searches, lds_u32 win,
-                                  bool want_cl, int (&cl)[5]) {
+                                  bool want_cl, int (&cl)[5], int level = -1) {
   Search<W, H, SKIP, true, TL> S;
-  S.load_src(c, lane, win);
+  S.load_src(c, lane, level < 0 ? win : nullptr);
   int n, num00 = 0;
-  S.diamond(c, lane, srow, scol, step_param, brow, bcol, n, steps);
+  auto run = [&](int sp, int& r, int& cc, int& n00) {
+    if (level < 0) S.diamond(c, lane, srow, scol, sp, r, cc, n00, steps);
+    else S.nstep_diamond(c, lane, level, srow, scol, sp, r, cc, n00, steps);
+  };
+  run(step_param, brow, bcol, n);
   ++searches;
   int bestsme = S.var_cost_at(c, lane, brow, bcol);
-  const int further = kMaxSteps - 1 - step_param;
+  const int further = (level < 0 ? kMaxSteps : nstep_steps(level)) - 1 - step_param;
   while (n < further) {
     ++n;
     int tr, tc;
-    S.diamond(c, lane, srow, scol, step_param + n, tr, tc, num00, steps);
+    run(step_param + n, tr, tc, num00);
     ++searches;
     const int sme = S.var_cost_at(c, lane, tr, tc);
     if (sme < bestsme) {
@@ -739,6 +850,30 @@ __device__ __forceinline__ void bigdia_site(int s, int i, int& dr, int& dc) {
   const int sh = s == 0 ? 0 : s - 1;
   dr = ((int)((pr >> (3 * i)) & 7) - 2) * (1 << sh);
   dc = ((int)((pc >> (3 * i)) & 7) - 2) * (1 << sh);
+}
+// The other pattern_search site sets: av1_init_motion_compensation_square
+// (mcomp.c:553-604: 8 points of r = 2^s, (-1,-1) (0,-1) (1,-1) (1,0) (1,1)
+// (0,1) (-1,1) (-1,0) x r) and _hex (:607-653: scale 0 the square's 8,
+// scale s >= 1 6 points (-1,-2) (1,-2) (2,0) (1,2) (-1,2) (-2,0) x 2^(s-1))
+enum { kPatBigdia = 0, kPatSquare = 1, kPatHex = 2 };
+constexpr int kSqR[8] = {-1, 0, 1, 1, 1, 0, -1, -1}, kSqC[8] = {-1, -1, -1, 0, 1, 1, 1, 0};
+constexpr int kHxR[8] = {-1, 1, 2, 1, -1, -2, 0, 0}, kHxC[8] = {-2, -2, 0, 2, 2, 0, 0, 0};
+constexpr uint32_t kSqPR = bigdia_pack(kSqR), kSqPC = bigdia_pack(kSqC);
+constexpr uint32_t kHxPR = bigdia_pack(kHxR), kHxPC = bigdia_pack(kHxC);
+__device__ __forceinline__ void pat_site(int kind, int s, int i, int& dr, int& dc) {
+  if (kind == kPatBigdia) {
+    bigdia_site(s, i, dr, dc);
+    return;
+  }
+  const bool sq = kind == kPatSquare || s == 0;
+  const uint32_t pr = sq ? kSqPR : kHxPR, pc = sq ? kSqPC : kHxPC;
+  const int sh = sq ? s : s - 1;
+  dr = ((int)((pr >> (3 * i)) & 7) - 2) * (1 << sh);
+  dc = ((int)((pc >> (3 * i)) & 7) - 2) * (1 << sh);
+}
+// searches_per_step of scale s
+__device__ __forceinline__ int pat_n(int kind, int s) {
+  return kind == kPatBigdia ? (s == 0 ? 4 : 8) : (kind == kPatHex && s > 0 ? 6 : 8);
 }
 
 // pattern_search (mcomp.c:1017-1245) over the BIGDIA sites: with
@@ -816,7 +951,7 @@ template <int W, int H, bool SKIP, bool TL, bool WINP = false>
 __device__ int pattern(const Ctx& c, int lane, int srow, int scol, int search_step, bool do_init,
                        bool want_cl, int (&cl)[5], int& brow, int& bcol, int& steps,
                        int& nsad, lds_u32 win = nullptr, uint32_t* vout = nullptr,
-                       bool prefilled = false) {
+                       bool prefilled = false, int kind = kPatBigdia) {
   static_assert(!WINP || (Win<W, H>::kOn && !TL), "window: w, h <= 32, linear layout");
   using WN = Win<W, H>;
   constexpr int NR = 2 * WN::R + 1;  // full-pel rows / columns a window spans
@@ -860,7 +995,7 @@ __device__ int pattern(const Ctx& c, int lane, int srow, int scol, int search_st
   // for invalid ones (calc_sad3 / _with_indices)
   auto check = [&](int s, int cnt, int idx, int clmode) -> int {
     int dr, dc;
-    bigdia_site(s, idx, dr, dc);
+    pat_site(kind, s, idx, dr, dc);
     const int r = br + dr, cc = bc + dc;
     // (check_bounds only skips this test when it holds)
     const bool valid =
@@ -895,20 +1030,36 @@ __device__ int pattern(const Ctx& c, int lane, int srow, int scol, int search_st
   };
   auto move = [&](int s, int k) {
     int dr, dc;
-    bigdia_site(s, k, dr, dc);
+    pat_site(kind, s, k, dr, dc);
     br += dr;
     bc += dc;
   };
   // next_chkpts_indices: k - 1, k, k + 1 (cyclic over n)
   // (n is 4 or 8: a mask, no per-lane select chain -- those compiled to
-  // exec-mask branches)
-  auto around = [](int j, int k, int n) { return (k + j - 1 + n) & (n - 1); };
+  // exec-mask branches; HEX's 6: two compares)
+  auto around = [](int j, int k, int n) {
+    if ((n & (n - 1)) == 0) return (k + j - 1 + n) & (n - 1);
+    int v = k + j - 1;
+    v += v < 0 ? n : 0;
+    return v >= n ? v - n : v;
+  };
+  // candidates a full scan of scale s evaluates: with every candidate in
+  // bounds the reference's calc_sad4 groups of four and then
+  // calc_sad_update_bestmv(num_candidates = n % 4, cand_start = n & ~3),
+  // whose loop never runs -- HEX's 6-point scales evaluate their first four
+  // (mcomp.c:1064-1077,1108-1122,964)
+  auto scan_n = [&](int s) {
+    const int n = pat_n(kind, s), d = 1 << s;
+    const bool all = br - d >= c.row_min && br + d <= c.row_max && bc - d >= c.col_min &&
+                     bc + d <= c.col_max;
+    return all ? (n & ~3) : n;
+  };
   int k = -1;
   if (do_init) {
     const int smax = best_init_s;
     best_init_s = -1;
     for (int t = 0; t <= smax; ++t) {
-      const int w = check(t, t == 0 ? 4 : 8, g, 0);
+      const int w = check(t, scan_n(t), g, 0);
       if (w < 0) continue;
       best_init_s = t;
       k = w;
@@ -916,13 +1067,14 @@ __device__ int pattern(const Ctx& c, int lane, int srow, int scol, int search_st
     if (best_init_s != -1) move(best_init_s, k);
   }
   if (best_init_s != -1) {
-    const int last_s = want_cl ? 1 : 0;  // num_candidates[0] == 4 for BIGDIA
+    // last_is_4 && cost_list: num_candidates[0] == 4 (BIGDIA only)
+    const int last_s = want_cl && kind == kPatBigdia ? 1 : 0;
     int best_site = -1;
     int s = best_init_s;
     for (; s >= last_s; --s) {
-      const int n = s == 0 ? 4 : 8;
+      const int n = pat_n(kind, s);
       if (!do_init || s != best_init_s) {
-        best_site = check(s, n, g, 0);
+        best_site = check(s, scan_n(s), g, 0);
         if (best_site < 0) continue;
         move(s, best_site);
         k = best_site;
@@ -935,7 +1087,7 @@ __device__ int pattern(const Ctx& c, int lane, int srow, int scol, int search_st
         }
       } while (best_site >= 0);
     }
-    if (s == 0 && want_cl) {
+    if (s == 0 && want_cl && kind == kPatBigdia) {
       cl[0] = (int)raw;
       has_sad = true;
       if (!do_init || s != best_init_s) {
@@ -997,7 +1149,17 @@ __device__ int pattern(const Ctx& c, int lane, int srow, int scol, int search_st
 constexpr int kDkWaves = LAVISH_DK_WAVES;
 
 // search_method values of SEARCH_METHODS (av1/encoder/mcomp_structs.h:56-86)
-enum { kDiamond = 0, kBigdia = 5, kFastDiamond = 8, kFastBigdia = 9, kVfastDiamond = 10 };
+enum {
+  kDiamond = 0, kNstep = 1, kNstep8 = 2, kHex = 4, kBigdia = 5, kSquare = 6, kFastHex = 7,
+  kFastDiamond = 8, kFastBigdia = 9, kVfastDiamond = 10
+};
+// the diamond_search_sad walks (full_pixel_diamond); the others are pattern searches
+__host__ __device__ __forceinline__ bool diamond_method(int m) {
+  return m == kDiamond || m == kNstep || m == kNstep8;
+}
+__host__ __device__ __forceinline__ int method_steps(int m) {
+  return m == kNstep ? 15 : m == kNstep8 ? 16 : kMaxSteps;
+}
 
 // search context of one job: its buffers, FullMvLimits, ref_mv and mv costs
 __device__ __forceinline__ Ctx job_ctx(const uint8_t* src, int ss, const uint8_t* ref, int rs,
@@ -1042,16 +1204,21 @@ __device__ __forceinline__ int job_search(const Ctx& c, int lane, int start_row,
     constexpr bool SK = decltype(skip_tag)::value;
     if constexpr (!PAT) {
       return full_pixel_diamond<W, H, SK, TL>(c, lane, start_row, start_col, step_param, br, bc,
-                                              steps, searches, win, want_cl, cl);
+                                              steps, searches, win, want_cl, cl,
+                                              method == kNstep ? 0 : method == kNstep8 ? 1 : -1);
     } else {
-      // bigdia (do_init 1) / fast_dia / vfast_dia / fast_bigdia (mcomp.c:1266-1316)
-      const int step = method == kBigdia        ? step_param
-                       : method == kFastDiamond ? max(kMaxSteps - 2, step_param)
+      // bigdia / hex / square (do_init 1), fast_dia / vfast_dia / fast_bigdia
+      // / fast_hex (do_init 0) (mcomp.c:1258-1316)
+      const bool init = method == kBigdia || method == kHex || method == kSquare;
+      const int step = init                     ? step_param
+                       : method == kFastDiamond || method == kFastHex ? max(kMaxSteps - 2, step_param)
                        : method == kVfastDiamond ? max(kMaxSteps - 1, step_param)
                                                  : max(kMaxSteps - 3, step_param);
-      return pattern<W, H, SK, TL, WINP>(c, lane, start_row, start_col, step,
-                                         method == kBigdia, want_cl, cl, br, bc, steps, searches,
-                                         win, vout, prefilled);
+      const int kind = method == kHex || method == kFastHex ? kPatHex
+                       : method == kSquare                  ? kPatSquare
+                                                            : kPatBigdia;
+      return pattern<W, H, SK, TL, WINP>(c, lane, start_row, start_col, step, init, want_cl, cl,
+                                         br, bc, steps, searches, win, vout, prefilled, kind);
     }
   };
   // use_downsampled_sad applies to blocks at least 16 high (mcomp.c:132-133)
@@ -2322,7 +2489,7 @@ void launch_tl(const uint8_t* src, int ss, const uint8_t* ref, int rs, const Lav
                int32_t* cost_lists, hipStream_t s) {
   int nwg = (njobs + kDkWaves - 1) / kDkWaves;
   nwg = (nwg + 7) & ~7;
-  if (method == kDiamond)
+  if (diamond_method(method))
     hipLaunchKernelGGL((diamond_kernel<W, H, false, TL>), dim3(nwg), dim3(64 * kDkWaves), 0, s, src, ss,
                        ref, rs, t, (const Job*)jobs, njobs, step_param, cost, skip, method, out,
                        cost_lists);
@@ -2423,14 +2590,13 @@ int fullpel_batch(const uint8_t* src, int src_stride, const uint8_t* ref, int re
                   const LavishRefTiles* tiles = nullptr) {
   if (njobs <= 0) return 0;
   if (tiles != nullptr && (tiles->data == nullptr || tiles->stride != ref_stride)) return -5;
-  if (step_param < 0 || step_param >= kMaxSteps) return -1;
+  if (step_param < 0 || step_param >= method_steps(method)) return -1;
   if (cost == nullptr || cost->mv_cost_type < 0 || cost->mv_cost_type > 4) return -2;
   if (cost->mv_cost_type == 0 &&
       (cost->mvjcost == nullptr || cost->mvcost[0] == nullptr || cost->mvcost[1] == nullptr))
     return -2;
-  if (method != kDiamond && method != kBigdia && method != kFastDiamond &&
-      method != kFastBigdia && method != kVfastDiamond)
-    return -4;
+  // every method of av1_full_pixel_search but CLAMPED_DIAMOND (3)
+  if (method < 0 || method > kVfastDiamond || method == 3) return -4;
 #define LAVISH_DIA_CASE(W, H)                                                                 \
   if (w == W && h == H) {                                                                     \
     launch<W, H>(src, src_stride, ref, ref_stride, tiles, jobs, njobs, step_param, *cost,     \

@@ -20,8 +20,9 @@ assert JOB_DTYPE.itemsize == 32 and RESULT_DTYPE.itemsize == 16
 
 MV_COST_ENTROPY, MV_COST_L1_LOWRES, MV_COST_L1_MIDRES, MV_COST_L1_HDRES, MV_COST_NONE = range(5)
 # SEARCH_METHODS (av1/encoder/mcomp_structs.h:56-86) the full-pel search takes
-SEARCH_METHODS = {"diamond": 0, "bigdia": 5, "fast_diamond": 8, "fast_bigdia": 9,
-                  "vfast_diamond": 10}
+# (all of them but CLAMPED_DIAMOND)
+SEARCH_METHODS = {"diamond": 0, "nstep": 1, "nstep_8pt": 2, "hex": 4, "bigdia": 5, "square": 6,
+                  "fast_hex": 7, "fast_diamond": 8, "fast_bigdia": 9, "vfast_diamond": 10}
 MV_MAX = (1 << 14) - 1
 MI_SIZE = 4
 AOM_INTERP_EXTEND = 4

@@ -162,7 +162,7 @@ C3_COST = 0     # MV_COST_ENTROPY (the RDO path's x->mv_cost_type)
 C3_SKIP = True  # use_downsampled_sad (>= 720p, speed_features.c:205-209)
 C3_CL = True    # cost list: subpel_search_method != SUBPEL_TREE (cond_cost_list)
 C3_WG_CAP = 512  # C3's workgroups beside C2 (profiles/r04_v11_*: the step's best)
-C3_MODE = "fused"  # C2 + C3 in one launch (lavish_txq_frame_search)
+C3_MODE = "streams"  # C3 on a second stream beside C2 (fused: measured slower)
 C3_EVERY = 10      # fused: a search unit every 10 units of the dispatch order
 # sub-pixel refinement after the full-pel search (c3sub): SUBPEL_TREE_PRUNED_MORE
 # (speed >= 4), subpel_force_stop EIGHTH_PEL, iters_per_step 1 (speed >= 2),
@@ -1964,10 +1964,14 @@ def main():
     c3_bytes = c3_algorithmic_bytes(c3_res, len(jobs_np), C3_BLOCK, C3_BLOCK, C3_SKIP, C3_CL) \
         + R.trefs.numel() + R.c3_tiles.data.numel() if do_c3 else 0
 
-    traffic = None
+    traffic = c3_hbm = traffic_src = None
     if os.path.exists(args.pmc_json):
         try:
-            traffic = json.load(open(args.pmc_json)).get("frame_hbm_bytes_per_launch")
+            pj = json.load(open(args.pmc_json))
+            traffic = pj.get("frame_hbm_bytes_per_launch")
+            c3_hbm = pj.get("diamond_hbm_bytes_per_launch")
+            traffic_src = "%s (round %s: %s)" % (os.path.relpath(args.pmc_json, ROOT),
+                                                  pj.get("round"), pj.get("command", ""))
         except (ValueError, OSError):
             traffic = None
 
@@ -1976,8 +1980,8 @@ def main():
         roof = {"bound": "hbm",
                 "kernel": "lavish_txq_frame (txq_multi_kernel<0> + <1>: one launch per VGPR class, 14 sizes)",
                 "achieved": round(c2_bytes / (c2_ms * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBS,
-                "unit": "GB/s", "traffic": traffic, "avg_launch_ms": round(c2_ms, 4),
-                "algorithmic_bytes_per_launch": c2_bytes}
+                "unit": "GB/s", "traffic": traffic, "traffic_source": traffic_src,
+                "avg_launch_ms": round(c2_ms, 4), "algorithmic_bytes_per_launch": c2_bytes}
     else:
         roof = {"bound": "hbm",
                 "kernel": "ref_tiles_kernel + diamond_kernel<16,16,false,true> "
@@ -2036,10 +2040,17 @@ def main():
     if legs_overlapped is not None:
         line["legs_overlapped_ms"] = legs_overlapped
     if do_c3:
+        # the search's candidate re-reads are served by L2: its
+        # algorithmic rate is not an HBM rate; the PMC bytes that reach HBM
+        # (tiles + search + cost tables) stand beside it
         line["c3"] = {"jobs": len(jobs_np),
                       "steps_per_job": round(float(c3_res["steps"].mean()), 2),
+                      "stats_from": "the timed region's last step",
                       "algorithmic_bytes": c3_bytes,
-                      "achieved_GBps": round(c3_bytes / (c3_ms * 1e-3) / 1e9, 1)}
+                      "algorithmic_GBps_L2_served": round(c3_bytes / (c3_ms * 1e-3) / 1e9, 1),
+                      "hbm_bytes_pmc": c3_hbm,
+                      "hbm_GBps_pmc": round(c3_hbm / (c3_ms * 1e-3) / 1e9, 1) if c3_hbm else None,
+                      "leg_ms": round(c3_ms, 4)}
     if args.workload == "rdo" and not args.no_c4:
         # the 4K 10-bit RDO configuration (BASELINE configs[3]), timed after
         # the headline region so the driver's run records it too

@@ -195,7 +195,10 @@ typedef struct OrcMsParams {
 } OrcMsParams;
 /* search methods (SEARCH_METHODS, av1/encoder/mcomp_structs.h) */
 /* SEARCH_METHODS values (av1/encoder/mcomp_structs.h:56-86) */
-enum { ORC_DIAMOND = 0, ORC_BIGDIA = 5, ORC_FAST_DIAMOND = 8, ORC_FAST_BIGDIA = 9, ORC_VFAST_DIAMOND = 10 };
+/* SEARCH_METHODS (av1/encoder/mcomp_structs.h:56-86) */
+enum { ORC_DIAMOND = 0, ORC_NSTEP = 1, ORC_NSTEP_8PT = 2, ORC_HEX = 4, ORC_BIGDIA = 5,
+       ORC_SQUARE = 6, ORC_FAST_HEX = 7, ORC_FAST_DIAMOND = 8, ORC_FAST_BIGDIA = 9,
+       ORC_VFAST_DIAMOND = 10 };
 /* av1_full_pixel_search (no mesh) with DIAMOND / FAST_BIGDIA / BIGDIA:
  * returns the var cost, writes the best FULLPEL_MV, the step count and,
  * when cost_list != NULL, the reference's 5-entry cost list. */

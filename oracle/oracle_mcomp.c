@@ -3,13 +3,17 @@
  * CPU restatement of the full-pixel motion search of the reference:
  *   av1_init_dsmotion_compensation     av1/encoder/mcomp.c:369-404 (level 0)
  *   av1_init_motion_compensation_bigdia av1/encoder/mcomp.c:498-550
+ *   av1_init_motion_compensation_nstep  av1/encoder/mcomp.c:450-494 (NSTEP, NSTEP_8PT)
+ *   av1_init_motion_compensation_square av1/encoder/mcomp.c:552-604
+ *   av1_init_motion_compensation_hex    av1/encoder/mcomp.c:606-653 (HEX, FAST_HEX)
  *   mv_cost / mv_err_cost / mvsad_err_cost (entropy, L1, none)
  *                                      av1/encoder/mcomp.c:255-360
  *   av1_get_mv_joint                   av1/encoder/encodemv.h:49-55
  *   diamond_search_sad                 av1/encoder/mcomp.c:1318-1477
  *   full_pixel_diamond                 av1/encoder/mcomp.c:1479-1526
- *   pattern_search (BIGDIA do_init_search 1, FAST_BIGDIA 0, cost lists)
- *                                      av1/encoder/mcomp.c:858-1245,1266-1316
+ *   pattern_search (BIGDIA / HEX / SQUARE do_init_search 1, FAST_BIGDIA /
+ *   FAST_DIAMOND / VFAST_DIAMOND / FAST_HEX 0, cost lists)
+ *                                      av1/encoder/mcomp.c:858-1245,1258-1316
  *   calc_int_sad_list                  av1/encoder/mcomp.c:789-838
  *   av1_full_pixel_search: method switch, downsampled-SAD quality recheck
  *                                      av1/encoder/mcomp.c:1755-1873
@@ -99,25 +103,80 @@ static void int_sad_list(const OrcMsParams *p, int br, int bc, int skip, int *cl
     if (cl[i + 1] != INT_MAX) cl[i + 1] += (int)mvsad_cost(p, br + nr[i], bc + nc[i]);
 }
 
-/* diamond_search_sad without second_pred / mask: returns bestsad, writes
- * the best mv and num00 (center steps).  *steps counts evaluated steps. */
-static unsigned diamond(const OrcMsParams *p, int srow, int scol, int search_step, int skip,
-                        int *brow, int *bcol, int *num00, int *steps) {
+/* a diamond_search_sad site configuration: per step its radius and search
+ * points (site 0 = the centre), num_search_steps */
+typedef struct {
+  int nsteps;
+  int radius[16], npts[16];
+  int dr[16][13], dc[16][13];
+} DiaCfg;
+
+/* av1_init_dsmotion_compensation (level 0): 11 steps, radius 2^step, the
+ * 8 points (-r,0) (r,0) (0,-r) (0,r) (-r,-r) (r,r) (-r,r) (r,-r) */
+static void dia_cfg_ds(DiaCfg *c) {
   static const int kDr[9] = { 0, -1, 1, 0, 0, -1, 1, -1, 1 };
   static const int kDc[9] = { 0, 0, 0, -1, 1, -1, 1, 1, -1 };
+  c->nsteps = MAX_STEPS;
+  for (int st = 0; st < MAX_STEPS; ++st) {
+    const int r = 1 << st;
+    c->radius[st] = r;
+    c->npts[st] = 8;
+    for (int i = 0; i <= 8; ++i) {
+      c->dr[st][i] = kDr[i] * r;
+      c->dc[st][i] = kDc[i] * r;
+    }
+  }
+}
+
+/* av1_init_motion_compensation_nstep (mcomp.c:452-494): level 0 (NSTEP) 15
+ * stages, 12 points at radius > 5 with tan_radius = max((int)(0.41 r), 1);
+ * level 1 (NSTEP_8PT) 16 stages of 8 points; the radius grows to
+ * max((int)(1.5 r + 0.5), r + 1) after each of the first 12 stages */
+static void dia_cfg_nstep(DiaCfg *c, int level) {
+  c->nsteps = level > 0 ? 16 : 15;
+  int radius = 1;
+  for (int st = 0; st < c->nsteps; ++st) {
+    int tan = (int)(0.41 * radius);
+    if (tan < 1) tan = 1;
+    int n = 12;
+    if (radius <= 5 || level > 0) {
+      tan = radius;
+      n = 8;
+    }
+    const int r = radius, t = tan;
+    const int mr[13] = { 0, -r, r, 0, 0, -r, r, -t, t, -r, r, t, -t };
+    const int mc[13] = { 0, 0, 0, -r, r, -t, t, r, -r, t, -t, r, -r };
+    for (int i = 0; i <= n; ++i) {
+      c->dr[st][i] = mr[i];
+      c->dc[st][i] = mc[i];
+    }
+    c->npts[st] = n;
+    c->radius[st] = radius;
+    if (st < 12) {
+      const int g = (int)(radius * 1.5 + 0.5);
+      radius = g > radius + 1 ? g : radius + 1;
+    }
+  }
+}
+
+/* diamond_search_sad without second_pred / mask: returns bestsad, writes
+ * the best mv and num00 (center steps).  *steps counts evaluated steps. */
+static unsigned diamond(const OrcMsParams *p, const DiaCfg *cfg, int srow, int scol,
+                        int search_step, int skip, int *brow, int *bcol, int *num00, int *steps) {
   if (scol < p->col_min) scol = p->col_min;
   if (scol > p->col_max) scol = p->col_max;
   if (srow < p->row_min) srow = p->row_min;
   if (srow > p->row_max) srow = p->row_max;
   int row = srow, col = scol, off_center = 0, center_steps = 0;
   unsigned best = mvsad_cost(p, row, col) + block_sad(p, row, col, skip);
-  const int tot = MAX_STEPS - search_step;
+  const int tot = cfg->nsteps - search_step;
   for (int step = tot - 1; step >= 0; --step) {
-    const int rad = 1 << step; /* cfg->radius[step] at level 0 */
+    const int rad = cfg->radius[step];
     int best_site = 0;
+    /* all_in: sites 1..4 (the axis points at the radius) in range */
     const int all_in = bounds_ok(p, row, col, rad);
-    for (int i = 1; i <= 8; ++i) {
-      const int r = row + kDr[i] * rad, c = col + kDc[i] * rad;
+    for (int i = 1; i <= cfg->npts[step]; ++i) {
+      const int r = row + cfg->dr[step][i], c = col + cfg->dc[step][i];
       if (!all_in && !in_range(p, r, c)) continue;
       const unsigned s = block_sad(p, r, c, skip);
       if (s < best) {
@@ -129,12 +188,21 @@ static unsigned diamond(const OrcMsParams *p, int srow, int scol, int search_ste
       }
     }
     ++*steps;
+    /* UPDATE_SEARCH_STEP (mcomp.c:1322-1342) */
     if (best_site) {
-      row += kDr[best_site] * rad;
-      col += kDc[best_site] * rad;
+      row += cfg->dr[step][best_site];
+      col += cfg->dc[step][best_site];
       off_center = 1;
     }
     if (!off_center) ++center_steps;
+    if (best_site == 0 && step > 2) {  /* steps of an equal radius below are skipped */
+      int next = cfg->radius[step - 1];
+      while (next == cfg->radius[step] && step > 2) {
+        ++center_steps;
+        --step;
+        next = cfg->radius[step - 1];
+      }
+    }
   }
   *brow = row;
   *bcol = col;
@@ -142,16 +210,17 @@ static unsigned diamond(const OrcMsParams *p, int srow, int scol, int search_ste
   return best;
 }
 
-static int full_pixel_diamond(const OrcMsParams *p, int srow, int scol, int step_param, int skip,
-                              int *cl, int *brow, int *bcol, int *steps) {
+static int full_pixel_diamond(const OrcMsParams *p, const DiaCfg *cfg, int srow, int scol,
+                              int step_param, int skip, int *cl, int *brow, int *bcol,
+                              int *steps) {
   int n, num00 = 0;
-  diamond(p, srow, scol, step_param, skip, brow, bcol, &n, steps);
+  diamond(p, cfg, srow, scol, step_param, skip, brow, bcol, &n, steps);
   int bestsme = var_cost(p, *brow, *bcol);
-  const int further = MAX_STEPS - 1 - step_param;
+  const int further = cfg->nsteps - 1 - step_param;
   while (n < further) {
     ++n;
     int tr, tc;
-    diamond(p, srow, scol, step_param + n, skip, &tr, &tc, &num00, steps);
+    diamond(p, cfg, srow, scol, step_param + n, skip, &tr, &tc, &num00, steps);
     const int sme = var_cost(p, tr, tc);
     if (sme < bestsme) {
       bestsme = sme;
@@ -167,11 +236,30 @@ static int full_pixel_diamond(const OrcMsParams *p, int srow, int scol, int step
   return bestsme;
 }
 
-/* ---- pattern_search over the BIGDIA sites (mcomp.c:1017-1245) ---- */
+/* ---- pattern_search (mcomp.c:1017-1245) over the BIGDIA, SQUARE and HEX
+ * sites (kind 0 / 1 / 2) ---- */
+enum { PAT_BIGDIA = 0, PAT_SQUARE = 1, PAT_HEX = 2 };
+#if defined(__GNUC__)
+#define ORC_TLS __thread
+#else
+#define ORC_TLS
+#endif
+static ORC_TLS int t_kind;
 static void bigdia_site(int s, int i, int *dr, int *dc) {
+  /* BIGDIA: scale 0 the 4 nearest, scale s >= 1 8 points of r = 2^(s-1) / 2r */
   static const int k0r[4] = { 0, 1, 0, -1 }, k0c[4] = { -1, 0, 1, 0 };
   static const int kr[8] = { -1, 0, 1, 2, 1, 0, -1, -2 }, kc[8] = { -1, -2, -1, 0, 1, 2, 1, 0 };
-  if (s == 0) {
+  /* SQUARE (and HEX scale 0): 8 points of r = 2^s */
+  static const int sr[8] = { -1, 0, 1, 1, 1, 0, -1, -1 }, sc[8] = { -1, -1, -1, 0, 1, 1, 1, 0 };
+  /* HEX scale s >= 1: 6 points (-r,-2r) (r,-2r) (2r,0) (r,2r) (-r,2r) (-2r,0), r = 2^(s-1) */
+  static const int hr[6] = { -1, 1, 2, 1, -1, -2 }, hc[6] = { -2, -2, 0, 2, 2, 0 };
+  if (t_kind == PAT_SQUARE || (t_kind == PAT_HEX && s == 0)) {
+    *dr = sr[i] << s;
+    *dc = sc[i] << s;
+  } else if (t_kind == PAT_HEX) {
+    *dr = hr[i] << (s - 1);
+    *dc = hc[i] << (s - 1);
+  } else if (s == 0) {
     *dr = k0r[i];
     *dc = k0c[i];
   } else {
@@ -180,7 +268,9 @@ static void bigdia_site(int s, int i, int *dr, int *dc) {
     *dc = kc[i] * r;
   }
 }
-static int ncand(int s) { return s == 0 ? 4 : 8; }
+static int ncand(int s) {
+  return t_kind == PAT_BIGDIA ? (s == 0 ? 4 : 8) : t_kind == PAT_HEX ? (s == 0 ? 8 : 6) : 8;
+}
 
 typedef struct {
   const OrcMsParams *p;
@@ -204,12 +294,18 @@ static int upd(PState *st, unsigned thissad, int r, int c) {
 
 /* calc_sad4 / calc_sad_update_bestmv over candidates [0, n) of scale s
  * around (br, bc); cost list entries get the raw SADs (sad4: all four; the
- * bounds-checked form: in-range ones only).  Returns the best site or -1. */
+ * bounds-checked form: in-range ones only).  Returns the best site or -1.
+ * With every candidate in bounds the reference runs calc_sad4 over the
+ * groups of four and then calc_sad_update_bestmv(num_candidates =
+ * n % 4, cand_start = n & ~3), whose loop (i = cand_start; i <
+ * num_candidates) never runs: HEX's 6-point scales evaluate only their first
+ * four candidates (mcomp.c:1064-1077,1108-1122,964). */
 static int scan_all(PState *st, int s, int br, int bc, int *cl) {
   const OrcMsParams *p = st->p;
   int best_site = -1;
   const int all = bounds_ok(p, br, bc, 1 << s);
-  for (int i = 0; i < ncand(s); ++i) {
+  const int n = all ? (ncand(s) & ~3) : ncand(s);
+  for (int i = 0; i < n; ++i) {
     int dr, dc;
     bigdia_site(s, i, &dr, &dc);
     if (!all && !in_range(p, br + dr, bc + dc)) continue;
@@ -247,9 +343,10 @@ static void next3(int k, int n, int *idx) {
   idx[2] = (k == n - 1) ? 0 : k + 1;
 }
 
-static int pattern_search(const OrcMsParams *p, int srow, int scol, int search_step,
+static int pattern_search(const OrcMsParams *p, int kind, int srow, int scol, int search_step,
                           int do_init, int skip, int *cl, int *brow, int *bcol, int *steps) {
   PState st = { p, skip, UINT_MAX, UINT_MAX, cl, steps };
+  t_kind = kind;
   if (search_step > MAX_STEPS - 1) search_step = MAX_STEPS - 1;
   int best_init_s = MAX_STEPS - 1 - search_step; /* search_steps[search_step] */
   if (scol < p->col_min) scol = p->col_min;
@@ -278,7 +375,8 @@ static int pattern_search(const OrcMsParams *p, int srow, int scol, int search_s
     }
   }
   if (best_init_s != -1) {
-    const int last_s = cl != NULL; /* num_candidates[0] == 4 for BIGDIA */
+    /* last_is_4 && cost_list: num_candidates[0] == 4 only for BIGDIA */
+    const int last_s = kind == PAT_BIGDIA && cl != NULL;
     int best_site = -1;
     s = best_init_s;
     for (; s >= last_s; s--) {
@@ -304,7 +402,7 @@ static int pattern_search(const OrcMsParams *p, int srow, int scol, int search_s
         }
       } while (best_site != -1);
     }
-    if (s == 0) { /* only with a cost list (last_s == 1) */
+    if (s == 0) { /* only BIGDIA with a cost list (last_s == 1) */
       cl[0] = (int)st.raw_best;
       costlist_has_sad = 1;
       if (!do_init || s != best_init_s) {
@@ -348,19 +446,24 @@ int orc_full_pixel_search(const OrcMsParams *p, int method, int start_row, int s
   for (;;) {
     if (cl) cl[0] = cl[1] = cl[2] = cl[3] = cl[4] = INT_MAX;
     int var;
-    if (method == ORC_DIAMOND) {
-      var = full_pixel_diamond(p, start_row, start_col, step_param, skip, cl, best_row, best_col,
-                               steps);
+    if (method == ORC_DIAMOND || method == ORC_NSTEP || method == ORC_NSTEP_8PT) {
+      DiaCfg cfg;
+      if (method == ORC_DIAMOND) dia_cfg_ds(&cfg);
+      else dia_cfg_nstep(&cfg, method == ORC_NSTEP_8PT);
+      var = full_pixel_diamond(p, &cfg, start_row, start_col, step_param, skip, cl, best_row,
+                               best_col, steps);
     } else {
-      /* bigdia_search: step_param, do_init 1; fast_dia / vfast_dia /
-       * fast_bigdia: AOMMAX(MAX_MVSEARCH_STEPS - 2 / 1 / 3, step_param),
-       * do_init 0 (mcomp.c:1266-1316) */
-      const int floor = method == ORC_FAST_DIAMOND ? MAX_STEPS - 2
+      /* bigdia / hex / square_search: step_param, do_init 1; fast_dia /
+       * vfast_dia / fast_bigdia / fast_hex: AOMMAX(MAX_MVSEARCH_STEPS - 2 /
+       * 1 / 3 / 2, step_param), do_init 0 (mcomp.c:1258-1316) */
+      const int floor = method == ORC_FAST_DIAMOND || method == ORC_FAST_HEX ? MAX_STEPS - 2
                         : method == ORC_VFAST_DIAMOND ? MAX_STEPS - 1
                         : MAX_STEPS - 3;
-      const int init = method == ORC_BIGDIA;
+      const int init = method == ORC_BIGDIA || method == ORC_HEX || method == ORC_SQUARE;
+      const int kind = method == ORC_HEX || method == ORC_FAST_HEX ? PAT_HEX
+                       : method == ORC_SQUARE ? PAT_SQUARE : PAT_BIGDIA;
       const int ss = init ? step_param : (step_param > floor ? step_param : floor);
-      var = pattern_search(p, start_row, start_col, ss, init, skip, cl, best_row, best_col,
+      var = pattern_search(p, kind, start_row, start_col, ss, init, skip, cl, best_row, best_col,
                            steps);
     }
     if (!skip) return var;

@@ -425,7 +425,8 @@ class OrcMvCost(ctypes.Structure):
                 ("mvcost", ctypes.c_void_p * 2)]
 
 
-FP_METHODS = {"diamond": 0, "bigdia": 5, "fast_diamond": 8, "fast_bigdia": 9, "vfast_diamond": 10}
+FP_METHODS = {"diamond": 0, "nstep": 1, "nstep_8pt": 2, "hex": 4, "bigdia": 5, "square": 6,
+              "fast_hex": 7, "fast_diamond": 8, "fast_bigdia": 9, "vfast_diamond": 10}
 
 
 def full_pixel_search_batch(src, ref, stride, w, h, jobs, method="diamond", step_param=0,

@@ -590,21 +590,50 @@ MS_CASES = [  # (method name, do-we-pass-a-cost-list, cost type, downsampled sad
 ]
 
 
-def gen_mcomp():
+# the search-site initialisers of av1_full_pixel_search's methods
+# (mcomp.c:369-653): (function, level)
+MS_INIT = {"DIAMOND": ("av1_init_dsmotion_compensation", 0),
+           "BIGDIA": ("av1_init_motion_compensation_bigdia", 0),
+           "FAST_BIGDIA": ("av1_init_motion_compensation_bigdia", 0),
+           "NSTEP": ("av1_init_motion_compensation_nstep", 0),
+           "NSTEP_8PT": ("av1_init_motion_compensation_nstep", 1),
+           "HEX": ("av1_init_motion_compensation_hex", 0),
+           "FAST_HEX": ("av1_init_motion_compensation_hex", 0),
+           "SQUARE": ("av1_init_motion_compensation_square", 0)}
+# fix_mcomp2: the methods other presets select (NSTEP at speed_features.c:
+# 1411,1459,1523; get_faster_search_method, mcomp.c:64-86), mesh refinement
+# off (force_mesh_thresh INT_MAX, as exhaustive_searches_thresh is at the
+# speeds using NSTEP without an exhaustive search)
+MS2_BLOCKS = [(16, 16, 6), (8, 8, 4), (32, 32, 3), (64, 64, 2), (16, 8, 3), (4, 4, 2)]
+MS2_CASES = [
+    ("NSTEP", 1, "MV_COST_ENTROPY", 1, 0), ("NSTEP", 0, "MV_COST_L1_HDRES", 0, 2),
+    ("NSTEP_8PT", 1, "MV_COST_ENTROPY", 0, 0), ("NSTEP_8PT", 0, "MV_COST_NONE", 1, 4),
+    ("HEX", 1, "MV_COST_ENTROPY", 1, 0), ("HEX", 0, "MV_COST_ENTROPY", 0, 3),
+    ("FAST_HEX", 1, "MV_COST_ENTROPY", 0, 0), ("FAST_HEX", 0, "MV_COST_L1_HDRES", 1, 10),
+    ("SQUARE", 1, "MV_COST_ENTROPY", 1, 0), ("SQUARE", 0, "MV_COST_NONE", 0, 5),
+]
+MS2_METHODS = ["NSTEP", "NSTEP_8PT", "HEX", "FAST_HEX", "SQUARE"]
+
+
+def gen_mcomp(blocks=None, cases=None, methods=("DIAMOND", "BIGDIA", "FAST_BIGDIA"),
+              name="fix_mcomp.npz", seed_off=4, mesh_thresh=0):
     """av1_full_pixel_search (av1/encoder/mcomp.c:1755-1895) over the DIAMOND,
     BIGDIA (do_init_search 1) and FAST_BIGDIA (do_init_search 0) methods with
     the entropy / L1 / none mv costs, with and without the downsampled-SAD
     speed feature and a cost list, on a small synthetic frame pair; plus the
     default-context mv cost tables and the mv limits of av1_set_mv_limits /
-    av1_set_mv_search_range."""
+    av1_set_mv_search_range.  (blocks, cases, methods, name: the same for
+    another method set -- fix_mcomp2.npz.)"""
+    blocks = MS_BLOCKS if blocks is None else blocks
+    cases = MS_CASES if cases is None else cases
     sys.path.insert(0, os.path.join(os.path.dirname(HERE), "..", "aom-av1-lavish_amd"))
     sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(HERE)), "aom-av1-lavish_amd"))
     import lavish_dsp.synth as synth
     out = nmv_cost_tables()
     tu = C.TU(REF, ["aom_dsp/sad.c", "aom_dsp/variance.c", "av1/encoder/mcomp.c"],
               C.reference_defines(REF))
-    check_errors(tu, ["av1_full_pixel_search", "av1_init_dsmotion_compensation",
-                      "av1_init_motion_compensation_bigdia", "av1_set_mv_search_range"])
+    check_errors(tu, ["av1_full_pixel_search", "av1_set_mv_search_range"] +
+                 sorted({MS_INIT[m][0] for m in methods}))
     E = tu.enums
     W, H, BORDER, NREF = 160, 128, 160, 2
     src_np, refs_np = synth.motion_planes(W, H, NREF, BORDER, seed=4321)
@@ -615,21 +644,19 @@ def gen_mcomp():
     ref_bufs = [tu.buffer("uint8_t", r.reshape(-1).tolist()) for r in refs_np]
     org = BORDER * stride + BORDER
     cfgs = {}
-    for m in ("DIAMOND", "BIGDIA", "FAST_BIGDIA"):
+    for m in methods:
         cfg = tu.struct_obj("search_site_config")
-        if m == "DIAMOND":
-            tu.func("av1_init_dsmotion_compensation")(cfg, stride, 0)
-        else:
-            tu.func("av1_init_motion_compensation_bigdia")(cfg, stride, 0)
+        fname, level = MS_INIT[m]
+        tu.func(fname)(cfg, stride, level)
         cfgs[m] = cfg
     mj = tu.buffer("int", out["mvjcost_lp"].tolist())
     mc = [tu.buffer("int", out["mvcost_lp"][k].tolist()) for k in range(2)]
     mc = [C.Pointer(c.buf, MV_MAX, c.ty) for c in mc]
     mi_params = tu.struct_obj("CommonModeInfoParams")
     _set(mi_params.buf[0], mi_rows=((H + 7) & ~7) // 4, mi_cols=((W + 7) & ~7) // 4)
-    rnd = ACMRandom(0xbaba + 4)
+    rnd = ACMRandom(0xbaba + seed_off)
     jobs = []
-    for (bw, bh, nblk) in MS_BLOCKS:
+    for (bw, bh, nblk) in blocks:
         fn = tu.func
         vtab = tu.struct_obj("aom_variance_fn_ptr_t")
         sz = "%dx%d" % (bw, bh)
@@ -637,7 +664,7 @@ def gen_mcomp():
              vf=fn("aom_variance%s" % sz), sdx4df=fn("aom_sad%sx4d" % sz),
              sdx3df=fn("aom_sad%sx3d" % sz), sdsx4df=fn("aom_sad_skip_%sx4d" % sz))
         bsize = E["BLOCK_%dX%d" % (bw, bh)]
-        for ci, (mname, use_cl, ctype, skip, step_param) in enumerate(MS_CASES):
+        for ci, (mname, use_cl, ctype, skip, step_param) in enumerate(cases):
             for b in range(nblk):
                 by = rnd.generate(H // bh) * bh
                 bx = rnd.generate(W // bw) * bw
@@ -664,7 +691,7 @@ def gen_mcomp():
                 P = ms.buf[0]
                 _set(P, bsize=bsize, vfp=vtab, search_method=E[mname], search_sites=cfgs[mname],
                      run_mesh_search=0, prune_mesh_search=0, mesh_search_mv_diff_threshold=4,
-                     force_mesh_thresh=0, fine_search_interval=0, is_intra_mode=0,
+                     force_mesh_thresh=mesh_thresh, fine_search_interval=0, is_intra_mode=0,
                      fast_obmc_search=0)
                 msb = _get(P, "ms_buffers")
                 _set(msb, ref=rbuf, src=sbuf, second_pred=None, mask=None, mask_stride=0,
@@ -697,9 +724,10 @@ def gen_mcomp():
                                   "row_min", "row_max", "error_per_bit", "sad_per_bit",
                                   "best_row", "best_col", "var", "cl0", "cl1", "cl2", "cl3",
                                   "cl4"])
-    out["cases"] = np.array([[["DIAMOND", "BIGDIA", "FAST_BIGDIA"].index(m), cl,
-                              E[ct], sk, sp] for m, cl, ct, sk, sp in MS_CASES], np.int32)
-    np.savez_compressed(os.path.join(HERE, "fix_mcomp.npz"), **out)
+    out["cases"] = np.array([[list(methods).index(m), cl, E[ct], sk, sp]
+                             for m, cl, ct, sk, sp in cases], np.int32)
+    out["methods"] = np.array(list(methods))
+    np.savez_compressed(os.path.join(HERE, name), **out)
 
 
 SP_CASES = [  # (subpel method, allow_hp, forced_stop, iters_per_step, cost type, cost list)
@@ -2130,7 +2158,7 @@ def main(argv):
     sections = argv or ["txfm", "qparams", "quant", "inv", "pixel", "wht", "nmv", "mcomp",
                         "subpel", "tpl", "qfacade", "costcoeffs", "trellis", "warp", "compound",
                         "convolve", "compound12", "txfeat", "trellis2", "tplmv", "subpel_up", "tplmv3",
-                        "rdselect"]
+                        "rdselect", "mcomp2"]
     t0 = time.time()
     ttx = None
     if "txfm" in sections or "inv" in sections or "wht" in sections:
@@ -2157,6 +2185,9 @@ def main(argv):
         gen_nmv()
     if "mcomp" in sections:
         gen_mcomp()
+    if "mcomp2" in sections:
+        gen_mcomp(MS2_BLOCKS, MS2_CASES, MS2_METHODS, "fix_mcomp2.npz", seed_off=5,
+                  mesh_thresh=0x7FFFFFFF)
     if "subpel" in sections:
         gen_subpel()
     if "tpl" in sections:

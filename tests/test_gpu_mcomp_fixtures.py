@@ -52,6 +52,41 @@ def test_full_pixel_search_vs_reference(F, tiled):
     assert n == len(F["jobs"])
 
 
+@pytest.mark.parametrize("tiled", [False, True])
+def test_full_pixel_search_methods2_vs_reference(tiled):
+    """The methods of tests/golden/fix_mcomp2.npz (av1_full_pixel_search
+    executed from the reference): NSTEP / NSTEP_8PT (the nstep site
+    configuration's 8 / 12-point steps, equal-radius step skipping), HEX /
+    FAST_HEX and SQUARE pattern searches, with and without cost lists and
+    the downsampled SAD -- bit-exact."""
+    import torch
+    from lavish_dsp import motion as M
+    F2 = dict(np.load(os.path.join(GOLD, "fix_mcomp2.npz")))
+    methods = [str(m).lower() for m in F2["methods"]]
+    src = torch.from_numpy(F2["src"]).cuda()
+    refs = torch.from_numpy(np.ascontiguousarray(F2["refs"])).cuda()
+    tiles = M.RefTiles(refs, src.stride(0)).build() if tiled else None
+    costs = M.MvCosts(F2["mvjcost_lp"], F2["mvcost_lp"])
+    n = 0
+    for case, bw, bh, epb, spb, rec, rows, J in mcomp_groups(F2):
+        m, use_cl, ctype, skip, sp = (int(v) for v in case)
+        cp = costs.cost_params(spb, epb, ctype)
+        out, cl = M.full_pixel_search_batch(src, refs, bw, bh, M.to_device(rec), cp,
+                                            methods[m], sp, bool(skip), bool(use_cl),
+                                            tiles=tiles)
+        torch.cuda.synchronize()
+        res = M.results_numpy(out)
+        msg = "%s case %s %dx%d" % (methods[m], [int(v) for v in case], bw, bh)
+        np.testing.assert_array_equal(res["best_row"], rows[:, J["best_row"]], err_msg=msg)
+        np.testing.assert_array_equal(res["best_col"], rows[:, J["best_col"]], err_msg=msg)
+        np.testing.assert_array_equal(res["bestsme"], rows[:, J["var"]], err_msg=msg)
+        if use_cl:
+            np.testing.assert_array_equal(cl.cpu().numpy(), rows[:, J["cl0"]:J["cl4"] + 1],
+                                          err_msg=msg)
+        n += len(rows)
+    assert n == len(F2["jobs"])
+
+
 def test_full_pixel_search_rejects(F):
     """Entropy cost without tables, unknown search methods and bad step
     params are refused (no launch)."""

@@ -224,6 +224,34 @@ def test_full_pixel_search_vs_reference():
     assert n == len(F["jobs"])
 
 
+def test_full_pixel_search_methods2_vs_reference():
+    """orc_full_pixel_search_batch against av1_full_pixel_search executed from
+    the reference for the methods of tests/golden/fix_mcomp2.npz: NSTEP /
+    NSTEP_8PT (diamond_search_sad over av1_init_motion_compensation_nstep's
+    sites, mcomp.c:452-494), HEX / FAST_HEX and SQUARE (pattern_search,
+    mcomp.c:553-653,1258-1289), mesh refinement off."""
+    F = _load("fix_mcomp2.npz")
+    methods = [str(m).lower() for m in F["methods"]]
+    stride = F["src"].shape[1]
+    n = 0
+    seen = set()
+    for case, bw, bh, epb, spb, rec, rows, J in mcomp_groups(F):
+        m, use_cl, ctype, skip, sp = (int(v) for v in case)
+        res, cl = O.full_pixel_search_batch(
+            F["src"], F["refs"], stride, bw, bh, rec, methods[m], sp, ctype, spb, epb,
+            F["mvjcost_lp"], F["mvcost_lp"], skip=bool(skip), cost_list=bool(use_cl))
+        msg = "case %s %dx%d" % (list(case), bw, bh)
+        np.testing.assert_array_equal(res["best_row"], rows[:, J["best_row"]], err_msg=msg)
+        np.testing.assert_array_equal(res["best_col"], rows[:, J["best_col"]], err_msg=msg)
+        np.testing.assert_array_equal(res["bestsme"], rows[:, J["var"]], err_msg=msg)
+        if use_cl:
+            np.testing.assert_array_equal(cl, rows[:, J["cl0"]:J["cl4"] + 1], err_msg=msg)
+        n += len(rows)
+        seen.add(methods[m])
+    assert n == len(F["jobs"])
+    assert seen == {"nstep", "nstep_8pt", "hex", "fast_hex", "square"}
+
+
 def test_subpel_search_vs_reference():
     """orc_subpel_search_batch against av1_find_best_sub_pixel_tree_pruned
     (_more) executed from the reference, from full-pel results with their
