@@ -1214,7 +1214,9 @@ __device__ __forceinline__ int job_search(const Ctx& c, int lane, int start_row,
                        : method == kFastDiamond || method == kFastHex ? max(kMaxSteps - 2, step_param)
                        : method == kVfastDiamond ? max(kMaxSteps - 1, step_param)
                                                  : max(kMaxSteps - 3, step_param);
-      const int kind = method == kHex || method == kFastHex ? kPatHex
+      // (WINP: the TPL wavefront, whose methods are the BIGDIA family only)
+      const int kind = WINP                                 ? kPatBigdia
+                       : method == kHex || method == kFastHex ? kPatHex
                        : method == kSquare                  ? kPatSquare
                                                             : kPatBigdia;
       return pattern<W, H, SK, TL, WINP>(c, lane, start_row, start_col, step, init, want_cl, cl,

@@ -1343,6 +1343,50 @@ void av1_highbd_dist_wtd_convolve_2d_copy_hip(const uint16_t *src, int src_strid
                                               uint16_t *dst, int dst_stride, int w, int h,
                                               LavishConvolveParams *conv_params, int bd);
 
+/* ---- scaled convolution --------------------------
+ * Replaces av1_convolve_2d_scale_c / av1_highbd_convolve_2d_scale_c
+ * (av1/common/convolve.c:488-574,992-1078) -- the inter predictor of a
+ * reference of another resolution (convolve_2d_scale_wrapper :576-588) --
+ * for a batch of w x h blocks sharing the x / y filters (host
+ * InterpFilterParams, taps <= 12) and the conv params (round_0, round_1,
+ * is_compound, do_average, use_dist_wtd_comp_avg, fwd_offset, bck_offset;
+ * its dst / dst_stride are replaced by conv_dst / conv_stride).  Per block:
+ * the element offset of the block's integer source position, the
+ * prediction and CONV_BUF offsets, and the scaled start positions and steps
+ * in 1/1024 pel (SCALE_SUBPEL_BITS): subpel_*_qn in [0, 1023], *_step_qn in
+ * [1, 2048] (a block outside them is left untouched).  w a power of two in
+ * [2, 128], h in [1, 128].  Device pointers; asynchronous on `stream`.
+ * highbd: u16 samples (bit_depth 8/10/12), else u8.  Returns 0, or < 0 on
+ * rejected arguments. */
+typedef struct LavishScaleJob {
+  int64_t src_off;
+  int64_t dst_off;
+  int64_t conv_off;
+  int32_t subpel_x_qn, x_step_qn, subpel_y_qn, y_step_qn;
+} LavishScaleJob;
+int lavish_convolve_2d_scale_batch(const void *src, int src_stride, void *dst, int dst_stride,
+                                   uint16_t *conv_dst, int conv_stride, int w, int h,
+                                   const LavishScaleJob *jobs, int njobs,
+                                   const LavishInterpFilterParams *filter_params_x,
+                                   const LavishInterpFilterParams *filter_params_y,
+                                   const LavishConvolveParams *conv_params, int bit_depth,
+                                   int highbd, void *stream);
+/* av1/common/av1_rtcd_defs.pl:580,583 (per-call shims, host buffers) */
+void av1_convolve_2d_scale_hip(const uint8_t *src, int src_stride, uint8_t *dst,
+                               int dst_stride, int w, int h,
+                               const LavishInterpFilterParams *filter_params_x,
+                               const LavishInterpFilterParams *filter_params_y,
+                               const int subpel_x_qn, const int x_step_qn,
+                               const int subpel_y_qn, const int y_step_qn,
+                               LavishConvolveParams *conv_params);
+void av1_highbd_convolve_2d_scale_hip(const uint16_t *src, int src_stride, uint16_t *dst,
+                                      int dst_stride, int w, int h,
+                                      const LavishInterpFilterParams *filter_params_x,
+                                      const LavishInterpFilterParams *filter_params_y,
+                                      const int subpel_x_qn, const int x_step_qn,
+                                      const int subpel_y_qn, const int y_step_qn,
+                                      LavishConvolveParams *conv_params, int bd);
+
 #ifdef __cplusplus
 }
 #endif

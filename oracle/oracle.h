@@ -454,6 +454,14 @@ void orc_warp_batch(const void *ref, int width, int height, int stride, void *pr
                     int p_stride, uint16_t *dst, int dst_stride, const void *jobs, long njobs,
                     int ss_x, int ss_y, int bd, int hbd, const OrcConvParams *cp, int threads);
 
+/* oracle_scale.c: av1_convolve_2d_scale_c / av1_highbd_convolve_2d_scale_c;
+ * fx / fy: 16 kernel rows of tx / ty taps */
+void orc_convolve_2d_scale(const void *src, int src_stride, void *dst, int dst_stride, int w,
+                           int h, const int16_t *fx, int tx, const int16_t *fy, int ty,
+                           int subpel_x_qn, int x_step_qn, int subpel_y_qn, int y_step_qn,
+                           const OrcConvParams *cp, uint16_t *conv, int conv_stride, int bd,
+                           int hbd);
+
 /* search_tx_type's RDCOST + first-strictly-lowest type choice (oracle_rdo.c) */
 int orc_rd_select(int rdmult, const int *rates, const int64_t *dists, int n, int64_t *rds);
 

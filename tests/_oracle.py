@@ -1005,6 +1005,32 @@ def dist_wtd_convolve(path, src, src_stride, dst, dst_stride, w, h, fx, fy, cp, 
        P(fya), len(fya), ctypes.byref(c), P(conv), conv_stride, bd, hbd)
 
 
+def interp_table(interp_filter, size):
+    """The 16 kernel rows (int16 [16, taps]) of av1_get_interp_filter_params_
+    with_block_size(interp_filter, size) as the oracle holds them."""
+    return np.stack([interp_kernel(interp_filter, size, p) for p in range(16)])
+
+
+def convolve_2d_scale(src, src_stride, dst, dst_stride, w, h, fx_table, fy_table, subpel_x_qn,
+                      x_step_qn, subpel_y_qn, y_step_qn, cp, conv, conv_stride, bd, hbd,
+                      src_off=0):
+    """orc_convolve_2d_scale in place on dst / conv (cp: OrcConvParams fields
+    incl. is_compound); src_off: element offset of the block's position."""
+    fn = lib().orc_convolve_2d_scale
+    fn.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
+                   ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_int] + \
+        [ctypes.c_int] * 4 + [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
+                              ctypes.c_int]
+    fn.restype = None
+    fx = np.ascontiguousarray(fx_table, np.int16)
+    fy = np.ascontiguousarray(fy_table, np.int16)
+    c = OrcConvParams(**cp)
+    base = src.ctypes.data + src_off * src.itemsize
+    fn(ctypes.c_void_p(base), src_stride, P(dst), dst_stride, w, h, P(fx), fx.shape[1], P(fy),
+       fy.shape[1], subpel_x_qn, x_step_qn, subpel_y_qn, y_step_qn, ctypes.byref(c), P(conv),
+       conv_stride, bd, hbd)
+
+
 def dist_wtd_batch(src, src_stride, dst, dst_stride, conv, conv_stride, w, h, jobs, fx_table,
                    fy_table, cp, bd=8, threads=1):
     """orc_dist_wtd_batch in place on dst / conv (jobs: lavish_dsp.compound.JOB_DTYPE,

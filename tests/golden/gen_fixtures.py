@@ -1480,6 +1480,97 @@ def gen_compound():
 
 
 # ----------------------------------------------------------------------------
+# scaled convolution (av1/common/convolve.c:488-574, 992-1078)
+# ----------------------------------------------------------------------------
+# (w, h, x_step_qn, y_step_qn): steps in 1/1024 pel per output pixel --
+# 1024 unscaled, 2048 the 2:1 downscale limit, 512 / 640 / 768 upscales,
+# 1365 / 1536 / 1843 downscales (av1_setup_scale_factors_for_frame's range)
+SCALE_CASES = [(4, 4, 2048, 2048), (8, 8, 1536, 1536), (16, 8, 1024, 1365), (8, 16, 768, 2048),
+               (32, 16, 1843, 1024), (16, 32, 512, 640), (64, 16, 2048, 1536),
+               (4, 8, 640, 1843), (128, 8, 1365, 768)]
+
+
+def gen_scale():
+    """av1_convolve_2d_scale_c and av1_highbd_convolve_2d_scale_c
+    (av1/common/convolve.c:488-574, 992-1078): the inter predictor of a
+    scaled reference (av1_make_inter_predictor -> convolve_2d_scale_wrapper,
+    :576-588), over the 1/1024-pel steps and start phases of the supported
+    scale range, filters REGULAR / SMOOTH / SHARP / BILINEAR and the 12-tap
+    MULTITAP_SHARP2 (4-tap kernels for 4-wide / 4-high blocks,
+    av1_get_interp_filter_params_with_block_size), bd 8 (both forms) / 10 /
+    12, and the conv-param forms: single prediction (is_compound 0,
+    get_conv_params_no_round's rounding), compound first pass, plain and
+    distance-weighted average."""
+    tu = C.TU(REF, ["aom/aom_integer.h", "aom_ports/mem.h", "aom_dsp/aom_dsp_common.h",
+                    "aom_dsp/aom_filter.h", "av1/common/enums.h", "av1/common/filter.h",
+                    "av1/common/convolve.h", "av1/common/convolve.c"],
+              C.reference_defines(REF))
+    names = ["av1_convolve_2d_scale_c", "av1_highbd_convolve_2d_scale_c",
+             "av1_get_interp_filter_params_with_block_size"]
+    check_errors(tu, names)
+    rnd = ACMRandom(0xbaba + 21)
+    SH, SW = 64, 224  # source window: the cases' scaled extents + the 12-tap margins
+    DS, CS = 128, 128  # dst / conv-buffer strides
+    org = 8 * SW + 8  # the block's integer position inside the window
+    rows, srcs, dsts, dsts_in, convs, convs_in = [], [], [], [], [], []
+    for hb, bd in ((0, 8), (1, 8), (1, 10), (1, 12)):
+        et = "uint16_t" if hb else "uint8_t"
+        fn = tu.func("av1_highbd_convolve_2d_scale_c" if hb else "av1_convolve_2d_scale_c")
+        for (w, h, xs, ys) in SCALE_CASES:
+            t0 = time.time()
+            # one source window per size, shared by the four forms
+            src = np.array(_pix(rnd, SH * SW, bd)).reshape(SH, SW)
+            assert ((h - 1) * ys + 1023 >> 10) + 12 + 8 <= SH and ((w - 1) * xs + 1023 >> 10) + 12 + 8 <= SW
+            sidx = len(srcs)
+            srcs.append(src.astype(np.uint16))
+            for mode in range(4):  # single, compound first pass, average, dist-wtd average
+                fxi, fyi = rnd.generate(5), rnd.generate(5)  # InterpFilter; 4: MULTITAP_SHARP2
+                spx, spy = rnd.generate(1024), rnd.generate(1024)
+                sp = tu.buffer(et, src.reshape(-1).tolist())
+                blk = C.Pointer(sp.buf, org, sp.ty)
+                d_in = _pix(rnd, h * DS, bd)
+                c_in = [rnd.rand16() & ((1 << (bd + 4)) - 1) for _ in range(h * CS)]
+                dp = tu.buffer(et, d_in)
+                cb = tu.buffer("CONV_BUF_TYPE", c_in)
+                cp = tu.struct_obj("ConvolveParams")
+                comp = int(mode > 0)
+                intbuf = bd + 7 - 3 + 2
+                r0 = 3 + (intbuf - 16 if intbuf > 16 else 0)
+                r1 = 7 if comp else 2 * 7 - 3 - (intbuf - 16 if intbuf > 16 else 0)
+                jj, ii = rnd.generate(4), rnd.generate(2)
+                fwd, bck = (QUANT_DIST[jj][ii], QUANT_DIST[jj][1 - ii]) if mode == 3 else (0, 0)
+                _set(cp.buf[0], do_average=int(mode > 1), dst=cb, dst_stride=CS, round_0=r0,
+                     round_1=r1, plane=0, is_compound=comp, use_dist_wtd_comp_avg=int(mode == 3),
+                     fwd_offset=fwd, bck_offset=bck)
+                fpx = tu.func("av1_get_interp_filter_params_with_block_size")(fxi, w)
+                fpy = tu.func("av1_get_interp_filter_params_with_block_size")(fyi, h)
+                a = [blk, SW, dp, DS, w, h, fpx, fpy, spx, xs, spy, ys, cp]
+                if hb:
+                    a.append(bd)
+                fn(*a)
+                # InterpFilterParams.taps: 12 for MULTITAP_SHARP2, else SUBPEL_TAPS
+                # (the 4-tap kernels are 8-entry rows, filter.h:244-252)
+                taps_x = 12 if fxi == 4 else 8
+                taps_y = 12 if fyi == 4 else 8
+                rows.append([hb, bd, w, h, mode, fxi, fyi, spx, xs, spy, ys, r0, r1, fwd, bck,
+                             taps_x, taps_y, sidx])
+                pad = lambda v, n: np.pad(np.array(v, np.uint16), (0, n - len(v)))
+                dsts_in.append(pad(d_in, 32 * DS))
+                dsts.append(pad(dp.buf, 32 * DS))
+                convs_in.append(pad(c_in, 32 * CS))
+                convs.append(pad(cb.buf, 32 * CS))
+            print("  scale hb %d bd %d %dx%d %.1fs" % (hb, bd, w, h, time.time() - t0))
+    out = {"rows": np.array(rows, np.int64), "src": np.stack(srcs),
+           "dst_in": np.stack(dsts_in), "dst": np.stack(dsts), "conv_in": np.stack(convs_in),
+           "conv": np.stack(convs), "geom": np.array([SW, DS, CS, org], np.int64),
+           "row_fields": np.array(["highbd", "bd", "w", "h", "mode", "filter_x", "filter_y",
+                                   "subpel_x_qn", "x_step_qn", "subpel_y_qn", "y_step_qn",
+                                   "round_0", "round_1", "fwd_offset", "bck_offset", "taps_x",
+                                   "taps_y", "src_index"])}
+    np.savez_compressed(os.path.join(HERE, "fix_scale.npz"), **out)
+
+
+# ----------------------------------------------------------------------------
 # single-reference convolutions (av1/common/convolve.c:76-188, 687-787)
 # ----------------------------------------------------------------------------
 CONV_SIZES = [(2, 2), (2, 4), (4, 2), (4, 4), (8, 4), (4, 8), (8, 8), (16, 16), (32, 8),
@@ -2158,7 +2249,7 @@ def main(argv):
     sections = argv or ["txfm", "qparams", "quant", "inv", "pixel", "wht", "nmv", "mcomp",
                         "subpel", "tpl", "qfacade", "costcoeffs", "trellis", "warp", "compound",
                         "convolve", "compound12", "txfeat", "trellis2", "tplmv", "subpel_up", "tplmv3",
-                        "rdselect", "mcomp2"]
+                        "rdselect", "mcomp2", "scale"]
     t0 = time.time()
     ttx = None
     if "txfm" in sections or "inv" in sections or "wht" in sections:
@@ -2218,6 +2309,8 @@ def main(argv):
         gen_rdselect()
     if "subpel_up" in sections:
         gen_subpel_up()
+    if "scale" in sections:
+        gen_scale()
     print("done in %.0fs" % (time.time() - t0))
 
 

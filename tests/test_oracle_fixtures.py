@@ -458,6 +458,44 @@ def test_dist_wtd_convolve_matches_reference():
         np.testing.assert_array_equal(dst.astype(np.uint16), F["dst"][k], err_msg=str(k))
 
 
+def scale_row(F, k):
+    """(getter, conv-param dict) of fix_scale.npz row k."""
+    J = {n: i for i, n in enumerate(F["row_fields"])}
+    r = F["rows"][k]
+    g = lambda n: int(r[J[n]])
+    m = g("mode")
+    cp = dict(do_average=int(m > 1), round_0=g("round_0"), round_1=g("round_1"),
+              is_compound=int(m > 0), use_dist_wtd_comp_avg=int(m == 3),
+              fwd_offset=g("fwd_offset"), bck_offset=g("bck_offset"))
+    return g, cp
+
+
+def test_convolve_2d_scale_matches_reference():
+    """orc_convolve_2d_scale against av1_convolve_2d_scale_c and
+    av1_highbd_convolve_2d_scale_c executed from the reference
+    (fix_scale.npz): 1/1024-pel steps 512 .. 2048 and start phases, the five
+    filters incl. 12-tap MULTITAP_SHARP2, bd 8 (both forms) / 10 / 12, single
+    prediction, compound first pass, plain and distance-weighted average."""
+    F = _load("fix_scale.npz")
+    SW, DS, CS, org = (int(v) for v in F["geom"])
+    modes = set()
+    for k in range(len(F["rows"])):
+        g, cp = scale_row(F, k)
+        hb, bd, w, h = g("highbd"), g("bd"), g("w"), g("h")
+        pdt = np.uint16 if hb else np.uint8
+        src = np.ascontiguousarray(F["src"][g("src_index")].astype(pdt))
+        dst = F["dst_in"][k].astype(pdt).copy()
+        conv = F["conv_in"][k].copy()
+        fx, fy = O.interp_table(g("filter_x"), w), O.interp_table(g("filter_y"), h)
+        assert fx.shape[1] == g("taps_x") and fy.shape[1] == g("taps_y")
+        O.convolve_2d_scale(src, SW, dst, DS, w, h, fx, fy, g("subpel_x_qn"), g("x_step_qn"),
+                            g("subpel_y_qn"), g("y_step_qn"), cp, conv, CS, bd, hb, src_off=org)
+        np.testing.assert_array_equal(conv, F["conv"][k], err_msg=str(k))
+        np.testing.assert_array_equal(dst.astype(np.uint16), F["dst"][k], err_msg=str(k))
+        modes.add(g("mode"))
+    assert modes == {0, 1, 2, 3}
+
+
 def test_convolve_sr_matches_reference():
     """orc convolve_block against av1_convolve_{x,y,2d}_sr_c and the highbd
     forms executed from the reference (fix_convolve.npz): bd 8/10/12, 2x2 ..
