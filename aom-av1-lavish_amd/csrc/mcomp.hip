@@ -1198,7 +1198,7 @@ __device__ __forceinline__ int job_search(const Ctx& c, int lane, int start_row,
                                           int step_param, int skip, int method, lds_u32 win,
                                           bool want_cl, int (&cl)[5], int& br, int& bc,
                                           int& steps, int& searches, uint32_t* vout = nullptr,
-                                          bool prefilled = false) {
+                                          bool prefilled = false, bool* skip_used = nullptr) {
   int sme;
   auto search = [&](auto skip_tag) {
     constexpr bool SK = decltype(skip_tag)::value;
@@ -1230,9 +1230,12 @@ __device__ __forceinline__ int job_search(const Ctx& c, int lane, int start_row,
     int sad, ssad;
     sad_and_skip<W, H>(c, lane, br, bc, sad, ssad);
     const int thresh = (W >> 2) * (H >> 2);
-    if (sad > thresh && abs(ssad - sad) * 10 >= max(sad, 1) * 9) sme = search(std::false_type{});
+    const bool redo = sad > thresh && abs(ssad - sad) * 10 >= max(sad, 1) * 9;
+    if (redo) sme = search(std::false_type{});
+    if (skip_used) *skip_used = !redo;
   } else {
     sme = search(std::false_type{});
+    if (skip_used) *skip_used = false;
   }
   return sme;
 }
@@ -1246,7 +1249,8 @@ __global__ __launch_bounds__(64 * kDkWaves, (W <= 16 && H <= 16) ? 8 : 7) void d
                                                       int step_param, LavishMvCostParams cost,
                                                       int skip, int method,
                                                       LavishDiamondResult* __restrict__ out,
-                                                      int32_t* __restrict__ cost_lists) {
+                                                      int32_t* __restrict__ cost_lists,
+                                                      uint8_t* __restrict__ sdf_kind) {
   // XCD-aware: consecutive job quads (neighbouring blocks) share an XCD's L2
   const int nwg = gridDim.x;  // multiple of 8
   const int wg = (blockIdx.x & 7) * (nwg >> 3) + (blockIdx.x >> 3);
@@ -1271,8 +1275,10 @@ __global__ __launch_bounds__(64 * kDkWaves, (W <= 16 && H <= 16) ? 8 : 7) void d
   const bool want_cl = cost_lists != nullptr;
   int cl[5] = {INT_MAX, INT_MAX, INT_MAX, INT_MAX, INT_MAX};
   int br, bc, steps = 0, searches = 0;
+  bool skip_used = false;
   const int sme = job_search<W, H, PAT, TL>(c, lane, jb.start_row, jb.start_col, step_param, skip,
-                                            method, win, want_cl, cl, br, bc, steps, searches);
+                                            method, win, want_cl, cl, br, bc, steps, searches,
+                                            nullptr, false, &skip_used);
   if (lane == 0) {
     LavishDiamondResult r;
     r.best_row = (int16_t)br;
@@ -1280,6 +1286,129 @@ __global__ __launch_bounds__(64 * kDkWaves, (W <= 16 && H <= 16) ? 8 : 7) void d
     r.bestsme = sme;
     r.steps = steps;
     r.searches = searches;
+    out[j] = r;
+    if (sdf_kind) sdf_kind[j] = skip_used;
+  }
+  if (want_cl && lane < 5) {
+    const int v = lane == 0 ? cl[0] : lane == 1 ? cl[1] : lane == 2 ? cl[2] : lane == 3 ? cl[3] : cl[4];
+    cost_lists[5 * (int64_t)j + lane] = v;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// The exhaustive mesh refinement of av1_full_pixel_search (mcomp.c:1818-1838,
+// 1875-1893 -> full_pixel_exhaustive :1603-1680 -> exhaustive_mesh_search
+// :1529-1601), after the search kernel, one wave per job: forced when the
+// search's variance passes force_mesh_thresh scaled to the block (NSTEP /
+// NSTEP_8PT), or run_mesh_search; pruned when the search moved by at most
+// mesh_search_mv_diff_threshold.  Each pass scans every step-th row and column
+// of the range around its clamped start (column step 4 at step 1, the
+// reference's 4-at-a-time calls, whose last partial group of a row stops one
+// short of end_col) with the search's sdf (sdf_kind: the downsampled SAD when
+// the search kept it); lane group g takes candidate base + g, and the keyed
+// minimum (cost * 8 + g) over 8 candidates against the running best is the
+// reference's sequential strict-< update.  The pass's best is the next pass's
+// centre; the var cost at the end replaces the search's result only when
+// smaller; the cost list is recomputed around the mesh's best either way (the
+// reference's full_pixel_exhaustive writes it).
+struct MeshArgs {
+  int run, nstep, thr, prune, diff, intra, fine;
+  int range[4], interval[4];
+};
+
+template <int W, int H, bool SK>
+__device__ int mesh_refine(const Ctx& c, int lane, const MeshArgs& m, int srow, int scol,
+                           bool want_cl, int (&cl)[5], int& br, int& bc) {
+  Search<W, H, SK> S;
+  S.load_src(c, lane);
+  const int g = lane >> 3;
+  int range = m.range[0], interval = m.interval[0];
+  const int div = range / interval;  // (the host checked the first pattern)
+  const int mag = max(abs(srow), abs(scol));
+  range = min(max(range, 5 * mag / 4), 256);
+  interval = max(interval, range / div);
+  if (m.fine) interval = min(interval, 4);
+  br = srow;
+  bc = scol;
+  auto pass = [&](int rng, int step) {
+    const int r0c = min(max(br, c.row_min), c.row_max), c0c = min(max(bc, c.col_min), c.col_max);
+    const int r0 = max(-rng, c.row_min - r0c), r1 = min(rng, c.row_max - r0c);
+    const int q0 = max(-rng, c.col_min - c0c), q1 = min(rng, c.col_max - c0c);
+    br = r0c;
+    bc = c0c;
+    uint32_t best = rdlane(S.group_sad(c, r0c, c0c), 0) + mvsad_cost(c, r0c, c0c);
+    if (r1 < r0 || q1 < q0) return;
+    const int nrows = (r1 - r0) / step + 1;
+    int ncols;
+    if (step > 1) {
+      ncols = (q1 - q0) / step + 1;
+    } else {
+      const int n = q1 - q0 + 1;
+      ncols = 4 * (n >> 2) + max((n & 3) - 1, 0);
+    }
+    if (ncols <= 0) return;
+    const int total = nrows * ncols;
+    for (int base = 0; base < total; base += 8) {
+      const int idx = base + g;
+      const bool valid = idx < total;
+      const int ri = idx / ncols, ci = idx - ri * ncols;
+      const int r = r0c + r0 + ri * step, cc = c0c + q0 + ci * step;
+      const MvRate mr = mvsad_rate(c, valid ? r : r0c, valid ? cc : c0c);
+      const uint32_t sad = S.group_sad(c, r, cc, valid, r0c, c0c);
+      const uint32_t key = (((sad + mvsad_finish(c, mr, r, cc)) << 3) | (uint32_t)g) |
+                           (valid ? 0u : ~0u);
+      const uint32_t kmin = groups_min(key);
+      if (kmin < (best << 3)) {
+        best = kmin >> 3;
+        const int bi = base + (int)(kmin & 7);
+        const int bri = bi / ncols;
+        br = r0c + r0 + bri * step;
+        bc = c0c + q0 + (bi - bri * ncols) * step;
+      }
+    }
+  };
+  pass(range, interval);
+  if (interval > 1 && range > 7) {
+    for (int i = 1; i < 4; ++i) {
+      pass(m.range[i], m.interval[i]);
+      if (m.interval[i] == 1) break;
+    }
+  }
+  if (want_cl) int_sad_list(S, c, lane, br, bc, false, cl);
+  return var_cost<W, H>(c, lane, br, bc);
+}
+
+template <int W, int H>
+__global__ __launch_bounds__(64 * kDkWaves) void mesh_kernel(
+    const uint8_t* __restrict__ src, int ss, const uint8_t* __restrict__ ref, int rs,
+    const Job* __restrict__ jobs, int njobs, LavishMvCostParams cost, MeshArgs m,
+    const uint8_t* __restrict__ sdf_kind, LavishDiamondResult* __restrict__ out,
+    int32_t* __restrict__ cost_lists) {
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int j = blockIdx.x * kDkWaves + wave;
+  if (j >= njobs) return;
+  const Job jb = jobs[j];
+  const Ctx c = job_ctx(src, ss, ref, rs, jb, cost);
+  LavishDiamondResult r = out[j];
+  const int var = r.bestsme;
+  bool run = m.run;
+  if (!run && m.nstep && var > m.thr) run = true;
+  if (!m.intra && m.prune &&
+      max(abs(jb.start_row - r.best_row), abs(jb.start_col - r.best_col)) <= m.diff)
+    run = false;
+  if (!run) return;
+  const bool want_cl = cost_lists != nullptr;
+  int cl[5];
+  int br, bc;
+  const int var_ex = sdf_kind[j] ? mesh_refine<W, H, true>(c, lane, m, r.best_row, r.best_col,
+                                                           want_cl, cl, br, bc)
+                                 : mesh_refine<W, H, false>(c, lane, m, r.best_row, r.best_col,
+                                                            want_cl, cl, br, bc);
+  if (lane == 0 && var_ex < var) {
+    r.best_row = (int16_t)br;
+    r.best_col = (int16_t)bc;
+    r.bestsme = var_ex;
     out[j] = r;
   }
   if (want_cl && lane < 5) {
@@ -2488,17 +2617,38 @@ template <int W, int H, bool TL>
 void launch_tl(const uint8_t* src, int ss, const uint8_t* ref, int rs, const LavishRefTiles& t,
                const LavishDiamondJob* jobs, int njobs, int step_param,
                const LavishMvCostParams& cost, int skip, int method, LavishDiamondResult* out,
-               int32_t* cost_lists, hipStream_t s) {
+               int32_t* cost_lists, hipStream_t s, uint8_t* sdf_kind = nullptr) {
   int nwg = (njobs + kDkWaves - 1) / kDkWaves;
   nwg = (nwg + 7) & ~7;
   if (diamond_method(method))
     hipLaunchKernelGGL((diamond_kernel<W, H, false, TL>), dim3(nwg), dim3(64 * kDkWaves), 0, s, src, ss,
                        ref, rs, t, (const Job*)jobs, njobs, step_param, cost, skip, method, out,
-                       cost_lists);
+                       cost_lists, sdf_kind);
   else
     hipLaunchKernelGGL((diamond_kernel<W, H, true, TL>), dim3(nwg), dim3(64 * kDkWaves), 0, s, src, ss,
                        ref, rs, t, (const Job*)jobs, njobs, step_param, cost, skip, method, out,
-                       cost_lists);
+                       cost_lists, sdf_kind);
+}
+
+thread_local StreamScratch t_mesh;
+
+// the search (diamond_kernel, recording each job's sdf) then mesh_kernel
+template <int W, int H>
+void launch_mesh(const uint8_t* src, int ss, const uint8_t* ref, int rs, const LavishRefTiles* t,
+                 const LavishDiamondJob* jobs, int njobs, int step_param,
+                 const LavishMvCostParams& cost, int skip, int method, LavishDiamondResult* out,
+                 int32_t* cost_lists, const MeshArgs& m, hipStream_t s) {
+  uint8_t* kind = (uint8_t*)t_mesh.acquire((size_t)njobs, s);
+  if (W <= 16 && t != nullptr)
+    launch_tl<W, H, (W <= 16)>(src, ss, ref, rs, *t, jobs, njobs, step_param, cost, skip, method,
+                               out, cost_lists, s, kind);
+  else
+    launch_tl<W, H, false>(src, ss, ref, rs, LavishRefTiles{}, jobs, njobs, step_param, cost,
+                           skip, method, out, cost_lists, s, kind);
+  hipLaunchKernelGGL((mesh_kernel<W, H>), dim3((njobs + kDkWaves - 1) / kDkWaves),
+                     dim3(64 * kDkWaves), 0, s, src, ss, ref, rs, (const Job*)jobs, njobs, cost,
+                     m, (const uint8_t*)kind, out, cost_lists);
+  t_mesh.release(s);
 }
 
 template <int W, int H>
@@ -2589,8 +2739,41 @@ int fullpel_batch(const uint8_t* src, int src_stride, const uint8_t* ref, int re
                   int h, const LavishDiamondJob* jobs, int njobs, int method, int step_param,
                   const LavishMvCostParams* cost, int use_downsampled_sad,
                   LavishDiamondResult* out, int32_t* cost_lists, hipStream_t s,
-                  const LavishRefTiles* tiles = nullptr) {
+                  const LavishRefTiles* tiles = nullptr, const LavishMeshParams* mesh = nullptr) {
   if (njobs <= 0) return 0;
+  // the mesh refinement: nothing to do unless it can run (run_mesh_search,
+  // or the variance trigger after NSTEP / NSTEP_8PT) and the first pattern is
+  // legal (full_pixel_exhaustive returns INT_MAX otherwise, changing nothing)
+  MeshArgs ma{};
+  bool with_mesh = false;
+  if (mesh != nullptr) {
+    const LavishMeshParams& mp = *mesh;
+    const bool nstep = method == kNstep || method == kNstep8;
+    const bool legal = mp.range[0] >= 7 && mp.range[0] <= 256 && mp.interval[0] >= 1 &&
+                       mp.interval[0] <= mp.range[0];
+    if ((mp.run_mesh_search || nstep) && legal) {
+      // every later pass the walk can reach needs a positive interval (the
+      // reference's would not end); passes follow while the interval is not 1
+      for (int i = 1; i < 4; ++i) {
+        if (mp.interval[i] < 1) return -6;
+        if (mp.interval[i] == 1) break;
+      }
+      with_mesh = true;
+      ma.run = mp.run_mesh_search != 0;
+      ma.nstep = nstep;
+      const int bw = 31 - __builtin_clz((unsigned)(w >> 2) | 1u);
+      const int bh = 31 - __builtin_clz((unsigned)(h >> 2) | 1u);
+      ma.thr = mp.force_mesh_thresh >> (10 - (bw + bh));  // mi_size_*_log2
+      ma.prune = mp.prune_mesh_search != 0;
+      ma.diff = mp.mesh_search_mv_diff_threshold;
+      ma.intra = mp.is_intra_mode != 0;
+      ma.fine = mp.fine_search_interval != 0;
+      for (int i = 0; i < 4; ++i) {
+        ma.range[i] = mp.range[i];
+        ma.interval[i] = mp.interval[i];
+      }
+    }
+  }
   if (tiles != nullptr && (tiles->data == nullptr || tiles->stride != ref_stride)) return -5;
   if (step_param < 0 || step_param >= method_steps(method)) return -1;
   if (cost == nullptr || cost->mv_cost_type < 0 || cost->mv_cost_type > 4) return -2;
@@ -2601,8 +2784,12 @@ int fullpel_batch(const uint8_t* src, int src_stride, const uint8_t* ref, int re
   if (method < 0 || method > kVfastDiamond || method == 3) return -4;
 #define LAVISH_DIA_CASE(W, H)                                                                 \
   if (w == W && h == H) {                                                                     \
-    launch<W, H>(src, src_stride, ref, ref_stride, tiles, jobs, njobs, step_param, *cost,     \
-                 use_downsampled_sad, method, out, cost_lists, s);                            \
+    if (with_mesh)                                                                            \
+      launch_mesh<W, H>(src, src_stride, ref, ref_stride, tiles, jobs, njobs, step_param,     \
+                        *cost, use_downsampled_sad, method, out, cost_lists, ma, s);          \
+    else                                                                                      \
+      launch<W, H>(src, src_stride, ref, ref_stride, tiles, jobs, njobs, step_param, *cost,   \
+                   use_downsampled_sad, method, out, cost_lists, s);                          \
     LAVISH_CHECK(hipGetLastError());                                                          \
     return 0;                                                                                 \
   }
@@ -2710,6 +2897,16 @@ extern "C" int lavish_full_pixel_search_batch(const uint8_t* src, int src_stride
   return fullpel_batch(src, src_stride, ref, ref_stride, w, h, jobs, njobs, search_method,
                        step_param, cost, use_downsampled_sad, out, cost_lists,
                        (hipStream_t)stream);
+}
+
+extern "C" int lavish_full_pixel_search_batch_mesh(
+    const uint8_t* src, int src_stride, const uint8_t* ref, int ref_stride,
+    const LavishRefTiles* tiles, int w, int h, const LavishDiamondJob* jobs, int njobs,
+    int search_method, int step_param, const LavishMvCostParams* cost, int use_downsampled_sad,
+    const LavishMeshParams* mesh, LavishDiamondResult* out, int32_t* cost_lists, void* stream) {
+  return fullpel_batch(src, src_stride, ref, ref_stride, w, h, jobs, njobs, search_method,
+                       step_param, cost, use_downsampled_sad, out, cost_lists,
+                       (hipStream_t)stream, tiles, mesh);
 }
 
 static int64_t tiles_nstrips(int stride) { return (stride + 15) / 16; }

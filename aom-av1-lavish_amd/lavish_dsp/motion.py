@@ -64,6 +64,33 @@ _lib.lavish_full_pixel_search_batch_tiled.argtypes = [
     _vp, _i32, _vp, _i32, ctypes.POINTER(RefTilesDesc), _i32, _i32, _vp, _i32, _i32, _i32,
     ctypes.POINTER(MvCostParams), _i32, _vp, _vp, _vp]
 _lib.lavish_full_pixel_search_batch_tiled.restype = _i32
+
+
+class MeshParams(ctypes.Structure):
+    """LavishMeshParams: the mesh fields of FULLPEL_MOTION_SEARCH_PARAMS
+    (av1/encoder/mcomp.h:114-123) and the pattern set mesh_patterns
+    [is_intra_mode] as (range, interval) pairs."""
+    _fields_ = [("run_mesh_search", ctypes.c_int32), ("force_mesh_thresh", ctypes.c_int32),
+                ("prune_mesh_search", ctypes.c_int32),
+                ("mesh_search_mv_diff_threshold", ctypes.c_int32),
+                ("fine_search_interval", ctypes.c_int32), ("is_intra_mode", ctypes.c_int32),
+                ("range", ctypes.c_int32 * 4), ("interval", ctypes.c_int32 * 4)]
+
+    @classmethod
+    def make(cls, patterns, run_mesh_search=0, force_mesh_thresh=0x7FFFFFFF,
+             prune_mesh_search=0, mesh_search_mv_diff_threshold=4, fine_search_interval=0,
+             is_intra_mode=0):
+        m = cls(run_mesh_search, force_mesh_thresh, prune_mesh_search,
+                mesh_search_mv_diff_threshold, fine_search_interval, is_intra_mode)
+        for i, (r, iv) in enumerate(patterns):
+            m.range[i], m.interval[i] = r, iv
+        return m
+
+
+_lib.lavish_full_pixel_search_batch_mesh.argtypes = [
+    _vp, _i32, _vp, _i32, ctypes.POINTER(RefTilesDesc), _i32, _i32, _vp, _i32, _i32, _i32,
+    ctypes.POINTER(MvCostParams), _i32, ctypes.POINTER(MeshParams), _vp, _vp, _vp]
+_lib.lavish_full_pixel_search_batch_mesh.restype = _i32
 if hasattr(_lib, "lavish_set_search_workgroup_cap"):  # (older experiment builds lack it)
     _lib.lavish_set_search_workgroup_cap.argtypes = [_i32]
     _lib.lavish_set_search_workgroup_cap.restype = _i32
@@ -260,11 +287,12 @@ def diamond_search_batch(src, ref, w, h, jobs, step_param=0, mv_cost_type=MV_COS
 
 def full_pixel_search_batch(src, ref, w, h, jobs, cost, method="diamond", step_param=0,
                             use_downsampled_sad=False, cost_list=False, out=None,
-                            cost_lists=None, stream=None, tiles=None):
+                            cost_lists=None, stream=None, tiles=None, mesh=None):
     """lavish_full_pixel_search_batch (av1_full_pixel_search): planes and jobs
     as diamond_search_batch, cost a MvCostParams (MvCosts.cost_params or
-    l1_cost_params).  Returns (RESULT_DTYPE byte tensor, int32 [n, 5] cost
-    lists or None)."""
+    l1_cost_params); mesh a MeshParams: lavish_full_pixel_search_batch_mesh
+    (the exhaustive mesh refinement).  Returns (RESULT_DTYPE byte tensor,
+    int32 [n, 5] cost lists or None)."""
     import torch
     assert src.dtype == torch.uint8 and ref.dtype == torch.uint8
     assert src.is_contiguous() and ref.is_contiguous(), "planes must be C-contiguous"
@@ -273,8 +301,16 @@ def full_pixel_search_batch(src, ref, w, h, jobs, cost, method="diamond", step_p
         out = torch.empty(nj * RESULT_DTYPE.itemsize, dtype=torch.uint8, device=src.device)
     if cost_list and cost_lists is None:
         cost_lists = torch.empty((nj, 5), dtype=torch.int32, device=src.device)
-    if tiles is not None:  # RefTiles of `ref`: candidate rows from the tiled copy
+    if tiles is not None:
         assert tiles.ref.data_ptr() == ref.data_ptr() and tiles.stride == src.stride(0)
+    if mesh is not None:
+        rc = _lib.lavish_full_pixel_search_batch_mesh(
+            _vp(src.data_ptr()), src.stride(0), _vp(ref.data_ptr()), src.stride(0),
+            ctypes.byref(tiles.desc) if tiles is not None else None, w, h, _vp(jobs.data_ptr()),
+            nj, SEARCH_METHODS[method], step_param, ctypes.byref(cost),
+            int(use_downsampled_sad), ctypes.byref(mesh), _vp(out.data_ptr()),
+            _vp(cost_lists.data_ptr()) if cost_list else None, _stream_ptr(stream))
+    elif tiles is not None:  # RefTiles of `ref`: candidate rows from the tiled copy
         rc = _lib.lavish_full_pixel_search_batch_tiled(
             _vp(src.data_ptr()), src.stride(0), _vp(ref.data_ptr()), src.stride(0),
             ctypes.byref(tiles.desc), w, h, _vp(jobs.data_ptr()), nj, SEARCH_METHODS[method],

@@ -611,6 +611,45 @@ int lavish_full_pixel_search_batch_tiled(const uint8_t *src, int src_stride,
                                          LavishDiamondResult *out,
                                          int32_t *cost_lists, void *stream);
 
+/* The mesh fields of FULLPEL_MOTION_SEARCH_PARAMS (av1/encoder/mcomp.h:
+ * 114-123), with the pattern set the search reads
+ * (mesh_patterns[is_intra_mode]: sf->mv_sf.mesh_patterns or
+ * intrabc_mesh_patterns, speed_features.c:25-44,2292-2308). */
+typedef struct LavishMeshParams {
+  int32_t run_mesh_search;
+  int32_t force_mesh_thresh;
+  int32_t prune_mesh_search;
+  int32_t mesh_search_mv_diff_threshold;
+  int32_t fine_search_interval;
+  int32_t is_intra_mode;
+  int32_t range[4]; /* MESH_PATTERN range / interval per step (MAX_MESH_STEP 4) */
+  int32_t interval[4];
+} LavishMeshParams;
+/* lavish_full_pixel_search_batch[_tiled] followed by the exhaustive mesh
+ * refinement of av1_full_pixel_search (mcomp.c:1818-1838, 1875-1893 ->
+ * full_pixel_exhaustive :1603-1680 -> exhaustive_mesh_search :1529-1601):
+ * per job, when run_mesh_search or (NSTEP / NSTEP_8PT) the variance exceeds
+ * force_mesh_thresh >> (10 - mi_size_wide_log2 - mi_size_high_log2), unless
+ * pruned (not intra, the search moved <= mesh_search_mv_diff_threshold),
+ * the mesh passes around the search's best with the search's sdf; its var
+ * cost replaces the result when smaller, and the cost list (when
+ * cost_lists) is the one around the mesh's best either way, as the reference
+ * writes it.  An illegal first pattern (range outside [7, 256], interval
+ * outside [1, range]) makes the mesh a no-op, as in the reference.  mesh:
+ * HOST pointer (NULL: no mesh); tiles may be NULL.  Same returns as
+ * lavish_full_pixel_search_batch, and -6 when a later pass the walk can
+ * reach has an interval < 1. */
+int lavish_full_pixel_search_batch_mesh(const uint8_t *src, int src_stride,
+                                        const uint8_t *ref, int ref_stride,
+                                        const LavishRefTiles *tiles, int w, int h,
+                                        const LavishDiamondJob *jobs, int njobs,
+                                        int search_method, int step_param,
+                                        const LavishMvCostParams *cost,
+                                        int use_downsampled_sad,
+                                        const LavishMeshParams *mesh,
+                                        LavishDiamondResult *out, int32_t *cost_lists,
+                                        void *stream);
+
 /* C2 and the C3 search in one launch: lavish_txq_frame(residual, ...) and
  * lavish_full_pixel_search_batch_tiled(src, ..., 16, 16, jobs, njobs,
  * DIAMOND, ...) with the same results, run as one grid (the 64-point sizes

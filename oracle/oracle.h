@@ -199,12 +199,23 @@ typedef struct OrcMsParams {
 enum { ORC_DIAMOND = 0, ORC_NSTEP = 1, ORC_NSTEP_8PT = 2, ORC_HEX = 4, ORC_BIGDIA = 5,
        ORC_SQUARE = 6, ORC_FAST_HEX = 7, ORC_FAST_DIAMOND = 8, ORC_FAST_BIGDIA = 9,
        ORC_VFAST_DIAMOND = 10 };
+/* the mesh fields of FULLPEL_MOTION_SEARCH_PARAMS (av1/encoder/mcomp.h:
+ * 114-123) with the pattern set mesh_patterns[is_intra_mode] */
+typedef struct OrcMeshParams {
+  int run_mesh_search, force_mesh_thresh, prune_mesh_search, mesh_search_mv_diff_threshold;
+  int fine_search_interval, is_intra_mode;
+  int range[4], interval[4];
+} OrcMeshParams;
 /* av1_full_pixel_search (no mesh) with DIAMOND / FAST_BIGDIA / BIGDIA:
  * returns the var cost, writes the best FULLPEL_MV, the step count and,
  * when cost_list != NULL, the reference's 5-entry cost list. */
 int orc_full_pixel_search(const OrcMsParams *p, int method, int start_row, int start_col,
                           int step_param, int *cost_list, int *best_row, int *best_col,
                           int *steps);
+/* with the mesh refinement (mesh NULL: none) */
+int orc_full_pixel_search_ex(const OrcMsParams *p, int method, int start_row, int start_col,
+                             int step_param, int *cost_list, int *best_row, int *best_col,
+                             int *steps, const OrcMeshParams *mesh);
 int orc_full_pixel_search_diamond(const OrcMsParams *p, int start_row,
                                   int start_col, int step_param, int *best_row,
                                   int *best_col, int *steps);
@@ -238,6 +249,12 @@ void orc_full_pixel_search_batch(const uint8_t *src, int src_stride, const uint8
                                  long njobs, int method, int step_param, const OrcMvCost *cost,
                                  int skip_sad, int32_t *cost_lists, OrcDiamondResult *out,
                                  int threads);
+void orc_full_pixel_search_batch_ex(const uint8_t *src, int src_stride, const uint8_t *ref,
+                                    int ref_stride, int w, int h, const OrcDiamondJob *jobs,
+                                    long njobs, int method, int step_param,
+                                    const OrcMvCost *cost, int skip_sad, int32_t *cost_lists,
+                                    OrcDiamondResult *out, int threads,
+                                    const OrcMeshParams *mesh);
 
 /* ---- sub-pixel refinement (oracle_subpel.c); layouts = LavishSubpelJob /
  * LavishSubpelResult.  MVs and limits in 1/8 pel. */

@@ -18,9 +18,12 @@
  *   av1_full_pixel_search: method switch, downsampled-SAD quality recheck
  *                                      av1/encoder/mcomp.c:1755-1873
  * with sdf/sdx4df = aom_sad / aom_sad_skip and vf = aom_variance of the
- * block size (oracle_dsp.c).  Mesh refinement is not restated (off at the
- * configurations here).  Pinned by tests/golden/fix_mcomp.npz, made by
- * executing the reference's own av1_full_pixel_search.
+ * block size (oracle_dsp.c), and the mesh refinement:
+ *   exhaustive_mesh_search             av1/encoder/mcomp.c:1529-1601
+ *   full_pixel_exhaustive              av1/encoder/mcomp.c:1603-1680
+ *   av1_full_pixel_search mesh tail    av1/encoder/mcomp.c:1818-1838,1875-1893
+ * Pinned by tests/golden/fix_mcomp*.npz, made by executing the reference's
+ * own av1_full_pixel_search.
  */
 #include <limits.h>
 #include <stdlib.h>
@@ -438,9 +441,102 @@ static int pattern_search(const OrcMsParams *p, int kind, int srow, int scol, in
   return var_cost(p, br, bc); /* get_mvpred_var_cost */
 }
 
-/* av1_full_pixel_search (mcomp.c:1755-1873) without mesh search */
-int orc_full_pixel_search(const OrcMsParams *p, int method, int start_row, int start_col,
-                          int step_param, int *cl, int *best_row, int *best_col, int *steps) {
+/* exhaustive_mesh_search (mcomp.c:1529-1601): every (step)-th row and column
+ * (column step 4 when step is 1, then 4 positions per call; the last partial
+ * group of a row stops one short of end_col) within range of the clamped
+ * start, sequential strict-< update of sad + mvsad_err_cost; returns best_sad */
+static unsigned mesh_pass(const OrcMsParams *p, int srow, int scol, int range, int step,
+                          int skip, int *brow, int *bcol) {
+  const int col_step = step > 1 ? step : 4;
+  srow = srow < p->row_min ? p->row_min : srow > p->row_max ? p->row_max : srow;
+  scol = scol < p->col_min ? p->col_min : scol > p->col_max ? p->col_max : scol;
+  *brow = srow;
+  *bcol = scol;
+  unsigned best = block_sad(p, srow, scol, skip) + mvsad_cost(p, srow, scol);
+  const int r0 = -range > p->row_min - srow ? -range : p->row_min - srow;
+  const int c0 = -range > p->col_min - scol ? -range : p->col_min - scol;
+  const int r1 = range < p->row_max - srow ? range : p->row_max - srow;
+  const int c1 = range < p->col_max - scol ? range : p->col_max - scol;
+  for (int r = r0; r <= r1; r += step) {
+    for (int c = c0; c <= c1; c += col_step) {
+      const int n = step > 1 ? 1 : (c + 3 <= c1 ? 4 : c1 - c);
+      for (int i = 0; i < n; ++i) {
+        const int row = srow + r, col = scol + c + i;
+        const unsigned sad = block_sad(p, row, col, skip);
+        if (sad >= best) continue; /* update_mvs_and_sad, mcomp.c:858-877 */
+        const unsigned cost = sad + mvsad_cost(p, row, col);
+        if (cost < best) {
+          best = cost;
+          *brow = row;
+          *bcol = col;
+        }
+      }
+    }
+  }
+  return best;
+}
+
+static int ilog2i(int v) {
+  int l = 0;
+  while ((1 << (l + 1)) <= v) ++l;
+  return l;
+}
+
+/* full_pixel_exhaustive (mcomp.c:1603-1680): INT_MAX for an illegal first
+ * pattern (cost list untouched), else the var cost at the mesh's best and
+ * the cost list around it */
+static int mesh_exhaustive(const OrcMsParams *p, const OrcMeshParams *m, int srow, int scol,
+                           int skip, int *cl, int *brow, int *bcol) {
+  int interval = m->interval[0], range = m->range[0];
+  *brow = srow;
+  *bcol = scol;
+  if (range < 7 || range > 256 || interval < 1 || interval > range) return INT_MAX;
+  const int div = range / interval;
+  const int mag = abs(srow) > abs(scol) ? abs(srow) : abs(scol);
+  if (5 * mag / 4 > range) range = 5 * mag / 4;
+  if (range > 256) range = 256;
+  if (range / div > interval) interval = range / div;
+  if (m->fine_search_interval && interval > 4) interval = 4;
+  mesh_pass(p, srow, scol, range, interval, skip, brow, bcol);
+  if (interval > 1 && range > 7) {
+    for (int i = 1; i < 4; ++i) {
+      mesh_pass(p, *brow, *bcol, m->range[i], m->interval[i], skip, brow, bcol);
+      if (m->interval[i] == 1) break;
+    }
+  }
+  if (cl) int_sad_list(p, *brow, *bcol, skip, cl, 0);
+  return var_cost(p, *brow, *bcol);
+}
+
+/* the mesh tail of av1_full_pixel_search (mcomp.c:1818-1838, 1875-1893):
+ * forced after NSTEP / NSTEP_8PT when the variance passes force_mesh_thresh
+ * scaled to the block, pruned when the search moved little */
+static int mesh_tail(const OrcMsParams *p, const OrcMeshParams *m, int method, int start_row,
+                     int start_col, int skip, int var, int *cl, int *best_row, int *best_col) {
+  int run = m->run_mesh_search;
+  if (!run && (method == ORC_NSTEP || method == ORC_NSTEP_8PT)) {
+    const int thr = m->force_mesh_thresh >> (10 - (ilog2i(p->w >> 2) + ilog2i(p->h >> 2)));
+    if (var > thr) run = 1;
+  }
+  if (!m->is_intra_mode && m->prune_mesh_search) {
+    const int dr = abs(start_row - *best_row), dc = abs(start_col - *best_col);
+    if ((dr > dc ? dr : dc) <= m->mesh_search_mv_diff_threshold) run = 0;
+  }
+  if (!run) return var;
+  int tr, tc;
+  const int var_ex = mesh_exhaustive(p, m, *best_row, *best_col, skip, cl, &tr, &tc);
+  if (var_ex < var) {
+    var = var_ex;
+    *best_row = tr;
+    *best_col = tc;
+  }
+  return var;
+}
+
+/* av1_full_pixel_search (mcomp.c:1755-1893); mesh NULL: no mesh refinement */
+int orc_full_pixel_search_ex(const OrcMsParams *p, int method, int start_row, int start_col,
+                             int step_param, int *cl, int *best_row, int *best_col, int *steps,
+                             const OrcMeshParams *mesh) {
   /* use_downsampled_sad only for blocks >= 16 high (mcomp.c:132-133) */
   int skip = p->skip_sad && p->h >= 16;
   for (;;) {
@@ -466,16 +562,28 @@ int orc_full_pixel_search(const OrcMsParams *p, int method, int start_row, int s
       var = pattern_search(p, kind, start_row, start_col, ss, init, skip, cl, best_row, best_col,
                            steps);
     }
-    if (!skip) return var;
+    if (!skip)
+      return mesh ? mesh_tail(p, mesh, method, start_row, start_col, skip, var, cl, best_row,
+                              best_col)
+                  : var;
     /* quality check of the row-skipping search (mcomp.c:1840-1867) */
     const uint8_t *r = p->ref + (ptrdiff_t)*best_row * p->ref_stride + *best_col;
     const int sad = (int)orc_sad(p->src, p->src_stride, r, p->ref_stride, p->w, p->h);
     const int ssad = (int)orc_sad_skip(p->src, p->src_stride, r, p->ref_stride, p->w, p->h);
     const int thresh = (p->w >> 2) * (p->h >> 2); /* 1 << (mi_w_log2 + mi_h_log2) */
     const int big = sad > 1 ? sad : 1;
-    if (!(sad > thresh && abs(ssad - sad) * 10 >= big * 9)) return var;
+    if (!(sad > thresh && abs(ssad - sad) * 10 >= big * 9))
+      return mesh ? mesh_tail(p, mesh, method, start_row, start_col, skip, var, cl, best_row,
+                              best_col)
+                  : var;
     skip = 0; /* redo the whole search with the full SAD */
   }
+}
+
+int orc_full_pixel_search(const OrcMsParams *p, int method, int start_row, int start_col,
+                          int step_param, int *cl, int *best_row, int *best_col, int *steps) {
+  return orc_full_pixel_search_ex(p, method, start_row, start_col, step_param, cl, best_row,
+                                  best_col, steps, NULL);
 }
 
 int orc_full_pixel_search_diamond(const OrcMsParams *p, int start_row, int start_col,
@@ -499,6 +607,7 @@ typedef struct {
   const uint8_t *src, *ref;
   int ss, rs, w, h, step_param, skip, method;
   const OrcMvCost *cost;
+  const OrcMeshParams *mesh;
   const OrcDiamondJob *jobs;
   OrcDiamondResult *out;
   int32_t *cls;
@@ -513,9 +622,9 @@ static void *batch_worker(void *v) {
                       jb->col_min, jb->col_max, jb->row_min, jb->row_max, jb->ref_mv_row,
                       jb->ref_mv_col, a->cost->mv_cost_type, a->skip, a->cost };
     int br, bc, steps = 0;
-    a->out[j].bestsme = orc_full_pixel_search(&p, a->method, jb->start_row, jb->start_col,
-                                              a->step_param, a->cls ? a->cls + 5 * j : NULL,
-                                              &br, &bc, &steps);
+    a->out[j].bestsme = orc_full_pixel_search_ex(&p, a->method, jb->start_row, jb->start_col,
+                                                 a->step_param, a->cls ? a->cls + 5 * j : NULL,
+                                                 &br, &bc, &steps, a->mesh);
     a->out[j].best_row = (int16_t)br;
     a->out[j].best_col = (int16_t)bc;
     a->out[j].steps = steps;
@@ -524,24 +633,34 @@ static void *batch_worker(void *v) {
   return NULL;
 }
 
-void orc_full_pixel_search_batch(const uint8_t *src, int src_stride, const uint8_t *ref,
-                                 int ref_stride, int w, int h, const OrcDiamondJob *jobs,
-                                 long njobs, int method, int step_param, const OrcMvCost *cost,
-                                 int skip_sad, int32_t *cost_lists, OrcDiamondResult *out,
-                                 int threads) {
+void orc_full_pixel_search_batch_ex(const uint8_t *src, int src_stride, const uint8_t *ref,
+                                    int ref_stride, int w, int h, const OrcDiamondJob *jobs,
+                                    long njobs, int method, int step_param,
+                                    const OrcMvCost *cost, int skip_sad, int32_t *cost_lists,
+                                    OrcDiamondResult *out, int threads,
+                                    const OrcMeshParams *mesh) {
   if (threads < 1) threads = 1;
   if (threads > 64) threads = 64;
   pthread_t tid[64];
   BatchArg args[64];
   for (int t = 0; t < threads; ++t) {
     args[t] = (BatchArg){ src, ref, src_stride, ref_stride, w, h, step_param, skip_sad, method,
-                          cost, jobs, out, cost_lists, njobs * t / threads,
+                          cost, mesh, jobs, out, cost_lists, njobs * t / threads,
                           njobs * (t + 1) / threads };
     if (threads > 1) pthread_create(&tid[t], NULL, batch_worker, &args[t]);
     else batch_worker(&args[t]);
   }
   if (threads > 1)
     for (int t = 0; t < threads; ++t) pthread_join(tid[t], NULL);
+}
+
+void orc_full_pixel_search_batch(const uint8_t *src, int src_stride, const uint8_t *ref,
+                                 int ref_stride, int w, int h, const OrcDiamondJob *jobs,
+                                 long njobs, int method, int step_param, const OrcMvCost *cost,
+                                 int skip_sad, int32_t *cost_lists, OrcDiamondResult *out,
+                                 int threads) {
+  orc_full_pixel_search_batch_ex(src, src_stride, ref, ref_stride, w, h, jobs, njobs, method,
+                                 step_param, cost, skip_sad, cost_lists, out, threads, NULL);
 }
 
 void orc_diamond_batch(const uint8_t *src, int src_stride, const uint8_t *ref, int ref_stride,

@@ -429,19 +429,40 @@ FP_METHODS = {"diamond": 0, "nstep": 1, "nstep_8pt": 2, "hex": 4, "bigdia": 5, "
               "fast_hex": 7, "fast_diamond": 8, "fast_bigdia": 9, "vfast_diamond": 10}
 
 
+class OrcMeshParams(ctypes.Structure):
+    """The mesh fields of FULLPEL_MOTION_SEARCH_PARAMS (mcomp.h:114-123) with
+    the pattern set mesh_patterns[is_intra_mode]; the field order of
+    MESH_FIELDS in tests/golden/gen_fixtures.py is (6 scalars, then range /
+    interval pairs)."""
+    _fields_ = [("run_mesh_search", ctypes.c_int), ("force_mesh_thresh", ctypes.c_int),
+                ("prune_mesh_search", ctypes.c_int),
+                ("mesh_search_mv_diff_threshold", ctypes.c_int),
+                ("fine_search_interval", ctypes.c_int), ("is_intra_mode", ctypes.c_int),
+                ("range", ctypes.c_int * 4), ("interval", ctypes.c_int * 4)]
+
+    @classmethod
+    def from_row(cls, row):
+        """From a fix_mcomp3 "mesh" row (MESH_FIELDS order)."""
+        r = [int(v) for v in row]
+        m = cls(*r[:6])
+        for i in range(4):
+            m.range[i], m.interval[i] = r[6 + 2 * i], r[7 + 2 * i]
+        return m
+
+
 def full_pixel_search_batch(src, ref, stride, w, h, jobs, method="diamond", step_param=0,
                             mv_cost_type=3, sad_per_bit=0, error_per_bit=0, mvjcost=None,
-                            mvcost=None, skip=False, cost_list=False, threads=1):
-    """orc_full_pixel_search_batch: av1_full_pixel_search with any of the
-    DIAMOND / FAST_BIGDIA / BIGDIA methods and any mv cost.  mvjcost int32[4],
-    mvcost int32[2][MV_VALS] (centred at MV_MAX) for MV_COST_ENTROPY.
-    Returns (results, cost_lists int32[n][5] or None)."""
+                            mvcost=None, skip=False, cost_list=False, threads=1, mesh=None):
+    """orc_full_pixel_search_batch_ex: av1_full_pixel_search with any method
+    and any mv cost, and the mesh refinement when `mesh` (OrcMeshParams) is
+    given.  mvjcost int32[4], mvcost int32[2][MV_VALS] (centred at MV_MAX) for
+    MV_COST_ENTROPY.  Returns (results, cost_lists int32[n][5] or None)."""
     L = lib()
-    fn = L.orc_full_pixel_search_batch
+    fn = L.orc_full_pixel_search_batch_ex
     fn.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
                    ctypes.c_int, ctypes.c_void_p, ctypes.c_long, ctypes.c_int, ctypes.c_int,
                    ctypes.POINTER(OrcMvCost), ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
-                   ctypes.c_int]
+                   ctypes.c_int, ctypes.POINTER(OrcMeshParams)]
     jobs = np.ascontiguousarray(jobs)
     keep = []
     c = OrcMvCost(mv_cost_type, sad_per_bit, error_per_bit)
@@ -458,7 +479,8 @@ def full_pixel_search_batch(src, ref, stride, w, h, jobs, method="diamond", step
                                         ("searches", "<i4")], align=True))
     cls = np.full((len(jobs), 5), 0x7FFFFFFF, np.int32) if cost_list else None
     fn(P(src), stride, P(ref), stride, w, h, P(jobs), len(jobs), FP_METHODS[method], step_param,
-       ctypes.byref(c), int(skip), P(cls) if cost_list else None, P(out), threads)
+       ctypes.byref(c), int(skip), P(cls) if cost_list else None, P(out), threads,
+       ctypes.byref(mesh) if mesh is not None else None)
     return out, cls
 
 

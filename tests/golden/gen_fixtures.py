@@ -613,6 +613,42 @@ MS2_CASES = [
     ("SQUARE", 1, "MV_COST_ENTROPY", 1, 0), ("SQUARE", 0, "MV_COST_NONE", 0, 5),
 ]
 MS2_METHODS = ["NSTEP", "NSTEP_8PT", "HEX", "FAST_HEX", "SQUARE"]
+# fix_mcomp3: the exhaustive mesh refinement of av1_full_pixel_search
+# (mcomp.c:1818-1893 -> full_pixel_exhaustive :1603-1680 ->
+# exhaustive_mesh_search :1529-1601): forced by the residue variance after
+# NSTEP / NSTEP_8PT (force_mesh_thresh), or run_mesh_search after any method;
+# prune_mesh_search, fine_search_interval, the intraBC pattern set, the range
+# growth with the start mv, and an illegal first range (a no-op).  Patterns:
+# good_quality_mesh_patterns[0 / 2 / 3], intrabc_mesh_patterns[4]
+# (speed_features.c:25-44), a small first range and an illegal one.
+MESH_PATTERNS = {"good0": [(64, 8), (28, 4), (15, 1), (7, 1)],
+                 "good2": [(64, 8), (14, 2), (7, 1), (7, 1)],
+                 "good3": [(64, 16), (24, 8), (12, 4), (7, 1)],
+                 "ibc4": [(64, 4), (16, 1), (0, 0), (0, 0)],
+                 "small": [(8, 2), (7, 1), (7, 1), (7, 1)],
+                 "bad": [(300, 8), (28, 4), (15, 1), (7, 1)]}
+MS3_BLOCKS = [(16, 16, 6), (8, 8, 4), (32, 32, 2), (16, 8, 3), (4, 4, 3), (64, 64, 1), (8, 32, 1)]
+MS3_CASES = [
+    ("NSTEP", 1, "MV_COST_ENTROPY", 1, 0, dict(force=0, pat="good0")),
+    ("NSTEP_8PT", 0, "MV_COST_L1_HDRES", 0, 2, dict(force=0, prune=1, diff=4, fine=1, pat="good3")),
+    ("DIAMOND", 1, "MV_COST_ENTROPY", 0, 3, dict(run=1, pat="good2")),
+    ("BIGDIA", 1, "MV_COST_NONE", 1, 0, dict(run=1, intra=1, prune=1, diff=64, pat="ibc4")),
+    ("NSTEP", 1, "MV_COST_ENTROPY", 0, 4, dict(force=1 << 16, pat="small")),
+    ("FAST_HEX", 1, "MV_COST_ENTROPY", 0, 0, dict(run=1, pat="bad")),
+    ("SQUARE", 0, "MV_COST_L1_HDRES", 1, 0, dict(run=1, prune=1, diff=0, pat="small")),
+]
+MS3_METHODS = ["NSTEP", "NSTEP_8PT", "DIAMOND", "BIGDIA", "FAST_HEX", "SQUARE"]
+MESH_FIELDS = ["run_mesh_search", "force_mesh_thresh", "prune_mesh_search",
+               "mesh_search_mv_diff_threshold", "fine_search_interval", "is_intra_mode"] + \
+    ["%s%d" % (f, i) for i in range(4) for f in ("range", "interval")]
+
+
+def mesh_row(m):
+    """MESH_FIELDS values of a case's mesh settings (None: mesh off)."""
+    m = m or {}
+    pat = MESH_PATTERNS[m.get("pat", "good0")]
+    return [m.get("run", 0), m.get("force", 0x7FFFFFFF), m.get("prune", 0), m.get("diff", 4),
+            m.get("fine", 0), m.get("intra", 0)] + [v for ri in pat for v in ri]
 
 
 def gen_mcomp(blocks=None, cases=None, methods=("DIAMOND", "BIGDIA", "FAST_BIGDIA"),
@@ -664,7 +700,7 @@ def gen_mcomp(blocks=None, cases=None, methods=("DIAMOND", "BIGDIA", "FAST_BIGDI
              vf=fn("aom_variance%s" % sz), sdx4df=fn("aom_sad%sx4d" % sz),
              sdx3df=fn("aom_sad%sx3d" % sz), sdsx4df=fn("aom_sad_skip_%sx4d" % sz))
         bsize = E["BLOCK_%dX%d" % (bw, bh)]
-        for ci, (mname, use_cl, ctype, skip, step_param) in enumerate(cases):
+        for ci, (mname, use_cl, ctype, skip, step_param, *_) in enumerate(cases):
             for b in range(nblk):
                 by = rnd.generate(H // bh) * bh
                 bx = rnd.generate(W // bw) * bw
@@ -689,10 +725,22 @@ def gen_mcomp(blocks=None, cases=None, methods=("DIAMOND", "BIGDIA", "FAST_BIGDI
                      stride=stride, width=W, height=H)
                 ms = tu.struct_obj("FULLPEL_MOTION_SEARCH_PARAMS")
                 P = ms.buf[0]
-                _set(P, bsize=bsize, vfp=vtab, search_method=E[mname], search_sites=cfgs[mname],
-                     run_mesh_search=0, prune_mesh_search=0, mesh_search_mv_diff_threshold=4,
-                     force_mesh_thresh=mesh_thresh, fine_search_interval=0, is_intra_mode=0,
-                     fast_obmc_search=0)
+                mrow = mesh_row(cases[ci][5]) if len(cases[ci]) > 5 else None
+                if mrow is None:
+                    _set(P, bsize=bsize, vfp=vtab, search_method=E[mname],
+                         search_sites=cfgs[mname], run_mesh_search=0, prune_mesh_search=0,
+                         mesh_search_mv_diff_threshold=4, force_mesh_thresh=mesh_thresh,
+                         fine_search_interval=0, is_intra_mode=0, fast_obmc_search=0)
+                else:
+                    _set(P, bsize=bsize, vfp=vtab, search_method=E[mname],
+                         search_sites=cfgs[mname], fast_obmc_search=0,
+                         **dict(zip(MESH_FIELDS[:6], mrow[:6])))
+                    pats = tu.buffer("struct MESH_PATTERN", 4)
+                    for i in range(4):
+                        _set(pats.buf[i], range=mrow[6 + 2 * i], interval=mrow[7 + 2 * i])
+                    # (the set the search reads: mesh_patterns[is_intra_mode])
+                    _get(P, "mesh_patterns")[0] = pats
+                    _get(P, "mesh_patterns")[1] = pats
                 msb = _get(P, "ms_buffers")
                 _set(msb, ref=rbuf, src=sbuf, second_pred=None, mask=None, mask_stride=0,
                      inv_mask=0, wsrc=None, obmc_mask=None)
@@ -725,7 +773,11 @@ def gen_mcomp(blocks=None, cases=None, methods=("DIAMOND", "BIGDIA", "FAST_BIGDI
                                   "best_row", "best_col", "var", "cl0", "cl1", "cl2", "cl3",
                                   "cl4"])
     out["cases"] = np.array([[list(methods).index(m), cl, E[ct], sk, sp]
-                             for m, cl, ct, sk, sp in cases], np.int32)
+                             for m, cl, ct, sk, sp, *_ in cases], np.int32)
+    if any(len(c) > 5 for c in cases):
+        out["mesh"] = np.array([mesh_row(c[5] if len(c) > 5 else None) for c in cases],
+                               np.int64)
+        out["mesh_fields"] = np.array(MESH_FIELDS)
     out["methods"] = np.array(list(methods))
     np.savez_compressed(os.path.join(HERE, name), **out)
 
@@ -2249,7 +2301,7 @@ def main(argv):
     sections = argv or ["txfm", "qparams", "quant", "inv", "pixel", "wht", "nmv", "mcomp",
                         "subpel", "tpl", "qfacade", "costcoeffs", "trellis", "warp", "compound",
                         "convolve", "compound12", "txfeat", "trellis2", "tplmv", "subpel_up", "tplmv3",
-                        "rdselect", "mcomp2", "scale"]
+                        "rdselect", "mcomp2", "scale", "mcomp3"]
     t0 = time.time()
     ttx = None
     if "txfm" in sections or "inv" in sections or "wht" in sections:
@@ -2279,6 +2331,8 @@ def main(argv):
     if "mcomp2" in sections:
         gen_mcomp(MS2_BLOCKS, MS2_CASES, MS2_METHODS, "fix_mcomp2.npz", seed_off=5,
                   mesh_thresh=0x7FFFFFFF)
+    if "mcomp3" in sections:
+        gen_mcomp(MS3_BLOCKS, MS3_CASES, MS3_METHODS, "fix_mcomp3.npz", seed_off=6)
     if "subpel" in sections:
         gen_subpel()
     if "tpl" in sections:

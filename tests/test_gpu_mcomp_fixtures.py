@@ -4,12 +4,15 @@ tests/golden/gen_fixtures.py): DIAMOND, BIGDIA (do_init_search 1) and
 FAST_BIGDIA, MV_COST_ENTROPY with the default-context nmv cost tables, L1 and
 none, with and without the downsampled-SAD speed feature (and its quality
 recheck) and with and without a cost list -- best mv, returned var cost and
-the five cost-list entries bit-exact.  No oracle in the loop."""
+the five cost-list entries bit-exact.  No oracle in the loop, except in
+test_full_pixel_search_mesh_vs_oracle (wider mesh settings against the
+restatement that fix_mcomp3 pins)."""
 import os
 
 import numpy as np
 import pytest
 
+import _oracle as O
 from _mcomp_fix import MS_METHODS, mcomp_groups
 
 pytestmark = pytest.mark.gpu
@@ -85,6 +88,115 @@ def test_full_pixel_search_methods2_vs_reference(tiled):
                                           err_msg=msg)
         n += len(rows)
     assert n == len(F2["jobs"])
+
+
+def _mesh(row):
+    from lavish_dsp import motion as M
+    r = [int(v) for v in row]
+    return M.MeshParams.make([(r[6 + 2 * i], r[7 + 2 * i]) for i in range(4)], *r[:6])
+
+
+@pytest.mark.parametrize("tiled", [False, True])
+def test_full_pixel_search_mesh_vs_reference(tiled):
+    """lavish_full_pixel_search_batch_mesh against av1_full_pixel_search with
+    the exhaustive mesh refinement executed from the reference
+    (tests/golden/fix_mcomp3.npz: force_mesh_thresh after NSTEP / NSTEP_8PT,
+    run_mesh_search after DIAMOND / BIGDIA / FAST_HEX / SQUARE, pruning, the
+    fine interval, the intraBC patterns, range growth, an illegal pattern;
+    cost lists, downsampled SAD) -- bit-exact."""
+    import torch
+    from lavish_dsp import motion as M
+    F3 = dict(np.load(os.path.join(GOLD, "fix_mcomp3.npz")))
+    methods = [str(m).lower() for m in F3["methods"]]
+    src = torch.from_numpy(F3["src"]).cuda()
+    refs = torch.from_numpy(np.ascontiguousarray(F3["refs"])).cuda()
+    tiles = M.RefTiles(refs, src.stride(0)).build() if tiled else None
+    costs = M.MvCosts(F3["mvjcost_lp"], F3["mvcost_lp"])
+    n = 0
+    for case, bw, bh, epb, spb, rec, rows, J in mcomp_groups(F3):
+        m, use_cl, ctype, skip, sp = (int(v) for v in case)
+        mesh = _mesh(F3["mesh"][int(rows[0, J["case"]])])
+        cp = costs.cost_params(spb, epb, ctype)
+        out, cl = M.full_pixel_search_batch(src, refs, bw, bh, M.to_device(rec), cp,
+                                            methods[m], sp, bool(skip), bool(use_cl),
+                                            tiles=tiles, mesh=mesh)
+        torch.cuda.synchronize()
+        res = M.results_numpy(out)
+        msg = "%s case %s %dx%d" % (methods[m], [int(v) for v in case], bw, bh)
+        np.testing.assert_array_equal(res["best_row"], rows[:, J["best_row"]], err_msg=msg)
+        np.testing.assert_array_equal(res["best_col"], rows[:, J["best_col"]], err_msg=msg)
+        np.testing.assert_array_equal(res["bestsme"], rows[:, J["var"]], err_msg=msg)
+        if use_cl:
+            np.testing.assert_array_equal(cl.cpu().numpy(), rows[:, J["cl0"]:J["cl4"] + 1],
+                                          err_msg=msg)
+        n += len(rows)
+    assert n == len(F3["jobs"])
+
+
+MESH_SETS = [  # (patterns, run, force_thresh, prune, diff, fine, intra)
+    ([(64, 8), (28, 4), (15, 1), (7, 1)], 1, 0x7FFFFFFF, 0, 4, 0, 0),
+    ([(64, 16), (24, 8), (12, 4), (7, 1)], 0, 0, 1, 2, 1, 0),
+    ([(9, 3), (7, 1), (0, 0), (0, 0)], 1, 0, 1, 1, 0, 1),
+    ([(16, 1), (7, 1), (7, 1), (7, 1)], 0, 1 << 14, 0, 4, 0, 0),
+]
+
+
+@pytest.mark.parametrize("mi", range(len(MESH_SETS)))
+@pytest.mark.parametrize("method", ["nstep", "nstep_8pt", "diamond", "fast_bigdia", "hex"])
+def test_full_pixel_search_mesh_vs_oracle(mi, method):
+    """The mesh refinement after five methods at four mesh settings (every
+    fix_mcomp3 job geometry, entropy cost, cost lists, downsampled SAD on
+    alternate sizes) against the oracle restatement (pinned to the reference
+    by the fixture test above)."""
+    import torch
+    from lavish_dsp import motion as M
+    F3 = dict(np.load(os.path.join(GOLD, "fix_mcomp3.npz")))
+    src = torch.from_numpy(F3["src"]).cuda()
+    refs = torch.from_numpy(np.ascontiguousarray(F3["refs"])).cuda()
+    costs = M.MvCosts(F3["mvjcost_lp"], F3["mvcost_lp"])
+    pats, run, thr, prune, diff, fine, intra = MESH_SETS[mi]
+    mesh = M.MeshParams.make(pats, run, thr, prune, diff, fine, intra)
+    omesh = O.OrcMeshParams(run, thr, prune, diff, fine, intra)
+    for i, (r, iv) in enumerate(pats):
+        omesh.range[i], omesh.interval[i] = r, iv
+    stride = F3["src"].shape[1]
+    for k, (case, bw, bh, epb, spb, rec, rows, J) in enumerate(mcomp_groups(F3)):
+        skip = k % 2
+        cp = costs.cost_params(spb, epb, 0)
+        out, cl = M.full_pixel_search_batch(src, refs, bw, bh, M.to_device(rec), cp, method, 1,
+                                            bool(skip), True, mesh=mesh)
+        torch.cuda.synchronize()
+        res = M.results_numpy(out)
+        exp, ecl = O.full_pixel_search_batch(F3["src"], F3["refs"], stride, bw, bh, rec, method,
+                                             1, 0, spb, epb, F3["mvjcost_lp"], F3["mvcost_lp"],
+                                             skip=bool(skip), cost_list=True, mesh=omesh)
+        msg = "%s %dx%d" % (method, bw, bh)
+        for f in ("best_row", "best_col", "bestsme"):
+            np.testing.assert_array_equal(res[f], exp[f], err_msg=msg + " " + f)
+        np.testing.assert_array_equal(cl.cpu().numpy(), ecl, err_msg=msg + " cost list")
+
+
+def test_full_pixel_search_mesh_rejects():
+    """A later mesh pass the walk can reach with interval < 1: -6 (the
+    reference's loop would not end); an illegal first pattern: the results
+    of the search without mesh."""
+    import torch
+    from lavish_dsp import motion as M
+    F3 = dict(np.load(os.path.join(GOLD, "fix_mcomp3.npz")))
+    src = torch.from_numpy(F3["src"]).cuda()
+    refs = torch.from_numpy(np.ascontiguousarray(F3["refs"])).cuda()
+    costs = M.MvCosts(F3["mvjcost_lp"], F3["mvcost_lp"])
+    case, bw, bh, epb, spb, rec, rows, J = next(iter(mcomp_groups(F3)))
+    cp = costs.cost_params(spb, epb, 0)
+    jobs = M.to_device(rec)
+    bad = M.MeshParams.make([(64, 8), (28, 0), (15, 1), (7, 1)], run_mesh_search=1)
+    with pytest.raises(ValueError):
+        M.full_pixel_search_batch(src, refs, bw, bh, jobs, cp, "diamond", 1, mesh=bad)
+    noop = M.MeshParams.make([(300, 8), (28, 0), (15, 1), (7, 1)], run_mesh_search=1)
+    a, _ = M.full_pixel_search_batch(src, refs, bw, bh, jobs, cp, "diamond", 1, mesh=noop)
+    b, _ = M.full_pixel_search_batch(src, refs, bw, bh, jobs, cp, "diamond", 1)
+    torch.cuda.synchronize()
+    assert torch.equal(a, b)
 
 
 def test_full_pixel_search_rejects(F):

@@ -252,6 +252,40 @@ def test_full_pixel_search_methods2_vs_reference():
     assert seen == {"nstep", "nstep_8pt", "hex", "fast_hex", "square"}
 
 
+def test_full_pixel_search_mesh_vs_reference():
+    """orc_full_pixel_search_batch_ex against av1_full_pixel_search executed
+    from the reference with the exhaustive mesh refinement
+    (tests/golden/fix_mcomp3.npz; exhaustive_mesh_search / full_pixel_exhaustive,
+    mcomp.c:1529-1680, the tail of av1_full_pixel_search :1818-1893): forced
+    by force_mesh_thresh after NSTEP / NSTEP_8PT, run_mesh_search after
+    DIAMOND / BIGDIA / FAST_HEX / SQUARE, pruning, the fine interval, the
+    intraBC pattern set, the range growth and an illegal pattern."""
+    F = _load("fix_mcomp3.npz")
+    methods = [str(m).lower() for m in F["methods"]]
+    stride = F["src"].shape[1]
+    n = moved = 0
+    for case, bw, bh, epb, spb, rec, rows, J in mcomp_groups(F):
+        m, use_cl, ctype, skip, sp = (int(v) for v in case)
+        mesh = O.OrcMeshParams.from_row(F["mesh"][int(rows[0, J["case"]])])
+        res, cl = O.full_pixel_search_batch(
+            F["src"], F["refs"], stride, bw, bh, rec, methods[m], sp, ctype, spb, epb,
+            F["mvjcost_lp"], F["mvcost_lp"], skip=bool(skip), cost_list=bool(use_cl), mesh=mesh)
+        plain, _ = O.full_pixel_search_batch(
+            F["src"], F["refs"], stride, bw, bh, rec, methods[m], sp, ctype, spb, epb,
+            F["mvjcost_lp"], F["mvcost_lp"], skip=bool(skip))
+        msg = "case %s %dx%d" % (list(case), bw, bh)
+        np.testing.assert_array_equal(res["best_row"], rows[:, J["best_row"]], err_msg=msg)
+        np.testing.assert_array_equal(res["best_col"], rows[:, J["best_col"]], err_msg=msg)
+        np.testing.assert_array_equal(res["bestsme"], rows[:, J["var"]], err_msg=msg)
+        if use_cl:
+            np.testing.assert_array_equal(cl, rows[:, J["cl0"]:J["cl4"] + 1], err_msg=msg)
+        moved += int(((plain["best_row"] != res["best_row"]) |
+                      (plain["best_col"] != res["best_col"])).sum())
+        n += len(rows)
+    assert n == len(F["jobs"])
+    assert moved > 0  # the mesh changed some results
+
+
 def test_subpel_search_vs_reference():
     """orc_subpel_search_batch against av1_find_best_sub_pixel_tree_pruned
     (_more) executed from the reference, from full-pel results with their
