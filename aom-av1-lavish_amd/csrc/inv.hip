@@ -79,18 +79,26 @@ __device__ __forceinline__ void inv_1d_then(int kind, const int32_t* in, F&& use
   }
 }
 
-// one tile: the P jobs from j0
+// LDS of one tile: the jobs, the staged coefficients and the row outputs
+// (rows >= KH are zero, not stored); bytes
+template <int W, int H>
+constexpr int inv_lds_bytes() {
+  using T = InvTile<W, H>;
+  return (int)(T::P * sizeof(InvJob)) + 4 * T::P * T::NC + 4 * T::P * T::KH * T::T1S;
+}
+
+// one tile: the P jobs from j0; lds: inv_lds_bytes<W, H>() bytes, 8-aligned
 template <int W, int H, int BDI, typename PIX>
 __device__ __forceinline__ void inv_tile(const int32_t* __restrict__ dq,
                                          const InvJob* __restrict__ jobs, int njobs, int j0,
-                                         PIX* __restrict__ dst, int stride) {
+                                         PIX* __restrict__ dst, int stride, char* lds) {
   using T = InvTile<W, H>;
   using C = TxCfg<W, H>;
   using B = Bd<BDI>;
   constexpr int P = T::P, T1S = T::T1S;
-  __shared__ int32_t cf[P * T::NC];
-  __shared__ int32_t t1[P * T::KH * T1S];   // rows >= KH are zero, not stored
-  __shared__ InvJob jb[P];
+  InvJob* const jb = (InvJob*)lds;
+  int32_t* const cf = (int32_t*)(lds + P * sizeof(InvJob));
+  int32_t* const t1 = cf + P * T::NC;
 
   const int lane = threadIdx.x;
   __syncthreads();  // the previous tile's readers of jb / cf / t1 are done
@@ -231,6 +239,7 @@ __global__ __launch_bounds__(64) void inv_tile_kernel(const int32_t* __restrict_
                                                       int slot_cap, PIX* __restrict__ dst,
                                                       int stride) {
   constexpr int P = InvTile<W, H>::P;
+  __shared__ __attribute__((aligned(16))) char lds[inv_lds_bytes<W, H>()];
   const int tps = slot_cnt ? (slot_cap + P - 1) / P : 1;  // tiles per slot
   const int ntiles = slot_cnt ? (njobs / slot_cap) * tps : (njobs + P - 1) / P;
   for (int t = blockIdx.x; t < ntiles; t += gridDim.x) {
@@ -238,9 +247,10 @@ __global__ __launch_bounds__(64) void inv_tile_kernel(const int32_t* __restrict_
       const int sl = t / tps, k = t - sl * tps;
       const int c = slot_cnt[sl];
       if (k * P >= c) continue;
-      inv_tile<W, H, BDI, PIX>(dq, jobs, sl * slot_cap + c, sl * slot_cap + k * P, dst, stride);
+      inv_tile<W, H, BDI, PIX>(dq, jobs, sl * slot_cap + c, sl * slot_cap + k * P, dst, stride,
+                               lds);
     } else {
-      inv_tile<W, H, BDI, PIX>(dq, jobs, njobs, t * P, dst, stride);
+      inv_tile<W, H, BDI, PIX>(dq, jobs, njobs, t * P, dst, stride, lds);
     }
   }
 }
@@ -279,7 +289,76 @@ int dispatch_bd(const int32_t* dq, const LavishInvJob* jobs, int njobs, const ui
   return 0;
 }
 
+// ---------------------------------------------------------------------------
+// The C4 reconstruction's inverse transforms in one launch (rdo.hip,
+// sb_decide_kernel's per-SB job slots): wave (k, sb) -- k-major, so the
+// first nsb waves take every SB's first tile -- runs tile k of the size SB
+// sb chose, if the SB has that many coded blocks; every other wave leaves at
+// once.  The sizes' tiles share one LDS buffer (the largest size's), so the
+// one kernel holds no more LDS than the largest per-size kernel.  Replaces
+// one launch per candidate size (and the fan-out / fan-in around them).
+template <int W, int H>
+constexpr int inv_tpsb() {  // tiles per SB of a size
+  return ((64 / W) * (64 / H) + InvTile<W, H>::P - 1) / InvTile<W, H>::P;
+}
+
+#define LAVISH_INV_SIZES(X)                                                                      \
+  X(0, 4, 4) X(1, 8, 8) X(2, 16, 16) X(3, 32, 32) X(4, 64, 64) X(5, 4, 8) X(6, 8, 4) X(7, 8, 16) \
+  X(8, 16, 8) X(9, 16, 32) X(10, 32, 16) X(11, 32, 64) X(12, 64, 32) X(13, 4, 16) X(14, 16, 4)  \
+  X(15, 8, 32) X(16, 32, 8) X(17, 16, 64) X(18, 64, 16)
+
+constexpr int inv_max_lds() {
+  int m = 0;
+#define LAVISH_INV_LDS(S, W, H) m = m > inv_lds_bytes<W, H>() ? m : inv_lds_bytes<W, H>();
+  LAVISH_INV_SIZES(LAVISH_INV_LDS)
+#undef LAVISH_INV_LDS
+  return m;
+}
+
+template <int BDI>
+__global__ __launch_bounds__(64) void recon_sb_kernel(InvSbArgs a) {
+  __shared__ __attribute__((aligned(16))) char lds[inv_max_lds()];
+  const int sb = blockIdx.x % a.nsb, k = blockIdx.x / a.nsb;
+  const int s = a.sb_tx_size[sb];
+  if (s >= 19) return;  // no candidate size tiles this SB: recon = pred
+  const int c = a.cnt[s][sb];
+  switch (s) {
+#define LAVISH_INV_CASE(S, W, H)                                                               \
+  case S: {                                                                                    \
+    constexpr int P = InvTile<W, H>::P, CAP = (64 / W) * (64 / H);                            \
+    if (k * P >= c) return;                                                                    \
+    inv_tile<W, H, BDI, uint16_t>(a.dq[S], (const InvJob*)a.jobs[S], sb * CAP + c,              \
+                                  sb * CAP + k * P, a.dst, a.stride, lds);                     \
+    return;                                                                                    \
+  }
+    LAVISH_INV_SIZES(LAVISH_INV_CASE)
+#undef LAVISH_INV_CASE
+    default: return;
+  }
+}
+
 }  // namespace
+
+int recon_sb_launch(const InvSbArgs& a, int bd, hipStream_t s) {
+  if (a.nsb <= 0) return 0;
+  int tps = 1;  // tiles per SB of the candidate size with the most
+  for (int t = 0; t < 19; ++t) {
+    if (!a.jobs[t]) continue;
+    int n = 0;
+#define LAVISH_INV_TPS(S, W, H) \
+    if (t == S) n = inv_tpsb<W, H>();
+    LAVISH_INV_SIZES(LAVISH_INV_TPS)
+#undef LAVISH_INV_TPS
+    tps = n > tps ? n : tps;
+  }
+  const dim3 grid((unsigned)(a.nsb * tps));
+  if (bd == 8) hipLaunchKernelGGL(recon_sb_kernel<0>, grid, dim3(64), 0, s, a);
+  else if (bd == 10) hipLaunchKernelGGL(recon_sb_kernel<1>, grid, dim3(64), 0, s, a);
+  else if (bd == 12) hipLaunchKernelGGL(recon_sb_kernel<2>, grid, dim3(64), 0, s, a);
+  else return -4;
+  LAVISH_CHECK(hipGetLastError());
+  return 0;
+}
 
 int inv_txfm_add_batch(const int32_t* dq, int tx_size, const LavishInvJob* jobs, int njobs,
                        void* dst, int stride, int bd, int highbd, hipStream_t s,

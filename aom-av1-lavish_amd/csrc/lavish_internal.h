@@ -45,6 +45,19 @@ int txq_plane_64(const int16_t* residual, int stride, int width, int height, int
 // inverse transform batch (inv.hip); slot_cnt (device, nullable): the job
 // list is njobs / slot_cap slots of slot_cap jobs, of which the first
 // slot_cnt[slot] are live (job lists built on the device)
+// the C4 reconstruction's inverse transforms in one launch (inv.hip): per
+// candidate size t (jobs[t] != nullptr) the per-SB job slots and counts
+// sb_decide_kernel wrote, the dequantized coefficients, the SBs' chosen sizes
+struct InvSbArgs {
+  const int32_t* dq[19];
+  const LavishInvJob* jobs[19];
+  const uint16_t* cnt[19];
+  const uint8_t* sb_tx_size;
+  int nsb;
+  uint16_t* dst;
+  int stride;
+};
+int recon_sb_launch(const InvSbArgs& a, int bd, hipStream_t s);
 int inv_txfm_add_batch(const int32_t* dq, int tx_size, const LavishInvJob* jobs, int njobs,
                        void* dst, int stride, int bd, int highbd, hipStream_t s,
                        const uint16_t* slot_cnt = nullptr, int slot_cap = 0);

@@ -188,6 +188,8 @@ struct SbArgs {
   int sbw, sbh;                        // superblocks per row / column
   int width, height, stride;
   uint8_t* sb_tx_size;
+  const uint16_t* pred;                // the SB's recon = pred, before the inverse adds
+  uint16_t* recon;
 };
 
 // per SB64: the candidate TX size whose blocks' summed RD cost is lowest
@@ -198,6 +200,8 @@ struct SbArgs {
 // not reconstructed at all.
 // One wave64 per SB: lanes stride the SB's blocks of a size, a 64-bit xor
 // reduction sums their costs; the size scan stays sequential (strict <).
+// The wave also writes the SB's reconstruction base (recon = pred), which
+// the inverse adds then build on.
 // Jobs go to the SB's own slot of each size's list (no atomics, nothing to
 // zero first): the chosen size's coded blocks, compacted by ballot, and a
 // count of 0 in every other size's slot.
@@ -207,6 +211,30 @@ __global__ __launch_bounds__(256) void sb_decide_kernel(SbArgs a) {
   if (sb >= a.sbw * a.sbh) return;
   const int sy = sb / a.sbw, sx = sb - sy * a.sbw;
   const int y1 = min(64, a.height - sy * 64), x1 = min(64, a.width - sx * 64);
+  {
+    // recon = pred over the SB: 16-byte rows when the SB is whole and aligned
+    const size_t o = (size_t)sy * 64 * a.stride + (size_t)sx * 64;
+    const uint16_t* p = a.pred + o;
+    uint16_t* r = a.recon + o;
+    const bool vec = x1 == 64 && ((((uintptr_t)p | (uintptr_t)r | ((uintptr_t)a.stride * 2)) & 15) == 0);
+    if (vec) {
+      typedef uint32_t u4 __attribute__((ext_vector_type(4)));
+      u4 v[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int row = i * 8 + (lane >> 3);
+        if (row < y1) v[i] = *(const u4*)(p + (size_t)row * a.stride + 8 * (lane & 7));
+      }
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int row = i * 8 + (lane >> 3);
+        if (row < y1) *(u4*)(r + (size_t)row * a.stride + 8 * (lane & 7)) = v[i];
+      }
+    } else {
+      for (int row = 0; row < y1; ++row)
+        if (lane < x1) r[(size_t)row * a.stride + lane] = p[(size_t)row * a.stride + lane];
+    }
+  }
   int64_t best = INT64_MAX;
   int best_s = 255;
   for (int i = 0; i < a.nsizes; ++i) {
@@ -435,6 +463,8 @@ int rdo_reconstruct_impl(uint32_t size_mask, const LavishRdoBlock* const* rec,
   a.height = height;
   a.stride = stride;
   a.sb_tx_size = sb_tx_size;
+  a.pred = pred;
+  a.recon = recon;
   const int nsb = a.sbw * a.sbh;
   size_t joff[19] = {}, coff[19] = {};
   const size_t bytes = recon_scratch_layout(a, nsb, joff, coff);
@@ -449,24 +479,23 @@ int rdo_reconstruct_impl(uint32_t size_mask, const LavishRdoBlock* const* rec,
     a.jobs[t] = (LavishInvJob*)(scratch + joff[t]);
     a.cnt[t] = (uint16_t*)(scratch + coff[t]);
   }
+  // the decision and recon = pred, then the chosen coded blocks' residuals
+  // added by one launch over every size (recon_sb_kernel, inv.hip): every SB
+  // chose one size, so the tiles write disjoint pixels
   hipLaunchKernelGGL(sb_decide_kernel, dim3((nsb + 3) / 4), dim3(256), 0, s, a);
   LAVISH_CHECK(hipGetLastError());
-  // recon = pred, then add the chosen coded blocks' residuals: the sizes'
-  // inverse launches side by side over the fan-out streams (every SB chose
-  // one size, so they write disjoint pixels; a size no SB chose still costs a
-  // launch of ~6 us, which then overlaps the others instead of following them)
-  LAVISH_CHECK(hipMemcpy2DAsync(recon, (size_t)stride * 2, pred, (size_t)stride * 2,
-                                (size_t)width * 2, height, hipMemcpyDeviceToDevice, s));
-  hipStream_t* fs = fan_out(s);
-  int rc = 0, k = 0;
-  for (int i = 0; i < a.nsizes && rc == 0; ++i) {
+  InvSbArgs ia{};
+  for (int i = 0; i < a.nsizes; ++i) {
     const int t = a.sizes[i];
-    if ((width / tx_w(t)) * (height / tx_h(t)) == 0) continue;
-    const int cap = (64 / tx_w(t)) * (64 / tx_h(t));
-    rc = inv_txfm_add_batch(dqcoeff[t], t, a.jobs[t], nsb * cap, recon, stride, bd, 1,
-                            fs[k++ % fan_width()], a.cnt[t], cap);
+    ia.dq[t] = dqcoeff[t];
+    ia.jobs[t] = a.jobs[t];
+    ia.cnt[t] = a.cnt[t];
   }
-  fan_in(s);
+  ia.sb_tx_size = sb_tx_size;
+  ia.nsb = nsb;
+  ia.dst = recon;
+  ia.stride = stride;
+  const int rc = recon_sb_launch(ia, bd, s);
   if (shared) t_rs.release(s);
   return rc;
 }

@@ -9,7 +9,15 @@ all-gather of the reconstructed row for next-row intra prediction").  Two
 forms, both one process per GPU over torch.distributed (RCCL on the GPUs,
 gloo on the CPU for the tests):
 
-band (the throughput form, `sharded_frame`):
+tiles (the one-step form, `tiled_frame`):
+  One rectangle per rank, a gr x gc grid of whole-SB tiles with the
+  smallest largest tile (`grid_partition`; at 4K exactly R C / G SBs per
+  rank for G = 2, 4, 8), computed as a single C4 step and all-gathered once.
+  A small rank share is latency-bound (a step costs about one decision
+  wave's lifetime whatever its width), so one step per rank, not a band's
+  and a tail's, is what the per-rank time scales with.
+
+band (`sharded_frame`):
   The frame's R SB rows are dealt as floor(R / G) contiguous full rows per
   rank plus the R mod G leftover rows cut into G equal column segments
   (one each), so every rank holds exactly R / G SB rows of work: at 4K
@@ -87,6 +95,37 @@ def partition(height, width, world):
                 y0 = (full * world + row) * SB
                 tail = (y0, min(y0 + SB, height), c0 * SB, min(c1 * SB, width))
         out.append((band, tail))
+    return out
+
+
+def grid_partition(height, width, world):
+    """The tile form's rectangles: one (y0, y1, x0, x1) per rank, rank-major
+    over a gr x gc grid (gr * gc = world) of whole-SB tiles -- SB rows and SB
+    columns dealt as evenly as integers allow.  The grid is the factorisation
+    with the smallest largest tile (ties: fewer column cuts, so rows stay
+    long): at 4K (34 x 60 SBs) 2 x 1, 2 x 2, 2 x 4 tiles of exactly R C / G
+    SBs for G = 2, 4, 8."""
+    R, C = sb_rows(height), sb_cols(width)
+    best = None
+    for gr in range(1, world + 1):
+        if world % gr:
+            continue
+        gc = world // gr
+        if gr > R or gc > C:
+            continue
+        biggest = -(-R // gr) * -(-C // gc)
+        if best is None or biggest < best[0] or (biggest == best[0] and gc < best[2]):
+            best = (biggest, gr, gc)
+    if best is None:
+        raise ValueError("a %dx%d frame has fewer SBs than %d ranks in any grid" %
+                         (width, height, world))
+    _, gr, gc = best
+    out = []
+    for i in range(gr):
+        r0, r1 = R * i // gr, R * (i + 1) // gr
+        for j in range(gc):
+            c0, c1 = C * j // gc, C * (j + 1) // gc
+            out.append((r0 * SB, min(r1 * SB, height), c0 * SB, min(c1 * SB, width)))
     return out
 
 
@@ -174,6 +213,21 @@ def sharded_frame(height, width, rank, world, process_rect, group=None, like=Non
     else:
         for f in fin:
             f()
+    return full
+
+
+def tiled_frame(height, width, rank, world, process_rect, group=None, like=None):
+    """The tile form: this rank's one grid_partition rectangle (a single C4
+    step, so a rank pays one step's latency, not a band's and a tail's),
+    then one all-gather of the equally padded tiles into the whole
+    reconstructed frame (identical on every rank)."""
+    import torch
+    rects = grid_partition(height, width, world)
+    local = process_rect(*rects[rank])
+    if world == 1:
+        return local
+    full = torch.empty((height, width), dtype=local.dtype, device=local.device)
+    _gather_rects(local, rects, full, group, async_op=False)()
     return full
 
 

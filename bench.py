@@ -85,7 +85,7 @@ def parse():
                          "captured HIP graph")
     ap.add_argument("--c5-chunks", type=int, default=4,
                     help="c5 wavefront: column chunks per SB row")
-    ap.add_argument("--c5-form", choices=("band", "wavefront"), default="band",
+    ap.add_argument("--c5-form", choices=("tiles", "band", "wavefront"), default="tiles",
                     help="C5 sharding: balanced band + tail segments with overlapped "
                          "all-gathers, or the row-wavefront with p2p edges (lavish_dsp/shard.py)")
     ap.add_argument("--c5-emulate", default="",
@@ -395,15 +395,15 @@ def c4_leg(L, steps, warmup, rdmult, qindex, W=3840, H=2160):
 
 
 def c5_leg(L, steps, warmup, rdmult, qindex, world, rank, W=3840, H=2160, graphs=True,
-           c4_ms=None):
+           c4_ms=None, form="tiles"):
     """C5 (BASELINE configs[4]) inside the default line at N > 1: the C4 step
-    of ONE 4K 10-bit frame sharded over the ranks in the band form
-    (lavish_dsp/shard.py: floor(R / G) SB rows per rank + a column segment of
-    the leftover rows, each part's reconstruction all-gathered over RCCL as
-    soon as it is computed), timed barrier to barrier, max over ranks; plus
-    each rank's compute alone (its band + tail rectangles, no exchange) and
-    the all-gathers alone (the same tensors, no compute), so the line shows
-    where the time goes."""
+    of ONE 4K 10-bit frame sharded over the ranks (lavish_dsp/shard.py) --
+    tiles: one grid tile of R C / G SBs per rank, one all-gather of the
+    tiles over RCCL; band: floor(R / G) SB rows per rank + a column segment
+    of the leftover rows, each part all-gathered as soon as it is computed
+    -- timed barrier to barrier, max over ranks; plus each rank's compute
+    alone (its rectangles, no exchange) and the all-gathers alone (the same
+    tensors, no compute), so the line shows where the time goes."""
     import torch
     import torch.distributed as dist
     import lavish_dsp.shard as shard
@@ -417,7 +417,10 @@ def c5_leg(L, steps, warmup, rdmult, qindex, world, rank, W=3840, H=2160, graphs
     frame_out = torch.empty_like(src)
     proc = shard.c4_rect_processor(src, pred, qp, rdmult, 10, frames, out=frame_out,
                                    graphs=graphs)
-    parts = shard.partition(H, W, world)
+    if form == "tiles":
+        parts = [(r,) for r in shard.grid_partition(H, W, world)]
+    else:
+        parts = shard.partition(H, W, world)
     mine = [r for r in parts[rank] if r is not None]
 
     def timed(fn, n):
@@ -439,12 +442,15 @@ def c5_leg(L, steps, warmup, rdmult, qindex, world, rank, W=3840, H=2160, graphs
     streams = [torch.cuda.Stream(), torch.cuda.Stream()] if graphs else None
 
     def frame_step():
-        shard.sharded_frame(H, W, rank, world, proc, streams=streams)
+        if form == "tiles":
+            shard.tiled_frame(H, W, rank, world, proc)
+        else:
+            shard.sharded_frame(H, W, rank, world, proc, streams=streams)
 
     caller = torch.cuda.current_stream()
 
     def compute_only():  # the rank's band and tail side by side, as in frame_step
-        if streams is None:
+        if streams is None or len(mine) == 1:
             for r in mine:
                 proc(*r)
             return
@@ -459,7 +465,7 @@ def c5_leg(L, steps, warmup, rdmult, qindex, world, rank, W=3840, H=2160, graphs
 
     # the exchange alone: each phase's all-gather of equal zero-padded parts
     gathers = []
-    for phase in range(2):
+    for phase in range(len(parts[0])):
         rects = [p[phase] for p in parts]
         if all(r is None for r in rects):
             continue
@@ -493,10 +499,12 @@ def c5_leg(L, steps, warmup, rdmult, qindex, world, rank, W=3840, H=2160, graphs
     else:
         per_rank = [round(comp_ms, 4)]
     sb = sb64_count(W, H)
+    how = ("tile form: one grid tile of whole SBs per rank, the tiles' reconstruction "
+           "all-gathered over RCCL" if form == "tiles" else
+           "band form: floor(R/G) SB rows + a column segment of the leftover rows per rank; "
+           "each part's reconstruction all-gathered over RCCL")
     out = {"workload": "c5: one %dx%d 10-bit frame per step, the C4 step sharded over %d ranks "
-                       "(band form: floor(R/G) SB rows + a column segment of the leftover rows "
-                       "per rank; each part's reconstruction all-gathered over RCCL)"
-                       % (W, H, world),
+                       "(%s)" % (W, H, world, how), "form": form,
            "n_ranks": world, "ms_per_frame": round(step_ms, 4),
            "SB64_per_s": round(sb / (step_ms * 1e-3), 1),
            "rank_rects": [list(p) for p in parts],
@@ -510,14 +518,15 @@ def c5_leg(L, steps, warmup, rdmult, qindex, world, rank, W=3840, H=2160, graphs
     return out
 
 
-def c5_emulate(H, W, proc, worlds, steps, warmup, frame_ms):
-    """On one GPU, rank g's share of the band form for each world size G:
-    its partition() rectangles (band and tail segment side by side on two
-    streams, as sharded_frame runs them) replayed as captured graphs
-    with nothing else on the device, timed with HIP events -- the
-    compute-only time of that rank at G GPUs (no exchange, no contention
-    from other ranks: each rank owns its GPU).  Reports every rank's time,
-    the slowest, and the compute-only speed-up frame_ms / slowest."""
+def c5_emulate(H, W, proc, worlds, steps, warmup, frame_ms, form="tiles"):
+    """On one GPU, rank g's share of the C5 form for each world size G --
+    tiles: its one grid_partition() tile; band: its partition() rectangles
+    (band and tail segment side by side on two streams, as sharded_frame
+    runs them) -- replayed as captured graphs with nothing else on the
+    device, timed with HIP events: the compute-only time of that rank at G
+    GPUs (no exchange, no contention from other ranks: each rank owns its
+    GPU).  Reports every rank's time, the slowest, and the compute-only
+    speed-up frame_ms / slowest."""
     import torch
     import lavish_dsp.shard as shard
     stream = torch.cuda.current_stream()
@@ -525,6 +534,9 @@ def c5_emulate(H, W, proc, worlds, steps, warmup, frame_ms):
     out = {}
 
     def rank_step(rects):  # band and tail side by side (shard.sharded_frame's streams)
+        if len(rects) == 1:
+            proc(*rects[0])
+            return
         ev = torch.cuda.Event()
         ev.record(stream)
         for st, r in zip(side, rects):
@@ -535,8 +547,11 @@ def c5_emulate(H, W, proc, worlds, steps, warmup, frame_ms):
             stream.wait_stream(st)
 
     for G in worlds:
-        parts = shard.partition(H, W, G)
-        per = []
+        if form == "tiles":
+            parts = [(r,) for r in shard.grid_partition(H, W, G)]
+        else:
+            parts = shard.partition(H, W, G)
+        per, enq = [], []
         for g in range(G):
             rects = [r for r in parts[g] if r is not None]
             for _ in range(warmup):
@@ -544,14 +559,18 @@ def c5_emulate(H, W, proc, worlds, steps, warmup, frame_ms):
             torch.cuda.synchronize()
             ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
                   for _ in range(steps)]
+            t0 = time.perf_counter()
             for a, b in ev:
                 a.record(stream)
                 rank_step(rects)
                 b.record(stream)
+            enq.append((time.perf_counter() - t0) / steps * 1e3)
             torch.cuda.synchronize()
             per.append(sum(a.elapsed_time(b) for a, b in ev) / steps)
         slow = max(per)
-        out[str(G)] = {"rank_ms": [round(x, 4) for x in per], "max_rank_ms": round(slow, 4),
+        out[str(G)] = {"form": form, "rank_ms": [round(x, 4) for x in per],
+                       "max_rank_ms": round(slow, 4),
+                       "host_enqueue_ms": round(max(enq), 4),
                        "projected_speedup_compute_only": round(frame_ms / slow, 3),
                        "rects": [list(p) for p in parts]}
     return out
@@ -597,6 +616,9 @@ def main_c4(args):
             def step():
                 return shard.wavefront_frame(H, W, rank, world, proc, chunks=args.c5_chunks,
                                              p2p_group=p2p, out=frame_out, streams=wstreams)
+        elif args.c5_form == "tiles":
+            def step():
+                return shard.tiled_frame(H, W, rank, world, proc)
         else:
             bstreams = None if args.c5_no_graphs else [torch.cuda.Stream(), torch.cuda.Stream()]
 
@@ -641,6 +663,7 @@ def main_c4(args):
     coded = c4_coded_blocks(L, fr) if args.workload != "c5" else None
     c4_bytes = c4_algorithmic_bytes(L, W, H, coded)
     band, tail = shard.partition(H, W, world)[rank]
+    tile = shard.grid_partition(H, W, world)[rank]
     line = {
         "metric": metric_name(args), "workload": args.workload,
         "value": round(value, 2),
@@ -666,7 +689,9 @@ def main_c4(args):
                            ("; SB rows sharded over ranks (%s form) + RCCL all-gather of "
                             "the reconstruction" % args.c5_form) if args.workload == "c5" else "",
                            sb),
-            "parallelism": ("sb-row %s x%d (rank %d: band %s, tail %s)"
+            "parallelism": (("sb grid tiles x%d (rank %d: tile %s)" % (world, rank, tile))
+                            if args.c5_form == "tiles" else
+                            "sb-row %s x%d (rank %d: band %s, tail %s)"
                             % ("band+tail segments" if args.c5_form == "band"
                                else "round-robin rows, p2p edge wavefront", world, rank, band,
                                tail))
@@ -688,7 +713,8 @@ def main_c4(args):
             *np.unique(fr.sb_tx_size.cpu().numpy(), return_counts=True)) if s < 19}
     if args.workload == "c5" and world == 1 and args.c5_emulate:
         line["c5_emulation"] = c5_emulate(H, W, proc, [int(g) for g in args.c5_emulate.replace(":", ",").split(",")],
-                                          args.steps, args.warmup, step_ms)
+                                          args.steps, args.warmup, step_ms,
+                                          form="band" if args.c5_form == "band" else "tiles")
     if args.workload == "c4" and world == 1:
         # the bound that applies: int32 VALU
         rv = c4_roofline(step_ms, W, H, fr.type_masks, coded, c4_bytes)
@@ -2067,7 +2093,8 @@ def main():
         # N > 1 the driver's scaling run measures it from this object
         line["c5"] = c5_leg(L, max(5, args.steps // 2), max(2, args.warmup), args.rdmult,
                             args.qindex, world, rank,
-                            c4_ms=line.get("c4", {}).get("ms_per_frame"))
+                            c4_ms=line.get("c4", {}).get("ms_per_frame"),
+                            form="band" if args.c5_form == "band" else "tiles")
     if rank == 0 and world == 1 and not args.no_cpu:
         line["cpu_baseline"] = cpu_baseline(args)
     if rank == 0:

@@ -1,6 +1,7 @@
 """Multi-process (gloo, CPU) tests of the C5 sharding (lavish_dsp/shard.py):
 the balanced band partition, the band form with its overlapped per-part
-all-gathers, and the row-wavefront form with point-to-point edges and the
+all-gathers, the tile form (one grid tile per rank, one gather), and the
+row-wavefront form with point-to-point edges and the
 per-wave row all-gather -- each rank processing its rectangles with the
 oracle's C4 pipeline, the sharded frame identical to the single-process
 result (the property that makes the sharding valid: SBs are independent
@@ -93,6 +94,8 @@ def _worker(rank, world, port, q, form):
         log = []
         if form == "band":
             full = shard.sharded_frame(H, W, rank, world, rect)
+        elif form == "tiles":
+            full = shard.tiled_frame(H, W, rank, world, rect)
         else:
             p2p = dist.new_group(list(range(world)))
             full = shard.wavefront_frame(H, W, rank, world, rect, chunks=3, p2p_group=p2p,
@@ -141,6 +144,44 @@ def test_band_form_matches_single_process(world):
         assert not isinstance(full, str), full
         np.testing.assert_array_equal(full, ref)
         assert done == [x for x in parts[r] if x is not None]  # band, then tail
+
+
+@pytest.mark.parametrize("world", [2, 3, 8])
+def test_tile_form_matches_single_process(world):
+    """One grid tile per rank, one gather: every rank ends with the
+    single-process frame and computed exactly its tile."""
+    got = _run(world, "tiles")
+    ref = _reference()
+    rects = _shard().grid_partition(*GEOM, world)
+    for r in range(world):
+        full, done, _ = got[r]
+        assert not isinstance(full, str), full
+        np.testing.assert_array_equal(full, ref)
+        assert done == [rects[r]]
+
+
+@pytest.mark.parametrize("H,W", [(2160, 3840), (1080, 1920), (200, 256), (288, 352)])
+def test_grid_partition_covers_and_balances(H, W):
+    """Every pixel in exactly one tile, tiles on SB boundaries; at 4K the
+    tiles of G = 2, 4, 8 hold exactly R C / G SBs."""
+    shard = _shard()
+    R, C = shard.sb_rows(H), shard.sb_cols(W)
+    for world in range(1, 9):
+        try:
+            rects = shard.grid_partition(H, W, world)
+        except ValueError:
+            assert all(world % gr or gr > R or world // gr > C for gr in range(1, world + 1))
+            continue
+        assert len(rects) == world
+        cov = np.zeros((H, W), np.int32)
+        for y0, y1, x0, x1 in rects:
+            assert y0 % 64 == 0 and x0 % 64 == 0 and y1 > y0 and x1 > x0
+            cov[y0:y1, x0:x1] += 1
+        assert (cov == 1).all(), world
+    for world in (2, 4, 8):
+        sbs = [-(-(y1 - y0) // 64) * -(-(x1 - x0) // 64)
+               for y0, y1, x0, x1 in shard.grid_partition(2160, 3840, world)]
+        assert sbs == [2040 // world] * world
 
 
 def test_partition_narrow_frames():
