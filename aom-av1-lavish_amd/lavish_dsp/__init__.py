@@ -358,15 +358,17 @@ class FrameOutputs:
         self.eob = P19(*[self.outs[s]["eob"].data_ptr() if s in self.outs else 0 for s in range(19)])
 
 
-def txq_frame(residual, frame_out, qp, bit_depth=8, quant_kind=QUANT_FP, stream=None):
-    """lavish_txq_frame: every size of `frame_out` over one residual plane, the
-    per-size kernels running concurrently on internal streams."""
+def txq_frame(residual, frame_out, qp, bit_depth=8, quant_kind=QUANT_FP, stream=None,
+              size_mask=None):
+    """lavish_txq_frame: every size of `frame_out` (or of those, the sizes in
+    size_mask) over one residual plane."""
     import torch
     assert residual.dtype == torch.int16 and residual.is_cuda
     assert residual.stride(1) == 1, "residual rows must be contiguous"
     H, W = residual.shape
+    mask = frame_out.size_mask if size_mask is None else frame_out.size_mask & size_mask
     rc = _lib.lavish_txq_frame(ctypes.c_void_p(residual.data_ptr()), residual.stride(0), W, H,
-                               frame_out.size_mask, frame_out.tm, bit_depth, quant_kind,
+                               mask, frame_out.tm, bit_depth, quant_kind,
                                ctypes.byref(qp), frame_out.q, frame_out.dq, frame_out.eob,
                                _stream_ptr(stream))
     if rc != 0:

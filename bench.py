@@ -96,10 +96,11 @@ def parse():
                     help="skip the c4 sub-object (4K 10-bit RDO step) of the default line")
     ap.add_argument("--c3-wg-cap", type=int, default=C3_WG_CAP,
                     help="workgroups of the C3 search when it runs beside C2 (0: no cap)")
-    ap.add_argument("--c3-mode", choices=("fused", "streams"), default=C3_MODE,
+    ap.add_argument("--c3-mode", choices=("fused", "streams", "split32"), default=C3_MODE,
                     help="how C3 runs beside C2: one launch with the search's job groups "
-                         "interleaved among C2's workgroups (lavish_txq_frame_search), or C3 on a "
-                         "second stream in at most --c3-wg-cap workgroups")
+                         "interleaved among C2's workgroups (lavish_txq_frame_search), C3 on a "
+                         "second stream in at most --c3-wg-cap workgroups (streams), or that "
+                         "with C2's 32-point sizes after C3 on the second stream (split32)")
     ap.add_argument("--c3-every", type=int, default=C3_EVERY,
                     help="fused: a search unit (8 workgroups) every this many units of the "
                          "dispatch order")
@@ -109,6 +110,9 @@ def parse():
                     help="run the C3 and C2 legs back to back on one stream (default: C3 on a "
                          "second stream beside C2)")
     ap.add_argument("--overlap", action="store_true", help=argparse.SUPPRESS)  # the default
+    ap.add_argument("--hw-queues", type=int, default=0,
+                    help="GPU_MAX_HW_QUEUES for this process (set before HIP starts; "
+                         "0: the runtime's default)")
     ap.add_argument("--fan-width", type=int, default=0,
                     help="1: C4's per-size kernels all on the caller's stream (isolated "
                          "per-kernel timings under a profiler; lavish_set_fan_width)")
@@ -162,7 +166,11 @@ C3_COST = 0     # MV_COST_ENTROPY (the RDO path's x->mv_cost_type)
 C3_SKIP = True  # use_downsampled_sad (>= 720p, speed_features.c:205-209)
 C3_CL = True    # cost list: subpel_search_method != SUBPEL_TREE (cond_cost_list)
 C3_WG_CAP = 512  # C3's workgroups beside C2 (profiles/r04_v11_*: the step's best)
-C3_MODE = "streams"  # C3 on a second stream beside C2 (fused: measured slower)
+# C3 on a second stream beside C2, C2's 32-point class after C3 on that
+# stream (0.717-0.720 vs 0.727-0.729 ms with the whole of C2 on the caller's
+# stream, profiles/r05_split32_ab.txt; fused: measured slower, DESIGN.md
+# section 5)
+C3_MODE = "split32"
 C3_EVERY = 10      # fused: a search unit every 10 units of the dispatch order
 # sub-pixel refinement after the full-pel search (c3sub): SUBPEL_TREE_PRUNED_MORE
 # (speed >= 4), subpel_force_stop EIGHTH_PEL, iters_per_step 1 (speed >= 2),
@@ -1741,6 +1749,7 @@ class RdoStep:
         self.overlap = self.do_c2 and self.do_c3 and not serial
         # fused: the overlapped step as one launch (C3 without the sub-pel leg)
         self.fused = self.overlap and c3_mode == "fused" and not self.do_sub
+        self.split32 = c3_mode == "split32"
         self.c3_wg_cap = c3_wg_cap
         self.c3_every = c3_every
         self.stream = torch.cuda.current_stream()
@@ -1750,6 +1759,8 @@ class RdoStep:
         self.sizes = [s for s in range(19) if L.TX_W[s] <= 32 and L.TX_H[s] <= 32]
         self.qp = L.build_quant_params(8, qindex, L.QUANT_FP)
         self.frame = L.FrameOutputs(self.res, self.sizes)
+        # the 32-point class of lavish_txq_frame (largest side 32)
+        self.mask32 = sum(1 << s for s in self.sizes if max(L.TX_W[s], L.TX_H[s]) == 32)
         # C3 input: padded current frame + references, jobs for every 16x16
         # block x ref
         self.src_np, self.refs_np = synth.motion_planes(W, H, refs, border, seed=seed)
@@ -1819,6 +1830,9 @@ class RdoStep:
                 ev[4].record(stream)
                 ev[5].record(stream)
             return
+        # split32: C2's 32-point class (few, latency-bound workgroups) follows
+        # C3 on the side stream, the <= 16-point class runs on the caller's
+        split = ovl and self.split32 and self.do_c2
         if ovl:  # the legs are independent: C3 (TA / latency bound) beside C2 (HBM writes)
             self.fork.record(stream)
             side.wait_event(self.fork)
@@ -1829,12 +1843,16 @@ class RdoStep:
             # slots and C2 stretches less: DESIGN.md section 5); alone, uncapped
             self.M.set_search_workgroup_cap(self.c3_wg_cap if ovl else 0)
             self.c3(side)
+            if split:
+                self.L.txq_frame(self.res, self.frame, self.qp, stream=side,
+                                 size_mask=self.mask32)
             if ev is not None:
                 ev[2].record(side)
         if self.do_c2:
             if ev is not None:
                 ev[3].record(stream)
-            self.L.txq_frame(self.res, self.frame, self.qp, stream=stream)
+            self.L.txq_frame(self.res, self.frame, self.qp, stream=stream,
+                             size_mask=~self.mask32 if split else None)
             if ev is not None:
                 ev[4].record(stream)
         if ovl:
@@ -1899,6 +1917,8 @@ def main():
     args = parse()
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         return spawn_ranks(args, sys.argv[1:])
+    if args.hw_queues:  # read by the HIP runtime when it starts (first device call)
+        os.environ["GPU_MAX_HW_QUEUES"] = str(args.hw_queues)
     if args.fan_width:
         import lavish_dsp
         lavish_dsp.set_fan_width(args.fan_width)

@@ -8,7 +8,8 @@ full_pixel_diamond :1479 -> diamond_search_sad :1318-1477) beside C2
 type, tx_search.c:2148-2312 -> encodemb.c:295-341).  The default step runs
 both as one launch (lavish_txq_frame_search: the search's job groups
 interleaved among the transform's workgroups); the "streams" form runs C3 on
-a side stream in at most 512 workgroups (lavish_set_search_workgroup_cap: the
+a side stream in at most 512 workgroups (the default "split32" form also
+runs C2's 32-point sizes after C3 on that stream) (lavish_set_search_workgroup_cap: the
 search kernel strides over virtual workgroups) beside C2 on the caller's
 stream.  Two consecutive steps run, then both legs' outputs are compared
 with the oracle; the search at workgroup caps {8, 64, 512, 0} and the fused
@@ -42,6 +43,7 @@ def step():
     b = _bench()
     R = b.RdoStep()  # the bench's defaults: 1080p, 7 refs, qindex 128, overlapped
     assert R.overlap and R.fused == (b.C3_MODE == "fused") and R.c3_wg_cap == 512
+    assert R.split32 == (b.C3_MODE == "split32")
     return b, R
 
 
@@ -91,22 +93,24 @@ def _check_c2(R, c2_expected, what):
                                       err_msg="%s: size %d eob" % (what, s))
 
 
-@pytest.mark.parametrize("mode", ["fused", "streams"])
+@pytest.mark.parametrize("mode", ["fused", "streams", "split32"])
 def test_timed_step_both_legs(step, c2_expected, c3_expected, mode):
     """Two steps as timed (fused: one launch; streams: C3 capped beside C2 on
-    two streams), then C3's results and cost lists and every C2 size's
-    qcoeff / dqcoeff / eob."""
+    two streams; split32: C2's 32-point sizes after C3 on the second stream,
+    the rest of C2 on the caller's), then C3's results and cost lists and
+    every C2 size's qcoeff / dqcoeff / eob."""
     import torch
     b, R = step
-    fused = R.fused
+    fused, split = R.fused, R.split32
     R.fused = mode == "fused"
+    R.split32 = mode == "split32"
     try:
         _poison(R)
         for _ in range(2):
             R.step()
         torch.cuda.synchronize()
     finally:
-        R.fused = fused
+        R.fused, R.split32 = fused, split
     assert R.L.status()[0] == 0, R.L.status()
     got = _check_c3(R, *c3_expected, what=mode)
     assert (np.abs(got["best_row"]) + np.abs(got["best_col"]) > 0).mean() > 0.5
