@@ -5,12 +5,13 @@ every 16x16 block x 7 references, downsampled SAD, MV_COST_ENTROPY over the
 default nmv tables, cost lists; av1_full_pixel_search, mcomp.c:1755 ->
 full_pixel_diamond :1479 -> diamond_search_sad :1318-1477) beside C2
 (lavish_txq_frame: every block of the 14 TX sizes <= 32x32 x every valid
-type, tx_search.c:2148-2312 -> encodemb.c:295-341).  The default step runs
-both as one launch (lavish_txq_frame_search: the search's job groups
-interleaved among the transform's workgroups); the "streams" form runs C3 on
-a side stream in at most 512 workgroups (the default "split32" form also
-runs C2's 32-point sizes after C3 on that stream) (lavish_set_search_workgroup_cap: the
-search kernel strides over virtual workgroups) beside C2 on the caller's
+type, tx_search.c:2148-2312 -> encodemb.c:295-341).  The default step
+("split32") runs C3 on a side stream in at most 512 workgroups
+(lavish_set_search_workgroup_cap: the search kernel strides over virtual
+workgroups) followed there by C2's 32-point sizes, and the rest of C2 on the
+caller's stream; "streams" keeps all of C2 on the caller's stream; "fused"
+runs C2 and C3 as one launch (lavish_txq_frame_search: the search's job
+groups interleaved among the transform's workgroups) on the caller's
 stream.  Two consecutive steps run, then both legs' outputs are compared
 with the oracle; the search at workgroup caps {8, 64, 512, 0} and the fused
 launch at interleaving strides {1, 3, 10, 40} must give identical results.
