@@ -1996,6 +1996,8 @@ def main():
         # per-kernel roofline is taken from a serial pass after it (isolated
         # legs, same inputs), not from the overlapped leg spans
         legs_overlapped = ({"c2_c3_fused_launch": round(c2_ms, 4)} if R.fused else
+                           {"c2_txq_frame_le16pt": round(c2_ms, 4),
+                            "c3_diamond_then_c2_32pt": round(c3_ms, 4)} if R.split32 else
                            {"c2_txq_frame": round(c2_ms, 4), "c3_diamond": round(c3_ms, 4)})
         KS = max(5, K // 2)
         evs = [tuple(torch.cuda.Event(enable_timing=True) for _ in range(6)) for _ in range(KS)]
