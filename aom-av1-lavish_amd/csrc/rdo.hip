@@ -254,8 +254,9 @@ __global__ __launch_bounds__(256) void sb_decide_kernel(SbArgs a) {
       v[q] = k < nblk ? a.rec[s][(sy * 64 / H + y) * bw + sx * 64 / W + x].rdcost : 0;
     }
     int64_t sum = sat_add(sat_add(v[0], v[1]), sat_add(v[2], v[3]));
-#pragma unroll
-    for (int m = 1; m < 64; m <<= 1) sum = sat_add(sum, __shfl_xor(sum, m));
+    sum = (int64_t)lane_reduce64<64>((uint64_t)sum, [](uint64_t x, uint64_t y) {
+      return (uint64_t)sat_add((int64_t)x, (int64_t)y);
+    });
     if (sum < best) {
       best = sum;
       best_s = s;

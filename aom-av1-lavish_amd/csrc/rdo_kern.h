@@ -32,6 +32,7 @@
 #include <type_traits>
 
 #include "coeffcost_dev.h"
+#include "lane_red.h"
 #include "lavish_internal.h"
 #include "quant_dev.h"
 #pragma once
@@ -285,8 +286,7 @@ __device__ __forceinline__ void rdo_types(const RdoArgs& a, const int32_t (&res)
         }
         last = q[c] != 0 ? max(last, iscan[rc] + 1) : last;
       }
-#pragma unroll
-      for (int m = 1; m < KH; m <<= 1) last = max(last, __shfl_xor(last, m));
+      last = lane_max<KH>(last);
       if constexpr (MODE == 0) {
         if (r == 0 && live && bb < nvalid && a.eob != nullptr)
           a.eob[(size_t)ti * a.nblocks + blk0 + bb] = (uint16_t)last;
@@ -360,8 +360,7 @@ __device__ __forceinline__ void rdo_types(const RdoArgs& a, const int32_t (&res)
                                          q[c], tc.dc_sign_ctx, nzmag, brmag);
             }
           }
-#pragma unroll
-          for (int m = 1; m < KH; m <<= 1) rate += __shfl_xor(rate, m);
+          rate = lane_sum<KH>(rate);
           rate = cc::txb_rate(s_cc, cls, tc.txb_skip_ctx, last, a.tx_type_cost[t], rate);
         } else {
           // rate_estimator: positions of the DCT_DCT scan below eob
@@ -371,16 +370,12 @@ __device__ __forceinline__ void rdo_types(const RdoArgs& a, const int32_t (&res)
             const uint32_t al = (uint32_t)abs(q[c]);
             if (a.iscan_dct[rc] < last) rate += get_msb(al + 1) + 1 + (al > 0);
           }
-#pragma unroll
-          for (int m = 1; m < KH; m <<= 1) rate += __shfl_xor(rate, m);
+          rate = lane_sum<KH>(rate);
           rate = (rate + 1) << 9;  // AV1_PROB_COST_SHIFT
         }
-#pragma unroll
-        for (int m = 1; m < KH; m <<= 1) {
-          satd += __shfl_xor(satd, m);
-          err += __shfl_xor(err, m);
-          sse += __shfl_xor(sse, m);
-        }
+        satd = lane_sum<KH>(satd);
+        err = lane_sum64<KH>(err);
+        sse = lane_sum64<KH>(sse);
         // av1_highbd_block_error rounding, then the TX-domain shift
         const int sh = 2 * (a.bd - 8);
         if (sh > 0) {
@@ -443,8 +438,7 @@ __device__ __forceinline__ void rdo_types(const RdoArgs& a, const int32_t (&res)
           const int d = p + res[k][r] - rec;  // src - recon
           ps += (uint64_t)(d * d);
         }
-#pragma unroll
-        for (int m = 1; m < W; m <<= 1) ps += __shfl_xor(ps, m);
+        ps = (uint64_t)lane_sum64<W>((int64_t)ps);
         if (c == 0) px->psse[b] = ps;
       }
       wave_sync();
@@ -727,8 +721,7 @@ void rdo_kernel(RdoArgs a) {
     if constexpr (MODE == 2) {
       // block_sse (tx_search.c:2079-2094): sum of squares of the residual,
       // highbd-rounded by 2 (bd - 8) bits, x 16
-#pragma unroll
-      for (int m = 1; m < W; m <<= 1) ss += __shfl_xor(ss, m);
+      ss = lane_sum64<W>(ss);
       constexpr int sh = 2 * (Bd<BDI>::bd - 8);
       if constexpr (sh > 0) ss = (ss + ((int64_t)1 << (sh - 1))) >> sh;
       if (c == 0) px->bsse[b] = ss * 16;

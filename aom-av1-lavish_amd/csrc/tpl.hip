@@ -22,6 +22,7 @@
 // quantization, error, rate and the inverse (row pass in registers, column
 // pass after a second transpose), and the reconstruction is written out.
 // The 1-D transforms are txfm_dev.h's (the C2 / C4 kernels' code).
+#include "lane_red.h"
 #include "lavish_internal.h"
 #include "quant_dev.h"
 
@@ -51,21 +52,15 @@ struct TplCfg {
 
 template <int N>
 __device__ __forceinline__ int seg_sum(int v) {
-#pragma unroll
-  for (int m = 1; m < N; m <<= 1) v += __shfl_xor(v, m);
-  return v;
+  return lane_sum<N>(v);
 }
 template <int N>
 __device__ __forceinline__ int64_t seg_sum64(int64_t v) {
-#pragma unroll
-  for (int m = 1; m < N; m <<= 1) v += __shfl_xor(v, m);
-  return v;
+  return lane_sum64<N>(v);
 }
 template <int N>
 __device__ __forceinline__ int seg_max(int v) {
-#pragma unroll
-  for (int m = 1; m < N; m <<= 1) v = max(v, __shfl_xor(v, m));
-  return v;
+  return lane_max<N>(v);
 }
 
 __device__ __forceinline__ int msb(unsigned v) { return 31 - __clz(v); }  // get_msb

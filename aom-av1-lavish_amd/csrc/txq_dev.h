@@ -3,6 +3,7 @@
 // launch (mcomp.hip, lavish_txq_frame_search).
 #pragma once
 
+#include "lane_red.h"
 #include "lavish_internal.h"
 #include "quant_dev.h"
 
@@ -124,8 +125,7 @@ __device__ __forceinline__ void txq_types(const TxqArgs& a,
         const int pos1 = iscan[rc] + 1;
         last = q != 0 ? max(last, pos1) : last;
       }
-#pragma unroll
-      for (int m = 1; m < H; m <<= 1) last = max(last, __shfl_xor(last, m));
+      last = lane_max<H>(last);
       if (r == 0 && b < nvalid && a.eob != nullptr)
         a.eob[(size_t)ti * a.nblocks + blk0 + b] = (uint16_t)last;
     }

@@ -116,11 +116,11 @@ int lavish_txq_plane(const int16_t *residual, int stride, int width,
                      int32_t *dqcoeff, uint16_t *eob, int32_t *coeff,
                      void *stream);
 
-/* Streams the per-size kernels of lavish_rdo_frame are dealt over: 1 .. 6
+/* Streams the per-size kernels of lavish_rdo_frame are dealt over: 1 .. 3
  * -- the caller's stream + streams - 1 internal streams, forked and joined
  * by events (default 3; 1: every size on the caller's stream, for isolated
- * per-kernel timings under a profiler).  Set it between calls.  Results are
- * identical.  Returns -1 for other values.  No reference counterpart. */
+ * per-kernel timings under a profiler).  Results are identical.  Returns -1
+ * for other values.  No reference counterpart. */
 int lavish_set_fan_width(int streams);
 
 /* Frame batch: lavish_txq_plane for every TX size whose bit is set in

@@ -231,6 +231,13 @@ def test_c5_partition_rects_on_gpu(L):
         out = torch.full_like(ts, -1)
         direct = shard.c4_rect_processor(ts, tp, qp, rdmult, 10, {}, out=out, graphs=graphs)
         streams = [torch.cuda.Stream() for _ in range(nst)] or None
+        if graphs and streams:
+            # every chunk's graph captured first, on one stream: captures and
+            # instantiations do not interleave with replays on other streams
+            # (a host crash inside hipGraphLaunch was seen twice in round 5's
+            # full-suite runs when they did; not reproduced in isolation)
+            shard.wavefront_frame(H, W, 0, 1, direct, chunks=4, out=out)
+            torch.cuda.synchronize()
         for _ in range(2):  # the second pass replays every cached chunk
             out.fill_(-1)
             wf = shard.wavefront_frame(H, W, 0, 1, direct, chunks=4, out=out, streams=streams)
