@@ -110,9 +110,6 @@ def parse():
                     help="run the C3 and C2 legs back to back on one stream (default: C3 on a "
                          "second stream beside C2)")
     ap.add_argument("--overlap", action="store_true", help=argparse.SUPPRESS)  # the default
-    ap.add_argument("--c3-order", default="raster",
-                    help="C3 job order: raster (reference-major, raster blocks) or tileWxH "
-                         "(a wave's 8 jobs a W x H tile of blocks, e.g. tile4x2)")
     ap.add_argument("--hw-queues", type=int, default=0,
                     help="GPU_MAX_HW_QUEUES for this process (set before HIP starts; "
                          "0: the runtime's default)")
@@ -1745,7 +1742,7 @@ class RdoStep:
 
     def __init__(self, workload="rdo", width=1920, height=1080, refs=7, border=160, qindex=128,
                  rdmult=2000, seed=1234, serial=False, c3_wg_cap=C3_WG_CAP, c3_mode=C3_MODE,
-                 c3_every=C3_EVERY, c3_order="raster"):
+                 c3_every=C3_EVERY):
         import torch
         import lavish_dsp as L
         import lavish_dsp.motion as M
@@ -1776,16 +1773,6 @@ class RdoStep:
         st = self.src_np.shape[1]
         self.ref_stride = st
         self.jobs_np = M.frame_jobs(W, H, st, border, self.src_np.size, C3_BLOCK, C3_BLOCK, refs)
-        if c3_order != "raster":
-            # a wave's 8 jobs as a tw x th tile of neighbouring blocks of one
-            # reference (raster: 8 blocks of one block row)
-            tw, th = (int(v) for v in c3_order[4:].split("x"))
-            nbx, nby = W // C3_BLOCK, H // C3_BLOCK
-            j = np.arange(len(self.jobs_np))
-            ref_k, blk = j // (nbx * nby), j % (nbx * nby)
-            by, bx = blk // nbx, blk % nbx
-            key = np.lexsort((bx % tw, by % th, bx // tw, by // th, ref_k))
-            self.jobs_np = np.ascontiguousarray(self.jobs_np[key])
         self.tsrc = torch.from_numpy(self.src_np).cuda()
         self.trefs = torch.from_numpy(self.refs_np).cuda()
         self.tjobs = M.to_device(self.jobs_np)
@@ -1974,7 +1961,7 @@ def main():
         torch.cuda.set_stream(torch.cuda.Stream(priority=-1))
     R = RdoStep(args.workload, W, H, args.refs, args.border, args.qindex, args.rdmult,
                 seed=1234 + rank, serial=args.serial, c3_wg_cap=args.c3_wg_cap,
-                c3_mode=args.c3_mode, c3_every=args.c3_every, c3_order=args.c3_order)
+                c3_mode=args.c3_mode, c3_every=args.c3_every)
     do_c2, do_c3, do_sub, overlap = R.do_c2, R.do_c3, R.do_sub, R.overlap
     stream, sizes, jobs_np, c3_cost = R.stream, R.sizes, R.jobs_np, R.c3_cost
     step = R.step
