@@ -29,7 +29,12 @@ struct QP {
 //  * b: ((t*32)*quant) >> 16 == (t*quant) >> 11 exactly (32 t q / 2^16);
 //    t*quant < 2^30 in lowbd, 64-bit in highbd; the final multiply by
 //    quant_shift is 64-bit (quant_shift may be any int16 in the per-call API).
-template <int LS, int QK, bool HBD>
+// F24: the caller's FAST range (tools/range_analysis.py: |coefficient| <
+// 2^21 for residuals <= kFastResidualMax) -- the highbd fp product and the
+// pass test of fp then fit 24-bit multiplies (v_mul_i32_i24 /
+// v_mul_hi_i32_i24, full rate) and 32-bit compares instead of the
+// quarter-rate 64-bit multiply; same bits.
+template <int LS, int QK, bool HBD, bool F24 = false>
 __device__ __forceinline__ int32_t quant_one(int32_t c, bool ac, const QP& qp) {
   const int32_t sgn = c >> 31;
   const int32_t a = (c ^ sgn) - sgn;
@@ -38,10 +43,12 @@ __device__ __forceinline__ int32_t quant_one(int32_t c, bool ac, const QP& qp) {
   int32_t q;
   if constexpr (QK == LAVISH_QUANT_FP) {
     const int32_t deq = ac ? qp.dequant[1] : qp.dequant[0];
-    const bool pass = ((int64_t)a << (1 + LS)) >= deq;
+    const bool pass = F24 ? (a << (1 + LS)) >= deq : ((int64_t)a << (1 + LS)) >= deq;
     if constexpr (!HBD) {
       const int32_t t = min(a + rnd, 32767);
       q = (sext24(t) * qt) >> (16 - LS);
+    } else if constexpr (F24) {
+      q = (int32_t)(((int64_t)sext24(a + rnd) * (int64_t)sext24(qt)) >> (16 - LS));
     } else {
       q = (int32_t)(((int64_t)(a + rnd) * qt) >> (16 - LS));
     }
@@ -64,13 +71,16 @@ __device__ __forceinline__ int32_t quant_one(int32_t c, bool ac, const QP& qp) {
   return (q ^ sgn) - sgn;
 }
 
-template <int LS>
+// F24: |q| < 2^21 (the FAST range): the product's low 32 bits -- the
+// reference's int multiply, wrap included -- from one 24-bit multiply
+template <int LS, bool F24 = false>
 __device__ __forceinline__ int32_t dequant_one(int32_t q, bool ac, const QP& qp) {
   const int32_t sgn = q >> 31;
   const int32_t aq = (q ^ sgn) - sgn;
   const int32_t d = ac ? qp.dequant[1] : qp.dequant[0];
   // (abs_q * dequant) >> log_scale as an int multiply (wraps like the reference)
-  const int32_t adq = (int32_t)((uint32_t)aq * (uint32_t)d) >> LS;
+  const int32_t adq =
+      F24 ? (int32_t)(sext24(aq) * sext24(d)) >> LS : (int32_t)((uint32_t)aq * (uint32_t)d) >> LS;
   return (adq ^ sgn) - sgn;
 }
 

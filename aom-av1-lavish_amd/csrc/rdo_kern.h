@@ -272,10 +272,10 @@ __device__ __forceinline__ void rdo_types(const RdoArgs& a, const int32_t (&res)
           if constexpr (MODE == 0) {
             if (a.coeff != nullptr && live && bb < nvalid) a.coeff[obase + rc] = v;
           }
-          q[c] = quant_one<LS, QK, HBD>(v, ac, a.qp);
+          q[c] = quant_one<LS, QK, HBD, FAST>(v, ac, a.qp);
         }
         if constexpr (DEC) {
-          const int32_t dq = dequant_one<LS>(q[c], ac, a.qp);
+          const int32_t dq = dequant_one<LS, FAST>(q[c], ac, a.qp);
           const int64_t d = (int64_t)v - dq;
           err += d * d;
           sse += (int64_t)v * v;
@@ -403,7 +403,7 @@ __device__ __forceinline__ void rdo_types(const RdoArgs& a, const int32_t (&res)
         int32_t vin[W], vout[W];
 #pragma unroll
         for (int c = 0; c < W; ++c) {
-          int32_t v = dequant_one<LS>(q[c], c != 0 || r != 0, a.qp);
+          int32_t v = dequant_one<LS, FAST>(q[c], c != 0 || r != 0, a.qp);
           if constexpr (C::rect2) v = rshift64((int64_t)v * 2896, 12);
           vin[c] = clamp_bits<B::clamp_in_row>(v);
         }
@@ -504,10 +504,10 @@ __device__ __forceinline__ void rdo_types(const RdoArgs& a, const int32_t (&res)
           if (a.dqcoeff != nullptr) {
             const int rc0 = i % NC;
             v4i d4;
-            d4.x = dequant_one<LS>(q4.x, rc0 != 0, a.qp);
-            d4.y = dequant_one<LS>(q4.y, 1, a.qp);
-            d4.z = dequant_one<LS>(q4.z, 1, a.qp);
-            d4.w = dequant_one<LS>(q4.w, 1, a.qp);
+            d4.x = dequant_one<LS, FAST>(q4.x, rc0 != 0, a.qp);
+            d4.y = dequant_one<LS, FAST>(q4.y, 1, a.qp);
+            d4.z = dequant_one<LS, FAST>(q4.z, 1, a.qp);
+            d4.w = dequant_one<LS, FAST>(q4.w, 1, a.qp);
             __builtin_nontemporal_store(d4, reinterpret_cast<v4i*>(&a.dqcoeff[gbase + i]));
           }
         }
@@ -549,10 +549,10 @@ __device__ __forceinline__ void rdo_types(const RdoArgs& a, const int32_t (&res)
       __builtin_nontemporal_store(q4, reinterpret_cast<v4i*>(&a.qcoeff[gbase + i]));
       const int rc0 = i % NC;
       v4i d4;
-      d4.x = dequant_one<LS>(q4.x, rc0 != 0, a.qp);
-      d4.y = dequant_one<LS>(q4.y, 1, a.qp);
-      d4.z = dequant_one<LS>(q4.z, 1, a.qp);
-      d4.w = dequant_one<LS>(q4.w, 1, a.qp);
+      d4.x = dequant_one<LS, FAST>(q4.x, rc0 != 0, a.qp);
+      d4.y = dequant_one<LS, FAST>(q4.y, 1, a.qp);
+      d4.z = dequant_one<LS, FAST>(q4.z, 1, a.qp);
+      d4.w = dequant_one<LS, FAST>(q4.w, 1, a.qp);
       __builtin_nontemporal_store(d4, reinterpret_cast<v4i*>(&a.dqcoeff[gbase + i]));
     }
   }
@@ -624,10 +624,10 @@ __device__ __forceinline__ void rdo_types(const RdoArgs& a, const int32_t (&res)
       __builtin_nontemporal_store(q4, reinterpret_cast<v4i*>(&a.qcoeff[gbase + i]));
       const int rc0 = i % NC;
       v4i d4;
-      d4.x = dequant_one<LS>(q4.x, rc0 != 0, a.qp);
-      d4.y = dequant_one<LS>(q4.y, 1, a.qp);
-      d4.z = dequant_one<LS>(q4.z, 1, a.qp);
-      d4.w = dequant_one<LS>(q4.w, 1, a.qp);
+      d4.x = dequant_one<LS, FAST>(q4.x, rc0 != 0, a.qp);
+      d4.y = dequant_one<LS, FAST>(q4.y, 1, a.qp);
+      d4.z = dequant_one<LS, FAST>(q4.z, 1, a.qp);
+      d4.w = dequant_one<LS, FAST>(q4.w, 1, a.qp);
       __builtin_nontemporal_store(d4, reinterpret_cast<v4i*>(&a.dqcoeff[gbase + i]));
     }
   }

@@ -119,7 +119,7 @@ __device__ __forceinline__ void txq_types(const TxqArgs& a,
           if (a.coeff != nullptr) {
             if (b < nvalid) a.coeff[obase + rc] = v;
           }
-          q = quant_one<LS, QK, HBD>(v, c != 0 || r != 0, a.qp);
+          q = quant_one<LS, QK, HBD, FAST>(v, c != 0 || r != 0, a.qp);
         }
         t2[b * N + rc] = q;
         const int pos1 = iscan[rc] + 1;
@@ -143,10 +143,10 @@ __device__ __forceinline__ void txq_types(const TxqArgs& a,
         if (a.dqcoeff != nullptr) {
           const int rc0 = i % N;  // N % 4 == 0: all four share the block
           v4i d4;
-          d4.x = dequant_one<LS>(q4.x, rc0 != 0, a.qp);  // only x can be DC
-          d4.y = dequant_one<LS>(q4.y, 1, a.qp);
-          d4.z = dequant_one<LS>(q4.z, 1, a.qp);
-          d4.w = dequant_one<LS>(q4.w, 1, a.qp);
+          d4.x = dequant_one<LS, FAST>(q4.x, rc0 != 0, a.qp);  // only x can be DC
+          d4.y = dequant_one<LS, FAST>(q4.y, 1, a.qp);
+          d4.z = dequant_one<LS, FAST>(q4.z, 1, a.qp);
+          d4.w = dequant_one<LS, FAST>(q4.w, 1, a.qp);
           __builtin_nontemporal_store(d4, reinterpret_cast<v4i*>(&a.dqcoeff[gbase + i]));
         }
       }
