@@ -68,11 +68,14 @@ struct RateCfg {
   const LavishTxbCtx* txb_ctx;
   const int32_t* tx_type_costs;
 };
+struct RdoArgs;
+// args_only (mode 1 only): fill *args_only instead of launching
 int rdo_plane(const uint16_t* src, const uint16_t* pred, int stride, int width, int height,
               int tx_size, uint32_t type_mask, int bd, const LavishQuantParams* qp, int rdmult,
               LavishRdoBlock* out, int32_t* qcoeff, int32_t* dqcoeff, hipStream_t s,
               int px = 0, const uint16_t* block_mask = nullptr,
-              const uint8_t* block_map = nullptr, const RateCfg* rate = nullptr);
+              const uint8_t* block_map = nullptr, const RateCfg* rate = nullptr,
+              RdoArgs* args_only = nullptr);
 
 // inter prediction batch (inter.hip); custom = an RTCD shim's own kernels
 int inter_pred_batch(const void* ref, int ref_stride, int ref_width, int ref_height, int ss_x,

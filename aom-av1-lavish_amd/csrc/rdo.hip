@@ -76,7 +76,8 @@ int rdo_plane_px64(RdoArgs& a, int tx_size, int width, int height, hipStream_t s
 int rdo_plane(const uint16_t* src, const uint16_t* pred, int stride, int width, int height,
               int tx_size, uint32_t type_mask, int bd, const LavishQuantParams* qp, int rdmult,
               LavishRdoBlock* out, int32_t* qcoeff, int32_t* dqcoeff, hipStream_t s, int px,
-              const uint16_t* block_mask, const uint8_t* block_map, const RateCfg* rate) {
+              const uint16_t* block_mask, const uint8_t* block_map, const RateCfg* rate,
+              RdoArgs* args_only) {
   if (tx_size < 0 || tx_size >= 19) return -1;
   if (qp == nullptr || out == nullptr || qcoeff == nullptr || dqcoeff == nullptr) return -3;
   if (bd != 8 && bd != 10 && bd != 12) return -3;
@@ -123,6 +124,10 @@ int rdo_plane(const uint16_t* src, const uint16_t* pred, int stride, int width, 
     }
     return rdo_launch_m2(tx_size, a, s);
   }
+  if (args_only != nullptr) {  // the caller launches (rdo_frame's small-size launch)
+    *args_only = a;
+    return 0;
+  }
   return rdo_launch_m1(tx_size, a, s);
 }
 
@@ -151,12 +156,44 @@ int rdo_frame(const uint16_t* src, const uint16_t* pred, int stride, int width, 
       order[j] = order[j - 1];
       order[j - 1] = t;
     }
+  // small rectangles: 16x16, 8x8 and 4x4 (all three present, each in the
+  // split form with four kind groups) as one launch on the caller's stream,
+  // the other sizes on the internal streams beside it
+  bool small = !px && fan_width() > 1;
+  RdoSmall sm{};
+  const int ssz[3] = {2, 1, 0};
+  for (int k = 0; k < 3 && small; ++k) {
+    const int t = ssz[k];
+    if (!((size_mask >> t) & 1)) {
+      small = false;
+      break;
+    }
+    const int tiles = (width / tx_w(t)) * (height / tx_h(t)) * tx_w(t) / 64;  // P = 64 / w
+    int groups = 0;
+    RdoArgs& a = sm.a[k];
+    const int rc = rdo_plane(src, pred, stride, width, height, t, type_masks[t], bd, qp, rdmult,
+                             out[t], qcoeff[t], dqcoeff[t], caller, 0, nullptr, nullptr, nullptr,
+                             &a);
+    if (rc) return rc;
+    for (int i = 0; i < a.ntypes; ++i) groups += a.newcol[i];
+    if (groups != 4 || tiles >= kRdoSplitTiles) small = false;
+    sm.first[k + 1] = sm.first[k] + (a.nblocks + 64 / tx_w(t) - 1) / (64 / tx_w(t));
+  }
   hipStream_t* fs = fan_out(caller);
   int rc = 0;
-  for (int i = 0; i < n && rc == 0; ++i) {
+  if (small) rc = rdo_small_launch_m1(sm, caller);
+  for (int i = 0, k = 0; i < n && rc == 0; ++i) {
     const int s = order[i];
+    if (small && (s == 0 || s == 1 || s == 2)) continue;
+    // (small: the internal streams first, the caller's stream runs the
+    // small-size launch)
+    const int w = fan_width();
+    // (measured against all of them on one internal stream or on the
+    // caller's after the small-size launch: 0.1595 vs 0.1619 / 0.1608 ms per
+    // C5 rank at G = 8, 3.36 vs 3.65 / 3.86 ms for the row wavefront)
+    hipStream_t st = small && w > 1 ? fs[1 + k++ % (w - 1)] : fs[i % w];
     rc = rdo_plane(src, pred, stride, width, height, s, type_masks[s], bd, qp, rdmult, out[s],
-                   qcoeff[s], dqcoeff[s], fs[i % fan_width()], px);
+                   qcoeff[s], dqcoeff[s], st, px);
   }
   fan_in(caller);
   return rc;
@@ -237,21 +274,38 @@ __global__ __launch_bounds__(256) void sb_decide_kernel(SbArgs a) {
   }
   int64_t best = INT64_MAX;
   int best_s = 255;
+  // costs are >= 0; a block without a candidate costs INT64_MAX, so the sums
+  // saturate there instead of wrapping (a sum of non-negative costs
+  // saturating at INT64_MAX is order-free).  nblk <= 256: up to 4 blocks
+  // per lane; the first kMaxSbSizes sizes' loads are all in flight together
+  // (one memory latency for the decision, not one per size)
+  constexpr int kMaxSbSizes = 5;
+  int64_t vv[kMaxSbSizes][4];
+#pragma unroll
+  for (int i = 0; i < kMaxSbSizes; ++i) {
+    const int s = i < a.nsizes ? a.sizes[i] : a.sizes[0];
+    const int W = tx_w_dev(s), H = tx_h_dev(s);
+    const bool tiles = i < a.nsizes && !(y1 % H || x1 % W);
+    const int bw = a.width / W, nx = max(x1 / W, 1), nblk = tiles ? (x1 / W) * (y1 / H) : 0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int k = lane + 64 * q;
+      const int y = k / nx, x = k - y * nx;
+      vv[i][q] = k < nblk ? a.rec[s][(sy * 64 / H + y) * bw + sx * 64 / W + x].rdcost : 0;
+    }
+  }
   for (int i = 0; i < a.nsizes; ++i) {
     const int s = a.sizes[i];
     const int W = tx_w_dev(s), H = tx_h_dev(s);
     if (y1 % H || x1 % W) continue;
     const int bw = a.width / W, nx = x1 / W, nblk = nx * (y1 / H);
-    // costs are >= 0; a block without a candidate costs INT64_MAX, so the
-    // sums saturate there instead of wrapping
-    // (nblk <= 256: the loads of up to 4 blocks per lane in flight together;
-    // a sum of non-negative costs saturating at INT64_MAX is order-free)
     int64_t v[4];
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const int k = lane + 64 * q;
       const int y = k / nx, x = k - y * nx;
-      v[q] = k < nblk ? a.rec[s][(sy * 64 / H + y) * bw + sx * 64 / W + x].rdcost : 0;
+      v[q] = i < kMaxSbSizes ? vv[i < kMaxSbSizes ? i : 0][q]
+                             : (k < nblk ? a.rec[s][(sy * 64 / H + y) * bw + sx * 64 / W + x].rdcost : 0);
     }
     int64_t sum = sat_add(sat_add(v[0], v[1]), sat_add(v[2], v[3]));
     sum = (int64_t)lane_reduce64<64>((uint64_t)sum, [](uint64_t x, uint64_t y) {

@@ -78,6 +78,20 @@ struct RdoArgs {
   LavishRdoBlock* out;
 };
 
+// The TX-domain decision (mode 1) of the 16x16, 8x8 and 4x4 sizes of one
+// rectangle in one launch, for small rectangles (every present size would
+// take the split form: fewer than kRdoSplitTiles tiles, four vertical-kind
+// groups): workgroups [first[k], first[k + 1]) run size slot k (0: 16x16,
+// 1: 8x8, 2: 4x4; the longest-lived first), four waves per tile as in the
+// split form.  Replaces three launches on three streams and the cross-queue
+// waits between them (~15-35 us each at these sizes).
+struct RdoSmall {
+  RdoArgs a[3];
+  int first[4];
+};
+constexpr int kRdoSplitTiles = 2048;  // below this many tiles a mode-1 launch splits
+int rdo_small_launch_m1(const RdoSmall& m, hipStream_t s);
+
 // per mode: one size's launch (rdo_m<MODE>.hip); -2 for a size the mode
 // does not instantiate
 int rdo_launch_m0(int tx_size, const RdoArgs& a, hipStream_t s);
@@ -121,7 +135,6 @@ constexpr int rdo_nvmax() {
   constexpr int M = W > H ? W : H;
   return M >= 64 ? 1 : (M == 32 ? 2 : 4);
 }
-constexpr int kRdoSplitTiles = 2048;  // below this many tiles a launch splits
 
 // Per-tile LDS of the pixel-domain mode (MODE 2): the prediction pixels, the
 // inverse transform's transposition buffer, and per-block sums.
@@ -135,10 +148,35 @@ struct PxLds {
   uint64_t psse[P]; // this type's sum of (src - recon)^2
 };
 
+// The LDS of one workgroup of rdo_kernel<W, H, MODE, ., NVM waves> as one
+// carved buffer (byte offsets), so a kernel running several sizes
+// (rdo_small_kernel) can overlay them: the column-pass output per wave, the
+// MODE 0 per-type coefficients, the per-wave winners, the MODE 2 pixel
+// state, and the per-block bookkeeping of rdo_types.
+constexpr int lds_align(int v, int a) { return (v + a - 1) / a * a; }
+template <int W, int H, int MODE, int NVM>
+struct RdoLds {
+  using T = RTile<W, H>;
+  static constexpr int t1 = 0;
+  static constexpr int t2 = lds_align(t1 + 4 * NVM * T::T1, 16);
+  static constexpr int tb = lds_align(t2 + 4 * (MODE == 0 ? T::T2 : 4), 16);
+  static constexpr int px = lds_align(tb + 4 * (MODE >= 1 ? NVM * T::T2 : 4), 16);
+  static constexpr int rank = lds_align(px + (MODE == 2 ? (int)sizeof(PxLds<W, H>) : 0), 16);
+  static constexpr int ok = lds_align(rank + 16 * T::P, 4);
+  static constexpr int cc = lds_align(ok + 2 * T::P, 16);
+  static constexpr int dead = lds_align(cc + 4 * (MODE == 3 ? cc::kTabCells : 1), 4);
+  static constexpr int win = lds_align(dead + T::P, 4);
+  static constexpr int brd = lds_align(win + T::P, 8);
+  static constexpr int brk = lds_align(brd + 8 * NVM * T::P, 4);
+  static constexpr int bytes = lds_align(brk + NVM * T::P, 16);
+};
+
 template <int W, int H, int MODE, bool FAST, int QK, bool HBD, int BDI, int NVM>
 __device__ __forceinline__ void rdo_types(const RdoArgs& a, const int32_t (&res)[RTile<W, H>::CPT][H],
                                           int32_t* t1, int32_t* t2, int32_t* tb0, PxLds<W, H>* px,
-                                          int lane, int blk0, int nvalid, int wave, int nv) {
+                                          int lane, int blk0, int nvalid, int wave, int nv,
+                                          char* lds) {
+  using LY = RdoLds<W, H, MODE, NVM>;
   using C = TxCfg<W, H>;
   using T = RTile<W, H>;
   using B = Bd<BDI>;
@@ -160,8 +198,8 @@ __device__ __forceinline__ void rdo_types(const RdoArgs& a, const int32_t (&res)
   // appear in the block's search order, and each type's position in that
   // order; identity without per-block data.  A zero mask means DCT_DCT only
   // (get_tx_mask's rule, tx_search.c:1885-1888).
-  __shared__ uint8_t s_rank[T::P][16];
-  __shared__ uint16_t s_ok[T::P];
+  uint8_t(*const s_rank)[16] = reinterpret_cast<uint8_t(*)[16]>(lds + LY::rank);
+  uint16_t* const s_ok = reinterpret_cast<uint16_t*>(lds + LY::ok);
   if constexpr (DEC) {
     if ((NVM > 1 ? (int)threadIdx.x : lane) < T::P) {  // (wave 0 for the workgroup)
       uint32_t ok = 0xFFFFu;
@@ -192,7 +230,7 @@ __device__ __forceinline__ void rdo_types(const RdoArgs& a, const int32_t (&res)
     else wave_sync();
   }
   // MODE 3: the cost tables
-  __shared__ int32_t s_cc[RATE ? cc::kTabCells : 1];
+  int32_t* const s_cc = reinterpret_cast<int32_t*>(lds + LY::cc);
   if constexpr (RATE) {  // (mode 3: one wave per tile)
     for (int i = lane; i < cc::kCostCells; i += 64) s_cc[i] = a.cc_cost[i];
     if (lane < cc::kEobCells) s_cc[cc::kCostCells + lane] = a.cc_eob[lane];
@@ -521,7 +559,7 @@ __device__ __forceinline__ void rdo_types(const RdoArgs& a, const int32_t (&res)
     // A block none of whose allowed types is in the evaluated set (possible
     // only with caller masks) has no candidate: record best_type
     // TX_TYPE_INVALID (255), eob 0, rdcost INT64_MAX, zero coefficients.
-    __shared__ uint8_t s_dead[T::P];
+    uint8_t* const s_dead = reinterpret_cast<uint8_t*>(lds + LY::dead);
 #pragma unroll
     for (int k = 0; k < T::RPT; ++k) {
       const int j = k * 64 + lane;
@@ -564,9 +602,10 @@ __device__ __forceinline__ void rdo_types(const RdoArgs& a, const int32_t (&res)
     // With the types over nv waves, each block's winner is the lowest
     // (rdcost, search rank) over the waves' bests: the sequential scan's
     // first type of strictly lowest cost, as every rank is distinct.
-    __shared__ uint8_t s_win[T::P];  // winning wave per block, 255: none
-    __shared__ int64_t s_brd[NVM][T::P];
-    __shared__ uint8_t s_brk[NVM][T::P];
+    // winning wave per block (255: none), each wave's best cost and rank
+    uint8_t* const s_win = reinterpret_cast<uint8_t*>(lds + LY::win);
+    int64_t(*const s_brd)[T::P] = reinterpret_cast<int64_t(*)[T::P]>(lds + LY::brd);
+    uint8_t(*const s_brk)[T::P] = reinterpret_cast<uint8_t(*)[T::P]>(lds + LY::brk);
     {
 #pragma unroll
       for (int k = 0; k < T::RPT; ++k) {
@@ -662,27 +701,18 @@ constexpr int rdo_waves() {
   return W * H >= 512 ? LAVISH_RDO_WV32 : 1;
 }
 
-template <int W, int H, int MODE, int BDI, bool SPLIT = false>
-__global__ __launch_bounds__(64 * (rdo_nvmax<W, H, MODE, SPLIT>()))
-__attribute__((amdgpu_waves_per_eu(rdo_waves<W, H, MODE>())))
-void rdo_kernel(RdoArgs a) {
+// one tile (P blocks) of rdo_kernel: tile index `tile`, the workgroup's
+// wave `wave` of nv sharing it (NVM > 1), its LDS (RdoLds bytes)
+template <int W, int H, int MODE, int BDI, int NVM>
+__device__ __forceinline__ void rdo_tile(const RdoArgs& a, int tile, int lane, int wave, int nv,
+                                         char* lds) {
   using T = RTile<W, H>;
-  constexpr int NVM = rdo_nvmax<W, H, MODE, SPLIT>();
-  __shared__ int32_t t1s[NVM * T::T1];
-  __shared__ __attribute__((aligned(16))) int32_t t2[MODE == 0 ? T::T2 : 4];
-  __shared__ __attribute__((aligned(16))) int32_t tb[MODE >= 1 ? NVM * T::T2 : 4];
-  __shared__ typename std::conditional<MODE == 2, PxLds<W, H>, int>::type pxs;
-  PxLds<W, H>* px = MODE == 2 ? reinterpret_cast<PxLds<W, H>*>(&pxs) : nullptr;
-
-  // NVM > 1: the workgroup's waves share one tile, each a share of the types
-  // (threadIdx.x & 63 for the lane made the compiler spill ~2x more in
-  // these register-bound kernels; the mbcnt lane id does not)
-  const int lane = NVM > 1 ? __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u))
-                           : (int)threadIdx.x;
-  const int wave = NVM > 1 ? __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) : 0;
-  const int nv = NVM > 1 ? (int)(blockDim.x >> 6) : 1;
-  int32_t* const t1 = t1s + wave * T::T1;
-  const int blk0 = blockIdx.x * T::P;
+  using LY = RdoLds<W, H, MODE, NVM>;
+  int32_t* const t2 = reinterpret_cast<int32_t*>(lds + LY::t2);
+  int32_t* const tb = reinterpret_cast<int32_t*>(lds + LY::tb);
+  PxLds<W, H>* px = MODE == 2 ? reinterpret_cast<PxLds<W, H>*>(lds + LY::px) : nullptr;
+  int32_t* const t1 = reinterpret_cast<int32_t*>(lds + LY::t1) + wave * T::T1;
+  const int blk0 = tile * T::P;
   if (blk0 >= a.nblocks) return;
   const int nvalid = min(T::P, a.nblocks - blk0);
 
@@ -732,13 +762,13 @@ void rdo_kernel(RdoArgs a) {
   if constexpr (MODE >= 1) {
     if (fast)
       rdo_types<W, H, MODE, true, LAVISH_QUANT_FP, true, BDI, NVM>(a, res, t1, t2, tb, px, lane,
-                                                                   blk0, nvalid, wave, nv);
+                                                                   blk0, nvalid, wave, nv, lds);
     else
       rdo_types<W, H, MODE, false, LAVISH_QUANT_FP, true, BDI, NVM>(a, res, t1, t2, tb, px, lane,
-                                                                    blk0, nvalid, wave, nv);
+                                                                    blk0, nvalid, wave, nv, lds);
   } else {
 #define LAVISH_RDO_RUN(F, Q, HB) \
-  rdo_types<W, H, 0, F, Q, HB, 0, 1>(a, res, t1, t2, tb, px, lane, blk0, nvalid, 0, 1)
+  rdo_types<W, H, 0, F, Q, HB, 0, 1>(a, res, t1, t2, tb, px, lane, blk0, nvalid, 0, 1, lds)
     if (a.quant_kind == LAVISH_QUANT_NONE) {
       if (fast) LAVISH_RDO_RUN(true, LAVISH_QUANT_NONE, false);
       else LAVISH_RDO_RUN(false, LAVISH_QUANT_NONE, false);
@@ -761,6 +791,41 @@ void rdo_kernel(RdoArgs a) {
     }
 #undef LAVISH_RDO_RUN
   }
+}
+
+template <int W, int H, int MODE, int BDI, bool SPLIT = false>
+__global__ __launch_bounds__(64 * (rdo_nvmax<W, H, MODE, SPLIT>()))
+__attribute__((amdgpu_waves_per_eu(rdo_waves<W, H, MODE>())))
+void rdo_kernel(RdoArgs a) {
+  constexpr int NVM = rdo_nvmax<W, H, MODE, SPLIT>();
+  __shared__ __attribute__((aligned(16))) char lds[RdoLds<W, H, MODE, NVM>::bytes];
+  // NVM > 1: the workgroup's waves share one tile, each a share of the types
+  // (threadIdx.x & 63 for the lane made the compiler spill ~2x more in
+  // these register-bound kernels; the mbcnt lane id does not)
+  const int lane = NVM > 1 ? __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u))
+                           : (int)threadIdx.x;
+  const int wave = NVM > 1 ? __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) : 0;
+  const int nv = NVM > 1 ? (int)(blockDim.x >> 6) : 1;
+  rdo_tile<W, H, MODE, BDI, NVM>(a, blockIdx.x, lane, wave, nv, lds);
+}
+
+template <int MODE>
+constexpr int rdo_small_lds() {
+  constexpr int a = RdoLds<16, 16, MODE, 4>::bytes, b = RdoLds<8, 8, MODE, 4>::bytes,
+                c = RdoLds<4, 4, MODE, 4>::bytes;
+  return a > b ? (a > c ? a : c) : (b > c ? b : c);
+}
+
+template <int MODE>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LAVISH_RDO_WV16)))
+void rdo_small_kernel(RdoSmall m) {
+  __shared__ __attribute__((aligned(16))) char lds[rdo_small_lds<MODE>()];
+  const int lane = __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int b = blockIdx.x;
+  if (b < m.first[1]) rdo_tile<16, 16, MODE, 0, 4>(m.a[0], b - m.first[0], lane, wave, 4, lds);
+  else if (b < m.first[2]) rdo_tile<8, 8, MODE, 0, 4>(m.a[1], b - m.first[1], lane, wave, 4, lds);
+  else rdo_tile<4, 4, MODE, 0, 4>(m.a[2], b - m.first[2], lane, wave, 4, lds);
 }
 
 template <int W, int H, int MODE>

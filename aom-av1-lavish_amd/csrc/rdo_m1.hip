@@ -5,4 +5,10 @@
 
 namespace lavish {
 int rdo_launch_m1(int tx_size, const RdoArgs& a, hipStream_t s) { return launch_size<1>(tx_size, a, s); }
+int rdo_small_launch_m1(const RdoSmall& m, hipStream_t s) {
+  if (m.first[3] <= 0) return 0;
+  hipLaunchKernelGGL(rdo_small_kernel<1>, dim3(m.first[3]), dim3(256), 0, s, m);
+  LAVISH_CHECK(hipGetLastError());
+  return 0;
+}
 }  // namespace lavish
