@@ -88,6 +88,15 @@ int fan_width();
 int set_fan_width(int w);
 hipStream_t* fan_out(hipStream_t caller);
 void fan_in(hipStream_t caller);
+// a private set of internal streams and fork / join events: while installed
+// (fan_use) this thread's fan_out / fan_in use it instead of the shared
+// per-thread set (nullptr: back to the shared set).  A captured graph's
+// fan-out gets its own set, so its fork / join events and streams are never
+// the ones uncaptured calls record and wait on.
+struct FanSet;
+FanSet* fan_create();
+void fan_destroy(FanSet* f);
+void fan_use(FanSet* f);
 
 // av1_highbd_iwht4x4_add (av1/common/idct.c:34-40) on a host u16 4x4 block
 // (wht.hip): the lossless branch of the inverse-transform shims

@@ -638,6 +638,7 @@ struct LavishRdoGraph {
   hipGraph_t graph = nullptr;
   hipGraphExec_t exec = nullptr;
   void* scratch = nullptr;
+  lavish::FanSet* fan = nullptr;  // the capture's own fork / join streams and events
 };
 
 extern "C" int lavish_rdo_graph_create(const uint16_t* src, const uint16_t* pred, int stride,
@@ -658,6 +659,12 @@ extern "C" int lavish_rdo_graph_create(const uint16_t* src, const uint16_t* pred
   if (rc) return rc;
   LavishRdoGraph* g = new LavishRdoGraph();
   LAVISH_CHECK(hipMalloc(&g->scratch, bytes > 0 ? bytes : 16));
+  // the warm-up and the capture fork / join over a private stream + event
+  // set: with the shared per-thread set, graphs captured after an uncaptured
+  // whole-4K-frame step on the same thread crashed the host inside
+  // hipGraphLaunch (round 5, tools/repro_c5test.py; not with the private set)
+  g->fan = lavish::fan_create();
+  lavish::fan_use(g->fan);
   hipStream_t cs;
   LAVISH_CHECK(hipStreamCreateWithFlags(&cs, hipStreamNonBlocking));
   // the warm-up below reads src / pred and writes every output buffer: order
@@ -680,6 +687,7 @@ extern "C" int lavish_rdo_graph_create(const uint16_t* src, const uint16_t* pred
                                       &bytes);
   LAVISH_CHECK(hipStreamSynchronize(cs));
   if (rc != 0) {
+    lavish::fan_use(nullptr);
     LAVISH_CHECK(hipStreamDestroy(cs));
     lavish_rdo_graph_destroy(g);
     return rc;
@@ -694,6 +702,7 @@ extern "C" int lavish_rdo_graph_create(const uint16_t* src, const uint16_t* pred
                                       &bytes);
   hipGraph_t graph = nullptr;
   LAVISH_CHECK(hipStreamEndCapture(cs, &graph));
+  lavish::fan_use(nullptr);
   LAVISH_CHECK(hipStreamDestroy(cs));
   g->graph = graph;
   if (rc == 0 && graph != nullptr)
@@ -717,5 +726,6 @@ extern "C" void lavish_rdo_graph_destroy(LavishRdoGraph* g) {
   if (g->exec) LAVISH_CHECK(hipGraphExecDestroy(g->exec));
   if (g->graph) LAVISH_CHECK(hipGraphDestroy(g->graph));
   if (g->scratch) LAVISH_CHECK(hipFree(g->scratch));
+  lavish::fan_destroy(g->fan);
   delete g;
 }

@@ -273,20 +273,48 @@ struct FrameStreams {
   hipEvent_t fork = nullptr, join[kFrameStreams] = {};
 };
 static thread_local FrameStreams t_fs;
+struct FanSet {
+  FrameStreams fs;
+};
+static thread_local FanSet* t_fan_own = nullptr;  // fan_use: a private set
+
+static void frame_streams_init(FrameStreams& f, int dev) {
+  for (int i = 1; i < kFrameStreams; ++i) {
+    LAVISH_CHECK(hipStreamCreateWithFlags(&f.s[i], hipStreamNonBlocking));
+    LAVISH_CHECK(hipEventCreateWithFlags(&f.join[i], hipEventDisableTiming));
+  }
+  LAVISH_CHECK(hipEventCreateWithFlags(&f.fork, hipEventDisableTiming));
+  f.device = dev;
+}
 
 static FrameStreams& frame_streams() {
+  if (t_fan_own != nullptr) return t_fan_own->fs;
   int dev = 0;
   LAVISH_CHECK(hipGetDevice(&dev));
-  if (t_fs.device != dev) {
-    for (int i = 1; i < kFrameStreams; ++i) {
-      LAVISH_CHECK(hipStreamCreateWithFlags(&t_fs.s[i], hipStreamNonBlocking));
-      LAVISH_CHECK(hipEventCreateWithFlags(&t_fs.join[i], hipEventDisableTiming));
-    }
-    LAVISH_CHECK(hipEventCreateWithFlags(&t_fs.fork, hipEventDisableTiming));
-    t_fs.device = dev;
-  }
+  if (t_fs.device != dev) frame_streams_init(t_fs, dev);
   return t_fs;
 }
+
+FanSet* fan_create() {
+  int dev = 0;
+  LAVISH_CHECK(hipGetDevice(&dev));
+  FanSet* f = new FanSet();
+  frame_streams_init(f->fs, dev);
+  return f;
+}
+
+void fan_destroy(FanSet* f) {
+  if (f == nullptr) return;
+  if (t_fan_own == f) t_fan_own = nullptr;
+  for (int i = 1; i < kFrameStreams; ++i) {
+    LAVISH_CHECK(hipStreamDestroy(f->fs.s[i]));
+    LAVISH_CHECK(hipEventDestroy(f->fs.join[i]));
+  }
+  LAVISH_CHECK(hipEventDestroy(f->fs.fork));
+  delete f;
+}
+
+void fan_use(FanSet* f) { t_fan_own = f; }
 
 // streams the per-size work of lavish_rdo_frame / lavish_rdo_reconstruct is
 // dealt over: the caller + fan_width() - 1 internal streams (default 3; 1:

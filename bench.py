@@ -83,8 +83,10 @@ def parse():
     ap.add_argument("--c5-no-graphs", action="store_true",
                     help="c5: launch each rectangle's step directly instead of replaying its "
                          "captured HIP graph")
-    ap.add_argument("--c5-chunks", type=int, default=4,
-                    help="c5 wavefront: column chunks per SB row")
+    ap.add_argument("--c5-chunks", type=int, default=1,
+                    help="c5 wavefront: column chunks per SB row (1: each row one step, "
+                         "the rows a chain on one stream; 4 chunks measured 24-25 ms per 4K "
+                         "frame in round 4 against 6.3-6.8 for 1)")
     ap.add_argument("--c5-form", choices=("tiles", "band", "wavefront"), default="tiles",
                     help="C5 sharding: balanced band + tail segments with overlapped "
                          "all-gathers, or the row-wavefront with p2p edges (lavish_dsp/shard.py)")

@@ -14,6 +14,7 @@
 * C5 at world 1: the SB-row band processor of lavish_dsp/shard.py over 3
   bands on 3 streams equals the whole-frame step.
 """
+import gc
 import os
 
 import numpy as np
@@ -226,24 +227,32 @@ def test_c5_partition_rects_on_gpu(L):
     torch.cuda.synchronize()
     np.testing.assert_array_equal(wf.cpu().numpy(), ref)
     # direct launches / each chunk a replayed HIP graph / graphs over 4
-    # streams with the chunk dependencies as events
-    for graphs, nst in ((False, 0), (True, 0), (True, 4)):
+    # streams with the chunk dependencies as events / one chunk per row (the
+    # bench's form: the rows in order on one of the streams, no events)
+    for graphs, nst, chunks in ((False, 0, 4), (True, 0, 4), (True, 4, 4), (True, 4, 1)):
         out = torch.full_like(ts, -1)
         direct = shard.c4_rect_processor(ts, tp, qp, rdmult, 10, {}, out=out, graphs=graphs)
         streams = [torch.cuda.Stream() for _ in range(nst)] or None
         if graphs and streams:
-            # every chunk's graph captured first, on one stream: captures and
-            # instantiations do not interleave with replays on other streams
-            # (a host crash inside hipGraphLaunch was seen twice in round 5's
-            # full-suite runs when they did; not reproduced in isolation)
-            shard.wavefront_frame(H, W, 0, 1, direct, chunks=4, out=out)
+            # every chunk's graph captured first, on one stream (as bench.py
+            # does); the captures run after the uncaptured whole-frame step
+            # above on this thread -- the order that crashed the host inside
+            # hipGraphLaunch before captures got their own fork / join set
+            shard.wavefront_frame(H, W, 0, 1, direct, chunks=chunks, out=out)
             torch.cuda.synchronize()
         for _ in range(2):  # the second pass replays every cached chunk
             out.fill_(-1)
-            wf = shard.wavefront_frame(H, W, 0, 1, direct, chunks=4, out=out, streams=streams)
+            wf = shard.wavefront_frame(H, W, 0, 1, direct, chunks=chunks, out=out,
+                                       streams=streams)
             torch.cuda.synchronize()
             assert wf.data_ptr() == out.data_ptr()
-            np.testing.assert_array_equal(out.cpu().numpy(), ref, err_msg="graphs %s" % graphs)
+            np.testing.assert_array_equal(out.cpu().numpy(), ref,
+                                          err_msg="graphs %s chunks %d" % (graphs, chunks))
+        # this case's graphs freed here, not by a later collection in the
+        # middle of the next case's replays
+        del direct, wf
+        gc.collect()
+        torch.cuda.synchronize()
 
 
 def test_rdo_graph_replays_new_inputs(L):
