@@ -2,6 +2,7 @@
 // rdo_kern.h, instantiated per mode in rdo_m0..3.hip), the frame-level step
 // (every candidate size, the per-SB TX-size decision, the reconstruction),
 // the 64-point pixel-domain path and the captured step (HIP graph).
+#include <cstddef>
 #include "rdo_kern.h"
 
 namespace lavish {
@@ -216,6 +217,10 @@ __device__ __forceinline__ int64_t sat_add(int64_t a, int64_t b) {
   return a > INT64_MAX - b ? INT64_MAX : a + b;
 }
 
+// sb_decide reads a block's (best_type, eob) as one 8-byte word
+static_assert(offsetof(LavishRdoBlock, best_type) == 0 && offsetof(LavishRdoBlock, eob) == 4,
+              "LavishRdoBlock layout");
+
 struct SbArgs {
   int nsizes;
   int sizes[19];                       // candidate order: largest area first
@@ -248,39 +253,33 @@ __global__ __launch_bounds__(256) void sb_decide_kernel(SbArgs a) {
   if (sb >= a.sbw * a.sbh) return;
   const int sy = sb / a.sbw, sx = sb - sy * a.sbw;
   const int y1 = min(64, a.height - sy * 64), x1 = min(64, a.width - sx * 64);
-  {
-    // recon = pred over the SB: 16-byte rows when the SB is whole and aligned
-    const size_t o = (size_t)sy * 64 * a.stride + (size_t)sx * 64;
-    const uint16_t* p = a.pred + o;
-    uint16_t* r = a.recon + o;
-    const bool vec = x1 == 64 && ((((uintptr_t)p | (uintptr_t)r | ((uintptr_t)a.stride * 2)) & 15) == 0);
-    if (vec) {
-      typedef uint32_t u4 __attribute__((ext_vector_type(4)));
-      u4 v[8];
+  // recon = pred over the SB: 16-byte rows when the SB is whole and aligned.
+  // Every load of the wave -- the copy's rows, and per candidate size its
+  // blocks' costs and (type, eob) pairs -- is issued before the first store
+  // or use, so the decision and the job list cost one memory latency, not
+  // three (copy, costs, then the chosen size's records).
+  const size_t o = (size_t)sy * 64 * a.stride + (size_t)sx * 64;
+  const uint16_t* p = a.pred + o;
+  uint16_t* r = a.recon + o;
+  const bool vec = x1 == 64 && ((((uintptr_t)p | (uintptr_t)r | ((uintptr_t)a.stride * 2)) & 15) == 0);
+  typedef uint32_t u4 __attribute__((ext_vector_type(4)));
+  u4 cp[8];
+  if (vec) {
 #pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        const int row = i * 8 + (lane >> 3);
-        if (row < y1) v[i] = *(const u4*)(p + (size_t)row * a.stride + 8 * (lane & 7));
-      }
-#pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        const int row = i * 8 + (lane >> 3);
-        if (row < y1) *(u4*)(r + (size_t)row * a.stride + 8 * (lane & 7)) = v[i];
-      }
-    } else {
-      for (int row = 0; row < y1; ++row)
-        if (lane < x1) r[(size_t)row * a.stride + lane] = p[(size_t)row * a.stride + lane];
+    for (int i = 0; i < 8; ++i) {
+      const int row = i * 8 + (lane >> 3);
+      if (row < y1) cp[i] = *(const u4*)(p + (size_t)row * a.stride + 8 * (lane & 7));
     }
   }
   int64_t best = INT64_MAX;
-  int best_s = 255;
+  int best_s = 255, best_i = -1;
   // costs are >= 0; a block without a candidate costs INT64_MAX, so the sums
   // saturate there instead of wrapping (a sum of non-negative costs
   // saturating at INT64_MAX is order-free).  nblk <= 256: up to 4 blocks
   // per lane; the first kMaxSbSizes sizes' loads are all in flight together
-  // (one memory latency for the decision, not one per size)
   constexpr int kMaxSbSizes = 5;
   int64_t vv[kMaxSbSizes][4];
+  uint64_t mm[kMaxSbSizes][4];  // (best_type, eob) of the same blocks
 #pragma unroll
   for (int i = 0; i < kMaxSbSizes; ++i) {
     const int s = i < a.nsizes ? a.sizes[i] : a.sizes[0];
@@ -291,8 +290,20 @@ __global__ __launch_bounds__(256) void sb_decide_kernel(SbArgs a) {
     for (int q = 0; q < 4; ++q) {
       const int k = lane + 64 * q;
       const int y = k / nx, x = k - y * nx;
-      vv[i][q] = k < nblk ? a.rec[s][(sy * 64 / H + y) * bw + sx * 64 / W + x].rdcost : 0;
+      const LavishRdoBlock* rb = a.rec[s] + ((sy * 64 / H + y) * bw + sx * 64 / W + x);
+      vv[i][q] = k < nblk ? rb->rdcost : 0;
+      mm[i][q] = k < nblk ? *(const uint64_t*)rb : 0;
     }
+  }
+  if (vec) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int row = i * 8 + (lane >> 3);
+      if (row < y1) *(u4*)(r + (size_t)row * a.stride + 8 * (lane & 7)) = cp[i];
+    }
+  } else {
+    for (int row = 0; row < y1; ++row)
+      if (lane < x1) r[(size_t)row * a.stride + lane] = p[(size_t)row * a.stride + lane];
   }
   for (int i = 0; i < a.nsizes; ++i) {
     const int s = a.sizes[i];
@@ -314,6 +325,7 @@ __global__ __launch_bounds__(256) void sb_decide_kernel(SbArgs a) {
     if (sum < best) {
       best = sum;
       best_s = s;
+      best_i = i;
     }
   }
   if (lane == 0) {
@@ -327,13 +339,21 @@ __global__ __launch_bounds__(256) void sb_decide_kernel(SbArgs a) {
   const int bw = a.width / W, nx = x1 / W, nblk = nx * (y1 / H), n = max_eob_dev(s);
   LavishInvJob* const slot = a.jobs[s] + (size_t)sb * ((64 / W) * (64 / H));
   int base = 0;
-  for (int k0 = 0; k0 < nblk; k0 += 64) {
-    const int k = k0 + lane;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    if (64 * q >= nblk) break;
+    const int k = 64 * q + lane;
     const int y = k / nx, x = k - y * nx;
     const int blk = (sy * 64 / H + y) * bw + sx * 64 / W + x;
     const bool live = k < nblk;
-    const LavishRdoBlock r = a.rec[s][live ? blk : 0];
-    const bool coded = live && r.eob != 0;
+    // the chosen size's (type, eob): from the batch above (a select over the
+    // sizes, no indexed private array), or loaded for a 6th+ size
+    uint64_t te = 0;
+#pragma unroll
+    for (int i = 0; i < kMaxSbSizes; ++i) te = best_i == i ? mm[i][q] : te;
+    if (best_i >= kMaxSbSizes) te = live ? *(const uint64_t*)(a.rec[s] + blk) : 0;
+    const int32_t btype = (int32_t)(uint32_t)te, beob = (int32_t)(te >> 32);
+    const bool coded = live && beob != 0;
     const uint64_t m = __builtin_amdgcn_ballot_w64(coded);
     if (coded) {
       const int at = base + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
@@ -341,8 +361,8 @@ __global__ __launch_bounds__(256) void sb_decide_kernel(SbArgs a) {
       LavishInvJob j;
       j.dst_off = (int64_t)(sy * 64 + y * H) * a.stride + sx * 64 + x * W;
       j.coeff_off = (int64_t)blk * n;
-      j.tx_type = r.best_type;
-      j.eob = r.eob;
+      j.tx_type = btype;
+      j.eob = beob;
       slot[at] = j;
     }
     base += __popcll(m);

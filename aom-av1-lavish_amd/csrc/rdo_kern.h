@@ -693,11 +693,16 @@ __device__ __forceinline__ void rdo_types(const RdoArgs& a, const int32_t (&res)
 #ifndef LAVISH_RDO_WV64
 #define LAVISH_RDO_WV64 2
 #endif
-template <int W, int H, int MODE>
+// (SPLIT: the small-grid instantiation.  A 64-point size there has a few
+// hundred blocks at most -- a wave per block, far fewer than the SIMDs --
+// so its wave's lifetime is the kernel's duration and occupancy buys
+// nothing: it asks for one wave per SIMD and keeps every value in VGPRs
+// instead of the 2-wave request's spills to scratch.)
+template <int W, int H, int MODE, bool SPLIT = false>
 constexpr int rdo_waves() {
   if (MODE != 1) return 1;
   if (W == 16 && H == 16) return LAVISH_RDO_WV16;
-  if (W * H >= 2048) return LAVISH_RDO_WV64;
+  if (W * H >= 2048) return SPLIT ? 1 : LAVISH_RDO_WV64;
   return W * H >= 512 ? LAVISH_RDO_WV32 : 1;
 }
 
@@ -795,7 +800,7 @@ __device__ __forceinline__ void rdo_tile(const RdoArgs& a, int tile, int lane, i
 
 template <int W, int H, int MODE, int BDI, bool SPLIT = false>
 __global__ __launch_bounds__(64 * (rdo_nvmax<W, H, MODE, SPLIT>()))
-__attribute__((amdgpu_waves_per_eu(rdo_waves<W, H, MODE>())))
+__attribute__((amdgpu_waves_per_eu(rdo_waves<W, H, MODE, SPLIT>())))
 void rdo_kernel(RdoArgs a) {
   constexpr int NVM = rdo_nvmax<W, H, MODE, SPLIT>();
   __shared__ __attribute__((aligned(16))) char lds[RdoLds<W, H, MODE, NVM>::bytes];
@@ -841,6 +846,12 @@ void launch_rdo(const RdoArgs& a, hipStream_t s) {
   if constexpr (NVM > 1) {
     if (nv > 1 && grid < kRdoSplitTiles) {
       hipLaunchKernelGGL((rdo_kernel<W, H, MODE, 0, true>), dim3(grid), dim3(64 * nv), 0, s, a);
+      LAVISH_CHECK(hipGetLastError());
+      return;
+    }
+  } else if constexpr (MODE == 1 && W * H >= 2048) {
+    if (grid < kRdoSplitTiles) {  // few blocks: the spill-free one-wave-per-SIMD build
+      hipLaunchKernelGGL((rdo_kernel<W, H, MODE, 0, true>), dim3(grid), dim3(64), 0, s, a);
       LAVISH_CHECK(hipGetLastError());
       return;
     }
