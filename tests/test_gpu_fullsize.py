@@ -229,7 +229,8 @@ def test_c5_partition_rects_on_gpu(L):
     # direct launches / each chunk a replayed HIP graph / graphs over 4
     # streams with the chunk dependencies as events / one chunk per row (the
     # bench's form: the rows in order on one of the streams, no events)
-    for graphs, nst, chunks in ((False, 0, 4), (True, 0, 4), (True, 4, 4), (True, 4, 1)):
+    for graphs, nst, chunks in ((False, 0, 4), (True, 0, 4), (True, 4, 4), (False, 4, 1),
+                                (True, 4, 1)):
         out = torch.full_like(ts, -1)
         direct = shard.c4_rect_processor(ts, tp, qp, rdmult, 10, {}, out=out, graphs=graphs)
         streams = [torch.cuda.Stream() for _ in range(nst)] or None
