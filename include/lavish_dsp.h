@@ -476,8 +476,10 @@ int lavish_rdo_reconstruct(uint32_t size_mask,
  * overlap).  No reference counterpart: a launch-count aid for callers that
  * run the step on many small rectangles.  Creation runs the step once
  * (uncaptured) after the work already queued on `stream` and waits for it:
- * it WRITES records, qcoeff, dqcoeff, recon and sb_tx_size.  -8: capture /
- * instantiation failed. */
+ * it WRITES records, qcoeff, dqcoeff, recon and sb_tx_size.  The graph owns
+ * its reconstruction scratch and the internal streams / fork-join events its
+ * capture forked over (none shared with uncaptured calls on the thread).
+ * -8: capture / instantiation failed. */
 typedef struct LavishRdoGraph LavishRdoGraph;
 int lavish_rdo_graph_create(const uint16_t *src, const uint16_t *pred, int stride,
                             int width, int height, uint32_t size_mask,
