@@ -658,7 +658,7 @@ struct LavishRdoGraph {
   hipGraph_t graph = nullptr;
   hipGraphExec_t exec = nullptr;
   void* scratch = nullptr;
-  lavish::FanSet* fan = nullptr;  // the capture's own fork / join streams and events
+  lavish::FanSet* fan = nullptr;  // the capture's own fork / join set (freed once instantiated)
 };
 
 extern "C" int lavish_rdo_graph_create(const uint16_t* src, const uint16_t* pred, int stride,
@@ -727,6 +727,12 @@ extern "C" int lavish_rdo_graph_create(const uint16_t* src, const uint16_t* pred
   g->graph = graph;
   if (rc == 0 && graph != nullptr)
     LAVISH_CHECK(hipGraphInstantiate(&g->exec, graph, nullptr, nullptr, 0));
+  // the fork / join set served the warm-up and the capture only: the
+  // instantiated graph's branches run on the runtime's own streams, so the
+  // set goes now instead of holding 2 streams + 3 events per graph for the
+  // graph's lifetime (every replay test runs after this release)
+  lavish::fan_destroy(g->fan);
+  g->fan = nullptr;
   if (rc != 0 || g->exec == nullptr) {
     lavish_rdo_graph_destroy(g);
     return rc ? rc : -8;

@@ -184,6 +184,14 @@ void scale_shim(const Pix* src, int ss, Pix* dst, int ds, int w, int h,
                 const LavishInterpFilterParams* fpx, const LavishInterpFilterParams* fpy,
                 int spx, int xs, int spy, int ys, LavishConvolveParams* cp, int bd) {
   if (w <= 0 || h <= 0 || !fpx || !fpy || !cp) return;
+  // a step or phase the kernel does not take: refuse before staging, so the
+  // caller's buffers stay untouched (the kernel would skip the block and the
+  // copy-back would hand over unwritten scratch)
+  if (xs < 1 || xs > kMaxStep || ys < 1 || ys > kMaxStep || spx < 0 || spy < 0 ||
+      spx > (1 << kScaleBits) - 1 || spy > (1 << kScaleBits) - 1) {
+    shim_reject("av1_convolve_2d_scale_hip", -6);
+    return;
+  }
   const int fo_x = fpx->taps / 2 - 1, fo_y = fpy->taps / 2 - 1;
   const int wx = (((w - 1) * xs + spx) >> kScaleBits) + fpx->taps;
   const int wy = (((h - 1) * ys + spy) >> kScaleBits) + fpy->taps;

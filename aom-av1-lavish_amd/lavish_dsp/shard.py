@@ -197,21 +197,23 @@ def sharded_frame(height, width, rank, world, process_rect, group=None, like=Non
                     with torch.cuda.stream(caller):  # allocated on the caller's stream
                         full = torch.empty((height, width), dtype=ref.dtype, device=ref.device)
                     st.wait_stream(caller)
-                fin.append(_gather_rects(local, rects, full, group, async_op=True))
+                fin.append((phase, _gather_rects(local, rects, full, group, async_op=True)))
         else:
             local = process_rect(*rect) if rect is not None else None
             if full is None:
                 ref = local if local is not None else like
                 full = torch.empty((height, width), dtype=ref.dtype, device=ref.device)
-            fin.append(_gather_rects(local, rects, full, group, async_op=True))
+            fin.append((phase, _gather_rects(local, rects, full, group, async_op=True)))
     if streams:
-        for phase, f in enumerate(fin):
+        # each finisher on the stream its phase ran on (a skipped phase 0
+        # leaves the tail's gather first in `fin`, still on streams[1])
+        for phase, f in fin:
             with torch.cuda.stream(streams[phase]):
                 f()
         for st in streams:
             caller.wait_stream(st)
     else:
-        for f in fin:
+        for _, f in fin:
             f()
     return full
 

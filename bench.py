@@ -61,6 +61,15 @@ def metric_name(args):
     return "superblocks/s, workload %s (component bench; not the headline metric)" % args.workload
 
 
+def _hw_queues(v):
+    """--hw-queues: 0 (the runtime's default) or 1..32 -- the HIP runtime
+    refuses GPU_MAX_HW_QUEUES above 32 only once the run has started."""
+    n = int(v)
+    if n != 0 and not 1 <= n <= 32:
+        raise argparse.ArgumentTypeError("--hw-queues must be 0 or within 1..32, got %d" % n)
+    return n
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1,
@@ -112,7 +121,7 @@ def parse():
                     help="run the C3 and C2 legs back to back on one stream (default: C3 on a "
                          "second stream beside C2)")
     ap.add_argument("--overlap", action="store_true", help=argparse.SUPPRESS)  # the default
-    ap.add_argument("--hw-queues", type=int, default=0,
+    ap.add_argument("--hw-queues", type=_hw_queues, default=0,
                     help="GPU_MAX_HW_QUEUES for this process (set before HIP starts; "
                          "0: the runtime's default)")
     ap.add_argument("--fan-width", type=int, default=0,
@@ -355,6 +364,12 @@ def c4_roofline(ms, W, H, masks, coded, nbytes):
             v = json.load(open(C4_VALU_JSON))
         except (ValueError, OSError):
             v = None
+        stale = c4_counts_stale(v) if v is not None else "unreadable"
+        if stale:
+            # the counts describe other code: report the
+            # algorithmic fraction only, and say why the counted ones are gone
+            roof["counts_stale"] = stale
+            v = None
         if v is not None:
             issued = float(v["valu_instr_per_step"]) * 64
             roof["issue_frac"] = round(issued / (ms * 1e-3) / 1e12 / VALU_PEAK_TOPS, 4)
@@ -362,8 +377,34 @@ def c4_roofline(ms, W, H, masks, coded, nbytes):
             roof["traffic"] = v.get("hbm_bytes_per_step")
             if roof["traffic"]:
                 roof["traffic_over_algorithmic"] = round(roof["traffic"] / nbytes, 3)
-            roof["counts"] = "profiles/c4_valu.json (%s)" % v.get("source", "")
+            roof["counts"] = "profiles/c4_valu.json (round %s: %s)" % (v.get("round"),
+                                                                      v.get("source", ""))
     return roof
+
+
+def c4_counts_stale(v):
+    """Why profiles/c4_valu.json no longer describes the library's C4 kernels
+    (None when it does): every counted kernel must still exist with the
+    resource signature (VGPR / SGPR / spills / LDS / scratch from the
+    code-object metadata, tools/kernel_resources.py) it had when counted."""
+    sig = v.get("kernels") or {}
+    if "round" not in v or not sig or any("signature" not in k for k in sig.values()):
+        return "no per-kernel signatures (written before round 6)"
+    try:
+        sys.path.insert(0, os.path.join(ROOT, "tools"))
+        import kernel_resources as KR
+        res = KR.kernel_resources(os.path.join(ROOT, "aom-av1-lavish_amd", "liblavish_hip.so"))
+        names = sorted(res)
+        now = {}
+        for n, d in zip(names, KR.demangled(names)):
+            k = (d or n).replace("void ", "").replace("lavish::(anonymous namespace)::", "")
+            now[k.split("(")[0]] = res[n]
+    except Exception as e:  # no llvm tools: cannot vouch for the counts
+        return "signature check unavailable (%s)" % type(e).__name__
+    for k, rec in sig.items():
+        if now.get(k) != rec["signature"]:
+            return "kernel %s changed since the counts (round %s)" % (k, v.get("round"))
+    return None
 
 
 def c4_leg(L, steps, warmup, rdmult, qindex, W=3840, H=2160):

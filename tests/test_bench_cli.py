@@ -69,3 +69,46 @@ def test_failed_rank_fails_the_run():
                          timeout=300)
     assert out.returncode != 0
     assert "ranks failed" in out.stderr
+
+
+def test_hw_queues_out_of_range_is_refused():
+    """--hw-queues outside 0..32 is rejected by argparse before any GPU work
+    (the runtime refused it only after the run had started)."""
+    out = subprocess.run([sys.executable, BENCH, "--hw-queues", "-1", "--dry-run"], env=_env(),
+                         capture_output=True, text=True, timeout=120)
+    assert out.returncode == 2
+    assert "--hw-queues" in out.stderr
+
+
+def _bench_module():
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("bench_cli_mod", BENCH)
+    b = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(b)
+    return b
+
+
+def test_c4_counts_staleness_check():
+    """bench.c4_roofline keeps profiles/c4_valu.json's issued-VALU / traffic
+    fields only while every counted kernel still has the resource signature
+    it was counted with (counters of rewritten kernels
+    had been printed as current)."""
+    import shutil
+    import pytest
+    if not shutil.which("c++filt") or not os.path.exists("/opt/rocm/lib/llvm/bin/llvm-readelf"):
+        pytest.skip("no llvm tools")
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import kernel_resources as KR
+    b = _bench_module()
+    lib = os.path.join(ROOT, "aom-av1-lavish_amd", "liblavish_hip.so")
+    res = KR.kernel_resources(lib)
+    names = sorted(res)
+    name, mangled = next((d, n) for n, d in zip(names, KR.demangled(names)) if "rdo_kernel<4, 4" in d)
+    short = name.replace("void ", "").replace("lavish::(anonymous namespace)::", "").split("(")[0]
+    good = {"round": 6, "kernels": {short: {"signature": res[mangled]}}}
+    assert b.c4_counts_stale(good) is None
+    bad = {"round": 6, "kernels": {short: {"signature": dict(res[mangled], vgpr_count=1)}}}
+    assert "changed" in b.c4_counts_stale(bad)
+    gone = {"round": 6, "kernels": {"no_such_kernel<1>": {"signature": res[mangled]}}}
+    assert b.c4_counts_stale(gone)
+    assert b.c4_counts_stale({"valu_instr_per_step": 1, "kernels": {}})

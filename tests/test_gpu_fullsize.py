@@ -256,6 +256,81 @@ def test_c5_partition_rects_on_gpu(L):
         torch.cuda.synchronize()
 
 
+def _rect_records(whole, s, rect, W, H, L):
+    """The whole-frame records of size s restricted to a rectangle (raster
+    order over the rectangle's blocks, as a rectangle's own step writes them)."""
+    w, h = L.TX_W[s], L.TX_H[s]
+    y0, y1, x0, x1 = rect
+    rec = L.rdo_records(whole.outs[s]).reshape(H // h, W // w)
+    return rec[y0 // h:y1 // h, x0 // w:x1 // w].reshape(-1)
+
+
+def test_c5_tile_form_on_gpu_as_timed(L):
+    """The C5 tile form exactly as bench.py's c5_leg (and --c5-emulate) runs
+    it: grid_partition(2160, 3840, G) for G = 2..8, each rank's tile through
+    c4_rect_processor(..., out=frame, graphs=True) -- one captured HIP graph
+    per tile writing its reconstruction straight into its view of the frame --
+    replayed twice (capture, then replay), and once more through the direct
+    (uncaptured) step.  The assembled frame, every tile's per-SB TX sizes and
+    every candidate size's records and coefficients equal the whole-frame
+    step's, which test_c4_4k_10bit_frame holds to the oracle.  Tiles are
+    multi-row, column-cut rectangles (17 x 15 SBs at G = 8): strided views,
+    the small-rectangle rdo_small_kernel selection, a fan set per graph.
+    Reference dependency: ethread.c:113-160 (SBs of one frame are
+    independent for C4 as defined)."""
+    import torch
+    import lavish_dsp.shard as shard
+    W, H, rdmult, qindex = 3840, 2160, 2000, 128
+    src, pred = _c4_planes(W, H)
+    ts = torch.from_numpy(src.view(np.int16)).cuda()
+    tp = torch.from_numpy(pred.view(np.int16)).cuda()
+    qp = L.build_quant_params(10, qindex, L.QUANT_FP)
+    whole = L.RdoFrame(ts)
+    L.rdo_frame(ts, tp, whole, qp, rdmult, 10)
+    torch.cuda.synchronize()
+    ref = whole.recon.cpu().numpy()
+    ref_sb = whole.sb_tx_size.cpu().numpy().reshape(34, 60)
+    for G in range(2, 9):
+        rects = shard.grid_partition(H, W, G)
+        assert len(rects) == G
+        for graphs in (True, False):
+            frame = torch.full_like(ts, -1)
+            frames = {}
+            proc = shard.c4_rect_processor(ts, tp, qp, rdmult, 10, frames, out=frame,
+                                           graphs=graphs)
+            for it in range(2 if graphs else 1):
+                frame.fill_(-1)
+                for r in rects:
+                    got = proc(*r)
+                    y0, y1, x0, x1 = r
+                    assert got.data_ptr() == frame[y0:y1, x0:x1].data_ptr()
+                torch.cuda.synchronize()
+                np.testing.assert_array_equal(frame.cpu().numpy(), ref,
+                                              err_msg="G %d graphs %s pass %d" % (G, graphs, it))
+            for r in rects:
+                fr = frames[r]
+                y0, y1, x0, x1 = r
+                np.testing.assert_array_equal(
+                    fr.sb_tx_size.cpu().numpy().reshape((y1 - y0 + 63) // 64, (x1 - x0 + 63) // 64),
+                    ref_sb[y0 // 64:(y1 + 63) // 64, x0 // 64:(x1 + 63) // 64],
+                    err_msg="G %d rect %s sb_tx_size" % (G, r))
+                for s in fr.sizes:
+                    w, h = L.TX_W[s], L.TX_H[s]
+                    exp = _rect_records(whole, s, r, W, H, L)
+                    got = L.rdo_records(fr.outs[s])
+                    for f in ("best_type", "eob", "rate", "satd", "dist", "sse", "rdcost"):
+                        np.testing.assert_array_equal(got[f], exp[f],
+                                                      err_msg="G %d %s size %d %s" % (G, r, s, f))
+                    if G in (2, 8):   # coefficients too (the largest and smallest tiles)
+                        nb = (W // w) * (H // h)
+                        q = whole.outs[s]["qcoeff"].view(H // h, W // w, -1)
+                        qe = q[y0 // h:y1 // h, x0 // w:x1 // w].reshape(-1, q.shape[-1])
+                        assert torch.equal(fr.outs[s]["qcoeff"], qe), (G, r, s, nb)
+            del proc, frames
+            gc.collect()
+            torch.cuda.synchronize()
+
+
 def test_rdo_graph_replays_new_inputs(L):
     """lavish_rdo_graph_create captures the C4 step for fixed buffers; a replay
     after the planes' contents change gives the direct step's result on the

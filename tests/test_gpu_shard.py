@@ -58,6 +58,12 @@ def _worker(rank, world, port, q, form):
             return gpu(y0, y1, x0, x1, above=above).cpu()
         if form == "band":
             full = shard.sharded_frame(H, W, rank, world, rect)
+        elif form == "band_streams":
+            # bench.py --c5-form band's arrangement: band and tail on two
+            # streams, each part's gather finished on its own stream
+            streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+            full = shard.sharded_frame(H, W, rank, world, rect, streams=streams)
+            torch.cuda.synchronize()
         else:
             p2p = dist.new_group(list(range(world)))
             full = shard.wavefront_frame(H, W, rank, world, rect, chunks=CHUNKS, p2p_group=p2p,
@@ -69,7 +75,7 @@ def _worker(rank, world, port, q, form):
         q.put((rank, repr(e) + traceback.format_exc()))
 
 
-@pytest.mark.parametrize("form", ["band", "wave"])
+@pytest.mark.parametrize("form", ["band", "band_streams", "wave"])
 def test_c5_two_ranks_hip_step(form):
     import torch
     import torch.multiprocessing as mp
