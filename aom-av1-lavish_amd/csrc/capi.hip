@@ -70,6 +70,7 @@ struct ScanSet {
   std::vector<int16_t> scan[3], iscan[3];
   const int16_t* dscan[3] = {nullptr, nullptr, nullptr};
   const int16_t* discan[3] = {nullptr, nullptr, nullptr};
+  const int16_t* discan_rows = nullptr;
 };
 static ScanSet g_scans[19];
 static std::once_flag g_scan_once;
@@ -134,6 +135,25 @@ const int16_t* dev_iscan(int s, int t) {
   if (!g_scans[s].discan[k]) g_scans[s].discan[k] = upload(g_scans[s].iscan[k]);
   return g_scans[s].discan[k];
 }
+// The three scan kinds' inverse scans of size s in lane-row order,
+// [kind][r][c] = iscan[kind][c * KH + r] (KW, KH = the kept dimensions, <= 32):
+// the rdo kernels' lane owning kept row r reads its KW positions as one
+// contiguous run (staged into LDS per workgroup).
+const int16_t* dev_iscan_rows(int s) {
+  init_scans();
+  std::lock_guard<std::mutex> lk(g_mu);
+  if (!g_scans[s].discan_rows) {
+    const int KW = kW[s] > 32 ? 32 : kW[s], KH = kH[s] > 32 ? 32 : kH[s];
+    std::vector<int16_t> v((size_t)3 * KW * KH);
+    for (int k = 0; k < 3; ++k)
+      for (int r = 0; r < KH; ++r)
+        for (int c = 0; c < KW; ++c)
+          v[((size_t)k * KH + r) * KW + c] = g_scans[s].iscan[k][c * KH + r];
+    g_scans[s].discan_rows = upload(v);
+  }
+  return g_scans[s].discan_rows;
+}
+
 const int16_t* dev_scan(int s, int t) {
   init_scans();
   std::lock_guard<std::mutex> lk(g_mu);

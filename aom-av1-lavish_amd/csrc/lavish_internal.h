@@ -34,6 +34,7 @@ const int16_t* host_scan(int tx_size, int tx_type);
 const int16_t* host_iscan(int tx_size, int tx_type);
 // device copies (uploaded on first use, per device)
 const int16_t* dev_iscan(int tx_size, int tx_type);
+const int16_t* dev_iscan_rows(int tx_size);  // [3 kinds][KH][KW], lane-row order
 const int16_t* dev_scan(int tx_size, int tx_type);
 
 // lavish_txq_plane for the 64-point TX sizes (rdo.hip)

@@ -2430,6 +2430,13 @@ __device__ void lj_pass(const Ctx& c, const LjSrc& s, int l, __amdgpu_buffer_rsr
   }
 }
 
+__device__ __forceinline__ void lj_jobs(
+    const uint8_t* __restrict__ src, int ss, const uint8_t* __restrict__ ref, int rs,
+    const LavishRefTiles& tiles, const Job* __restrict__ jobs, int njobs, int step_param,
+    const LavishMvCostParams& cost, const int32_t* dec, int skip,
+    LavishDiamondResult* __restrict__ out, int32_t* __restrict__ cost_lists, int j0,
+    uint32_t* res);
+
 // one group of WPG x 8 jobs: virtual workgroup vwg of nvwg (a multiple of 8)
 template <int WPG>
 __device__ __forceinline__ void lj_group(
@@ -2442,12 +2449,24 @@ __device__ __forceinline__ void lj_group(
   const int wg = (vwg & 7) * (nvwg >> 3) + (vwg >> 3);
   const int lane = threadIdx.x & 63;
   const int wave = WPG == 1 ? 0 : threadIdx.x >> 6;
-  const int jg = lane >> 3, l = lane & 7;
   const int j0 = (wg * WPG + wave) * kLjJobs;
   if (j0 >= njobs) return;
+  lj_jobs(src, ss, ref, rs, tiles, jobs, njobs, step_param, cost, dec, skip, out, cost_lists, j0,
+          res_s[wave][lane >> 3]);
+}
+
+// the eight jobs j0 .. j0 + 7 of one wave (res: this lane group's LDS slot
+// for the runs' results)
+__device__ __forceinline__ void lj_jobs(
+    const uint8_t* __restrict__ src, int ss, const uint8_t* __restrict__ ref, int rs,
+    const LavishRefTiles& tiles, const Job* __restrict__ jobs, int njobs, int step_param,
+    const LavishMvCostParams& cost, const int32_t* dec, int skip,
+    LavishDiamondResult* __restrict__ out, int32_t* __restrict__ cost_lists, int j0,
+    uint32_t* res) {
+  const int lane = threadIdx.x & 63;
+  const int jg = lane >> 3, l = lane & 7;
   const int j = min(j0 + jg, njobs - 1);  // a surplus group repeats the last job, never stores
   const bool mine_job = j0 + jg < njobs;
-  uint32_t* res = res_s[wave][jg];
   const Job jb = jobs[j];
   Ctx c;
   c.src = src + jb.src_off;
@@ -2551,6 +2570,49 @@ __global__ __launch_bounds__(64 * WPG, LAVISH_LJ_WAVES) void diamond_lj_kernel(
                   cost_lists, v, nvwg);
 }
 
+// The capped grid with work pulled from queues: beside C2 the search runs in
+// `cap` workgroups (lavish_set_search_workgroup_cap) that each process many
+// 8-job wave units.  Dealt statically (grid-stride over virtual workgroups),
+// ceil(groups / cap) rounds set the leg's length while most workgroups sit
+// idle in the last round (1760 groups over 512 workgroups: 223 do 4, 289 do
+// 3) and every wave of a workgroup waits for its slowest unit.  Here every
+// wave pulls its next unit from a queue with one returning atomic: the
+// units of XCD label x = blockIdx % 8 (blocks b and b + 8 share an XCD, so
+// neighbouring blocks' reference tiles stay in one L2, as with the static
+// mapping) are the contiguous range [units x / 8, units (x + 1) / 8); a
+// label's workgroups drain it together.  queue: 8 counters 16 ints apart,
+// zero at launch (mvcost_dec_kernel or lj_queue_zero clears them on the
+// same stream).  The order of the units changes no result.
+constexpr int kLjQueueStride = 16;  // ints between two labels' counters (64 B)
+
+template <int WPG>
+__global__ __launch_bounds__(64 * WPG, LAVISH_LJ_WAVES) void diamond_lj_dyn_kernel(
+    const uint8_t* __restrict__ src, int ss, const uint8_t* __restrict__ ref, int rs,
+    LavishRefTiles tiles, const Job* __restrict__ jobs, int njobs, int step_param,
+    LavishMvCostParams cost, const int32_t* dec, int skip, LavishDiamondResult* __restrict__ out,
+    int32_t* __restrict__ cost_lists, int* __restrict__ queue) {
+  __shared__ uint32_t res_s[WPG][kLjJobs][kMaxSteps];
+  const int units = (njobs + kLjJobs - 1) / kLjJobs;
+  const int x = blockIdx.x & 7;
+  const int u0 = units * x / 8, u1 = units * (x + 1) / 8;
+  const int lane = threadIdx.x & 63;
+  const int wave = WPG == 1 ? 0 : threadIdx.x >> 6;
+  uint32_t* res = res_s[wave][lane >> 3];
+  int* q = queue + x * kLjQueueStride;
+  for (;;) {
+    int t = 0;
+    if (lane == 0) t = __hip_atomic_fetch_add(q, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    t = __builtin_amdgcn_readfirstlane(t);
+    if (u0 + t >= u1) break;  // every wave of the label ends here once the range is drained
+    lj_jobs(src, ss, ref, rs, tiles, jobs, njobs, step_param, cost, dec, skip, out, cost_lists,
+            (u0 + t) * kLjJobs, res);
+  }
+}
+
+__global__ void lj_queue_zero(int* __restrict__ queue) {
+  if (threadIdx.x < 8 * kLjQueueStride) queue[threadIdx.x] = 0;
+}
+
 // ---------------------------------------------------------------------------
 // C2 + C3 in one launch (lavish_txq_frame_search): the <= 16-point class of
 // lavish_txq_frame (txq_multi_body<0>) and the 16x16 DIAMOND search's job
@@ -2597,10 +2659,13 @@ __global__ __launch_bounds__(256, 4) void txq_search_kernel(TxqDispatch d, TxqAr
 }
 
 // the decimated entropy cost tables of mvsad_rate_dec
+// (+ the search queue's counters zeroed, when given)
 __global__ __launch_bounds__(256) void mvcost_dec_kernel(const int32_t* __restrict__ mvcost0,
                                                          const int32_t* __restrict__ mvcost1,
-                                                         int32_t* __restrict__ dec) {
+                                                         int32_t* __restrict__ dec,
+                                                         int* __restrict__ queue) {
   const int i = blockIdx.x * 256 + threadIdx.x;
+  if (queue != nullptr && i < 8 * kLjQueueStride) queue[i] = 0;
   if (i >= 2 * kMvDecN) return;
   const int k = (i % kMvDecN) - kMvDecHalf;
   dec[i] = (i < kMvDecN ? mvcost0 : mvcost1)[8 * k];
@@ -2612,6 +2677,9 @@ thread_local StreamScratch t_mvdec;
 // 0: one per 32 jobs): lavish_set_search_workgroup_cap
 static std::atomic<int> g_lj_cap{0};
 static int lj_grid_cap() { return g_lj_cap.load(std::memory_order_relaxed); }
+// a capped grid: 1 = units pulled from queues (default), 0 = the static
+// grid-stride (lavish_set_search_schedule, A/B)
+static std::atomic<int> g_lj_queue{1};
 
 template <int W, int H, bool TL>
 void launch_tl(const uint8_t* src, int ss, const uint8_t* ref, int rs, const LavishRefTiles& t,
@@ -2665,16 +2733,33 @@ void launch(const uint8_t* src, int ss, const uint8_t* ref, int rs, const Lavish
           const int nwg = (((waves + wpg - 1) / wpg) + 7) & ~7;
           const int cap = lj_grid_cap();
           const int grid = cap > 0 && cap < nwg ? cap : nwg;
+          // a capped grid pulls its units from the queues (diamond_lj_dyn_kernel)
+          const bool dyn = grid < nwg && g_lj_queue.load(std::memory_order_relaxed);
+          constexpr size_t kDecBytes = 2 * kMvDecN * sizeof(int32_t);
+          const size_t qbytes = dyn ? 8 * kLjQueueStride * sizeof(int) : 0;
           int32_t* dec = nullptr;
-          if (cost.mv_cost_type == 0) {
-            dec = (int32_t*)t_mvdec.acquire(2 * kMvDecN * sizeof(int32_t), s);
-            hipLaunchKernelGGL(mvcost_dec_kernel, dim3((2 * kMvDecN + 255) / 256), dim3(256), 0,
-                               s, cost.mvcost[0], cost.mvcost[1], dec);
+          int* queue = nullptr;
+          char* scr = nullptr;
+          if (cost.mv_cost_type == 0 || dyn) {
+            scr = (char*)t_mvdec.acquire(kDecBytes + qbytes, s);
+            if (dyn) queue = (int*)(scr + kDecBytes);
           }
-          hipLaunchKernelGGL(diamond_lj_kernel<wpg>, dim3(grid), dim3(64 * wpg), 0, s, src, ss, ref,
-                               rs, *t, (const Job*)jobs, njobs, step_param, cost,
+          if (cost.mv_cost_type == 0) {
+            dec = (int32_t*)scr;
+            hipLaunchKernelGGL(mvcost_dec_kernel, dim3((2 * kMvDecN + 255) / 256), dim3(256), 0,
+                               s, cost.mvcost[0], cost.mvcost[1], dec, queue);
+          } else if (dyn) {
+            hipLaunchKernelGGL(lj_queue_zero, dim3(1), dim3(8 * kLjQueueStride), 0, s, queue);
+          }
+          if (dyn)
+            hipLaunchKernelGGL(diamond_lj_dyn_kernel<wpg>, dim3(grid), dim3(64 * wpg), 0, s, src,
+                               ss, ref, rs, *t, (const Job*)jobs, njobs, step_param, cost,
+                               (const int32_t*)dec, skip, out, cost_lists, queue);
+          else
+            hipLaunchKernelGGL(diamond_lj_kernel<wpg>, dim3(grid), dim3(64 * wpg), 0, s, src, ss,
+                               ref, rs, *t, (const Job*)jobs, njobs, step_param, cost,
                                (const int32_t*)dec, skip, out, cost_lists, nwg);
-          if (dec) t_mvdec.release(s);
+          if (scr) t_mvdec.release(s);
           return;
         }
       }
@@ -2812,6 +2897,12 @@ extern "C" int lavish_dbg_tpl_prof(unsigned long long* out16, int reset) {
   return 0;
 }
 #endif
+
+extern "C" int lavish_set_search_schedule(int queued) {
+  if (queued != 0 && queued != 1) return -1;
+  lavish::g_lj_queue.store(queued, std::memory_order_relaxed);
+  return 0;
+}
 
 extern "C" int lavish_set_search_workgroup_cap(int workgroups) {
   if (workgroups < 0) return -1;
@@ -2994,7 +3085,7 @@ extern "C" int lavish_txq_frame_search(
   if (c.units > 0 && cost->mv_cost_type == 0) {
     c.dec = (const int32_t*)t_mvdec.acquire(2 * kMvDecN * sizeof(int32_t), s);
     hipLaunchKernelGGL(mvcost_dec_kernel, dim3((2 * kMvDecN + 255) / 256), dim3(256), 0, s,
-                       cost->mvcost[0], cost->mvcost[1], (int32_t*)c.dec);
+                       cost->mvcost[0], cost->mvcost[1], (int32_t*)c.dec, (int*)nullptr);
   }
   // the search units must all lie inside the grid: units * every may not
   // pass the grid's units (clamp the spacing)

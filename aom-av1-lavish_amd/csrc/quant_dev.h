@@ -74,10 +74,8 @@ __device__ __forceinline__ int32_t quant_one(int32_t c, bool ac, const QP& qp) {
 // F24: |q| < 2^23 -- the FAST range bounds |coeff| < 2^21, and quant_b's
 // worst case with the largest per-call quant_shift (2^16) reaches about
 // 2^22.6, still inside 24 bits -- so the product's low 32 bits (the
-// reference's int multiply, wrap included) come from one 24-bit multiply.
-// The multiply is done as uint32 (defined wrap in C++); the operands are
-// sign-extended 24-bit values, which lets the backend select v_mul_u32_u24 /
-// v_mul_i32_i24.
+// reference's int multiply, wrap included) come from one 24-bit multiply,
+// mul_i24 (txfm_dev.h: v_mul_i32_i24, no C++ overflow).
 template <int LS, bool F24 = false>
 __device__ __forceinline__ int32_t dequant_one(int32_t q, bool ac, const QP& qp) {
   const int32_t sgn = q >> 31;
@@ -85,8 +83,7 @@ __device__ __forceinline__ int32_t dequant_one(int32_t q, bool ac, const QP& qp)
   const int32_t d = ac ? qp.dequant[1] : qp.dequant[0];
   // (abs_q * dequant) >> log_scale as an int multiply (wraps like the reference)
   const int32_t adq =
-      F24 ? (int32_t)((uint32_t)sext24(aq) * (uint32_t)sext24(d)) >> LS
-          : (int32_t)((uint32_t)aq * (uint32_t)d) >> LS;
+      F24 ? mul_i24(aq, d) >> LS : (int32_t)((uint32_t)aq * (uint32_t)d) >> LS;
   return (adq ^ sgn) - sgn;
 }
 

@@ -15,8 +15,10 @@ int fill_types(RdoArgs& a, int tx_size, uint32_t type_mask) {
     if (!((type_mask >> t) & 1)) continue;
     if (!tx_type_valid(tx_size, t)) return -5;
     a.iscan_type[a.ntypes] = dev_iscan(tx_size, t);
+    a.scan_kind[a.ntypes] = scan_kind(t);
     a.types[a.ntypes++] = t;
   }
+  a.scan_rows = dev_iscan_rows(tx_size);
   int n = 0;
   for (int vk = 0; vk < 4; ++vk) {
     bool first = true;

@@ -53,6 +53,9 @@ struct RdoArgs {
   int rdmult;      // mode 1
   QP qp;
   const int16_t* iscan_type[16];  // per slot: inverse scan of the type (n)
+  int scan_kind[16];              // per slot: its scan kind (0 default, 1 mcol, 2 mrow)
+  const int16_t* scan_rows;       // the 3 kinds' inverse scans in lane-row order
+                                  // ([kind][KH][KW], dev_iscan_rows)
   // evaluation order: slots grouped by vertical 1-D kind (one column pass per
   // group); newcol[i] = 1 where order[i] starts a group
   int order[16];
@@ -168,8 +171,21 @@ struct RdoLds {
   static constexpr int win = lds_align(dead + T::P, 4);
   static constexpr int brd = lds_align(win + T::P, 8);
   static constexpr int brk = lds_align(brd + 8 * NVM * T::P, 4);
-  static constexpr int bytes = lds_align(brk + NVM * T::P, 16);
+  static constexpr int scan = lds_align(brk + NVM * T::P, 16);  // int16 [3][KH][KW]
+  static constexpr int bytes = lds_align(scan + 2 * 3 * T::NC, 16);
 };
+
+// dist_block_tx_domain's finish of a block sum of squares
+// (tx_search.c:1077-1116): av1_highbd_block_error's rounding by 2 (bd - 8)
+// bits, then the TX-domain shift (MAX_TX_SCALE - tx_scale) * 2
+template <int LS>
+__device__ __forceinline__ int64_t tx_dist(int64_t v, int bd) {
+  const int sh = 2 * (bd - 8);
+  if (sh > 0) v = (v + ((int64_t)1 << (sh - 1))) >> sh;
+  constexpr int dshift = (1 - LS) * 2;
+  if constexpr (dshift >= 0) return v >> dshift;
+  else return v << -dshift;
+}
 
 template <int W, int H, int MODE, bool FAST, int QK, bool HBD, int BDI, int NVM>
 __device__ __forceinline__ void rdo_types(const RdoArgs& a, const int32_t (&res)[RTile<W, H>::CPT][H],
@@ -200,6 +216,19 @@ __device__ __forceinline__ void rdo_types(const RdoArgs& a, const int32_t (&res)
   // (get_tx_mask's rule, tx_search.c:1885-1888).
   uint8_t(*const s_rank)[16] = reinterpret_cast<uint8_t(*)[16]>(lds + LY::rank);
   uint16_t* const s_ok = reinterpret_cast<uint16_t*>(lds + LY::ok);
+  // the three scan kinds' inverse scans in lane-row order, staged once per
+  // tile: a lane's KW positions of kept row r are one contiguous LDS read
+  // per type (global loads per coefficient had been VMEM requests and
+  // waits in the middle of the quantizer)
+  int16_t* const s_scan = reinterpret_cast<int16_t*>(lds + LY::scan);
+  {
+    constexpr int NV4 = 3 * NC / 8;  // 16-byte chunks (NC >= 16)
+    const int tid = NVM > 1 ? (int)threadIdx.x : lane;
+    const int nth = NVM > 1 ? 64 * NVM : 64;
+    for (int i = tid; i < NV4; i += nth)
+      reinterpret_cast<v4i*>(s_scan)[i] = reinterpret_cast<const v4i*>(a.scan_rows)[i];
+    if constexpr (!DEC) wave_sync();  // (DEC: the barrier below covers it)
+  }
   if constexpr (DEC) {
     if ((NVM > 1 ? (int)threadIdx.x : lane) < T::P) {  // (wave 0 for the workgroup)
       uint32_t ok = 0xFFFFu;
@@ -250,7 +279,7 @@ __device__ __forceinline__ void rdo_types(const RdoArgs& a, const int32_t (&res)
     const int kr = ht == 3 ? 2 : (ht == 0 ? 0 : 1);
     const bool ud = vt == 2;
     const bool lr = ht == 2;  // FLIPADST rows: the column results read right to left
-    const int16_t* iscan = a.iscan_type[ti];
+    const int16_t* const srow = s_scan + __builtin_amdgcn_readfirstlane(a.scan_kind[ti]) * NC;
 
     // ---- columns (av1_fwd_txfm2d.c:88-106), once per vertical kind; only
     // rows < KH are kept ----
@@ -297,6 +326,9 @@ __device__ __forceinline__ void rdo_types(const RdoArgs& a, const int32_t (&res)
       int last = 0, satd = 0;
       int64_t err = 0, sse = 0;
       const size_t obase = ((size_t)ti * a.nblocks + blk0 + bb) * NC;
+      // the type's inverse scan of this lane's row (LDS, lane-row order:
+      // the KW positions contiguous)
+      const int16_t* const isc = srow + r * KW;
 #pragma unroll
       for (int c = 0; c < KW; ++c) {
         int32_t v = round_shift_1<-C::s2>(out[c]);
@@ -314,15 +346,26 @@ __device__ __forceinline__ void rdo_types(const RdoArgs& a, const int32_t (&res)
         }
         if constexpr (DEC) {
           const int32_t dq = dequant_one<LS, FAST>(q[c], ac, a.qp);
-          const int64_t d = (int64_t)v - dq;
-          err += d * d;
-          sse += (int64_t)v * v;
+          if constexpr (FAST) {
+            // the certified range: |v| < 2^19 (tools/range_analysis.py
+            // max|coeff|), |dq| <= |v| + dequant (int16), so v - dq and v
+            // fit 24 signed bits and each square is one v_mul_i32_i24 +
+            // v_mul_hi_i32_i24 pair (the int64 forms were three quarter-rate
+            // 64-bit multiplies per coefficient)
+            const int32_t d = v - dq;
+            err += (int64_t)sext24(d) * (int64_t)sext24(d);
+            sse += (int64_t)sext24(v) * (int64_t)sext24(v);
+          } else {
+            const int64_t d = (int64_t)v - dq;
+            err += d * d;
+            sse += (int64_t)v * v;
+          }
           satd += abs(v);
         }
         if constexpr (MODE == 0) {
           if (live) t2[bb * NC + rc] = q[c];
         }
-        last = q[c] != 0 ? max(last, iscan[rc] + 1) : last;
+        last = q[c] != 0 ? max(last, isc[c] + 1) : last;
       }
       last = lane_max<KH>(last);
       if constexpr (MODE == 0) {
@@ -386,7 +429,7 @@ __device__ __forceinline__ void rdo_types(const RdoArgs& a, const int32_t (&res)
 #pragma unroll
           for (int c = 0; c < KW; ++c) {
             const int rc = c * KH + r;
-            const int i = iscan[rc];
+            const int i = isc[c];
             if (i < last) {
               const int nzmag = (int)((nzs[c >> 3] >> (4 * (c & 7))) & 15u);
               // get_br_ctx's raw sum, needed only above level 2
@@ -402,33 +445,22 @@ __device__ __forceinline__ void rdo_types(const RdoArgs& a, const int32_t (&res)
           rate = cc::txb_rate(s_cc, cls, tc.txb_skip_ctx, last, a.tx_type_cost[t], rate);
         } else {
           // rate_estimator: positions of the DCT_DCT scan below eob
+          const int16_t* const dct = s_scan + r * KW;
 #pragma unroll
           for (int c = 0; c < KW; ++c) {
-            const int rc = c * KH + r;
             const uint32_t al = (uint32_t)abs(q[c]);
-            if (a.iscan_dct[rc] < last) rate += get_msb(al + 1) + 1 + (al > 0);
+            if (dct[c] < last) rate += get_msb(al + 1) + 1 + (al > 0);
           }
           rate = lane_sum<KH>(rate);
           rate = (rate + 1) << 9;  // AV1_PROB_COST_SHIFT
         }
-        satd = lane_sum<KH>(satd);
+        // only the block error enters the cost: the SATD and the sse are
+        // record fields of the winner, so each lane keeps its unreduced
+        // partial sums of them and they are reduced once, after the type
+        // loop (every lane of a block takes the same winner)
         err = lane_sum64<KH>(err);
-        sse = lane_sum64<KH>(sse);
-        // av1_highbd_block_error rounding, then the TX-domain shift
-        const int sh = 2 * (a.bd - 8);
-        if (sh > 0) {
-          const int64_t rnd = (int64_t)1 << (sh - 1);
-          err = (err + rnd) >> sh;
-          sse = (sse + rnd) >> sh;
-        }
-        constexpr int dshift = (1 - LS) * 2;  // (MAX_TX_SCALE - tx_scale) * 2
-        if constexpr (dshift >= 0) {
-          st_dist[k] = err >> dshift;
-          st_sse[k] = sse >> dshift;
-        } else {
-          st_dist[k] = err << -dshift;
-          st_sse[k] = sse << -dshift;
-        }
+        st_dist[k] = tx_dist<LS>(err, a.bd);
+        st_sse[k] = sse;
         st_last[k] = last;
         st_rate[k] = rate;
         st_satd[k] = satd;
@@ -554,6 +586,15 @@ __device__ __forceinline__ void rdo_types(const RdoArgs& a, const int32_t (&res)
     }
   }
 
+  if constexpr (DEC) {
+    // the winners' SATD and (TX-domain modes) sse, reduced once (see the
+    // type loop)
+#pragma unroll
+    for (int k = 0; k < T::RPT; ++k) {
+      best_satd[k] = lane_sum<KH>(best_satd[k]);
+      if constexpr (MODE != 2) best_sse[k] = tx_dist<LS>(lane_sum64<KH>(best_sse[k]), a.bd);
+    }
+  }
   if constexpr (DEC && NVM == 1) {
     // decision records (one lane per block) and the winner's coefficients.
     // A block none of whose allowed types is in the evaluated set (possible

@@ -15,13 +15,18 @@
 // (the CONV_BUF stored) / average (plain or distance-weighted with the
 // buffer, then offset, round, clip).
 //
-// One 256-thread workgroup per block: the horizontal pass's outputs go to
-// LDS (rows coalesced across threads; the scaled source reads of
-// neighbouring threads fall in the same rows), a barrier, then the vertical
-// pass (threads take output pixels, rows coalesced).  Steps up to 2048
-// (the 2:1 downscale limit of av1_is_valid_scale) bound the intermediate at
-// 2 h + taps rows.  Kernel rows of the caller's filters travel as kernel
-// arguments.
+// Blocks per 256-thread workgroup: NB = 256 / (w h) for blocks below 256
+// pixels (16 for 4x4, capped), one otherwise; each block's slice of the
+// workgroup (256 / NB threads) runs the horizontal pass into the block's LDS
+// intermediate, a barrier, then the vertical pass.  The kernel is
+// instantiated per tap count pair (TX, TY) in {(8, 8), (12, 12), (4, 4),
+// (4, 8), (8, 4), (2, 2)} (0, 0: any count at run time): the tap loops
+// unroll, a horizontal output's TX source pixels come in one byte-addressed
+// vector load (8 u8 = one dwordx2, 8 u16 = one dwordx4; the runtime-bound
+// loop issued one dependent load per tap), and the 16 kernel rows of the
+// caller's filters sit in LDS (32-byte rows: one ds_read_b128 per 8 taps).
+// Steps up to 2048 (the 2:1 downscale limit of av1_is_valid_scale) bound the
+// intermediate at 2 h + taps rows.
 #include "lavish_internal.h"
 
 namespace lavish {
@@ -40,47 +45,121 @@ struct ScaleArgs {
   const LavishScaleJob* jobs;
   int src_stride, dst_stride, conv_stride, w, h, lw, njobs, bd;
   int tx, ty;
+  int nb, im_cap;  // blocks per workgroup, int16 slots of one block's intermediate
   int16_t fx[16][kMaxTaps], fy[16][kMaxTaps];
   int r0, r1, offset_bits, round_offset, round_bits, is_compound, do_average, dist_wtd, fwd, bck;
 };
 
-template <typename Pix>
+constexpr int kFRow = 16;  // LDS kernel row stride (int16): 32 bytes
+
+// the T source pixels p[0 .. T - 1] of one tap window, one vector load where
+// T is fixed (byte-addressed: the queues run in unaligned-access mode)
+template <typename Pix, int T>
+__device__ __forceinline__ void load_taps(const Pix* p, int (&v)[T]) {
+  if constexpr (sizeof(Pix) == 1 && T == 8) {
+    const u32x2u d = *(const u32x2u*)p;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] = (d[k >> 2] >> (8 * (k & 3))) & 0xFF;
+  } else if constexpr (sizeof(Pix) == 1 && T == 12) {
+    const u32x2u d = *(const u32x2u*)p;
+    const uint32_t e = *(const u32u*)(p + 8);
+#pragma unroll
+    for (int k = 0; k < 12; ++k) v[k] = ((k < 8 ? d[k >> 2] : e) >> (8 * (k & 3))) & 0xFF;
+  } else if constexpr (sizeof(Pix) == 1 && T == 4) {
+    const uint32_t d = *(const u32u*)p;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) v[k] = (d >> (8 * k)) & 0xFF;
+  } else if constexpr (sizeof(Pix) == 2 && T == 8) {
+    const u32x4u d = *(const u32x4u*)p;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] = (d[k >> 1] >> (16 * (k & 1))) & 0xFFFF;
+  } else if constexpr (sizeof(Pix) == 2 && T == 12) {
+    const u32x4u d = *(const u32x4u*)p;
+    const u32x2u e = *(const u32x2u*)(p + 8);
+#pragma unroll
+    for (int k = 0; k < 12; ++k)
+      v[k] = ((k < 8 ? d[k >> 1] : e[(k - 8) >> 1]) >> (16 * (k & 1))) & 0xFFFF;
+  } else if constexpr (sizeof(Pix) == 2 && T == 4) {
+    const u32x2u d = *(const u32x2u*)p;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) v[k] = (d[k >> 1] >> (16 * (k & 1))) & 0xFFFF;
+  } else {
+#pragma unroll
+    for (int k = 0; k < T; ++k) v[k] = p[k];
+  }
+}
+
+template <typename Pix, int T>
+__device__ __forceinline__ int32_t taps_dot(const Pix* p, const int16_t* f, int32_t s) {
+  int v[T];
+  load_taps<Pix, T>(p, v);
+#pragma unroll
+  for (int k = 0; k < T; ++k) s += f[k] * v[k];
+  return s;
+}
+
+template <typename Pix, int TX, int TY>
 __global__ __launch_bounds__(256) void scale_kernel(ScaleArgs a) {
-  extern __shared__ int16_t im[];
-  const LavishScaleJob jb = a.jobs[blockIdx.x];
+  extern __shared__ __attribute__((aligned(16))) int16_t lds[];
+  int16_t* fxs = lds;                 // [16][kFRow]
+  int16_t* fys = lds + 16 * kFRow;    // [16][kFRow]
   const int t = threadIdx.x;
-  const int w = a.w, h = a.h, lw = a.lw, tx = a.tx, ty = a.ty;
+  for (int e = t; e < 2 * 16 * kFRow; e += 256) {
+    const int tab = e / (16 * kFRow), r = (e / kFRow) & 15, k = e % kFRow;
+    lds[e] = k < kMaxTaps ? (tab ? a.fy[r][k] : a.fx[r][k]) : 0;
+  }
+  const int nb = a.nb, tpb = 256 / nb;
+  const int slot = t / tpb, tb = t - slot * tpb;
+  const int job = blockIdx.x * nb + slot;
+  int16_t* im = lds + 2 * 16 * kFRow + slot * a.im_cap;
+  const int w = a.w, h = a.h, lw = a.lw;
+  const int tx = TX ? TX : a.tx, ty = TY ? TY : a.ty;
+  LavishScaleJob jb{};
+  if (job < a.njobs) jb = a.jobs[job];
   const int xs = jb.x_step_qn, ys = jb.y_step_qn, spx = jb.subpel_x_qn, spy = jb.subpel_y_qn;
   // (outside the supported steps the block is left alone: its intermediate
-  // would not fit the launch's LDS)
-  if (xs < 1 || xs > kMaxStep || ys < 1 || ys > kMaxStep || spx < 0 || spy < 0 ||
-      spx > (1 << kScaleBits) - 1 || spy > (1 << kScaleBits) - 1)
-    return;
+  // would not fit the launch's LDS; a slot past the batch does nothing)
+  const bool valid = job < a.njobs && xs >= 1 && xs <= kMaxStep && ys >= 1 && ys <= kMaxStep &&
+                     spx >= 0 && spy >= 0 && spx <= (1 << kScaleBits) - 1 &&
+                     spy <= (1 << kScaleBits) - 1;
+  __syncthreads();  // the kernel rows
   const Pix* src = (const Pix*)a.src + jb.src_off;
   const int im_h = (((h - 1) * ys + spy) >> kScaleBits) + ty;
   const int fo_y = ty / 2 - 1, fo_x = tx / 2 - 1;
   // horizontal filter (convolve.c:509-527): im_h rows from fo_y above the block
-  for (int e = t; e < im_h * w; e += 256) {
-    const int y = e >> lw, x = e & (w - 1);
-    const int x_qn = spx + x * xs;
-    const Pix* p = src + (int64_t)(y - fo_y) * a.src_stride + (x_qn >> kScaleBits) - fo_x;
-    const int16_t* f = a.fx[(x_qn & ((1 << kScaleBits) - 1)) >> kScaleExtra];
-    int32_t s = 1 << (a.bd + kFBits - 1);
-    for (int k = 0; k < tx; ++k) s += f[k] * (int)p[k];
-    im[e] = (int16_t)((s + ((1 << a.r0) >> 1)) >> a.r0);
+  if (valid) {
+    for (int e = tb; e < im_h * w; e += tpb) {
+      const int y = e >> lw, x = e & (w - 1);
+      const int x_qn = spx + x * xs;
+      const Pix* p = src + (int64_t)(y - fo_y) * a.src_stride + (x_qn >> kScaleBits) - fo_x;
+      const int16_t* f = fxs + ((x_qn & ((1 << kScaleBits) - 1)) >> kScaleExtra) * kFRow;
+      int32_t s = 1 << (a.bd + kFBits - 1);
+      if constexpr (TX != 0) {
+        s = taps_dot<Pix, TX>(p, f, s);
+      } else {
+        for (int k = 0; k < tx; ++k) s += f[k] * (int)p[k];
+      }
+      im[e] = (int16_t)((s + ((1 << a.r0) >> 1)) >> a.r0);
+    }
   }
   __syncthreads();
+  if (!valid) return;
   // vertical filter and the finish (:530-573)
   Pix* dst = (Pix*)a.dst + jb.dst_off;
   uint16_t* conv = a.conv + jb.conv_off;
   const int pmax = (1 << a.bd) - 1;
-  for (int e = t; e < h * w; e += 256) {
+  for (int e = tb; e < h * w; e += tpb) {
     const int y = e >> lw, x = e & (w - 1);
     const int y_qn = spy + y * ys;
-    const int16_t* f = a.fy[(y_qn & ((1 << kScaleBits) - 1)) >> kScaleExtra];
-    const int16_t* col = im + (((y_qn >> kScaleBits)) << lw) + x;
+    const int16_t* f = fys + ((y_qn & ((1 << kScaleBits) - 1)) >> kScaleExtra) * kFRow;
+    const int16_t* col = im + ((y_qn >> kScaleBits) << lw) + x;
     int32_t s = 1 << a.offset_bits;
-    for (int k = 0; k < ty; ++k) s += f[k] * (int)col[k << lw];
+    if constexpr (TY != 0) {
+#pragma unroll
+      for (int k = 0; k < TY; ++k) s += f[k] * (int)col[k << lw];
+    } else {
+      for (int k = 0; k < ty; ++k) s += f[k] * (int)col[k << lw];
+    }
     const int32_t res = (uint16_t)((s + ((1 << a.r1) >> 1)) >> a.r1);  // CONV_BUF_TYPE
     int32_t tmp;
     if (a.is_compound) {
@@ -98,6 +177,23 @@ __global__ __launch_bounds__(256) void scale_kernel(ScaleArgs a) {
     const int v = (tmp + ((1 << a.round_bits) >> 1)) >> a.round_bits;
     dst[(int64_t)y * a.dst_stride + x] = (Pix)min(max(v, 0), pmax);
   }
+}
+
+template <typename Pix>
+void scale_launch(const ScaleArgs& a, int grid, size_t lds, hipStream_t s) {
+#define LAVISH_SCALE_K(X, Y)                                                                   \
+  if (a.tx == X && a.ty == Y) {                                                                \
+    hipLaunchKernelGGL((scale_kernel<Pix, X, Y>), dim3(grid), dim3(256), lds, s, a);           \
+    return;                                                                                    \
+  }
+  LAVISH_SCALE_K(8, 8)
+  LAVISH_SCALE_K(12, 12)
+  LAVISH_SCALE_K(4, 4)
+  LAVISH_SCALE_K(4, 8)
+  LAVISH_SCALE_K(8, 4)
+  LAVISH_SCALE_K(2, 2)
+#undef LAVISH_SCALE_K
+  hipLaunchKernelGGL((scale_kernel<Pix, 0, 0>), dim3(grid), dim3(256), lds, s, a);
 }
 
 }  // namespace
@@ -149,13 +245,17 @@ int scale_batch(const void* src, int src_stride, void* dst, int dst_stride, uint
   a.dist_wtd = cp->use_dist_wtd_comp_avg;
   a.fwd = cp->fwd_offset;
   a.bck = cp->bck_offset;
-  // the largest intermediate a supported step can make
+  // the largest intermediate a supported step can make, per block slot
+  // (rounded to 8 int16: each slot 16-byte aligned)
   const int im_rows = (((h - 1) * kMaxStep + (1 << kScaleBits) - 1) >> kScaleBits) + a.ty;
-  const size_t lds = (size_t)im_rows * w * sizeof(int16_t);
+  a.im_cap = (im_rows * w + 7) & ~7;
+  a.nb = w * h >= 256 ? 1 : min(16, 256 / (w * h));
+  const int grid = (njobs + a.nb - 1) / a.nb;
+  const size_t lds = (size_t)(2 * 16 * kFRow + a.nb * a.im_cap) * sizeof(int16_t);
   if (highbd)
-    hipLaunchKernelGGL(scale_kernel<uint16_t>, dim3(njobs), dim3(256), lds, s, a);
+    scale_launch<uint16_t>(a, grid, lds, s);
   else
-    hipLaunchKernelGGL(scale_kernel<uint8_t>, dim3(njobs), dim3(256), lds, s, a);
+    scale_launch<uint8_t>(a, grid, lds, s);
   LAVISH_CHECK(hipGetLastError());
   return 0;
 }

@@ -59,6 +59,17 @@ __device__ __forceinline__ constexpr int32_t cospi(int j) {
 // same bits with 4 VALU ops instead of ~10.
 __device__ __forceinline__ int32_t sext24(int32_t x) { return (x << 8) >> 8; }
 
+// The low 32 bits of the product of the operands' sign-extended low 24 bits
+// (v_mul_i32_i24, full rate).  Written as the instruction: where the
+// optimizer can prove an operand already fits 24 bits it drops the sign
+// extension of __mul24 / sext24 forms, and the selector then falls back to
+// the quarter-rate v_mul_lo_u32 (seen in rdo_kernel's dequantisation).
+__device__ __forceinline__ int32_t mul_i24(int32_t a, int32_t b) {
+  int32_t r;
+  asm("v_mul_i32_i24 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+
 template <int BIT, bool FAST = false>
 __device__ __forceinline__ int32_t hbtf(int32_t w0, int32_t in0, int32_t w1,
                                         int32_t in1) {
@@ -291,13 +302,18 @@ __device__ __forceinline__ void fadst(const int32_t* in, int32_t* out) {
   }
 }
 
-template <int N>
+// FAST: the inputs are half_btf operands of the certified range (< 2^23,
+// tools/range_analysis.py), so the x 5793 products are one 24-bit multiply
+// pair (v_mul_i32_i24 + v_mul_hi_i32_i24) instead of a quarter-rate 64-bit
+// multiply
+template <int N, bool FAST = false>
 __device__ __forceinline__ void fidentity(const int32_t* in, int32_t* out) {
 #pragma unroll
   for (int i = 0; i < N; ++i) {
-    if constexpr (N == 4) out[i] = rshift64((int64_t)in[i] * 5793, 12);
+    const int64_t x = FAST ? (int64_t)sext24(in[i]) : (int64_t)in[i];
+    if constexpr (N == 4) out[i] = rshift64(x * 5793, 12);
     else if constexpr (N == 8) out[i] = (int32_t)((uint32_t)in[i] * 2u);
-    else if constexpr (N == 16) out[i] = rshift64((int64_t)in[i] * 2 * 5793, 12);
+    else if constexpr (N == 16) out[i] = rshift64(x * (2 * 5793), 12);
     else out[i] = (int32_t)((uint32_t)in[i] * 4u);
   }
 }
@@ -310,7 +326,7 @@ __device__ __forceinline__ void fwd_1d(int kind, const int32_t* in, int32_t* out
   } else if (kind == 1) {
     if constexpr (N <= 16) fadst<N, BIT, FAST>(in, out);
   } else {
-    if constexpr (N <= 32) fidentity<N>(in, out);
+    if constexpr (N <= 32) fidentity<N, FAST>(in, out);
   }
 }
 

@@ -94,6 +94,9 @@ _lib.lavish_full_pixel_search_batch_mesh.restype = _i32
 if hasattr(_lib, "lavish_set_search_workgroup_cap"):  # (older experiment builds lack it)
     _lib.lavish_set_search_workgroup_cap.argtypes = [_i32]
     _lib.lavish_set_search_workgroup_cap.restype = _i32
+if hasattr(_lib, "lavish_set_search_schedule"):
+    _lib.lavish_set_search_schedule.argtypes = [_i32]
+    _lib.lavish_set_search_schedule.restype = _i32
 
 
 class RefTiles:
@@ -153,6 +156,15 @@ def set_search_workgroup_cap(workgroups):
     rc = _lib.lavish_set_search_workgroup_cap(int(workgroups))
     if rc:
         raise ValueError("lavish_set_search_workgroup_cap(%r): %d" % (workgroups, rc))
+
+
+def set_search_schedule(queued):
+    """lavish_set_search_schedule: a capped search pulls its wave units from
+    per-XCD queues (True, the default) or strides statically (False);
+    results do not depend on it."""
+    rc = _lib.lavish_set_search_schedule(1 if queued else 0)
+    if rc:
+        raise ValueError("lavish_set_search_schedule(%r): %d" % (queued, rc))
 
 
 def default_mv_cost_tables(allow_hp=False):

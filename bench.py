@@ -79,7 +79,7 @@ def parse():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--workload", choices=("rdo", "c2", "c3", "c3sub", "c4", "c4px", "c5", "inter",
-                                           "tpl", "rate", "pixel", "warp", "compound"),
+                                           "tpl", "rate", "pixel", "warp", "compound", "scale", "mesh"),
                     default="rdo")
     ap.add_argument("--rdmult", type=int, default=2000)
     ap.add_argument("--width", type=int, default=1920)
@@ -107,6 +107,9 @@ def parse():
                     help="skip the c4 sub-object (4K 10-bit RDO step) of the default line")
     ap.add_argument("--c3-wg-cap", type=int, default=C3_WG_CAP,
                     help="workgroups of the C3 search when it runs beside C2 (0: no cap)")
+    ap.add_argument("--c3-static", action="store_true",
+                    help="the capped C3 search strides statically over virtual workgroups "
+                         "instead of pulling its wave units from per-XCD queues (A/B)")
     ap.add_argument("--c3-mode", choices=("fused", "streams", "split32"), default=C3_MODE,
                     help="how C3 runs beside C2: one launch with the search's job groups "
                          "interleaved among C2's workgroups (lavish_txq_frame_search), C3 on a "
@@ -1170,6 +1173,290 @@ def cpu_baseline_warp(args):
                       % (passes, W, Hs, sb, len(jobs), threads, dt)}
 
 
+SCALE_STEP = 1536      # 1/1024 pel per output pixel: a reference at 1.5x the frame's size
+SCALE_BORDER = 32
+
+
+def scale_setup(W, H, nrefs, seed):
+    """Scaled-prediction workload (av1_convolve_2d_scale, the inter predictor
+    of a reference of another resolution): nrefs 8-bit references at 1.5x
+    the frame's size (3 W / 2 x 3 H / 2, SCALE_BORDER pixels of edge
+    replication), one LavishScaleJob per 16x16 block x reference: the
+    block's position scaled by 1.5 (x_step_qn = y_step_qn = 1536) plus a
+    seeded motion of +-8 reference pixels at a seeded 1/1024-pel phase."""
+    import lavish_dsp.scale as Sc
+    import lavish_dsp.synth as synth
+    Wr, Hr, b = W * 3 // 2, H * 3 // 2, SCALE_BORDER
+    refs = np.stack([synth.pad_plane(synth.frame(Wr, Hr, 8, seed + k).astype(np.uint8), b)
+                     for k in range(nrefs)])
+    st = refs.shape[2]
+    rng = np.random.default_rng(seed)
+    nbx, nby = W // C3_BLOCK, H // C3_BLOCK
+    ys = np.repeat(np.arange(nby) * C3_BLOCK, nbx)
+    xs = np.tile(np.arange(nbx) * C3_BLOCK, nby)
+    n = len(ys)
+    jobs = np.zeros(nrefs * n, Sc.JOB_DTYPE)
+    for k in range(nrefs):
+        sl = slice(k * n, (k + 1) * n)
+        qx = xs * SCALE_STEP + rng.integers(-8 * 1024, 8 * 1024, n)
+        qy = ys * SCALE_STEP + rng.integers(-8 * 1024, 8 * 1024, n)
+        qx = np.clip(qx, 0, None)
+        qy = np.clip(qy, 0, None)
+        jobs["src_off"][sl] = k * refs[0].size + ((qy >> 10) + b) * st + (qx >> 10) + b
+        jobs["subpel_x_qn"][sl] = qx & 1023
+        jobs["subpel_y_qn"][sl] = qy & 1023
+        jobs["dst_off"][sl] = k * W * H + ys * W + xs
+    jobs["x_step_qn"] = SCALE_STEP
+    jobs["y_step_qn"] = SCALE_STEP
+    return refs, st, jobs
+
+
+def scale_bytes(W, H, nrefs, njobs, bw=16, bh=16):
+    """Algorithmic bytes of one step: every reference plane read once (the
+    blocks' source windows tile it; their 7-pixel tap margins overlap and are
+    L2 hits), every prediction pixel written once, the 40-byte job records."""
+    return nrefs * (W * 3 // 2) * (H * 3 // 2) + njobs * (bw * bh + 40)
+
+
+SCALE_CP = dict(do_average=0, round_0=3, round_1=11, is_compound=0, use_dist_wtd_comp_avg=0,
+                fwd_offset=0, bck_offset=0)
+
+
+def cpu_baseline_scale(args):
+    """orc_convolve_2d_scale_batch (the oracle's av1_convolve_2d_scale_c
+    restatement) on a 1920x256 strip of the same workload, all host cores."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import _oracle as O
+    W, Hs = args.width, 256
+    refs, st, jobs = scale_setup(W, Hs, args.refs, 1234)
+    tab = compound_tables()
+    dst = np.zeros(args.refs * W * Hs, np.uint8)
+    threads = host_cores()
+    sb = sb64_count(W, Hs)
+    n = 0
+    t0 = time.perf_counter()
+    while True:
+        O.convolve_2d_scale_batch(refs.reshape(-1), st, dst, W, None, 0, C3_BLOCK, C3_BLOCK, jobs,
+                                  tab, tab, SCALE_CP, threads=threads)
+        n += 1
+        dt = time.perf_counter() - t0
+        if dt >= args.cpu_seconds:
+            break
+    return {"value": round(n * sb / dt, 2), "unit": "SB64/s", "cores": threads, "kind": "port",
+            "sample": "%d passes of a %dx%d strip (%d SB64, %d blocks) through the scaled "
+                      "prediction step, oracle C restatement (-O3, %d pthreads), %.1f s"
+                      % (n, W, Hs, sb, len(jobs), threads, dt)}
+
+
+def main_scale(args):
+    """Scaled inter prediction (av1_convolve_2d_scale, single prediction,
+    8-bit, EIGHTTAP_REGULAR) of every 16x16 block of a 1080p frame from
+    every reference at 1.5x resolution (lavish_convolve_2d_scale_batch),
+    one frame per step."""
+    import torch
+    import torch.distributed as dist
+    import lavish_dsp as L
+    import lavish_dsp.scale as Sc
+    from lavish_dsp.compound import filter_params
+    from lavish_dsp.inter import ConvolveParams
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local_rank)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    W, H = args.width, args.height
+    refs, st, jobs_np = scale_setup(W, H, args.refs, 1234 + rank)
+    tref = torch.from_numpy(refs.reshape(-1)).cuda()
+    pred = torch.empty(args.refs * W * H, dtype=torch.uint8, device="cuda")
+    tjobs = torch.from_numpy(jobs_np.view(np.uint8)).cuda()
+    fp, keep = filter_params(compound_tables())
+    c = SCALE_CP
+    cp = ConvolveParams(c["do_average"], None, 0, c["round_0"], c["round_1"], 0,
+                        c["is_compound"], c["use_dist_wtd_comp_avg"], c["fwd_offset"],
+                        c["bck_offset"])
+    stream = torch.cuda.current_stream()
+
+    def step():
+        Sc.convolve_2d_scale_batch(tref, st, pred, W, None, 0, C3_BLOCK, C3_BLOCK, tjobs,
+                                   len(jobs_np), fp, fp, cp, 8, stream=stream)
+
+    line = _timed_line(args, step, stream, world, rank, W, H, dtype="u8",
+                       data="synthetic (seeded 1080p frame, seeded 1.5x references, "
+                            "lavish_dsp/synth.py; seeded motion and phases)",
+                       workload="scale: %dx%d 8-bit; av1_convolve_2d_scale (single prediction, "
+                                "EIGHTTAP_REGULAR, x / y step %d/1024) of every %dx%d block x "
+                                "%d refs at 1.5x resolution, %d blocks"
+                                % (W, H, SCALE_STEP, C3_BLOCK, C3_BLOCK, args.refs,
+                                   len(jobs_np)),
+                       kernel="scale_kernel<u8, 8, 8> (lavish_convolve_2d_scale_batch)",
+                       nbytes=scale_bytes(W, H, args.refs, len(jobs_np)))
+    if rank == 0 and world == 1 and not args.no_cpu:
+        line["cpu_baseline"] = cpu_baseline_scale(args)
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+# the temporal filter's full-pel search (temporal_filter.c:113-160): NSTEP at
+# av1_init_search_range(1920) = 0, MV_COST_L1_HDRES, run_mesh_search = 1,
+# good_quality_mesh_patterns[min(speed 6, MAX_MESH_SPEED)] (speed_features.c:26-33,
+# 2291-2298), mesh_search_mv_diff_threshold 4, no pruning; 16x16 blocks
+# (TF_BLOCK_SIZE), cost list on
+MESH_PATTERNS = [(64, 16), (24, 8), (12, 4), (7, 1)]
+
+
+def mesh_candidates(patterns=MESH_PATTERNS):
+    """Nominal mesh candidates per job (exhaustive_mesh_search, mcomp.c:1529-1601):
+    per pass ((2 range) / interval + 1)^2 positions around its centre,
+    unclamped (jobs near the frame edge clamp their ranges: an upper bound)."""
+    return sum((2 * r // max(iv, 1) + 1) ** 2 for r, iv in patterns)
+
+
+def mesh_setup(W, H, nrefs, seed):
+    import lavish_dsp.motion as M
+    import lavish_dsp.synth as synth
+    border = 160
+    src, refs = synth.motion_planes(W, H, nrefs, border, seed=seed)
+    st = src.shape[1]
+    jobs = M.frame_jobs(W, H, st, border, src.size, C3_BLOCK, C3_BLOCK, nrefs)
+    return src, refs, st, jobs
+
+
+def cpu_baseline_mesh(args):
+    """The oracle's av1_full_pixel_search (NSTEP + the mesh refinement) on a
+    1920x256 strip of the same workload, all host cores."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import _oracle as O
+    W, Hs = args.width, 256
+    src, refs, st, jobs = mesh_setup(W, Hs, args.refs, 1234)
+    om = O.OrcMeshParams(1, 0x7FFFFFFF, 0, 4, 0, 0)
+    for i, (r, iv) in enumerate(MESH_PATTERNS):
+        om.range[i], om.interval[i] = r, iv
+    threads = host_cores()
+    sb = sb64_count(W, Hs)
+    n = 0
+    t0 = time.perf_counter()
+    while True:
+        O.full_pixel_search_batch(src.reshape(-1), refs.reshape(-1), st, C3_BLOCK, C3_BLOCK, jobs,
+                                  "nstep", 0, 3, 0, 0, skip=False, cost_list=True,
+                                  threads=threads, mesh=om)
+        n += 1
+        dt = time.perf_counter() - t0
+        if dt >= args.cpu_seconds:
+            break
+    return {"value": round(n * sb / dt, 2), "unit": "SB64/s", "cores": threads, "kind": "port",
+            "sample": "%d passes of a %dx%d strip (%d SB64, %d jobs) through NSTEP + the mesh "
+                      "refinement, oracle C restatement (-O3, %d pthreads), %.1f s"
+                      % (n, W, Hs, sb, len(jobs), threads, dt)}
+
+
+def main_mesh(args):
+    """The temporal filter's full-pel motion search (NSTEP, then the
+    exhaustive mesh refinement on every job: run_mesh_search = 1) of every
+    16x16 block of a 1080p frame against each reference
+    (lavish_full_pixel_search_batch_mesh: the search kernel, then
+    mesh_kernel), one frame per step."""
+    import torch
+    import torch.distributed as dist
+    import lavish_dsp.motion as M
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local_rank)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    W, H = args.width, args.height
+    src, refs, st, jobs_np = mesh_setup(W, H, args.refs, 1234 + rank)
+    tsrc, trefs = torch.from_numpy(src).cuda(), torch.from_numpy(refs).cuda()
+    tjobs = M.to_device(jobs_np)
+    cp = M.l1_cost_params(M.MV_COST_L1_HDRES)
+    mesh = M.MeshParams.make(MESH_PATTERNS, run_mesh_search=1)
+    nj = len(jobs_np)
+    out = torch.empty(nj * M.RESULT_DTYPE.itemsize, dtype=torch.uint8, device="cuda")
+    cl = torch.empty((nj, 5), dtype=torch.int32, device="cuda")
+    stream = torch.cuda.current_stream()
+
+    def step():
+        M.full_pixel_search_batch(tsrc, trefs, C3_BLOCK, C3_BLOCK, tjobs, cp, "nstep", 0, False,
+                                  True, out=out, cost_lists=cl, stream=stream, mesh=mesh)
+
+    cand = mesh_candidates()
+    nbytes = nj * cand * C3_BLOCK * C3_BLOCK
+    line = _timed_line(args, step, stream, world, rank, W, H, dtype="u8",
+                       data="synthetic (seeded 1080p motion planes, lavish_dsp/synth.py)",
+                       workload="mesh: %dx%d 8-bit; the temporal filter's av1_full_pixel_search "
+                                "(NSTEP, step_param 0, MV_COST_L1_HDRES, run_mesh_search 1, mesh "
+                                "patterns %s, cost list) of every %dx%d block x %d refs, %d jobs"
+                                % (W, H, MESH_PATTERNS, C3_BLOCK, C3_BLOCK, args.refs, nj),
+                       kernel="diamond_kernel<16,16,NSTEP> + mesh_kernel<16,16> "
+                              "(lavish_full_pixel_search_batch_mesh)",
+                       nbytes=nbytes)
+    # the candidates' SAD reads overlap (neighbouring positions share rows):
+    # L2-served, as C3's; no HBM bound is claimed for them
+    r = line["roofline"]
+    r["bound"] = "l2-served SAD reads (nominal)"
+    r["note"] = ("algorithmic bytes = jobs x %d nominal mesh candidates (unclamped) x 256 B "
+                 "of candidate rows read by the SADs; the NSTEP walk's own reads not counted; "
+                 "frac against the HBM peak for scale only" % cand)
+    if rank == 0 and world == 1 and not args.no_cpu:
+        line["cpu_baseline"] = cpu_baseline_mesh(args)
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def _timed_line(args, step, stream, world, rank, W, H, dtype, data, workload, kernel, nbytes):
+    """The contract's line for a one-launch component workload: W warmup
+    steps, K timed steps bracketed by barrier + synchronize, max over ranks;
+    the roofline from HIP events on the launch's stream."""
+    import torch
+    import torch.distributed as dist
+    import lavish_dsp as L
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+          for _ in range(args.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        ev[k][0].record(stream)
+        step()
+        ev[k][1].record(stream)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    status = L.status()
+    if status[0] != 0:
+        raise RuntimeError("HIP error during bench: %s" % (status,))
+    k_ms = sum(a.elapsed_time(b) for a, b in ev) / args.steps
+    sb = sb64_count(W, H)
+    achieved = nbytes / (k_ms * 1e-3) / 1e9
+    return {
+        "metric": metric_name(args), "workload": args.workload,
+        "value": round(world * sb * args.steps / elapsed, 2), "unit": "SB64/s",
+        "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": dtype, "data": data,
+        "config": {"workload": workload + "; %d SB64/frame" % sb,
+                   "parallelism": "frame-per-rank x%d" % world},
+        "roofline": {"bound": "hbm", "kernel": kernel, "achieved": round(achieved, 1),
+                     "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                     "avg_launch_ms": round(k_ms, 4), "algorithmic_bytes_per_launch": nbytes},
+    }
+
+
 def main_warp(args):
     """Affine warp prediction (av1_warp_affine_c, single prediction, 8-bit)
     of every 16x16 block of a 1080p frame against every reference with its
@@ -1977,6 +2264,10 @@ def main():
         return main_inter(args)
     if args.workload == "pixel":
         return main_pixel(args)
+    if args.workload == "scale":
+        return main_scale(args)
+    if args.workload == "mesh":
+        return main_mesh(args)
     if args.workload == "warp":
         return main_warp(args)
     if args.workload == "compound":
@@ -2005,6 +2296,8 @@ def main():
     R = RdoStep(args.workload, W, H, args.refs, args.border, args.qindex, args.rdmult,
                 seed=1234 + rank, serial=args.serial, c3_wg_cap=args.c3_wg_cap,
                 c3_mode=args.c3_mode, c3_every=args.c3_every)
+    if args.c3_static:
+        R.M.set_search_schedule(False)
     do_c2, do_c3, do_sub, overlap = R.do_c2, R.do_c3, R.do_sub, R.overlap
     stream, sizes, jobs_np, c3_cost = R.stream, R.sizes, R.jobs_np, R.c3_cost
     step = R.step

@@ -681,6 +681,13 @@ int lavish_txq_frame_search(const int16_t *residual, int stride, int width, int 
  * the encoder's threads). */
 int lavish_set_search_workgroup_cap(int workgroups);
 
+/* How a capped 16x16 DIAMOND search deals its 8-job wave units: 1 (default)
+ * every wave pulls its next unit from one of 8 queues (one per XCD label
+ * blockIdx % 8, the label's units a contiguous range of blocks); 0 the
+ * static grid-stride over virtual workgroups.  Results do not depend on it;
+ * -1 for another value.  No reference counterpart. */
+int lavish_set_search_schedule(int queued);
+
 /* ---- sub-pixel refinement ------------------------
  * av1_find_best_sub_pixel_tree_pruned_more (av1/encoder/mcomp.c:2907-2981;
  * subpel_search_method SUBPEL_TREE_PRUNED_MORE, speed >= 4) without a cost

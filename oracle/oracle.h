@@ -478,6 +478,11 @@ void orc_convolve_2d_scale(const void *src, int src_stride, void *dst, int dst_s
                            int subpel_x_qn, int x_step_qn, int subpel_y_qn, int y_step_qn,
                            const OrcConvParams *cp, uint16_t *conv, int conv_stride, int bd,
                            int hbd);
+/* the same over a batch of blocks (LavishScaleJob layout), over pthreads */
+void orc_convolve_2d_scale_batch(const void *src, int src_stride, void *dst, int dst_stride,
+                                 uint16_t *conv, int conv_stride, int w, int h, const void *jobs,
+                                 long njobs, const int16_t *fx, int tx, const int16_t *fy, int ty,
+                                 const OrcConvParams *cp, int bd, int hbd, int threads);
 
 /* search_tx_type's RDCOST + first-strictly-lowest type choice (oracle_rdo.c) */
 int orc_rd_select(int rdmult, const int *rates, const int64_t *dists, int n, int64_t *rds);

@@ -89,3 +89,73 @@ void orc_convolve_2d_scale(const void *src, int src_stride, void *dst, int dst_s
   }
   free(im);
 }
+
+/* Batch driver for the `scale` bench workload's CPU baseline: jobs in the
+ * LavishScaleJob layout (one w x h block each), one conv form, over
+ * pthreads. */
+#include <pthread.h>
+
+typedef struct {
+  int64_t src_off, dst_off, conv_off;
+  int32_t subpel_x_qn, x_step_qn, subpel_y_qn, y_step_qn;
+} ScaleJob;
+
+typedef struct {
+  const void *src;
+  void *dst;
+  uint16_t *conv;
+  const ScaleJob *jobs;
+  const int16_t *fx, *fy;
+  const OrcConvParams *cp;
+  int src_stride, dst_stride, conv_stride, w, h, tx, ty, bd, hbd;
+  long lo, hi;
+} ScaleArg;
+
+static void *scale_worker(void *p) {
+  const ScaleArg *a = (const ScaleArg *)p;
+  const int es = a->hbd ? 2 : 1;
+  for (long j = a->lo; j < a->hi; ++j) {
+    const ScaleJob *jb = &a->jobs[j];
+    orc_convolve_2d_scale((const char *)a->src + jb->src_off * es, a->src_stride,
+                          a->dst ? (char *)a->dst + jb->dst_off * es : NULL, a->dst_stride, a->w,
+                          a->h, a->fx, a->tx, a->fy, a->ty, jb->subpel_x_qn, jb->x_step_qn,
+                          jb->subpel_y_qn, jb->y_step_qn, a->cp,
+                          a->conv ? a->conv + jb->conv_off : NULL, a->conv_stride, a->bd, a->hbd);
+  }
+  return NULL;
+}
+
+void orc_convolve_2d_scale_batch(const void *src, int src_stride, void *dst, int dst_stride,
+                                 uint16_t *conv, int conv_stride, int w, int h, const void *jobs,
+                                 long njobs, const int16_t *fx, int tx, const int16_t *fy, int ty,
+                                 const OrcConvParams *cp, int bd, int hbd, int threads) {
+  if (threads < 1) threads = 1;
+  if (threads > 256) threads = 256;
+  pthread_t tid[256];
+  ScaleArg args[256];
+  for (int t = 0; t < threads; ++t) {
+    ScaleArg *a = &args[t];
+    a->src = src;
+    a->dst = dst;
+    a->conv = conv;
+    a->jobs = (const ScaleJob *)jobs;
+    a->fx = fx;
+    a->fy = fy;
+    a->cp = cp;
+    a->src_stride = src_stride;
+    a->dst_stride = dst_stride;
+    a->conv_stride = conv_stride;
+    a->w = w;
+    a->h = h;
+    a->tx = tx;
+    a->ty = ty;
+    a->bd = bd;
+    a->hbd = hbd;
+    a->lo = njobs * t / threads;
+    a->hi = njobs * (t + 1) / threads;
+    if (threads > 1) pthread_create(&tid[t], NULL, scale_worker, a);
+    else scale_worker(a);
+  }
+  if (threads > 1)
+    for (int t = 0; t < threads; ++t) pthread_join(tid[t], NULL);
+}

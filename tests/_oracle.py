@@ -1071,6 +1071,25 @@ def dist_wtd_batch(src, src_stride, dst, dst_stride, conv, conv_stride, w, h, jo
        threads)
 
 
+def convolve_2d_scale_batch(src, src_stride, dst, dst_stride, conv, conv_stride, w, h, jobs,
+                            fx_table, fy_table, cp, bd=8, threads=1):
+    """orc_convolve_2d_scale_batch in place on dst / conv (jobs:
+    lavish_dsp.scale.JOB_DTYPE; fx_table / fy_table: int16 [16, taps];
+    conv None outside the compound forms)."""
+    fn = lib().orc_convolve_2d_scale_batch
+    fn.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p] + \
+        [ctypes.c_int] * 3 + [ctypes.c_void_p, ctypes.c_long, ctypes.c_void_p, ctypes.c_int,
+                              ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p] + [ctypes.c_int] * 3
+    fn.restype = None
+    fx = np.ascontiguousarray(fx_table, np.int16)
+    fy = np.ascontiguousarray(fy_table, np.int16)
+    c = OrcConvParams(**cp)
+    jobs = np.ascontiguousarray(jobs)
+    fn(P(src), src_stride, P(dst) if dst is not None else None, dst_stride,
+       P(conv) if conv is not None else None, conv_stride, w, h, P(jobs), len(jobs), P(fx),
+       fx.shape[1], P(fy), fy.shape[1], ctypes.byref(c), bd, int(src.dtype == np.uint16), threads)
+
+
 def rd_select(rdmult, rates, dists):
     """orc_rd_select: RDCOST of each (rate, dist) and the index of the first
     strictly lowest (search_tx_type's update)."""

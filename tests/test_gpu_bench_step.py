@@ -136,18 +136,24 @@ def test_fused_launch_interleave_sweep(step, c2_expected, c3_expected, every):
     _check_c2(R, c2_expected, "every %d" % every)
 
 
+@pytest.mark.parametrize("queued", [True, False])
 @pytest.mark.parametrize("cap", [8, 64, 512, 0])
-def test_search_workgroup_cap_sweep(step, c3_expected, cap):
-    """The capped search (grid-stride over virtual workgroups) is the
-    uncapped search: identical results at every cap."""
+def test_search_workgroup_cap_sweep(step, c3_expected, cap, queued):
+    """The capped search -- wave units pulled from the per-XCD queues
+    (diamond_lj_dyn_kernel, the default) or the static grid-stride over
+    virtual workgroups -- is the uncapped search: identical results at every
+    cap, twice in a row (the queues start from zero each launch)."""
     import torch
     b, R = step
-    R.c3_out.fill_(0x55)
-    R.c3_cl.fill_(-7)
     R.M.set_search_workgroup_cap(cap)
+    R.M.set_search_schedule(queued)
     try:
-        R.c3(R.stream)
-        torch.cuda.synchronize()
+        for it in range(2):
+            R.c3_out.fill_(0x55)
+            R.c3_cl.fill_(-7)
+            R.c3(R.stream)
+            torch.cuda.synchronize()
+            _check_c3(R, *c3_expected, what="cap %d queued %s pass %d" % (cap, queued, it))
     finally:
         R.M.set_search_workgroup_cap(0)
-    _check_c3(R, *c3_expected, what="cap %d" % cap)
+        R.M.set_search_schedule(True)

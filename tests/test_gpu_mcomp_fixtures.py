@@ -367,3 +367,35 @@ def test_subpel_tree_upsampled_vs_oracle(stype, bw, bh):
     got = M.subpel_results_numpy(out)
     for f in ("best_row", "best_col", "besterr", "distortion", "sse"):
         np.testing.assert_array_equal(got[f], exp[f], err_msg=f)
+
+
+def test_mesh_bench_workload_vs_oracle():
+    """bench.py --workload mesh's call (the temporal filter's search: NSTEP,
+    MV_COST_L1_HDRES, run_mesh_search on every job, the speed-6 mesh
+    patterns, cost lists) on a 1920x128 strip x 7 references against the
+    oracle restatement (pinned to av1_full_pixel_search by fix_mcomp3)."""
+    import importlib.util
+    import torch
+    from lavish_dsp import motion as M
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    spec = importlib.util.spec_from_file_location("bench", os.path.join(root, "bench.py"))
+    b = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(b)
+    W, H, R = 1920, 128, 7
+    src, refs, st, jobs = b.mesh_setup(W, H, R, 5)
+    mesh = M.MeshParams.make(b.MESH_PATTERNS, run_mesh_search=1)
+    out, cl = M.full_pixel_search_batch(torch.from_numpy(src).cuda(), torch.from_numpy(refs).cuda(),
+                                        16, 16, M.to_device(jobs),
+                                        M.l1_cost_params(M.MV_COST_L1_HDRES), "nstep", 0, False,
+                                        True, mesh=mesh)
+    torch.cuda.synchronize()
+    om = O.OrcMeshParams(1, 0x7FFFFFFF, 0, 4, 0, 0)
+    for i, (r, iv) in enumerate(b.MESH_PATTERNS):
+        om.range[i], om.interval[i] = r, iv
+    exp, ecl = O.full_pixel_search_batch(src.reshape(-1), refs.reshape(-1), st, 16, 16, jobs,
+                                         "nstep", 0, 3, 0, 0, skip=False, cost_list=True,
+                                         threads=8, mesh=om)
+    res = M.results_numpy(out)
+    for f in ("best_row", "best_col", "bestsme"):
+        np.testing.assert_array_equal(res[f], exp[f], err_msg=f)
+    np.testing.assert_array_equal(cl.cpu().numpy(), ecl)

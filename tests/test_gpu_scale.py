@@ -212,3 +212,36 @@ def test_scale_rejects(S):
             S.convolve_2d_scale_batch(src, 64, src, 8, None, 0, w, h, jobs, 1, fpx, fpx, cp, 8)
     with pytest.raises(ValueError):  # lowbd at bd 10
         S.convolve_2d_scale_batch(src, 64, src, 8, None, 0, 8, 8, jobs, 1, fpx, fpx, cp, 10)
+
+
+def _bench():
+    import importlib.util
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    spec = importlib.util.spec_from_file_location("bench", os.path.join(root, "bench.py"))
+    b = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(b)
+    return b
+
+
+def test_scale_bench_workload_vs_oracle(S):
+    """bench.py --workload scale's call (every 16x16 block x 7 references at
+    1.5x resolution, EIGHTTAP_REGULAR, single prediction, 8-bit) on a
+    1920x256 strip of the same construction, against the oracle's batch
+    restatement (orc_convolve_2d_scale_batch, pinned by fix_scale)."""
+    import torch
+    from lavish_dsp.compound import filter_params
+    b = _bench()
+    W, H, R = 1920, 256, 7
+    refs, st, jobs = b.scale_setup(W, H, R, 99)
+    tab = b.compound_tables()
+    fp, keep = filter_params(tab)
+    pred = torch.full((R * W * H,), 7, dtype=torch.uint8, device="cuda")
+    S.convolve_2d_scale_batch(torch.from_numpy(refs.reshape(-1)).cuda(), st, pred, W, None, 0,
+                              16, 16, torch.from_numpy(jobs.view(np.uint8)).cuda(), len(jobs),
+                              fp, fp, _cparams(b.SCALE_CP), 8)
+    torch.cuda.synchronize()
+    exp = np.full(R * W * H, 7, np.uint8)
+    O.convolve_2d_scale_batch(refs.reshape(-1), st, exp, W, None, 0, 16, 16, jobs, tab, tab,
+                              b.SCALE_CP, threads=8)
+    np.testing.assert_array_equal(pred.cpu().numpy(), exp)
+    assert (exp != 7).mean() > 0.9

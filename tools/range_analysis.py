@@ -114,6 +114,9 @@ SHIFT = {(4, 4): (2, 0, 0), (8, 8): (2, -1, 0), (16, 16): (2, -2, 0), (32, 32): 
 CBC = [[13, 13, 13, 0, 0], [13, 13, 13, 12, 0], [13, 13, 13, 12, 13], [0, 13, 13, 12, 13], [0, 0, 13, 12, 13]]
 CBR = [[13, 13, 12, 0, 0], [13, 13, 13, 12, 0], [13, 13, 12, 13, 12], [0, 12, 13, 12, 11], [0, 0, 12, 11, 10]]
 
+_last_out = [0]
+
+
 def analyse(W, H, T):
     st = St()
     s0, s1, s2 = SHIFT[(W, H)]
@@ -126,16 +129,31 @@ def analyse(W, H, T):
         m = max(col)
         m = (m + (1 << -s1) - 1) >> -s1 if s1 < 0 else m
         worst_row_in = max(worst_row_in, m)
+    out = 0
     for kr in (0, 1, 2):
         if kr == 1 and W > 16: continue
         if kr != 0 and (W == 64 or H == 64): continue
-        one_d(st, kr, [worst_row_in] * W, W, CBR[wl][hl])
+        row = one_d(st, kr, [worst_row_in] * W, W, CBR[wl][hl])
+        m = max(row)
+        m = (m + (1 << -s2) - 1) >> -s2 if s2 < 0 else m << s2
+        if 2 * W == H or 2 * H == W:   # the 2:1 sizes' NewSqrt2 scaling (x 5793 >> 12)
+            m = (m * 5793 + 4095) >> 12
+        out = max(out, m)
+    _last_out[0] = out
     return st.op, st.sum
+
+
+def coeff_bound(W, H, T):
+    """max |coefficient| out of the forward 2-D transform of a residual
+    bounded by T (what the quantizer and the block error see)."""
+    analyse(W, H, T)
+    return _last_out[0]
 
 if __name__ == "__main__":
     for T in (255, 1023, 4095):
         print("T =", T)
         for (W, H) in SHIFT:
             op, sm = analyse(W, H, T)
-            print("  %2dx%-2d  max|operand| 2^%.2f  max|sum| 2^%.2f  %s" % (
-                W, H, math.log2(op), math.log2(sm), "OK" if op < 2 ** 23 and sm < 2 ** 31 else "--"))
+            print("  %2dx%-2d  max|operand| 2^%.2f  max|sum| 2^%.2f  max|coeff| 2^%.2f  %s" % (
+                W, H, math.log2(op), math.log2(sm), math.log2(_last_out[0]),
+                "OK" if op < 2 ** 23 and sm < 2 ** 31 else "--"))
