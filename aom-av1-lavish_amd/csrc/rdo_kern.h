@@ -266,6 +266,20 @@ __device__ __forceinline__ void rdo_types(const RdoArgs& a, const int32_t (&res)
     wave_sync();
   }
 
+  // MODE 1, FAST: highbd quantize_fp with uniform per-(dc, ac) constants
+  // (quant_one / dequant_one restated in the cheap instruction classes; see
+  // coef_fast): rounding, quant << 16, the pass threshold
+  // ceil(dequant / 2^(1 + LS)) - 1, dequant
+  int qf_rnd[2], qf_thr1[2], qf_deq[2];
+  uint32_t qf_qsh[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    qf_rnd[i] = (a.qp.round[i] + ((1 << LS) >> 1)) >> LS;
+    qf_qsh[i] = (uint32_t)(uint16_t)a.qp.quant[i] << 16;
+    qf_deq[i] = a.qp.dequant[i];
+    qf_thr1[i] = ((qf_deq[i] + (1 << (1 + LS)) - 1) >> (1 + LS)) - 1;
+  }
+
   int grp = -1;  // vertical-kind group of order[oi]; group g runs on wave g % nv
   for (int oi = 0; oi < a.ntypes; ++oi) {
     if constexpr (NVM > 1) {
@@ -279,7 +293,8 @@ __device__ __forceinline__ void rdo_types(const RdoArgs& a, const int32_t (&res)
     const int kr = ht == 3 ? 2 : (ht == 0 ? 0 : 1);
     const bool ud = vt == 2;
     const bool lr = ht == 2;  // FLIPADST rows: the column results read right to left
-    const int16_t* const srow = s_scan + __builtin_amdgcn_readfirstlane(a.scan_kind[ti]) * NC;
+    const int skind = __builtin_amdgcn_readfirstlane(a.scan_kind[ti]);
+    const int16_t* const srow = s_scan + skind * NC;
 
     // ---- columns (av1_fwd_txfm2d.c:88-106), once per vertical kind; only
     // rows < KH are kept ----
@@ -323,12 +338,58 @@ __device__ __forceinline__ void rdo_types(const RdoArgs& a, const int32_t (&res)
       }
       fwd_1d<W, C::cos_bit_row, FAST>(kr, in, out);
       int32_t q[KW];
-      int last = 0, satd = 0;
+      int last = 0, satd = 0, rall = 0;
       int64_t err = 0, sse = 0;
       const size_t obase = ((size_t)ti * a.nblocks + blk0 + bb) * NC;
       // the type's inverse scan of this lane's row (LDS, lane-row order:
       // the KW positions contiguous)
       const int16_t* const isc = srow + r * KW;
+      // (the rows of 32-point sizes keep the generic form: 32 unrolled
+      // coefficients of this one spill at the 32x32 kernel's 2-wave budget)
+      constexpr bool CHEAP = MODE == 1 && FAST && KW <= 16;
+      if constexpr (CHEAP) {
+        // quantize_fp (highbd, av1_quantize.c:174-194) + dequantisation +
+        // block error / sse / SATD / eob / rate_estimator terms on the
+        // certified range (|v| < 2^19, tools/range_analysis.py), in the
+        // VALU's cheap classes (tools/microbench/valu_rates.hip: add / sub /
+        // xor / and / ashr issue in ~2 cycles, multiplies, max, cndmask,
+        // 64-bit ops and DPP in ~4): with a = |v|,
+        //   pass  <=> a << (1 + LS) >= dequant <=> a > thr1 (uniform): a mask
+        //   |q|   = ((a + rnd) * quant) >> (16 - LS) = mulhi((a + rnd) << LS,
+        //           quant << 16) (exact: the product stays below 2^64)
+        //   |dq|  = (|q| * dequant) >> LS (24-bit multiply)
+        //   v - dq = sign(v) (a - |dq|): err += (a - |dq|)^2, sse += a^2
+        //   eob   = max over nonzero |q| of iscan + 1, nonzero = (|q| + 2^23 - 1) >> 23
+        //   rate_estimator term msb(|q| + 1) + 1 + (|q| > 0) = 32 - clz(|q| + 1) + nz
+        // bit-exact with quant_one / dequant_one (the same integers).
+        const bool dcl = r == 0;  // column 0 of row 0 is the DC coefficient
+        const int rnd0 = dcl ? qf_rnd[0] : qf_rnd[1];
+        const uint32_t qsh0 = dcl ? qf_qsh[0] : qf_qsh[1];
+        const int thr0 = dcl ? qf_thr1[0] : qf_thr1[1];
+        const int deq0 = dcl ? qf_deq[0] : qf_deq[1];
+#pragma unroll
+        for (int c = 0; c < KW; ++c) {
+          int32_t v = round_shift_1<-C::s2>(out[c]);
+          if constexpr (C::rect2) v = rshift64((int64_t)v * 5793, 12);
+          const int rnd = c ? qf_rnd[1] : rnd0;
+          const uint32_t qsh = c ? qf_qsh[1] : qsh0;
+          const int thr1 = c ? qf_thr1[1] : thr0;
+          const int deq = c ? qf_deq[1] : deq0;
+          const int32_t sgn = v >> 31;
+          const int32_t av = (v ^ sgn) - sgn;
+          const int32_t pass = (thr1 - av) >> 31;  // -1 where the coefficient is kept
+          const int32_t qa = (int32_t)__umulhi((uint32_t)(av + rnd) << LS, qsh) & pass;
+          const int32_t dqa = mul_i24(qa, deq) >> LS;
+          const int32_t e = av - dqa;
+          err += (int64_t)e * e;
+          sse += (int64_t)av * av;
+          satd += av;
+          const int32_t nz = (qa + 0x7FFFFF) >> 23;
+          last = max(last, ((int)isc[c] + 1) & -nz);
+          rall += 32 - __builtin_clz((uint32_t)qa + 1u) + nz;
+          q[c] = (qa ^ sgn) - sgn;
+        }
+      } else {
 #pragma unroll
       for (int c = 0; c < KW; ++c) {
         int32_t v = round_shift_1<-C::s2>(out[c]);
@@ -366,6 +427,7 @@ __device__ __forceinline__ void rdo_types(const RdoArgs& a, const int32_t (&res)
           if (live) t2[bb * NC + rc] = q[c];
         }
         last = q[c] != 0 ? max(last, isc[c] + 1) : last;
+      }
       }
       last = lane_max<KH>(last);
       if constexpr (MODE == 0) {
@@ -443,6 +505,13 @@ __device__ __forceinline__ void rdo_types(const RdoArgs& a, const int32_t (&res)
           }
           rate = lane_sum<KH>(rate);
           rate = cc::txb_rate(s_cc, cls, tc.txb_skip_ctx, last, a.tx_type_cost[t], rate);
+        } else if (CHEAP && skind == 0) {
+          // rate_estimator over the DCT_DCT scan below eob: for a type of the
+          // default scan (the 2-D classes) eob comes from that same scan, so
+          // every position at or past it is zero and costs 1 -- the sum is
+          // the whole block's minus (n - eob), no per-position test
+          rate = lane_sum<KH>(rall) - (NC - last);
+          rate = (rate + 1) << 9;  // AV1_PROB_COST_SHIFT
         } else {
           // rate_estimator: positions of the DCT_DCT scan below eob
           const int16_t* const dct = s_scan + r * KW;

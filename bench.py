@@ -179,7 +179,7 @@ C3_BLOCK = 16
 C3_COST = 0     # MV_COST_ENTROPY (the RDO path's x->mv_cost_type)
 C3_SKIP = True  # use_downsampled_sad (>= 720p, speed_features.c:205-209)
 C3_CL = True    # cost list: subpel_search_method != SUBPEL_TREE (cond_cost_list)
-C3_WG_CAP = 512  # C3's workgroups beside C2 (profiles/r04_v11_*: the step's best)
+C3_WG_CAP = 384  # C3's workgroups beside C2 (1.5 per CU; the queue-fed search: profiles/r06_c3_cap_sweep.txt)
 # C3 on a second stream beside C2, C2's 32-point class after C3 on that
 # stream (0.717-0.720 vs 0.727-0.729 ms with the whole of C2 on the caller's
 # stream, profiles/r05_split32_ab.txt; fused: measured slower, DESIGN.md

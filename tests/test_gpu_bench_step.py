@@ -6,14 +6,14 @@ default nmv tables, cost lists; av1_full_pixel_search, mcomp.c:1755 ->
 full_pixel_diamond :1479 -> diamond_search_sad :1318-1477) beside C2
 (lavish_txq_frame: every block of the 14 TX sizes <= 32x32 x every valid
 type, tx_search.c:2148-2312 -> encodemb.c:295-341).  The default step
-("split32") runs C3 on a side stream in at most 512 workgroups
+("split32") runs C3 on a side stream in at most 384 workgroups
 (lavish_set_search_workgroup_cap: the search kernel strides over virtual
 workgroups) followed there by C2's 32-point sizes, and the rest of C2 on the
 caller's stream; "streams" keeps all of C2 on the caller's stream; "fused"
 runs C2 and C3 as one launch (lavish_txq_frame_search: the search's job
 groups interleaved among the transform's workgroups) on the caller's
 stream.  Two consecutive steps run, then both legs' outputs are compared
-with the oracle; the search at workgroup caps {8, 64, 512, 0} and the fused
+with the oracle; the search at workgroup caps {8, 64, 384, 512, 0} and the fused
 launch at interleaving strides {1, 3, 10, 40} must give identical results.
 """
 import os
@@ -43,7 +43,7 @@ def step():
     assert torch.cuda.is_available()
     b = _bench()
     R = b.RdoStep()  # the bench's defaults: 1080p, 7 refs, qindex 128, overlapped
-    assert R.overlap and R.fused == (b.C3_MODE == "fused") and R.c3_wg_cap == 512
+    assert R.overlap and R.fused == (b.C3_MODE == "fused") and R.c3_wg_cap == 384
     assert R.split32 == (b.C3_MODE == "split32")
     return b, R
 
@@ -137,7 +137,7 @@ def test_fused_launch_interleave_sweep(step, c2_expected, c3_expected, every):
 
 
 @pytest.mark.parametrize("queued", [True, False])
-@pytest.mark.parametrize("cap", [8, 64, 512, 0])
+@pytest.mark.parametrize("cap", [8, 64, 384, 512, 0])
 def test_search_workgroup_cap_sweep(step, c3_expected, cap, queued):
     """The capped search -- wave units pulled from the per-XCD queues
     (diamond_lj_dyn_kernel, the default) or the static grid-stride over
