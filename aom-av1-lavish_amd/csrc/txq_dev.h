@@ -79,6 +79,17 @@ __device__ __forceinline__ void txq_types(const TxqArgs& a,
     wave_sync();
   }
 
+  // lowbd quantize_fp on the FAST range (the C2 bench path), uniform per
+  // (dc, ac): the rounding, quant, the pass threshold ceil(dequant /
+  // 2^(1 + LS)) - 1 (see the coefficient loop)
+  int qf_rnd[2], qf_thr1[2], qf_qt[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    qf_rnd[i] = (a.qp.round[i] + ((1 << LS) >> 1)) >> LS;
+    qf_qt[i] = a.qp.quant[i];
+    qf_thr1[i] = ((a.qp.dequant[i] + (1 << (1 + LS)) - 1) >> (1 + LS)) - 1;
+  }
+
   for (int ci = c0; ci < c1; ++ci) {
     const int ti = __builtin_amdgcn_readfirstlane(a.chunk_ti[ci]);
     const int t = __builtin_amdgcn_readfirstlane(a.types[ti]);
@@ -107,6 +118,38 @@ __device__ __forceinline__ void txq_types(const TxqArgs& a,
       // scan of this type's scan kind is row skind of the LDS table
       const int16_t* iscan = isc + skind * N;
       int last = 0;
+      if constexpr (QK == LAVISH_QUANT_FP && FAST && !HBD) {
+        // av1_quantize_fp_c (av1_quantize.c:174-194, lowbd) restated in the
+        // VALU's 2-cycle classes (tools/microbench/valu_rates.hip: add / sub
+        // / xor / and / ashr ~2 cycles; multiplies, min / max, cndmask,
+        // shifts left ~4): a = |v|; pass <=> a << (1 + LS) >= dequant <=>
+        // a > thr1, a mask; q = (min(a + rnd, 32767) * quant) >> (16 - LS)
+        // (24-bit multiply: both < 2^15); eob = max over nonzero q of
+        // iscan + 1, nonzero = (q + 2^23 - 1) >> 23 (q < 2^23).  The same
+        // integers as quant_one.
+        const bool dcl = r == 0;
+        const int rnd0 = dcl ? qf_rnd[0] : qf_rnd[1];
+        const int qt0 = dcl ? qf_qt[0] : qf_qt[1];
+        const int thr0 = dcl ? qf_thr1[0] : qf_thr1[1];
+#pragma unroll
+        for (int c = 0; c < W; ++c) {
+          int32_t v = round_shift_1<-C::s2>(out[c]);
+          if constexpr (C::rect2) v = rshift64((int64_t)v * 5793, 12);
+          const int rc = c * H + r;
+          if (a.coeff != nullptr) {
+            if (b < nvalid) a.coeff[obase + rc] = v;
+          }
+          const int32_t sgn = v >> 31;
+          const int32_t av = (v ^ sgn) - sgn;
+          const int32_t pass = ((c ? qf_thr1[1] : thr0) - av) >> 31;
+          const int32_t t = min(av + (c ? qf_rnd[1] : rnd0), 32767);
+          const int32_t qa = (mul_i24(t, c ? qf_qt[1] : qt0) >> (16 - LS)) & pass;
+          const int32_t q = (qa ^ sgn) - sgn;
+          t2[b * N + rc] = q;
+          const int32_t nz = (qa + 0x7FFFFF) >> 23;
+          last = max(last, ((int)iscan[rc] + 1) & -nz);
+        }
+      } else {
 #pragma unroll
       for (int c = 0; c < W; ++c) {
         int32_t v = round_shift_1<-C::s2>(out[c]);
@@ -124,6 +167,7 @@ __device__ __forceinline__ void txq_types(const TxqArgs& a,
         t2[b * N + rc] = q;
         const int pos1 = iscan[rc] + 1;
         last = q != 0 ? max(last, pos1) : last;
+      }
       }
       last = lane_max<H>(last);
       if (r == 0 && b < nvalid && a.eob != nullptr)
