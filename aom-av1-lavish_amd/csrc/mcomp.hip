@@ -2227,24 +2227,54 @@ __device__ __forceinline__ void lj_sads(const Ctx& c, const LjSrc& s, int l,
   }
 }
 
-// lj_sads (downsampled rows) for offsets into the tiled copy computed by the
-// caller: lane l's row 2l of each candidate
-template <int N>
-__device__ __forceinline__ void lj_sads_off(const LjSrc& s, __amdgpu_buffer_rsrc_t trs, int oob,
-                                            const uint32_t (&off)[N], const bool (&v)[N],
-                                            uint32_t (&out)[N]) {
-  u32x4 t[N];
+// The 8 candidates' group SADs of a diamond step, lane l of each 8-lane
+// group keeping the one of site l: a reduce-scatter over the group instead
+// of 8 full group sums and a select.  Stage 1 pairs lane l with its mirror
+// 7 - l (row_half_mirror): the lane keeps the half of the sites it will end
+// with (0-3 below lane 4, 4-7 above), adds its partner's partial sums of
+// that half and hands over the other; stages 2 and 3 do the same with lane
+// l ^ 2 and l ^ 1 (quad_perm), so lane l ends with site 4 b2 + 2 b1 + b0 =
+// l summed over all 8 lanes: 21 DPP adds / selects per step instead of 24
+// DPP adds + 8 selects.  The same sums as group_sum8 (integer adds).
+__device__ __forceinline__ uint32_t scatter_sum8(const uint32_t (&p)[8], int l) {
+  const bool hi = l & 4, m1 = l & 2, m0 = l & 1;
+  uint32_t q[4], r[2];
 #pragma unroll
-  for (int i = 0; i < N; ++i)
+  for (int k = 0; k < 4; ++k) {
+    const uint32_t send = hi ? p[k] : p[k + 4];
+    const uint32_t keep = hi ? p[k + 4] : p[k];
+    q[k] = keep + (uint32_t)__builtin_amdgcn_update_dpp(0, (int)send, 0x141, 0xF, 0xF, false);
+  }
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const uint32_t send = m1 ? q[k] : q[k + 2];
+    const uint32_t keep = m1 ? q[k + 2] : q[k];
+    r[k] = keep + (uint32_t)__builtin_amdgcn_update_dpp(0, (int)send, 0x4E, 0xF, 0xF, false);
+  }
+  const uint32_t send = m0 ? r[0] : r[1];
+  const uint32_t keep = m0 ? r[1] : r[0];
+  return keep + (uint32_t)__builtin_amdgcn_update_dpp(0, (int)send, 0xB1, 0xF, 0xF, false);
+}
+
+// the 8-site step (downsampled rows) at offsets into the tiled copy computed
+// by the caller, lane l reading row 2l of each candidate: lane l gets site
+// l's group SAD
+__device__ __forceinline__ uint32_t lj_step_sad(const LjSrc& s, __amdgpu_buffer_rsrc_t trs,
+                                                int oob, const uint32_t (&off)[8],
+                                                const bool (&v)[8], int l) {
+  u32x4 t[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
     t[i] = __builtin_amdgcn_raw_buffer_load_b128(trs, v[i] ? (int)off[i] : oob, 0, 0);
+  uint32_t p[8];
 #pragma unroll
-  for (int i = 0; i < N; ++i) {
+  for (int i = 0; i < 8; ++i) {
     uint32_t acc = sad4(s.sk[0], t[i].x, 0);
     acc = sad4(s.sk[1], t[i].y, acc);
     acc = sad4(s.sk[2], t[i].z, acc);
-    acc = sad4(s.sk[3], t[i].w, acc);
-    out[i] = 2 * group_sum8(acc);
+    p[i] = sad4(s.sk[3], t[i].w, acc);
   }
+  return 2 * scatter_sum8(p, l);
 }
 
 // mvsad_err_cost's table reads for the entropy cost through the decimated
@@ -2337,12 +2367,7 @@ __device__ void lj_pass(const Ctx& c, const LjSrc& s, int l, __amdgpu_buffer_rsr
         const int dr = site_dr(t), dc = site_dc(t);
         vv[t] = active && (dr < 0 ? up : dr > 0 ? dn : true) && (dc < 0 ? lf : dc > 0 ? rt : true);
       }
-      if (active) {
-        uint32_t sd[8];
-        lj_sads_off<8>(s, trs, oob, off, vv, sd);
-#pragma unroll
-        for (int i = 0; i < 8; ++i) mine = l == i ? sd[i] : mine;
-      }
+      if (active) mine = lj_step_sad(s, trs, oob, off, vv, l);
     } else
     if (active)  // finished jobs' lanes off for the whole step (one branch; measured neutral, r04_v6)
 #pragma unroll
