@@ -280,8 +280,13 @@ __device__ __forceinline__ void rdo_types(const RdoArgs& a, const int32_t (&res)
     qf_thr1[i] = ((qf_deq[i] + (1 << (1 + LS)) - 1) >> (1 + LS)) - 1;
   }
 
+  // the 64-point sizes have one candidate type (EXT_TX_SET_DCTONLY,
+  // tx_type_valid): with a constant trip count the residual columns die at
+  // the column pass instead of staying live through every row pass
+  constexpr bool ONE_TYPE = W == 64 || H == 64;
+  const int ntypes = ONE_TYPE ? 1 : a.ntypes;
   int grp = -1;  // vertical-kind group of order[oi]; group g runs on wave g % nv
-  for (int oi = 0; oi < a.ntypes; ++oi) {
+  for (int oi = 0; oi < ntypes; ++oi) {
     if constexpr (NVM > 1) {
       grp += __builtin_amdgcn_readfirstlane(a.newcol[oi]);
       if (grp % nv != wave) continue;
@@ -803,16 +808,16 @@ __device__ __forceinline__ void rdo_types(const RdoArgs& a, const int32_t (&res)
 #ifndef LAVISH_RDO_WV64
 #define LAVISH_RDO_WV64 2
 #endif
-// (SPLIT: the small-grid instantiation.  A 64-point size there has a few
-// hundred blocks at most -- a wave per block, far fewer than the SIMDs --
-// so its wave's lifetime is the kernel's duration and occupancy buys
-// nothing: it asks for one wave per SIMD and keeps every value in VGPRs
-// instead of the 2-wave request's spills to scratch.)
+// (The 64-point sizes fit the 2-wave request without spills since their
+// type loop has a constant trip count (rdo_types' ONE_TYPE: 256 VGPRs with
+// 426 spilled -> 216, none); until round 6 they ran a one-wave-per-SIMD
+// build below 2048 tiles -- the 4K frame's 2040 64x64 blocks included -- to
+// avoid the spills.)
 template <int W, int H, int MODE, bool SPLIT = false>
 constexpr int rdo_waves() {
   if (MODE != 1) return 1;
   if (W == 16 && H == 16) return LAVISH_RDO_WV16;
-  if (W * H >= 2048) return SPLIT ? 1 : LAVISH_RDO_WV64;
+  if (W * H >= 2048) return LAVISH_RDO_WV64;
   return W * H >= 512 ? LAVISH_RDO_WV32 : 1;
 }
 
@@ -956,12 +961,6 @@ void launch_rdo(const RdoArgs& a, hipStream_t s) {
   if constexpr (NVM > 1) {
     if (nv > 1 && grid < kRdoSplitTiles) {
       hipLaunchKernelGGL((rdo_kernel<W, H, MODE, 0, true>), dim3(grid), dim3(64 * nv), 0, s, a);
-      LAVISH_CHECK(hipGetLastError());
-      return;
-    }
-  } else if constexpr (MODE == 1 && W * H >= 2048) {
-    if (grid < kRdoSplitTiles) {  // few blocks: the spill-free one-wave-per-SIMD build
-      hipLaunchKernelGGL((rdo_kernel<W, H, MODE, 0, true>), dim3(grid), dim3(64), 0, s, a);
       LAVISH_CHECK(hipGetLastError());
       return;
     }
