@@ -157,6 +157,23 @@ struct PxLds {
 // MODE 0 per-type coefficients, the per-wave winners, the MODE 2 pixel
 // state, and the per-block bookkeeping of rdo_types.
 constexpr int lds_align(int v, int a) { return (v + a - 1) / a * a; }
+// The mode-1 decision of the 32-point sizes keeps the tile's residual in LDS
+// (int16: any residual of bit depth <= 12) rather than in a lane's 32 VGPRs,
+// which stayed live through every type's row pass (two vertical kinds, DCT
+// and IDTX, so the second column pass needs it after the first row pass):
+// the 32x32 kernel spilled at its 2-wave register budget.
+// Measured slower and off (LAVISH_RDO_RES_LDS=1 builds it): spill-free
+// (32x32: 256 VGPRs with 24 spilled -> 227, none) but its 27 KB of LDS fits
+// 6 workgroups per CU instead of 7, 61 -> 73 us for the 4K frame's 32x32
+// leg (profiles/r06_ab_same_box.txt).
+#ifndef LAVISH_RDO_RES_LDS
+#define LAVISH_RDO_RES_LDS 0
+#endif
+template <int W, int H, int MODE>
+constexpr bool rdo_res_lds() {
+  return LAVISH_RDO_RES_LDS && MODE == 1 && W != 64 && H != 64 && (W == 32 || H == 32);
+}
+
 template <int W, int H, int MODE, int NVM>
 struct RdoLds {
   using T = RTile<W, H>;
@@ -172,7 +189,10 @@ struct RdoLds {
   static constexpr int brd = lds_align(win + T::P, 8);
   static constexpr int brk = lds_align(brd + 8 * NVM * T::P, 4);
   static constexpr int scan = lds_align(brk + NVM * T::P, 16);  // int16 [3][KH][KW]
-  static constexpr int bytes = lds_align(scan + 2 * 3 * T::NC, 16);
+  // the 32-point sizes' residual (int16 [CPT][H][64 lanes], rdo_res_lds)
+  static constexpr int rs = lds_align(scan + 2 * 3 * T::NC, 16);
+  static constexpr int bytes =
+      lds_align(rs + (rdo_res_lds<W, H, MODE>() ? 2 * T::CPT * H * 64 : 0), 16);
 };
 
 // dist_block_tx_domain's finish of a block sum of squares
@@ -309,11 +329,21 @@ __device__ __forceinline__ void rdo_types(const RdoArgs& a, const int32_t (&res)
         const int j = k * 64 + lane;
         const int b = j / W, c = j % W;
         int32_t in[H], out[H];
-#pragma unroll
-        for (int r = 0; r < H; ++r) {
-          const int32_t x = ud ? res[k][H - 1 - r] : res[k][r];
+        auto col_in = [&](int r, int32_t x) {
           if constexpr (FAST) in[r] = x * (1 << C::s0);
           else in[r] = round_shift_1<-C::s0>(x);
+        };
+        if constexpr (rdo_res_lds<W, H, MODE>()) {
+          const int16_t* const rl = reinterpret_cast<const int16_t*>(lds + LY::rs) + k * H * 64 + lane;
+#pragma unroll
+          for (int r = 0; r < H; ++r) col_in(r, rl[(ud ? H - 1 - r : r) * 64]);
+        } else if (ud) {  // FLIPADST columns: rows bottom to top (a uniform branch:
+                          // the select per row had compiled to VGPR-indexed moves)
+#pragma unroll
+          for (int r = 0; r < H; ++r) col_in(r, res[k][H - 1 - r]);
+        } else {
+#pragma unroll
+          for (int r = 0; r < H; ++r) col_in(r, res[k][r]);
         }
         fwd_1d<H, C::cos_bit_col, FAST>(kc, in, out);
 #pragma unroll
@@ -858,6 +888,8 @@ __device__ __forceinline__ void rdo_tile(const RdoArgs& a, int tile, int lane, i
           if constexpr (MODE == 2) px->pred[(b * H + r) * W + c] = (uint16_t)p;
         }
         res[k][r] = v;
+        if constexpr (rdo_res_lds<W, H, MODE>())
+          reinterpret_cast<int16_t*>(lds + LY::rs)[(k * H + r) * 64 + lane] = (int16_t)v;
         amax = max(amax, abs(v));
         ss += (int64_t)v * v;
       }
@@ -865,6 +897,8 @@ __device__ __forceinline__ void rdo_tile(const RdoArgs& a, int tile, int lane, i
 #pragma unroll
       for (int r = 0; r < H; ++r) {
         res[k][r] = 0;
+        if constexpr (rdo_res_lds<W, H, MODE>())
+          reinterpret_cast<int16_t*>(lds + LY::rs)[(k * H + r) * 64 + lane] = 0;
         if constexpr (MODE == 2) px->pred[(b * H + r) * W + c] = 0;
       }
     }
