@@ -250,8 +250,9 @@ def test_benched_kernels_no_scratch():
                    "spill counts move with the toolchain")
 def test_rdo_decision_kernels_spill_pin():
     """The C4 decision kernels' registers, spills, scratch and LDS as
-    profiles/r06_rdo_kernel_resources.json recorded them (round 6: every
-    one spill-free at its occupancy request) -- a
+    profiles/r06_rdo_kernel_resources.json recorded them (round 6: all
+    spill-free at their occupancy requests but the 32x32 split-form build,
+    14 VGPRs) -- a
     toolchain or code change that moves them shows here (XFAIL) and calls
     for re-measuring the occupancy requests (profiles/r04_v2_rdo_occupancy_ab.json
     measured the requests against spill-free ones in round 4)."""
