@@ -263,3 +263,24 @@ def test_rdo_decision_kernels_spill_pin():
         for k in ("vgpr_count", "vgpr_spill_count", "private_segment_fixed_size",
                   "group_segment_fixed_size"):
             assert got.get(k) == v.get(k), (name, k, got.get(k), v.get(k))
+
+
+@pytest.mark.xfail(strict=False, reason="perf-regression pin, not correctness: exact SGPR "
+                   "spill counts move with the toolchain")
+def test_search_kernels_sgpr_spill_pin():
+    """SGPR spills of the latency-bound search kernels as round 6 left them
+    (DESIGN.md §4): diamond_lj_kernel 21 (parked at entry, none reloaded in
+    the step loop), tpl_mv_kernel<false> / <true> 130 / 142 (kernel
+    arguments parked in VGPR lanes, none reloaded in the candidate rounds).
+    A change that raises them shows here (XFAIL) and calls for checking
+    where the new reloads land."""
+    by = _kernel_resources_by_name()
+    pin = {"diamond_lj_kernel<4>": 21, "diamond_lj_dyn_kernel<4>": 21,
+           "tpl_mv_kernel<false>": 130, "tpl_mv_kernel<true>": 142}
+    seen = set()
+    for name, v in by.items():
+        for k, n in pin.items():
+            if k in name:
+                assert v.get("sgpr_spill_count", 0) <= n, (name, v.get("sgpr_spill_count"))
+                seen.add(k)
+    assert seen == set(pin)
